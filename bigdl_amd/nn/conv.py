@@ -1,0 +1,524 @@
+"""Convolution layers.
+
+Reference: S/nn/SpatialConvolution.scala (983 LoC; updateOutput :253-362, updateGradInput :364-426,
+accGradParameters :435-520), SpatialShareConvolution.scala, SpatialDilatedConvolution.scala:58,
+SpatialFullConvolution.scala:71, SpatialSeparableConvolution.scala:54, VolumetricConvolution.scala:51,
+VolumetricFullConvolution.scala, TemporalConvolution.scala:49, LocallyConnected1D/2D.scala,
+SpatialConvolutionMap.scala.
+
+GPU engine: SpatialConvolution / SpatialShareConvolution / SpatialDilatedConvolution run on the
+implicit-GEMM MFMA kernels (csrc/conv_igemm.hip): forward with fused bias (+ BatchNorm statistics when a
+BN follows — see nn/fusion.py), data gradient through the same kernel family, weight gradient
+accumulated in fp32 straight into the flat gradient buffer. Constructor argument order follows the
+reference (kernelW before kernelH, strides / pads W before H).
+"""
+import math
+
+import torch
+import torch.nn.functional as F
+
+from .. import ops
+from ..ops import conv as cv
+from .abstractnn import AutogradModule, TensorModule
+from .init_methods import RandomUniform, Zeros
+
+CL = torch.channels_last
+BF16 = torch.bfloat16
+
+
+def _same_pad(inp, k, s, d=1):
+    out = -(-inp // s)
+    total = max((out - 1) * s + (k - 1) * d + 1 - inp, 0)
+    return total // 2, total - total // 2
+
+
+class SpatialConvolution(TensorModule):
+    def __init__(self, nInputPlane, nOutputPlane, kernelW, kernelH, strideW=1, strideH=1, padW=0, padH=0,
+                 nGroup=1, propagateBack=True, wRegularizer=None, bRegularizer=None, initWeight=None,
+                 initBias=None, initGradWeight=None, initGradBias=None, withBias=True, format="NCHW",
+                 dilationW=1, dilationH=1):
+        super().__init__()
+        assert nInputPlane % nGroup == 0 and nOutputPlane % nGroup == 0
+        self.nInputPlane, self.nOutputPlane = nInputPlane, nOutputPlane
+        self.kernelW, self.kernelH = kernelW, kernelH
+        self.strideW, self.strideH = strideW, strideH
+        self.padW, self.padH = padW, padH
+        self.dilationW, self.dilationH = dilationW, dilationH
+        self.nGroup = nGroup
+        self.propagateBack = propagateBack
+        self.withBias = withBias
+        self.format = format
+        self.wRegularizer, self.bRegularizer = wRegularizer, bRegularizer
+        self.emit_stats = False      # set by nn.fusion when a BatchNorm consumes this conv's output
+        self.fuse_relu = False
+        self.register_parameter("weight", "gradWeight",
+                                torch.empty(nOutputPlane, nInputPlane // nGroup, kernelH, kernelW))
+        if withBias:
+            self.register_parameter("bias", "gradBias", torch.empty(nOutputPlane))
+        else:
+            self.bias = None
+            self.gradBias = None
+        self.weightInitMethod = RandomUniform()
+        self.biasInitMethod = RandomUniform()
+        self.reset()
+        if initWeight is not None:
+            self.weight.copy_(torch.as_tensor(initWeight).reshape(self.weight.shape))
+        if initBias is not None and withBias:
+            self.bias.copy_(torch.as_tensor(initBias).reshape(self.bias.shape))
+        if initGradWeight is not None:
+            self.gradWeight.copy_(torch.as_tensor(initGradWeight).reshape(self.weight.shape))
+        if initGradBias is not None and withBias:
+            self.gradBias.copy_(torch.as_tensor(initGradBias).reshape(self.bias.shape))
+
+    def reset(self):
+        fan_in = self.nInputPlane // self.nGroup * self.kernelH * self.kernelW
+        stdv = 1.0 / math.sqrt(fan_in)
+        with torch.no_grad():
+            if isinstance(self.weightInitMethod, RandomUniform) and self.weightInitMethod.lower is None:
+                RandomUniform(-stdv, stdv).init(self.weight)
+            else:
+                self.weightInitMethod.init(self.weight)
+            if self.bias is not None:
+                if isinstance(self.biasInitMethod, RandomUniform) and self.biasInitMethod.lower is None:
+                    RandomUniform(-stdv, stdv).init(self.bias)
+                else:
+                    self.biasInitMethod.init(self.bias)
+        self._w16 = {} if not self._w16_managed else self._w16
+
+    def _place(self, attr, t):
+        if t.dim() == 4 and t.is_cuda:
+            return t.contiguous(memory_format=CL)
+        return t.contiguous()
+
+    # ---------------------------------------------------------------- geometry
+    def _pads(self, H, W):
+        if self.padW == -1 and self.padH == -1:
+            ph = _same_pad(H, self.kernelH, self.strideH, self.dilationH)[0]
+            pw = _same_pad(W, self.kernelW, self.strideW, self.dilationW)[0]
+            return ph, pw
+        return self.padH, self.padW
+
+    def _nchw(self, x):
+        if self.format == "NHWC":
+            return x.permute(0, 3, 1, 2)
+        return x
+
+    def _fmt_out(self, y):
+        if self.format == "NHWC":
+            return y.permute(0, 2, 3, 1)
+        return y
+
+    # ---------------------------------------------------------------- forward
+    def updateOutput(self, input):
+        x = self._nchw(input)
+        squeeze = x.dim() == 3
+        if squeeze:
+            x = x.unsqueeze(0)
+        ph, pw = self._pads(x.shape[2], x.shape[3])
+        if x.is_cuda and self.nGroup == 1:
+            y = self._fwd_gpu(x, ph, pw)
+        elif x.is_cuda:
+            y = self._fwd_gpu_grouped(x, ph, pw)
+        else:
+            y = F.conv2d(x.float(), self.weight, self.bias, (self.strideH, self.strideW), (ph, pw),
+                         (self.dilationH, self.dilationW), self.nGroup)
+            if self.fuse_relu:
+                y = torch.relu(y)
+        if squeeze:
+            y = y.squeeze(0)
+        return self._fmt_out(y)
+
+    def _w16_padded(self):
+        w16 = self.w16("weight")
+        if w16.shape[1] % 8 != 0:
+            w16 = cv.weight_krsc_bf16(w16.float())
+        return w16
+
+    def _fwd_gpu(self, x, ph, pw):
+        x16 = cv.to_nhwc_bf16(x)
+        self._x16 = x16
+        w16 = self._w16_padded()
+        stats = None
+        if self.emit_stats and self.train:
+            stats = torch.zeros(2 * self.nOutputPlane, dtype=torch.float32, device=x.device)
+        y = cv.conv2d_fwd(x16, w16, self.bias, (self.strideH, self.strideW), (ph, pw),
+                          (self.dilationH, self.dilationW), relu=self.fuse_relu, stats=stats)
+        if stats is not None:
+            y._bn_stats = stats
+        self._geom = (x.shape, ph, pw)
+        return y
+
+    def _fwd_gpu_grouped(self, x, ph, pw):
+        G = self.nGroup
+        cin, cout = self.nInputPlane // G, self.nOutputPlane // G
+        outs = []
+        w = self.weight
+        self._x16 = cv.to_nhwc_bf16(x) if x.shape[1] % 8 == 0 else None
+        for g in range(G):
+            xg = cv.to_nhwc_bf16(x[:, g * cin:(g + 1) * cin].contiguous(memory_format=CL))
+            wg = cv.weight_krsc_bf16(w[g * cout:(g + 1) * cout])
+            bg = self.bias[g * cout:(g + 1) * cout] if self.bias is not None else None
+            outs.append(cv.conv2d_fwd(xg, wg, bg, (self.strideH, self.strideW), (ph, pw),
+                                      (self.dilationH, self.dilationW), relu=self.fuse_relu))
+        self._geom = (x.shape, ph, pw)
+        return torch.cat(outs, dim=1).contiguous(memory_format=CL)
+
+    # ---------------------------------------------------------------- backward
+    def updateGradInput(self, input, gradOutput):
+        if not self.propagateBack:
+            return None
+        x = self._nchw(input)
+        gy = self._nchw(gradOutput)
+        squeeze = x.dim() == 3
+        if squeeze:
+            x, gy = x.unsqueeze(0), gy.unsqueeze(0)
+        ph, pw = self._pads(x.shape[2], x.shape[3])
+        if gy.is_cuda:
+            gy = self._relu_mask(gy)
+            gi = self._dgrad_gpu(x, gy, ph, pw)
+        else:
+            gy = self._relu_mask(gy)
+            gi = torch.nn.grad.conv2d_input(x.shape, self.weight, gy.float(), (self.strideH, self.strideW),
+                                            (ph, pw), (self.dilationH, self.dilationW), self.nGroup)
+        if squeeze:
+            gi = gi.squeeze(0)
+        return self._fmt_out(gi)
+
+    def _relu_mask(self, gy):
+        if not self.fuse_relu:
+            return gy
+        if gy.is_cuda and gy.dtype == BF16:
+            return ops.relu_bwd_gpu(gy.contiguous(memory_format=CL), self.output)
+        return gy * (self.output > 0)
+
+    def _dgrad_gpu(self, x, gy, ph, pw):
+        gy16 = gy if (gy.dtype == BF16 and gy.is_contiguous(memory_format=CL)) else gy.to(BF16, memory_format=CL)
+        if self.nGroup == 1:
+            w16 = self._w16_padded()
+            wt = cv.transpose_w(w16)
+            Cp = w16.shape[1]
+            xs = (x.shape[0], Cp, x.shape[2], x.shape[3])
+            gi = cv.conv2d_dgrad(gy16, wt, xs, (self.strideH, self.strideW), (ph, pw),
+                                 (self.dilationH, self.dilationW))
+            if Cp != x.shape[1]:
+                gi = gi[:, : x.shape[1]].contiguous(memory_format=CL)
+            return gi
+        G = self.nGroup
+        cin, cout = self.nInputPlane // G, self.nOutputPlane // G
+        parts = []
+        for g in range(G):
+            wg = cv.weight_krsc_bf16(self.weight[g * cout:(g + 1) * cout])
+            gyg = gy16[:, g * cout:(g + 1) * cout].contiguous(memory_format=CL)
+            xs = (x.shape[0], wg.shape[1], x.shape[2], x.shape[3])
+            gi = cv.conv2d_dgrad(gyg, cv.transpose_w(wg), xs, (self.strideH, self.strideW), (ph, pw),
+                                 (self.dilationH, self.dilationW))
+            parts.append(gi[:, :cin])
+        return torch.cat(parts, dim=1).contiguous(memory_format=CL)
+
+    def accGradParameters(self, input, gradOutput):
+        x = self._nchw(input)
+        gy = self._nchw(gradOutput)
+        if x.dim() == 3:
+            x, gy = x.unsqueeze(0), gy.unsqueeze(0)
+        ph, pw = self._pads(x.shape[2], x.shape[3])
+        if gy.is_cuda:
+            gy = self._relu_mask(gy) if self.fuse_relu and not getattr(self, "_masked_cached", False) else gy
+            self._wgrad_gpu(x, gy, ph, pw)
+            return
+        gy = self._relu_mask(gy).float()
+        gw = torch.nn.grad.conv2d_weight(x.float(), self.weight.shape, gy, (self.strideH, self.strideW), (ph, pw),
+                                         (self.dilationH, self.dilationW), self.nGroup)
+        self.gradWeight.add_(gw, alpha=self.scaleW)
+        if self.bias is not None:
+            self.gradBias.add_(gy.sum(dim=(0, 2, 3)), alpha=self.scaleB)
+
+    def _wgrad_gpu(self, x, gy, ph, pw):
+        gy16 = gy if (gy.dtype == BF16 and gy.is_contiguous(memory_format=CL)) else gy.to(BF16, memory_format=CL)
+        x16 = getattr(self, "_x16", None)
+        if x16 is None or x16.shape[0] != x.shape[0] or x16.shape[2:] != x.shape[2:]:
+            x16 = cv.to_nhwc_bf16(x)
+        st, pd, dl = (self.strideH, self.strideW), (ph, pw), (self.dilationH, self.dilationW)
+        if self.nGroup != 1:
+            G = self.nGroup
+            cin, cout = self.nInputPlane // G, self.nOutputPlane // G
+            for g in range(G):
+                xg = cv.to_nhwc_bf16(x[:, g * cin:(g + 1) * cin].contiguous(memory_format=CL))
+                gyg = gy16[:, g * cout:(g + 1) * cout].contiguous(memory_format=CL)
+                dw = torch.zeros(cout, xg.shape[1], self.kernelH, self.kernelW, device=x.device).contiguous(
+                    memory_format=CL)
+                db = torch.zeros(cout, device=x.device) if self.bias is not None else None
+                cv.conv2d_wgrad(gyg, xg, dw, db, st, pd, dl)
+                self.gradWeight[g * cout:(g + 1) * cout].add_(dw[:, :cin], alpha=self.scaleW)
+                if db is not None:
+                    self.gradBias[g * cout:(g + 1) * cout].add_(db, alpha=self.scaleB)
+            return
+        direct = (x16.shape[1] == self.nInputPlane and self.scaleW == 1.0 and self.scaleB == 1.0
+                  and self.gradWeight.is_contiguous(memory_format=CL))
+        if direct:
+            cv.conv2d_wgrad(gy16, x16, self.gradWeight, self.gradBias, st, pd, dl)
+        else:
+            dw = torch.zeros(self.nOutputPlane, x16.shape[1], self.kernelH, self.kernelW,
+                             device=x.device).contiguous(memory_format=CL)
+            db = torch.zeros(self.nOutputPlane, device=x.device) if self.bias is not None else None
+            cv.conv2d_wgrad(gy16, x16, dw, db, st, pd, dl)
+            self.gradWeight.add_(dw[:, : self.nInputPlane], alpha=self.scaleW)
+            if db is not None:
+                self.gradBias.add_(db, alpha=self.scaleB)
+
+    def clearState(self):
+        super().clearState()
+        self._x16 = None
+        return self
+
+    def __repr__(self):
+        return (f"SpatialConvolution({self.nInputPlane} -> {self.nOutputPlane}, {self.kernelW} x {self.kernelH}, "
+                f"{self.strideW}, {self.strideH}, {self.padW}, {self.padH})")
+
+
+class SpatialShareConvolution(SpatialConvolution):
+    """Reference shares im2col buffers across layers to save host memory (ResNet ``optnet``). On the GPU
+    engine there is no im2col buffer at all (implicit GEMM), so this is SpatialConvolution."""
+
+
+class SpatialDilatedConvolution(SpatialConvolution):
+    def __init__(self, nInputPlane, nOutputPlane, kW, kH, dW=1, dH=1, padW=0, padH=0, dilationW=1, dilationH=1,
+                 wRegularizer=None, bRegularizer=None):
+        super().__init__(nInputPlane, nOutputPlane, kW, kH, dW, dH, padW, padH, wRegularizer=wRegularizer,
+                         bRegularizer=bRegularizer, dilationW=dilationW, dilationH=dilationH)
+
+
+class SpatialFullConvolution(AutogradModule):
+    """Transposed convolution (deconvolution). Weight (nInputPlane, nOutputPlane/nGroup, kH, kW)."""
+
+    def __init__(self, nInputPlane, nOutputPlane, kW, kH, dW=1, dH=1, padW=0, padH=0, adjW=0, adjH=0, nGroup=1,
+                 noBias=False, wRegularizer=None, bRegularizer=None):
+        super().__init__()
+        self.nInputPlane, self.nOutputPlane = nInputPlane, nOutputPlane
+        self.kW, self.kH, self.dW, self.dH = kW, kH, dW, dH
+        self.padW, self.padH, self.adjW, self.adjH, self.nGroup = padW, padH, adjW, adjH, nGroup
+        self.wRegularizer, self.bRegularizer = wRegularizer, bRegularizer
+        self.register_parameter("weight", "gradWeight", torch.empty(nInputPlane, nOutputPlane // nGroup, kH, kW))
+        if not noBias:
+            self.register_parameter("bias", "gradBias", torch.empty(nOutputPlane))
+        else:
+            self.bias = None
+        self.reset()
+
+    def reset(self):
+        stdv = 1.0 / math.sqrt(self.kW * self.kH * self.nInputPlane)
+        RandomUniform(-stdv, stdv).init(self.weight)
+        if self.bias is not None:
+            RandomUniform(-stdv, stdv).init(self.bias)
+
+    def fn(self, x):
+        if isinstance(x, torch.Tensor):
+            adj = (self.adjH, self.adjW)
+        else:  # Table(input, sizeTensor)
+            x = x[1]
+            adj = (self.adjH, self.adjW)
+        return F.conv_transpose2d(x.to(self.weight.dtype), self.weight, self.bias, (self.dH, self.dW),
+                                  (self.padH, self.padW), adj, self.nGroup)
+
+
+class SpatialSeparableConvolution(AutogradModule):
+    def __init__(self, nInputChannel, nOutputChannel, depthMultiplier, kW, kH, sW=1, sH=1, pW=0, pH=0,
+                 hasBias=True, dataFormat="NCHW", wRegularizer=None, bRegularizer=None, pRegularizer=None):
+        super().__init__()
+        self.cin, self.cout, self.dm = nInputChannel, nOutputChannel, depthMultiplier
+        self.k, self.s, self.p = (kH, kW), (sH, sW), (pH, pW)
+        self.dataFormat = dataFormat
+        self.register_parameter("depthWeight", "depthGradWeight", torch.empty(nInputChannel * depthMultiplier, 1, kH, kW))
+        self.register_parameter("pointWeight", "pointGradWeight",
+                                torch.empty(nOutputChannel, nInputChannel * depthMultiplier, 1, 1))
+        if hasBias:
+            self.register_parameter("bias", "gradBias", torch.zeros(nOutputChannel))
+        else:
+            self.bias = None
+        self.reset()
+
+    def reset(self):
+        RandomUniform().init(self.depthWeight)
+        RandomUniform().init(self.pointWeight)
+
+    def fn(self, x):
+        if self.dataFormat == "NHWC":
+            x = x.permute(0, 3, 1, 2)
+        y = F.conv2d(x.to(self.depthWeight.dtype), self.depthWeight, None, self.s, self.p, groups=self.cin)
+        y = F.conv2d(y, self.pointWeight, self.bias)
+        return y.permute(0, 2, 3, 1) if self.dataFormat == "NHWC" else y
+
+
+class SpatialConvolutionMap(AutogradModule):
+    """Convolution with an explicit connection table (rows: (inputPlane, outputPlane), 1-based)."""
+
+    def __init__(self, connTable, kW, kH, dW=1, dH=1, padW=0, padH=0):
+        super().__init__()
+        ct = torch.as_tensor(connTable, dtype=torch.long)
+        self.connTable = ct
+        self.nInputPlane = int(ct[:, 0].max())
+        self.nOutputPlane = int(ct[:, 1].max())
+        self.kW, self.kH, self.dW, self.dH, self.padW, self.padH = kW, kH, dW, dH, padW, padH
+        self.register_parameter("weight", "gradWeight", torch.empty(ct.shape[0], kH, kW))
+        self.register_parameter("bias", "gradBias", torch.empty(self.nOutputPlane))
+        mask = torch.zeros(self.nOutputPlane, self.nInputPlane, 1, 1)
+        for i, o in ct.tolist():
+            mask[o - 1, i - 1] = 1
+        self._mask = mask
+        self.reset()
+
+    @staticmethod
+    def full(nin, nout):
+        return [[i, o] for o in range(1, nout + 1) for i in range(1, nin + 1)]
+
+    @staticmethod
+    def oneToOne(n):
+        return [[i, i] for i in range(1, n + 1)]
+
+    def reset(self):
+        stdv = 1.0 / math.sqrt(self.kW * self.kH * self.nInputPlane)
+        RandomUniform(-stdv, stdv).init(self.weight)
+        RandomUniform(-stdv, stdv).init(self.bias)
+
+    def fn(self, x):
+        W = torch.zeros(self.nOutputPlane, self.nInputPlane, self.kH, self.kW, dtype=self.weight.dtype,
+                        device=self.weight.device)
+        idx_o = self.connTable[:, 1].to(self.weight.device) - 1
+        idx_i = self.connTable[:, 0].to(self.weight.device) - 1
+        W = W.index_put((idx_o, idx_i), self.weight)
+        return F.conv2d(x.to(W.dtype), W, self.bias, (self.dH, self.dW), (self.padH, self.padW))
+
+
+class VolumetricConvolution(AutogradModule):
+    def __init__(self, nInputPlane, nOutputPlane, kT, kW, kH, dT=1, dW=1, dH=1, padT=0, padW=0, padH=0,
+                 withBias=True, wRegularizer=None, bRegularizer=None):
+        super().__init__()
+        self.k, self.s, self.p = (kT, kH, kW), (dT, dH, dW), (padT, padH, padW)
+        self.nInputPlane, self.nOutputPlane = nInputPlane, nOutputPlane
+        self.wRegularizer, self.bRegularizer = wRegularizer, bRegularizer
+        self.register_parameter("weight", "gradWeight", torch.empty(nOutputPlane, nInputPlane, kT, kH, kW))
+        if withBias:
+            self.register_parameter("bias", "gradBias", torch.empty(nOutputPlane))
+        else:
+            self.bias = None
+        self.reset()
+
+    def reset(self):
+        stdv = 1.0 / math.sqrt(self.k[0] * self.k[1] * self.k[2] * self.nInputPlane)
+        RandomUniform(-stdv, stdv).init(self.weight)
+        if self.bias is not None:
+            RandomUniform(-stdv, stdv).init(self.bias)
+
+    def fn(self, x):
+        if self.p == (-1, -1, -1):
+            pads = [_same_pad(x.shape[2 + i], self.k[i], self.s[i]) for i in range(3)]
+            x = F.pad(x, (pads[2][0], pads[2][1], pads[1][0], pads[1][1], pads[0][0], pads[0][1]))
+            p = 0
+        else:
+            p = self.p
+        return F.conv3d(x.to(self.weight.dtype), self.weight, self.bias, self.s, p)
+
+
+class VolumetricFullConvolution(AutogradModule):
+    def __init__(self, nInputPlane, nOutputPlane, kT, kW, kH, dT=1, dW=1, dH=1, padT=0, padW=0, padH=0, adjT=0,
+                 adjW=0, adjH=0, nGroup=1, noBias=False, wRegularizer=None, bRegularizer=None):
+        super().__init__()
+        self.k, self.s, self.p, self.adj, self.g = (kT, kH, kW), (dT, dH, dW), (padT, padH, padW), (adjT, adjH, adjW), nGroup
+        self.register_parameter("weight", "gradWeight", torch.empty(nInputPlane, nOutputPlane // nGroup, kT, kH, kW))
+        if not noBias:
+            self.register_parameter("bias", "gradBias", torch.empty(nOutputPlane))
+        else:
+            self.bias = None
+        stdv = 1.0 / math.sqrt(kT * kW * kH * nInputPlane)
+        RandomUniform(-stdv, stdv).init(self.weight)
+        if self.bias is not None:
+            RandomUniform(-stdv, stdv).init(self.bias)
+
+    def fn(self, x):
+        return F.conv_transpose3d(x.to(self.weight.dtype), self.weight, self.bias, self.s, self.p, self.adj, self.g)
+
+
+class TemporalConvolution(AutogradModule):
+    """1-D convolution over (batch, frames, inputFrameSize) (reference TemporalConvolution.scala:49)."""
+
+    def __init__(self, inputFrameSize, outputFrameSize, kernelW, strideW=1, propagateBack=True,
+                 wRegularizer=None, bRegularizer=None, initWeight=None, initBias=None):
+        super().__init__()
+        self.inputFrameSize, self.outputFrameSize, self.kernelW, self.strideW = (inputFrameSize, outputFrameSize,
+                                                                                  kernelW, strideW)
+        self.wRegularizer, self.bRegularizer = wRegularizer, bRegularizer
+        self.register_parameter("weight", "gradWeight", torch.empty(outputFrameSize, inputFrameSize * kernelW))
+        self.register_parameter("bias", "gradBias", torch.empty(outputFrameSize))
+        stdv = 1.0 / math.sqrt(kernelW * inputFrameSize)
+        RandomUniform(-stdv, stdv).init(self.weight)
+        RandomUniform(-stdv, stdv).init(self.bias)
+        if initWeight is not None:
+            self.weight.copy_(torch.as_tensor(initWeight).reshape(self.weight.shape))
+        if initBias is not None:
+            self.bias.copy_(torch.as_tensor(initBias).reshape(self.bias.shape))
+
+    def fn(self, x):
+        squeeze = x.dim() == 2
+        if squeeze:
+            x = x.unsqueeze(0)
+        w = self.weight.view(self.outputFrameSize, self.kernelW, self.inputFrameSize).permute(0, 2, 1)
+        y = F.conv1d(x.to(w.dtype).transpose(1, 2), w, self.bias, self.strideW).transpose(1, 2)
+        return y.squeeze(0) if squeeze else y
+
+
+class LocallyConnected2D(AutogradModule):
+    def __init__(self, nInputPlane, inputWidth, inputHeight, nOutputPlane, kernelW, kernelH, strideW=1, strideH=1,
+                 padW=0, padH=0, propagateBack=True, wRegularizer=None, bRegularizer=None, withBias=True,
+                 format="NCHW"):
+        super().__init__()
+        self.cin, self.cout = nInputPlane, nOutputPlane
+        self.k, self.s, self.p = (kernelH, kernelW), (strideH, strideW), (padH, padW)
+        self.oh = (inputHeight + 2 * padH - kernelH) // strideH + 1
+        self.ow = (inputWidth + 2 * padW - kernelW) // strideW + 1
+        self.format = format
+        L = self.oh * self.ow
+        self.register_parameter("weight", "gradWeight", torch.empty(L, nOutputPlane, nInputPlane * kernelH * kernelW))
+        if withBias:
+            self.register_parameter("bias", "gradBias", torch.empty(L, nOutputPlane))
+        else:
+            self.bias = None
+        stdv = 1.0 / math.sqrt(kernelW * kernelH * nInputPlane)
+        RandomUniform(-stdv, stdv).init(self.weight)
+        if self.bias is not None:
+            RandomUniform(-stdv, stdv).init(self.bias)
+
+    def fn(self, x):
+        if self.format == "NHWC":
+            x = x.permute(0, 3, 1, 2)
+        cols = F.unfold(x.to(self.weight.dtype), self.k, padding=self.p, stride=self.s)   # N, CKK, L
+        y = torch.einsum("nkl,lok->nol", cols, self.weight)
+        if self.bias is not None:
+            y = y + self.bias.t().unsqueeze(0)
+        y = y.reshape(x.shape[0], self.cout, self.oh, self.ow)
+        return y.permute(0, 2, 3, 1) if self.format == "NHWC" else y
+
+
+class LocallyConnected1D(AutogradModule):
+    def __init__(self, nInputFrame, inputFrameSize, outputFrameSize, kernelW, strideW=1, propagateBack=True,
+                 wRegularizer=None, bRegularizer=None):
+        super().__init__()
+        self.nOut = (nInputFrame - kernelW) // strideW + 1
+        self.kW, self.sW, self.inS, self.outS = kernelW, strideW, inputFrameSize, outputFrameSize
+        self.register_parameter("weight", "gradWeight", torch.empty(self.nOut, outputFrameSize, inputFrameSize * kernelW))
+        self.register_parameter("bias", "gradBias", torch.empty(self.nOut, outputFrameSize))
+        stdv = 1.0 / math.sqrt(kernelW * inputFrameSize)
+        RandomUniform(-stdv, stdv).init(self.weight)
+        RandomUniform(-stdv, stdv).init(self.bias)
+
+    def fn(self, x):
+        squeeze = x.dim() == 2
+        if squeeze:
+            x = x.unsqueeze(0)
+        win = x.to(self.weight.dtype).unfold(1, self.kW, self.sW)          # N, L, in, kW
+        win = win.permute(0, 1, 3, 2).reshape(x.shape[0], self.nOut, -1)
+        y = torch.einsum("nlk,lok->nlo", win, self.weight) + self.bias
+        return y.squeeze(0) if squeeze else y
+
+
+__all__ = ["SpatialConvolution", "SpatialShareConvolution", "SpatialDilatedConvolution", "SpatialFullConvolution",
+           "SpatialSeparableConvolution", "SpatialConvolutionMap", "VolumetricConvolution",
+           "VolumetricFullConvolution", "TemporalConvolution", "LocallyConnected1D", "LocallyConnected2D"]

@@ -1,0 +1,104 @@
+"""BatchNorm ops (GPU: csrc/batchnorm.hip; CPU: fp32 torch reference).
+
+Reference semantics (S/nn/SpatialBatchNormalization.scala:418-480, S/nn/BatchNormalization.scala:51):
+biased batch variance for normalisation, unbiased variance for the running estimate,
+``running = momentum * batch + (1 - momentum) * running``.
+"""
+import torch
+
+from . import native
+
+
+def _P(x):
+    return x.numel() // x.shape[1]
+
+
+def bn_forward_gpu(x, gamma, beta, rmean, rvar, eps, momentum, training, stats=None, res=None, relu=False,
+                   out=None, sync_fn=None):
+    """Returns (y, save_mean, save_invstd, scale).
+
+    x: (N, C, H, W) bf16 channels_last (or (N, C) bf16 contiguous). ``stats`` may hold the (sum, sumsq)
+    already produced by the preceding conv epilogue; otherwise they are computed here. ``sync_fn(stats)``
+    (sync-BN) may all-reduce the [2, C] fp32 stats buffer across replicas before finalize.
+    """
+    C = x.shape[1]
+    P = _P(x)
+    C_ = native.get()
+    dev = x.device
+    if out is None:
+        out = torch.empty_like(x)
+    scale = torch.empty(C, dtype=torch.float32, device=dev)
+    shift = torch.empty(C, dtype=torch.float32, device=dev)
+    smean = torch.empty(C, dtype=torch.float32, device=dev)
+    sinv = torch.empty(C, dtype=torch.float32, device=dev)
+    if training:
+        if stats is None:
+            stats = torch.zeros(2 * C, dtype=torch.float32, device=dev)
+            C_.bn_stats(x, stats, P, C)
+        if sync_fn is not None:
+            P = sync_fn(stats, P)
+    else:
+        stats = torch.zeros(2 * C, dtype=torch.float32, device=dev) if stats is None else stats
+    C_.bn_finalize(stats, gamma, beta, rmean, rvar, smean, sinv, scale, shift, P, C, float(eps), float(momentum),
+                   bool(training))
+    C_.bn_apply(x, scale, shift, res, out, _P(x), C, bool(relu))
+    return out, smean, sinv
+
+
+def bn_backward_gpu(dz, z, x, smean, sinv, gamma, dgamma, dbeta, training=True, need_dres=False, need_dx=True,
+                    sync_fn=None):
+    """Backward of y = relu?(bn(x) [+ res]).
+
+    dz: gradient w.r.t. the (post-relu) output; z: the forward output (ReLU mask) or None.
+    Returns (dx, dres) — dres is the gradient flowing into the residual branch (= masked dz).
+    """
+    C = x.shape[1]
+    P = _P(x)
+    C_ = native.get()
+    red = None
+    if training:
+        red = torch.zeros(2 * C, dtype=torch.float32, device=x.device)
+        C_.bn_bwd_reduce(dz, z, x, smean, red, P, C)
+        if sync_fn is not None:
+            P = sync_fn(red, P)
+    dx = torch.empty_like(x) if need_dx else None
+    dres = torch.empty_like(x) if need_dres else None
+    C_.bn_bwd_apply(dz, z, x, smean, sinv, gamma, red, dx, dres, dgamma, dbeta, P, C)
+    return dx, dres
+
+
+# ---------------------------------------------------------------- CPU reference
+def bn_forward_cpu(x, gamma, beta, rmean, rvar, eps, momentum, training):
+    dims = [0] + list(range(2, x.dim()))
+    shape = [1, -1] + [1] * (x.dim() - 2)
+    if training:
+        mean = x.mean(dim=dims)
+        var = x.var(dim=dims, unbiased=False)
+        n = x.numel() // x.shape[1]
+        if rmean is not None:
+            unb = var * n / max(n - 1, 1)
+            rmean.mul_(1 - momentum).add_(momentum * mean)
+            rvar.mul_(1 - momentum).add_(momentum * unb)
+    else:
+        mean, var = rmean, rvar
+    invstd = torch.rsqrt(var + eps)
+    xhat = (x - mean.view(shape)) * invstd.view(shape)
+    y = xhat
+    if gamma is not None:
+        y = y * gamma.view(shape) + beta.view(shape)
+    return y, mean, invstd
+
+
+def bn_backward_cpu(x, gy, mean, invstd, gamma, training=True):
+    dims = [0] + list(range(2, x.dim()))
+    shape = [1, -1] + [1] * (x.dim() - 2)
+    xhat = (x - mean.view(shape)) * invstd.view(shape)
+    g = gamma.view(shape) if gamma is not None else 1.0
+    dgamma = (gy * xhat).sum(dim=dims)
+    dbeta = gy.sum(dim=dims)
+    if training:
+        n = x.numel() // x.shape[1]
+        gx = g * invstd.view(shape) * (gy - dbeta.view(shape) / n - xhat * dgamma.view(shape) / n)
+    else:
+        gx = g * invstd.view(shape) * gy
+    return gx, dgamma, dbeta

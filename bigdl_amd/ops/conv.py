@@ -1,0 +1,126 @@
+"""Convolution / linear ops.
+
+GPU path: bf16 NHWC (torch ``channels_last``) activations and KRSC (channels_last) weights, dispatched to
+the implicit-GEMM MFMA kernels of ``csrc/conv_igemm.hip``. CPU path: fp32 torch reference (the analogue of
+the reference's MklBlas engine, used for the LeNet local-CPU configuration and as the numerics oracle).
+
+Reference: S/nn/SpatialConvolution.scala:253-520 (fwd / bwd-data / bwd-weight), S/nn/Linear.scala:84-160.
+"""
+import torch
+import torch.nn.functional as F
+
+from . import native
+
+CL = torch.channels_last
+BF16 = torch.bfloat16
+
+
+def out_size(inp, k, s, p, d=1, ceil=False):
+    eff = d * (k - 1) + 1
+    num = inp + 2 * p - eff
+    if ceil:
+        o = -(-num // s) + 1
+        if (o - 1) * s >= inp + p:
+            o -= 1
+        return o
+    return num // s + 1
+
+
+def to_nhwc_bf16(x, cpad=8):
+    """Convert an activation to the GPU compute layout (bf16 channels_last, C padded to a multiple of 8)."""
+    N, C, H, W = x.shape
+    Cp = -(-C // cpad) * cpad
+    if x.dtype == BF16 and Cp == C and x.is_contiguous(memory_format=CL):
+        return x
+    if x.dtype == torch.float32 and x.is_contiguous():
+        y = torch.empty((N, Cp, H, W), dtype=BF16, device=x.device, memory_format=CL)
+        native.get().nchw_to_nhwc(x, y, Cp)
+        return y
+    y = x.to(dtype=BF16, memory_format=CL)
+    if Cp != C:
+        y = F.pad(y, (0, 0, 0, 0, 0, Cp - C)).contiguous(memory_format=CL)
+    return y
+
+
+def weight_krsc_bf16(w, cpad=8):
+    """(K, C, R, S) weight -> bf16 channels_last with C padded to a multiple of ``cpad``."""
+    K, C, R, S = w.shape
+    Cp = -(-C // cpad) * cpad
+    if w.dtype == BF16 and Cp == C and w.is_contiguous(memory_format=CL):
+        return w
+    if Cp != C:
+        w = F.pad(w, (0, 0, 0, 0, 0, Cp - C))
+    return w.to(dtype=BF16, memory_format=CL)
+
+
+def conv2d_fwd(x, w16, bias, stride, pad, dil=(1, 1), relu=False, stats=None, out=None):
+    """y = conv(x, w) + bias (+ReLU); optionally accumulate per-channel (sum, sumsq) of y into ``stats``.
+
+    x: (N, C, H, W) bf16 channels_last (C % 8 == 0); w16: (K, C, R, S) bf16 channels_last.
+    """
+    N, C, H, W = x.shape
+    K, Cw, R, S = w16.shape
+    assert Cw == C, f"conv2d_fwd: channel mismatch {Cw} vs {C}"
+    sh, sw = stride
+    ph, pw = pad
+    dh, dw = dil
+    OH, OW = out_size(H, R, sh, ph, dh), out_size(W, S, sw, pw, dw)
+    if out is None:
+        out = torch.empty((N, K, OH, OW), dtype=BF16, device=x.device, memory_format=CL)
+    M = N * OH * OW
+    geo = [N, H, W, C, OH, OW, R, S, sh, -ph, dh, 1, sw, -pw, dw, 1, M, K, R * S * C, K]
+    native.get().conv_nt(x, w16, out, bias, stats, geo, relu)
+    return out
+
+
+def conv2d_dgrad(dy, w16t, x_shape, stride, pad, dil=(1, 1), out=None):
+    """dx = conv_transpose(dy, w). ``w16t`` is the (C, R, S, K)-ordered transposed weight (see transpose_w)."""
+    N, C, H, W = x_shape
+    _, K, OH, OW = dy.shape
+    R, S = w16t.shape[1], w16t.shape[2]
+    sh, sw = stride
+    ph, pw = pad
+    dh, dw = dil
+    if out is None:
+        out = torch.empty((N, C, H, W), dtype=BF16, device=dy.device, memory_format=CL)
+    geo = [N, OH, OW, K, H, W, R, S, 1, ph, -dh, sh, 1, pw, -dw, sw, N * H * W, C, R * S * K, C]
+    native.get().conv_nt(dy, w16t, out, None, None, geo, False)
+    return out
+
+
+def transpose_w(w16, out=None):
+    """(K, C, R, S) channels_last bf16 -> contiguous (C, R, S, K) bf16 for the data-gradient GEMM."""
+    K, C, R, S = w16.shape
+    if out is None:
+        out = torch.empty((C, R, S, K), dtype=BF16, device=w16.device)
+    native.get().transpose_krsc(w16, out, K, R * S, C)
+    return out
+
+
+def conv2d_wgrad(dy, x, dw32, dbias32, stride, pad, dil=(1, 1)):
+    """dW (fp32, (K, C, R, S) channels_last buffer) += conv weight gradient; dbias += sum(dy)."""
+    N, C, H, W = x.shape
+    _, K, OH, OW = dy.shape
+    Kw, Cw, R, S = dw32.shape
+    assert Kw == K and Cw == C
+    sh, sw = stride
+    ph, pw = pad
+    dh, dw = dil
+    geo = [N, H, W, C, OH, OW, R, S, sh, sw, ph, pw, dh, dw, N * OH * OW, K, R * S * C, K]
+    native.get().conv_wgrad(dy, x, dw32, dbias32, geo)
+
+
+# ------------------------------------------------------------------------------------------------
+# CPU reference path (fp32, NCHW): used by the local CPU engine and as the numerics oracle in tests.
+# ------------------------------------------------------------------------------------------------
+def conv2d_cpu(x, w, b, stride, pad, dil=(1, 1), groups=1):
+    return F.conv2d(x, w, b, stride=stride, padding=pad, dilation=dil, groups=groups)
+
+
+def conv2d_grads_cpu(x, w, gy, stride, pad, dil=(1, 1), groups=1, need_input=True):
+    gi = None
+    if need_input:
+        gi = torch.nn.grad.conv2d_input(x.shape, w, gy, stride=stride, padding=pad, dilation=dil, groups=groups)
+    gw = torch.nn.grad.conv2d_weight(x, w.shape, gy, stride=stride, padding=pad, dilation=dil, groups=groups)
+    gb = gy.sum(dim=(0, 2, 3))
+    return gi, gw, gb

@@ -1,0 +1,50 @@
+"""Pooling ops. GPU: csrc/elementwise.hip (NHWC bf16, 8 channels per lane, gather-form backward).
+
+Reference: NNPrimitive.maxPoolingForwardFloat / BackwardFloat (S/nn/NNPrimitive.scala:654-936),
+S/nn/SpatialMaxPooling.scala:62, S/nn/SpatialAveragePooling.scala:62.
+"""
+import torch
+
+from . import native
+from .conv import out_size
+
+CL = torch.channels_last
+
+
+def pool_out(H, W, kh, kw, sh, sw, ph, pw, ceil):
+    return out_size(H, kh, sh, ph, 1, ceil), out_size(W, kw, sw, pw, 1, ceil)
+
+
+def maxpool_fwd_gpu(x, kh, kw, sh, sw, ph, pw, ceil=False):
+    N, C, H, W = x.shape
+    OH, OW = pool_out(H, W, kh, kw, sh, sw, ph, pw, ceil)
+    y = torch.empty((N, C, OH, OW), dtype=x.dtype, device=x.device, memory_format=CL)
+    idx = torch.empty((N, C, OH, OW), dtype=torch.uint8, device=x.device, memory_format=CL)
+    native.get().maxpool_fwd(x, y, idx, [N, H, W, C, OH, OW, kh, kw, sh, sw, ph, pw])
+    return y, idx
+
+
+def maxpool_bwd_gpu(dy, idx, x_shape, kh, kw, sh, sw, ph, pw):
+    N, C, H, W = x_shape
+    OH, OW = dy.shape[2], dy.shape[3]
+    dy = dy.contiguous(memory_format=CL)
+    dx = torch.empty((N, C, H, W), dtype=dy.dtype, device=dy.device, memory_format=CL)
+    native.get().maxpool_bwd(dy, idx, dx, [N, H, W, C, OH, OW, kh, kw, sh, sw, ph, pw])
+    return dx
+
+
+def avgpool_fwd_gpu(x, kh, kw, sh, sw, ph, pw, ceil=False, count_pad=True):
+    N, C, H, W = x.shape
+    OH, OW = pool_out(H, W, kh, kw, sh, sw, ph, pw, ceil)
+    y = torch.empty((N, C, OH, OW), dtype=x.dtype, device=x.device, memory_format=CL)
+    native.get().avgpool_fwd(x, y, [N, H, W, C, OH, OW, kh, kw, sh, sw, ph, pw], bool(count_pad))
+    return y
+
+
+def avgpool_bwd_gpu(dy, x_shape, kh, kw, sh, sw, ph, pw, count_pad=True):
+    N, C, H, W = x_shape
+    OH, OW = dy.shape[2], dy.shape[3]
+    dy = dy.contiguous(memory_format=CL)
+    dx = torch.empty((N, C, H, W), dtype=dy.dtype, device=dy.device, memory_format=CL)
+    native.get().avgpool_bwd(dy, dx, [N, H, W, C, OH, OW, kh, kw, sh, sw, ph, pw], bool(count_pad))
+    return dx

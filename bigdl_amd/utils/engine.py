@@ -1,0 +1,154 @@
+"""Engine: process/device topology and runtime configuration.
+
+Reference: S/utils/Engine.scala:41-600 (``init`` :106-119, ``parseExecutorAndCore`` :485-567 which maps
+``local[N]`` → 1 node × N cores, engine type :210-216, thread pools :349-380).
+
+MI355X-native mapping: the unit of parallelism is a *device rank* — one process per GPU, wired together
+with ``torch.distributed`` over RCCL/xGMI (backend ``nccl``). ``local[N]`` therefore means N ranks on this
+node (launched by torchrun), not N CPU threads. With no GPU the engine runs the fp32 CPU path and uses the
+``gloo`` backend for multi-process jobs (that is how the distributed code is tested in CI).
+"""
+import os
+import re
+import threading
+
+import torch
+
+
+class EngineType:
+    GPU = "gpu"        # bf16 NHWC compute on gfx950 HIP kernels (the default when a GPU is present)
+    CPU = "cpu"        # fp32 torch CPU path (reference "MklBlas"-like local engine)
+
+
+class _Engine:
+    def __init__(self):
+        self._initialized = False
+        self.node_number = 1
+        self.core_number = 1
+        self.engine_type = None
+        self.master = None
+        self._lock = threading.Lock()
+        self.properties = {}
+        self._pg_owned = False
+
+    # ------------------------------------------------------------------ init
+    def init(self, master=None, node_number=None, core_number=None, engine_type=None, dist=None):
+        """Initialise the engine.
+
+        master: ``local[N]`` / ``local[*]`` string (Spark-master syntax, kept for API parity).
+        dist: force (True/False) initialising ``torch.distributed`` from the torchrun environment.
+        """
+        with self._lock:
+            if master is None:
+                master = os.environ.get("BIGDL_MASTER", None)
+            self.master = master
+            world = int(os.environ.get("WORLD_SIZE", "1"))
+            if master is not None:
+                n, c = parse_master(master)
+                self.node_number = n
+                self.core_number = c if c is not None else max(world, 1)
+            if node_number is not None:
+                self.node_number = node_number
+            if core_number is not None:
+                self.core_number = core_number
+            if engine_type is None:
+                engine_type = os.environ.get("BIGDL_ENGINE_TYPE")
+            if engine_type is None:
+                engine_type = EngineType.GPU if torch.cuda.is_available() else EngineType.CPU
+            self.engine_type = engine_type
+            if dist is None:
+                dist = world > 1
+            if dist:
+                self._init_dist()
+            self._initialized = True
+        return self
+
+    def _init_dist(self):
+        import torch.distributed as td
+
+        if td.is_initialized():
+            return
+        backend = "nccl" if (self.engine_type == EngineType.GPU and torch.cuda.is_available()) else "gloo"
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29500")
+        if backend == "nccl":
+            torch.cuda.set_device(self.local_rank())
+            td.init_process_group(backend, device_id=torch.device("cuda", self.local_rank()))
+        else:
+            td.init_process_group(backend)
+        self._pg_owned = True
+
+    def shutdown(self):
+        import torch.distributed as td
+
+        if self._pg_owned and td.is_initialized():
+            td.destroy_process_group()
+            self._pg_owned = False
+
+    # ------------------------------------------------------------------ queries
+    def isInitialized(self):
+        return self._initialized
+
+    def nodeNumber(self):
+        return self.node_number
+
+    def coreNumber(self):
+        return self.core_number
+
+    def getEngineType(self):
+        if self.engine_type is None:
+            return EngineType.GPU if torch.cuda.is_available() else EngineType.CPU
+        return self.engine_type
+
+    def setEngineType(self, t):
+        self.engine_type = t
+
+    def rank(self):
+        import torch.distributed as td
+
+        return td.get_rank() if td.is_available() and td.is_initialized() else int(os.environ.get("RANK", "0"))
+
+    def world_size(self):
+        import torch.distributed as td
+
+        return td.get_world_size() if td.is_available() and td.is_initialized() else 1
+
+    def local_rank(self):
+        return int(os.environ.get("LOCAL_RANK", "0"))
+
+    def device(self):
+        if self.getEngineType() == EngineType.GPU and torch.cuda.is_available():
+            return torch.device("cuda", self.local_rank() if torch.cuda.device_count() > 1 else 0)
+        return torch.device("cpu")
+
+    def checkSingleton(self):
+        return True
+
+    def setProperty(self, k, v):
+        self.properties[k] = v
+
+    def getProperty(self, k, default=None):
+        return self.properties.get(k, os.environ.get(k, default))
+
+
+def parse_master(master):
+    """Reference Engine.parseExecutorAndCore (S/utils/Engine.scala:485-567).
+
+    ``local`` → (1, 1); ``local[N]`` → (1, N); ``local[*]`` → (1, #GPUs or #CPUs);
+    ``spark://…``/``yarn``/``k8s`` style masters are accepted with an explicit core count from env.
+    """
+    m = re.fullmatch(r"local(?:\[(\*|\d+)\])?", master.strip())
+    if m:
+        g = m.group(1)
+        if g is None:
+            return 1, 1
+        if g == "*":
+            n = torch.cuda.device_count() if torch.cuda.is_available() else (os.cpu_count() or 1)
+            return 1, n
+        return 1, int(g)
+    nodes = int(os.environ.get("BIGDL_NODE_NUMBER", "1"))
+    cores = os.environ.get("BIGDL_CORE_NUMBER")
+    return nodes, int(cores) if cores else None
+
+
+Engine = _Engine()

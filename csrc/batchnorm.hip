@@ -1,0 +1,250 @@
+// BatchNorm for NHWC bf16 activations with fp32 statistics (gfx950).
+//
+// Replaces S/nn/SpatialBatchNormalization.scala (NCHW train fwd :1211, bwd :1048, NHWC :299-640) and
+// the MKL-DNN BN primitive (S/nn/mkldnn/SpatialBatchNormalization.scala:212-344). MI355X design:
+//  * two-phase reduce: every workgroup reduces a slab of rows for all channels in registers (16-byte
+//    loads = 8 channels per lane), combines rows through LDS, then one fp32 atomic per channel;
+//  * the stats phase is usually skipped entirely: the conv epilogue (conv_igemm.hip) already emits
+//    sum / sum-of-squares for the BN that follows it;
+//  * apply phase fuses the affine transform, the residual add of a ResNet block (CAddTable) and the
+//    trailing ReLU into one pass; backward fuses the ReLU mask and emits the residual-branch gradient.
+// Cross-replica sync-BN (S/utils/ParameterSynchronizer.scala) plugs in between reduce and finalize: the
+// [2][C] fp32 stats buffer is all-reduced over RCCL by the Python layer.
+#include "common.h"
+#include "kernels.h"
+
+namespace {
+
+// Generic per-channel reduction over P rows of C channels (C % 8 == 0).
+// MODE 0: stats     -> out[c] += x,          out[C+c] += x*x
+// MODE 1: bwd       -> out[c] += dy,         out[C+c] += dy*(x-mean)  with dy = dz * (z>0 ? 1 : 0 if z)
+template <int MODE>
+__global__ __launch_bounds__(256) void chan_reduce_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dz,
+                                                          const bf16_t* __restrict__ z, const float* __restrict__ mean,
+                                                          float* __restrict__ out, long P, int C, long rows_per_block) {
+  __shared__ float sm[256 * 16];
+  const int G = C >> 3;
+  const int tid = threadIdx.x;
+  const long rbeg = blockIdx.x * rows_per_block;
+  const long rend = min(P, rbeg + rows_per_block);
+  for (int gbase = 0; gbase < G; gbase += 256) {
+    const int gcount = min(256, G - gbase);
+    const int rpi = 256 / gcount;          // rows per iteration
+    const int g = gbase + tid % gcount, rsub = tid / gcount;
+    float a1[8], a2[8], mu[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { a1[e] = 0.f; a2[e] = 0.f; mu[e] = 0.f; }
+    if (MODE == 1 && rsub < rpi) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) mu[e] = mean[g * 8 + e];
+    }
+    if (rsub < rpi) {
+      for (long r = rbeg + rsub; r < rend; r += rpi) {
+        const size_t off = (size_t)r * C + g * 8;
+        const v4u vx = *reinterpret_cast<const v4u*>(x + off);
+        if (MODE == 0) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float l = lo_bf(vx[e]), h = hi_bf(vx[e]);
+            a1[2 * e] += l; a1[2 * e + 1] += h;
+            a2[2 * e] += l * l; a2[2 * e + 1] += h * h;
+          }
+        } else {
+          const v4u vd = *reinterpret_cast<const v4u*>(dz + off);
+          v4u vz = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
+          if (z) vz = *reinterpret_cast<const v4u*>(z + off);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float dl = lo_bf(vd[e]), dh = hi_bf(vd[e]);
+            if (z) { if (!(lo_bf(vz[e]) > 0.f)) dl = 0.f; if (!(hi_bf(vz[e]) > 0.f)) dh = 0.f; }
+            a1[2 * e] += dl; a1[2 * e + 1] += dh;
+            a2[2 * e] += dl * (lo_bf(vx[e]) - mu[2 * e]);
+            a2[2 * e + 1] += dh * (hi_bf(vx[e]) - mu[2 * e + 1]);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { sm[tid * 16 + e] = a1[e]; sm[tid * 16 + 8 + e] = a2[e]; }
+    __syncthreads();
+    // reduce over rsub for each (g, e, which)
+    for (int w = tid; w < gcount * 16; w += 256) {
+      const int gg = w >> 4, slot = w & 15;
+      float t = 0.f;
+      for (int rs = 0; rs < rpi; ++rs) t += sm[(rs * gcount + gg) * 16 + slot];
+      const int ch = (gbase + gg) * 8 + (slot & 7);
+      atomicAdd(out + (slot < 8 ? 0 : C) + ch, t);
+    }
+    __syncthreads();
+  }
+}
+
+__global__ void bn_finalize_kernel(const float* __restrict__ stats, const float* __restrict__ gamma,
+                                   const float* __restrict__ beta, float* run_mean, float* run_var, float* save_mean,
+                                   float* save_invstd, float* scale, float* shift, long P, int C, float eps,
+                                   float momentum, int training) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float mean, invstd;
+  if (training) {
+    mean = stats[c] / (float)P;
+    const float var = fmaxf(stats[C + c] / (float)P - mean * mean, 0.f);
+    invstd = rsqrtf(var + eps);
+    save_mean[c] = mean;
+    save_invstd[c] = invstd;
+    if (run_mean) {
+      const float unbiased = P > 1 ? var * (float)P / (float)(P - 1) : var;
+      run_mean[c] = momentum * mean + (1.f - momentum) * run_mean[c];
+      run_var[c] = momentum * unbiased + (1.f - momentum) * run_var[c];
+    }
+  } else {
+    mean = run_mean[c];
+    invstd = rsqrtf(run_var[c] + eps);
+    if (save_mean) { save_mean[c] = mean; save_invstd[c] = invstd; }
+  }
+  const float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
+  scale[c] = g * invstd;
+  shift[c] = b - mean * g * invstd;
+}
+
+__global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* __restrict__ x, const float* __restrict__ scale,
+                                                       const float* __restrict__ shift, const bf16_t* __restrict__ res,
+                                                       bf16_t* __restrict__ y, long ngran, int C, int relu) {
+  const int G = C >> 3;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < ngran; i += (long)gridDim.x * blockDim.x) {
+    const int c0 = (int)(i % G) * 8;
+    const v4u vx = reinterpret_cast<const v4u*>(x)[i];
+    v4u vr = {0u, 0u, 0u, 0u};
+    if (res) vr = reinterpret_cast<const v4u*>(res)[i];
+    const v4f s0 = *reinterpret_cast<const v4f*>(scale + c0), s1 = *reinterpret_cast<const v4f*>(scale + c0 + 4);
+    const v4f b0 = *reinterpret_cast<const v4f*>(shift + c0), b1 = *reinterpret_cast<const v4f*>(shift + c0 + 4);
+    const float sc[8] = {s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
+    const float sh[8] = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+    v4u o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float l = lo_bf(vx[e]) * sc[2 * e] + sh[2 * e];
+      float h = hi_bf(vx[e]) * sc[2 * e + 1] + sh[2 * e + 1];
+      if (res) { l += lo_bf(vr[e]); h += hi_bf(vr[e]); }
+      if (relu) { l = fmaxf(l, 0.f); h = fmaxf(h, 0.f); }
+      o[e] = pack2bf(l, h);
+    }
+    reinterpret_cast<v4u*>(y)[i] = o;
+  }
+}
+
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16_t* __restrict__ dz, const bf16_t* __restrict__ z,
+                                                           const bf16_t* __restrict__ x, const float* __restrict__ mean,
+                                                           const float* __restrict__ invstd, const float* __restrict__ gamma,
+                                                           const float* __restrict__ red, bf16_t* __restrict__ dx,
+                                                           bf16_t* __restrict__ dres, long ngran, int C, float invP,
+                                                           int training) {
+  const int G = C >> 3;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < ngran; i += (long)gridDim.x * blockDim.x) {
+    const int c0 = (int)(i % G) * 8;
+    const v4u vd = reinterpret_cast<const v4u*>(dz)[i];
+    v4u vz = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
+    if (z) vz = reinterpret_cast<const v4u*>(z)[i];
+    const v4u vx = reinterpret_cast<const v4u*>(x)[i];
+    v4u o, od;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float dy[2] = {lo_bf(vd[e]), hi_bf(vd[e])};
+      const float zz[2] = {lo_bf(vz[e]), hi_bf(vz[e])};
+      const float xx[2] = {lo_bf(vx[e]), hi_bf(vx[e])};
+      float r[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int c = c0 + 2 * e + h;
+        if (z && !(zz[h] > 0.f)) dy[h] = 0.f;
+        const float is = invstd[c];
+        const float g = gamma ? gamma[c] : 1.f;
+        if (training) {
+          const float mdy = red[c] * invP;
+          const float mdyx = red[C + c] * invP * is;       // mean(dy * xhat)
+          const float xh = (xx[h] - mean[c]) * is;
+          r[h] = g * is * (dy[h] - mdy - xh * mdyx);
+        } else {
+          r[h] = g * is * dy[h];
+        }
+      }
+      o[e] = pack2bf(r[0], r[1]);
+      od[e] = pack2bf(dy[0], dy[1]);
+    }
+    reinterpret_cast<v4u*>(dx)[i] = o;
+    if (dres) reinterpret_cast<v4u*>(dres)[i] = od;
+  }
+}
+
+__global__ void bn_param_grad_kernel(const float* __restrict__ red, const float* __restrict__ invstd, float* dgamma,
+                                     float* dbeta, int C) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  if (dgamma) dgamma[c] += red[C + c] * invstd[c];
+  if (dbeta) dbeta[c] += red[c];
+}
+
+int grid_for(long work, int per_block, int cap) {
+  long g = (work + per_block - 1) / per_block;
+  if (g > cap) g = cap;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+void launch_reduce(int mode, const bf16_t* x, const bf16_t* dz, const bf16_t* z, const float* mean, float* out, long P,
+                   int C, hipStream_t st) {
+  const int G = C >> 3;
+  const int rpi = 256 / (G < 256 ? G : 256);
+  long blocks = (P + rpi * 16 - 1) / (rpi * 16);   // >= 16 rows per thread
+  if (blocks > 2048) blocks = 2048;
+  if (blocks < 1) blocks = 1;
+  const long rpb = (P + blocks - 1) / blocks;
+  blocks = (P + rpb - 1) / rpb;
+  if (mode == 0) chan_reduce_kernel<0><<<(int)blocks, 256, 0, st>>>(x, dz, z, mean, out, P, C, rpb);
+  else chan_reduce_kernel<1><<<(int)blocks, 256, 0, st>>>(x, dz, z, mean, out, P, C, rpb);
+}
+
+}  // namespace
+
+extern "C" {
+
+void bigdl_bn_stats(const uint16_t* x, float* stats, long P, int C, hipStream_t st) {
+  launch_reduce(0, x, nullptr, nullptr, nullptr, stats, P, C, st);
+  HIP_LAUNCH_CHECK();
+}
+
+void bigdl_bn_finalize(const float* stats, const float* gamma, const float* beta, float* run_mean, float* run_var,
+                       float* save_mean, float* save_invstd, float* scale, float* shift, long P, int C, float eps,
+                       float momentum, int training, hipStream_t st) {
+  bn_finalize_kernel<<<(C + 255) / 256, 256, 0, st>>>(stats, gamma, beta, run_mean, run_var, save_mean, save_invstd,
+                                                       scale, shift, P, C, eps, momentum, training);
+  HIP_LAUNCH_CHECK();
+}
+
+void bigdl_bn_apply(const uint16_t* x, const float* scale, const float* shift, const uint16_t* res, uint16_t* y,
+                    long P, int C, int relu, hipStream_t st) {
+  const long ngran = P * (C >> 3);
+  bn_apply_kernel<<<grid_for(ngran, 256, 8192), 256, 0, st>>>(x, scale, shift, res, y, ngran, C, relu);
+  HIP_LAUNCH_CHECK();
+}
+
+void bigdl_bn_bwd_reduce(const uint16_t* dz, const uint16_t* z, const uint16_t* x, const float* mean, float* red,
+                         long P, int C, hipStream_t st) {
+  launch_reduce(1, x, dz, z, mean, red, P, C, st);
+  HIP_LAUNCH_CHECK();
+}
+
+void bigdl_bn_bwd_apply(const uint16_t* dz, const uint16_t* z, const uint16_t* x, const float* mean,
+                        const float* invstd, const float* gamma, const float* red, uint16_t* dx, uint16_t* dres,
+                        float* dgamma, float* dbeta, long P, int C, hipStream_t st) {
+  const long ngran = P * (C >> 3);
+  const int training = red != nullptr;
+  if (dx)
+    bn_bwd_apply_kernel<<<grid_for(ngran, 256, 8192), 256, 0, st>>>(dz, z, x, mean, invstd, gamma, red, dx, dres,
+                                                                    ngran, C, 1.f / (float)P, training);
+  if (training && (dgamma || dbeta))
+    bn_param_grad_kernel<<<(C + 255) / 256, 256, 0, st>>>(red, invstd, dgamma, dbeta, C);
+  HIP_LAUNCH_CHECK();
+}
+
+}  // extern "C"

@@ -1,0 +1,226 @@
+// Torch binding layer for the bigdl_amd HIP kernel library.
+//
+// Thin by design: Python (bigdl_amd/ops) owns allocation and buffer reuse (so whole training steps can be
+// captured into one HIP graph); this file only validates tensors, extracts raw pointers and launches the
+// C-ABI kernels of csrc/*.hip on the current HIP stream.
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+#include <vector>
+#include "kernels.h"
+
+namespace {
+
+using at::Tensor;
+using OptT = c10::optional<Tensor>;
+
+hipStream_t stream() { return at::hip::getCurrentHIPStream().stream(); }
+
+void check(const Tensor& t, at::ScalarType dt, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.scalar_type() == dt, name, " has dtype ", t.scalar_type(), ", expected ", dt);
+}
+const uint16_t* cbf(const Tensor& t, const char* n) { check(t, at::kBFloat16, n); return (const uint16_t*)t.data_ptr(); }
+uint16_t* mbf(const Tensor& t, const char* n) { check(t, at::kBFloat16, n); return (uint16_t*)t.data_ptr(); }
+const float* cf(const Tensor& t, const char* n) { check(t, at::kFloat, n); return (const float*)t.data_ptr(); }
+float* mf(const Tensor& t, const char* n) { check(t, at::kFloat, n); return (float*)t.data_ptr(); }
+const uint16_t* ocbf(const OptT& t, const char* n) { return (t && t->defined()) ? cbf(*t, n) : nullptr; }
+uint16_t* ombf(const OptT& t, const char* n) { return (t && t->defined()) ? mbf(*t, n) : nullptr; }
+const float* ocf(const OptT& t, const char* n) { return (t && t->defined()) ? cf(*t, n) : nullptr; }
+float* omf(const OptT& t, const char* n) { return (t && t->defined()) ? mf(*t, n) : nullptr; }
+
+// geo = [Nb, Hs, Ws, Cs, OH, OW, R, S, mul_h, off_h, step_h, div_h, mul_w, off_w, step_w, div_w, M, Ncol, Kdim, ldo]
+void conv_nt(const Tensor& src, const Tensor& wt, const Tensor& out, const OptT& bias, const OptT& stats,
+             std::vector<int64_t> geo, bool relu) {
+  TORCH_CHECK(geo.size() == 20, "conv_nt: bad geometry");
+  ConvArgs a;
+  a.src = cbf(src, "src"); a.wt = cbf(wt, "wt"); a.out = mbf(out, "out");
+  a.bias = ocf(bias, "bias"); a.stats = omf(stats, "stats");
+  int* f = &a.Nb;
+  for (int i = 0; i < 20; ++i) f[i] = (int)geo[i];
+  a.relu = relu ? 1 : 0;
+  TORCH_CHECK(src.numel() >= (int64_t)a.Nb * a.Hs * a.Ws * a.Cs, "conv_nt: src too small");
+  TORCH_CHECK(wt.numel() >= (int64_t)a.Ncol * a.Kdim, "conv_nt: weight too small");
+  TORCH_CHECK(out.numel() >= (int64_t)(a.M - 1) * a.ldo + a.Ncol, "conv_nt: out too small");
+  TORCH_CHECK(a.M == a.Nb * a.OH * a.OW, "conv_nt: M mismatch");
+  TORCH_CHECK(a.Kdim == a.R * a.S * a.Cs, "conv_nt: Kdim mismatch");
+  const int rc = bigdl_conv_nt(&a, stream());
+  TORCH_CHECK(rc == 0, "conv_nt: unsupported shape (channels must be a multiple of 8)");
+}
+
+// geo = [Nb, Hs, Ws, Cs, OH, OW, R, S, sh, sw, ph, pw, dh, dw, M, Ncol, Kdim, ldy]
+void conv_wgrad(const Tensor& dy, const Tensor& src, const Tensor& dw, const OptT& dbias, std::vector<int64_t> geo) {
+  TORCH_CHECK(geo.size() == 18, "conv_wgrad: bad geometry");
+  WgradArgs a;
+  a.dy = cbf(dy, "dy"); a.src = cbf(src, "src"); a.dw = mf(dw, "dw"); a.dbias = omf(dbias, "dbias");
+  int* f = &a.Nb;
+  for (int i = 0; i < 18; ++i) f[i] = (int)geo[i];
+  a.m_per_split = 0;
+  TORCH_CHECK(dw.numel() >= (int64_t)a.Ncol * a.Kdim, "conv_wgrad: dw too small");
+  TORCH_CHECK(a.M == a.Nb * a.OH * a.OW, "conv_wgrad: M mismatch");
+  TORCH_CHECK(dy.numel() >= (int64_t)(a.M - 1) * a.ldy + a.Ncol, "conv_wgrad: dy too small");
+  TORCH_CHECK(src.numel() >= (int64_t)a.Nb * a.Hs * a.Ws * a.Cs, "conv_wgrad: src too small");
+  const int rc = bigdl_conv_wgrad(&a, stream());
+  TORCH_CHECK(rc == 0, "conv_wgrad: unsupported shape (channels must be a multiple of 8)");
+}
+
+void transpose_krsc(const Tensor& w, const Tensor& wt, int64_t K, int64_t RS, int64_t C) {
+  TORCH_CHECK(w.numel() == K * RS * C && wt.numel() == K * RS * C, "transpose_krsc: size mismatch");
+  bigdl_transpose_krsc(cbf(w, "w"), mbf(wt, "wt"), (int)K, (int)RS, (int)C, stream());
+}
+
+void bn_stats(const Tensor& x, const Tensor& stats, int64_t P, int64_t C) {
+  TORCH_CHECK(C % 8 == 0 && x.numel() == P * C, "bn_stats: shape");
+  bigdl_bn_stats(cbf(x, "x"), mf(stats, "stats"), P, (int)C, stream());
+}
+void bn_finalize(const Tensor& stats, const OptT& gamma, const OptT& beta, const OptT& rmean, const OptT& rvar,
+                 const OptT& smean, const OptT& sinv, const Tensor& scale, const Tensor& shift, int64_t P, int64_t C,
+                 double eps, double momentum, bool training) {
+  bigdl_bn_finalize(cf(stats, "stats"), ocf(gamma, "gamma"), ocf(beta, "beta"), omf(rmean, "rmean"),
+                    omf(rvar, "rvar"), omf(smean, "smean"), omf(sinv, "sinv"), mf(scale, "scale"),
+                    mf(shift, "shift"), P, (int)C, (float)eps, (float)momentum, training ? 1 : 0, stream());
+}
+void bn_apply(const Tensor& x, const Tensor& scale, const Tensor& shift, const OptT& res, const Tensor& y, int64_t P,
+              int64_t C, bool relu) {
+  TORCH_CHECK(C % 8 == 0 && x.numel() == P * C && y.numel() == P * C, "bn_apply: shape");
+  bigdl_bn_apply(cbf(x, "x"), cf(scale, "scale"), cf(shift, "shift"), ocbf(res, "res"), mbf(y, "y"), P, (int)C,
+                 relu ? 1 : 0, stream());
+}
+void bn_bwd_reduce(const Tensor& dz, const OptT& z, const Tensor& x, const Tensor& mean, const Tensor& red, int64_t P,
+                   int64_t C) {
+  TORCH_CHECK(C % 8 == 0 && x.numel() == P * C && dz.numel() == P * C, "bn_bwd_reduce: shape");
+  bigdl_bn_bwd_reduce(cbf(dz, "dz"), ocbf(z, "z"), cbf(x, "x"), cf(mean, "mean"), mf(red, "red"), P, (int)C,
+                      stream());
+}
+void bn_bwd_apply(const Tensor& dz, const OptT& z, const Tensor& x, const Tensor& mean, const Tensor& invstd,
+                  const OptT& gamma, const OptT& red, const OptT& dx, const OptT& dres, const OptT& dgamma,
+                  const OptT& dbeta, int64_t P, int64_t C) {
+  bigdl_bn_bwd_apply(cbf(dz, "dz"), ocbf(z, "z"), cbf(x, "x"), cf(mean, "mean"), cf(invstd, "invstd"),
+                     ocf(gamma, "gamma"), ocf(red, "red"), ombf(dx, "dx"), ombf(dres, "dres"), omf(dgamma, "dgamma"),
+                     omf(dbeta, "dbeta"), P, (int)C, stream());
+}
+
+void relu_fwd(const Tensor& x, const Tensor& y) {
+  TORCH_CHECK(x.numel() == y.numel(), "relu: size");
+  bigdl_relu_fwd(cbf(x, "x"), mbf(y, "y"), x.numel(), stream());
+}
+void relu_bwd(const Tensor& dy, const Tensor& y, const Tensor& dx) {
+  TORCH_CHECK(dy.numel() == y.numel() && dx.numel() == y.numel(), "relu_bwd: size");
+  bigdl_relu_bwd(cbf(dy, "dy"), cbf(y, "y"), mbf(dx, "dx"), y.numel(), stream());
+}
+void add_bf16(const Tensor& a, const Tensor& b, const Tensor& y) {
+  TORCH_CHECK(a.numel() == b.numel() && a.numel() == y.numel(), "add: size");
+  bigdl_add_bf16(cbf(a, "a"), cbf(b, "b"), mbf(y, "y"), a.numel(), stream());
+}
+void nchw_to_nhwc(const Tensor& x, const Tensor& y, int64_t Cp) {
+  TORCH_CHECK(x.dim() == 4 && x.is_contiguous(), "nchw_to_nhwc: x must be contiguous NCHW");
+  const int N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  TORCH_CHECK(y.numel() == (int64_t)N * H * W * Cp && Cp >= C, "nchw_to_nhwc: y size");
+  bigdl_nchw_f32_to_nhwc_bf16(cf(x, "x"), mbf(y, "y"), N, C, H, W, (int)Cp, stream());
+}
+void cast_f32_bf16(const Tensor& x, const Tensor& y) {
+  TORCH_CHECK(x.numel() == y.numel() && x.is_contiguous() && y.is_contiguous(), "cast: size");
+  bigdl_cast_f32_bf16(cf(x, "x"), mbf(y, "y"), x.numel(), stream());
+}
+void cast_bf16_f32(const Tensor& x, const Tensor& y) {
+  TORCH_CHECK(x.numel() == y.numel() && x.is_contiguous() && y.is_contiguous(), "cast: size");
+  bigdl_cast_bf16_f32(cbf(x, "x"), mf(y, "y"), x.numel(), stream());
+}
+
+// pg = [N, H, W, C, OH, OW, kh, kw, sh, sw, ph, pw]
+void maxpool_fwd(const Tensor& x, const Tensor& y, const Tensor& idx, std::vector<int64_t> g) {
+  TORCH_CHECK(g.size() == 12 && g[3] % 8 == 0 && g[6] * g[7] <= 256, "maxpool: geometry");
+  TORCH_CHECK(idx.scalar_type() == at::kByte && idx.numel() == y.numel(), "maxpool: idx");
+  bigdl_maxpool_fwd(cbf(x, "x"), mbf(y, "y"), (uint8_t*)idx.data_ptr(), g[0], g[1], g[2], g[3], g[4], g[5], g[6], g[7],
+                    g[8], g[9], g[10], g[11], stream());
+}
+void maxpool_bwd(const Tensor& dy, const Tensor& idx, const Tensor& dx, std::vector<int64_t> g) {
+  TORCH_CHECK(g.size() == 12 && g[3] % 8 == 0, "maxpool_bwd: geometry");
+  bigdl_maxpool_bwd(cbf(dy, "dy"), (const uint8_t*)idx.data_ptr(), mbf(dx, "dx"), g[0], g[1], g[2], g[3], g[4], g[5],
+                    g[6], g[7], g[8], g[9], g[10], g[11], stream());
+}
+void avgpool_fwd(const Tensor& x, const Tensor& y, std::vector<int64_t> g, bool count_pad) {
+  TORCH_CHECK(g.size() == 12 && g[3] % 8 == 0, "avgpool: geometry");
+  bigdl_avgpool_fwd(cbf(x, "x"), mbf(y, "y"), g[0], g[1], g[2], g[3], g[4], g[5], g[6], g[7], g[8], g[9], g[10], g[11],
+                    count_pad ? 1 : 0, stream());
+}
+void avgpool_bwd(const Tensor& dy, const Tensor& dx, std::vector<int64_t> g, bool count_pad) {
+  TORCH_CHECK(g.size() == 12 && g[3] % 8 == 0, "avgpool_bwd: geometry");
+  bigdl_avgpool_bwd(cbf(dy, "dy"), mbf(dx, "dx"), g[0], g[1], g[2], g[3], g[4], g[5], g[6], g[7], g[8], g[9], g[10],
+                    g[11], count_pad ? 1 : 0, stream());
+}
+
+void softmax_xent(const Tensor& logits, const Tensor& labels, const OptT& loss, const OptT& dlogits, double label_base,
+                  double grad_scale) {
+  TORCH_CHECK(logits.dim() == 2 && logits.is_contiguous(), "softmax_xent: logits must be contiguous [B, K]");
+  const int B = logits.size(0), K = logits.size(1);
+  TORCH_CHECK(labels.numel() == B, "softmax_xent: labels");
+  const bool bf = logits.scalar_type() == at::kBFloat16;
+  const uint16_t* lb = bf ? cbf(logits, "logits") : nullptr;
+  const float* lf = bf ? nullptr : cf(logits, "logits");
+  uint16_t* db = nullptr; float* df = nullptr;
+  if (dlogits && dlogits->defined()) {
+    TORCH_CHECK(dlogits->numel() == logits.numel(), "softmax_xent: dlogits");
+    if (dlogits->scalar_type() == at::kBFloat16) db = mbf(*dlogits, "dlogits"); else df = mf(*dlogits, "dlogits");
+  }
+  bigdl_softmax_xent(lb, lf, cf(labels, "labels"), omf(loss, "loss"), db, df, B, K, (float)label_base,
+                     (float)grad_scale, stream());
+}
+
+void sgd_step(const Tensor& w, const Tensor& g, const OptT& mom, const OptT& w16, double lr, double wd,
+              double momentum, double dampening, bool nesterov, bool first) {
+  TORCH_CHECK(w.numel() == g.numel(), "sgd: size");
+  bigdl_sgd_step(mf(w, "w"), cf(g, "g"), omf(mom, "mom"), ombf(w16, "w16"), w.numel(), (float)lr, (float)wd,
+                 (float)momentum, (float)dampening, nesterov ? 1 : 0, first ? 1 : 0, stream());
+}
+void adam_step(const Tensor& w, const Tensor& g, const Tensor& m, const Tensor& v, const OptT& w16, double lr,
+               double b1, double b2, double eps, double wd, double bc1, double bc2) {
+  bigdl_adam_step(mf(w, "w"), cf(g, "g"), mf(m, "m"), mf(v, "v"), ombf(w16, "w16"), w.numel(), (float)lr, (float)b1,
+                  (float)b2, (float)eps, (float)wd, (float)bc1, (float)bc2, stream());
+}
+void sumsq(const Tensor& x, const Tensor& out) { bigdl_sumsq(cf(x, "x"), mf(out, "out"), x.numel(), stream()); }
+void scale_f32(const Tensor& x, const OptT& sdev, double s) {
+  bigdl_scale_f32(mf(x, "x"), x.numel(), ocf(sdev, "scale"), (float)s, stream());
+}
+void lstm_cell_fwd(const Tensor& gates, const OptT& c_prev, const Tensor& c, const Tensor& h, const Tensor& act) {
+  const int B = gates.size(0), H = gates.size(1) / 4;
+  bigdl_lstm_cell_fwd(cf(gates, "gates"), ocf(c_prev, "c_prev"), mf(c, "c"), mf(h, "h"), mf(act, "act"), B, H,
+                      stream());
+}
+void lstm_cell_bwd(const Tensor& act, const OptT& c_prev, const Tensor& c, const OptT& dh, const OptT& dc_next,
+                   const Tensor& dgates, const OptT& dc_prev) {
+  const int B = act.size(0), H = act.size(1) / 4;
+  bigdl_lstm_cell_bwd(cf(act, "act"), ocf(c_prev, "c_prev"), cf(c, "c"), ocf(dh, "dh"), ocf(dc_next, "dc_next"),
+                      mf(dgates, "dgates"), omf(dc_prev, "dc_prev"), B, H, stream());
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "bigdl_amd native HIP kernels for gfx950 (MI355X)";
+  m.def("conv_nt", &conv_nt);
+  m.def("conv_wgrad", &conv_wgrad);
+  m.def("transpose_krsc", &transpose_krsc);
+  m.def("bn_stats", &bn_stats);
+  m.def("bn_finalize", &bn_finalize);
+  m.def("bn_apply", &bn_apply);
+  m.def("bn_bwd_reduce", &bn_bwd_reduce);
+  m.def("bn_bwd_apply", &bn_bwd_apply);
+  m.def("relu_fwd", &relu_fwd);
+  m.def("relu_bwd", &relu_bwd);
+  m.def("add_bf16", &add_bf16);
+  m.def("nchw_to_nhwc", &nchw_to_nhwc);
+  m.def("cast_f32_bf16", &cast_f32_bf16);
+  m.def("cast_bf16_f32", &cast_bf16_f32);
+  m.def("maxpool_fwd", &maxpool_fwd);
+  m.def("maxpool_bwd", &maxpool_bwd);
+  m.def("avgpool_fwd", &avgpool_fwd);
+  m.def("avgpool_bwd", &avgpool_bwd);
+  m.def("softmax_xent", &softmax_xent);
+  m.def("sgd_step", &sgd_step);
+  m.def("adam_step", &adam_step);
+  m.def("sumsq", &sumsq);
+  m.def("scale_f32", &scale_f32);
+  m.def("lstm_cell_fwd", &lstm_cell_fwd);
+  m.def("lstm_cell_bwd", &lstm_cell_bwd);
+  m.attr("arch") = "gfx950";
+}

@@ -1,0 +1,461 @@
+// Implicit-GEMM convolution for gfx950 (MI355X), NHWC bf16 activations, fp32 accumulation.
+//
+// Replaces the reference's per-sample im2col + MKL sgemm path
+// (S/nn/SpatialConvolution.scala:253-362 updateOutput, :364-426 updateGradInput, :435-520
+// accGradParameters; NNPrimitive.im2colFloat S/nn/NNPrimitive.scala:108) and the MKL-DNN
+// conv primitives (S/nn/mkldnn/SpatialConvolution.scala:331-589). Design is MI355X-first:
+//
+//  * one kernel family for fwd and dgrad ("NT" GEMM: C[m][n] = sum_k A[m][k] * B[n][k]) where the
+//    A rows are gathered on the fly from the NHWC source tensor (no im2col buffer in HBM): a 16-byte
+//    granule of 8 channels of one input pixel is one lane's global load;
+//  * MFMA v_mfma_f32_16x16x32_bf16, 64-lane waves, 4 waves per workgroup, BK = 64;
+//  * register-staged, double-buffered LDS tiles with an XOR swizzle of the 16-byte slot by row so the
+//    ds_read_b128 fragment reads are spread across banks (cdna_hip_programming.md T2);
+//  * operands swapped in the MFMA (weights as the "A" operand) so each lane ends up owning four
+//    consecutive output channels of one pixel: 8-byte bf16 stores along the NHWC channel dim;
+//  * fused epilogue: + bias, ReLU, and per-channel BatchNorm statistics (sum, sum of squares) reduced
+//    across the 16 lanes that share a channel and added with one atomic per channel per wave;
+//  * weight-gradient kernel ("TN" GEMM over the pixel dimension) reads both operands from row-major
+//    NHWC tiles with the gfx950 transposed LDS read ds_read_b64_tr_b16, split-K over pixels with
+//    fp32 atomics into the flat fp32 gradient buffer (bias gradient folded into the same pass);
+//  * XCD-aware bijective block remap so neighbouring tiles share an XCD L2.
+#include "common.h"
+#include "kernels.h"
+
+
+namespace {
+
+constexpr int BK = 64;          // K elements per LDS stage (8 granules of 16 B per row)
+
+template <int BM, int BN, int WM, bool FASTK, bool DIV>
+__global__ __launch_bounds__(256, 2) void conv_nt_kernel(ConvArgs a) {
+  constexpr int WN = 4 / WM;
+  constexpr int TM = BM / WM, TN = BN / WN;      // per-wave tile
+  constexpr int MI = TM / 16, NI = TN / 16;      // MFMA tiles per wave
+  constexpr int AROWS = BM / 32, BROWS = BN / 32; // rows loaded per thread per stage
+  constexpr int STAGE = (BM + BN) * BK;           // bf16 elements per LDS stage
+  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int tiles_n = (a.Ncol + BN - 1) / BN;
+  const int tiles_m = (a.M + BM - 1) / BM;
+  const int nwg = tiles_m * tiles_n;
+  const int bid = xcd_remap(blockIdx.x, nwg);
+  // n fastest: the tiles_n blocks that share one A panel run back to back (same XCD after remap)
+  const int tm = bid / tiles_n, tn = bid % tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  // ---- per-thread A-row precompute (rows fixed through the K loop) ----
+  const int lrow = tid >> 3, lg = tid & 7;
+  int a_pix[AROWS], a_h[AROWS], a_w[AROWS];
+  const int ohw = a.OH * a.OW;
+#pragma unroll
+  for (int i = 0; i < AROWS; ++i) {
+    const int m = m0 + lrow + 32 * i;
+    if (m < a.M) {
+      const int nb = m / ohw, rem = m - nb * ohw;
+      const int oh = rem / a.OW, ow = rem - oh * a.OW;
+      a_pix[i] = nb * a.Hs * a.Ws;
+      a_h[i] = oh * a.mul_h + a.off_h;
+      a_w[i] = ow * a.mul_w + a.off_w;
+    } else {
+      a_pix[i] = 0; a_h[i] = -(1 << 28); a_w[i] = -(1 << 28);
+    }
+  }
+  const bf16_t* wrow[BROWS];
+  bool bvalid[BROWS];
+#pragma unroll
+  for (int i = 0; i < BROWS; ++i) {
+    const int n = n0 + lrow + 32 * i;
+    bvalid[i] = n < a.Ncol;
+    wrow[i] = a.wt + (size_t)(bvalid[i] ? n : 0) * a.Kdim;
+  }
+
+  v4u ra[AROWS], rb[BROWS];
+  const int SC = a.S * a.Cs;
+  auto gload = [&](int kt) {
+    int kk, r, s, c;
+    bool kvalid;
+    if constexpr (FASTK) {
+      const int k0 = kt * BK;                 // whole BK chunk shares (r, s)
+      r = k0 / SC; const int rem = k0 - r * SC;
+      s = rem / a.Cs; c = rem - s * a.Cs + lg * 8;
+      kk = k0 + lg * 8; kvalid = true;
+    } else {
+      kk = kt * BK + lg * 8;
+      kvalid = kk < a.Kdim;
+      const int kc = kvalid ? kk : 0;
+      r = kc / SC; const int rem = kc - r * SC;
+      s = rem / a.Cs; c = rem - s * a.Cs;
+    }
+#pragma unroll
+    for (int i = 0; i < AROWS; ++i) {
+      int ch = a_h[i] + r * a.step_h, cw = a_w[i] + s * a.step_w;
+      bool ok = kvalid;
+      if constexpr (DIV) {
+        ok = ok && ch >= 0 && cw >= 0 && (ch % a.div_h) == 0 && (cw % a.div_w) == 0;
+        ch /= a.div_h; cw /= a.div_w;
+      }
+      ok = ok && (unsigned)ch < (unsigned)a.Hs && (unsigned)cw < (unsigned)a.Ws;
+      v4u v = {0u, 0u, 0u, 0u};
+      if (ok) v = *reinterpret_cast<const v4u*>(a.src + ((size_t)(a_pix[i] + ch * a.Ws + cw) * a.Cs + c));
+      ra[i] = v;
+    }
+#pragma unroll
+    for (int i = 0; i < BROWS; ++i) {
+      v4u v = {0u, 0u, 0u, 0u};
+      if (bvalid[i] && kvalid) v = *reinterpret_cast<const v4u*>(wrow[i] + kk);
+      rb[i] = v;
+    }
+  };
+  auto swz = [](int row, int g) { return row * BK + ((g ^ (row & 7)) << 3); };
+  auto swrite = [&](int buf) {
+    bf16_t* A = lds + buf * STAGE;
+    bf16_t* B = A + BM * BK;
+#pragma unroll
+    for (int i = 0; i < AROWS; ++i) *reinterpret_cast<v4u*>(A + swz(lrow + 32 * i, lg)) = ra[i];
+#pragma unroll
+    for (int i = 0; i < BROWS; ++i) *reinterpret_cast<v4u*>(B + swz(lrow + 32 * i, lg)) = rb[i];
+  };
+
+  v4f acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (a.Kdim + BK - 1) / BK;
+  gload(0);
+  swrite(0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) gload(kt + 1);   // next stage in flight during the MFMAs
+    const bf16_t* A = lds + cur * STAGE;
+    const bf16_t* B = A + BM * BK;
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks) {
+      v8s fa[MI], fb[NI];
+      const int g = ks * 4 + (lane >> 4);
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int row = wm * TM + i * 16 + (lane & 15);
+        fa[i] = *reinterpret_cast<const v8s*>(A + swz(row, g));
+      }
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        const int row = wn * TN + j * 16 + (lane & 15);
+        fb[j] = *reinterpret_cast<const v8s*>(B + swz(row, g));
+      }
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < nk) swrite(cur ^ 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue: D[n][m], lane owns n = 4*(lane>>4)+j (j=0..3), m = lane&15 ----
+  const bool vec_ok = (a.Ncol & 3) == 0 && (a.ldo & 3) == 0;
+#pragma unroll
+  for (int j = 0; j < NI; ++j) {
+    const int nb = n0 + wn * TN + j * 16 + (lane >> 4) * 4;
+    float bs[4] = {0.f, 0.f, 0.f, 0.f};
+    if (a.bias) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) bs[e] = (nb + e < a.Ncol) ? a.bias[nb + e] : 0.f;
+    }
+    float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int m = m0 + wm * TM + i * 16 + (lane & 15);
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float t = acc[i][j][e] + bs[e];
+        if (a.relu) t = fmaxf(t, 0.f);
+        v[e] = t;
+      }
+      const unsigned p0 = pack2bf(v[0], v[1]), p1 = pack2bf(v[2], v[3]);
+      if (m < a.M) {
+        if (a.stats) {
+          s1[0] += lo_bf(p0); s1[1] += hi_bf(p0); s1[2] += lo_bf(p1); s1[3] += hi_bf(p1);
+          s2[0] += lo_bf(p0) * lo_bf(p0); s2[1] += hi_bf(p0) * hi_bf(p0);
+          s2[2] += lo_bf(p1) * lo_bf(p1); s2[3] += hi_bf(p1) * hi_bf(p1);
+        }
+        bf16_t* o = a.out + (size_t)m * a.ldo + nb;
+        if (vec_ok && nb + 3 < a.Ncol) {
+          *reinterpret_cast<v2u*>(o) = v2u{p0, p1};
+        } else {
+          const unsigned pp[2] = {p0, p1};
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (nb + e < a.Ncol) o[e] = (bf16_t)((pp[e >> 1] >> ((e & 1) * 16)) & 0xffff);
+        }
+      }
+    }
+    if (a.stats) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          s1[e] += __shfl_xor(s1[e], o, 64);
+          s2[e] += __shfl_xor(s2[e], o, 64);
+        }
+      }
+      if ((lane & 15) == 0) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (nb + e < a.Ncol) {
+            atomicAdd(a.stats + nb + e, s1[e]);
+            atomicAdd(a.stats + a.Ncol + nb + e, s2[e]);
+          }
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Weight gradient: dW[n][kk] += sum_m dY[m][n] * im2col(X)[m][kk]   (fp32 out, split-K over m)
+// ------------------------------------------------------------------------------------------------
+
+constexpr int WBM = 64;    // pixels (reduction) per LDS stage
+constexpr int WT = 128;    // output tile: 128 n x 128 kk
+
+__device__ __forceinline__ int wswz(int row, int col) {  // [WBM][128] bf16 image, 16 slots/row
+  return row * WT + ((((col >> 3) ^ (row & 15))) << 3) + (col & 7);
+}
+
+__global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(WgradArgs a) {
+  constexpr int STAGE = 2 * WBM * WT;
+  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * STAGE];
+  __shared__ float red[256 * 8];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wk = wave >> 1, wn = wave & 1;     // wave tile: 64 kk x 64 n
+  const int tiles_n = (a.Ncol + WT - 1) / WT, tiles_k = (a.Kdim + WT - 1) / WT;
+  const int ntile = tiles_n * tiles_k;
+  const int t = xcd_remap(blockIdx.x, ntile);
+  const int tk = t / tiles_n, tn = t % tiles_n;
+  const int n0 = tn * WT, k0 = tk * WT;
+  const int mbeg = blockIdx.y * a.m_per_split;
+  const int mend = min(a.M, mbeg + a.m_per_split);
+  if (mbeg >= mend) return;
+
+  // loader mapping: row = tid>>4 (+16*i), granule g = tid&15 (8 elements)
+  const int lrow = tid >> 4, lg = tid & 15;
+  const int nn = n0 + lg * 8;
+  const bool nvalid = nn < a.Ncol;
+  const int kk = k0 + lg * 8;
+  const bool kvalid = kk < a.Kdim;
+  const int SC = a.S * a.Cs;
+  int r = 0, s = 0, c = 0;
+  if (kvalid) { r = kk / SC; int rem = kk - r * SC; s = rem / a.Cs; c = rem - s * a.Cs; }
+  const int roff = r * a.dh - a.ph, soff = s * a.dwl - a.pw;
+
+  // per-row pixel coordinates, advanced incrementally by WBM each stage
+  int pnb[4], poh[4], pow_[4];
+  const int ohw = a.OH * a.OW;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = mbeg + lrow + 16 * i;
+    pnb[i] = m / ohw; const int rem = m - pnb[i] * ohw;
+    poh[i] = rem / a.OW; pow_[i] = rem - poh[i] * a.OW;
+  }
+  v4u rdy[4], rx[4];
+  float bsum[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) bsum[e] = 0.f;
+  const bool do_bias = a.dbias != nullptr && tk == 0;
+
+  auto gload = [&](int mb) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = mb + lrow + 16 * i;
+      v4u vd = {0u, 0u, 0u, 0u}, vx = {0u, 0u, 0u, 0u};
+      if (m < mend) {
+        if (nvalid) vd = *reinterpret_cast<const v4u*>(a.dy + (size_t)m * a.ldy + nn);
+        const int ih = poh[i] * a.sh + roff, iw = pow_[i] * a.sw + soff;
+        if (kvalid && (unsigned)ih < (unsigned)a.Hs && (unsigned)iw < (unsigned)a.Ws)
+          vx = *reinterpret_cast<const v4u*>(
+              a.src + ((size_t)(pnb[i] * a.Hs + ih) * a.Ws + iw) * a.Cs + c);
+      }
+      rdy[i] = vd; rx[i] = vx;
+      // advance this row's pixel by WBM
+      pow_[i] += WBM;
+      if (pow_[i] >= a.OW) {
+        const int qw = pow_[i] / a.OW;
+        pow_[i] -= qw * a.OW;
+        poh[i] += qw;
+        if (poh[i] >= a.OH) { const int qh = poh[i] / a.OH; poh[i] -= qh * a.OH; pnb[i] += qh; }
+      }
+    }
+  };
+  auto swrite = [&](int buf) {
+    bf16_t* D = lds + buf * STAGE;
+    bf16_t* X = D + WBM * WT;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = lrow + 16 * i;
+      *reinterpret_cast<v4u*>(D + wswz(row, lg * 8)) = rdy[i];
+      *reinterpret_cast<v4u*>(X + wswz(row, lg * 8)) = rx[i];
+      if (do_bias) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { bsum[2 * e] += lo_bf(rdy[i][e]); bsum[2 * e + 1] += hi_bf(rdy[i][e]); }
+      }
+    }
+  };
+
+  v4f acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+
+  // transposed-read lane geometry (ds_read_b64_tr_b16): lane 4q+p of each 16-lane group addresses
+  // row q, columns 4p..4p+3 of a 4x16 block; lane i receives column i of the 4 rows.
+  const int G = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+
+  gload(mbeg);
+  swrite(0);
+  __syncthreads();
+  int cur = 0;
+  for (int mb = mbeg; mb < mend; mb += WBM) {
+    const bool more = mb + WBM < mend;
+    if (more) gload(mb + WBM);
+    const bf16_t* D = lds + cur * STAGE;
+    const bf16_t* X = D + WBM * WT;
+#pragma unroll
+    for (int ks = 0; ks < WBM / 32; ++ks) {
+      v8s fx[4], fd[4];
+      const int rbase = ks * 32 + 8 * G + q;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int col = wk * 64 + i * 16 + 4 * p;
+        v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(v4s))(X + wswz(rbase, col)));
+        v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(v4s))(X + wswz(rbase + 4, col)));
+        fx[i] = v8s{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int col = wn * 64 + j * 16 + 4 * p;
+        v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(v4s))(D + wswz(rbase, col)));
+        v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(v4s))(D + wswz(rbase + 4, col)));
+        fd[j] = v8s{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fx[i], fd[j], acc[i][j], 0, 0, 0);
+    }
+    if (more) swrite(cur ^ 1);
+    __syncthreads();
+    cur ^= 1;
+  }
+
+  // D[kk][n]: lane holds kk = 4*(lane>>4)+e (e=0..3) for n = lane&15
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int kb = k0 + wk * 64 + i * 16 + 4 * (lane >> 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = n0 + wn * 64 + j * 16 + (lane & 15);
+      if (n < a.Ncol) {
+        float* o = a.dw + (size_t)n * a.Kdim + kb;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (kb + e < a.Kdim) atomicAdd(o + e, acc[i][j][e]);
+      }
+    }
+  }
+  if (do_bias) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) red[e * 256 + tid] = bsum[e];
+    __syncthreads();
+    if (tid < 128) {  // 16 granules x 8 channels; sum over the 16 row-groups
+      const int g = tid >> 3, e = tid & 7;
+      float tot = 0.f;
+      for (int rg = 0; rg < 16; ++rg) tot += red[e * 256 + rg * 16 + g];
+      const int n = n0 + g * 8 + e;
+      if (n < a.Ncol) atomicAdd(a.dbias + n, tot);
+    }
+  }
+}
+
+__global__ void transpose_krsc_kernel(const bf16_t* __restrict__ w, bf16_t* __restrict__ wt, int K, int RS,
+                                      int C) {
+  // wt[c][rs][k] = w[k][rs][c]
+  const size_t total = (size_t)K * RS * C;
+  for (size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x; idx < total; idx += (size_t)gridDim.x * blockDim.x) {
+    const int k = idx % K;
+    const size_t t = idx / K;
+    const int rs = t % RS;
+    const int c = t / RS;
+    wt[idx] = w[((size_t)k * RS + rs) * C + c];
+  }
+}
+
+template <int BM, int BN, int WM>
+void launch_nt(const ConvArgs& a, bool fastk, bool div, hipStream_t st) {
+  const int nwg = ((a.M + BM - 1) / BM) * ((a.Ncol + BN - 1) / BN);
+  dim3 grid(nwg), block(256);
+  if (fastk) {
+    if (div) conv_nt_kernel<BM, BN, WM, true, true><<<grid, block, 0, st>>>(a);
+    else conv_nt_kernel<BM, BN, WM, true, false><<<grid, block, 0, st>>>(a);
+  } else {
+    if (div) conv_nt_kernel<BM, BN, WM, false, true><<<grid, block, 0, st>>>(a);
+    else conv_nt_kernel<BM, BN, WM, false, false><<<grid, block, 0, st>>>(a);
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+// Forward or data-gradient implicit GEMM. Returns 0 on success, negative on unsupported shapes.
+int bigdl_conv_nt(const ConvArgs* a, hipStream_t st) {
+  if (a->Cs % 8 != 0 || a->Kdim % 8 != 0) return -1;
+  const bool fastk = (a->Cs % BK) == 0;
+  const bool div = a->div_h > 1 || a->div_w > 1;
+  if (a->Ncol <= 64) launch_nt<128, 64, 2>(*a, fastk, div, st);
+  else launch_nt<128, 128, 2>(*a, fastk, div, st);
+  HIP_LAUNCH_CHECK();
+  return 0;
+}
+
+int bigdl_conv_wgrad(const WgradArgs* a_in, hipStream_t st) {
+  WgradArgs a = *a_in;
+  if (a.Cs % 8 != 0 || a.Ncol % 8 != 0 || a.Kdim % 8 != 0) return -1;
+  const int tiles = ((a.Ncol + WT - 1) / WT) * ((a.Kdim + WT - 1) / WT);
+  // ~2 workgroups per CU in one dispatch wave; every split adds a full fp32 atomic pass over its
+  // tile, so also cap the atomic traffic (splits x |dW| x 4 B) at ~32 MB (~25 us at the chip rate).
+  int splits = (512 + tiles - 1) / tiles;
+  const long tile_bytes = (long)tiles * WT * WT * 4;
+  const int cap_atomic = (int)((32l << 20) / tile_bytes);
+  if (splits > cap_atomic) splits = cap_atomic;
+  const int maxsplit = (a.M + 4 * WBM - 1) / (4 * WBM);   // >= 4 LDS stages per split
+  if (splits > maxsplit) splits = maxsplit;
+  if (splits < 1) splits = 1;
+  int mps = (a.M + splits - 1) / splits;
+  mps = (mps + WBM - 1) / WBM * WBM;
+  splits = (a.M + mps - 1) / mps;
+  a.m_per_split = mps;
+  dim3 grid(tiles, splits), block(256);
+  conv_wgrad_kernel<<<grid, block, 0, st>>>(a);
+  HIP_LAUNCH_CHECK();
+  return 0;
+}
+
+void bigdl_transpose_krsc(const bf16_t* w, bf16_t* wt, int K, int RS, int C, hipStream_t st) {
+  const size_t total = (size_t)K * RS * C;
+  int blocks = (int)((total + 255) / 256);
+  if (blocks > 4096) blocks = 4096;
+  transpose_krsc_kernel<<<blocks, 256, 0, st>>>(w, wt, K, RS, C);
+  HIP_LAUNCH_CHECK();
+}
+
+}  // extern "C"

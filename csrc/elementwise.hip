@@ -1,0 +1,464 @@
+// Vectorized elementwise / layout / pooling / loss / optimizer kernels for gfx950.
+//
+// Reference counterparts: ReLU/Threshold (S/nn/ReLU.scala:42, S/nn/Threshold.scala:38), CAddTable
+// (S/nn/CAddTable.scala:82), NNPrimitive.maxPoolingForwardFloat/BackwardFloat (S/nn/NNPrimitive.scala:654,
+// :714, NHWC :841, :936), SpatialAveragePooling (S/nn/SpatialAveragePooling.scala:323), LogSoftMax +
+// ClassNLLCriterion (S/nn/LogSoftMax.scala:49, S/nn/ClassNLLCriterion.scala:69 = CrossEntropyCriterion
+// S/nn/CrossEntropyCriterion.scala:31), SGD / Adam (S/optim/SGD.scala:54-120, S/optim/Adam.scala:36),
+// L2-norm clipping (S/parameters/ParameterOperations.scala:71-133), LSTM cell (S/nn/LSTM.scala:158-185).
+// Every memory-bound kernel moves 16 bytes per lane (cdna_hip_programming.md Guideline 13).
+#include "common.h"
+#include "kernels.h"
+
+namespace {
+
+inline int grid_cap(long work, int cap = 8192) {
+  long g = (work + 255) / 256;
+  if (g > cap) g = cap;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+#define GRID_STRIDE(i, n) for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < (n); i += (long)gridDim.x * blockDim.x)
+
+__global__ void relu_fwd_kernel(const v4u* __restrict__ x, v4u* __restrict__ y, long n8) {
+  GRID_STRIDE(i, n8) {
+    v4u v = x[i], o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = pack2bf(fmaxf(lo_bf(v[e]), 0.f), fmaxf(hi_bf(v[e]), 0.f));
+    y[i] = o;
+  }
+}
+__global__ void relu_bwd_kernel(const v4u* __restrict__ dy, const v4u* __restrict__ y, v4u* __restrict__ dx, long n8) {
+  GRID_STRIDE(i, n8) {
+    const v4u d = dy[i], v = y[i];
+    v4u o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const unsigned lo = lo_bf(v[e]) > 0.f ? (d[e] & 0xffffu) : 0u;
+      const unsigned hi = hi_bf(v[e]) > 0.f ? (d[e] & 0xffff0000u) : 0u;
+      o[e] = lo | hi;
+    }
+    dx[i] = o;
+  }
+}
+__global__ void add_kernel(const v4u* __restrict__ a, const v4u* __restrict__ b, v4u* __restrict__ y, long n8) {
+  GRID_STRIDE(i, n8) {
+    const v4u u = a[i], v = b[i];
+    v4u o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = pack2bf(lo_bf(u[e]) + lo_bf(v[e]), hi_bf(u[e]) + hi_bf(v[e]));
+    y[i] = o;
+  }
+}
+// tail-safe scalar versions for n % 8 != 0
+__global__ void relu_fwd_tail(const bf16_t* x, bf16_t* y, long s, long n) {
+  GRID_STRIDE(i, n - s) y[s + i] = f2bf(fmaxf(bf2f(x[s + i]), 0.f));
+}
+__global__ void relu_bwd_tail(const bf16_t* dy, const bf16_t* y, bf16_t* dx, long s, long n) {
+  GRID_STRIDE(i, n - s) dx[s + i] = bf2f(y[s + i]) > 0.f ? dy[s + i] : (bf16_t)0;
+}
+__global__ void add_tail(const bf16_t* a, const bf16_t* b, bf16_t* y, long s, long n) {
+  GRID_STRIDE(i, n - s) y[s + i] = f2bf(bf2f(a[s + i]) + bf2f(b[s + i]));
+}
+
+// NCHW fp32 (the user-facing BigDL layout) -> NHWC bf16 with channel padding to Cp (zeros)
+__global__ void nchw_to_nhwc_kernel(const float* __restrict__ x, bf16_t* __restrict__ y, int N, int C, int H, int W,
+                                    int Cp) {
+  const long total = (long)N * H * W * Cp;
+  GRID_STRIDE(i, total) {
+    const int c = i % Cp;
+    const long p = i / Cp;
+    const int w = p % W;
+    const long t = p / W;
+    const int h = t % H;
+    const int n = t / H;
+    y[i] = c < C ? f2bf(x[(((long)n * C + c) * H + h) * W + w]) : (bf16_t)0;
+  }
+}
+__global__ void cast_f32_bf16_kernel(const float* __restrict__ x, bf16_t* __restrict__ y, long n) {
+  const long n4 = n >> 2;
+  GRID_STRIDE(i, n4) {
+    const v4f v = reinterpret_cast<const v4f*>(x)[i];
+    reinterpret_cast<v2u*>(y)[i] = v2u{pack2bf(v[0], v[1]), pack2bf(v[2], v[3])};
+  }
+  GRID_STRIDE(j, n - n4 * 4) y[n4 * 4 + j] = f2bf(x[n4 * 4 + j]);
+}
+__global__ void cast_bf16_f32_kernel(const bf16_t* __restrict__ x, float* __restrict__ y, long n) {
+  GRID_STRIDE(i, n) y[i] = bf2f(x[i]);
+}
+
+// ---------------- pooling (NHWC, 8 channels per lane) ----------------
+__global__ void maxpool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, uint8_t* __restrict__ idx,
+                                   int N, int H, int W, int C, int OH, int OW, int kh, int kw, int sh, int sw, int ph,
+                                   int pw) {
+  const int G = C >> 3;
+  const long total = (long)N * OH * OW * G;
+  GRID_STRIDE(i, total) {
+    const int g = i % G;
+    long p = i / G;
+    const int ow = p % OW; p /= OW;
+    const int oh = p % OH;
+    const int n = p / OH;
+    float best[8];
+    uint8_t bi[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { best[e] = -INFINITY; bi[e] = 0; }
+    for (int r = 0; r < kh; ++r) {
+      const int ih = oh * sh - ph + r;
+      if ((unsigned)ih >= (unsigned)H) continue;
+      for (int s = 0; s < kw; ++s) {
+        const int iw = ow * sw - pw + s;
+        if ((unsigned)iw >= (unsigned)W) continue;
+        const v4u v = *reinterpret_cast<const v4u*>(x + (((long)n * H + ih) * W + iw) * C + g * 8);
+        const uint8_t widx = (uint8_t)(r * kw + s);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float l = lo_bf(v[e]), h = hi_bf(v[e]);
+          if (l > best[2 * e] || (l != l)) { best[2 * e] = l; bi[2 * e] = widx; }
+          if (h > best[2 * e + 1] || (h != h)) { best[2 * e + 1] = h; bi[2 * e + 1] = widx; }
+        }
+      }
+    }
+    v4u o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = pack2bf(best[2 * e], best[2 * e + 1]);
+    reinterpret_cast<v4u*>(y)[i] = o;
+    uint2 packed;
+    packed.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | ((unsigned)bi[3] << 24);
+    packed.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | ((unsigned)bi[7] << 24);
+    reinterpret_cast<uint2*>(idx)[i] = packed;
+  }
+}
+
+// gather-form backward: deterministic, no atomics
+__global__ void maxpool_bwd_kernel(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ idx, bf16_t* __restrict__ dx,
+                                   int N, int H, int W, int C, int OH, int OW, int kh, int kw, int sh, int sw, int ph,
+                                   int pw) {
+  const int G = C >> 3;
+  const long total = (long)N * H * W * G;
+  GRID_STRIDE(i, total) {
+    const int g = i % G;
+    long p = i / G;
+    const int iw = p % W; p /= W;
+    const int ih = p % H;
+    const int n = p / H;
+    float acc[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+    const int oh_lo = max(0, (ih + ph - kh + sh) / sh), oh_hi = min(OH - 1, (ih + ph) / sh);
+    const int ow_lo = max(0, (iw + pw - kw + sw) / sw), ow_hi = min(OW - 1, (iw + pw) / sw);
+    for (int oh = oh_lo; oh <= oh_hi; ++oh) {
+      const int r = ih + ph - oh * sh;
+      if (r < 0 || r >= kh) continue;
+      for (int ow = ow_lo; ow <= ow_hi; ++ow) {
+        const int s = iw + pw - ow * sw;
+        if (s < 0 || s >= kw) continue;
+        const long o = (((long)n * OH + oh) * OW + ow) * G + g;
+        const uint2 ix = reinterpret_cast<const uint2*>(idx)[o];
+        const v4u d = reinterpret_cast<const v4u*>(dy)[o];
+        const unsigned widx = r * kw + s;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const unsigned b = ((e < 4 ? ix.x : ix.y) >> ((e & 3) * 8)) & 0xff;
+          if (b == widx) acc[e] += (e & 1) ? hi_bf(d[e >> 1]) : lo_bf(d[e >> 1]);
+        }
+      }
+    }
+    v4u out;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) out[e] = pack2bf(acc[2 * e], acc[2 * e + 1]);
+    reinterpret_cast<v4u*>(dx)[i] = out;
+  }
+}
+
+__device__ __forceinline__ int pool_count(int oh, int ow, int H, int W, int kh, int kw, int sh, int sw, int ph, int pw,
+                                          int count_pad) {
+  int hs = oh * sh - ph, ws = ow * sw - pw;
+  int he = min(hs + kh, H + ph), we = min(ws + kw, W + pw);
+  const int pool = (he - hs) * (we - ws);
+  if (count_pad) return pool;
+  hs = max(hs, 0); ws = max(ws, 0); he = min(he, H); we = min(we, W);
+  return max((he - hs) * (we - ws), 1);
+}
+
+__global__ void avgpool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, int N, int H, int W, int C,
+                                   int OH, int OW, int kh, int kw, int sh, int sw, int ph, int pw, int count_pad) {
+  const int G = C >> 3;
+  const long total = (long)N * OH * OW * G;
+  GRID_STRIDE(i, total) {
+    const int g = i % G;
+    long p = i / G;
+    const int ow = p % OW; p /= OW;
+    const int oh = p % OH;
+    const int n = p / OH;
+    float acc[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+    for (int r = 0; r < kh; ++r) {
+      const int ih = oh * sh - ph + r;
+      if ((unsigned)ih >= (unsigned)H) continue;
+      for (int s = 0; s < kw; ++s) {
+        const int iw = ow * sw - pw + s;
+        if ((unsigned)iw >= (unsigned)W) continue;
+        const v4u v = *reinterpret_cast<const v4u*>(x + (((long)n * H + ih) * W + iw) * C + g * 8);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { acc[2 * e] += lo_bf(v[e]); acc[2 * e + 1] += hi_bf(v[e]); }
+      }
+    }
+    const float inv = 1.f / (float)pool_count(oh, ow, H, W, kh, kw, sh, sw, ph, pw, count_pad);
+    v4u o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = pack2bf(acc[2 * e] * inv, acc[2 * e + 1] * inv);
+    reinterpret_cast<v4u*>(y)[i] = o;
+  }
+}
+
+__global__ void avgpool_bwd_kernel(const bf16_t* __restrict__ dy, bf16_t* __restrict__ dx, int N, int H, int W, int C,
+                                   int OH, int OW, int kh, int kw, int sh, int sw, int ph, int pw, int count_pad) {
+  const int G = C >> 3;
+  const long total = (long)N * H * W * G;
+  GRID_STRIDE(i, total) {
+    const int g = i % G;
+    long p = i / G;
+    const int iw = p % W; p /= W;
+    const int ih = p % H;
+    const int n = p / H;
+    float acc[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+    const int oh_lo = max(0, (ih + ph - kh + sh) / sh), oh_hi = min(OH - 1, (ih + ph) / sh);
+    const int ow_lo = max(0, (iw + pw - kw + sw) / sw), ow_hi = min(OW - 1, (iw + pw) / sw);
+    for (int oh = oh_lo; oh <= oh_hi; ++oh) {
+      const int r = ih + ph - oh * sh;
+      if (r < 0 || r >= kh) continue;
+      for (int ow = ow_lo; ow <= ow_hi; ++ow) {
+        const int s = iw + pw - ow * sw;
+        if (s < 0 || s >= kw) continue;
+        const float inv = 1.f / (float)pool_count(oh, ow, H, W, kh, kw, sh, sw, ph, pw, count_pad);
+        const v4u d = *reinterpret_cast<const v4u*>(dy + (((long)n * OH + oh) * OW + ow) * C + g * 8);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { acc[2 * e] += lo_bf(d[e]) * inv; acc[2 * e + 1] += hi_bf(d[e]) * inv; }
+      }
+    }
+    v4u o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = pack2bf(acc[2 * e], acc[2 * e + 1]);
+    reinterpret_cast<v4u*>(dx)[i] = o;
+  }
+}
+
+// ---------------- fused log-softmax + NLL: one wave per row ----------------
+__global__ __launch_bounds__(256) void softmax_xent_kernel(const bf16_t* __restrict__ lb, const float* __restrict__ lf,
+                                                           const float* __restrict__ labels, float* __restrict__ loss,
+                                                           bf16_t* __restrict__ db, float* __restrict__ df, int B, int K,
+                                                           float label_base, float grad_scale) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= B) return;
+  auto ld = [&](int k) -> float { return lb ? bf2f(lb[(long)row * K + k]) : lf[(long)row * K + k]; };
+  float mx = -INFINITY;
+  for (int k = lane; k < K; k += 64) mx = fmaxf(mx, ld(k));
+  mx = wave_max(mx);
+  float se = 0.f;
+  for (int k = lane; k < K; k += 64) se += __expf(ld(k) - mx);
+  se = wave_sum(se);
+  const float lse = mx + __logf(se);
+  const int tgt = (int)(labels[row] - label_base);
+  if (lane == 0 && loss) {
+    const float xt = (tgt >= 0 && tgt < K) ? ld(tgt) : lse;
+    atomicAdd(loss, (lse - xt) * grad_scale);
+  }
+  if (db || df) {
+    const float inv = 1.f / se;
+    for (int k = lane; k < K; k += 64) {
+      float g = __expf(ld(k) - mx) * inv - (k == tgt ? 1.f : 0.f);
+      g *= grad_scale;
+      if (db) db[(long)row * K + k] = f2bf(g);
+      else df[(long)row * K + k] = g;
+    }
+  }
+}
+
+// ---------------- optimizers on flat fp32 buffers ----------------
+__global__ void sgd_kernel(float* __restrict__ w, const float* __restrict__ g, float* __restrict__ mom,
+                           bf16_t* __restrict__ w16, long n, float lr, float wd, float momentum, float dampening,
+                           int nesterov, int first) {
+  GRID_STRIDE(i, n) {
+    float wi = w[i];
+    float d = g[i] + wd * wi;
+    if (momentum != 0.f) {
+      float b = first ? d : momentum * mom[i] + (1.f - dampening) * d;
+      mom[i] = b;
+      d = nesterov ? d + momentum * b : b;
+    }
+    wi -= lr * d;
+    w[i] = wi;
+    if (w16) w16[i] = f2bf(wi);
+  }
+}
+
+__global__ void adam_kernel(float* __restrict__ w, const float* __restrict__ g, float* __restrict__ m,
+                            float* __restrict__ v, bf16_t* __restrict__ w16, long n, float lr, float b1, float b2,
+                            float eps, float wd, float bc1, float bc2) {
+  GRID_STRIDE(i, n) {
+    float wi = w[i];
+    const float gi = g[i] + wd * wi;
+    const float mi = b1 * m[i] + (1.f - b1) * gi;
+    const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
+    m[i] = mi; v[i] = vi;
+    // BigDL Adam: x -= lr * sqrt(1-b2^t)/(1-b1^t) * m / (sqrt(v) + eps)
+    wi -= lr * (sqrtf(bc2) / bc1) * mi / (sqrtf(vi) + eps);
+    w[i] = wi;
+    if (w16) w16[i] = f2bf(wi);
+  }
+}
+
+__global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ x, float* __restrict__ out, long n) {
+  float acc = 0.f;
+  GRID_STRIDE(i, n) { const float v = x[i]; acc += v * v; }
+  acc = wave_sum(acc);
+  __shared__ float sm[4];
+  if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(out, sm[0] + sm[1] + sm[2] + sm[3]);
+}
+
+__global__ void scale_kernel(float* __restrict__ x, long n, const float* __restrict__ sdev, float s) {
+  const float f = sdev ? sdev[0] : s;
+  GRID_STRIDE(i, n) x[i] *= f;
+}
+
+// ---------------- LSTM cell pointwise (gate order: input, hidden(cell), forget, output) ----------------
+__device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + __expf(-x)); }
+
+__global__ void lstm_fwd_kernel(const float* __restrict__ gates, const float* __restrict__ c_prev, float* __restrict__ c,
+                                float* __restrict__ h, float* __restrict__ act, int B, int H) {
+  const long total = (long)B * H;
+  GRID_STRIDE(idx, total) {
+    const int b = idx / H, j = idx % H;
+    const float* gr = gates + (long)b * 4 * H;
+    const float ig = sigm(gr[j]), gg = tanhf(gr[H + j]), fg = sigm(gr[2 * H + j]), og = sigm(gr[3 * H + j]);
+    const float cp = c_prev ? c_prev[idx] : 0.f;
+    const float cn = fg * cp + ig * gg;
+    c[idx] = cn;
+    h[idx] = og * tanhf(cn);
+    float* ar = act + (long)b * 4 * H;
+    ar[j] = ig; ar[H + j] = gg; ar[2 * H + j] = fg; ar[3 * H + j] = og;
+  }
+}
+
+__global__ void lstm_bwd_kernel(const float* __restrict__ act, const float* __restrict__ c_prev, const float* __restrict__ c,
+                                const float* __restrict__ dh, const float* __restrict__ dc_next, float* __restrict__ dgates,
+                                float* __restrict__ dc_prev, int B, int H) {
+  const long total = (long)B * H;
+  GRID_STRIDE(idx, total) {
+    const int b = idx / H, j = idx % H;
+    const float* ar = act + (long)b * 4 * H;
+    const float ig = ar[j], gg = ar[H + j], fg = ar[2 * H + j], og = ar[3 * H + j];
+    const float tc = tanhf(c[idx]);
+    const float dhv = dh ? dh[idx] : 0.f;
+    const float dcv = dhv * og * (1.f - tc * tc) + (dc_next ? dc_next[idx] : 0.f);
+    const float cp = c_prev ? c_prev[idx] : 0.f;
+    float* dg = dgates + (long)b * 4 * H;
+    dg[j] = dcv * gg * ig * (1.f - ig);
+    dg[H + j] = dcv * ig * (1.f - gg * gg);
+    dg[2 * H + j] = dcv * cp * fg * (1.f - fg);
+    dg[3 * H + j] = dhv * tc * og * (1.f - og);
+    if (dc_prev) dc_prev[idx] = dcv * fg;
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+void bigdl_relu_fwd(const uint16_t* x, uint16_t* y, long n, hipStream_t st) {
+  const long n8 = n >> 3;
+  if (n8) relu_fwd_kernel<<<grid_cap(n8), 256, 0, st>>>((const v4u*)x, (v4u*)y, n8);
+  if (n8 * 8 < n) relu_fwd_tail<<<1, 256, 0, st>>>(x, y, n8 * 8, n);
+  HIP_LAUNCH_CHECK();
+}
+void bigdl_relu_bwd(const uint16_t* dy, const uint16_t* y, uint16_t* dx, long n, hipStream_t st) {
+  const long n8 = n >> 3;
+  if (n8) relu_bwd_kernel<<<grid_cap(n8), 256, 0, st>>>((const v4u*)dy, (const v4u*)y, (v4u*)dx, n8);
+  if (n8 * 8 < n) relu_bwd_tail<<<1, 256, 0, st>>>(dy, y, dx, n8 * 8, n);
+  HIP_LAUNCH_CHECK();
+}
+void bigdl_add_bf16(const uint16_t* a, const uint16_t* b, uint16_t* y, long n, hipStream_t st) {
+  const long n8 = n >> 3;
+  if (n8) add_kernel<<<grid_cap(n8), 256, 0, st>>>((const v4u*)a, (const v4u*)b, (v4u*)y, n8);
+  if (n8 * 8 < n) add_tail<<<1, 256, 0, st>>>(a, b, y, n8 * 8, n);
+  HIP_LAUNCH_CHECK();
+}
+void bigdl_nchw_f32_to_nhwc_bf16(const float* x, uint16_t* y, int N, int C, int H, int W, int Cp, hipStream_t st) {
+  nchw_to_nhwc_kernel<<<grid_cap((long)N * H * W * Cp), 256, 0, st>>>(x, y, N, C, H, W, Cp);
+  HIP_LAUNCH_CHECK();
+}
+void bigdl_cast_f32_bf16(const float* x, uint16_t* y, long n, hipStream_t st) {
+  cast_f32_bf16_kernel<<<grid_cap(n / 4 + 1), 256, 0, st>>>(x, y, n);
+  HIP_LAUNCH_CHECK();
+}
+void bigdl_cast_bf16_f32(const uint16_t* x, float* y, long n, hipStream_t st) {
+  cast_bf16_f32_kernel<<<grid_cap(n), 256, 0, st>>>(x, y, n);
+  HIP_LAUNCH_CHECK();
+}
+void bigdl_maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* idx, int N, int H, int W, int C, int OH, int OW,
+                       int kh, int kw, int sh, int sw, int ph, int pw, hipStream_t st) {
+  maxpool_fwd_kernel<<<grid_cap((long)N * OH * OW * (C / 8)), 256, 0, st>>>(x, y, idx, N, H, W, C, OH, OW, kh, kw, sh,
+                                                                            sw, ph, pw);
+  HIP_LAUNCH_CHECK();
+}
+void bigdl_maxpool_bwd(const uint16_t* dy, const uint8_t* idx, uint16_t* dx, int N, int H, int W, int C, int OH,
+                       int OW, int kh, int kw, int sh, int sw, int ph, int pw, hipStream_t st) {
+  maxpool_bwd_kernel<<<grid_cap((long)N * H * W * (C / 8)), 256, 0, st>>>(dy, idx, dx, N, H, W, C, OH, OW, kh, kw, sh,
+                                                                          sw, ph, pw);
+  HIP_LAUNCH_CHECK();
+}
+void bigdl_avgpool_fwd(const uint16_t* x, uint16_t* y, int N, int H, int W, int C, int OH, int OW, int kh, int kw,
+                       int sh, int sw, int ph, int pw, int count_pad, hipStream_t st) {
+  avgpool_fwd_kernel<<<grid_cap((long)N * OH * OW * (C / 8)), 256, 0, st>>>(x, y, N, H, W, C, OH, OW, kh, kw, sh, sw,
+                                                                            ph, pw, count_pad);
+  HIP_LAUNCH_CHECK();
+}
+void bigdl_avgpool_bwd(const uint16_t* dy, uint16_t* dx, int N, int H, int W, int C, int OH, int OW, int kh, int kw,
+                       int sh, int sw, int ph, int pw, int count_pad, hipStream_t st) {
+  avgpool_bwd_kernel<<<grid_cap((long)N * H * W * (C / 8)), 256, 0, st>>>(dy, dx, N, H, W, C, OH, OW, kh, kw, sh, sw,
+                                                                          ph, pw, count_pad);
+  HIP_LAUNCH_CHECK();
+}
+void bigdl_softmax_xent(const uint16_t* lb, const float* lf, const float* labels, float* loss, uint16_t* db, float* df,
+                        int B, int K, float label_base, float grad_scale, hipStream_t st) {
+  softmax_xent_kernel<<<(B + 3) / 4, 256, 0, st>>>(lb, lf, labels, loss, db, df, B, K, label_base, grad_scale);
+  HIP_LAUNCH_CHECK();
+}
+void bigdl_sgd_step(float* w, const float* g, float* mom, uint16_t* w16, long n, float lr, float wd, float momentum,
+                    float dampening, int nesterov, int first, hipStream_t st) {
+  sgd_kernel<<<grid_cap(n), 256, 0, st>>>(w, g, mom, w16, n, lr, wd, momentum, dampening, nesterov, first);
+  HIP_LAUNCH_CHECK();
+}
+void bigdl_adam_step(float* w, const float* g, float* m, float* v, uint16_t* w16, long n, float lr, float beta1,
+                     float beta2, float eps, float wd, float bc1, float bc2, hipStream_t st) {
+  adam_kernel<<<grid_cap(n), 256, 0, st>>>(w, g, m, v, w16, n, lr, beta1, beta2, eps, wd, bc1, bc2);
+  HIP_LAUNCH_CHECK();
+}
+void bigdl_sumsq(const float* x, float* out, long n, hipStream_t st) {
+  sumsq_kernel<<<grid_cap(n, 2048), 256, 0, st>>>(x, out, n);
+  HIP_LAUNCH_CHECK();
+}
+void bigdl_scale_f32(float* x, long n, const float* sdev, float s, hipStream_t st) {
+  scale_kernel<<<grid_cap(n), 256, 0, st>>>(x, n, sdev, s);
+  HIP_LAUNCH_CHECK();
+}
+void bigdl_lstm_cell_fwd(const float* gates, const float* c_prev, float* c, float* h, float* act, int B, int H,
+                         hipStream_t st) {
+  lstm_fwd_kernel<<<grid_cap((long)B * H), 256, 0, st>>>(gates, c_prev, c, h, act, B, H);
+  HIP_LAUNCH_CHECK();
+}
+void bigdl_lstm_cell_bwd(const float* act, const float* c_prev, const float* c, const float* dh, const float* dc_next,
+                         float* dgates, float* dc_prev, int B, int H, hipStream_t st) {
+  lstm_bwd_kernel<<<grid_cap((long)B * H), 256, 0, st>>>(act, c_prev, c, dh, dc_next, dgates, dc_prev, B, H);
+  HIP_LAUNCH_CHECK();
+}
+
+}  // extern "C"

@@ -1,0 +1,88 @@
+// C ABI of the bigdl_amd HIP kernel library (csrc/*.hip). The torch binding layer
+// (csrc/bindings.cpp) is the only caller; the kernels themselves never include torch headers.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+struct ConvArgs {
+  const uint16_t* src;
+  const uint16_t* wt;
+  uint16_t* out;
+  const float* bias;
+  float* stats;
+  int Nb, Hs, Ws, Cs;
+  int OH, OW;
+  int R, S;
+  int mul_h, off_h, step_h, div_h;
+  int mul_w, off_w, step_w, div_w;
+  int M, Ncol, Kdim, ldo;
+  int relu;
+};
+
+struct WgradArgs {
+  const uint16_t* dy;
+  const uint16_t* src;
+  float* dw;
+  float* dbias;
+  int Nb, Hs, Ws, Cs, OH, OW, R, S;
+  int sh, sw, ph, pw, dh, dwl;
+  int M, Ncol, Kdim, ldy;
+  int m_per_split;
+};
+
+extern "C" {
+int bigdl_conv_nt(const ConvArgs* a, hipStream_t st);
+int bigdl_conv_wgrad(const WgradArgs* a, hipStream_t st);
+void bigdl_transpose_krsc(const uint16_t* w, uint16_t* wt, int K, int RS, int C, hipStream_t st);
+
+// batch norm (NHWC bf16, fp32 statistics)
+void bigdl_bn_stats(const uint16_t* x, float* stats, long P, int C, hipStream_t st);
+void bigdl_bn_finalize(const float* stats, const float* gamma, const float* beta, float* run_mean,
+                       float* run_var, float* save_mean, float* save_invstd, float* scale, float* shift,
+                       long P, int C, float eps, float momentum, int training, hipStream_t st);
+void bigdl_bn_apply(const uint16_t* x, const float* scale, const float* shift, const uint16_t* res,
+                    uint16_t* y, long P, int C, int relu, hipStream_t st);
+void bigdl_bn_bwd_reduce(const uint16_t* dz, const uint16_t* z, const uint16_t* x, const float* mean,
+                         float* red, long P, int C, hipStream_t st);
+void bigdl_bn_bwd_apply(const uint16_t* dz, const uint16_t* z, const uint16_t* x, const float* mean,
+                        const float* invstd, const float* gamma, const float* red, uint16_t* dx,
+                        uint16_t* dres, float* dgamma, float* dbeta, long P, int C, hipStream_t st);
+
+// elementwise
+void bigdl_relu_fwd(const uint16_t* x, uint16_t* y, long n, hipStream_t st);
+void bigdl_relu_bwd(const uint16_t* dy, const uint16_t* y, uint16_t* dx, long n, hipStream_t st);
+void bigdl_add_bf16(const uint16_t* a, const uint16_t* b, uint16_t* y, long n, hipStream_t st);
+void bigdl_nchw_f32_to_nhwc_bf16(const float* x, uint16_t* y, int N, int C, int H, int W, int Cp,
+                                 hipStream_t st);
+void bigdl_cast_f32_bf16(const float* x, uint16_t* y, long n, hipStream_t st);
+void bigdl_cast_bf16_f32(const uint16_t* x, float* y, long n, hipStream_t st);
+
+// pooling (NHWC bf16)
+void bigdl_maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* idx, int N, int H, int W, int C, int OH,
+                       int OW, int kh, int kw, int sh, int sw, int ph, int pw, hipStream_t st);
+void bigdl_maxpool_bwd(const uint16_t* dy, const uint8_t* idx, uint16_t* dx, int N, int H, int W, int C,
+                       int OH, int OW, int kh, int kw, int sh, int sw, int ph, int pw, hipStream_t st);
+void bigdl_avgpool_fwd(const uint16_t* x, uint16_t* y, int N, int H, int W, int C, int OH, int OW, int kh,
+                       int kw, int sh, int sw, int ph, int pw, int count_pad, hipStream_t st);
+void bigdl_avgpool_bwd(const uint16_t* dy, uint16_t* dx, int N, int H, int W, int C, int OH, int OW, int kh,
+                       int kw, int sh, int sw, int ph, int pw, int count_pad, hipStream_t st);
+
+// fused log-softmax + NLL (cross entropy) over rows of logits
+void bigdl_softmax_xent(const uint16_t* logits_bf16, const float* logits_f32, const float* labels,
+                        float* loss, uint16_t* dlogits_bf16, float* dlogits_f32, int B, int K,
+                        float label_base, float grad_scale, hipStream_t st);
+
+// optimizers over flat fp32 buffers (optional bf16 shadow written in the same pass)
+void bigdl_sgd_step(float* w, const float* g, float* mom, uint16_t* w16, long n, float lr, float wd,
+                    float momentum, float dampening, int nesterov, int first, hipStream_t st);
+void bigdl_adam_step(float* w, const float* g, float* m, float* v, uint16_t* w16, long n, float lr,
+                     float beta1, float beta2, float eps, float wd, float bc1, float bc2, hipStream_t st);
+void bigdl_sumsq(const float* x, float* out, long n, hipStream_t st);
+void bigdl_scale_f32(float* x, long n, const float* scale_dev, float scale, hipStream_t st);
+
+// LSTM cell pointwise (gates pre-activations -> c, h), fwd & bwd
+void bigdl_lstm_cell_fwd(const float* gates, const float* c_prev, float* c, float* h, float* act, int B,
+                         int H, hipStream_t st);
+void bigdl_lstm_cell_bwd(const float* act, const float* c_prev, const float* c, const float* dh,
+                         const float* dc_next, float* dgates, float* dc_prev, int B, int H, hipStream_t st);
+}

@@ -1,0 +1,223 @@
+"""Numerics of every HIP kernel vs a plain PyTorch fp32 reference of the same op (GPU only)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+CL = torch.channels_last
+BF = torch.bfloat16
+
+
+def _dev():
+    return torch.device("cuda:0")
+
+
+def _rel(a, b):
+    a = a.float()
+    b = b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+CONV_CASES = [
+    # N, C, H, W, K, R, S, stride, pad
+    (2, 64, 14, 14, 64, 3, 3, 1, 1),
+    (2, 64, 14, 14, 128, 1, 1, 1, 0),
+    (3, 32, 9, 11, 48, 3, 3, 2, 1),
+    (2, 128, 8, 8, 256, 1, 1, 2, 0),
+    (2, 8, 30, 30, 64, 7, 7, 2, 3),     # stem-like (C padded to 8)
+    (4, 256, 7, 7, 512, 3, 3, 1, 1),
+    (1, 16, 5, 5, 24, 5, 5, 1, 0),
+]
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_fwd_dgrad_wgrad(case):
+    from bigdl_amd.ops import conv as cv
+
+    N, C, H, W, K, R, S, st, pd = case
+    torch.manual_seed(0)
+    dev = _dev()
+    x32 = torch.randn(N, C, H, W, device=dev)
+    w32 = torch.randn(K, C, R, S, device=dev) * (1.0 / (C * R * S) ** 0.5)
+    b32 = torch.randn(K, device=dev)
+    x = x32.to(BF, memory_format=CL)
+    w = w32.to(BF, memory_format=CL)
+    xr, wr = x.float(), w.float()
+    # forward (+bias, +stats)
+    stats = torch.zeros(2 * K, device=dev)
+    y = cv.conv2d_fwd(x, w, b32, (st, st), (pd, pd), stats=stats)
+    yr = F.conv2d(xr, wr, b32, stride=st, padding=pd)
+    assert y.shape == yr.shape
+    assert _rel(y, yr) < 1e-2
+    assert _rel(stats[:K], y.float().sum(dim=(0, 2, 3))) < 2e-2
+    assert _rel(stats[K:], (y.float() ** 2).sum(dim=(0, 2, 3))) < 2e-2
+    # relu epilogue
+    y2 = cv.conv2d_fwd(x, w, b32, (st, st), (pd, pd), relu=True)
+    assert _rel(y2, torch.relu(yr)) < 1e-2
+    # dgrad
+    gy = torch.randn_like(yr).to(BF, memory_format=CL)
+    wt = cv.transpose_w(w)
+    dx = cv.conv2d_dgrad(gy, wt, x.shape, (st, st), (pd, pd))
+    dxr = torch.nn.grad.conv2d_input(x.shape, wr, gy.float(), stride=st, padding=pd)
+    assert _rel(dx, dxr) < 1e-2
+    # wgrad
+    dw = torch.zeros(K, C, R, S, device=dev).contiguous(memory_format=CL)
+    db = torch.zeros(K, device=dev)
+    cv.conv2d_wgrad(gy, x, dw, db, (st, st), (pd, pd))
+    dwr = torch.nn.grad.conv2d_weight(xr, wr.shape, gy.float(), stride=st, padding=pd)
+    assert _rel(dw, dwr) < 1e-2
+    assert _rel(db, gy.float().sum(dim=(0, 2, 3))) < 1e-2
+
+
+def test_linear_as_conv1x1():
+    from bigdl_amd.ops import conv as cv
+
+    dev = _dev()
+    B, I, O = 37, 96, 200
+    x = torch.randn(B, I, 1, 1, device=dev).to(BF, memory_format=CL)
+    w = (torch.randn(O, I, 1, 1, device=dev) * 0.1).to(BF, memory_format=CL)
+    y = cv.conv2d_fwd(x, w, None, (1, 1), (0, 0))
+    assert _rel(y.view(B, O), x.view(B, I).float() @ w.view(O, I).float().t()) < 1e-2
+
+
+@pytest.mark.parametrize("res,relu", [(False, False), (False, True), (True, True)])
+def test_bn_fwd_bwd(res, relu):
+    from bigdl_amd.ops import bn
+
+    dev = _dev()
+    N, C, H, W = 4, 64, 9, 7
+    x = (torch.randn(N, C, H, W, device=dev) * 2 + 0.5).to(BF, memory_format=CL)
+    r = torch.randn(N, C, H, W, device=dev).to(BF, memory_format=CL) if res else None
+    g = torch.rand(C, device=dev) + 0.5
+    b = torch.randn(C, device=dev)
+    rm, rv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+    y, sm, si = bn.bn_forward_gpu(x, g, b, rm, rv, 1e-3, 0.1, True, res=r, relu=relu)
+    xr = x.float().requires_grad_(True)
+    ref = F.batch_norm(xr, None, None, g, b, True, 0.1, 1e-3)
+    if res:
+        ref = ref + r.float()
+    if relu:
+        ref = torch.relu(ref)
+    assert _rel(y, ref) < 1e-2
+    assert _rel(rm, 0.1 * x.float().mean(dim=(0, 2, 3))) < 1e-3
+    gz = torch.randn_like(ref)
+    ref.backward(gz)
+    dg, dbt = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
+    gzb = gz.to(BF, memory_format=CL)
+    dx, dres = bn.bn_backward_gpu(gzb, y if relu else None, x, sm, si, g, dg, dbt, need_dres=res)
+    # reference computed on the bf16-rounded gradient
+    xr2 = x.float().requires_grad_(True)
+    out2 = F.batch_norm(xr2, None, None, g, b, True, 0.1, 1e-3)
+    if res:
+        out2 = out2 + r.float()
+    if relu:
+        out2 = torch.relu(out2)
+    out2.backward(gzb.float())
+    assert _rel(dx, xr2.grad) < 2e-2
+    if res:
+        mask = (y.float() > 0).float() if relu else 1.0
+        assert _rel(dres, gzb.float() * mask) < 1e-2
+
+
+def test_maxpool_avgpool():
+    from bigdl_amd.ops import pool
+
+    dev = _dev()
+    x = torch.randn(2, 64, 15, 15, device=dev).to(BF, memory_format=CL)
+    y, idx = pool.maxpool_fwd_gpu(x, 3, 3, 2, 2, 1, 1)
+    xr = x.float().requires_grad_(True)
+    yr = F.max_pool2d(xr, 3, 2, 1)
+    assert torch.equal(y.float(), yr)
+    gy = torch.randn_like(yr).to(BF, memory_format=CL)
+    dx = pool.maxpool_bwd_gpu(gy, idx, x.shape, 3, 3, 2, 2, 1, 1)
+    yr.backward(gy.float())
+    assert _rel(dx, xr.grad) < 1e-2
+    a = pool.avgpool_fwd_gpu(x, 7, 7, 1, 1, 0, 0)
+    xr = x.float().requires_grad_(True)
+    ar = F.avg_pool2d(xr, 7, 1, 0)
+    assert _rel(a, ar) < 1e-2
+    ga = torch.randn_like(ar).to(BF, memory_format=CL)
+    da = pool.avgpool_bwd_gpu(ga, x.shape, 7, 7, 1, 1, 0, 0)
+    ar.backward(ga.float())
+    assert _rel(da, xr.grad) < 1e-2
+
+
+def test_softmax_xent():
+    from bigdl_amd import ops
+
+    dev = _dev()
+    B, K = 33, 1000
+    logits = torch.randn(B, K, device=dev).to(BF)
+    labels = torch.randint(1, K + 1, (B,), device=dev).float()
+    loss, dl = ops.softmax_xent_gpu(logits, labels, label_base=1.0)
+    lr = logits.float().requires_grad_(True)
+    ref = F.cross_entropy(lr, labels.long() - 1)
+    ref.backward()
+    assert abs(loss.item() - ref.item()) < 1e-3 * max(1.0, abs(ref.item()))
+    assert _rel(dl, lr.grad) < 1e-2
+
+
+def test_relu_add_cast():
+    from bigdl_amd import ops
+
+    dev = _dev()
+    x = torch.randn(1001, device=dev).to(BF)
+    y = ops.relu_gpu(x)
+    assert torch.equal(y, torch.relu(x))
+    dy = torch.randn(1001, device=dev).to(BF)
+    dx = ops.relu_bwd_gpu(dy, y)
+    assert torch.equal(dx, dy * (y > 0))
+    z = ops.add_gpu(x, dy)
+    assert _rel(z, x.float() + dy.float()) < 1e-2
+    f = torch.randn(1003, device=dev)
+    assert _rel(ops.to_f32(ops.to_bf16(f)), f) < 1e-2
+
+
+def test_sgd_adam_kernels():
+    from bigdl_amd.ops import native
+
+    C = native.get()
+    dev = _dev()
+    n = 5000
+    w = torch.randn(n, device=dev)
+    g = torch.randn(n, device=dev)
+    mom = torch.zeros(n, device=dev)
+    w16 = torch.empty(n, dtype=BF, device=dev)
+    wr, br = w.clone(), None
+    for it in range(3):
+        C.sgd_step(w, g, mom, w16, 0.1, 1e-4, 0.9, 0.0, False, it == 0)
+        d = g + 1e-4 * wr
+        br = d.clone() if br is None else 0.9 * br + d
+        wr = wr - 0.1 * br
+    assert _rel(w, wr) < 1e-5
+    assert _rel(w16, wr) < 1e-2
+    s = torch.zeros(1, device=dev)
+    C.sumsq(g, s)
+    assert abs(s.item() - (g * g).sum().item()) < 1e-2 * s.item()
+
+
+def test_lstm_cell():
+    from bigdl_amd.ops import native
+
+    C = native.get()
+    dev = _dev()
+    B, H = 5, 33
+    gates = torch.randn(B, 4 * H, device=dev, requires_grad=True)
+    cp = torch.randn(B, H, device=dev, requires_grad=True)
+    c = torch.empty(B, H, device=dev)
+    h = torch.empty(B, H, device=dev)
+    act = torch.empty(B, 4 * H, device=dev)
+    C.lstm_cell_fwd(gates.detach(), cp.detach(), c, h, act)
+    i, gg, f, o = gates.split(H, dim=1)
+    cr = torch.sigmoid(f) * cp + torch.sigmoid(i) * torch.tanh(gg)
+    hr = torch.sigmoid(o) * torch.tanh(cr)
+    assert _rel(c, cr) < 1e-5 and _rel(h, hr) < 1e-5
+    dh = torch.randn(B, H, device=dev)
+    dcn = torch.randn(B, H, device=dev)
+    (hr * dh + cr * dcn).sum().backward()
+    dg = torch.empty(B, 4 * H, device=dev)
+    dcp = torch.empty(B, H, device=dev)
+    C.lstm_cell_bwd(act, cp.detach(), c, dh, dcn, dg, dcp)
+    assert _rel(dg, gates.grad) < 1e-4
+    assert _rel(dcp, cp.grad) < 1e-4
