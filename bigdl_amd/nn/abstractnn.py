@@ -157,7 +157,7 @@ class AbstractModule(metaclass=_RecordInit):
         pass
 
     def _apply_regularizers(self):
-        if self.wRegularizer is None and self.bRegularizer is None:
+        if (self.wRegularizer is None and self.bRegularizer is None) or getattr(self, "_reg_folded", False):
             return
         for (w, g) in self._params:
             reg = self.bRegularizer if w == "bias" else self.wRegularizer
@@ -213,7 +213,7 @@ class AbstractModule(metaclass=_RecordInit):
         for g in self._all_params()[1]:
             g.zero_()
 
-    def getParameters(self):
+    def getParameters(self, pad_multiple=1):
         """Compact every weight (and gradient) into ONE contiguous fp32 storage and return 1-D views of it.
 
         Reference: AbstractModule.getParameters (AbstractModule.scala:988) + Module.flatten
@@ -228,8 +228,9 @@ class AbstractModule(metaclass=_RecordInit):
         if getattr(self, "_flat", None) is not None and self._flat_ok(ws, gs):
             return self._flat
         total = sum(w.numel() for w in ws)
-        fw = torch.zeros(total, dtype=torch.float32, device=dev)
-        fg = torch.zeros(total, dtype=torch.float32, device=dev)
+        padded = -(-total // pad_multiple) * pad_multiple
+        fw = torch.zeros(padded, dtype=torch.float32, device=dev)
+        fg = torch.zeros(padded, dtype=torch.float32, device=dev)
         views = []
         off = 0
         for w, g in zip(ws, gs):
@@ -242,6 +243,7 @@ class AbstractModule(metaclass=_RecordInit):
             views.append((vw, vg, off, n, stride))
             off += n
         self._rebind_params(views)
+        self._flat_total = total
         self._flat = (fw, fg)
         self._flat_views = views
         return fw, fg

@@ -161,7 +161,13 @@ class Container(AbstractModule):
 
 
 class Sequential(Container):
+    _residual_plan = None   # set by nn.fusion for ResNet blocks on the GPU engine
+
     def updateOutput(self, input):
+        if self._residual_plan is not None:
+            from .fusion import residual_forward
+
+            return residual_forward(self, input)
         x = input
         for m in self.modules:
             x = m.forward(x)
@@ -171,6 +177,12 @@ class Sequential(Container):
         import time
 
         t0 = time.perf_counter_ns()
+        if self._residual_plan is not None:
+            from .fusion import residual_backward
+
+            self.gradInput = residual_backward(self, input, gradOutput)
+            self.backward_time += time.perf_counter_ns() - t0
+            return self.gradInput
         g = gradOutput
         for i in range(len(self.modules) - 1, -1, -1):
             inp = self.modules[i - 1].output if i > 0 else input

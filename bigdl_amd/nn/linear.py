@@ -1,0 +1,421 @@
+"""Dense layers. Reference: S/nn/Linear.scala:84-160 (fwd addmm, bwd-data :128, bwd-weight :154),
+SparseLinear.scala, Bilinear.scala, LookupTable.scala:47, LookupTableSparse.scala, MM.scala, MV.scala,
+Cosine.scala, CosineDistance.scala, Euclidean.scala, PairwiseDistance.scala, DotProduct.scala,
+CrossProduct.scala, Maxout.scala, Highway.scala.
+
+GPU engine: Linear runs on the MFMA GEMM kernels of csrc/conv_igemm.hip (a Linear layer IS a 1x1
+convolution over a 1x1 image: fwd = NT GEMM with fused bias/ReLU, dgrad = NT GEMM against the transposed
+weight, wgrad = split-K TN GEMM accumulated in fp32 into the flat gradient buffer). Feature sizes that are
+not multiples of 8 are zero-padded on the fly.
+"""
+import math
+
+import torch
+import torch.nn.functional as F
+
+from .. import ops
+from ..ops import conv as cv
+from .abstractnn import AutogradModule, TensorModule
+from .init_methods import RandomUniform
+
+BF16 = torch.bfloat16
+CL = torch.channels_last
+
+
+def _pad8(n):
+    return -(-n // 8) * 8
+
+
+class Linear(TensorModule):
+    def __init__(self, inputSize, outputSize, withBias=True, wRegularizer=None, bRegularizer=None,
+                 initWeight=None, initBias=None, initGradWeight=None, initGradBias=None):
+        super().__init__()
+        self.inputSize, self.outputSize, self.withBias = inputSize, outputSize, withBias
+        self.wRegularizer, self.bRegularizer = wRegularizer, bRegularizer
+        self.fuse_relu = False
+        self.register_parameter("weight", "gradWeight", torch.empty(outputSize, inputSize))
+        if withBias:
+            self.register_parameter("bias", "gradBias", torch.empty(outputSize))
+        else:
+            self.bias = self.gradBias = None
+        stdv = 1.0 / math.sqrt(inputSize)
+        self.weightInitMethod = RandomUniform(-stdv, stdv)
+        self.biasInitMethod = RandomUniform(-stdv, stdv)
+        self.reset()
+        if initWeight is not None:
+            self.weight.copy_(torch.as_tensor(initWeight).reshape(self.weight.shape))
+        if initBias is not None and withBias:
+            self.bias.copy_(torch.as_tensor(initBias).reshape(self.bias.shape))
+        if initGradWeight is not None:
+            self.gradWeight.copy_(torch.as_tensor(initGradWeight).reshape(self.weight.shape))
+        if initGradBias is not None and withBias:
+            self.gradBias.copy_(torch.as_tensor(initGradBias).reshape(self.bias.shape))
+
+    def reset(self):
+        with torch.no_grad():
+            self.weightInitMethod.init(self.weight, "out_in")
+            if self.bias is not None:
+                self.biasInitMethod.init(self.bias)
+
+    # ------------------------------------------------------------------ GPU helpers
+    def _padded(self):
+        return _pad8(self.inputSize) != self.inputSize or _pad8(self.outputSize) != self.outputSize
+
+    def _w16_4d(self):
+        """(Op, Ip, 1, 1) bf16 weight (zero padded to multiples of 8)."""
+        w16 = self.w16("weight")
+        Ip, Op = _pad8(self.inputSize), _pad8(self.outputSize)
+        if Ip != self.inputSize or Op != self.outputSize:
+            w16 = F.pad(w16, (0, Ip - self.inputSize, 0, Op - self.outputSize))
+        return w16.contiguous().view(Op, Ip, 1, 1)
+
+    def _x4d(self, x):
+        B = x.shape[0]
+        Ip = _pad8(self.inputSize)
+        if x.dtype != BF16:
+            x = ops.to_bf16(x.contiguous()) if x.dtype == torch.float32 else x.to(BF16)
+        x = x.contiguous()
+        if Ip != self.inputSize:
+            x = F.pad(x, (0, Ip - self.inputSize))
+        return x.view(B, Ip, 1, 1)
+
+    def updateOutput(self, input):
+        x = input
+        lead = None
+        if x.dim() == 1:
+            x = x.unsqueeze(0)
+        elif x.dim() > 2:
+            lead = x.shape[:-1]
+            x = x.reshape(-1, x.shape[-1])
+        if x.is_cuda:
+            x4 = self._x4d(x)
+            self._x4 = x4
+            bias = self.bias
+            Op = _pad8(self.outputSize)
+            if bias is not None and Op != self.outputSize:
+                bias = F.pad(bias, (0, Op - self.outputSize))
+            y = cv.conv2d_fwd(x4, self._w16_4d(), bias, (1, 1), (0, 0), relu=self.fuse_relu)
+            y = y.view(x.shape[0], Op)
+            if Op != self.outputSize:
+                y = y[:, : self.outputSize].contiguous()
+        else:
+            y = F.linear(x.float(), self.weight, self.bias)
+            if self.fuse_relu:
+                y = torch.relu(y)
+        if input.dim() == 1:
+            y = y.squeeze(0)
+        elif lead is not None:
+            y = y.reshape(tuple(lead) + (self.outputSize,))
+        return y
+
+    def _gy2d(self, gradOutput):
+        g = gradOutput
+        if g.dim() == 1:
+            g = g.unsqueeze(0)
+        elif g.dim() > 2:
+            g = g.reshape(-1, g.shape[-1])
+        if self.fuse_relu:
+            out = self.output.reshape(g.shape)
+            g = g * (out > 0).to(g.dtype)
+        return g
+
+    def updateGradInput(self, input, gradOutput):
+        g = self._gy2d(gradOutput)
+        if g.is_cuda:
+            B = g.shape[0]
+            Op, Ip = _pad8(self.outputSize), _pad8(self.inputSize)
+            g16 = g.to(BF16).contiguous()
+            if Op != self.outputSize:
+                g16 = F.pad(g16, (0, Op - self.outputSize))
+            g4 = g16.view(B, Op, 1, 1)
+            wt = cv.transpose_w(self._w16_4d())           # (Ip, 1, 1, Op)
+            gi = cv.conv2d_dgrad(g4, wt, (B, Ip, 1, 1), (1, 1), (0, 0)).view(B, Ip)
+            if Ip != self.inputSize:
+                gi = gi[:, : self.inputSize].contiguous()
+            self._g16 = g4
+        else:
+            gi = g.float() @ self.weight
+        return gi.reshape(input.shape)
+
+    def accGradParameters(self, input, gradOutput):
+        g = self._gy2d(gradOutput)
+        if g.is_cuda:
+            g4 = getattr(self, "_g16", None)
+            if g4 is None or g4.shape[0] != g.shape[0]:
+                Op = _pad8(self.outputSize)
+                g16 = g.to(BF16).contiguous()
+                if Op != self.outputSize:
+                    g16 = F.pad(g16, (0, Op - self.outputSize))
+                g4 = g16.view(g.shape[0], Op, 1, 1)
+            x4 = self._x4
+            direct = (not self._padded()) and self.scaleW == 1.0 and self.scaleB == 1.0
+            if direct:
+                cv.conv2d_wgrad(g4, x4, self.gradWeight.view(self.outputSize, self.inputSize, 1, 1),
+                                self.gradBias, (1, 1), (0, 0))
+            else:
+                Op, Ip = g4.shape[1], x4.shape[1]
+                dw = torch.zeros(Op, Ip, 1, 1, device=g.device)
+                db = torch.zeros(Op, device=g.device) if self.bias is not None else None
+                cv.conv2d_wgrad(g4, x4, dw, db, (1, 1), (0, 0))
+                self.gradWeight.add_(dw.view(Op, Ip)[: self.outputSize, : self.inputSize], alpha=self.scaleW)
+                if db is not None:
+                    self.gradBias.add_(db[: self.outputSize], alpha=self.scaleB)
+            self._g16 = None
+            return
+        x = input
+        if x.dim() == 1:
+            x = x.unsqueeze(0)
+        elif x.dim() > 2:
+            x = x.reshape(-1, x.shape[-1])
+        gf = g.float()
+        self.gradWeight.add_(gf.t() @ x.float(), alpha=self.scaleW)
+        if self.bias is not None:
+            self.gradBias.add_(gf.sum(0), alpha=self.scaleB)
+
+    def __repr__(self):
+        return f"Linear({self.inputSize} -> {self.outputSize})"
+
+
+class SparseLinear(AutogradModule):
+    """Linear over a sparse (COO) input (reference SparseLinear.scala; wide & deep models)."""
+
+    def __init__(self, inputSize, outputSize, withBias=True, backwardStart=-1, backwardLength=-1,
+                 wRegularizer=None, bRegularizer=None, initWeight=None, initBias=None):
+        super().__init__()
+        self.inputSize, self.outputSize = inputSize, outputSize
+        self.register_parameter("weight", "gradWeight", torch.empty(outputSize, inputSize))
+        if withBias:
+            self.register_parameter("bias", "gradBias", torch.empty(outputSize))
+        else:
+            self.bias = None
+        stdv = 1.0 / math.sqrt(inputSize)
+        RandomUniform(-stdv, stdv).init(self.weight)
+        if self.bias is not None:
+            RandomUniform(-stdv, stdv).init(self.bias)
+
+    def fn(self, x):
+        if x.is_sparse:
+            y = torch.sparse.mm(x.float(), self.weight.t())
+        else:
+            y = x.float() @ self.weight.t()
+        return y + self.bias if self.bias is not None else y
+
+
+class Bilinear(AutogradModule):
+    def __init__(self, inputSize1, inputSize2, outputSize, biasRes=True, wRegularizer=None, bRegularizer=None):
+        super().__init__()
+        self.register_parameter("weight", "gradWeight", torch.empty(outputSize, inputSize1, inputSize2))
+        if biasRes:
+            self.register_parameter("bias", "gradBias", torch.empty(outputSize))
+        else:
+            self.bias = None
+        stdv = 1.0 / math.sqrt(inputSize1)
+        RandomUniform(-stdv, stdv).init(self.weight)
+        if self.bias is not None:
+            RandomUniform(-stdv, stdv).init(self.bias)
+
+    def fn(self, x):
+        return F.bilinear(x[1].float(), x[2].float(), self.weight, self.bias)
+
+
+class LookupTable(TensorModule):
+    """Embedding lookup with 1-based indices (reference LookupTable.scala:47, incl. maxNorm renorm)."""
+
+    def __init__(self, nIndex, nOutput, paddingValue=0.0, maxNorm=float("inf"), normType=2.0,
+                 shouldScaleGradByFreq=False, wRegularizer=None, maskZero=False):
+        super().__init__()
+        self.nIndex, self.nOutput = nIndex, nOutput
+        self.paddingValue, self.maxNorm, self.normType = paddingValue, maxNorm, normType
+        self.shouldScaleGradByFreq, self.maskZero = shouldScaleGradByFreq, maskZero
+        self.wRegularizer = wRegularizer
+        self.register_parameter("weight", "gradWeight", torch.empty(nIndex, nOutput))
+        self.reset()
+
+    def reset(self):
+        with torch.no_grad():
+            self.weight.normal_(0, 1)
+
+    def _idx(self, input):
+        idx = input.long() - 1
+        if self.maskZero:
+            idx = idx.clamp_min(-1)
+        return idx
+
+    def updateOutput(self, input):
+        idx = self._idx(input)
+        if self.maxNorm != float("inf"):
+            with torch.no_grad():
+                rows = idx[idx >= 0].unique()
+                w = self.weight[rows]
+                n = w.norm(p=self.normType, dim=1, keepdim=True)
+                scale = torch.where(n > self.maxNorm, self.maxNorm / (n + 1e-7), torch.ones_like(n))
+                self.weight[rows] = w * scale
+        safe = idx.clamp_min(0)
+        out = self.weight[safe]
+        if self.maskZero:
+            out = out * (idx >= 0).unsqueeze(-1).to(out.dtype)
+        return out
+
+    def updateGradInput(self, input, gradOutput):
+        return torch.zeros_like(input, dtype=torch.float32)
+
+    def accGradParameters(self, input, gradOutput):
+        idx = self._idx(input).reshape(-1)
+        g = gradOutput.reshape(-1, self.nOutput).float()
+        keep = idx >= 0
+        if self.paddingValue != 0:
+            keep = keep & (idx != int(self.paddingValue) - 1)
+        idx, g = idx[keep], g[keep]
+        if self.shouldScaleGradByFreq:
+            cnt = torch.bincount(idx, minlength=self.nIndex).float()
+            g = g / cnt[idx].unsqueeze(1)
+        self.gradWeight.index_add_(0, idx.to(self.gradWeight.device), g.to(self.gradWeight.device), alpha=self.scaleW)
+
+
+class LookupTableSparse(AutogradModule):
+    """Sparse-id embedding with ``combiner`` in {sum, mean, sqrtn} (reference LookupTableSparse.scala:47)."""
+
+    def __init__(self, nIndex, nOutput, combiner="sum", maxNorm=-1.0, wRegularizer=None):
+        super().__init__()
+        self.combiner = combiner
+        self.register_parameter("weight", "gradWeight", torch.empty(nIndex, nOutput).normal_(0, 1))
+
+    def fn(self, x):
+        ids, weights = (x[1], x[2]) if not isinstance(x, torch.Tensor) else (x, None)
+        dense = ids.to_dense() if ids.is_sparse else ids
+        idx = dense.long() - 1
+        mask = (idx >= 0).float()
+        w = mask if weights is None else (weights.to_dense() if weights.is_sparse else weights).float() * mask
+        emb = self.weight[idx.clamp_min(0)] * w.unsqueeze(-1)
+        s = emb.sum(1)
+        if self.combiner == "mean":
+            s = s / w.sum(1, keepdim=True).clamp_min(1e-12)
+        elif self.combiner == "sqrtn":
+            s = s / (w * w).sum(1, keepdim=True).sqrt().clamp_min(1e-12)
+        return s
+
+
+class MM(AutogradModule):
+    def __init__(self, transA=False, transB=False):
+        super().__init__()
+        self.transA, self.transB = transA, transB
+
+    def fn(self, x):
+        a, b = x[1], x[2]
+        if self.transA:
+            a = a.transpose(-1, -2)
+        if self.transB:
+            b = b.transpose(-1, -2)
+        return a @ b
+
+
+class MV(AutogradModule):
+    def __init__(self, trans=False):
+        super().__init__()
+        self.trans = trans
+
+    def fn(self, x):
+        m, v = x[1], x[2]
+        if self.trans:
+            m = m.transpose(-1, -2)
+        return (m @ v.unsqueeze(-1)).squeeze(-1)
+
+
+class DotProduct(AutogradModule):
+    def fn(self, x):
+        return (x[1] * x[2]).sum(-1)
+
+
+class CosineDistance(AutogradModule):
+    def fn(self, x):
+        return F.cosine_similarity(x[1].float(), x[2].float(), dim=-1, eps=1e-12)
+
+
+class PairwiseDistance(AutogradModule):
+    def __init__(self, norm=2):
+        super().__init__()
+        self.norm = norm
+
+    def fn(self, x):
+        return (x[1] - x[2]).abs().pow(self.norm).sum(-1).pow(1.0 / self.norm)
+
+
+class Cosine(AutogradModule):
+    """Cosine similarity of the input to each of outputSize learnable vectors."""
+
+    def __init__(self, inputSize, outputSize):
+        super().__init__()
+        self.register_parameter("weight", "gradWeight", torch.empty(outputSize, inputSize))
+        stdv = 1.0 / math.sqrt(inputSize)
+        RandomUniform(-stdv, stdv).init(self.weight)
+
+    def fn(self, x):
+        xs = x if x.dim() > 1 else x.unsqueeze(0)
+        y = F.normalize(xs.float(), dim=1, eps=1e-12) @ F.normalize(self.weight, dim=1, eps=1e-12).t()
+        return y if x.dim() > 1 else y.squeeze(0)
+
+
+class Euclidean(AutogradModule):
+    def __init__(self, inputSize, outputSize, fastBackward=True):
+        super().__init__()
+        self.register_parameter("weight", "gradWeight", torch.empty(inputSize, outputSize))
+        stdv = 1.0 / math.sqrt(inputSize)
+        RandomUniform(-stdv, stdv).init(self.weight)
+
+    def fn(self, x):
+        xs = x if x.dim() > 1 else x.unsqueeze(0)
+        d = (xs.float().unsqueeze(2) - self.weight.unsqueeze(0)).pow(2).sum(1).sqrt()
+        return d if x.dim() > 1 else d.squeeze(0)
+
+
+class CrossProduct(AutogradModule):
+    """Pairwise dot products between all tensors of the input table."""
+
+    def __init__(self, numTensor=0, embeddingSize=0):
+        super().__init__()
+
+    def fn(self, x):
+        ts = x.toSeq()
+        outs = []
+        for i in range(len(ts)):
+            for j in range(i + 1, len(ts)):
+                outs.append((ts[i] * ts[j]).sum(-1, keepdim=True))
+        return torch.cat(outs, dim=-1)
+
+
+class Maxout(AutogradModule):
+    def __init__(self, inputSize, outputSize, maxoutNumber, withBias=True, wRegularizer=None, bRegularizer=None,
+                 initWeight=None, initBias=None):
+        super().__init__()
+        self.outputSize, self.k = outputSize, maxoutNumber
+        self.register_parameter("weight", "gradWeight", torch.empty(outputSize * maxoutNumber, inputSize))
+        self.register_parameter("bias", "gradBias", torch.empty(outputSize * maxoutNumber))
+        stdv = 1.0 / math.sqrt(inputSize)
+        RandomUniform(-stdv, stdv).init(self.weight)
+        RandomUniform(-stdv, stdv).init(self.bias)
+
+    def fn(self, x):
+        y = F.linear(x.float(), self.weight, self.bias)
+        return y.view(y.shape[0], self.outputSize, self.k).max(dim=2).values
+
+
+class Highway(AutogradModule):
+    def __init__(self, size, withBias=True, activation=None, wRegularizer=None, bRegularizer=None):
+        super().__init__()
+        self.size = size
+        self.register_parameter("weight", "gradWeight", torch.empty(2 * size, size))
+        self.register_parameter("bias", "gradBias", torch.zeros(2 * size))
+        self.activation = activation
+        stdv = 1.0 / math.sqrt(size)
+        RandomUniform(-stdv, stdv).init(self.weight)
+
+    def fn(self, x):
+        y = F.linear(x.float(), self.weight, self.bias)
+        t = torch.sigmoid(y[:, : self.size])
+        h = y[:, self.size:]
+        h = torch.tanh(h) if self.activation is None else self.activation.fn(h)
+        return t * h + (1 - t) * x.float()
+
+
+__all__ = ["Linear", "SparseLinear", "Bilinear", "LookupTable", "LookupTableSparse", "MM", "MV", "DotProduct",
+           "CosineDistance", "PairwiseDistance", "Cosine", "Euclidean", "CrossProduct", "Maxout", "Highway"]

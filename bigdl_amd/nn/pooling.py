@@ -1,0 +1,189 @@
+"""Pooling layers. Reference: S/nn/SpatialMaxPooling.scala:62, SpatialAveragePooling.scala:62,
+VolumetricMaxPooling.scala, VolumetricAveragePooling.scala, TemporalMaxPooling.scala; primitives in
+NNPrimitive.scala:654-1051. GPU engine: NHWC kernels in csrc/elementwise.hip."""
+import torch
+import torch.nn.functional as F
+
+from ..ops import pool as P
+from .abstractnn import AutogradModule, TensorModule
+
+BF16 = torch.bfloat16
+CL = torch.channels_last
+
+
+def _same(inp, k, s):
+    out = -(-inp // s)
+    total = max((out - 1) * s + k - inp, 0)
+    return total // 2
+
+
+def _gpu_ok(x):
+    return x.is_cuda and x.dim() == 4 and x.shape[1] % 8 == 0
+
+
+def _prep(x):
+    if x.dtype != BF16 or not x.is_contiguous(memory_format=CL):
+        x = x.to(BF16, memory_format=CL)
+    return x
+
+
+class SpatialMaxPooling(TensorModule):
+    def __init__(self, kW, kH, dW=None, dH=None, padW=0, padH=0, format="NCHW"):
+        super().__init__()
+        self.kW, self.kH = kW, kH
+        self.dW, self.dH = dW if dW is not None else kW, dH if dH is not None else kH
+        self.padW, self.padH = padW, padH
+        self.format = format
+        self.ceilMode = False
+
+    def ceil(self):
+        self.ceilMode = True
+        return self
+
+    def floor(self):
+        self.ceilMode = False
+        return self
+
+    def _pads(self, H, W):
+        if self.padW == -1 and self.padH == -1:
+            return _same(H, self.kH, self.dH), _same(W, self.kW, self.dW)
+        return self.padH, self.padW
+
+    def updateOutput(self, input):
+        x = input.permute(0, 3, 1, 2) if self.format == "NHWC" else input
+        sq = x.dim() == 3
+        if sq:
+            x = x.unsqueeze(0)
+        ph, pw = self._pads(x.shape[2], x.shape[3])
+        if _gpu_ok(x):
+            y, self._idx = P.maxpool_fwd_gpu(_prep(x), self.kH, self.kW, self.dH, self.dW, ph, pw, self.ceilMode)
+        else:
+            y, self._idx = F.max_pool2d(x, (self.kH, self.kW), (self.dH, self.dW), (ph, pw),
+                                        ceil_mode=self.ceilMode, return_indices=True)
+        y = y.squeeze(0) if sq else y
+        return y.permute(0, 2, 3, 1) if self.format == "NHWC" else y
+
+    def updateGradInput(self, input, gradOutput):
+        x = input.permute(0, 3, 1, 2) if self.format == "NHWC" else input
+        g = gradOutput.permute(0, 3, 1, 2) if self.format == "NHWC" else gradOutput
+        sq = x.dim() == 3
+        if sq:
+            x, g = x.unsqueeze(0), g.unsqueeze(0)
+        ph, pw = self._pads(x.shape[2], x.shape[3])
+        if _gpu_ok(x):
+            gi = P.maxpool_bwd_gpu(_prep(g), self._idx, x.shape, self.kH, self.kW, self.dH, self.dW, ph, pw)
+        else:
+            gi = F.max_unpool2d(g, self._idx, (self.kH, self.kW), (self.dH, self.dW), (ph, pw), output_size=x.shape[2:])
+        gi = gi.squeeze(0) if sq else gi
+        return gi.permute(0, 2, 3, 1) if self.format == "NHWC" else gi
+
+    def __repr__(self):
+        return f"SpatialMaxPooling({self.kW}, {self.kH}, {self.dW}, {self.dH}, {self.padW}, {self.padH})"
+
+
+class SpatialAveragePooling(TensorModule):
+    def __init__(self, kW, kH, dW=1, dH=1, padW=0, padH=0, globalPooling=False, ceilMode=False,
+                 countIncludePad=True, divide=True, format="NCHW"):
+        super().__init__()
+        self.kW, self.kH, self.dW, self.dH, self.padW, self.padH = kW, kH, dW, dH, padW, padH
+        self.globalPooling, self.ceilMode, self.countIncludePad, self.divide = (globalPooling, ceilMode,
+                                                                                countIncludePad, divide)
+        self.format = format
+
+    def ceil(self):
+        self.ceilMode = True
+        return self
+
+    def floor(self):
+        self.ceilMode = False
+        return self
+
+    def _geom(self, x):
+        if self.globalPooling:
+            return x.shape[2], x.shape[3], 1, 1, 0, 0
+        if self.padW == -1 and self.padH == -1:
+            return (self.kH, self.kW, self.dH, self.dW, _same(x.shape[2], self.kH, self.dH),
+                    _same(x.shape[3], self.kW, self.dW))
+        return self.kH, self.kW, self.dH, self.dW, self.padH, self.padW
+
+    def updateOutput(self, input):
+        x = input.permute(0, 3, 1, 2) if self.format == "NHWC" else input
+        sq = x.dim() == 3
+        if sq:
+            x = x.unsqueeze(0)
+        kh, kw, sh, sw, ph, pw = self._geom(x)
+        if _gpu_ok(x) and self.divide:
+            y = P.avgpool_fwd_gpu(_prep(x), kh, kw, sh, sw, ph, pw, self.ceilMode, self.countIncludePad)
+        else:
+            y = F.avg_pool2d(x, (kh, kw), (sh, sw), (ph, pw), self.ceilMode, self.countIncludePad)
+            if not self.divide:
+                y = y * (kh * kw)
+        y = y.squeeze(0) if sq else y
+        return y.permute(0, 2, 3, 1) if self.format == "NHWC" else y
+
+    def updateGradInput(self, input, gradOutput):
+        x = input.permute(0, 3, 1, 2) if self.format == "NHWC" else input
+        g = gradOutput.permute(0, 3, 1, 2) if self.format == "NHWC" else gradOutput
+        sq = x.dim() == 3
+        if sq:
+            x, g = x.unsqueeze(0), g.unsqueeze(0)
+        kh, kw, sh, sw, ph, pw = self._geom(x)
+        if _gpu_ok(x) and self.divide:
+            gi = P.avgpool_bwd_gpu(_prep(g), x.shape, kh, kw, sh, sw, ph, pw, self.countIncludePad)
+        else:
+            xr = x.detach().float().requires_grad_(True)
+            with torch.enable_grad():
+                y = F.avg_pool2d(xr, (kh, kw), (sh, sw), (ph, pw), self.ceilMode, self.countIncludePad)
+                if not self.divide:
+                    y = y * (kh * kw)
+            gi = torch.autograd.grad(y, xr, g.float())[0].to(x.dtype)
+        gi = gi.squeeze(0) if sq else gi
+        return gi.permute(0, 2, 3, 1) if self.format == "NHWC" else gi
+
+
+class VolumetricMaxPooling(AutogradModule):
+    def __init__(self, kT, kW, kH, dT=None, dW=None, dH=None, padT=0, padW=0, padH=0):
+        super().__init__()
+        self.k = (kT, kH, kW)
+        self.s = (dT or kT, dH or kH, dW or kW)
+        self.p = (padT, padH, padW)
+        self.ceilMode = False
+
+    def ceil(self):
+        self.ceilMode = True
+        return self
+
+    def fn(self, x):
+        return F.max_pool3d(x, self.k, self.s, self.p, ceil_mode=self.ceilMode)
+
+
+class VolumetricAveragePooling(AutogradModule):
+    def __init__(self, kT, kW, kH, dT=None, dW=None, dH=None, padT=0, padW=0, padH=0, countIncludePad=True,
+                 ceilMode=False):
+        super().__init__()
+        self.k = (kT, kH, kW)
+        self.s = (dT or kT, dH or kH, dW or kW)
+        self.p = (padT, padH, padW)
+        self.countIncludePad, self.ceilMode = countIncludePad, ceilMode
+
+    def fn(self, x):
+        return F.avg_pool3d(x, self.k, self.s, self.p, self.ceilMode, self.countIncludePad)
+
+
+class TemporalMaxPooling(AutogradModule):
+    """Max over time of (batch, frames, features) input (reference TemporalMaxPooling.scala)."""
+
+    def __init__(self, kW, dW=None):
+        super().__init__()
+        self.kW, self.dW = kW, dW if dW is not None else kW
+
+    def fn(self, x):
+        sq = x.dim() == 2
+        if sq:
+            x = x.unsqueeze(0)
+        y = F.max_pool1d(x.transpose(1, 2), self.kW, self.dW).transpose(1, 2)
+        return y.squeeze(0) if sq else y
+
+
+__all__ = ["SpatialMaxPooling", "SpatialAveragePooling", "VolumetricMaxPooling", "VolumetricAveragePooling",
+           "TemporalMaxPooling"]

@@ -167,10 +167,20 @@ void softmax_xent(const Tensor& logits, const Tensor& labels, const OptT& loss, 
 }
 
 void sgd_step(const Tensor& w, const Tensor& g, const OptT& mom, const OptT& w16, double lr, double wd,
-              double momentum, double dampening, bool nesterov, bool first) {
+              double momentum, double dampening, bool nesterov, bool first, const OptT& lr_dev,
+              const OptT& seg_off, const OptT& seg_wd, int64_t base) {
   TORCH_CHECK(w.numel() == g.numel(), "sgd: size");
-  bigdl_sgd_step(mf(w, "w"), cf(g, "g"), omf(mom, "mom"), ombf(w16, "w16"), w.numel(), (float)lr, (float)wd,
-                 (float)momentum, (float)dampening, nesterov ? 1 : 0, first ? 1 : 0, stream());
+  const long* so = nullptr;
+  int nseg = 0;
+  if (seg_off && seg_off->defined()) {
+    TORCH_CHECK(seg_off->scalar_type() == at::kLong && seg_off->is_cuda(), "sgd: seg_off must be int64 GPU");
+    so = (const long*)seg_off->data_ptr();
+    nseg = (int)seg_off->numel();
+    TORCH_CHECK(seg_wd && seg_wd->numel() == nseg, "sgd: seg_wd size");
+  }
+  bigdl_sgd_step(mf(w, "w"), cf(g, "g"), omf(mom, "mom"), ombf(w16, "w16"), w.numel(), ocf(lr_dev, "lr_dev"),
+                 (float)lr, (float)wd, (float)momentum, (float)dampening, nesterov ? 1 : 0, first ? 1 : 0, so,
+                 ocf(seg_wd, "seg_wd"), nseg, (long)base, stream());
 }
 void adam_step(const Tensor& w, const Tensor& g, const Tensor& m, const Tensor& v, const OptT& w16, double lr,
                double b1, double b2, double eps, double wd, double bc1, double bc2) {
@@ -216,7 +226,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("avgpool_fwd", &avgpool_fwd);
   m.def("avgpool_bwd", &avgpool_bwd);
   m.def("softmax_xent", &softmax_xent);
-  m.def("sgd_step", &sgd_step);
+  m.def("sgd_step", &sgd_step, py::arg("w"), py::arg("g"), py::arg("mom"), py::arg("w16"), py::arg("lr"), py::arg("wd"), py::arg("momentum"), py::arg("dampening"), py::arg("nesterov"), py::arg("first"), py::arg("lr_dev") = py::none(), py::arg("seg_off") = py::none(), py::arg("seg_wd") = py::none(), py::arg("base") = 0);
   m.def("adam_step", &adam_step);
   m.def("sumsq", &sumsq);
   m.def("scale_f32", &scale_f32);

@@ -281,18 +281,34 @@ __global__ __launch_bounds__(256) void softmax_xent_kernel(const bf16_t* __restr
 }
 
 // ---------------- optimizers on flat fp32 buffers ----------------
+// Segment-wise weight decay: the flat buffer is a concatenation of parameter tensors; seg_off[i] is the
+// first (global) element of segment i and seg_wd[i] its L2 coefficient (folded layer regularizers).
+__device__ __forceinline__ float seg_decay(const long* __restrict__ seg_off, const float* __restrict__ seg_wd,
+                                           int nseg, long gi) {
+  int lo = 0, hi = nseg - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (seg_off[mid] <= gi) lo = mid; else hi = mid - 1;
+  }
+  return seg_wd[lo];
+}
+
 __global__ void sgd_kernel(float* __restrict__ w, const float* __restrict__ g, float* __restrict__ mom,
-                           bf16_t* __restrict__ w16, long n, float lr, float wd, float momentum, float dampening,
-                           int nesterov, int first) {
+                           bf16_t* __restrict__ w16, long n, const float* __restrict__ lr_dev, float lr, float wd,
+                           float momentum, float dampening, int nesterov, int first, const long* __restrict__ seg_off,
+                           const float* __restrict__ seg_wd, int nseg, long base) {
+  const float rate = lr_dev ? lr_dev[0] : lr;
   GRID_STRIDE(i, n) {
     float wi = w[i];
-    float d = g[i] + wd * wi;
+    float decay = wd;
+    if (nseg) decay += seg_decay(seg_off, seg_wd, nseg, base + i);
+    float d = g[i] + decay * wi;
     if (momentum != 0.f) {
       float b = first ? d : momentum * mom[i] + (1.f - dampening) * d;
       mom[i] = b;
       d = nesterov ? d + momentum * b : b;
     }
-    wi -= lr * d;
+    wi -= rate * d;
     w[i] = wi;
     if (w16) w16[i] = f2bf(wi);
   }
@@ -432,9 +448,11 @@ void bigdl_softmax_xent(const uint16_t* lb, const float* lf, const float* labels
   softmax_xent_kernel<<<(B + 3) / 4, 256, 0, st>>>(lb, lf, labels, loss, db, df, B, K, label_base, grad_scale);
   HIP_LAUNCH_CHECK();
 }
-void bigdl_sgd_step(float* w, const float* g, float* mom, uint16_t* w16, long n, float lr, float wd, float momentum,
-                    float dampening, int nesterov, int first, hipStream_t st) {
-  sgd_kernel<<<grid_cap(n), 256, 0, st>>>(w, g, mom, w16, n, lr, wd, momentum, dampening, nesterov, first);
+void bigdl_sgd_step(float* w, const float* g, float* mom, uint16_t* w16, long n, const float* lr_dev, float lr,
+                    float wd, float momentum, float dampening, int nesterov, int first, const long* seg_off,
+                    const float* seg_wd, int nseg, long base, hipStream_t st) {
+  sgd_kernel<<<grid_cap(n), 256, 0, st>>>(w, g, mom, w16, n, lr_dev, lr, wd, momentum, dampening, nesterov, first,
+                                          seg_off, seg_wd, nseg, base);
   HIP_LAUNCH_CHECK();
 }
 void bigdl_adam_step(float* w, const float* g, float* m, float* v, uint16_t* w16, long n, float lr, float beta1,

@@ -73,8 +73,9 @@ void bigdl_softmax_xent(const uint16_t* logits_bf16, const float* logits_f32, co
                         float label_base, float grad_scale, hipStream_t st);
 
 // optimizers over flat fp32 buffers (optional bf16 shadow written in the same pass)
-void bigdl_sgd_step(float* w, const float* g, float* mom, uint16_t* w16, long n, float lr, float wd,
-                    float momentum, float dampening, int nesterov, int first, hipStream_t st);
+void bigdl_sgd_step(float* w, const float* g, float* mom, uint16_t* w16, long n, const float* lr_dev, float lr,
+                    float wd, float momentum, float dampening, int nesterov, int first, const long* seg_off,
+                    const float* seg_wd, int nseg, long base, hipStream_t st);
 void bigdl_adam_step(float* w, const float* g, float* m, float* v, uint16_t* w16, long n, float lr,
                      float beta1, float beta2, float eps, float wd, float bc1, float bc2, hipStream_t st);
 void bigdl_sumsq(const float* x, float* out, long n, hipStream_t st);
