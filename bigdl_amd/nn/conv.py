@@ -18,6 +18,7 @@ import torch
 import torch.nn.functional as F
 
 from .. import ops
+from ..ops import bn as bnops
 from ..ops import conv as cv
 from .abstractnn import AutogradModule, TensorModule
 from .init_methods import RandomUniform, Zeros
@@ -140,7 +141,7 @@ class SpatialConvolution(TensorModule):
         w16 = self._w16_padded()
         stats = None
         if self.emit_stats and self.train:
-            stats = torch.zeros(2 * self.nOutputPlane, dtype=torch.float32, device=x.device)
+            stats = bnops.new_stats(self.nOutputPlane, x.device)
         y = cv.conv2d_fwd(x16, w16, self.bias, (self.strideH, self.strideW), (ph, pw),
                           (self.dilationH, self.dilationW), relu=self.fuse_relu, stats=stats)
         if stats is not None:

@@ -13,13 +13,29 @@ def _P(x):
     return x.numel() // x.shape[1]
 
 
+def stat_slots():
+    return native.get().STAT_SLOTS
+
+
+def new_stats(C, device):
+    """Zeroed [STAT_SLOTS][2][C] fp32 accumulation buffer (see csrc/batchnorm.hip)."""
+    return torch.zeros(stat_slots() * 2 * C, dtype=torch.float32, device=device)
+
+
+def _reduce_slots_for_sync(buf, C, P, sync_fn):
+    red = torch.empty(2 * C, dtype=torch.float32, device=buf.device)
+    native.get().bn_slot_reduce(buf, stat_slots(), C, red)
+    P = sync_fn(red, P)
+    return red, 1, P
+
+
 def bn_forward_gpu(x, gamma, beta, rmean, rvar, eps, momentum, training, stats=None, res=None, relu=False,
                    out=None, sync_fn=None):
-    """Returns (y, save_mean, save_invstd, scale).
+    """Returns (y, save_mean, save_invstd).
 
-    x: (N, C, H, W) bf16 channels_last (or (N, C) bf16 contiguous). ``stats`` may hold the (sum, sumsq)
-    already produced by the preceding conv epilogue; otherwise they are computed here. ``sync_fn(stats)``
-    (sync-BN) may all-reduce the [2, C] fp32 stats buffer across replicas before finalize.
+    x: (N, C, H, W) bf16 channels_last (or (N, C) bf16 contiguous). ``stats`` may hold the slotted
+    (sum, sumsq) already produced by the preceding conv epilogue; otherwise they are computed here.
+    ``sync_fn(buf[2C], count) -> total count`` (sync-BN) all-reduces the statistics across replicas.
     """
     C = x.shape[1]
     P = _P(x)
@@ -31,17 +47,19 @@ def bn_forward_gpu(x, gamma, beta, rmean, rvar, eps, momentum, training, stats=N
     shift = torch.empty(C, dtype=torch.float32, device=dev)
     smean = torch.empty(C, dtype=torch.float32, device=dev)
     sinv = torch.empty(C, dtype=torch.float32, device=dev)
+    nslots = stat_slots()
+    Ptot = P
     if training:
         if stats is None:
-            stats = torch.zeros(2 * C, dtype=torch.float32, device=dev)
+            stats = new_stats(C, dev)
             C_.bn_stats(x, stats, P, C)
         if sync_fn is not None:
-            P = sync_fn(stats, P)
+            stats, nslots, Ptot = _reduce_slots_for_sync(stats, C, P, sync_fn)
     else:
-        stats = torch.zeros(2 * C, dtype=torch.float32, device=dev) if stats is None else stats
-    C_.bn_finalize(stats, gamma, beta, rmean, rvar, smean, sinv, scale, shift, P, C, float(eps), float(momentum),
-                   bool(training))
-    C_.bn_apply(x, scale, shift, res, out, _P(x), C, bool(relu))
+        stats, nslots = scale, 0  # unused in inference mode
+    C_.bn_finalize(stats, nslots, gamma, beta, rmean, rvar, smean, sinv, scale, shift, Ptot, C, float(eps),
+                   float(momentum), bool(training))
+    C_.bn_apply(x, scale, shift, res, out, P, C, bool(relu))
     return out, smean, sinv
 
 
@@ -55,15 +73,17 @@ def bn_backward_gpu(dz, z, x, smean, sinv, gamma, dgamma, dbeta, training=True, 
     C = x.shape[1]
     P = _P(x)
     C_ = native.get()
-    red = None
+    red, nslots, Ptot = None, 0, P
     if training:
-        red = torch.zeros(2 * C, dtype=torch.float32, device=x.device)
+        red = new_stats(C, x.device)
         C_.bn_bwd_reduce(dz, z, x, smean, red, P, C)
+        nslots = stat_slots()
         if sync_fn is not None:
-            P = sync_fn(red, P)
+            red, nslots, Ptot = _reduce_slots_for_sync(red, C, P, sync_fn)
+    coef = torch.empty(3 * C, dtype=torch.float32, device=x.device)
     dx = torch.empty_like(x) if need_dx else None
     dres = torch.empty_like(x) if need_dres else None
-    C_.bn_bwd_apply(dz, z, x, smean, sinv, gamma, red, dx, dres, dgamma, dbeta, P, C)
+    C_.bn_bwd_apply(dz, z, x, smean, sinv, gamma, red, nslots, coef, dx, dres, dgamma, dbeta, Ptot, C)
     return dx, dres
 
 

@@ -67,24 +67,85 @@ def conv2d_fwd(x, w16, bias, stride, pad, dil=(1, 1), relu=False, stats=None, ou
     OH, OW = out_size(H, R, sh, ph, dh), out_size(W, S, sw, pw, dw)
     if out is None:
         out = torch.empty((N, K, OH, OW), dtype=BF16, device=x.device, memory_format=CL)
-    M = N * OH * OW
-    geo = [N, H, W, C, OH, OW, R, S, sh, -ph, dh, 1, sw, -pw, dw, 1, M, K, R * S * C, K]
-    native.get().conv_nt(x, w16, out, bias, stats, geo, relu)
+    native.get().conv_nt(x, w16, out, bias, stats, _fwd_geo(N, H, W, C, OH, OW, sh, sw, R * S * C, K),
+                         _fwd_taps(R, S, ph, pw, dh, dw), relu)
     return out
 
 
-def conv2d_dgrad(dy, w16t, x_shape, stride, pad, dil=(1, 1), out=None):
-    """dx = conv_transpose(dy, w). ``w16t`` is the (C, R, S, K)-ordered transposed weight (see transpose_w)."""
-    N, C, H, W = x_shape
-    _, K, OH, OW = dy.shape
-    R, S = w16t.shape[1], w16t.shape[2]
+_TAP_CACHE = {}
+
+
+def _fwd_taps(R, S, ph, pw, dh, dw):
+    key = ("f", R, S, ph, pw, dh, dw)
+    t = _TAP_CACHE.get(key)
+    if t is None:
+        t = []
+        for r in range(R):
+            for s in range(S):
+                t += [r * dh - ph, s * dw - pw, r * S + s]
+        _TAP_CACHE[key] = t
+    return t
+
+
+def _fwd_geo(N, H, W, C, OH, OW, sh, sw, ldw, K):
+    return [N, H, W, C, OH, OW, sh, sw, ldw, K, K, OH, OW, 1, 1, 0, 0]
+
+
+def dgrad_phases(H, W, R, S, stride, pad, dil):
+    """Decompose the data gradient of a stride-(sh, sw) conv into sh*sw dense phase GEMMs.
+
+    Output pixel h = a + sh*i receives tap r iff (a + ph - r*dh) % sh == 0, from dY row
+    i + (a + ph - r*dh) / sh. Returns [(a, b, nI, nJ, taps)] (taps as flat [th, tw, tap_index] triples);
+    phases without taps are omitted (their pixels get zero gradient).
+    """
     sh, sw = stride
     ph, pw = pad
     dh, dw = dil
+    key = ("d", H, W, R, S, sh, sw, ph, pw, dh, dw)
+    res = _TAP_CACHE.get(key)
+    if res is not None:
+        return res
+    res = []
+    for a in range(sh):
+        for b in range(sw):
+            nI, nJ = -(-(H - a) // sh), -(-(W - b) // sw)
+            if nI <= 0 or nJ <= 0:
+                continue
+            taps = []
+            for r in range(R):
+                if (a + ph - r * dh) % sh:
+                    continue
+                for s in range(S):
+                    if (b + pw - s * dw) % sw:
+                        continue
+                    taps += [(a + ph - r * dh) // sh, (b + pw - s * dw) // sw, r * S + s]
+            if taps:
+                res.append((a, b, nI, nJ, taps))
+    _TAP_CACHE[key] = res
+    return res
+
+
+def conv2d_dgrad(dy, w16t, x_shape, stride, pad, dil=(1, 1), out=None):
+    """dx = conv_transpose(dy, w). ``w16t`` is the (C, R, S, K)-ordered transposed weight (see transpose_w).
+
+    Stride > 1 runs one dense implicit GEMM per stride phase (no zero-insertion, no masked MFMAs).
+    """
+    N, C, H, W = x_shape
+    _, K, OH, OW = dy.shape
+    R, S = w16t.shape[1], w16t.shape[2]
+    phases = dgrad_phases(H, W, R, S, stride, pad, dil)
+    covered = sum(nI * nJ for (_, _, nI, nJ, _) in phases)
     if out is None:
         out = torch.empty((N, C, H, W), dtype=BF16, device=dy.device, memory_format=CL)
-    geo = [N, OH, OW, K, H, W, R, S, 1, ph, -dh, sh, 1, pw, -dw, sw, N * H * W, C, R * S * K, C]
-    native.get().conv_nt(dy, w16t, out, None, None, geo, False)
+        if covered != H * W:
+            out.zero_()
+    elif covered != H * W:
+        out.zero_()
+    C_ = native.get()
+    ldw = R * S * K
+    for (a, b, nI, nJ, taps) in phases:
+        geo = [N, OH, OW, K, nI, nJ, 1, 1, ldw, C, C, H, W, stride[0], stride[1], a, b]
+        C_.conv_nt(dy, w16t, out, None, None, geo, taps, False)
     return out
 
 

@@ -13,6 +13,8 @@
 #include "common.h"
 #include "kernels.h"
 
+#define STAT_SLOTS BIGDL_STAT_SLOTS
+
 namespace {
 
 // Generic per-channel reduction over P rows of C channels (C % 8 == 0).
@@ -73,13 +75,15 @@ __global__ __launch_bounds__(256) void chan_reduce_kernel(const bf16_t* __restri
       float t = 0.f;
       for (int rs = 0; rs < rpi; ++rs) t += sm[(rs * gcount + gg) * 16 + slot];
       const int ch = (gbase + gg) * 8 + (slot & 7);
-      atomicAdd(out + (slot < 8 ? 0 : C) + ch, t);
+      // spread over STAT_SLOTS copies: thousands of workgroups adding into the same 2C words serialise at
+      // the memory-side atomic unit (MI355X_MICROARCH "contention"); finalize sums the slots.
+      atomicAdd(out + (size_t)(blockIdx.x & (STAT_SLOTS - 1)) * 2 * C + (slot < 8 ? 0 : C) + ch, t);
     }
     __syncthreads();
   }
 }
 
-__global__ void bn_finalize_kernel(const float* __restrict__ stats, const float* __restrict__ gamma,
+__global__ void bn_finalize_kernel(const float* __restrict__ stats, int nslots, const float* __restrict__ gamma,
                                    const float* __restrict__ beta, float* run_mean, float* run_var, float* save_mean,
                                    float* save_invstd, float* scale, float* shift, long P, int C, float eps,
                                    float momentum, int training) {
@@ -87,8 +91,10 @@ __global__ void bn_finalize_kernel(const float* __restrict__ stats, const float*
   if (c >= C) return;
   float mean, invstd;
   if (training) {
-    mean = stats[c] / (float)P;
-    const float var = fmaxf(stats[C + c] / (float)P - mean * mean, 0.f);
+    double s1 = 0.0, s2 = 0.0;
+    for (int k = 0; k < nslots; ++k) { s1 += stats[(size_t)k * 2 * C + c]; s2 += stats[(size_t)k * 2 * C + C + c]; }
+    mean = (float)(s1 / (double)P);
+    const float var = fmaxf((float)(s2 / (double)P - (double)mean * mean), 0.f);
     invstd = rsqrtf(var + eps);
     save_mean[c] = mean;
     save_invstd[c] = invstd;
@@ -133,12 +139,46 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* __restrict_
   }
 }
 
+// Per-channel backward coefficients: dx = A*dy + B*x + D (dy = dz masked by the fused ReLU), with
+//   A = g*is, B = -g*is^2*mean(dy*xhat)/... , D = g*is*(mean*is*m_dyx - m_dy); param grads folded in.
+__global__ void bn_bwd_coeff_kernel(const float* __restrict__ red, int nslots, const float* __restrict__ mean,
+                                    const float* __restrict__ invstd, const float* __restrict__ gamma,
+                                    float* __restrict__ coef, float* dgamma, float* dbeta, long P, int C, int training) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float is = invstd[c];
+  const float g = gamma ? gamma[c] : 1.f;
+  float A = g * is, B = 0.f, D = 0.f;
+  if (training) {
+    double sdy = 0.0, sdyx = 0.0;
+    for (int k = 0; k < nslots; ++k) { sdy += red[(size_t)k * 2 * C + c]; sdyx += red[(size_t)k * 2 * C + C + c]; }
+    const float mdy = (float)(sdy / (double)P);
+    const float mdyx = (float)(sdyx / (double)P) * is;     // mean(dy * xhat)
+    B = -g * is * is * mdyx;
+    D = g * is * (mean[c] * is * mdyx - mdy);
+    if (dgamma) dgamma[c] += (float)sdyx * is;
+    if (dbeta) dbeta[c] += (float)sdy;
+  }
+  coef[c] = A; coef[C + c] = B; coef[2 * C + c] = D;
+}
+
+__global__ void bn_slot_reduce_kernel(const float* __restrict__ in, int nslots, int C, float* __restrict__ out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= 2 * C) return;
+  float t = 0.f;
+  for (int k = 0; k < nslots; ++k) t += in[(size_t)k * 2 * C + c];
+  out[c] = t;
+}
+
+__device__ __forceinline__ void load8(const float* p, float* v) {
+  const v4f a = *reinterpret_cast<const v4f*>(p), b = *reinterpret_cast<const v4f*>(p + 4);
+  v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3]; v[4] = b[0]; v[5] = b[1]; v[6] = b[2]; v[7] = b[3];
+}
+
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16_t* __restrict__ dz, const bf16_t* __restrict__ z,
-                                                           const bf16_t* __restrict__ x, const float* __restrict__ mean,
-                                                           const float* __restrict__ invstd, const float* __restrict__ gamma,
-                                                           const float* __restrict__ red, bf16_t* __restrict__ dx,
-                                                           bf16_t* __restrict__ dres, long ngran, int C, float invP,
-                                                           int training) {
+                                                           const bf16_t* __restrict__ x, const float* __restrict__ coef,
+                                                           bf16_t* __restrict__ dx, bf16_t* __restrict__ dres, long ngran,
+                                                           int C) {
   const int G = C >> 3;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < ngran; i += (long)gridDim.x * blockDim.x) {
     const int c0 = (int)(i % G) * 8;
@@ -146,42 +186,23 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16_t* __restr
     v4u vz = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
     if (z) vz = reinterpret_cast<const v4u*>(z)[i];
     const v4u vx = reinterpret_cast<const v4u*>(x)[i];
+    float A[8], B[8], D[8];
+    load8(coef + c0, A);
+    load8(coef + C + c0, B);
+    load8(coef + 2 * C + c0, D);
     v4u o, od;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      float dy[2] = {lo_bf(vd[e]), hi_bf(vd[e])};
-      const float zz[2] = {lo_bf(vz[e]), hi_bf(vz[e])};
-      const float xx[2] = {lo_bf(vx[e]), hi_bf(vx[e])};
-      float r[2];
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int c = c0 + 2 * e + h;
-        if (z && !(zz[h] > 0.f)) dy[h] = 0.f;
-        const float is = invstd[c];
-        const float g = gamma ? gamma[c] : 1.f;
-        if (training) {
-          const float mdy = red[c] * invP;
-          const float mdyx = red[C + c] * invP * is;       // mean(dy * xhat)
-          const float xh = (xx[h] - mean[c]) * is;
-          r[h] = g * is * (dy[h] - mdy - xh * mdyx);
-        } else {
-          r[h] = g * is * dy[h];
-        }
-      }
-      o[e] = pack2bf(r[0], r[1]);
-      od[e] = pack2bf(dy[0], dy[1]);
+      float d0 = lo_bf(vd[e]), d1 = hi_bf(vd[e]);
+      if (z) { if (!(lo_bf(vz[e]) > 0.f)) d0 = 0.f; if (!(hi_bf(vz[e]) > 0.f)) d1 = 0.f; }
+      const float r0 = A[2 * e] * d0 + B[2 * e] * lo_bf(vx[e]) + D[2 * e];
+      const float r1 = A[2 * e + 1] * d1 + B[2 * e + 1] * hi_bf(vx[e]) + D[2 * e + 1];
+      o[e] = pack2bf(r0, r1);
+      od[e] = pack2bf(d0, d1);
     }
-    reinterpret_cast<v4u*>(dx)[i] = o;
+    if (dx) reinterpret_cast<v4u*>(dx)[i] = o;
     if (dres) reinterpret_cast<v4u*>(dres)[i] = od;
   }
-}
-
-__global__ void bn_param_grad_kernel(const float* __restrict__ red, const float* __restrict__ invstd, float* dgamma,
-                                     float* dbeta, int C) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  if (dgamma) dgamma[c] += red[C + c] * invstd[c];
-  if (dbeta) dbeta[c] += red[c];
 }
 
 int grid_for(long work, int per_block, int cap) {
@@ -213,11 +234,16 @@ void bigdl_bn_stats(const uint16_t* x, float* stats, long P, int C, hipStream_t 
   HIP_LAUNCH_CHECK();
 }
 
-void bigdl_bn_finalize(const float* stats, const float* gamma, const float* beta, float* run_mean, float* run_var,
-                       float* save_mean, float* save_invstd, float* scale, float* shift, long P, int C, float eps,
-                       float momentum, int training, hipStream_t st) {
-  bn_finalize_kernel<<<(C + 255) / 256, 256, 0, st>>>(stats, gamma, beta, run_mean, run_var, save_mean, save_invstd,
-                                                       scale, shift, P, C, eps, momentum, training);
+void bigdl_bn_finalize(const float* stats, int nslots, const float* gamma, const float* beta, float* run_mean,
+                       float* run_var, float* save_mean, float* save_invstd, float* scale, float* shift, long P, int C,
+                       float eps, float momentum, int training, hipStream_t st) {
+  bn_finalize_kernel<<<(C + 255) / 256, 256, 0, st>>>(stats, nslots, gamma, beta, run_mean, run_var, save_mean,
+                                                       save_invstd, scale, shift, P, C, eps, momentum, training);
+  HIP_LAUNCH_CHECK();
+}
+
+void bigdl_bn_slot_reduce(const float* in, int nslots, int C, float* out, hipStream_t st) {
+  bn_slot_reduce_kernel<<<(2 * C + 255) / 256, 256, 0, st>>>(in, nslots, C, out);
   HIP_LAUNCH_CHECK();
 }
 
@@ -235,15 +261,14 @@ void bigdl_bn_bwd_reduce(const uint16_t* dz, const uint16_t* z, const uint16_t* 
 }
 
 void bigdl_bn_bwd_apply(const uint16_t* dz, const uint16_t* z, const uint16_t* x, const float* mean,
-                        const float* invstd, const float* gamma, const float* red, uint16_t* dx, uint16_t* dres,
-                        float* dgamma, float* dbeta, long P, int C, hipStream_t st) {
+                        const float* invstd, const float* gamma, const float* red, int nslots, float* coef,
+                        uint16_t* dx, uint16_t* dres, float* dgamma, float* dbeta, long P, int C, int training,
+                        hipStream_t st) {
+  bn_bwd_coeff_kernel<<<(C + 255) / 256, 256, 0, st>>>(red, nslots, mean, invstd, gamma, coef, dgamma, dbeta, P, C,
+                                                        training);
   const long ngran = P * (C >> 3);
-  const int training = red != nullptr;
-  if (dx)
-    bn_bwd_apply_kernel<<<grid_for(ngran, 256, 8192), 256, 0, st>>>(dz, z, x, mean, invstd, gamma, red, dx, dres,
-                                                                    ngran, C, 1.f / (float)P, training);
-  if (training && (dgamma || dbeta))
-    bn_param_grad_kernel<<<(C + 255) / 256, 256, 0, st>>>(red, invstd, dgamma, dbeta, C);
+  if (dx || dres)
+    bn_bwd_apply_kernel<<<grid_for(ngran, 256, 8192), 256, 0, st>>>(dz, z, x, coef, dx, dres, ngran, C);
   HIP_LAUNCH_CHECK();
 }
 

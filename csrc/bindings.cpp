@@ -6,6 +6,7 @@
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
 #include <vector>
+#include <algorithm>
 #include "kernels.h"
 
 namespace {
@@ -28,21 +29,35 @@ uint16_t* ombf(const OptT& t, const char* n) { return (t && t->defined()) ? mbf(
 const float* ocf(const OptT& t, const char* n) { return (t && t->defined()) ? cf(*t, n) : nullptr; }
 float* omf(const OptT& t, const char* n) { return (t && t->defined()) ? mf(*t, n) : nullptr; }
 
-// geo = [Nb, Hs, Ws, Cs, OH, OW, R, S, mul_h, off_h, step_h, div_h, mul_w, off_w, step_w, div_w, M, Ncol, Kdim, ldo]
+// geo = [Nb, Hs, Ws, Cs, OH, OW, mul_h, mul_w, ldw, Ncol, ldo, OHo, OWo, omul_h, omul_w, ooff_h, ooff_w]
+// taps = flat [tap_h0, tap_w0, tap_k0, tap_h1, ...]
 void conv_nt(const Tensor& src, const Tensor& wt, const Tensor& out, const OptT& bias, const OptT& stats,
-             std::vector<int64_t> geo, bool relu) {
-  TORCH_CHECK(geo.size() == 20, "conv_nt: bad geometry");
+             std::vector<int64_t> geo, std::vector<int64_t> taps, bool relu) {
+  TORCH_CHECK(geo.size() == 17, "conv_nt: bad geometry");
+  if (stats && stats->defined())
+    TORCH_CHECK(stats->numel() >= BIGDL_STAT_SLOTS * 2 * geo[9], "conv_nt: stats must hold STAT_SLOTS x 2Ncol");
+  TORCH_CHECK(taps.size() % 3 == 0 && !taps.empty() && taps.size() / 3 <= CONV_MAX_TAPS, "conv_nt: bad taps");
   ConvArgs a;
   a.src = cbf(src, "src"); a.wt = cbf(wt, "wt"); a.out = mbf(out, "out");
   a.bias = ocf(bias, "bias"); a.stats = omf(stats, "stats");
-  int* f = &a.Nb;
-  for (int i = 0; i < 20; ++i) f[i] = (int)geo[i];
+  a.Nb = geo[0]; a.Hs = geo[1]; a.Ws = geo[2]; a.Cs = geo[3]; a.OH = geo[4]; a.OW = geo[5];
+  a.mul_h = geo[6]; a.mul_w = geo[7]; a.ldw = geo[8]; a.Ncol = geo[9]; a.ldo = geo[10];
+  a.OHo = geo[11]; a.OWo = geo[12]; a.omul_h = geo[13]; a.omul_w = geo[14]; a.ooff_h = geo[15]; a.ooff_w = geo[16];
+  a.ntaps = (int)(taps.size() / 3);
+  a.Kdim = a.ntaps * a.Cs;
+  a.M = a.Nb * a.OH * a.OW;
+  a.ident_out = (a.OHo == a.OH && a.OWo == a.OW && a.omul_h == 1 && a.omul_w == 1 && a.ooff_h == 0 && a.ooff_w == 0);
   a.relu = relu ? 1 : 0;
+  int max_tk = 0;
+  for (int t = 0; t < a.ntaps; ++t) {
+    a.tap_h[t] = (short)taps[3 * t]; a.tap_w[t] = (short)taps[3 * t + 1]; a.tap_k[t] = (short)taps[3 * t + 2];
+    max_tk = std::max(max_tk, (int)a.tap_k[t]);
+  }
   TORCH_CHECK(src.numel() >= (int64_t)a.Nb * a.Hs * a.Ws * a.Cs, "conv_nt: src too small");
-  TORCH_CHECK(wt.numel() >= (int64_t)a.Ncol * a.Kdim, "conv_nt: weight too small");
-  TORCH_CHECK(out.numel() >= (int64_t)(a.M - 1) * a.ldo + a.Ncol, "conv_nt: out too small");
-  TORCH_CHECK(a.M == a.Nb * a.OH * a.OW, "conv_nt: M mismatch");
-  TORCH_CHECK(a.Kdim == a.R * a.S * a.Cs, "conv_nt: Kdim mismatch");
+  TORCH_CHECK(wt.numel() >= (int64_t)(a.Ncol - 1) * a.ldw + (int64_t)(max_tk + 1) * a.Cs, "conv_nt: weight too small");
+  TORCH_CHECK(out.numel() >= ((int64_t)a.Nb * a.OHo * a.OWo - 1) * a.ldo + a.Ncol, "conv_nt: out too small");
+  TORCH_CHECK((a.OH - 1) * a.omul_h + a.ooff_h < a.OHo && (a.OW - 1) * a.omul_w + a.ooff_w < a.OWo,
+              "conv_nt: output placement out of range");
   const int rc = bigdl_conv_nt(&a, stream());
   TORCH_CHECK(rc == 0, "conv_nt: unsupported shape (channels must be a multiple of 8)");
 }
@@ -70,14 +85,20 @@ void transpose_krsc(const Tensor& w, const Tensor& wt, int64_t K, int64_t RS, in
 
 void bn_stats(const Tensor& x, const Tensor& stats, int64_t P, int64_t C) {
   TORCH_CHECK(C % 8 == 0 && x.numel() == P * C, "bn_stats: shape");
+  TORCH_CHECK(stats.numel() >= BIGDL_STAT_SLOTS * 2 * C, "bn_stats: stats must hold STAT_SLOTS x 2C");
   bigdl_bn_stats(cbf(x, "x"), mf(stats, "stats"), P, (int)C, stream());
 }
-void bn_finalize(const Tensor& stats, const OptT& gamma, const OptT& beta, const OptT& rmean, const OptT& rvar,
-                 const OptT& smean, const OptT& sinv, const Tensor& scale, const Tensor& shift, int64_t P, int64_t C,
-                 double eps, double momentum, bool training) {
-  bigdl_bn_finalize(cf(stats, "stats"), ocf(gamma, "gamma"), ocf(beta, "beta"), omf(rmean, "rmean"),
+void bn_finalize(const Tensor& stats, int64_t nslots, const OptT& gamma, const OptT& beta, const OptT& rmean,
+                 const OptT& rvar, const OptT& smean, const OptT& sinv, const Tensor& scale, const Tensor& shift,
+                 int64_t P, int64_t C, double eps, double momentum, bool training) {
+  TORCH_CHECK(stats.numel() >= nslots * 2 * C, "bn_finalize: stats size");
+  bigdl_bn_finalize(cf(stats, "stats"), (int)nslots, ocf(gamma, "gamma"), ocf(beta, "beta"), omf(rmean, "rmean"),
                     omf(rvar, "rvar"), omf(smean, "smean"), omf(sinv, "sinv"), mf(scale, "scale"),
                     mf(shift, "shift"), P, (int)C, (float)eps, (float)momentum, training ? 1 : 0, stream());
+}
+void bn_slot_reduce(const Tensor& in, int64_t nslots, int64_t C, const Tensor& out) {
+  TORCH_CHECK(in.numel() >= nslots * 2 * C && out.numel() >= 2 * C, "bn_slot_reduce: size");
+  bigdl_bn_slot_reduce(cf(in, "in"), (int)nslots, (int)C, mf(out, "out"), stream());
 }
 void bn_apply(const Tensor& x, const Tensor& scale, const Tensor& shift, const OptT& res, const Tensor& y, int64_t P,
               int64_t C, bool relu) {
@@ -88,15 +109,19 @@ void bn_apply(const Tensor& x, const Tensor& scale, const Tensor& shift, const O
 void bn_bwd_reduce(const Tensor& dz, const OptT& z, const Tensor& x, const Tensor& mean, const Tensor& red, int64_t P,
                    int64_t C) {
   TORCH_CHECK(C % 8 == 0 && x.numel() == P * C && dz.numel() == P * C, "bn_bwd_reduce: shape");
+  TORCH_CHECK(red.numel() >= BIGDL_STAT_SLOTS * 2 * C, "bn_bwd_reduce: red must hold STAT_SLOTS x 2C");
   bigdl_bn_bwd_reduce(cbf(dz, "dz"), ocbf(z, "z"), cbf(x, "x"), cf(mean, "mean"), mf(red, "red"), P, (int)C,
                       stream());
 }
 void bn_bwd_apply(const Tensor& dz, const OptT& z, const Tensor& x, const Tensor& mean, const Tensor& invstd,
-                  const OptT& gamma, const OptT& red, const OptT& dx, const OptT& dres, const OptT& dgamma,
-                  const OptT& dbeta, int64_t P, int64_t C) {
+                  const OptT& gamma, const OptT& red, int64_t nslots, const Tensor& coef, const OptT& dx,
+                  const OptT& dres, const OptT& dgamma, const OptT& dbeta, int64_t P, int64_t C) {
+  TORCH_CHECK(coef.numel() >= 3 * C, "bn_bwd_apply: coef size");
+  const bool training = red && red->defined();
   bigdl_bn_bwd_apply(cbf(dz, "dz"), ocbf(z, "z"), cbf(x, "x"), cf(mean, "mean"), cf(invstd, "invstd"),
-                     ocf(gamma, "gamma"), ocf(red, "red"), ombf(dx, "dx"), ombf(dres, "dres"), omf(dgamma, "dgamma"),
-                     omf(dbeta, "dbeta"), P, (int)C, stream());
+                     ocf(gamma, "gamma"), ocf(red, "red"), (int)nslots, mf(coef, "coef"), ombf(dx, "dx"),
+                     ombf(dres, "dres"), omf(dgamma, "dgamma"), omf(dbeta, "dbeta"), P, (int)C, training ? 1 : 0,
+                     stream());
 }
 
 void relu_fwd(const Tensor& x, const Tensor& y) {
@@ -213,6 +238,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_stats", &bn_stats);
   m.def("bn_finalize", &bn_finalize);
   m.def("bn_apply", &bn_apply);
+  m.def("bn_slot_reduce", &bn_slot_reduce);
+  m.attr("STAT_SLOTS") = BIGDL_STAT_SLOTS;
   m.def("bn_bwd_reduce", &bn_bwd_reduce);
   m.def("bn_bwd_apply", &bn_bwd_apply);
   m.def("relu_fwd", &relu_fwd);

@@ -27,7 +27,7 @@ namespace {
 
 constexpr int BK = 64;          // K elements per LDS stage (8 granules of 16 B per row)
 
-template <int BM, int BN, int WM, bool FASTK, bool DIV>
+template <int BM, int BN, int WM, bool FASTK>
 __global__ __launch_bounds__(256, 2) void conv_nt_kernel(ConvArgs a) {
   constexpr int WN = 4 / WM;
   constexpr int TM = BM / WM, TN = BN / WN;      // per-wave tile
@@ -57,8 +57,8 @@ __global__ __launch_bounds__(256, 2) void conv_nt_kernel(ConvArgs a) {
       const int nb = m / ohw, rem = m - nb * ohw;
       const int oh = rem / a.OW, ow = rem - oh * a.OW;
       a_pix[i] = nb * a.Hs * a.Ws;
-      a_h[i] = oh * a.mul_h + a.off_h;
-      a_w[i] = ow * a.mul_w + a.off_w;
+      a_h[i] = oh * a.mul_h;
+      a_w[i] = ow * a.mul_w;
     } else {
       a_pix[i] = 0; a_h[i] = -(1 << 28); a_w[i] = -(1 << 28);
     }
@@ -69,35 +69,31 @@ __global__ __launch_bounds__(256, 2) void conv_nt_kernel(ConvArgs a) {
   for (int i = 0; i < BROWS; ++i) {
     const int n = n0 + lrow + 32 * i;
     bvalid[i] = n < a.Ncol;
-    wrow[i] = a.wt + (size_t)(bvalid[i] ? n : 0) * a.Kdim;
+    wrow[i] = a.wt + (size_t)(bvalid[i] ? n : 0) * a.ldw;
   }
 
   v4u ra[AROWS], rb[BROWS];
-  const int SC = a.S * a.Cs;
   auto gload = [&](int kt) {
-    int kk, r, s, c;
+    int t, c, wk;
     bool kvalid;
     if constexpr (FASTK) {
-      const int k0 = kt * BK;                 // whole BK chunk shares (r, s)
-      r = k0 / SC; const int rem = k0 - r * SC;
-      s = rem / a.Cs; c = rem - s * a.Cs + lg * 8;
-      kk = k0 + lg * 8; kvalid = true;
+      const int k0 = kt * BK;                 // the whole BK chunk lies in one tap (Cs % BK == 0)
+      t = k0 / a.Cs;
+      c = k0 - t * a.Cs + lg * 8;
+      kvalid = true;
     } else {
-      kk = kt * BK + lg * 8;
+      const int kk = kt * BK + lg * 8;
       kvalid = kk < a.Kdim;
       const int kc = kvalid ? kk : 0;
-      r = kc / SC; const int rem = kc - r * SC;
-      s = rem / a.Cs; c = rem - s * a.Cs;
+      t = kc / a.Cs;
+      c = kc - t * a.Cs;
     }
+    const int th = a.tap_h[t], tw = a.tap_w[t];
+    wk = a.tap_k[t] * a.Cs + c;
 #pragma unroll
     for (int i = 0; i < AROWS; ++i) {
-      int ch = a_h[i] + r * a.step_h, cw = a_w[i] + s * a.step_w;
-      bool ok = kvalid;
-      if constexpr (DIV) {
-        ok = ok && ch >= 0 && cw >= 0 && (ch % a.div_h) == 0 && (cw % a.div_w) == 0;
-        ch /= a.div_h; cw /= a.div_w;
-      }
-      ok = ok && (unsigned)ch < (unsigned)a.Hs && (unsigned)cw < (unsigned)a.Ws;
+      const int ch = a_h[i] + th, cw = a_w[i] + tw;
+      const bool ok = kvalid && (unsigned)ch < (unsigned)a.Hs && (unsigned)cw < (unsigned)a.Ws;
       v4u v = {0u, 0u, 0u, 0u};
       if (ok) v = *reinterpret_cast<const v4u*>(a.src + ((size_t)(a_pix[i] + ch * a.Ws + cw) * a.Cs + c));
       ra[i] = v;
@@ -105,7 +101,7 @@ __global__ __launch_bounds__(256, 2) void conv_nt_kernel(ConvArgs a) {
 #pragma unroll
     for (int i = 0; i < BROWS; ++i) {
       v4u v = {0u, 0u, 0u, 0u};
-      if (bvalid[i] && kvalid) v = *reinterpret_cast<const v4u*>(wrow[i] + kk);
+      if (bvalid[i] && kvalid) v = *reinterpret_cast<const v4u*>(wrow[i] + wk);
       rb[i] = v;
     }
   };
@@ -172,6 +168,12 @@ __global__ __launch_bounds__(256, 2) void conv_nt_kernel(ConvArgs a) {
 #pragma unroll
     for (int i = 0; i < MI; ++i) {
       const int m = m0 + wm * TM + i * 16 + (lane & 15);
+      long orow = m;
+      if (!a.ident_out && m < a.M) {
+        const int nb = m / ohw, rem = m - nb * ohw;
+        const int oh = rem / a.OW, ow = rem - oh * a.OW;
+        orow = ((long)nb * a.OHo + oh * a.omul_h + a.ooff_h) * a.OWo + ow * a.omul_w + a.ooff_w;
+      }
       float v[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -186,7 +188,7 @@ __global__ __launch_bounds__(256, 2) void conv_nt_kernel(ConvArgs a) {
           s2[0] += lo_bf(p0) * lo_bf(p0); s2[1] += hi_bf(p0) * hi_bf(p0);
           s2[2] += lo_bf(p1) * lo_bf(p1); s2[3] += hi_bf(p1) * hi_bf(p1);
         }
-        bf16_t* o = a.out + (size_t)m * a.ldo + nb;
+        bf16_t* o = a.out + (size_t)orow * a.ldo + nb;
         if (vec_ok && nb + 3 < a.Ncol) {
           *reinterpret_cast<v2u*>(o) = v2u{p0, p1};
         } else {
@@ -210,8 +212,9 @@ __global__ __launch_bounds__(256, 2) void conv_nt_kernel(ConvArgs a) {
 #pragma unroll
         for (int e = 0; e < 4; ++e)
           if (nb + e < a.Ncol) {
-            atomicAdd(a.stats + nb + e, s1[e]);
-            atomicAdd(a.stats + a.Ncol + nb + e, s2[e]);
+            float* sp = a.stats + (size_t)(bid & (BIGDL_STAT_SLOTS - 1)) * 2 * a.Ncol;  // slot: see batchnorm.hip
+            atomicAdd(sp + nb + e, s1[e]);
+            atomicAdd(sp + a.Ncol + nb + e, s2[e]);
           }
       }
     }
@@ -400,16 +403,11 @@ __global__ void transpose_krsc_kernel(const bf16_t* __restrict__ w, bf16_t* __re
 }
 
 template <int BM, int BN, int WM>
-void launch_nt(const ConvArgs& a, bool fastk, bool div, hipStream_t st) {
+void launch_nt(const ConvArgs& a, bool fastk, hipStream_t st) {
   const int nwg = ((a.M + BM - 1) / BM) * ((a.Ncol + BN - 1) / BN);
   dim3 grid(nwg), block(256);
-  if (fastk) {
-    if (div) conv_nt_kernel<BM, BN, WM, true, true><<<grid, block, 0, st>>>(a);
-    else conv_nt_kernel<BM, BN, WM, true, false><<<grid, block, 0, st>>>(a);
-  } else {
-    if (div) conv_nt_kernel<BM, BN, WM, false, true><<<grid, block, 0, st>>>(a);
-    else conv_nt_kernel<BM, BN, WM, false, false><<<grid, block, 0, st>>>(a);
-  }
+  if (fastk) conv_nt_kernel<BM, BN, WM, true><<<grid, block, 0, st>>>(a);
+  else conv_nt_kernel<BM, BN, WM, false><<<grid, block, 0, st>>>(a);
 }
 
 }  // namespace
@@ -418,11 +416,11 @@ extern "C" {
 
 // Forward or data-gradient implicit GEMM. Returns 0 on success, negative on unsupported shapes.
 int bigdl_conv_nt(const ConvArgs* a, hipStream_t st) {
-  if (a->Cs % 8 != 0 || a->Kdim % 8 != 0) return -1;
+  if (a->Cs % 8 != 0 || a->Kdim != a->ntaps * a->Cs || a->ntaps < 1 || a->ntaps > CONV_MAX_TAPS) return -1;
+  if (a->M <= 0) return 0;
   const bool fastk = (a->Cs % BK) == 0;
-  const bool div = a->div_h > 1 || a->div_w > 1;
-  if (a->Ncol <= 64) launch_nt<128, 64, 2>(*a, fastk, div, st);
-  else launch_nt<128, 128, 2>(*a, fastk, div, st);
+  if (a->Ncol <= 64) launch_nt<128, 64, 2>(*a, fastk, st);
+  else launch_nt<128, 128, 2>(*a, fastk, st);
   HIP_LAUNCH_CHECK();
   return 0;
 }

@@ -4,6 +4,12 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#define CONV_MAX_TAPS 64
+// Implicit-GEMM "NT" convolution launch (forward, or one stride phase of the data gradient):
+//   out[orow(m)][n] = sum_{t < ntaps, c < Cs} src[pix(m) + (o_h*mul_h + tap_h[t], o_w*mul_w + tap_w[t])][c]
+//                                             * wt[n*ldw + tap_k[t]*Cs + c]
+// where m = (nb, o_h, o_w) over the Nb x OH x OW grid and orow(m) places the row in an OHo x OWo output grid
+// at (o_h*omul_h + ooff_h, o_w*omul_w + ooff_w) (identity when ident_out).
 struct ConvArgs {
   const uint16_t* src;
   const uint16_t* wt;
@@ -12,11 +18,12 @@ struct ConvArgs {
   float* stats;
   int Nb, Hs, Ws, Cs;
   int OH, OW;
-  int R, S;
-  int mul_h, off_h, step_h, div_h;
-  int mul_w, off_w, step_w, div_w;
+  int mul_h, mul_w;
+  int ntaps, ldw;
   int M, Ncol, Kdim, ldo;
+  int OHo, OWo, omul_h, omul_w, ooff_h, ooff_w, ident_out;
   int relu;
+  short tap_h[CONV_MAX_TAPS], tap_w[CONV_MAX_TAPS], tap_k[CONV_MAX_TAPS];
 };
 
 struct WgradArgs {
@@ -35,18 +42,22 @@ int bigdl_conv_nt(const ConvArgs* a, hipStream_t st);
 int bigdl_conv_wgrad(const WgradArgs* a, hipStream_t st);
 void bigdl_transpose_krsc(const uint16_t* w, uint16_t* wt, int K, int RS, int C, hipStream_t st);
 
-// batch norm (NHWC bf16, fp32 statistics)
+// batch norm (NHWC bf16, fp32 statistics). Statistics / backward-reduction buffers are
+// [BIGDL_STAT_SLOTS][2][C] fp32, zeroed by the caller; producers add into slot (block id % slots).
+#define BIGDL_STAT_SLOTS 32
 void bigdl_bn_stats(const uint16_t* x, float* stats, long P, int C, hipStream_t st);
-void bigdl_bn_finalize(const float* stats, const float* gamma, const float* beta, float* run_mean,
+void bigdl_bn_finalize(const float* stats, int nslots, const float* gamma, const float* beta, float* run_mean,
                        float* run_var, float* save_mean, float* save_invstd, float* scale, float* shift,
                        long P, int C, float eps, float momentum, int training, hipStream_t st);
+void bigdl_bn_slot_reduce(const float* in, int nslots, int C, float* out, hipStream_t st);
 void bigdl_bn_apply(const uint16_t* x, const float* scale, const float* shift, const uint16_t* res,
                     uint16_t* y, long P, int C, int relu, hipStream_t st);
 void bigdl_bn_bwd_reduce(const uint16_t* dz, const uint16_t* z, const uint16_t* x, const float* mean,
                          float* red, long P, int C, hipStream_t st);
 void bigdl_bn_bwd_apply(const uint16_t* dz, const uint16_t* z, const uint16_t* x, const float* mean,
-                        const float* invstd, const float* gamma, const float* red, uint16_t* dx,
-                        uint16_t* dres, float* dgamma, float* dbeta, long P, int C, hipStream_t st);
+                        const float* invstd, const float* gamma, const float* red, int nslots, float* coef,
+                        uint16_t* dx, uint16_t* dres, float* dgamma, float* dbeta, long P, int C, int training,
+                        hipStream_t st);
 
 // elementwise
 void bigdl_relu_fwd(const uint16_t* x, uint16_t* y, long n, hipStream_t st);

@@ -45,13 +45,16 @@ def test_conv_fwd_dgrad_wgrad(case):
     w = w32.to(BF, memory_format=CL)
     xr, wr = x.float(), w.float()
     # forward (+bias, +stats)
-    stats = torch.zeros(2 * K, device=dev)
+    from bigdl_amd.ops import bn as bnops
+
+    stats = bnops.new_stats(K, dev)
     y = cv.conv2d_fwd(x, w, b32, (st, st), (pd, pd), stats=stats)
     yr = F.conv2d(xr, wr, b32, stride=st, padding=pd)
     assert y.shape == yr.shape
     assert _rel(y, yr) < 1e-2
-    assert _rel(stats[:K], y.float().sum(dim=(0, 2, 3))) < 2e-2
-    assert _rel(stats[K:], (y.float() ** 2).sum(dim=(0, 2, 3))) < 2e-2
+    st2 = stats.view(bnops.stat_slots(), 2, K).sum(0)
+    assert _rel(st2[0], y.float().sum(dim=(0, 2, 3))) < 2e-2
+    assert _rel(st2[1], (y.float() ** 2).sum(dim=(0, 2, 3))) < 2e-2
     # relu epilogue
     y2 = cv.conv2d_fwd(x, w, b32, (st, st), (pd, pd), relu=True)
     assert _rel(y2, torch.relu(yr)) < 1e-2
