@@ -18,11 +18,14 @@ def add_activity(a, b):
     if b is None:
         return a
     if isinstance(a, torch.Tensor):
-        if a.is_cuda and a.dtype == torch.bfloat16 and a.shape == b.shape:
+        if a.is_cuda and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16 and a.shape == b.shape:
             from .. import ops
 
             return ops.add_gpu(a, b)
-        return a + b.to(a.dtype)
+        if a.dtype != b.dtype:  # mixed precision at a graph edge: accumulate in the wider type
+            wide = torch.promote_types(a.dtype, b.dtype)
+            return a.to(wide) + b.to(wide)
+        return a + b
     out = Table()
     for k in set(a.keys()) | set(b.keys()):
         out[k] = add_activity(a.get(k), b.get(k))

@@ -199,8 +199,12 @@ class SpatialConvolution(TensorModule):
             wt = cv.transpose_w(w16)
             Cp = w16.shape[1]
             xs = (x.shape[0], Cp, x.shape[2], x.shape[3])
+            addend = getattr(self, "_dgrad_addend", None)
+            self._dgrad_addend = None
+            if addend is not None and Cp != x.shape[1]:
+                raise RuntimeError("dgrad addend requires unpadded channels")
             gi = cv.conv2d_dgrad(gy16, wt, xs, (self.strideH, self.strideW), (ph, pw),
-                                 (self.dilationH, self.dilationW))
+                                 (self.dilationH, self.dilationW), addend=addend)
             if Cp != x.shape[1]:
                 gi = gi[:, : x.shape[1]].contiguous(memory_format=CL)
             return gi

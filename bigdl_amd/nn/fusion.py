@@ -93,10 +93,17 @@ def residual_backward(seq, x, gradOutput):
     branch, short, bn = seq._residual_plan
     dh, dres = bn.backward_fused(seq._res_h, gradOutput, need_dres=True)
     bn.gradInput = dh
-    g = dh
+    # shortcut first, so its gradient can be summed inside the epilogue of the branch's first dgrad GEMM
+    gs = short.backward(x, dres)
     mods = branch.modules
+    first = mods[0]
+    fold = (isinstance(first, SpatialConvolution) and first.propagateBack and first.nGroup == 1
+            and first.format == "NCHW" and first.nInputPlane % 8 == 0 and gs is not None
+            and gs.dtype == x.dtype and gs.shape == x.shape)
+    g = dh
     for i in range(len(mods) - 2, -1, -1):
         inp = mods[i - 1].output if i > 0 else x
+        if i == 0 and fold:
+            first._dgrad_addend = gs
         g = mods[i].backward(inp, g)
-    gs = short.backward(x, dres)
-    return add_activity(g, gs)
+    return g if fold else add_activity(g, gs)

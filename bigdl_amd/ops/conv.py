@@ -125,27 +125,37 @@ def dgrad_phases(H, W, R, S, stride, pad, dil):
     return res
 
 
-def conv2d_dgrad(dy, w16t, x_shape, stride, pad, dil=(1, 1), out=None):
-    """dx = conv_transpose(dy, w). ``w16t`` is the (C, R, S, K)-ordered transposed weight (see transpose_w).
+def conv2d_dgrad(dy, w16t, x_shape, stride, pad, dil=(1, 1), out=None, addend=None):
+    """dx = conv_transpose(dy, w) [+ addend]. ``w16t`` is the (C, R, S, K)-ordered transposed weight.
 
     Stride > 1 runs one dense implicit GEMM per stride phase (no zero-insertion, no masked MFMAs).
+    ``addend`` (same shape/layout as dx) is summed in the GEMM epilogue — used to fold the residual
+    branch gradient of a ResNet block into the block-input gradient.
     """
     N, C, H, W = x_shape
     _, K, OH, OW = dy.shape
     R, S = w16t.shape[1], w16t.shape[2]
     phases = dgrad_phases(H, W, R, S, stride, pad, dil)
     covered = sum(nI * nJ for (_, _, nI, nJ, _) in phases)
+    if addend is not None and not addend.is_contiguous(memory_format=CL):
+        addend = addend.contiguous(memory_format=CL)
     if out is None:
-        out = torch.empty((N, C, H, W), dtype=BF16, device=dy.device, memory_format=CL)
-        if covered != H * W:
-            out.zero_()
+        if covered != H * W and addend is not None:
+            out = addend.clone(memory_format=CL)
+        else:
+            out = torch.empty((N, C, H, W), dtype=BF16, device=dy.device, memory_format=CL)
+            if covered != H * W:
+                out.zero_()
     elif covered != H * W:
-        out.zero_()
+        if addend is not None:
+            out.copy_(addend)
+        else:
+            out.zero_()
     C_ = native.get()
     ldw = R * S * K
     for (a, b, nI, nJ, taps) in phases:
         geo = [N, OH, OW, K, nI, nJ, 1, 1, ldw, C, C, H, W, stride[0], stride[1], a, b]
-        C_.conv_nt(dy, w16t, out, None, None, geo, taps, False)
+        C_.conv_nt(dy, w16t, out, None, None, geo, taps, False, addend)
     return out
 
 

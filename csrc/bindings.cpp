@@ -32,7 +32,7 @@ float* omf(const OptT& t, const char* n) { return (t && t->defined()) ? mf(*t, n
 // geo = [Nb, Hs, Ws, Cs, OH, OW, mul_h, mul_w, ldw, Ncol, ldo, OHo, OWo, omul_h, omul_w, ooff_h, ooff_w]
 // taps = flat [tap_h0, tap_w0, tap_k0, tap_h1, ...]
 void conv_nt(const Tensor& src, const Tensor& wt, const Tensor& out, const OptT& bias, const OptT& stats,
-             std::vector<int64_t> geo, std::vector<int64_t> taps, bool relu) {
+             std::vector<int64_t> geo, std::vector<int64_t> taps, bool relu, const OptT& addend) {
   TORCH_CHECK(geo.size() == 17, "conv_nt: bad geometry");
   if (stats && stats->defined())
     TORCH_CHECK(stats->numel() >= BIGDL_STAT_SLOTS * 2 * geo[9], "conv_nt: stats must hold STAT_SLOTS x 2Ncol");
@@ -40,6 +40,8 @@ void conv_nt(const Tensor& src, const Tensor& wt, const Tensor& out, const OptT&
   ConvArgs a;
   a.src = cbf(src, "src"); a.wt = cbf(wt, "wt"); a.out = mbf(out, "out");
   a.bias = ocf(bias, "bias"); a.stats = omf(stats, "stats");
+  a.addend = ocbf(addend, "addend");
+  if (a.addend) TORCH_CHECK(addend->numel() == out.numel(), "conv_nt: addend must match out");
   a.Nb = geo[0]; a.Hs = geo[1]; a.Ws = geo[2]; a.Cs = geo[3]; a.OH = geo[4]; a.OW = geo[5];
   a.mul_h = geo[6]; a.mul_w = geo[7]; a.ldw = geo[8]; a.Ncol = geo[9]; a.ldo = geo[10];
   a.OHo = geo[11]; a.OWo = geo[12]; a.omul_h = geo[13]; a.omul_w = geo[14]; a.ooff_h = geo[15]; a.ooff_w = geo[16];
@@ -232,7 +234,8 @@ void lstm_cell_bwd(const Tensor& act, const OptT& c_prev, const Tensor& c, const
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "bigdl_amd native HIP kernels for gfx950 (MI355X)";
-  m.def("conv_nt", &conv_nt);
+  m.def("conv_nt", &conv_nt, py::arg("src"), py::arg("wt"), py::arg("out"), py::arg("bias"), py::arg("stats"),
+        py::arg("geo"), py::arg("taps"), py::arg("relu"), py::arg("addend") = py::none());
   m.def("conv_wgrad", &conv_wgrad);
   m.def("transpose_krsc", &transpose_krsc);
   m.def("bn_stats", &bn_stats);

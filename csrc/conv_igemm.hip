@@ -174,10 +174,21 @@ __global__ __launch_bounds__(256, 2) void conv_nt_kernel(ConvArgs a) {
         const int oh = rem / a.OW, ow = rem - oh * a.OW;
         orow = ((long)nb * a.OHo + oh * a.omul_h + a.ooff_h) * a.OWo + ow * a.omul_w + a.ooff_w;
       }
+      float ad[4] = {0.f, 0.f, 0.f, 0.f};
+      if (a.addend && m < a.M) {  // fused residual-gradient sum (ResNet block input gradient)
+        const bf16_t* ap = a.addend + (size_t)orow * a.ldo + nb;
+        if (vec_ok && nb + 3 < a.Ncol) {
+          const v2u q = *reinterpret_cast<const v2u*>(ap);
+          ad[0] = lo_bf(q[0]); ad[1] = hi_bf(q[0]); ad[2] = lo_bf(q[1]); ad[3] = hi_bf(q[1]);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) ad[e] = (nb + e < a.Ncol) ? bf2f(ap[e]) : 0.f;
+        }
+      }
       float v[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        float t = acc[i][j][e] + bs[e];
+        float t = acc[i][j][e] + bs[e] + ad[e];
         if (a.relu) t = fmaxf(t, 0.f);
         v[e] = t;
       }

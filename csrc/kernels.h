@@ -16,6 +16,7 @@ struct ConvArgs {
   uint16_t* out;
   const float* bias;
   float* stats;
+  const uint16_t* addend;   // optional [rows][ldo] bf16 added in the epilogue (same placement as out)
   int Nb, Hs, Ws, Cs;
   int OH, OW;
   int mul_h, mul_w;
