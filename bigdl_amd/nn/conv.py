@@ -140,7 +140,7 @@ class SpatialConvolution(TensorModule):
         self._x16 = x16
         w16 = self._w16_padded()
         stats = None
-        if self.emit_stats and self.train:
+        if self.emit_stats and self.train and self.nOutputPlane % 8 == 0:
             stats = bnops.new_stats(self.nOutputPlane, x.device)
         y = cv.conv2d_fwd(x16, w16, self.bias, (self.strideH, self.strideW), (ph, pw),
                           (self.dilationH, self.dilationW), relu=self.fuse_relu, stats=stats)
@@ -196,6 +196,9 @@ class SpatialConvolution(TensorModule):
         gy16 = gy if (gy.dtype == BF16 and gy.is_contiguous(memory_format=CL)) else gy.to(BF16, memory_format=CL)
         if self.nGroup == 1:
             w16 = self._w16_padded()
+            if gy16.shape[1] % 8:   # output channels not a multiple of 8: zero-pad K for the GEMM
+                gy16 = cv.pad_dim(gy16, 1)
+                w16 = cv.pad_dim(w16, 0)
             wt = cv.transpose_w(w16)
             Cp = w16.shape[1]
             xs = (x.shape[0], Cp, x.shape[2], x.shape[3])
@@ -212,8 +215,8 @@ class SpatialConvolution(TensorModule):
         cin, cout = self.nInputPlane // G, self.nOutputPlane // G
         parts = []
         for g in range(G):
-            wg = cv.weight_krsc_bf16(self.weight[g * cout:(g + 1) * cout])
-            gyg = gy16[:, g * cout:(g + 1) * cout].contiguous(memory_format=CL)
+            wg = cv.pad_dim(cv.weight_krsc_bf16(self.weight[g * cout:(g + 1) * cout]), 0)
+            gyg = cv.pad_dim(gy16[:, g * cout:(g + 1) * cout].contiguous(memory_format=CL), 1)
             xs = (x.shape[0], wg.shape[1], x.shape[2], x.shape[3])
             gi = cv.conv2d_dgrad(gyg, cv.transpose_w(wg), xs, (self.strideH, self.strideW), (ph, pw),
                                  (self.dilationH, self.dilationW))
@@ -248,27 +251,29 @@ class SpatialConvolution(TensorModule):
             cin, cout = self.nInputPlane // G, self.nOutputPlane // G
             for g in range(G):
                 xg = cv.to_nhwc_bf16(x[:, g * cin:(g + 1) * cin].contiguous(memory_format=CL))
-                gyg = gy16[:, g * cout:(g + 1) * cout].contiguous(memory_format=CL)
-                dw = torch.zeros(cout, xg.shape[1], self.kernelH, self.kernelW, device=x.device).contiguous(
+                gyg = cv.pad_dim(gy16[:, g * cout:(g + 1) * cout].contiguous(memory_format=CL), 1)
+                dw = torch.zeros(gyg.shape[1], xg.shape[1], self.kernelH, self.kernelW, device=x.device).contiguous(
                     memory_format=CL)
-                db = torch.zeros(cout, device=x.device) if self.bias is not None else None
+                db = torch.zeros(gyg.shape[1], device=x.device) if self.bias is not None else None
                 cv.conv2d_wgrad(gyg, xg, dw, db, st, pd, dl)
-                self.gradWeight[g * cout:(g + 1) * cout].add_(dw[:, :cin], alpha=self.scaleW)
+                self.gradWeight[g * cout:(g + 1) * cout].add_(dw[:cout, :cin], alpha=self.scaleW)
                 if db is not None:
-                    self.gradBias[g * cout:(g + 1) * cout].add_(db, alpha=self.scaleB)
+                    self.gradBias[g * cout:(g + 1) * cout].add_(db[:cout], alpha=self.scaleB)
             return
-        direct = (x16.shape[1] == self.nInputPlane and self.scaleW == 1.0 and self.scaleB == 1.0
+        K = self.nOutputPlane
+        direct = (x16.shape[1] == self.nInputPlane and K % 8 == 0 and self.scaleW == 1.0 and self.scaleB == 1.0
                   and self.gradWeight.is_contiguous(memory_format=CL))
         if direct:
             cv.conv2d_wgrad(gy16, x16, self.gradWeight, self.gradBias, st, pd, dl)
         else:
-            dw = torch.zeros(self.nOutputPlane, x16.shape[1], self.kernelH, self.kernelW,
+            gyp = cv.pad_dim(gy16, 1)
+            dw = torch.zeros(gyp.shape[1], x16.shape[1], self.kernelH, self.kernelW,
                              device=x.device).contiguous(memory_format=CL)
-            db = torch.zeros(self.nOutputPlane, device=x.device) if self.bias is not None else None
-            cv.conv2d_wgrad(gy16, x16, dw, db, st, pd, dl)
-            self.gradWeight.add_(dw[:, : self.nInputPlane], alpha=self.scaleW)
+            db = torch.zeros(gyp.shape[1], device=x.device) if self.bias is not None else None
+            cv.conv2d_wgrad(gyp, x16, dw, db, st, pd, dl)
+            self.gradWeight.add_(dw[:K, : self.nInputPlane], alpha=self.scaleW)
             if db is not None:
-                self.gradBias.add_(db, alpha=self.scaleB)
+                self.gradBias.add_(db[:K], alpha=self.scaleB)
 
     def clearState(self):
         super().clearState()

@@ -73,7 +73,11 @@ class SpatialMaxPooling(TensorModule):
         if _gpu_ok(x):
             gi = P.maxpool_bwd_gpu(_prep(g), self._idx, x.shape, self.kH, self.kW, self.dH, self.dW, ph, pw)
         else:
-            gi = F.max_unpool2d(g, self._idx, (self.kH, self.kW), (self.dH, self.dW), (ph, pw), output_size=x.shape[2:])
+            # overlapping windows must SUM their gradients (max_unpool2d would overwrite): use autograd
+            xr = x.detach().float().requires_grad_(True)
+            with torch.enable_grad():
+                y = F.max_pool2d(xr, (self.kH, self.kW), (self.dH, self.dW), (ph, pw), ceil_mode=self.ceilMode)
+            gi = torch.autograd.grad(y, xr, g.float())[0].to(x.dtype)
         gi = gi.squeeze(0) if sq else gi
         return gi.permute(0, 2, 3, 1) if self.format == "NHWC" else gi
 

@@ -27,6 +27,8 @@ def relu_gpu(x, out=None):
 def relu_bwd_gpu(dy, y, out=None):
     if out is None:
         out = torch.empty_like(y)
+    if dy.dtype != BF16:
+        dy = dy.to(BF16)
     dy = dy.contiguous(memory_format=_fmt(y))
     native.get().relu_bwd(dy, y, out)
     return out

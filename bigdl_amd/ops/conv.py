@@ -53,6 +53,19 @@ def weight_krsc_bf16(w, cpad=8):
     return w.to(dtype=BF16, memory_format=CL)
 
 
+def pad_dim(t, dim, mult=8):
+    """Zero-pad dimension ``dim`` of a 4-D bf16 tensor to a multiple of ``mult`` (keeps channels_last)."""
+    n = t.shape[dim]
+    npad = -(-n // mult) * mult
+    if npad == n:
+        return t
+    shape = list(t.shape)
+    shape[dim] = npad
+    out = torch.zeros(shape, dtype=t.dtype, device=t.device).contiguous(memory_format=CL)
+    out.narrow(dim, 0, n).copy_(t)
+    return out
+
+
 def conv2d_fwd(x, w16, bias, stride, pad, dil=(1, 1), relu=False, stats=None, out=None):
     """y = conv(x, w) + bias (+ReLU); optionally accumulate per-channel (sum, sumsq) of y into ``stats``.
 

@@ -27,6 +27,13 @@ namespace {
 
 constexpr int BK = 64;          // K elements per LDS stage (8 granules of 16 B per row)
 
+// 16 zero bytes in global memory: out-of-range lanes (padding taps, tile tails) load from here instead of
+// branching around the load, which keeps the staging code branch-free (no exec-mask save/restore).
+__device__ __attribute__((aligned(64))) bf16_t g_zero_granule[32];
+__device__ __forceinline__ v4u load16(const bf16_t* p, bool ok) {
+  return *reinterpret_cast<const v4u*>(ok ? p : g_zero_granule);
+}
+
 template <int BM, int BN, int WM, bool FASTK>
 __global__ __launch_bounds__(256, 2) void conv_nt_kernel(ConvArgs a) {
   constexpr int WN = 4 / WM;
@@ -94,15 +101,11 @@ __global__ __launch_bounds__(256, 2) void conv_nt_kernel(ConvArgs a) {
     for (int i = 0; i < AROWS; ++i) {
       const int ch = a_h[i] + th, cw = a_w[i] + tw;
       const bool ok = kvalid && (unsigned)ch < (unsigned)a.Hs && (unsigned)cw < (unsigned)a.Ws;
-      v4u v = {0u, 0u, 0u, 0u};
-      if (ok) v = *reinterpret_cast<const v4u*>(a.src + ((size_t)(a_pix[i] + ch * a.Ws + cw) * a.Cs + c));
-      ra[i] = v;
+      ra[i] = load16(a.src + (unsigned)((a_pix[i] + ch * a.Ws + cw) * a.Cs + c), ok);
     }
 #pragma unroll
     for (int i = 0; i < BROWS; ++i) {
-      v4u v = {0u, 0u, 0u, 0u};
-      if (bvalid[i] && kvalid) v = *reinterpret_cast<const v4u*>(wrow[i] + wk);
-      rb[i] = v;
+      rb[i] = load16(wrow[i] + wk, bvalid[i] && kvalid);
     }
   };
   auto swz = [](int row, int g) { return row * BK + ((g ^ (row & 7)) << 3); };
@@ -270,42 +273,45 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(WgradArgs a) {
   if (kvalid) { r = kk / SC; int rem = kk - r * SC; s = rem / a.Cs; c = rem - s * a.Cs; }
   const int roff = r * a.dh - a.ph, soff = s * a.dwl - a.pw;
 
-  // per-row pixel coordinates, advanced incrementally by WBM each stage
-  int pnb[4], poh[4], pow_[4];
+  // Per-stage pixel table, built one stage ahead by wave 0 (one div/mod chain per pixel instead of per
+  // loader row): entry = {P = (nb*Hs + oh*sh - ph)*Ws + ow*sw - pw, packed (oh*sh - ph, ow*sw - pw)}.
+  __shared__ int2 tbl[2][WBM];
   const int ohw = a.OH * a.OW;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int m = mbeg + lrow + 16 * i;
-    pnb[i] = m / ohw; const int rem = m - pnb[i] * ohw;
-    poh[i] = rem / a.OW; pow_[i] = rem - poh[i] * a.OW;
-  }
+  const int rdh = r * a.dh, sdw = s * a.dwl;
+  const int tapoff = rdh * a.Ws + sdw;
+  auto build_table = [&](int mb, int slot) {
+    if (tid < WBM) {
+      const int m = mb + tid;
+      int2 e;
+      if (m < mend) {
+        const int nb = m / ohw, rem = m - nb * ohw;
+        const int oh = rem / a.OW, ow = rem - oh * a.OW;
+        const int hb = oh * a.sh - a.ph, wb = ow * a.sw - a.pw;
+        e.x = (nb * a.Hs + hb) * a.Ws + wb;
+        e.y = (hb << 16) | (wb & 0xffff);
+      } else {
+        e.x = 0;
+        e.y = (int)0x80008000;  // hb = wb = -32768: never in range
+      }
+      tbl[slot][tid] = e;
+    }
+  };
   v4u rdy[4], rx[4];
   float bsum[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) bsum[e] = 0.f;
   const bool do_bias = a.dbias != nullptr && tk == 0;
 
-  auto gload = [&](int mb) {
+  auto gload = [&](int mb, int slot) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int m = mb + lrow + 16 * i;
-      v4u vd = {0u, 0u, 0u, 0u}, vx = {0u, 0u, 0u, 0u};
-      if (m < mend) {
-        if (nvalid) vd = *reinterpret_cast<const v4u*>(a.dy + (size_t)m * a.ldy + nn);
-        const int ih = poh[i] * a.sh + roff, iw = pow_[i] * a.sw + soff;
-        if (kvalid && (unsigned)ih < (unsigned)a.Hs && (unsigned)iw < (unsigned)a.Ws)
-          vx = *reinterpret_cast<const v4u*>(
-              a.src + ((size_t)(pnb[i] * a.Hs + ih) * a.Ws + iw) * a.Cs + c);
-      }
-      rdy[i] = vd; rx[i] = vx;
-      // advance this row's pixel by WBM
-      pow_[i] += WBM;
-      if (pow_[i] >= a.OW) {
-        const int qw = pow_[i] / a.OW;
-        pow_[i] -= qw * a.OW;
-        poh[i] += qw;
-        if (poh[i] >= a.OH) { const int qh = poh[i] / a.OH; poh[i] -= qh * a.OH; pnb[i] += qh; }
-      }
+      const int row = lrow + 16 * i;
+      const int m = mb + row;
+      const int2 e = tbl[slot][row];
+      const int ih = (e.y >> 16) + rdh, iw = ((int)(short)(e.y & 0xffff)) + sdw;
+      rdy[i] = load16(a.dy + (unsigned)(m * a.ldy + nn), nvalid && m < mend);
+      rx[i] = load16(a.src + (unsigned)((e.x + tapoff) * a.Cs + c),
+                     kvalid && (unsigned)ih < (unsigned)a.Hs && (unsigned)iw < (unsigned)a.Ws);
     }
   };
   auto swrite = [&](int buf) {
@@ -333,13 +339,17 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(WgradArgs a) {
   // row q, columns 4p..4p+3 of a 4x16 block; lane i receives column i of the 4 rows.
   const int G = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
 
-  gload(mbeg);
+  build_table(mbeg, 0);
+  build_table(mbeg + WBM, 1);
+  __syncthreads();
+  gload(mbeg, 0);
   swrite(0);
   __syncthreads();
   int cur = 0;
   for (int mb = mbeg; mb < mend; mb += WBM) {
     const bool more = mb + WBM < mend;
-    if (more) gload(mb + WBM);
+    if (more) gload(mb + WBM, cur ^ 1);          // table of stage t+1 (built last iteration)
+    build_table(mb + 2 * WBM, cur);              // table of stage t+2 into the slot stage t used
     const bf16_t* D = lds + cur * STAGE;
     const bf16_t* X = D + WBM * WT;
 #pragma unroll
