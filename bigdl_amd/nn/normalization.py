@@ -116,7 +116,8 @@ class BatchNormalization(TensorModule):
             return self._from_nchw(y)
         xf = x.float()
         y, mean, invstd = bnops.bn_forward_cpu(xf, self.weight, self.bias, self.runningMean, self.runningVar, self.eps,
-                                               self.momentum, self.train)
+                                               self.momentum, self.train,
+                                               sync_fn=self.sync_fn if self.train else None)
         if residual is not None:
             y = y + residual.float()
         if self.fuse_relu:
@@ -166,7 +167,8 @@ class BatchNormalization(TensorModule):
         gy = self._to_nchw(gradOutput).float()
         if self.fuse_relu:
             gy = gy * (self._to_nchw(self.output) > 0)
-        return bnops.bn_backward_cpu(self._xin, gy, self.saveMean, self.saveStd, self.weight, self.train)
+        return bnops.bn_backward_cpu(self._xin, gy, self.saveMean, self.saveStd, self.weight, self.train,
+                                     sync_fn=self.sync_fn if self.train else None)
 
     def updateGradInput(self, input, gradOutput):
         x = self._to_nchw(input)

@@ -88,13 +88,20 @@ def bn_backward_gpu(dz, z, x, smean, sinv, gamma, dgamma, dbeta, training=True, 
 
 
 # ---------------------------------------------------------------- CPU reference
-def bn_forward_cpu(x, gamma, beta, rmean, rvar, eps, momentum, training):
+def bn_forward_cpu(x, gamma, beta, rmean, rvar, eps, momentum, training, sync_fn=None):
     dims = [0] + list(range(2, x.dim()))
     shape = [1, -1] + [1] * (x.dim() - 2)
     if training:
-        mean = x.mean(dim=dims)
-        var = x.var(dim=dims, unbiased=False)
         n = x.numel() // x.shape[1]
+        if sync_fn is not None:
+            buf = torch.cat([x.sum(dim=dims), (x * x).sum(dim=dims)]).double()
+            n = sync_fn(buf, n)
+            C = x.shape[1]
+            mean = (buf[:C] / n).float()
+            var = (buf[C:] / n - (buf[:C] / n) ** 2).clamp_min(0).float()
+        else:
+            mean = x.mean(dim=dims)
+            var = x.var(dim=dims, unbiased=False)
         if rmean is not None:
             unb = var * n / max(n - 1, 1)
             rmean.mul_(1 - momentum).add_(momentum * mean)
@@ -109,7 +116,7 @@ def bn_forward_cpu(x, gamma, beta, rmean, rvar, eps, momentum, training):
     return y, mean, invstd
 
 
-def bn_backward_cpu(x, gy, mean, invstd, gamma, training=True):
+def bn_backward_cpu(x, gy, mean, invstd, gamma, training=True, sync_fn=None):
     dims = [0] + list(range(2, x.dim()))
     shape = [1, -1] + [1] * (x.dim() - 2)
     xhat = (x - mean.view(shape)) * invstd.view(shape)
@@ -118,7 +125,13 @@ def bn_backward_cpu(x, gy, mean, invstd, gamma, training=True):
     dbeta = gy.sum(dim=dims)
     if training:
         n = x.numel() // x.shape[1]
-        gx = g * invstd.view(shape) * (gy - dbeta.view(shape) / n - xhat * dgamma.view(shape) / n)
+        sdg, sdb = dgamma, dbeta
+        if sync_fn is not None:
+            buf = torch.cat([dbeta, dgamma]).double()
+            n = sync_fn(buf, n)
+            C = x.shape[1]
+            sdb, sdg = buf[:C].float(), buf[C:].float()
+        gx = g * invstd.view(shape) * (gy - sdb.view(shape) / n - xhat * sdg.view(shape) / n)
     else:
         gx = g * invstd.view(shape) * gy
     return gx, dgamma, dbeta

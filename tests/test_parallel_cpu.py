@@ -1,0 +1,63 @@
+"""Distributed pieces on the CPU engine over gloo: synchronized BatchNorm (reference
+T/nn/SpatialBatchNormalizationSpec / S/utils/ParameterSynchronizer.scala) and the sharded AllReduceParameter."""
+import torch
+
+from bigdl_amd.utils.testing import run_distributed
+
+
+def _sync_bn_job(rank, world, x_full, gy_full):
+    from bigdl_amd import nn
+    from bigdl_amd.parallel.sync_bn import enable_sync_bn
+
+    bn = nn.SpatialBatchNormalization(3)
+    seq = nn.Sequential().add(bn)
+    assert enable_sync_bn(seq) == 1
+    n = x_full.shape[0] // world
+    x = x_full[rank * n:(rank + 1) * n]
+    gy = gy_full[rank * n:(rank + 1) * n]
+    y = seq.forward(x)
+    gx = seq.backward(x, gy)
+    return y, gx, bn.gradWeight.clone(), bn.gradBias.clone(), bn.runningMean.clone()
+
+
+def test_sync_bn_matches_global_batch():
+    from bigdl_amd import nn
+
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(8, 3, 4, 4, generator=g) * 2 + 1
+    gy = torch.randn(8, 3, 4, 4, generator=g)
+    res = run_distributed(_sync_bn_job, 2, (x, gy))
+    ref = nn.SpatialBatchNormalization(3)
+    y = ref.forward(x)
+    gx = ref.backward(x, gy)
+    ys = torch.cat([res[0][0], res[1][0]])
+    gxs = torch.cat([res[0][1], res[1][1]])
+    assert torch.allclose(ys, y, atol=1e-5)
+    assert torch.allclose(gxs, gx, atol=1e-5)
+    # parameter gradients are per-replica partial sums (the optimizer all-reduces them)
+    assert torch.allclose(res[0][2] + res[1][2], ref.gradWeight, atol=1e-4)
+    assert torch.allclose(res[0][3] + res[1][3], ref.gradBias, atol=1e-4)
+    assert torch.allclose(res[0][4], ref.runningMean, atol=1e-5)
+
+
+def _arp_job(rank, world):
+    from bigdl_amd.parallel.allreduce_parameter import AllReduceParameter
+
+    arp = AllReduceParameter(1000)
+    w = torch.full((arp.padded,), float(rank))
+    arp.init(w)
+    g = torch.arange(arp.padded, dtype=torch.float32) * (rank + 1)
+    shard = arp.reduce_scatter_gradients(g).clone()
+    w[arp.start:arp.end] += 10 * (rank + 1)
+    arp.all_gather_weights(w)
+    return w.clone(), shard, arp.padded, arp.shard
+
+
+def test_allreduce_parameter_shards():
+    res = run_distributed(_arp_job, 2)
+    padded, shard = res[0][2], res[0][3]
+    assert padded % 128 == 0 and padded >= 1000 and shard * 2 == padded
+    full = torch.arange(padded, dtype=torch.float32) * 1.5     # AVG of (1x, 2x)
+    assert torch.allclose(res[0][1], full[:shard]) and torch.allclose(res[1][1], full[shard:])
+    expect = torch.cat([torch.full((shard,), 10.0), torch.full((shard,), 20.0)])  # broadcast rank0 weights (0)
+    assert torch.equal(res[0][0], expect) and torch.equal(res[1][0], expect)
