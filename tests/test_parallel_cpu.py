@@ -5,11 +5,20 @@ import torch
 from bigdl_amd.utils.testing import run_distributed
 
 
+def _bn():
+    from bigdl_amd import nn
+
+    bn = nn.SpatialBatchNormalization(3)
+    bn.weight.copy_(torch.tensor([0.5, 1.0, 2.0]))
+    bn.bias.copy_(torch.tensor([0.1, -0.2, 0.3]))
+    return bn
+
+
 def _sync_bn_job(rank, world, x_full, gy_full):
     from bigdl_amd import nn
     from bigdl_amd.parallel.sync_bn import enable_sync_bn
 
-    bn = nn.SpatialBatchNormalization(3)
+    bn = _bn()
     seq = nn.Sequential().add(bn)
     assert enable_sync_bn(seq) == 1
     n = x_full.shape[0] // world
@@ -27,7 +36,7 @@ def test_sync_bn_matches_global_batch():
     x = torch.randn(8, 3, 4, 4, generator=g) * 2 + 1
     gy = torch.randn(8, 3, 4, 4, generator=g)
     res = run_distributed(_sync_bn_job, 2, (x, gy))
-    ref = nn.SpatialBatchNormalization(3)
+    ref = _bn()
     y = ref.forward(x)
     gx = ref.backward(x, gy)
     ys = torch.cat([res[0][0], res[1][0]])
