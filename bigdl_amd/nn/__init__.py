@@ -11,6 +11,7 @@ from .init_methods import *  # noqa: F401,F403
 from .linear import *  # noqa: F401,F403
 from .normalization import *  # noqa: F401,F403
 from .pooling import *  # noqa: F401,F403
+from .recurrent import *  # noqa: F401,F403
 from .shape_ops import *  # noqa: F401,F403
 from .table_ops import *  # noqa: F401,F403
 from ..optim.regularizer import L1L2Regularizer, L1Regularizer, L2Regularizer  # noqa: F401

@@ -1,0 +1,787 @@
+"""Recurrent layers: Cell, RnnCell, LSTM, LSTMPeephole, GRU, ConvLSTMPeephole(3D), MultiRNNCell, Recurrent,
+BiRecurrent, RecurrentDecoder, TimeDistributed.
+
+Reference: S/nn/Cell.scala:46 (hiddensShape, preTopology, T(input, hidden) protocol), S/nn/Recurrent.scala:47-330
+(preTopology hoisted out of the time loop and run once over [batch*time] rows, hidden state threaded through
+per-step cell clones, maskZero, get/setHiddenState), S/nn/LSTM.scala:46-176 (gate order i, g, f, o),
+S/nn/GRU.scala (r, z, n; h' = (1-z)*n + z*h), S/nn/RNN.scala:49 (RnnCell), S/nn/LSTMPeephole.scala (gate order
+i, f, g, o; peepholes on c_{t-1} for i/f and on c_t for o), S/nn/ConvLSTMPeephole.scala:53 and
+ConvLSTMPeephole3D.scala (conv gates, SAME padding for padding=-1), S/nn/MultiRNNCell.scala:36,
+S/nn/BiRecurrent.scala:41 (reverse-time twin + merge, default CAddTable), S/nn/RecurrentDecoder.scala:79 (output of
+step t is the input of step t+1), S/nn/TimeDistributed.scala.
+
+Execution model (MI355X): the reference clones the cell graph once per time step and runs every tiny op
+through the module machinery. Here the input projection (``preTopology``) is ONE large GEMM over all B*T rows
+(the MFMA Linear kernels on the GPU engine); the time loop is recorded once with torch autograd on fp32 leaves
+of the cell weights, so backward is a single reverse sweep. LSTM (tanh/sigmoid, p == 0) bypasses the generic
+loop entirely: a sequence-level autograd Function runs ``h @ U^T`` (library GEMM) + the fused HIP cell kernel
+(csrc/elementwise.hip lstm_fwd_kernel / lstm_bwd_kernel: all four gate nonlinearities, the cell update and
+the gradient of both in one pass) per step, and computes dU with ONE [4H, T*B] x [T*B, H] GEMM after the
+reverse sweep instead of T small ones.
+"""
+import torch
+import torch.nn.functional as F
+
+__all__ = ["Cell", "RnnCell", "LSTM", "LSTMPeephole", "GRU", "ConvLSTMPeephole", "ConvLSTMPeephole3D", "MultiRNNCell",
+           "Recurrent", "RecurrentDecoder", "BiRecurrent", "TimeDistributed"]
+
+from .. import ops
+from ..utils.table import Table
+from .abstractnn import AbstractModule
+from .activation import CMul, Sigmoid, Tanh
+from .containers import Container
+from .conv import SpatialConvolution, VolumetricConvolution, _same_pad
+from .linear import Linear
+
+
+# ---------------------------------------------------------------------------------------------- helpers
+def _param_modules(mods):
+    """Leaf modules that own parameters, in traversal order, without duplicates."""
+    out, seen = [], set()
+
+    def walk(m):
+        if id(m) in seen:
+            return
+        seen.add(id(m))
+        if m._params:
+            out.append(m)
+        for c in m.modules_list():
+            walk(c)
+
+    for m in mods:
+        if m is not None:
+            walk(m)
+    return out
+
+
+class _Leaves:
+    """Temporarily replace module weights by fp32 autograd leaves (the reference shares one weight set across
+    all time-step clones, Recurrent.scala:198 ``share``; autograd sums the per-step contributions)."""
+
+    def __init__(self, mods, requires_grad=True):
+        self.entries = [(m, w, g) for m in _param_modules(mods) for (w, g) in m._params
+                        if getattr(m, w, None) is not None]
+        self.requires_grad = requires_grad
+        self.leaves = []
+
+    def __enter__(self):
+        self.saved = [getattr(m, w) for m, w, _ in self.entries]
+        self.leaves = [t.detach().float().requires_grad_(self.requires_grad) for t in self.saved]
+        for (m, w, _), leaf in zip(self.entries, self.leaves):
+            object.__setattr__(m, w, leaf)
+        return self
+
+    def __exit__(self, *exc):
+        for (m, w, _), t in zip(self.entries, self.saved):
+            object.__setattr__(m, w, t)
+        return False
+
+    def accumulate(self, grads):
+        for (m, w, g), gr in zip(self.entries, grads):
+            if gr is None or m._frozen:
+                continue
+            gt = getattr(m, g)
+            gt.add_(gr.to(gt.dtype).reshape(gt.shape), alpha=m.scaleB if w == "bias" else m.scaleW)
+        for m in {id(m): m for m, _, _ in self.entries}.values():
+            if not m._frozen:
+                m._apply_regularizers()
+
+
+def _act(m):
+    """Differentiable functional form of an activation module."""
+    if m is None:
+        return None
+    if hasattr(m, "fn"):
+        return m.fn
+    name = type(m).__name__
+    if name == "ReLU":
+        return torch.relu
+    raise ValueError(f"unsupported cell activation {name}")
+
+
+def _is(m, cls):
+    return type(m) is cls
+
+
+def _hidden_to_activity(hid):
+    return hid[0] if len(hid) == 1 else Table(*hid)
+
+
+def _activity_to_hidden(a):
+    if isinstance(a, torch.Tensor):
+        return [a]
+    if isinstance(a, Table):
+        out = []
+        for i in range(1, len(a) + 1):
+            out.extend(_activity_to_hidden(a[i]))
+        return out
+    return list(a)
+
+
+def _copy_module_state(dst, src):
+    """Copy parameters and buffers positionally (used when deserializing a cell whose sub-structure is
+    rebuilt by its constructor)."""
+    for a, b in zip(_param_modules([dst]), _param_modules([src])):
+        for (w, _), (w2, _) in zip(a._params, b._params):
+            ta, tb = getattr(a, w, None), getattr(b, w2, None)
+            if ta is not None and tb is not None:
+                ta.data.copy_(tb.reshape(ta.shape))
+
+
+# ---------------------------------------------------------------------------------------------- cells
+class Cell(Container):
+    """Abstract recurrent cell: ``step(x_t, hidden) -> (output_t, new_hidden)``.
+
+    ``x_t`` is this step's slice of the preTopology output (or of the raw input when the cell has none).
+    Standalone use follows the reference protocol: ``forward(T(input, hidden)) -> T(output, hidden)`` where
+    ``hidden`` is a Tensor for one-state cells and a Table for LSTM-like cells.
+    """
+
+    def __init__(self, hiddensShape, regularizers=None):
+        super().__init__()
+        self.hiddensShape = list(hiddensShape)
+        self.preTopology = None
+        self.regularizers = regularizers
+
+    def _set_pre(self, m):
+        self.preTopology = m
+        if m is not None:
+            self.modules.insert(0, m)
+
+    def hiddenSizeOfPreTopo(self):
+        return self.hiddensShape[0]
+
+    def step_modules(self):
+        return [m for m in self.modules if m is not self.preTopology]
+
+    def init_hidden(self, B, x_t):
+        return [torch.zeros(B, h, device=x_t.device, dtype=torch.float32) for h in self.hiddensShape]
+
+    def pre_fn(self, x):
+        """Differentiable preTopology (used when the projection cannot be hoisted out of the time loop)."""
+        p = self.preTopology
+        if p is None:
+            return x
+        if isinstance(p, Linear):
+            return F.linear(x, p.weight, p.bias)
+        raise ValueError(f"unsupported preTopology {type(p).__name__}")
+
+    def step(self, x, hid):
+        raise NotImplementedError
+
+    def sequence(self, x2, hid, mask=None):
+        """Run ``step`` over the time dimension of x2 [B, T, ...]; returns (out [B, T, ...], last hidden)."""
+        outs = []
+        for t in range(x2.shape[1]):
+            o, nh = self.step(x2[:, t], hid)
+            if mask is not None:
+                m = mask[:, t]
+                nh = [torch.where(m.view((-1,) + (1,) * (a.dim() - 1)), a, b) for a, b in zip(nh, hid)]
+                o = o * m.view((-1,) + (1,) * (o.dim() - 1)).to(o.dtype)
+            outs.append(o)
+            hid = nh
+        return torch.stack(outs, 1), hid
+
+    # standalone cell (T(input, hidden) -> T(output, hidden))
+    def updateOutput(self, input):
+        x, h = input[1], input[2]
+        xl = x.detach().float().requires_grad_(True)
+        hl = [t.detach().float().requires_grad_(True) for t in _activity_to_hidden(h)]
+        with _Leaves(self.modules) as L, torch.enable_grad():
+            o, nh = self.step(self.pre_fn(xl), hl)
+        self._ag = (xl, hl, L, o, nh)
+        return Table(o.detach(), _hidden_to_activity([t.detach() for t in nh]))
+
+    def updateGradInput(self, input, gradOutput):
+        xl, hl, L, o, nh = self._ag
+        outs, gouts = [o], [gradOutput[1].float()]
+        gh = gradOutput[2] if len(gradOutput) >= 2 else None
+        if gh is not None:
+            for t, g in zip(nh, _activity_to_hidden(gh)):
+                outs.append(t)
+                gouts.append(g.float())
+        grads = torch.autograd.grad(outs, [xl] + hl + L.leaves, gouts, allow_unused=True, retain_graph=True)
+        gx = grads[0] if grads[0] is not None else torch.zeros_like(xl)
+        ghs = [g if g is not None else torch.zeros_like(t) for g, t in zip(grads[1:1 + len(hl)], hl)]
+        self._pending = grads[1 + len(hl):]
+        return Table(gx.to(input[1].dtype), _hidden_to_activity(ghs))
+
+    def accGradParameters(self, input, gradOutput):
+        pending = getattr(self, "_pending", None)
+        if pending is not None:
+            self._ag[2].accumulate(pending)
+            self._pending = None
+
+    def _set_children(self, children):
+        src = Container(*children)
+        _copy_module_state(self, src)
+
+
+class RnnCell(Cell):
+    """h_t = activation(W x_t + b + U h_{t-1} + b_U) (S/nn/RNN.scala:49)."""
+
+    def __init__(self, inputSize=4, hiddenSize=3, activation=None, isInputWithBias=True, isHiddenWithBias=True,
+                 wRegularizer=None, uRegularizer=None, bRegularizer=None):
+        super().__init__([hiddenSize], [wRegularizer, uRegularizer, bRegularizer])
+        self.inputSize, self.hiddenSize = inputSize, hiddenSize
+        self.activation = activation if activation is not None else Tanh()
+        self._set_pre(Linear(inputSize, hiddenSize, withBias=isInputWithBias, wRegularizer=wRegularizer,
+                             bRegularizer=bRegularizer))
+        self.h2h = Linear(hiddenSize, hiddenSize, withBias=isHiddenWithBias, wRegularizer=uRegularizer)
+        self.modules.append(self.h2h)
+
+    def step(self, x, hid):
+        h = _act(self.activation)(x + F.linear(hid[0], self.h2h.weight, self.h2h.bias))
+        return h, [h]
+
+
+class _LSTMSeq(torch.autograd.Function):
+    """Whole-sequence LSTM (gate order i, g, f, o) with the fused HIP cell kernels on the GPU engine."""
+
+    @staticmethod
+    def _cell_fwd(g, c_prev, c, h, act):
+        if g.is_cuda:
+            ops.native.get().lstm_cell_fwd(g, c_prev, c, h, act)
+            return
+        H = c.shape[1]
+        i, gg, f, o = (torch.sigmoid(g[:, :H]), torch.tanh(g[:, H:2 * H]), torch.sigmoid(g[:, 2 * H:3 * H]),
+                       torch.sigmoid(g[:, 3 * H:]))
+        c.copy_(f * c_prev + i * gg)
+        h.copy_(o * torch.tanh(c))
+        act.copy_(torch.cat([i, gg, f, o], 1))
+
+    @staticmethod
+    def _cell_bwd(act, c_prev, c, dh, dc_next, dg, dc_prev):
+        if act.is_cuda:
+            ops.native.get().lstm_cell_bwd(act, c_prev, c, dh, dc_next, dg, dc_prev)
+            return
+        H = c.shape[1]
+        i, gg, f, o = act[:, :H], act[:, H:2 * H], act[:, 2 * H:3 * H], act[:, 3 * H:]
+        tc = torch.tanh(c)
+        dc = dh * o * (1 - tc * tc) + dc_next
+        dg.copy_(torch.cat([dc * gg * i * (1 - i), dc * i * (1 - gg * gg), dc * c_prev * f * (1 - f),
+                            dh * tc * o * (1 - o)], 1))
+        dc_prev.copy_(dc * f)
+
+    @staticmethod
+    def forward(ctx, xg, h0, c0, U):
+        B, T, G = xg.shape
+        H = G // 4
+        hs = xg.new_empty(T, B, H)
+        cs = xg.new_empty(T, B, H)
+        acts = xg.new_empty(T, B, G)
+        Ut = U.t()
+        h, c = h0.contiguous(), c0.contiguous()
+        for t in range(T):
+            g = torch.addmm(xg[:, t], h, Ut)
+            _LSTMSeq._cell_fwd(g, c, cs[t], hs[t], acts[t])
+            h, c = hs[t], cs[t]
+        ctx.save_for_backward(h0, c0, U, hs, cs, acts)
+        return hs.transpose(0, 1).contiguous(), hs[-1].clone(), cs[-1].clone()
+
+    @staticmethod
+    def backward(ctx, dout, dhT, dcT):
+        h0, c0, U, hs, cs, acts = ctx.saved_tensors
+        T, B, H = hs.shape
+        dgs = acts.new_empty(T, B, 4 * H)
+        dh_next = dhT.contiguous() if dhT is not None else hs.new_zeros(B, H)
+        dc_next = dcT.contiguous() if dcT is not None else hs.new_zeros(B, H)
+        dc_prev = hs.new_empty(B, H)
+        c0 = c0.contiguous()
+        for t in range(T - 1, -1, -1):
+            dh = dh_next + dout[:, t] if dout is not None else dh_next
+            c_prev = cs[t - 1] if t > 0 else c0
+            _LSTMSeq._cell_bwd(acts[t], c_prev, cs[t], dh.contiguous(), dc_next, dgs[t], dc_prev)
+            dh_next = dgs[t] @ U
+            dc_next, dc_prev = dc_prev, dc_next
+        hprev = torch.cat([h0.unsqueeze(0), hs[:-1]], 0).reshape(T * B, H)
+        dU = dgs.reshape(T * B, 4 * H).t() @ hprev
+        return dgs.transpose(0, 1), dh_next, dc_next, dU
+
+
+class LSTM(Cell):
+    """Long short-term memory cell (S/nn/LSTM.scala:46). Hidden = T(h, c); gate order (i, g, f, o)."""
+
+    def __init__(self, inputSize, hiddenSize, p=0.0, activation=None, innerActivation=None, wRegularizer=None,
+                 uRegularizer=None, bRegularizer=None):
+        super().__init__([hiddenSize, hiddenSize], [wRegularizer, uRegularizer, bRegularizer])
+        self.inputSize, self.hiddenSize, self.p = inputSize, hiddenSize, p
+        self.activation = activation if activation is not None else Tanh()
+        self.innerActivation = innerActivation if innerActivation is not None else Sigmoid()
+        self._set_pre(Linear(inputSize, 4 * hiddenSize, wRegularizer=wRegularizer, bRegularizer=bRegularizer))
+        self.h2g = Linear(hiddenSize, 4 * hiddenSize, withBias=p != 0, wRegularizer=uRegularizer,
+                          bRegularizer=bRegularizer if p != 0 else None)
+        self.modules.append(self.h2g)
+
+    def hiddenSizeOfPreTopo(self):
+        return 4 * self.hiddenSize
+
+    def _fused_ok(self):
+        return self.p == 0 and _is(self.activation, Tanh) and _is(self.innerActivation, Sigmoid)
+
+    def _gate_inputs(self, x, h):
+        """p != 0: the reference uses four independent Dropout+Linear branches per gate (LSTM.scala:68-96);
+        here the recurrent input gets four independent dropout masks (one per gate block of U)."""
+        H = self.hiddenSize
+        if self.p != 0 and self.train:
+            keep = 1.0 - self.p
+            hm = torch.stack([torch.bernoulli(torch.full_like(h, keep)) / keep for _ in range(4)])
+            U = self.h2g.weight.view(4, H, H)
+            hg = torch.bmm(h.unsqueeze(0) * hm, U.transpose(1, 2)).permute(1, 0, 2).reshape(h.shape[0], 4 * H)
+            if self.h2g.bias is not None:
+                hg = hg + self.h2g.bias
+            return x + hg
+        return x + F.linear(h, self.h2g.weight, self.h2g.bias)
+
+    def step(self, x, hid):
+        h, c = hid
+        H = self.hiddenSize
+        g = self._gate_inputs(x, h)
+        sig, tanh = _act(self.innerActivation), _act(self.activation)
+        i, gg, f, o = sig(g[:, :H]), tanh(g[:, H:2 * H]), sig(g[:, 2 * H:3 * H]), sig(g[:, 3 * H:])
+        c2 = f * c + i * gg
+        h2 = o * tanh(c2)
+        return h2, [h2, c2]
+
+    def sequence(self, x2, hid, mask=None):
+        if mask is None and self._fused_ok():
+            out, h, c = _LSTMSeq.apply(x2.contiguous(), hid[0], hid[1], self.h2g.weight)
+            return out, [h, c]
+        return super().sequence(x2, hid, mask)
+
+
+class LSTMPeephole(Cell):
+    """LSTM with peephole connections (S/nn/LSTMPeephole.scala). preTopology order (i, f, g, o)."""
+
+    def __init__(self, inputSize, hiddenSize, p=0.0, wRegularizer=None, uRegularizer=None, bRegularizer=None):
+        super().__init__([hiddenSize, hiddenSize], [wRegularizer, uRegularizer, bRegularizer])
+        self.inputSize, self.hiddenSize, self.p = inputSize, hiddenSize, p
+        self._set_pre(Linear(inputSize, 4 * hiddenSize, wRegularizer=wRegularizer, bRegularizer=bRegularizer))
+        self.h2g = Linear(hiddenSize, 4 * hiddenSize, withBias=False, wRegularizer=uRegularizer)
+        self.peepI, self.peepF, self.peepO = CMul([hiddenSize]), CMul([hiddenSize]), CMul([hiddenSize])
+        self.modules += [self.h2g, self.peepI, self.peepF, self.peepO]
+
+    def hiddenSizeOfPreTopo(self):
+        return 4 * self.hiddenSize
+
+    def step(self, x, hid):
+        h, c = hid
+        H = self.hiddenSize
+        g = x + F.linear(h, self.h2g.weight)
+        i = torch.sigmoid(g[:, :H] + self.peepI.weight * c)
+        f = torch.sigmoid(g[:, H:2 * H] + self.peepF.weight * c)
+        gg = torch.tanh(g[:, 2 * H:3 * H])
+        c2 = f * c + i * gg
+        o = torch.sigmoid(g[:, 3 * H:] + self.peepO.weight * c2)
+        h2 = o * torch.tanh(c2)
+        return h2, [h2, c2]
+
+
+class GRU(Cell):
+    """Gated recurrent unit (S/nn/GRU.scala). preTopology order (r, z, n); h' = (1 - z) * n + z * h."""
+
+    def __init__(self, inputSize, outputSize, p=0.0, activation=None, innerActivation=None, wRegularizer=None,
+                 uRegularizer=None, bRegularizer=None):
+        super().__init__([outputSize], [wRegularizer, uRegularizer, bRegularizer])
+        self.inputSize, self.outputSize, self.p = inputSize, outputSize, p
+        self.activation = activation if activation is not None else Tanh()
+        self.innerActivation = innerActivation if innerActivation is not None else Sigmoid()
+        self._set_pre(Linear(inputSize, 3 * outputSize, wRegularizer=wRegularizer, bRegularizer=bRegularizer))
+        self.h2g = Linear(outputSize, 2 * outputSize, withBias=False, wRegularizer=uRegularizer)
+        self.h2n = Linear(outputSize, outputSize, withBias=False, wRegularizer=uRegularizer)
+        self.modules += [self.h2g, self.h2n]
+
+    def hiddenSizeOfPreTopo(self):
+        return 3 * self.outputSize
+
+    def _drop(self, t):
+        if self.p != 0 and self.train:
+            return F.dropout(t, self.p, True)
+        return t
+
+    def step(self, x, hid):
+        h = hid[0]
+        H = self.outputSize
+        sig, act = _act(self.innerActivation), _act(self.activation)
+        rz = sig(x[:, :2 * H] + F.linear(self._drop(h), self.h2g.weight))
+        r, z = rz[:, :H], rz[:, H:]
+        n = act(x[:, 2 * H:] + F.linear(self._drop(r * h), self.h2n.weight))
+        h2 = (1 - z) * n + z * h
+        return h2, [h2]
+
+
+class _ConvLSTMBase(Cell):
+    _nd = 2
+
+    def __init__(self, inputSize, outputSize, kernelI, kernelC, stride=1, padding=-1, activation=None,
+                 innerActivation=None, wRegularizer=None, uRegularizer=None, bRegularizer=None, cRegularizer=None,
+                 withPeephole=True):
+        super().__init__([outputSize, outputSize], [wRegularizer, uRegularizer, bRegularizer, cRegularizer])
+        self.inputSize, self.outputSize = inputSize, outputSize
+        self.kernelI, self.kernelC, self.stride, self.padding = kernelI, kernelC, stride, padding
+        self.withPeephole = withPeephole
+        self.activation = activation if activation is not None else Tanh()
+        self.innerActivation = innerActivation if innerActivation is not None else Sigmoid()
+        if self._nd == 2:
+            self.i2g = SpatialConvolution(inputSize, 4 * outputSize, kernelI, kernelI, stride, stride, padding,
+                                          padding, wRegularizer=wRegularizer, bRegularizer=bRegularizer)
+            self.h2g = SpatialConvolution(outputSize, 4 * outputSize, kernelC, kernelC, stride, stride, padding,
+                                          padding, withBias=False, wRegularizer=uRegularizer)
+        else:
+            self.i2g = VolumetricConvolution(inputSize, 4 * outputSize, kernelI, kernelI, kernelI, stride, stride,
+                                             stride, padding, padding, padding, wRegularizer=wRegularizer,
+                                             bRegularizer=bRegularizer)
+            self.h2g = VolumetricConvolution(outputSize, 4 * outputSize, kernelC, kernelC, kernelC, stride, stride,
+                                             stride, padding, padding, padding, withBias=False,
+                                             wRegularizer=uRegularizer)
+        self.modules += [self.i2g, self.h2g]
+        if withPeephole:
+            shape = [1, outputSize] + [1] * self._nd
+            self.peepI, self.peepF, self.peepO = (CMul(shape, cRegularizer), CMul(shape, cRegularizer),
+                                                  CMul(shape, cRegularizer))
+            self.modules += [self.peepI, self.peepF, self.peepO]
+
+    def _conv(self, x, conv, k):
+        fn = F.conv2d if self._nd == 2 else F.conv3d
+        w = conv.weight
+        if self.padding == -1:
+            pads = []
+            for d in range(self._nd - 1, -1, -1):
+                pads.extend(_same_pad(x.shape[2 + d], k, self.stride))
+            x = F.pad(x, pads)
+            pad = 0
+        else:
+            pad = self.padding
+        return fn(x, w, conv.bias, self.stride, pad)
+
+    def init_hidden(self, B, x_t):
+        spatial = []
+        for d in range(self._nd):
+            n = x_t.shape[2 + d]
+            if self.padding == -1:
+                spatial.append(-(-n // self.stride))
+            else:
+                spatial.append((n + 2 * self.padding - self.kernelI) // self.stride + 1)
+        return [torch.zeros(B, self.outputSize, *spatial, device=x_t.device, dtype=torch.float32)
+                for _ in range(2)]
+
+    def step(self, x, hid):
+        h, c = hid
+        C = self.outputSize
+        g = self._conv(x, self.i2g, self.kernelI) + self._conv(h, self.h2g, self.kernelC)
+        sig, act = _act(self.innerActivation), _act(self.activation)
+        gi, gf, gh, go = g[:, :C], g[:, C:2 * C], g[:, 2 * C:3 * C], g[:, 3 * C:]
+        if self.withPeephole:
+            gi = gi + self.peepI.weight * c
+            gf = gf + self.peepF.weight * c
+        c2 = sig(gf) * c + sig(gi) * act(gh)
+        if self.withPeephole:
+            go = go + self.peepO.weight * c2
+        h2 = sig(go) * act(c2)
+        return h2, [h2, c2]
+
+
+class ConvLSTMPeephole(_ConvLSTMBase):
+    """Convolutional LSTM with peepholes over [B, T, C, H, W] (S/nn/ConvLSTMPeephole.scala:53)."""
+    _nd = 2
+
+
+class ConvLSTMPeephole3D(_ConvLSTMBase):
+    """Volumetric convolutional LSTM over [B, T, C, D, H, W] (S/nn/ConvLSTMPeephole3D.scala)."""
+    _nd = 3
+
+
+class MultiRNNCell(Cell):
+    """Stack of cells applied within one time step (S/nn/MultiRNNCell.scala:36). Hidden = concatenation of
+    the cells' hidden states (a Table of Tables through get/setHiddenState)."""
+
+    def __init__(self, cells):
+        cells = list(cells)
+        super().__init__(sum((c.hiddensShape for c in cells), []))
+        self.cells = cells
+        self.modules = list(cells)
+
+    def hiddenSizeOfPreTopo(self):
+        return self.cells[0].inputSize if hasattr(self.cells[0], "inputSize") else None
+
+    def init_hidden(self, B, x_t):
+        out = []
+        x = x_t
+        for c in self.cells:
+            hs = c.init_hidden(B, x)
+            out.extend(hs)
+            x = hs[0]
+        return out
+
+    def step(self, x, hid):
+        new, off = [], 0
+        for c in self.cells:
+            n = len(c.hiddensShape)
+            o, nh = c.step(c.pre_fn(x), hid[off:off + n])
+            new.extend(nh)
+            off += n
+            x = o
+        return x, new
+
+    def _set_children(self, children):
+        _copy_module_state(self, Container(*children))
+
+
+# ---------------------------------------------------------------------------------------------- drivers
+class Recurrent(Container):
+    """Runs a Cell over [batch, time, ...] input (S/nn/Recurrent.scala:47). Output [batch, time, hidden...]."""
+
+    def __init__(self, batchNormParams=None, maskZero=False):
+        super().__init__()
+        self.batchNormParams = batchNormParams
+        self.maskZero = maskZero
+        self.cell = None
+        self.bn = None
+        self._init_hidden = None
+        self._last_hidden = None
+
+    def add(self, cell):
+        assert isinstance(cell, Cell), "Recurrent.add expects a Cell"
+        self.cell = cell
+        self.modules = [cell]
+        if self.batchNormParams is not None:
+            if cell.preTopology is None:
+                raise ValueError("batchNormParams need a cell with a preTopology")
+            from .normalization import BatchNormalization
+
+            bp = self.batchNormParams
+            self.bn = BatchNormalization(cell.hiddenSizeOfPreTopo(), **(bp if isinstance(bp, dict) else {}))
+            self.modules.append(self.bn)
+        return self
+
+    def getCell(self):
+        return self.cell
+
+    def _set_children(self, children):
+        self.add(children[0])
+        if self.bn is not None and len(children) > 1:
+            self.bn = children[1]
+            self.modules[1] = children[1]
+
+    def getHiddenState(self):
+        if self._last_hidden is None:
+            raise RuntimeError("getHiddenState need to be called after updateOutput")
+        return _hidden_to_activity(self._last_hidden)
+
+    def setHiddenState(self, hiddenState):
+        self._init_hidden = None if hiddenState is None else _activity_to_hidden(hiddenState)
+
+    def _project(self, input):
+        cell = self.cell
+        B, T = input.shape[:2]
+        if cell.preTopology is None:
+            return input, None
+        flat = input.reshape((B * T,) + tuple(input.shape[2:]))
+        x2 = cell.preTopology.forward(flat)
+        if self.bn is not None:
+            x2 = self.bn.forward(x2)
+        return x2.reshape((B, T) + tuple(x2.shape[1:])), flat
+
+    def updateOutput(self, input):
+        assert input.dim() in (3, 5, 6), "Recurrent: input should be [batch, times, ...]"
+        B = input.shape[0]
+        x2, self._flat = self._project(input)
+        need_grad = self.train
+        x2l = x2.detach().float().requires_grad_(need_grad)
+        h0 = self._init_hidden if self._init_hidden is not None else self.cell.init_hidden(B, x2l[:, 0])
+        h0l = [h.detach().float().to(x2l.device).requires_grad_(need_grad) for h in h0]
+        mask = None
+        if self.maskZero:
+            mask = input.reshape(B, input.shape[1], -1).abs().amax(-1) != 0
+        with _Leaves(self.cell.step_modules(), need_grad) as L, torch.set_grad_enabled(need_grad):
+            out, hid = self.cell.sequence(x2l, h0l, mask)
+        self._ag = (x2l, h0l, L, out, hid) if need_grad else None
+        self._last_hidden = [t.detach() for t in hid]
+        return out.detach()
+
+    def updateGradInput(self, input, gradOutput):
+        if self._ag is None:
+            raise RuntimeError("Recurrent: backward called without a training forward")
+        x2l, h0l, L, out, hid = self._ag
+        targets = [x2l] + L.leaves + h0l
+        grads = torch.autograd.grad([out], targets, [gradOutput.float()], allow_unused=True, retain_graph=True)
+        gx2 = grads[0] if grads[0] is not None else torch.zeros_like(x2l)
+        n = len(L.leaves)
+        self._pending = grads[1:1 + n]
+        self.gradHiddenState = [g for g in grads[1 + n:]]
+        pre = self.cell.preTopology
+        if pre is None:
+            return gx2.to(input.dtype)
+        B, T = input.shape[:2]
+        g = gx2.reshape((B * T,) + tuple(gx2.shape[2:]))
+        if self.bn is not None:
+            self._gbn = g
+            g = self.bn.updateGradInput(pre.output, g)
+        self._gpre = g
+        gi = pre.updateGradInput(self._flat, g)
+        return gi.reshape(input.shape).to(input.dtype)
+
+    def accGradParameters(self, input, gradOutput):
+        if getattr(self, "_pending", None) is not None:
+            self._ag[2].accumulate(self._pending)
+            self._pending = None
+        pre = self.cell.preTopology
+        if pre is not None and not pre._frozen:
+            if self.bn is not None and not self.bn._frozen:
+                self.bn.accGradParameters(pre.output, self._gbn)
+                self.bn._apply_regularizers()
+            pre.accGradParameters(self._flat, self._gpre)
+            pre._apply_regularizers()
+
+    def backward(self, input, gradOutput):
+        self.gradInput = self.updateGradInput(input, gradOutput)
+        if not self._frozen:
+            self.accGradParameters(input, gradOutput)
+        return self.gradInput
+
+    def clearState(self):
+        super().clearState()
+        self._ag = None
+        return self
+
+
+class RecurrentDecoder(Recurrent):
+    """Feeds the output of step t as the input of step t+1 for ``outputLength`` steps
+    (S/nn/RecurrentDecoder.scala:79). Input [batch, hidden...]; output [batch, outputLength, hidden...]."""
+
+    def __init__(self, outputLength):
+        super().__init__()
+        self.outputLength = outputLength
+
+    def updateOutput(self, input):
+        B = input.shape[0]
+        cell = self.cell
+        need_grad = self.train
+        xl = input.detach().float().requires_grad_(need_grad)
+        with _Leaves(cell.modules, need_grad) as L, torch.set_grad_enabled(need_grad):
+            x = xl
+            hid = self._init_hidden if self._init_hidden is not None else cell.init_hidden(B, cell.pre_fn(x))
+            hid = [h.detach().float().to(xl.device).requires_grad_(need_grad) for h in hid]
+            h0l = hid
+            outs = []
+            for _ in range(self.outputLength):
+                o, hid = cell.step(cell.pre_fn(x), hid)
+                outs.append(o)
+                x = o
+            out = torch.stack(outs, 1)
+        self._ag = (xl, h0l, L, out, hid) if need_grad else None
+        self._last_hidden = [t.detach() for t in hid]
+        return out.detach()
+
+    def updateGradInput(self, input, gradOutput):
+        xl, h0l, L, out, hid = self._ag
+        grads = torch.autograd.grad([out], [xl] + L.leaves + h0l, [gradOutput.float()], allow_unused=True,
+                                    retain_graph=True)
+        n = len(L.leaves)
+        self._pending = grads[1:1 + n]
+        self.gradHiddenState = list(grads[1 + n:])
+        gx = grads[0] if grads[0] is not None else torch.zeros_like(xl)
+        return gx.to(input.dtype)
+
+    def accGradParameters(self, input, gradOutput):
+        if getattr(self, "_pending", None) is not None:
+            self._ag[2].accumulate(self._pending)
+            self._pending = None
+
+
+class BiRecurrent(Container):
+    """Forward and time-reversed Recurrent over the same (or split) input, merged (S/nn/BiRecurrent.scala:41)."""
+
+    def __init__(self, merge=None, batchNormParams=None, isSplitInput=False):
+        super().__init__()
+        from .table_ops import CAddTable
+
+        self.isSplitInput = isSplitInput
+        self.batchNormParams = batchNormParams
+        self.layer = Recurrent(batchNormParams)
+        self.revLayer = Recurrent(batchNormParams)
+        self.merge = merge if merge is not None else CAddTable(True)
+        self.modules = [self.layer, self.revLayer, self.merge]
+
+    def add(self, cell):
+        self.layer.add(cell)
+        self.revLayer.add(cell.cloneModule())
+        return self
+
+    def getMerge(self):
+        return self.merge
+
+    def _set_children(self, children):
+        self.layer, self.revLayer, self.merge = children
+        self.modules = list(children)
+
+    def _split(self, x):
+        if not self.isSplitInput:
+            return x, x
+        d = x.shape[2] // 2
+        return x[:, :, :d], x[:, :, d:]
+
+    def updateOutput(self, input):
+        a, b = self._split(input)
+        self._ins = (a, b.flip(1))
+        o1 = self.layer.forward(self._ins[0])
+        o2 = self.revLayer.forward(self._ins[1]).flip(1)
+        return self.merge.forward(Table(o1, o2))
+
+    def updateGradInput(self, input, gradOutput):
+        o1 = self.layer.output
+        o2 = self.revLayer.output.flip(1)
+        gm = self.merge.backward(Table(o1, o2), gradOutput)
+        g1 = self.layer.backward(self._ins[0], gm[1])
+        g2 = self.revLayer.backward(self._ins[1], gm[2].flip(1).contiguous()).flip(1)
+        if self.isSplitInput:
+            return torch.cat([g1, g2], 2)
+        return g1 + g2
+
+    def backward(self, input, gradOutput):
+        self.gradInput = self.updateGradInput(input, gradOutput)
+        return self.gradInput
+
+    def accGradParameters(self, input, gradOutput):
+        pass
+
+
+class TimeDistributed(Container):
+    """Applies ``layer`` to every time step by folding time into batch (S/nn/TimeDistributed.scala)."""
+
+    def __init__(self, layer, maskZero=False):
+        super().__init__(layer)
+        self.layer = layer
+        self.maskZero = maskZero
+
+    def _fold(self, x):
+        return x.reshape((x.shape[0] * x.shape[1],) + tuple(x.shape[2:]))
+
+    def updateOutput(self, input):
+        B, T = input.shape[:2]
+        y = self.layer.forward(self._fold(input))
+        y = y.reshape((B, T) + tuple(y.shape[1:]))
+        if self.maskZero:
+            m = input.reshape(B, T, -1).abs().amax(-1) != 0
+            y = y * m.view(B, T, *([1] * (y.dim() - 2))).to(y.dtype)
+        return y
+
+    def _gfold(self, input, gradOutput):
+        g = gradOutput
+        if self.maskZero:
+            B, T = input.shape[:2]
+            m = input.reshape(B, T, -1).abs().amax(-1) != 0
+            g = g * m.view(B, T, *([1] * (g.dim() - 2))).to(g.dtype)
+        return self._fold(g)
+
+    def updateGradInput(self, input, gradOutput):
+        gi = self.layer.updateGradInput(self._fold(input), self._gfold(input, gradOutput))
+        return gi.reshape(input.shape)
+
+    def accGradParameters(self, input, gradOutput):
+        self.layer.accGradParameters(self._fold(input), self._gfold(input, gradOutput))
+
+    def backward(self, input, gradOutput):
+        gi = self.layer.backward(self._fold(input), self._gfold(input, gradOutput))
+        self.gradInput = gi.reshape(input.shape)
+        return self.gradInput

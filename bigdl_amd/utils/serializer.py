@@ -108,8 +108,7 @@ def _init_has_modules(m):
 
     args, kw = getattr(m, "_init_args", ((), {}))
     return any(isinstance(a, AbstractModule) for a in list(args) + list(kw.values())) and \
-        type(m).__name__ in ("Bottle", "MapTable", "TimeDistributed", "Recurrent", "BiRecurrent",
-                             "RecurrentDecoder")
+        type(m).__name__ in ("Bottle", "MapTable", "TimeDistributed")
 
 
 def _dec(v, tensors):
@@ -173,9 +172,13 @@ def decode_module(d, tensors):
         kw = {k: _dec(x, tensors) for k, x in d["init"]["kw"].items()}
         m = cls(*args, **kw)
         if "children" in d:
-            m.modules = []
-            for c in d["children"]:
-                m.add(decode_module(c, tensors))
+            children = [decode_module(c, tensors) for c in d["children"]]
+            if hasattr(m, "_set_children"):   # modules whose constructor builds their own sub-structure
+                m._set_children(children)
+            else:
+                m.modules = []
+                for c in children:
+                    m.add(c)
     for k, v in d.get("attrs", {}).items():
         try:
             setattr(m, k, tuple(v) if isinstance(getattr(m, k, None), tuple) else v)

@@ -1,0 +1,187 @@
+"""Recurrent family on the CPU engine (reference T/nn/LSTMSpec, GRUSpec, RecurrentSpec, BiRecurrentSpec,
+ConvLSTMPeepholeSpec, RecurrentDecoderSpec, TimeDistributedSpec, MultiRNNCellSpec).
+
+Oracles: torch.nn.LSTM with permuted gate blocks (BigDL order i, g, f, o vs torch i, f, g, o), hand-written
+per-step loops for GRU (BigDL applies U_n to r*h, unlike cuDNN-style GRU), and finite differences."""
+import pytest
+import torch
+
+from bigdl_amd import nn
+from bigdl_amd.utils.gradient_checker import GradientChecker
+from bigdl_amd.utils.random_generator import RNG
+from bigdl_amd.utils.table import T
+
+
+def _torch_lstm_from(cell):
+    H = cell.hiddenSize
+    ref = torch.nn.LSTM(cell.inputSize, H, batch_first=True)
+    perm = torch.cat([torch.arange(0, H), torch.arange(2 * H, 3 * H), torch.arange(H, 2 * H),
+                      torch.arange(3 * H, 4 * H)])
+    with torch.no_grad():
+        ref.weight_ih_l0.copy_(cell.preTopology.weight[perm])
+        ref.bias_ih_l0.copy_(cell.preTopology.bias[perm])
+        ref.weight_hh_l0.copy_(cell.h2g.weight[perm])
+        ref.bias_hh_l0.zero_()
+    return ref, perm
+
+
+def test_lstm_matches_torch_lstm_fwd_bwd():
+    RNG.setSeed(1)
+    cell = nn.LSTM(6, 5)
+    rec = nn.Recurrent().add(cell)
+    ref, perm = _torch_lstm_from(cell)
+    x = torch.randn(3, 7, 6)
+    y = rec.forward(x)
+    xr = x.clone().requires_grad_()
+    yr, (hr, cr) = ref(xr)
+    assert torch.allclose(y, yr, atol=1e-5)
+    h = rec.getHiddenState()
+    assert torch.allclose(h[1], hr[0], atol=1e-5) and torch.allclose(h[2], cr[0], atol=1e-5)
+    gy = torch.randn_like(y)
+    rec.zeroGradParameters()
+    gx = rec.backward(x, gy)
+    yr.backward(gy)
+    assert torch.allclose(gx, xr.grad, atol=1e-5)
+    assert torch.allclose(cell.h2g.gradWeight[perm], ref.weight_hh_l0.grad, atol=1e-4)
+    assert torch.allclose(cell.preTopology.gradWeight[perm], ref.weight_ih_l0.grad, atol=1e-4)
+    assert torch.allclose(cell.preTopology.gradBias[perm], ref.bias_ih_l0.grad, atol=1e-4)
+
+
+def test_lstm_fused_sequence_equals_generic_steps():
+    RNG.setSeed(2)
+    cell = nn.LSTM(4, 6)
+    x2 = torch.randn(2, 5, 24, requires_grad=True)
+    h0 = [torch.randn(2, 6, requires_grad=True), torch.randn(2, 6, requires_grad=True)]
+    U = cell.h2g.weight.detach().clone().requires_grad_()
+    cell.h2g.weight = U
+    o1, hid1 = cell.sequence(x2, h0)
+    o2, hid2 = nn.Cell.sequence(cell, x2, h0)
+    assert torch.allclose(o1, o2, atol=1e-6)
+    g = torch.randn_like(o1)
+    ga = torch.autograd.grad([o1, hid1[1]], [x2, U] + h0, [g, torch.ones_like(hid1[1])])
+    gb = torch.autograd.grad([o2, hid2[1]], [x2, U] + h0, [g, torch.ones_like(hid2[1])])
+    for a, b in zip(ga, gb):
+        assert torch.allclose(a, b, atol=1e-5)
+
+
+def _gru_reference(cell, x):
+    H = cell.outputSize
+    W, b = cell.preTopology.weight, cell.preTopology.bias
+    Urz, Un = cell.h2g.weight, cell.h2n.weight
+    h = torch.zeros(x.shape[0], H)
+    outs = []
+    for t in range(x.shape[1]):
+        xt = x[:, t] @ W.t() + b
+        rz = torch.sigmoid(xt[:, :2 * H] + h @ Urz.t())
+        r, z = rz[:, :H], rz[:, H:]
+        n = torch.tanh(xt[:, 2 * H:] + (r * h) @ Un.t())
+        h = (1 - z) * n + z * h
+        outs.append(h)
+    return torch.stack(outs, 1)
+
+
+def test_gru_matches_formula():
+    RNG.setSeed(3)
+    cell = nn.GRU(4, 3)
+    rec = nn.Recurrent().add(cell)
+    x = torch.randn(2, 6, 4)
+    assert torch.allclose(rec.forward(x), _gru_reference(cell, x), atol=1e-5)
+
+
+@pytest.mark.parametrize("make", [
+    lambda: nn.Recurrent().add(nn.RnnCell(4, 3, nn.Tanh())),
+    lambda: nn.Recurrent().add(nn.GRU(4, 3)),
+    lambda: nn.Recurrent().add(nn.LSTMPeephole(4, 3)),
+    lambda: nn.Recurrent().add(nn.LSTM(4, 3)),
+    lambda: nn.Recurrent().add(nn.MultiRNNCell([nn.LSTM(4, 3), nn.GRU(3, 3)])),
+    lambda: nn.BiRecurrent().add(nn.LSTM(4, 3)),
+    lambda: nn.BiRecurrent(nn.JoinTable(3, 3), isSplitInput=True).add(nn.GRU(2, 3)),
+], ids=["rnn", "gru", "peephole", "lstm", "multi", "birnn", "birnn_split_join"])
+def test_recurrent_gradients(make):
+    RNG.setSeed(4)
+    m = make()
+    x = torch.randn(2, 3, 4)
+    gc = GradientChecker(1e-2, 3e-2)
+    ok, worst = gc.checkLayer(m, x)
+    assert ok, worst
+    ok, worst = gc.checkWeight(m, x)
+    assert ok, worst
+
+
+def test_conv_lstm_peephole_shapes_and_gradients():
+    RNG.setSeed(5)
+    m = nn.Recurrent().add(nn.ConvLSTMPeephole(2, 3, 3, 3))
+    x = torch.randn(2, 3, 2, 5, 5)
+    y = m.forward(x)
+    assert y.shape == (2, 3, 3, 5, 5)
+    gc = GradientChecker(1e-2, 3e-2)
+    assert gc.checkLayer(m, x)[0]
+    assert gc.checkWeight(m, x)[0]
+    m3 = nn.Recurrent().add(nn.ConvLSTMPeephole3D(2, 2, 3, 3))
+    y3 = m3.forward(torch.randn(1, 2, 2, 3, 4, 4))
+    assert y3.shape == (1, 2, 2, 3, 4, 4)
+
+
+def test_mask_zero_keeps_state_and_zeroes_output():
+    RNG.setSeed(6)
+    m = nn.Recurrent(maskZero=True).add(nn.LSTM(3, 4))
+    x = torch.randn(2, 5, 3)
+    x[1, 3:] = 0
+    y = m.forward(x)
+    assert torch.all(y[1, 3:] == 0)
+    ref = nn.Recurrent().add(m.getCell())
+    y2 = ref.forward(x[1:2, :3])
+    assert torch.allclose(y[1:2, :3], y2, atol=1e-6)
+
+
+def test_set_hidden_state_and_decoder():
+    RNG.setSeed(7)
+    m = nn.Recurrent().add(nn.LSTM(3, 4))
+    x = torch.randn(2, 4, 3)
+    full = m.forward(x)
+    m.forward(x[:, :2])
+    h = m.getHiddenState()
+    m.setHiddenState(h)
+    rest = m.forward(x[:, 2:])
+    assert torch.allclose(rest, full[:, 2:], atol=1e-6)
+    dec = nn.RecurrentDecoder(5).add(nn.LSTM(4, 4))
+    y = dec.forward(torch.randn(2, 4))
+    assert y.shape == (2, 5, 4)
+    gc = GradientChecker(1e-2, 3e-2)
+    assert gc.checkLayer(dec, torch.randn(2, 4))[0]
+
+
+def test_standalone_cell_table_protocol():
+    RNG.setSeed(8)
+    cell = nn.LSTM(3, 4)
+    x, h, c = torch.randn(2, 3), torch.randn(2, 4), torch.randn(2, 4)
+    out = cell.forward(T(x, T(h, c)))
+    assert out[1].shape == (2, 4) and torch.equal(out[1], out[2][1])
+    g = cell.backward(T(x, T(h, c)), T(torch.ones(2, 4), T(torch.zeros(2, 4), torch.zeros(2, 4))))
+    assert g[1].shape == (2, 3) and g[2][2].shape == (2, 4)
+
+
+def test_time_distributed_and_criterion():
+    RNG.setSeed(9)
+    td = nn.TimeDistributed(nn.Linear(4, 2))
+    x = torch.randn(3, 5, 4)
+    y = td.forward(x)
+    assert torch.allclose(y, x @ td.layer.weight.t() + td.layer.bias, atol=1e-6)
+    gc = GradientChecker(1e-2, 3e-2)
+    assert gc.checkLayer(td, x)[0] and gc.checkWeight(td, x)[0]
+
+
+def test_recurrent_serialization_roundtrip(tmp_path):
+    from bigdl_amd.nn.module import Module
+
+    RNG.setSeed(10)
+    m = nn.Sequential().add(nn.Recurrent().add(nn.LSTM(3, 4))).add(nn.TimeDistributed(nn.Linear(4, 2)))
+    b = nn.BiRecurrent().add(nn.GRU(3, 4))
+    x = torch.randn(2, 5, 3)
+    p = str(tmp_path / "m.bigdl")
+    m.saveModule(p)
+    m2 = Module.loadModule(p)
+    assert torch.allclose(m.forward(x), m2.forward(x), atol=1e-6)
+    b.saveModule(p, overWrite=True)
+    b2 = Module.loadModule(p)
+    assert torch.allclose(b.forward(x), b2.forward(x), atol=1e-6)
