@@ -1,0 +1,41 @@
+"""Scaled-dot-product attention core: softmax(q k^T + bias) v over [B, heads, L, depth] tensors.
+
+Reference: the MM(transB) -> CAddTable(bias) -> SoftMax -> Dropout -> MM chain of S/nn/Attention.scala:90-103.
+Math path (CPU engine, and any shape the fused kernel does not cover): explicit GEMMs + softmax under autograd
+(q is pre-scaled by depth^-0.5 as in SplitHeads(mul=true), Attention.scala:256-275).
+"""
+import torch
+
+from . import native
+
+
+def _flash_ok(q, k, v, bias, dropout_p):
+    if not q.is_cuda or dropout_p > 0.0:
+        return False
+    if not native.available() or not hasattr(native.get(), "flash_attn_fwd"):
+        return False
+    d = q.shape[-1]
+    return d in (64, 128) and q.shape[-2] >= 1 and k.shape[-2] >= 1
+
+
+def attention_math(q, k, v, bias=None, dropout_p=0.0, training=False):
+    s = torch.matmul(q, k.transpose(-1, -2))
+    if bias is not None:
+        s = s + bias
+    p = torch.softmax(s, dim=-1)
+    if training and dropout_p > 0.0:
+        p = torch.nn.functional.dropout(p, dropout_p, True)
+    return torch.matmul(p, v)
+
+
+def attention(q, k, v, bias=None, dropout_p=0.0, training=False, causal=False):
+    """q: [B, H, Lq, D] (already scaled), k/v: [B, H, Lk, D], bias broadcastable to [B, H, Lq, Lk].
+
+    ``causal`` is a hint that ``bias`` is the lower-triangular -1e9 mask (Transformer SelfAttentionMask), which
+    lets the fused kernel skip fully-masked key blocks.
+    """
+    if _flash_ok(q, k, v, bias, dropout_p if training else 0.0):
+        from .flash_attention import flash_attention
+
+        return flash_attention(q, k, v, None if causal else bias, causal)
+    return attention_math(q, k, v, bias, dropout_p, training)
