@@ -301,18 +301,41 @@ class Optimizer:
             losses = losses / step.comm.world
         vals = losses.cpu().tolist()
         st = self.state
+        wall = time.perf_counter() - wall0
         for (itn, _, rec), v in zip(pending, vals):
             st["Loss"] = v
             if self.trainSummary is not None and step.comm.rank == 0:
-                self.trainSummary.addScalar("Loss", v, itn)
-                self.trainSummary.addScalar("LearningRate", -self._optim_method().getLearningRate(), itn)
-        wall = time.perf_counter() - wall0
+                self._save_summary(itn, v, rec * step.comm.world / max(wall / len(pending), 1e-9))
         if step.comm.rank == 0:
             thr = sum(p[2] for p in pending) / max(self.metrics.get("computing time") * len(pending), 1e-9)
             logger.info("%s Trained %d records in %.4f seconds. Throughput is %.1f records/second. Loss is %.5f. %s",
                         self._header(st["epoch"], st["recordsProcessedThisEpoch"], st["neval"] - 1, wall),
                         pending[-1][2], self.metrics.get("computing time"), thr, vals[-1],
                         self._optim_method().getHyperParameter())
+
+    def _save_summary(self, itn, loss, throughput):
+        """Reference AbstractOptimizer.saveSummary (S/optim/AbstractOptimizer.scala:47): scalar tags gated by
+        their TrainSummary triggers, parameter histograms under the "Parameters" trigger."""
+        ts = self.trainSummary
+        trig_state = dict(self.state.items()) if hasattr(self.state, "items") else dict(self.state)
+        trig_state["neval"] = itn + 1
+        values = {"Loss": loss, "Throughput": throughput,
+                  "LearningRate": -self._optim_method().getLearningRate()}
+        triggers = ts.getScalarTriggers() if hasattr(ts, "getScalarTriggers") else [("Loss", None)]
+        for tag, trig in triggers:
+            if tag in values and (trig is None or trig(trig_state)):
+                ts.addScalar(tag, values[tag], itn)
+        ptrig = ts.getSummaryTrigger("Parameters") if hasattr(ts, "getSummaryTrigger") else None
+        if ptrig is not None and ptrig(trig_state):
+            for m in self.model.flattened_layers():
+                if m.modules_list():
+                    continue
+                for w, g in m._params:
+                    t, gt = getattr(m, w, None), getattr(m, g, None)
+                    if t is not None:
+                        ts.addHistogram(f"{m.getName()}/{w}", t, itn)
+                    if gt is not None:
+                        ts.addHistogram(f"{m.getName()}/{g}", gt, itn)
 
     def _validate(self, step):
         if self.validationTrigger is None or self.validationDataSet is None:
