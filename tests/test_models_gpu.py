@@ -150,3 +150,20 @@ def test_lenet_gpu_matches_cpu():
     fc = torch.cat([t.reshape(-1) for t in cpu.parameters()[1]])
     fg = torch.cat([t.float().cpu().reshape(-1) for t in gpu.parameters()[1]])
     assert _rel(fg, fc) < 5e-2
+
+
+@pytest.mark.parametrize("name,shape", [("VggForCifar10", (4, 3, 32, 32)),
+                                        ("Inception_v1_NoAuxClassifier", (2, 3, 224, 224)),
+                                        ("Inception_v2_NoAuxClassifier", (2, 3, 224, 224))])
+def test_zoo_models_gpu_match_cpu(name, shape):
+    """Concat branches, LRN, ceil-mode pooling, BN eps 1e-3 and dropout-free eval on the GPU engine."""
+    from bigdl_amd import models as M
+    from bigdl_amd.utils.random_generator import RNG
+
+    RNG.setSeed(11)
+    cpu = getattr(M, name)(10)
+    cpu.evaluate()
+    gpu = copy.deepcopy(cpu).to("cuda")
+    gpu.evaluate()
+    x = torch.randn(*shape)
+    assert _rel(gpu.forward(x.cuda()), cpu.forward(x)) < 5e-2
