@@ -222,7 +222,7 @@ def test_module_api_misc():
     m.modules[0].weight.data.fill_(0.5)
     assert torch.all(w[:12] == 0.5)  # parameters are views of the flat buffer
     m.freeze()
-    x = r(2, 3)
+    x = torch.ones(2, 3)      # 0.5 * 3 + |bias| < 1 keeps every ReLU open
     m.forward(x)
     m.zeroGradParameters()
     m.backward(x, torch.ones(2, 4))
