@@ -230,6 +230,37 @@ void lstm_cell_bwd(const Tensor& act, const OptT& c_prev, const Tensor& c, const
                       mf(dgates, "dgates"), omf(dc_prev, "dc_prev"), B, H, stream());
 }
 
+void image_augment(const Tensor& src, const Tensor& params, const Tensor& out, std::vector<double> mean,
+                   std::vector<double> std, bool rgb) {
+  TORCH_CHECK(src.is_cuda() && src.scalar_type() == at::kByte && src.dim() == 4 && src.size(3) == 3 &&
+                  src.is_contiguous(), "image_augment: src must be a contiguous uint8 [N, H, W, 3] device tensor");
+  TORCH_CHECK(params.scalar_type() == at::kInt && params.is_contiguous() && params.numel() == 3 * src.size(0),
+              "image_augment: params must be int32 [N, 3]");
+  TORCH_CHECK(mean.size() == 3 && std.size() == 3, "image_augment: mean/std need 3 entries");
+  const int N = src.size(0), H = src.size(1), W = src.size(2);
+  const bool bf = out.scalar_type() == at::kBFloat16;
+  int OH, OW;
+  if (bf) {
+    TORCH_CHECK(out.dim() == 4 && out.size(3) == 3 && out.is_contiguous(), "image_augment: bf16 out is [N, OH, OW, 3]");
+    OH = out.size(1), OW = out.size(2);
+  } else {
+    TORCH_CHECK(out.scalar_type() == at::kFloat && out.dim() == 4 && out.size(1) == 3 && out.is_contiguous(),
+                "image_augment: fp32 out is [N, 3, OH, OW]");
+    OH = out.size(2), OW = out.size(3);
+  }
+  TORCH_CHECK(out.size(0) == N && OH <= H && OW <= W, "image_augment: crop larger than the image");
+  auto pc = params.cpu();
+  const int* p = pc.data_ptr<int>();
+  for (int n = 0; n < N; ++n)
+    TORCH_CHECK(p[3 * n] >= 0 && p[3 * n] + OH <= H && p[3 * n + 1] >= 0 && p[3 * n + 1] + OW <= W,
+                "image_augment: crop window out of bounds for sample ", n);
+  float m[3], inv[3];
+  for (int c = 0; c < 3; ++c) m[c] = (float)mean[c], inv[c] = (float)(1.0 / std[c]);
+  auto pd = params.is_cuda() ? params : params.to(src.device());
+  bigdl_image_augment(src.data_ptr<uint8_t>(), pd.data_ptr<int>(), out.data_ptr(), N, H, W, OH, OW, m, inv,
+                      rgb ? 1 : 0, bf ? 1 : 0, stream());
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -262,5 +293,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("scale_f32", &scale_f32);
   m.def("lstm_cell_fwd", &lstm_cell_fwd);
   m.def("lstm_cell_bwd", &lstm_cell_bwd);
+  m.def("image_augment", &image_augment);
   m.attr("arch") = "gfx950";
 }

@@ -1,0 +1,135 @@
+"""Data pipeline on the CPU: MNIST/CIFAR readers, BGR/grey image transformers, multi-threaded batching,
+vision ImageFeature augmentations, text pipeline (reference T/dataset/**, T/transform/vision/image/**)."""
+import io
+
+import numpy as np
+import pytest
+import torch
+
+from bigdl_amd import dataset as D
+from bigdl_amd.dataset.image import encode_bgr_record
+from bigdl_amd.dataset.mnist_cifar import load_cifar_file, write_mnist
+from bigdl_amd.transform.vision import image as V
+from bigdl_amd.utils.random_generator import RNG
+
+
+def test_mnist_reader_and_grey_pipeline(tmp_path):
+    imgs = np.random.RandomState(0).randint(0, 256, (10, 28, 28)).astype(np.uint8)
+    labels = np.arange(10) % 10
+    write_mnist(tmp_path / "x", tmp_path / "y", imgs, labels)
+    recs = D.load_mnist(str(tmp_path / "x"), str(tmp_path / "y"))
+    assert len(recs) == 10 and recs[3].label == 4.0
+    pipe = D.BytesToGreyImg(28, 28) >> D.GreyImgNormalizer(0.13, 0.31) >> D.GreyImgCropper(24, 24) >> \
+        D.GreyImgToBatch(4)
+    batches = list(pipe(iter(recs)))
+    assert [b.size() for b in batches] == [4, 4, 2]
+    assert batches[0].getInput().shape == (4, 24, 24)
+    first = torch.tensor(imgs[0], dtype=torch.float32) / 255.0
+    assert abs(float(((first - 0.13) / 0.31).max()) - float(batches[0].getInput()[0].max())) < 0.6
+
+
+def test_cifar_reader_layout(tmp_path):
+    rec = np.zeros((2, 3073), dtype=np.uint8)
+    rec[0, 0], rec[1, 0] = 3, 7
+    rec[0, 1:1025] = 200            # R plane
+    rec[0, 1025:2049] = 100         # G plane
+    rec[0, 2049:] = 50              # B plane
+    p = tmp_path / "b.bin"
+    p.write_bytes(rec.tobytes())
+    recs = load_cifar_file(str(p), [])
+    assert recs[0].label == 4.0 and recs[1].label == 8.0
+    img = D.BGRImage().copy(recs[0].data)
+    assert img.content.shape == (32, 32, 3)
+    assert img.content[0, 0].tolist() == [50.0, 100.0, 200.0]        # B, G, R
+    assert img.toTensor(True)[:, 0, 0].tolist() == [200.0, 100.0, 50.0]
+
+
+def test_bgr_transformers_and_mt_batching():
+    RNG.setSeed(1)
+    recs = [D.ByteRecord(encode_bgr_record(torch.randint(0, 256, (36, 36, 3), dtype=torch.uint8)), i % 3 + 1)
+            for i in range(10)]
+    norm = D.BGRImgNormalizer(0.5, 0.5, 0.5, 0.25, 0.25, 0.25)
+    tf = D.BytesToBGRImg() >> D.BGRImgRdmCropper(32, 32, 4) >> D.HFlip(0.5) >> norm >> D.ColorJitter() >> \
+        D.Lighting()
+    mt = D.MTLabeledBGRImgToBatch(32, 32, 4, tf, threads=3)
+    batches = list(mt(iter(recs)))
+    assert sum(b.size() for b in batches) == 10
+    assert batches[0].getInput().shape == (4, 3, 32, 32)
+    labels = sorted(float(v) for b in batches for v in b.getTarget())
+    assert labels == sorted(float(i % 3 + 1) for i in range(10))
+    single = list((D.BytesToBGRImg() >> D.BGRImgCropper(30, 30, D.CropCenter) >> D.BGRImgToBatch(5))(iter(recs)))
+    assert single[0].getInput().shape == (5, 3, 30, 30)
+
+
+def test_local_image_files_and_reader(tmp_path):
+    from PIL import Image
+
+    for c in ("cat", "dog"):
+        (tmp_path / c).mkdir()
+        for i in range(2):
+            Image.fromarray(np.full((20, 30, 3), 40 * i, dtype=np.uint8)).save(tmp_path / c / f"{i}.png")
+    paths = D.LocalImageFiles.readPaths(str(tmp_path))
+    assert [p.label for p in paths] == [1.0, 1.0, 2.0, 2.0]
+    imgs = list(D.LocalImgReader(scaleTo=10)(iter(paths)))
+    assert imgs[0].content.shape == (10, 15, 3)
+
+
+def _feature(h=40, w=50):
+    from PIL import Image
+
+    arr = np.random.RandomState(2).randint(0, 256, (h, w, 3)).astype(np.uint8)
+    buf = io.BytesIO()
+    Image.fromarray(arr).save(buf, format="PNG")
+    return V.ImageFeature(buf.getvalue(), label=torch.tensor([2.0]), uri="x.png"), arr
+
+
+def test_vision_pipeline_and_frame():
+    RNG.setSeed(3)
+    f, arr = _feature()
+    frame = V.ImageFrame.array([f])
+    pipe = V.BytesToMat() >> V.Resize(36, 48) >> V.Brightness(-10, 10) >> V.Contrast(0.8, 1.2) >> \
+        V.Saturation(0.8, 1.2) >> V.Hue(-10, 10) >> V.RandomCrop(32, 32) >> V.HFlip() >> \
+        V.ChannelNormalize(123, 117, 104, 58, 57, 57) >> V.MatToTensor(toRGB=True) >> \
+        V.ImageFrameToSample(targetKeys=["label"])
+    frame.transform(pipe)
+    out = frame.array[0]
+    assert out.isValid() and out[V.ImageFeature.imageTensor].shape == (3, 32, 32)
+    assert out.getOriginalSize() == (40, 50, 3)
+    mb = list(V.ImageFeatureToMiniBatch(1).apply(iter(frame.array)))
+    assert mb[0].getInput().shape == (1, 3, 32, 32)
+
+
+def test_hsv_roundtrip_and_geometry():
+    m = torch.randint(0, 256, (8, 9, 3)).float()
+    assert torch.allclose(V.hsv_to_bgr(V.bgr_to_hsv(m)), m, atol=1e-3)
+    f = V.ImageFeature()
+    f[V.ImageFeature.mat] = m
+    V.Expand(minExpandRatio=2, maxExpandRatio=2).transform(f)
+    assert f.opencvMat().shape == (16, 18, 3)
+    V.CenterCrop(6, 4).transform(f)
+    assert f.opencvMat().shape == (4, 6, 3)
+    V.Filler(0, 0, 0.5, 0.5, 7).transform(f)
+    assert float(f.opencvMat()[0, 0, 0]) == 7.0
+    f2 = V.ImageFeature()
+    f2[V.ImageFeature.mat] = torch.rand(300, 400, 3) * 255
+    V.RandomAlterAspect(cropLength=64).transform(f2)
+    assert f2.opencvMat().shape == (64, 64, 3)
+    V.ScaleResize(32, 50).transform(f2)
+    assert f2.opencvMat().shape[0] == 32
+    bad = V.ImageFeature(b"not an image")
+    V.BytesToMat().transform(bad)
+    assert not bad.isValid()
+
+
+def test_text_pipeline():
+    text = ["The cat sat. The dog ran!", "A cat ran."]
+    sents = [s for p in D.SentenceSplitter()(iter(text)) for s in p]
+    toks = list(D.SentenceTokenizer()(iter(sents)))
+    assert toks[0] == ["the", "cat", "sat", "."]
+    padded = list(D.SentenceBiPadding()(iter(toks)))
+    dic = D.Dictionary(padded, vocabSize=6)
+    assert dic.getVocabSize() == 6 and dic.getIndex("zebra") == 5
+    ls = list(D.TextToLabeledSentence(dic)(iter(padded)))
+    s = list(D.LabeledSentenceToSample(dic.getVocabSize(), fixDataLength=7, fixLabelLength=7)(iter(ls)))
+    assert s[0].feature().shape == (7, 6) and s[0].label().shape == (7,)
+    assert float(s[0].label().min()) >= 1

@@ -224,3 +224,16 @@ def test_lstm_cell():
     C.lstm_cell_bwd(act, cp.detach(), c, dh, dcn, dg, dcp)
     assert _rel(dg, gates.grad) < 1e-4
     assert _rel(dcp, cp.grad) < 1e-4
+
+
+@pytest.mark.parametrize("nhwc", [False, True])
+def test_image_augment_kernel(nhwc):
+    from bigdl_amd.ops.image import augment_batch, augment_batch_ref, random_crop_params
+
+    torch.manual_seed(0)
+    src = torch.randint(0, 256, (6, 40, 48, 3), dtype=torch.uint8)
+    p = random_crop_params(6, 40, 48, 32, 30)
+    mean, std = (123.7, 116.3, 103.5), (58.4, 57.1, 57.4)
+    ref = augment_batch_ref(src, p, 32, 30, mean, std, True, nhwc)
+    out = augment_batch(src.cuda(), p, 32, 30, mean, std, True, nhwc).cpu()
+    assert torch.allclose(out.float(), ref.float(), atol=2e-2 if nhwc else 1e-5)
