@@ -19,16 +19,16 @@ class Module:
         return load_torch(path)
 
     @staticmethod
-    def loadCaffe(model, defPath, modelPath, matchAll=True):
+    def loadCaffe(model, defPath, modelPath, matchAll=True, customizedConverters=None):
         from ..interop.caffe import load_caffe_into
 
-        return load_caffe_into(model, defPath, modelPath, matchAll)
+        return load_caffe_into(model, defPath, modelPath, matchAll, customizedConverters)
 
     @staticmethod
-    def loadCaffeModel(defPath, modelPath):
+    def loadCaffeModel(defPath, modelPath, customizedConverters=None):
         from ..interop.caffe import load_caffe
 
-        return load_caffe(defPath, modelPath)
+        return load_caffe(defPath, modelPath, customizedConverters)[0]
 
     @staticmethod
     def flatten(parameters):
