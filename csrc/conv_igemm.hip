@@ -21,6 +21,7 @@
 //  * XCD-aware bijective block remap so neighbouring tiles share an XCD L2.
 #include "common.h"
 #include "kernels.h"
+#include <stdlib.h>
 
 
 namespace {
@@ -32,6 +33,90 @@ constexpr int BK = 64;          // K elements per LDS stage (8 granules of 16 B 
 __device__ __attribute__((aligned(64))) bf16_t g_zero_granule[32];
 __device__ __forceinline__ v4u load16(const bf16_t* p, bool ok) {
   return *reinterpret_cast<const v4u*>(ok ? p : g_zero_granule);
+}
+
+// Fused epilogue shared by the NT kernels: D[n][m] (weights were the MFMA A operand), so lane owns
+// channels n = 4*(lane>>4)+j (j=0..3) of pixel m = lane&15: + bias, + addend, ReLU, bf16 store along the
+// NHWC channel dim, per-channel BatchNorm (sum, sumsq) partials with one atomic per channel per wave.
+template <int MI, int NI, int TM, int TN>
+__device__ __forceinline__ void nt_epilogue(const ConvArgs& a, v4f (&acc)[MI][NI], int mbase, int nbase, int lane,
+                                            int bid) {
+  const int ohw = a.OH * a.OW;
+  const bool vec_ok = (a.Ncol & 3) == 0 && (a.ldo & 3) == 0;
+#pragma unroll
+  for (int j = 0; j < NI; ++j) {
+    const int nb = nbase + j * 16 + (lane >> 4) * 4;
+    float bs[4] = {0.f, 0.f, 0.f, 0.f};
+    if (a.bias) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) bs[e] = (nb + e < a.Ncol) ? a.bias[nb + e] : 0.f;
+    }
+    float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int m = mbase + i * 16 + (lane & 15);
+      long orow = m;
+      if (!a.ident_out && m < a.M) {
+        const int nb = m / ohw, rem = m - nb * ohw;
+        const int oh = rem / a.OW, ow = rem - oh * a.OW;
+        orow = ((long)nb * a.OHo + oh * a.omul_h + a.ooff_h) * a.OWo + ow * a.omul_w + a.ooff_w;
+      }
+      float ad[4] = {0.f, 0.f, 0.f, 0.f};
+      if (a.addend && m < a.M) {  // fused residual-gradient sum (ResNet block input gradient)
+        const bf16_t* ap = a.addend + (size_t)orow * a.ldo + nb;
+        if (vec_ok && nb + 3 < a.Ncol) {
+          const v2u q = *reinterpret_cast<const v2u*>(ap);
+          ad[0] = lo_bf(q[0]); ad[1] = hi_bf(q[0]); ad[2] = lo_bf(q[1]); ad[3] = hi_bf(q[1]);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) ad[e] = (nb + e < a.Ncol) ? bf2f(ap[e]) : 0.f;
+        }
+      }
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float t = acc[i][j][e] + bs[e] + ad[e];
+        if (a.relu) t = fmaxf(t, 0.f);
+        v[e] = t;
+      }
+      const unsigned p0 = pack2bf(v[0], v[1]), p1 = pack2bf(v[2], v[3]);
+      if (m < a.M) {
+        if (a.stats) {
+          s1[0] += lo_bf(p0); s1[1] += hi_bf(p0); s1[2] += lo_bf(p1); s1[3] += hi_bf(p1);
+          s2[0] += lo_bf(p0) * lo_bf(p0); s2[1] += hi_bf(p0) * hi_bf(p0);
+          s2[2] += lo_bf(p1) * lo_bf(p1); s2[3] += hi_bf(p1) * hi_bf(p1);
+        }
+        bf16_t* o = a.out + (size_t)orow * a.ldo + nb;
+        if (vec_ok && nb + 3 < a.Ncol) {
+          *reinterpret_cast<v2u*>(o) = v2u{p0, p1};
+        } else {
+          const unsigned pp[2] = {p0, p1};
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (nb + e < a.Ncol) o[e] = (bf16_t)((pp[e >> 1] >> ((e & 1) * 16)) & 0xffff);
+        }
+      }
+    }
+    if (a.stats) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          s1[e] += __shfl_xor(s1[e], o, 64);
+          s2[e] += __shfl_xor(s2[e], o, 64);
+        }
+      }
+      if ((lane & 15) == 0) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (nb + e < a.Ncol) {
+            float* sp = a.stats + (size_t)(bid & (BIGDL_STAT_SLOTS - 1)) * 2 * a.Ncol;  // slot: see batchnorm.hip
+            atomicAdd(sp + nb + e, s1[e]);
+            atomicAdd(sp + a.Ncol + nb + e, s2[e]);
+          }
+      }
+    }
+  }
 }
 
 template <int BM, int BN, int WM, bool FASTK>
@@ -157,82 +242,123 @@ __global__ __launch_bounds__(256, 2) void conv_nt_kernel(ConvArgs a) {
     __syncthreads();
   }
 
-  // ---- epilogue: D[n][m], lane owns n = 4*(lane>>4)+j (j=0..3), m = lane&15 ----
-  const bool vec_ok = (a.Ncol & 3) == 0 && (a.ldo & 3) == 0;
+  nt_epilogue<MI, NI, TM, TN>(a, acc, m0 + wm * TM, n0 + wn * TN, lane, bid);
+}
+
+// ------------------------------------------------------------------------------------------------
+// LDS-DMA variant of the NT kernel (Cs % 64 == 0): operands go global -> LDS with
+// global_load_lds_dwordx4 (no VGPR staging, no ds_write pass, no address-swizzle VALU on the write
+// side). The DMA writes wave-base + 16*lane, so each wave instruction fills 8 rows x 128 B of the
+// lane-linear LDS image; the XOR swizzle that keeps the ds_read_b128 fragment reads conflict-free is
+// applied on the *source* side: the lane that lands in slot s of row r fetches granule s ^ (r & 7)
+// (cdna_hip_programming.md §5 "Async global->LDS copy", T2). Two LDS stages; the DMA for stage k+1 is
+// in flight during the MFMAs of stage k and retired by the barrier that ends the step.
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ void glds16(const void* g, LDS_PTR(void) l) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g, l, 16, 0, 0);
+}
+
+template <int BM, int BN, int WM>
+__global__ __launch_bounds__(256, 2) void conv_nt_glds_kernel(ConvArgs a) {
+  constexpr int WN = 4 / WM;
+  constexpr int TM = BM / WM, TN = BN / WN;
+  constexpr int MI = TM / 16, NI = TN / 16;
+  constexpr int AI = BM / 32, BI = BN / 32;       // DMA instructions per thread per stage (8 rows each x 4 waves)
+  constexpr int STAGE = (BM + BN) * BK;
+  __shared__ __attribute__((aligned(1024))) bf16_t lds[2 * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WN, wn = wave % WN;
+  const int tiles_n = (a.Ncol + BN - 1) / BN;
+  const int tiles_m = (a.M + BM - 1) / BM;
+  const int nwg = tiles_m * tiles_n;
+  const int bid = xcd_remap(blockIdx.x, nwg);
+  const int tm = bid / tiles_n, tn = bid % tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  // DMA lane geometry: instruction i of wave w covers rows (i*4 + w)*8 .. +8; lane -> row += lane>>3,
+  // slot lane&7, which holds granule (lane&7) ^ (row&7) = (lane ^ (lane>>3)) & 7.
+  const int rsub = lane >> 3;
+  const int gsrc = (lane ^ rsub) & 7;
+  int a_pix[AI], a_h[AI], a_w[AI];
+  const int ohw = a.OH * a.OW;
 #pragma unroll
-  for (int j = 0; j < NI; ++j) {
-    const int nb = n0 + wn * TN + j * 16 + (lane >> 4) * 4;
-    float bs[4] = {0.f, 0.f, 0.f, 0.f};
-    if (a.bias) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) bs[e] = (nb + e < a.Ncol) ? a.bias[nb + e] : 0.f;
-    }
-    float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int i = 0; i < MI; ++i) {
-      const int m = m0 + wm * TM + i * 16 + (lane & 15);
-      long orow = m;
-      if (!a.ident_out && m < a.M) {
-        const int nb = m / ohw, rem = m - nb * ohw;
-        const int oh = rem / a.OW, ow = rem - oh * a.OW;
-        orow = ((long)nb * a.OHo + oh * a.omul_h + a.ooff_h) * a.OWo + ow * a.omul_w + a.ooff_w;
-      }
-      float ad[4] = {0.f, 0.f, 0.f, 0.f};
-      if (a.addend && m < a.M) {  // fused residual-gradient sum (ResNet block input gradient)
-        const bf16_t* ap = a.addend + (size_t)orow * a.ldo + nb;
-        if (vec_ok && nb + 3 < a.Ncol) {
-          const v2u q = *reinterpret_cast<const v2u*>(ap);
-          ad[0] = lo_bf(q[0]); ad[1] = hi_bf(q[0]); ad[2] = lo_bf(q[1]); ad[3] = hi_bf(q[1]);
-        } else {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) ad[e] = (nb + e < a.Ncol) ? bf2f(ap[e]) : 0.f;
-        }
-      }
-      float v[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float t = acc[i][j][e] + bs[e] + ad[e];
-        if (a.relu) t = fmaxf(t, 0.f);
-        v[e] = t;
-      }
-      const unsigned p0 = pack2bf(v[0], v[1]), p1 = pack2bf(v[2], v[3]);
-      if (m < a.M) {
-        if (a.stats) {
-          s1[0] += lo_bf(p0); s1[1] += hi_bf(p0); s1[2] += lo_bf(p1); s1[3] += hi_bf(p1);
-          s2[0] += lo_bf(p0) * lo_bf(p0); s2[1] += hi_bf(p0) * hi_bf(p0);
-          s2[2] += lo_bf(p1) * lo_bf(p1); s2[3] += hi_bf(p1) * hi_bf(p1);
-        }
-        bf16_t* o = a.out + (size_t)orow * a.ldo + nb;
-        if (vec_ok && nb + 3 < a.Ncol) {
-          *reinterpret_cast<v2u*>(o) = v2u{p0, p1};
-        } else {
-          const unsigned pp[2] = {p0, p1};
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            if (nb + e < a.Ncol) o[e] = (bf16_t)((pp[e >> 1] >> ((e & 1) * 16)) & 0xffff);
-        }
-      }
-    }
-    if (a.stats) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) {
-          s1[e] += __shfl_xor(s1[e], o, 64);
-          s2[e] += __shfl_xor(s2[e], o, 64);
-        }
-      }
-      if ((lane & 15) == 0) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          if (nb + e < a.Ncol) {
-            float* sp = a.stats + (size_t)(bid & (BIGDL_STAT_SLOTS - 1)) * 2 * a.Ncol;  // slot: see batchnorm.hip
-            atomicAdd(sp + nb + e, s1[e]);
-            atomicAdd(sp + a.Ncol + nb + e, s2[e]);
-          }
-      }
+  for (int i = 0; i < AI; ++i) {
+    const int m = m0 + (i * 4 + wave) * 8 + rsub;
+    if (m < a.M) {
+      const int nb = m / ohw, rem = m - nb * ohw;
+      const int oh = rem / a.OW, ow = rem - oh * a.OW;
+      a_pix[i] = nb * a.Hs * a.Ws;
+      a_h[i] = oh * a.mul_h;
+      a_w[i] = ow * a.mul_w;
+    } else {
+      a_pix[i] = 0; a_h[i] = -(1 << 28); a_w[i] = -(1 << 28);
     }
   }
+  const bf16_t* wrow[BI];
+  bool bvalid[BI];
+#pragma unroll
+  for (int i = 0; i < BI; ++i) {
+    const int n = n0 + (i * 4 + wave) * 8 + rsub;
+    bvalid[i] = n < a.Ncol;
+    wrow[i] = a.wt + (size_t)(bvalid[i] ? n : 0) * a.ldw + gsrc * 8;
+  }
+
+  auto issue = [&](int kt, int buf) {
+    const int k0 = kt * BK;
+    const int t = k0 / a.Cs;
+    const int c = k0 - t * a.Cs + gsrc * 8;
+    const int th = a.tap_h[t], tw = a.tap_w[t];
+    const int wk = a.tap_k[t] * a.Cs + (k0 - t * a.Cs);
+    bf16_t* A = lds + buf * STAGE;
+    bf16_t* B = A + BM * BK;
+#pragma unroll
+    for (int i = 0; i < AI; ++i) {
+      const int ch = a_h[i] + th, cw = a_w[i] + tw;
+      const bool ok = (unsigned)ch < (unsigned)a.Hs && (unsigned)cw < (unsigned)a.Ws;
+      const bf16_t* src = ok ? a.src + (unsigned)((a_pix[i] + ch * a.Ws + cw) * a.Cs + c) : g_zero_granule;
+      glds16(src, (LDS_PTR(void))(A + (i * 4 + wave) * 8 * BK));
+    }
+#pragma unroll
+    for (int i = 0; i < BI; ++i) {
+      const bf16_t* src = bvalid[i] ? wrow[i] + wk : g_zero_granule;
+      glds16(src, (LDS_PTR(void))(B + (i * 4 + wave) * 8 * BK));
+    }
+  };
+  auto swz = [](int row, int g) { return row * BK + ((g ^ (row & 7)) << 3); };
+
+  v4f acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = a.Kdim / BK;
+  issue(0, 0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) issue(kt + 1, cur ^ 1);
+    const bf16_t* A = lds + cur * STAGE;
+    const bf16_t* B = A + BM * BK;
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks) {
+      v8s fa[MI], fb[NI];
+      const int g = ks * 4 + (lane >> 4);
+#pragma unroll
+      for (int i = 0; i < MI; ++i) fa[i] = *reinterpret_cast<const v8s*>(A + swz(wm * TM + i * 16 + (lane & 15), g));
+#pragma unroll
+      for (int j = 0; j < NI; ++j) fb[j] = *reinterpret_cast<const v8s*>(B + swz(wn * TN + j * 16 + (lane & 15), g));
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+    }
+    __syncthreads();   // retires the stage-(k+1) DMA (vmcnt(0)) and the stage-k fragment reads
+  }
+  nt_epilogue<MI, NI, TM, TN>(a, acc, m0 + wm * TM, n0 + wn * TN, lane, bid);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -431,6 +557,21 @@ void launch_nt(const ConvArgs& a, bool fastk, hipStream_t st) {
   else conv_nt_kernel<BM, BN, WM, false><<<grid, block, 0, st>>>(a);
 }
 
+template <int BM, int BN, int WM>
+void launch_nt_glds(const ConvArgs& a, hipStream_t st) {
+  const int nwg = ((a.M + BM - 1) / BM) * ((a.Ncol + BN - 1) / BN);
+  conv_nt_glds_kernel<BM, BN, WM><<<dim3(nwg), dim3(256), 0, st>>>(a);
+}
+
+// BIGDL_CONV_IMPL: 1 (default) = LDS-DMA kernel where Cs % 64 == 0, 0 = register-staged kernel everywhere.
+int conv_impl() {
+  static int v = [] {
+    const char* e = getenv("BIGDL_CONV_IMPL");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
+
 }  // namespace
 
 extern "C" {
@@ -440,8 +581,14 @@ int bigdl_conv_nt(const ConvArgs* a, hipStream_t st) {
   if (a->Cs % 8 != 0 || a->Kdim != a->ntaps * a->Cs || a->ntaps < 1 || a->ntaps > CONV_MAX_TAPS) return -1;
   if (a->M <= 0) return 0;
   const bool fastk = (a->Cs % BK) == 0;
-  if (a->Ncol <= 64) launch_nt<128, 64, 2>(*a, fastk, st);
-  else launch_nt<128, 128, 2>(*a, fastk, st);
+  if (fastk && conv_impl() == 1) {
+    if (a->Ncol <= 64) launch_nt_glds<128, 64, 2>(*a, st);
+    else launch_nt_glds<128, 128, 2>(*a, st);
+  } else if (a->Ncol <= 64) {
+    launch_nt<128, 64, 2>(*a, fastk, st);
+  } else {
+    launch_nt<128, 128, 2>(*a, fastk, st);
+  }
   HIP_LAUNCH_CHECK();
   return 0;
 }

@@ -31,13 +31,20 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--only", type=str, default="", help="comma-separated shape indices")
+    ap.add_argument("--no-miopen", action="store_true")
+    ap.add_argument("--ops", type=str, default="fwd,dgrad,wgrad")
     args = ap.parse_args()
+    only = {int(i) for i in args.only.split(",") if i}
+    ops = set(args.ops.split(","))
     N = args.batch
     dev = torch.device("cuda")
     tot = {"ours_fwd": 0, "ours_dgrad": 0, "ours_wgrad": 0, "miopen_fwd": 0, "miopen_dgrad": 0, "miopen_wgrad": 0}
     flops_total = 0
     rows = []
-    for (C, H, K, R, st, pd, cnt) in SHAPES:
+    for si, (C, H, K, R, st, pd, cnt) in enumerate(SHAPES):
+        if only and si not in only:
+            continue
         x = torch.randn(N, C, H, H, device=dev).to(BF, memory_format=CL)
         w = (torch.randn(K, C, R, R, device=dev) * 0.05).to(BF, memory_format=CL)
         b = torch.zeros(K, device=dev)
@@ -47,12 +54,17 @@ def main():
         dw = torch.zeros(K, C, R, R, device=dev).contiguous(memory_format=CL)
         db = torch.zeros(K, device=dev)
         fl = 2.0 * N * OH * OH * K * C * R * R
-        t_f = timeit(lambda: cv.conv2d_fwd(x, w, b, (st, st), (pd, pd)), args.iters)
-        t_d = timeit(lambda: cv.conv2d_dgrad(gy, wt, x.shape, (st, st), (pd, pd)), args.iters)
-        t_w = timeit(lambda: (dw.zero_(), cv.conv2d_wgrad(gy, x, dw, db, (st, st), (pd, pd))), args.iters)
-        m_f = timeit(lambda: F.conv2d(x, w, None, st, pd), args.iters)
-        m_d = timeit(lambda: torch.ops.aten.convolution_backward(gy, x, w, None, (st, st), (pd, pd), (1, 1), False, (0, 0), 1, (True, False, False)), args.iters)
-        m_w = timeit(lambda: torch.ops.aten.convolution_backward(gy, x, w, None, (st, st), (pd, pd), (1, 1), False, (0, 0), 1, (False, True, False)), args.iters)
+        nan = float("nan")
+        t_f = timeit(lambda: cv.conv2d_fwd(x, w, b, (st, st), (pd, pd)), args.iters) if "fwd" in ops else nan
+        t_d = timeit(lambda: cv.conv2d_dgrad(gy, wt, x.shape, (st, st), (pd, pd)), args.iters) if "dgrad" in ops else nan
+        t_w = timeit(lambda: (dw.zero_(), cv.conv2d_wgrad(gy, x, dw, db, (st, st), (pd, pd))), args.iters) \
+            if "wgrad" in ops else nan
+        if args.no_miopen:
+            m_f = m_d = m_w = nan
+        else:
+          m_f = timeit(lambda: F.conv2d(x, w, None, st, pd), args.iters)
+          m_d = timeit(lambda: torch.ops.aten.convolution_backward(gy, x, w, None, (st, st), (pd, pd), (1, 1), False, (0, 0), 1, (True, False, False)), args.iters)
+          m_w = timeit(lambda: torch.ops.aten.convolution_backward(gy, x, w, None, (st, st), (pd, pd), (1, 1), False, (0, 0), 1, (False, True, False)), args.iters)
         row = dict(C=C, H=H, K=K, R=R, s=st, cnt=cnt, fwd_ms=round(t_f, 3), dgrad_ms=round(t_d, 3), wgrad_ms=round(t_w, 3),
                    miopen_fwd=round(m_f, 3), miopen_dgrad=round(m_d, 3), miopen_wgrad=round(m_w, 3),
                    fwd_tflops=round(fl / t_f / 1e9, 1), dgrad_tflops=round(fl / t_d / 1e9, 1), wgrad_tflops=round(fl / t_w / 1e9, 1))
