@@ -294,5 +294,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("lstm_cell_fwd", &lstm_cell_fwd);
   m.def("lstm_cell_bwd", &lstm_cell_bwd);
   m.def("image_augment", &image_augment);
+  m.def("set_conv_impl", &bigdl_set_conv_impl);
+  m.def("get_conv_impl", &bigdl_get_conv_impl);
   m.attr("arch") = "gfx950";
 }

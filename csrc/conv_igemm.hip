@@ -119,6 +119,96 @@ __device__ __forceinline__ void nt_epilogue(const ConvArgs& a, v4f (&acc)[MI][NI
   }
 }
 
+// Coalescing epilogue (Ncol % 8 == 0, ldo % 8 == 0): each wave parks its fp32 TM x TN tile in its own
+// slice of the (now idle) staging LDS — [pixel][channel], 16-byte granules XOR-swizzled by pixel so both
+// the 16-byte writes (lanes of 16 consecutive pixels) and the 2 x 16-byte reads (lanes along a pixel row)
+// are conflict-free — then re-reads it row-wise: a lane owns 8 channels of one pixel, so every store is
+// 16 B and one wave instruction writes 64/(TN/8) whole pixel rows of TN channels. bias / addend / ReLU /
+// BN statistics are applied in the row phase (the addend is read with the same 16-byte coalesced pattern).
+template <int MI, int NI, int TM, int TN>
+__device__ __forceinline__ void nt_epilogue_lds(const ConvArgs& a, v4f (&acc)[MI][NI], int mbase, int nbase,
+                                                int lane, int bid, float* wl) {
+  constexpr int GR = TN / 4;            // 16-byte fp32 granules per pixel row
+  constexpr int LPR = TN / 8;           // lanes per pixel row in the read phase
+  constexpr int PPI = 64 / LPR;         // pixels per read instruction
+  static_assert(TN % 8 == 0 && 64 % LPR == 0, "tile");
+  auto gpos = [](int p, int g) { return (p * GR + (g ^ (p & (GR - 1)))) * 4; };
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int p = i * 16 + (lane & 15);
+      const int g = j * 4 + (lane >> 4);
+      *reinterpret_cast<v4f*>(wl + gpos(p, g)) = acc[i][j];
+    }
+  __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's LDS writes landed (wave-private slice)
+  const int ohw = a.OH * a.OW;
+  const int q = lane % LPR;              // this lane's 8-channel group within the wave tile
+  const int n = nbase + q * 8;
+  const bool nok = n < a.Ncol;
+  float bs[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) bs[e] = (a.bias && nok) ? a.bias[n + e] : 0.f;
+  float s1[8], s2[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) s1[e] = s2[e] = 0.f;
+#pragma unroll
+  for (int r = 0; r < TM / PPI; ++r) {
+    const int p = r * PPI + lane / LPR;
+    const int m = mbase + p;
+    const v4f lo = *reinterpret_cast<const v4f*>(wl + gpos(p, 2 * q));
+    const v4f hi = *reinterpret_cast<const v4f*>(wl + gpos(p, 2 * q + 1));
+    if (m < a.M && nok) {
+      long orow = m;
+      if (!a.ident_out) {
+        const int nb = m / ohw, rem = m - nb * ohw;
+        const int oh = rem / a.OW, ow = rem - oh * a.OW;
+        orow = ((long)nb * a.OHo + oh * a.omul_h + a.ooff_h) * a.OWo + ow * a.omul_w + a.ooff_w;
+      }
+      float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      if (a.addend) {
+        const v4u ad = *reinterpret_cast<const v4u*>(a.addend + (size_t)orow * a.ldo + n);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { v[2 * e] += lo_bf(ad[e]); v[2 * e + 1] += hi_bf(ad[e]); }
+      }
+      v4u o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float x0 = v[2 * e] + bs[2 * e], x1 = v[2 * e + 1] + bs[2 * e + 1];
+        if (a.relu) { x0 = fmaxf(x0, 0.f); x1 = fmaxf(x1, 0.f); }
+        o[e] = pack2bf(x0, x1);
+      }
+      if (a.stats) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float y0 = lo_bf(o[e]), y1 = hi_bf(o[e]);
+          s1[2 * e] += y0; s2[2 * e] += y0 * y0;
+          s1[2 * e + 1] += y1; s2[2 * e + 1] += y1 * y1;
+        }
+      }
+      *reinterpret_cast<v4u*>(a.out + (size_t)orow * a.ldo + n) = o;
+    }
+  }
+  if (a.stats) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+#pragma unroll
+      for (int o = LPR; o < 64; o <<= 1) {
+        s1[e] += __shfl_xor(s1[e], o, 64);
+        s2[e] += __shfl_xor(s2[e], o, 64);
+      }
+    }
+    if (lane < LPR && nok) {
+      float* sp = a.stats + (size_t)(bid & (BIGDL_STAT_SLOTS - 1)) * 2 * a.Ncol;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        atomicAdd(sp + n + e, s1[e]);
+        atomicAdd(sp + a.Ncol + n + e, s2[e]);
+      }
+    }
+  }
+}
+
 template <int BM, int BN, int WM, bool FASTK>
 __global__ __launch_bounds__(256, 2) void conv_nt_kernel(ConvArgs a) {
   constexpr int WN = 4 / WM;
@@ -242,7 +332,11 @@ __global__ __launch_bounds__(256, 2) void conv_nt_kernel(ConvArgs a) {
     __syncthreads();
   }
 
-  nt_epilogue<MI, NI, TM, TN>(a, acc, m0 + wm * TM, n0 + wn * TN, lane, bid);
+  if ((a.Ncol & 7) == 0 && (a.ldo & 7) == 0)
+    nt_epilogue_lds<MI, NI, TM, TN>(a, acc, m0 + wm * TM, n0 + wn * TN, lane, bid,
+                                    reinterpret_cast<float*>(lds) + wave * TM * TN);
+  else
+    nt_epilogue<MI, NI, TM, TN>(a, acc, m0 + wm * TM, n0 + wn * TN, lane, bid);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -358,7 +452,148 @@ __global__ __launch_bounds__(256, 2) void conv_nt_glds_kernel(ConvArgs a) {
     }
     __syncthreads();   // retires the stage-(k+1) DMA (vmcnt(0)) and the stage-k fragment reads
   }
-  nt_epilogue<MI, NI, TM, TN>(a, acc, m0 + wm * TM, n0 + wn * TN, lane, bid);
+  if ((a.Ncol & 7) == 0 && (a.ldo & 7) == 0)
+    nt_epilogue_lds<MI, NI, TM, TN>(a, acc, m0 + wm * TM, n0 + wn * TN, lane, bid,
+                                    reinterpret_cast<float*>(lds) + wave * TM * TN);
+  else
+    nt_epilogue<MI, NI, TM, TN>(a, acc, m0 + wm * TM, n0 + wn * TN, lane, bid);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Deep-pipelined LDS-DMA NT kernel for large grids: 256 pixels x BN channels per workgroup, 8 waves,
+// BK = 64, THREE LDS stages with two K-tiles of DMA in flight across each barrier: the step ends with a
+// counted `s_waitcnt vmcnt(L)` (L = DMA instructions of one tile, so only tile k+1 is retired while tile
+// k+2 keeps streaming) and a raw s_barrier — never __syncthreads(), whose vmcnt(0) would drain the
+// pipeline (cdna_hip_programming.md §5 "Pipelining across barriers"). All LDS — the three stages and the
+// tap table — lives in one __shared__ array, and the loop issues no VGPR-destination global load, so the
+// compiler has no reason to insert a vmcnt(0) of its own (§5 "Projection GEMM" item 4).
+// ------------------------------------------------------------------------------------------------
+template <int BN, int WGM, int WGN>
+__global__ __launch_bounds__(512, 1) void conv_nt_p3_kernel(ConvArgs a) {
+  constexpr int BM = 256;
+  constexpr int TM = BM / WGM, TN = BN / WGN;     // per-wave tile (pixels x channels)
+  constexpr int MI = TM / 16, NI = TN / 16;
+  constexpr int AI = BM / 64, BI = BN / 64;       // DMA instructions per thread per stage (8 waves x 8 rows)
+  constexpr int L = AI + BI;
+  constexpr int STAGE = (BM + BN) * BK;
+  constexpr int NSTAGE = 3;
+  __shared__ __attribute__((aligned(1024))) bf16_t lds[NSTAGE * STAGE + 3 * CONV_MAX_TAPS];
+  short* taps = reinterpret_cast<short*>(lds + NSTAGE * STAGE);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WGN, wn = wave % WGN;
+  const int tiles_n = (a.Ncol + BN - 1) / BN;
+  const int tiles_m = (a.M + BM - 1) / BM;
+  const int nwg = tiles_m * tiles_n;
+  const int bid = xcd_remap(blockIdx.x, nwg);
+  const int tm = bid / tiles_n, tn = bid % tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  if (tid < a.ntaps) {
+    taps[tid] = a.tap_h[tid];
+    taps[CONV_MAX_TAPS + tid] = a.tap_w[tid];
+    taps[2 * CONV_MAX_TAPS + tid] = a.tap_k[tid];
+  }
+
+  const int rsub = lane >> 3;
+  const int gsrc = (lane ^ rsub) & 7;
+  int a_pix[AI], a_h[AI], a_w[AI];
+  const int ohw = a.OH * a.OW;
+#pragma unroll
+  for (int i = 0; i < AI; ++i) {
+    const int m = m0 + (i * 8 + wave) * 8 + rsub;
+    if (m < a.M) {
+      const int nb = m / ohw, rem = m - nb * ohw;
+      const int oh = rem / a.OW, ow = rem - oh * a.OW;
+      a_pix[i] = nb * a.Hs * a.Ws;
+      a_h[i] = oh * a.mul_h;
+      a_w[i] = ow * a.mul_w;
+    } else {
+      a_pix[i] = 0; a_h[i] = -(1 << 28); a_w[i] = -(1 << 28);
+    }
+  }
+  const bf16_t* wrow[BI];
+  bool bvalid[BI];
+#pragma unroll
+  for (int i = 0; i < BI; ++i) {
+    const int n = n0 + (i * 8 + wave) * 8 + rsub;
+    bvalid[i] = n < a.Ncol;
+    wrow[i] = a.wt + (size_t)(bvalid[i] ? n : 0) * a.ldw + gsrc * 8;
+  }
+  __syncthreads();   // tap table visible (no DMA outstanding yet)
+
+  auto issue = [&](int kt, int buf) {
+    const int k0 = kt * BK;
+    const int t = k0 / a.Cs;
+    const int cin = k0 - t * a.Cs;
+    const int th = taps[t], tw = taps[CONV_MAX_TAPS + t];
+    const int wk = taps[2 * CONV_MAX_TAPS + t] * a.Cs + cin;
+    const int c = cin + gsrc * 8;
+    bf16_t* A = lds + buf * STAGE;
+    bf16_t* B = A + BM * BK;
+#pragma unroll
+    for (int i = 0; i < AI; ++i) {
+      const int ch = a_h[i] + th, cw = a_w[i] + tw;
+      const bool ok = (unsigned)ch < (unsigned)a.Hs && (unsigned)cw < (unsigned)a.Ws;
+      const bf16_t* src = ok ? a.src + (unsigned)((a_pix[i] + ch * a.Ws + cw) * a.Cs + c) : g_zero_granule;
+      glds16(src, (LDS_PTR(void))(A + (i * 8 + wave) * 8 * BK));
+    }
+#pragma unroll
+    for (int i = 0; i < BI; ++i) {
+      const bf16_t* src = bvalid[i] ? wrow[i] + wk : g_zero_granule;
+      glds16(src, (LDS_PTR(void))(B + (i * 8 + wave) * 8 * BK));
+    }
+  };
+  auto swz = [](int row, int g) { return row * BK + ((g ^ (row & 7)) << 3); };
+
+  v4f acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = a.Kdim / BK;
+  issue(0, 0);
+  if (nk > 1) {
+    issue(1, 1);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(L) : "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  int cur = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    const bool more2 = kt + 2 < nk;
+    if (more2) issue(kt + 2, cur == 0 ? 2 : cur - 1);
+    const bf16_t* A = lds + cur * STAGE;
+    const bf16_t* B = A + BM * BK;
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks) {
+      v8s fa[MI], fb[NI];
+      const int g = ks * 4 + (lane >> 4);
+#pragma unroll
+      for (int i = 0; i < MI; ++i) fa[i] = *reinterpret_cast<const v8s*>(A + swz(wm * TM + i * 16 + (lane & 15), g));
+#pragma unroll
+      for (int j = 0; j < NI; ++j) fb[j] = *reinterpret_cast<const v8s*>(B + swz(wn * TN + j * 16 + (lane & 15), g));
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+    }
+    // retire tile k+1 (tile k+2 stays in flight), then make every wave's reads of this stage and every
+    // wave's tile-(k+1) DMA ordered before anything after the barrier
+    if (more2) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(L) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    cur = cur == 2 ? 0 : cur + 1;
+  }
+  if ((a.Ncol & 7) == 0 && (a.ldo & 7) == 0)
+    nt_epilogue_lds<MI, NI, TM, TN>(a, acc, m0 + wm * TM, n0 + wn * TN, lane, bid,
+                                    reinterpret_cast<float*>(lds) + wave * TM * TN);
+  else
+    nt_epilogue<MI, NI, TM, TN>(a, acc, m0 + wm * TM, n0 + wn * TN, lane, bid);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -368,8 +603,14 @@ __global__ __launch_bounds__(256, 2) void conv_nt_glds_kernel(ConvArgs a) {
 constexpr int WBM = 64;    // pixels (reduction) per LDS stage
 constexpr int WT = 128;    // output tile: 128 n x 128 kk
 
-__device__ __forceinline__ int wswz(int row, int col) {  // [WBM][128] bf16 image, 16 slots/row
-  return row * WT + ((((col >> 3) ^ (row & 15))) << 3) + (col & 7);
+// [WBM][128] bf16 image, 16 granules of 16 B per row, granule g of row r stored at g ^ f(r).
+// f is chosen for the ds_read_b64_tr_b16 fragment reads: a 16-lane group reads rows {q} (q = 0..3) x a granule
+// pair {g0, g0+1} (g0 even), and its 32-lane partner reads rows {8+q}: f(r) = 2(r&3) | 8((r>>3)&1) | ((r>>2)&1)
+// sends those 32 lanes' 8-byte halves to 32 distinct bank pairs (conflict-free); within a row it is a
+// permutation, so the 16-byte staging writes stay conflict-free too.
+__device__ __forceinline__ int wswz(int row, int col) {
+  const int f = ((row & 3) << 1) | (((row >> 3) & 1) << 3) | ((row >> 2) & 1);
+  return row * WT + ((((col >> 3) ^ f)) << 3) + (col & 7);
 }
 
 __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(WgradArgs a) {
@@ -563,25 +804,41 @@ void launch_nt_glds(const ConvArgs& a, hipStream_t st) {
   conv_nt_glds_kernel<BM, BN, WM><<<dim3(nwg), dim3(256), 0, st>>>(a);
 }
 
-// BIGDL_CONV_IMPL: 1 (default) = LDS-DMA kernel where Cs % 64 == 0, 0 = register-staged kernel everywhere.
+template <int BN, int WGM, int WGN>
+void launch_nt_p3(const ConvArgs& a, hipStream_t st) {
+  const int nwg = ((a.M + 255) / 256) * ((a.Ncol + BN - 1) / BN);
+  conv_nt_p3_kernel<BN, WGM, WGN><<<dim3(nwg), dim3(512), 0, st>>>(a);
+}
+
+// BIGDL_CONV_IMPL: 2 = deep-pipelined 256-pixel kernel on grids that fill the chip,
+// 1 (default) = LDS-DMA kernel where Cs % 64 == 0, 0 = register-staged kernel everywhere.
+int g_conv_impl = -1;
 int conv_impl() {
-  static int v = [] {
+  if (g_conv_impl < 0) {
     const char* e = getenv("BIGDL_CONV_IMPL");
-    return e ? atoi(e) : 1;
-  }();
-  return v;
+    g_conv_impl = e ? atoi(e) : 1;
+  }
+  return g_conv_impl;
 }
 
 }  // namespace
 
 extern "C" {
 
+void bigdl_set_conv_impl(int impl) { g_conv_impl = impl; }
+int bigdl_get_conv_impl() { return conv_impl(); }
+
 // Forward or data-gradient implicit GEMM. Returns 0 on success, negative on unsupported shapes.
 int bigdl_conv_nt(const ConvArgs* a, hipStream_t st) {
   if (a->Cs % 8 != 0 || a->Kdim != a->ntaps * a->Cs || a->ntaps < 1 || a->ntaps > CONV_MAX_TAPS) return -1;
   if (a->M <= 0) return 0;
   const bool fastk = (a->Cs % BK) == 0;
-  if (fastk && conv_impl() == 1) {
+  const int impl = conv_impl();
+  const long p3_tiles = (long)((a->M + 255) / 256) * ((a->Ncol + 127) / 128);
+  if (fastk && impl == 2 && p3_tiles >= 256) {
+    if (a->Ncol <= 64) launch_nt_p3<64, 8, 1>(*a, st);
+    else launch_nt_p3<128, 4, 2>(*a, st);
+  } else if (fastk && impl >= 1) {
     if (a->Ncol <= 64) launch_nt_glds<128, 64, 2>(*a, st);
     else launch_nt_glds<128, 128, 2>(*a, st);
   } else if (a->Ncol <= 64) {

@@ -99,6 +99,9 @@ void bigdl_lstm_cell_fwd(const float* gates, const float* c_prev, float* c, floa
 void bigdl_lstm_cell_bwd(const float* act, const float* c_prev, const float* c, const float* dh,
                          const float* dc_next, float* dgates, float* dc_prev, int B, int H, hipStream_t st);
 
+void bigdl_set_conv_impl(int impl);
+int bigdl_get_conv_impl();
+
 // Input pipeline: crop + flip + channel reorder + normalise of a uint8 [N, H, W, 3] BGR batch.
 // params: int32 [N][3] = (y0, x0, flip). Output fp32 NCHW [N, 3, OH, OW] or bf16 NHWC [N, OH, OW, 3].
 void bigdl_image_augment(const uint8_t* src, const int* params, void* out, int N, int H, int W, int OH, int OW,

@@ -73,6 +73,47 @@ def test_conv_fwd_dgrad_wgrad(case):
     assert _rel(db, gy.float().sum(dim=(0, 2, 3))) < 1e-2
 
 
+BIG_CASES = [
+    # N, C, H, K, R, stride, pad: grids large enough for the 256-pixel deep-pipelined kernel
+    (32, 64, 56, 128, 3, 1, 1),
+    (32, 256, 56, 64, 1, 1, 0),
+    (16, 128, 56, 256, 3, 2, 1),
+    (8, 512, 28, 1000, 1, 1, 0),     # Ncol tail (1000 % 128 != 0)
+]
+
+
+@pytest.mark.parametrize("impl", [0, 1, 2])
+@pytest.mark.parametrize("case", BIG_CASES)
+def test_conv_nt_variants_large(case, impl):
+    """Register-staged (0), LDS-DMA (1) and deep-pipelined 3-stage LDS-DMA (2) NT kernels, fwd (+stats) and
+    dgrad, vs fp32 torch."""
+    from bigdl_amd.ops import bn as bnops
+    from bigdl_amd.ops import conv as cv
+    from bigdl_amd.ops import native
+
+    N, C, H, K, R, st, pd = case
+    C_ = native.get()
+    old = C_.get_conv_impl()
+    C_.set_conv_impl(impl)
+    try:
+        torch.manual_seed(1)
+        dev = _dev()
+        x = torch.randn(N, C, H, H, device=dev).to(BF, memory_format=CL)
+        w = (torch.randn(K, C, R, R, device=dev) * (1.0 / (C * R * R) ** 0.5)).to(BF, memory_format=CL)
+        stats = bnops.new_stats(K, dev)
+        y = cv.conv2d_fwd(x, w, None, (st, st), (pd, pd), stats=stats)
+        yr = F.conv2d(x.float(), w.float(), None, stride=st, padding=pd)
+        assert _rel(y, yr) < 1e-2
+        st2 = stats.view(bnops.stat_slots(), 2, K).sum(0)
+        assert _rel(st2[0], y.float().sum(dim=(0, 2, 3))) < 2e-2
+        gy = torch.randn_like(yr).to(BF, memory_format=CL)
+        dx = cv.conv2d_dgrad(gy, cv.transpose_w(w), x.shape, (st, st), (pd, pd))
+        dxr = torch.nn.grad.conv2d_input(x.shape, w.float(), gy.float(), stride=st, padding=pd)
+        assert _rel(dx, dxr) < 1e-2
+    finally:
+        C_.set_conv_impl(old)
+
+
 def test_linear_as_conv1x1():
     from bigdl_amd.ops import conv as cv
 
