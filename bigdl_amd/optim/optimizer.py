@@ -171,6 +171,8 @@ class Optimizer:
         pass
 
     # ---------------------------------------------------------------- core loop
+    _overlap = False
+
     def _optim_method(self):
         if len(self.optimMethods) != 1:
             raise NotImplementedError("per-submodule optim methods: use ParallelOptimizer")
@@ -178,7 +180,7 @@ class Optimizer:
 
     def _make_step(self, comm=None):
         return TrainStep(self.model, self.criterion, self._optim_method(), device=self.device, comm=comm,
-                         compress=self.compress)
+                         compress=self.compress, overlap=self._overlap)
 
     def _clip(self, step):
         g = step.g_shard
@@ -263,12 +265,16 @@ class Optimizer:
             t1 = time.perf_counter()
             step.zero_grad()
             loss = step.forward_backward(batch.getInput(), batch.getTarget())
-            step.comm.reduce_scatter_gradients(step.g, out=step.g_shard)
-            if self.constantClip is not None or self.l2NormClip is not None:
+            if step.bucketed is not None:          # ParallelOptimizer: buckets already in flight
                 self._clip(step)
-            om.optimize(lambda _: (loss, step.g_shard), step.w_shard)
-            if world > 1:
-                step.comm.all_gather_weights(step.w16 if step.w16 is not None else step.w)
+                step.bucketed.update(loss)
+            else:
+                step.comm.reduce_scatter_gradients(step.g, out=step.g_shard)
+                if self.constantClip is not None or self.l2NormClip is not None:
+                    self._clip(step)
+                om.optimize(lambda _: (loss, step.g_shard), step.w_shard)
+                if world > 1:
+                    step.comm.all_gather_weights(step.w16 if step.w16 is not None else step.w)
             self.metrics.add("computing time", time.perf_counter() - t1)
             records = batch.size() * world
             pending.append((st["neval"], loss.detach() if torch.is_tensor(loss) else torch.tensor(float(loss)),
@@ -381,6 +387,20 @@ class DistriOptimizer(Optimizer):
 
     def _epoch_size(self):
         return self.dataset.size()
+
+
+class ParallelOptimizer(DistriOptimizer):
+    """Data-parallel training with layer-wise bucketed gradient reduce-scatter overlapped with backward
+    (reference ParallelOptimizer.scala:42-791; mechanism in parallel/bucketed.py)."""
+
+    _overlap = True
+
+    def __new__(cls, *args, **kw):
+        return object.__new__(cls)
+
+    def _clip(self, step):
+        if self.constantClip is not None or self.l2NormClip is not None:
+            raise NotImplementedError("gradient clipping needs the whole gradient; use DistriOptimizer")
 
 
 def create(model, training_set, criterion, end_trigger=None, batch_size=32, optim_method=None, **kw):

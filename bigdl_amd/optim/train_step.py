@@ -60,7 +60,8 @@ def fold_regularizers(model, total, device):
 
 
 class TrainStep:
-    def __init__(self, model, criterion, optim_method, device=None, comm=None, compress=None, fuse=True):
+    def __init__(self, model, criterion, optim_method, device=None, comm=None, compress=None, fuse=True,
+                 overlap=None, bucket_elems=8 << 20):
         from ..utils.engine import Engine
 
         self.device = torch.device(device) if device is not None else Engine.device()
@@ -100,6 +101,17 @@ class TrainStep:
             optim_method.attach_shadow(self.comm.shard_of(self.w16))
         self.loss = None
         self._graph = None
+        # ParallelOptimizer-style bucketed reduce-scatter overlapped with backward (parallel/bucketed.py)
+        from ..nn.containers import Sequential
+
+        if overlap is None:
+            overlap = self.comm.world > 1 and isinstance(model, Sequential) and compress is None
+        self.bucketed = None
+        if overlap and self.comm.world > 1:
+            from ..parallel.bucketed import BucketedGradSync
+
+            self.bucketed = BucketedGradSync(model, self.w, self.g, self.w16, optim_method, self.comm.world,
+                                             self.comm.rank, self.comm.group, bucket_elems, total)
 
     def zero_grad(self):
         self.g.zero_()
@@ -110,10 +122,16 @@ class TrainStep:
         out = m.forward(x)
         loss = c.forward(out, y)
         gout = c.backward(out, y)
-        m.backward(x, gout)
+        if self.bucketed is not None:
+            self.bucketed.backward(x, gout)
+        else:
+            m.backward(x, gout)
         return loss
 
     def sync_and_update(self, loss):
+        if self.bucketed is not None:
+            self.bucketed.update(loss)
+            return
         self.comm.reduce_scatter_gradients(self.g, out=self.g_shard)
         self.optim.optimize(lambda _: (loss, self.g_shard), self.w_shard)
         if self.comm.world > 1:

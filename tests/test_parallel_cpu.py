@@ -70,3 +70,55 @@ def test_allreduce_parameter_shards():
     assert torch.allclose(res[0][1], full[:shard]) and torch.allclose(res[1][1], full[shard:])
     expect = torch.cat([torch.full((shard,), 10.0), torch.full((shard,), 20.0)])  # broadcast rank0 weights (0)
     assert torch.equal(res[0][0], expect) and torch.equal(res[1][0], expect)
+
+
+def _bucketed_job(rank, world, data, iters, bucket):
+    import torch as _t
+    from bigdl_amd import nn as _nn
+    from bigdl_amd import optim as _O
+    from bigdl_amd.optim.train_step import TrainStep
+    from bigdl_amd.utils.random_generator import RNG
+
+    RNG.setSeed(5)
+    model = _nn.Sequential().add(_nn.Linear(6, 16)).add(_nn.Tanh()) \
+        .add(_nn.Sequential().add(_nn.Linear(16, 16)).add(_nn.ReLU())).add(_nn.Linear(16, 2))
+    step = TrainStep(model, _nn.MSECriterion(), _O.SGD(0.05, momentum=0.9, dampening=0.0), device="cpu",
+                     overlap=True, bucket_elems=bucket)
+    assert step.bucketed is not None and len(step.bucketed.bounds) >= 2
+    X, Y = data
+    n = X.shape[0] // world
+    for i in range(iters):
+        step.step(X[rank * n:(rank + 1) * n], Y[rank * n:(rank + 1) * n])
+    w, _ = model.getParameters()
+    return w[:model._flat_total].clone()
+
+
+def _plain_job(rank, world, data, iters):
+    from bigdl_amd import nn as _nn
+    from bigdl_amd import optim as _O
+    from bigdl_amd.optim.train_step import TrainStep
+    from bigdl_amd.utils.random_generator import RNG
+
+    RNG.setSeed(5)
+    model = _nn.Sequential().add(_nn.Linear(6, 16)).add(_nn.Tanh()) \
+        .add(_nn.Sequential().add(_nn.Linear(16, 16)).add(_nn.ReLU())).add(_nn.Linear(16, 2))
+    step = TrainStep(model, _nn.MSECriterion(), _O.SGD(0.05, momentum=0.9, dampening=0.0), device="cpu",
+                     overlap=False)
+    X, Y = data
+    n = X.shape[0] // world
+    for i in range(iters):
+        step.step(X[rank * n:(rank + 1) * n], Y[rank * n:(rank + 1) * n])
+    step.comm.all_gather_weights(step.w)
+    w, _ = model.getParameters()
+    return w[:model._flat_total].clone()
+
+
+def test_bucketed_overlap_equals_plain_zero1():
+    """ParallelOptimizer-style bucketed reduce-scatter during backward == one post-backward reduce-scatter."""
+    g = torch.Generator().manual_seed(0)
+    X = torch.randn(16, 6, generator=g)
+    Y = torch.randn(16, 2, generator=g)
+    a = run_distributed(_bucketed_job, 2, ((X, Y), 4, 128))
+    b = run_distributed(_plain_job, 2, ((X, Y), 4))
+    assert torch.allclose(a[0], a[1], atol=1e-6)
+    assert torch.allclose(a[0], b[0], atol=1e-5)
