@@ -35,6 +35,31 @@ def all_module_classes():
     return dict(_REGISTRY)
 
 
+def _detach_nonleaf(v):
+    if isinstance(v, torch.Tensor):
+        return v.detach() if v.grad_fn is not None else v
+    if isinstance(v, Table):
+        if not any(isinstance(x, (torch.Tensor, Table)) and _has_nonleaf(x) for _, x in v.items()):
+            return v
+        t = Table()
+        for k, x in v.items():
+            t[k] = _detach_nonleaf(x)
+        return t
+    if isinstance(v, (list, tuple)) and any(_has_nonleaf(x) for x in v):
+        return type(v)(_detach_nonleaf(x) for x in v) if isinstance(v, list) else tuple(_detach_nonleaf(x) for x in v)
+    return v
+
+
+def _has_nonleaf(v):
+    if isinstance(v, torch.Tensor):
+        return v.grad_fn is not None
+    if isinstance(v, Table):
+        return any(_has_nonleaf(x) for _, x in v.items())
+    if isinstance(v, (list, tuple)):
+        return any(_has_nonleaf(x) for x in v)
+    return False
+
+
 class _RecordInit(type):
     """Records the constructor arguments of every module (used by the serializer and cloneModule)."""
 
@@ -442,8 +467,8 @@ class AbstractModule(metaclass=_RecordInit):
                 setattr(new, k, None if k != "_w16" else {})
             elif isinstance(v, torch.Tensor):
                 setattr(new, k, v.detach().clone(memory_format=torch.preserve_format))
-            else:
-                setattr(new, k, copy.deepcopy(v, memo))
+            else:   # cached autograd activations (non-leaf tensors) are copied as plain data
+                setattr(new, k, copy.deepcopy(_detach_nonleaf(v), memo))
         new._w16_managed = False
         return new
 

@@ -230,6 +230,55 @@ void lstm_cell_bwd(const Tensor& act, const OptT& c_prev, const Tensor& c, const
                       mf(dgates, "dgates"), omf(dc_prev, "dc_prev"), B, H, stream());
 }
 
+// int8 path (csrc/quant.hip)
+void quantize_act(const Tensor& x, const Tensor& q, const Tensor& amax, const Tensor& scale, int64_t N, int64_t P,
+                  int64_t C, int64_t Cp) {
+  TORCH_CHECK(x.is_cuda() && x.is_contiguous(), "quantize_act: x must be a contiguous device tensor");
+  const bool bf = x.scalar_type() == at::kBFloat16;
+  TORCH_CHECK(bf || x.scalar_type() == at::kFloat, "quantize_act: x must be bf16 or fp32");
+  TORCH_CHECK(x.numel() == N * P * C, "quantize_act: x size");
+  TORCH_CHECK(q.scalar_type() == at::kChar && q.is_contiguous() && q.numel() == N * P * Cp && Cp % 16 == 0 && Cp >= C,
+              "quantize_act: q must be int8 [N][P][Cp], Cp % 16 == 0");
+  TORCH_CHECK(amax.numel() >= N && scale.numel() >= N && amax.scalar_type() == at::kFloat, "quantize_act: amax/scale");
+  bigdl_quantize_act(x.data_ptr(), bf ? 1 : 0, q.data_ptr<int8_t>(), amax.data_ptr<float>(), scale.data_ptr<float>(),
+                     (int)N, P, (int)C, (int)Cp, stream());
+}
+
+void conv_i8(const Tensor& src, const Tensor& wt, const Tensor& out, const OptT& bias, const Tensor& xscale,
+             const Tensor& wscale, std::vector<int64_t> geo, std::vector<int64_t> taps, bool relu) {
+  TORCH_CHECK(geo.size() == 17, "conv_i8: bad geometry");
+  TORCH_CHECK(src.scalar_type() == at::kChar && wt.scalar_type() == at::kChar && src.is_cuda() && wt.is_cuda() &&
+                  src.is_contiguous() && wt.is_contiguous(), "conv_i8: src/wt must be contiguous int8 device tensors");
+  const bool f32 = out.scalar_type() == at::kFloat;
+  TORCH_CHECK(f32 || out.scalar_type() == at::kBFloat16, "conv_i8: out bf16 or fp32");
+  TORCH_CHECK(taps.size() % 3 == 0 && !taps.empty() && taps.size() / 3 <= CONV_MAX_TAPS, "conv_i8: bad taps");
+  ConvArgs a;
+  a.src = reinterpret_cast<const uint16_t*>(src.data_ptr<int8_t>());
+  a.wt = reinterpret_cast<const uint16_t*>(wt.data_ptr<int8_t>());
+  a.out = reinterpret_cast<uint16_t*>(out.data_ptr());
+  a.bias = ocf(bias, "bias"); a.stats = nullptr; a.addend = nullptr;
+  a.Nb = geo[0]; a.Hs = geo[1]; a.Ws = geo[2]; a.Cs = geo[3]; a.OH = geo[4]; a.OW = geo[5];
+  a.mul_h = geo[6]; a.mul_w = geo[7]; a.ldw = geo[8]; a.Ncol = geo[9]; a.ldo = geo[10];
+  a.OHo = geo[11]; a.OWo = geo[12]; a.omul_h = geo[13]; a.omul_w = geo[14]; a.ooff_h = geo[15]; a.ooff_w = geo[16];
+  a.ntaps = (int)(taps.size() / 3);
+  a.Kdim = a.ntaps * a.Cs;
+  a.M = a.Nb * a.OH * a.OW;
+  a.ident_out = 1;
+  a.relu = relu ? 1 : 0;
+  int max_tk = 0;
+  for (int t = 0; t < a.ntaps; ++t) {
+    a.tap_h[t] = (short)taps[3 * t]; a.tap_w[t] = (short)taps[3 * t + 1]; a.tap_k[t] = (short)taps[3 * t + 2];
+    max_tk = std::max(max_tk, (int)a.tap_k[t]);
+  }
+  TORCH_CHECK(src.numel() >= (int64_t)a.Nb * a.Hs * a.Ws * a.Cs, "conv_i8: src too small");
+  TORCH_CHECK(wt.numel() >= (int64_t)(a.Ncol - 1) * a.ldw + (int64_t)(max_tk + 1) * a.Cs, "conv_i8: weight too small");
+  TORCH_CHECK(out.numel() >= (int64_t)(a.M - 1) * a.ldo + a.Ncol, "conv_i8: out too small");
+  TORCH_CHECK(xscale.numel() >= a.Nb && wscale.numel() >= a.Ncol && xscale.scalar_type() == at::kFloat &&
+                  wscale.scalar_type() == at::kFloat, "conv_i8: scales");
+  const int rc = bigdl_conv_i8(&a, xscale.data_ptr<float>(), wscale.data_ptr<float>(), f32 ? 1 : 0, stream());
+  TORCH_CHECK(rc == 0, "conv_i8: unsupported shape (channels must be a multiple of 16)");
+}
+
 void image_augment(const Tensor& src, const Tensor& params, const Tensor& out, std::vector<double> mean,
                    std::vector<double> std, bool rgb) {
   TORCH_CHECK(src.is_cuda() && src.scalar_type() == at::kByte && src.dim() == 4 && src.size(3) == 3 &&
@@ -294,6 +343,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("lstm_cell_fwd", &lstm_cell_fwd);
   m.def("lstm_cell_bwd", &lstm_cell_bwd);
   m.def("image_augment", &image_augment);
+  m.def("quantize_act", &quantize_act);
+  m.def("conv_i8", &conv_i8);
   m.def("set_conv_impl", &bigdl_set_conv_impl);
   m.def("get_conv_impl", &bigdl_get_conv_impl);
   m.attr("arch") = "gfx950";

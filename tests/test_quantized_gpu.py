@@ -1,0 +1,104 @@
+"""Int8 HIP kernels (csrc/quant.hip) vs exact integer / CPU-emulated references (GPU only)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from bigdl_amd import nn
+from bigdl_amd.ops import native
+from bigdl_amd.quantized import QuantizedLinear, QuantizedSpatialConvolution, quantize_per_sample_ref
+from bigdl_amd.quantized.modules import quantize_act_gpu
+from bigdl_amd.utils.random_generator import RNG
+
+pytestmark = pytest.mark.gpu
+CL = torch.channels_last
+
+
+def _rel(a, b):
+    return float((a.float() - b.float()).norm() / (b.float().norm() + 1e-12))
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_quantize_act_matches_reference(dtype):
+    torch.manual_seed(0)
+    x = torch.randn(3, 5, 7, 24).to(dtype)
+    q, s = quantize_act_gpu(x.cuda(), 24, 32)
+    qr, sr = quantize_per_sample_ref(x)
+    assert torch.equal(q.cpu()[..., :24].reshape(3, 5, 7, 24), qr)
+    assert torch.all(q.cpu()[..., 24:] == 0)
+    assert torch.allclose(s.cpu(), sr)
+
+
+# N, C, H, W, K, R, S, stride, pad, dil
+I8_CASES = [
+    (2, 16, 9, 9, 24, 3, 3, 1, 1, 1),
+    (3, 64, 14, 14, 200, 1, 1, 1, 0, 1),
+    (2, 48, 11, 13, 64, 3, 3, 2, 1, 1),
+    (1, 32, 12, 12, 16, 3, 3, 1, 2, 2),
+    (4, 128, 7, 7, 130, 3, 3, 1, 1, 1),
+    (2, 16, 20, 20, 8, 7, 7, 2, 3, 1),
+]
+
+
+@pytest.mark.parametrize("case", I8_CASES)
+def test_conv_i8_exact_integer(case):
+    """Scales are forced to exactly 1 (row maxima 127), so the fp32 output must equal the integer conv."""
+    from bigdl_amd.ops.conv import _fwd_taps, out_size
+
+    N, C, H, W, K, R, S, st, pd, dl = case
+    g = torch.Generator().manual_seed(1)
+    x = torch.randint(-127, 128, (N, H, W, C), generator=g, dtype=torch.int8)
+    w = torch.randint(-127, 128, (K, R, S, C), generator=g, dtype=torch.int8)
+    OH, OW = out_size(H, R, st, pd, dl), out_size(W, S, st, pd, dl)
+    ref = F.conv2d(x.permute(0, 3, 1, 2).double(), w.permute(0, 3, 1, 2).double(), None, st, pd, dl)
+    ref = ref.permute(0, 2, 3, 1).reshape(N * OH * OW, K)
+    bias = torch.arange(K, dtype=torch.float32)
+    out = torch.full((N * OH * OW, K), float("nan"), device="cuda")
+    ones_x, ones_w = torch.ones(N, device="cuda"), torch.ones(K, device="cuda")
+    geo = [N, H, W, C, OH, OW, st, st, R * S * C, K, K, OH, OW, 1, 1, 0, 0]
+    native.get().conv_i8(x.cuda(), w.cuda(), out, bias.cuda(), ones_x, ones_w, geo,
+                         _fwd_taps(R, S, pd, pd, dl, dl), False)
+    torch.cuda.synchronize()
+    assert torch.equal(out.cpu().double(), ref + bias.double())
+
+
+def test_quantized_linear_gpu_matches_cpu():
+    RNG.setSeed(2)
+    f = nn.Linear(300, 77)
+    q = QuantizedLinear(300, 77, initWeight=f.weight, initBias=f.bias)
+    x = torch.randn(33, 300)
+    y_cpu = q.forward(x).clone()
+    q.cuda()
+    y = q.forward(x.cuda())
+    assert y.dtype == torch.float32
+    assert torch.allclose(y.cpu(), y_cpu, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("groups", [1, 2])
+def test_quantized_conv_gpu_matches_cpu(groups):
+    RNG.setSeed(4)
+    f = nn.SpatialConvolution(32, 64, 3, 3, 1, 1, 1, 1, nGroup=groups)
+    q = QuantizedSpatialConvolution(32, 64, 3, 3, 1, 1, 1, 1, nGroup=groups, initWeight=f.weight, initBias=f.bias)
+    q.fuse_relu = True
+    x = torch.randn(4, 32, 15, 15)
+    y_cpu = q.forward(x).clone()
+    q.cuda()
+    y = q.forward(x.cuda().contiguous(memory_format=CL))
+    assert y.dtype == torch.bfloat16 and y.is_contiguous(memory_format=CL)
+    assert _rel(y.cpu(), y_cpu) < 1e-2
+
+
+def test_quantized_resnet_block_model_gpu():
+    RNG.setSeed(6)
+    seq = nn.Sequential()
+    seq.add(nn.SpatialConvolution(3, 32, 3, 3, 1, 1, 1, 1)).add(nn.SpatialBatchNormalization(32)).add(nn.ReLU())
+    seq.add(nn.SpatialConvolution(32, 64, 3, 3, 2, 2, 1, 1)).add(nn.SpatialBatchNormalization(64)).add(nn.ReLU())
+    seq.add(nn.SpatialAveragePooling(8, 8, 1, 1)).add(nn.Reshape([64])).add(nn.Linear(64, 10))
+    seq.evaluate()
+    x = torch.randn(8, 3, 16, 16)
+    ref = seq.forward(x).clone()
+    q = seq.quantize()
+    y_cpu = q.forward(x).clone()
+    assert _rel(y_cpu, ref) < 0.05
+    q.cuda()
+    y = q.forward(x.cuda())
+    assert _rel(y.float().cpu(), y_cpu) < 2e-2
