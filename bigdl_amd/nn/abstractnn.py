@@ -142,6 +142,8 @@ class AbstractModule(metaclass=_RecordInit):
     # ------------------------------------------------------------------ forward / backward
     def forward(self, input):
         t0 = time.perf_counter_ns()
+        if getattr(input, "_is_bigdl_tensor", False):     # bigdl_amd.tensor.Tensor -> its torch tensor
+            input = input._t
         if self._sync is not None:
             self._sync.before_forward(self)
         try:
@@ -159,6 +161,10 @@ class AbstractModule(metaclass=_RecordInit):
 
     def backward(self, input, gradOutput):
         t0 = time.perf_counter_ns()
+        if getattr(input, "_is_bigdl_tensor", False):
+            input = input._t
+        if getattr(gradOutput, "_is_bigdl_tensor", False):
+            gradOutput = gradOutput._t
         self.gradInput = self.updateGradInput(input, gradOutput)
         if not self._frozen:
             self.accGradParameters(input, gradOutput)
@@ -659,10 +665,14 @@ class AbstractCriterion(metaclass=_RecordInit):
         self._device = torch.device("cpu")
 
     def forward(self, input, target):
+        input = input._t if getattr(input, "_is_bigdl_tensor", False) else input
+        target = target._t if getattr(target, "_is_bigdl_tensor", False) else target
         self.output = self.updateOutput(input, target)
         return self.output
 
     def backward(self, input, target):
+        input = input._t if getattr(input, "_is_bigdl_tensor", False) else input
+        target = target._t if getattr(target, "_is_bigdl_tensor", False) else target
         self.gradInput = self.updateGradInput(input, target)
         return self.gradInput
 
