@@ -279,6 +279,56 @@ void conv_i8(const Tensor& src, const Tensor& wt, const Tensor& out, const OptT&
   TORCH_CHECK(rc == 0, "conv_i8: unsupported shape (channels must be a multiple of 16)");
 }
 
+// detection (csrc/detection.hip)
+static void check_f32(const Tensor& t, const char* n) {
+  TORCH_CHECK(t.is_cuda() && t.is_contiguous() && t.scalar_type() == at::kFloat, n, ": contiguous fp32 device tensor");
+}
+
+int64_t nms(const Tensor& boxes_sorted, double thresh, bool normalized, int64_t max_keep, const Tensor& keep,
+            const Tensor& count) {
+  check_f32(boxes_sorted, "nms boxes");
+  const int64_t n = boxes_sorted.numel() / 4;
+  TORCH_CHECK(boxes_sorted.dim() == 2 && boxes_sorted.size(1) == 4, "nms: boxes must be [n, 4]");
+  TORCH_CHECK(keep.scalar_type() == at::kInt && keep.numel() >= n && count.scalar_type() == at::kInt &&
+                  count.numel() >= 1, "nms: keep / count int32 buffers");
+  const int64_t words = (n + 63) / 64;
+  TORCH_CHECK(words <= 256, "nms: at most 16384 boxes");
+  auto ws = at::empty({std::max<int64_t>(n * words, 1)}, boxes_sorted.options().dtype(at::kLong));
+  const int rc = bigdl_nms(boxes_sorted.data_ptr<float>(), (int)n, (float)thresh, normalized ? 1 : 0, (int)max_keep,
+                           reinterpret_cast<unsigned long long*>(ws.data_ptr<int64_t>()), keep.data_ptr<int>(),
+                           count.data_ptr<int>(), stream());
+  TORCH_CHECK(rc == 0, "nms failed");
+  return n;
+}
+
+void roi_align_fwd(const Tensor& x, const Tensor& rois, const Tensor& out, double scale, int64_t sampling) {
+  check_f32(x, "roi_align x"); check_f32(rois, "roi_align rois"); check_f32(out, "roi_align out");
+  TORCH_CHECK(x.dim() == 4 && rois.dim() == 2 && (rois.size(1) == 4 || rois.size(1) == 5) && out.dim() == 4 &&
+                  out.size(0) == rois.size(0) && out.size(1) == x.size(1), "roi_align: shapes");
+  bigdl_roi_align_fwd(x.data_ptr<float>(), rois.data_ptr<float>(), out.data_ptr<float>(), (int)rois.size(0),
+                      (int)rois.size(1), (int)x.size(1), (int)x.size(2), (int)x.size(3), (int)out.size(2),
+                      (int)out.size(3), (float)scale, (int)sampling, stream());
+}
+
+void roi_pool_fwd(const Tensor& x, const Tensor& rois, const Tensor& out, const Tensor& argmax, double scale) {
+  check_f32(x, "roi_pool x"); check_f32(rois, "roi_pool rois"); check_f32(out, "roi_pool out");
+  TORCH_CHECK(x.dim() == 4 && rois.dim() == 2 && rois.size(1) == 5 && out.dim() == 4 && out.size(0) == rois.size(0) &&
+                  out.size(1) == x.size(1) && argmax.scalar_type() == at::kInt && argmax.numel() == out.numel(),
+              "roi_pool: shapes");
+  bigdl_roi_pool_fwd(x.data_ptr<float>(), rois.data_ptr<float>(), out.data_ptr<float>(), argmax.data_ptr<int>(),
+                     (int)rois.size(0), (int)x.size(1), (int)x.size(2), (int)x.size(3), (int)out.size(2),
+                     (int)out.size(3), (float)scale, stream());
+}
+
+void roi_pool_bwd(const Tensor& gy, const Tensor& argmax, const Tensor& rois, const Tensor& gx) {
+  check_f32(gy, "roi_pool gy"); check_f32(rois, "roi_pool rois"); check_f32(gx, "roi_pool gx");
+  TORCH_CHECK(gy.dim() == 4 && gx.dim() == 4 && argmax.numel() == gy.numel() && rois.size(0) == gy.size(0),
+              "roi_pool_bwd: shapes");
+  bigdl_roi_pool_bwd(gy.data_ptr<float>(), argmax.data_ptr<int>(), rois.data_ptr<float>(), gx.data_ptr<float>(),
+                     (int)gy.size(0), (int)gx.size(1), (int)gx.size(2), (int)gx.size(3), (int)gy.size(2),
+                     (int)gy.size(3), stream());
+}
+
 void image_augment(const Tensor& src, const Tensor& params, const Tensor& out, std::vector<double> mean,
                    std::vector<double> std, bool rgb) {
   TORCH_CHECK(src.is_cuda() && src.scalar_type() == at::kByte && src.dim() == 4 && src.size(3) == 3 &&
@@ -345,6 +395,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("image_augment", &image_augment);
   m.def("quantize_act", &quantize_act);
   m.def("conv_i8", &conv_i8);
+  m.def("nms", &nms);
+  m.def("roi_align_fwd", &roi_align_fwd);
+  m.def("roi_pool_fwd", &roi_pool_fwd);
+  m.def("roi_pool_bwd", &roi_pool_bwd);
   m.def("set_conv_impl", &bigdl_set_conv_impl);
   m.def("get_conv_impl", &bigdl_get_conv_impl);
   m.attr("arch") = "gfx950";

@@ -112,4 +112,15 @@ int bigdl_get_conv_impl();
 // params: int32 [N][3] = (y0, x0, flip). Output fp32 NCHW [N, 3, OH, OW] or bf16 NHWC [N, OH, OW, 3].
 void bigdl_image_augment(const uint8_t* src, const int* params, void* out, int N, int H, int W, int OH, int OW,
                          const float* mean, const float* inv_std, int rgb, int nhwc_bf16, hipStream_t st);
+
+// Detection (csrc/detection.hip): greedy NMS over score-sorted boxes (mask_ws: n * ceil(n/64) uint64),
+// RoiAlign forward, RoiPooling forward (argmax) / backward.
+int bigdl_nms(const float* boxes_sorted, int n, float thresh, int normalized, int max_keep,
+              unsigned long long* mask_ws, int* keep_out, int* count_out, hipStream_t st);
+int bigdl_roi_align_fwd(const float* x, const float* rois, float* out, int R, int rcols, int C, int H, int W,
+                        int PH, int PW, float scale, int sampling, hipStream_t st);
+int bigdl_roi_pool_fwd(const float* x, const float* rois, float* out, int* argmax, int R, int C, int H, int W,
+                       int PH, int PW, float scale, hipStream_t st);
+int bigdl_roi_pool_bwd(const float* gy, const int* argmax, const float* rois, float* gx, int R, int C, int H, int W,
+                       int PH, int PW, hipStream_t st);
 }
