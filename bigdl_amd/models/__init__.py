@@ -6,3 +6,4 @@ from .lenet import LeNet5, LeNet5Graph  # noqa: F401
 from .resnet import ResNet, ResNet50, ResNetGraph  # noqa: F401
 from .rnn import PTBModel, SimpleRNN  # noqa: F401
 from .vgg import Vgg_16, Vgg_16Graph, Vgg_19, Vgg_19Graph, VggForCifar10, VggForCifar10Graph  # noqa: F401
+from .maskrcnn import MaskRCNN, MaskRCNNParams  # noqa: F401
