@@ -16,6 +16,8 @@ from .shape_ops import *  # noqa: F401,F403
 from .table_ops import *  # noqa: F401,F403
 from .transformer import *  # noqa: F401,F403
 from .detection import *  # noqa: F401,F403
+from .penalty import *  # noqa: F401,F403
+from .tree_lstm import *  # noqa: F401,F403
 from ..optim.regularizer import L1L2Regularizer, L1Regularizer, L2Regularizer  # noqa: F401
 from ..utils.table import T, Table  # noqa: F401
 from .module import Module  # noqa: F401

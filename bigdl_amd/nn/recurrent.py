@@ -22,7 +22,7 @@ reverse sweep instead of T small ones.
 import torch
 import torch.nn.functional as F
 
-__all__ = ["Cell", "RnnCell", "LSTM", "LSTMPeephole", "GRU", "ConvLSTMPeephole", "ConvLSTMPeephole3D", "MultiRNNCell",
+__all__ = ["Cell", "RnnCell", "RNN", "LSTM", "LSTMPeephole", "GRU", "ConvLSTMPeephole", "ConvLSTMPeephole3D", "MultiRNNCell",
            "Recurrent", "RecurrentDecoder", "BiRecurrent", "TimeDistributed"]
 
 from .. import ops
@@ -785,3 +785,6 @@ class TimeDistributed(Container):
         gi = self.layer.backward(self._fold(input), self._gfold(input, gradOutput))
         self.gradInput = gi.reshape(input.shape)
         return self.gradInput
+
+
+RNN = RnnCell   # reference file S/nn/RNN.scala defines RnnCell
