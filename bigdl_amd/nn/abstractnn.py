@@ -22,8 +22,14 @@ from ..utils.table import Table
 _REGISTRY = {}
 
 
+def module_key(cls):
+    """Registry / serialization key of a module class. Keras-style layers share names with torch-style ones
+    (Dense vs Linear is fine, but LSTM, Sequential, Reshape, ... collide), so they are namespaced."""
+    return ("keras." if cls.__module__.startswith("bigdl_amd.keras") else "") + cls.__name__
+
+
 def register(cls):
-    _REGISTRY[cls.__name__] = cls
+    _REGISTRY[module_key(cls)] = cls
     return cls
 
 
@@ -72,7 +78,7 @@ class _RecordInit(type):
     def __init__(cls, name, bases, ns):
         super().__init__(name, bases, ns)
         if not name.startswith("_"):
-            _REGISTRY[name] = cls
+            _REGISTRY[module_key(cls)] = cls
 
 
 def to_device_tensor(t, device):

@@ -99,6 +99,25 @@ class SpatialConvolution(TensorModule):
             return ph, pw
         return self.padH, self.padW
 
+    def _same_extra(self, H, W):
+        """Extra bottom/right zero rows when TF-style SAME padding is asymmetric (pad total odd)."""
+        if not (self.padW == -1 and self.padH == -1):
+            return 0, 0
+        bh, ah = _same_pad(H, self.kernelH, self.strideH, self.dilationH)
+        bw, aw = _same_pad(W, self.kernelW, self.strideW, self.dilationW)
+        return ah - bh, aw - bw
+
+    def _prep(self, x):
+        """(input padded for asymmetric SAME, symmetric pads, extra rows, extra cols)."""
+        H, W = x.shape[2], x.shape[3]
+        ph, pw = self._pads(H, W)
+        eh, ew = self._same_extra(H, W)
+        if eh or ew:
+            x = F.pad(x, (0, ew, 0, eh))
+            if x.is_cuda:
+                x = x.contiguous(memory_format=CL)
+        return x, ph, pw, eh, ew
+
     def _nchw(self, x):
         if self.format == "NHWC":
             return x.permute(0, 3, 1, 2)
@@ -115,7 +134,7 @@ class SpatialConvolution(TensorModule):
         squeeze = x.dim() == 3
         if squeeze:
             x = x.unsqueeze(0)
-        ph, pw = self._pads(x.shape[2], x.shape[3])
+        x, ph, pw, _, _ = self._prep(x)
         if x.is_cuda and self.nGroup == 1:
             y = self._fwd_gpu(x, ph, pw)
         elif x.is_cuda:
@@ -173,7 +192,8 @@ class SpatialConvolution(TensorModule):
         squeeze = x.dim() == 3
         if squeeze:
             x, gy = x.unsqueeze(0), gy.unsqueeze(0)
-        ph, pw = self._pads(x.shape[2], x.shape[3])
+        H, W = x.shape[2], x.shape[3]
+        x, ph, pw, eh, ew = self._prep(x)
         if gy.is_cuda:
             gy = self._relu_mask(gy)
             gi = self._dgrad_gpu(x, gy, ph, pw)
@@ -181,6 +201,10 @@ class SpatialConvolution(TensorModule):
             gy = self._relu_mask(gy)
             gi = torch.nn.grad.conv2d_input(x.shape, self.weight, gy.float(), (self.strideH, self.strideW),
                                             (ph, pw), (self.dilationH, self.dilationW), self.nGroup)
+        if eh or ew:
+            gi = gi[:, :, :H, :W]
+            if gi.is_cuda:
+                gi = gi.contiguous(memory_format=CL)
         if squeeze:
             gi = gi.squeeze(0)
         return self._fmt_out(gi)
@@ -228,7 +252,7 @@ class SpatialConvolution(TensorModule):
         gy = self._nchw(gradOutput)
         if x.dim() == 3:
             x, gy = x.unsqueeze(0), gy.unsqueeze(0)
-        ph, pw = self._pads(x.shape[2], x.shape[3])
+        x, ph, pw, _, _ = self._prep(x)
         if gy.is_cuda:
             gy = self._relu_mask(gy) if self.fuse_relu and not getattr(self, "_masked_cached", False) else gy
             self._wgrad_gpu(x, gy, ph, pw)

@@ -413,9 +413,20 @@ class Highway(AutogradModule):
         y = F.linear(x.float(), self.weight, self.bias)
         t = torch.sigmoid(y[:, : self.size])
         h = y[:, self.size:]
-        h = torch.tanh(h) if self.activation is None else self.activation.fn(h)
+        h = torch.tanh(h) if self.activation is None else _act_fn(self.activation, h)
         return t * h + (1 - t) * x.float()
 
 
 __all__ = ["Linear", "SparseLinear", "Bilinear", "LookupTable", "LookupTableSparse", "MM", "MV", "DotProduct",
            "CosineDistance", "PairwiseDistance", "Cosine", "Euclidean", "CrossProduct", "Maxout", "Highway"]
+
+
+def _act_fn(m, x):
+    """Differentiable application of an activation module inside an autograd-derived layer."""
+    if hasattr(m, "fn"):
+        return m.fn(x)
+    name = type(m).__name__
+    fns = {"ReLU": torch.relu, "Tanh": torch.tanh, "Sigmoid": torch.sigmoid, "Identity": lambda t: t}
+    if name in fns:
+        return fns[name](x)
+    return m.updateOutput(x)

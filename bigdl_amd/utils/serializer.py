@@ -14,6 +14,8 @@ import os
 
 import torch
 
+from ..nn.abstractnn import module_key
+
 from ..utils.table import Table
 
 FORMAT_VERSION = 1
@@ -51,7 +53,7 @@ def _enc(v, ctx):
     if isinstance(v, AbstractModule):
         return {"__module__": encode_module(v, ctx)}
     if isinstance(v, AbstractCriterion):
-        return {"__criterion__": type(v).__name__, "args": _enc_args(v, ctx)}
+        return {"__criterion__": module_key(type(v)), "args": _enc_args(v, ctx)}
     if isinstance(v, (list, tuple)):
         return {"__seq__": [_enc(x, ctx) for x in v], "tuple": isinstance(v, tuple)}
     if isinstance(v, dict):
@@ -72,7 +74,7 @@ def _enc_args(m, ctx):
 def encode_module(m, ctx):
     from ..nn.graph import Graph
 
-    d = {"class": type(m).__name__, "init": _enc_args(m, ctx), "name": m._name, "train": m.train,
+    d = {"class": module_key(type(m)), "init": _enc_args(m, ctx), "name": m._name, "train": m.train,
          "frozen": m._frozen}
     d["attrs"] = {k: v for k, v in vars(m).items()
                   if not k.startswith("_") and k not in _SKIP_ATTRS and _is_simple(v)}

@@ -81,7 +81,10 @@ LAYERS = [
 
 @pytest.mark.parametrize("name,mk,inp", LAYERS, ids=[l[0] for l in LAYERS])
 def test_layer_gradients(name, mk, inp):
+    from bigdl_amd.utils.random_generator import RNG
+
     torch.manual_seed(1)
+    RNG.setSeed(1)
     m = mk()
     x = inp()
     gc = GradientChecker(1e-2, 3e-2)
