@@ -179,7 +179,8 @@ def _escape(s):
 
 def _scalar(tok, kind):
     if tok[0] in "\"'":
-        return _unescape(tok[1:-1])
+        v = _unescape(tok[1:-1])
+        return v.encode("latin-1") if kind == "bytes" else v
     if kind in ("float", "double"):
         return float(tok)
     if kind in _VARINT_KINDS and kind not in ("enum", "bool"):

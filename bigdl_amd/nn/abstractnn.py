@@ -25,7 +25,12 @@ _REGISTRY = {}
 def module_key(cls):
     """Registry / serialization key of a module class. Keras-style layers share names with torch-style ones
     (Dense vs Linear is fine, but LSTM, Sequential, Reshape, ... collide), so they are namespaced."""
-    return ("keras." if cls.__module__.startswith("bigdl_amd.keras") else "") + cls.__name__
+    mod = cls.__module__
+    if mod.startswith("bigdl_amd.keras"):
+        return "keras." + cls.__name__
+    if mod == "bigdl_amd.nn.tf_ops":
+        return "ops." + cls.__name__
+    return cls.__name__
 
 
 def register(cls):
@@ -519,6 +524,11 @@ class AbstractModule(metaclass=_RecordInit):
 
         save_caffe(self, prototxtPath, modelPath, overwrite)
         return self
+
+    def saveTF(self, inputs, path, byteOrder=None, dataFormat="NHWC"):
+        from ..interop.tensorflow import save_tf
+
+        return save_tf(self, inputs, path, byteOrder, dataFormat)
 
     def saveTorch(self, path, overWrite=False):
         from ..interop.torchfile import save_torch

@@ -31,6 +31,18 @@ class Module:
         return load_caffe(defPath, modelPath, customizedConverters)[0]
 
     @staticmethod
+    def loadTF(path, inputs, outputs, byteOrder=None, binFile=None, generatedBackward=True):
+        from ..interop.tensorflow import load_tf
+
+        return load_tf(path, inputs, outputs, byteOrder, binFile, generatedBackward)
+
+    @staticmethod
+    def loadONNX(path):
+        from ..interop.onnx import load_onnx
+
+        return load_onnx(path)
+
+    @staticmethod
     def flatten(parameters):
         """Compact a list of tensors into one storage; returns the flat tensor (views rebound in place)."""
         total = sum(p.numel() for p in parameters)
