@@ -72,10 +72,18 @@ void conv_wgrad(const Tensor& dy, const Tensor& src, const Tensor& dw, const Opt
   int* f = &a.Nb;
   for (int i = 0; i < 18; ++i) f[i] = (int)geo[i];
   a.m_per_split = 0;
+  a.ws = nullptr;
+  a.splits = 0;
   TORCH_CHECK(dw.numel() >= (int64_t)a.Ncol * a.Kdim, "conv_wgrad: dw too small");
   TORCH_CHECK(a.M == a.Nb * a.OH * a.OW, "conv_wgrad: M mismatch");
   TORCH_CHECK(dy.numel() >= (int64_t)(a.M - 1) * a.ldy + a.Ncol, "conv_wgrad: dy too small");
   TORCH_CHECK(src.numel() >= (int64_t)a.Nb * a.Hs * a.Ws * a.Cs, "conv_wgrad: src too small");
+  Tensor ws;
+  const long wsn = bigdl_conv_wgrad_plan(&a);
+  if (wsn > 0) {     // split-K partials in a caching-allocator workspace (graph-capture safe)
+    ws = at::empty({wsn}, dw.options().dtype(at::kFloat));
+    a.ws = ws.data_ptr<float>();
+  }
   const int rc = bigdl_conv_wgrad(&a, stream());
   TORCH_CHECK(rc == 0, "conv_wgrad: unsupported shape (channels must be a multiple of 8)");
 }

@@ -777,6 +777,210 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(WgradArgs a) {
   }
 }
 
+// LDS-DMA weight-gradient kernel: same tile / fragment geometry as conv_wgrad_kernel, but the [pixel][channel]
+// operand tiles are streamed with global_load_lds (no VGPR staging, no LDS write instructions). A wave's
+// DMA instruction fills 4 consecutive rows x 16 granules; lane l writes slot l&15 of row 4j + (l>>4), so the
+// wswz row permutation f(row) is fixed per (lane, wave) and applied on the source side: the lane fetches
+// granule (l&15) ^ f. For the im2col operand that fixes each lane's (tap, channel) for the whole kernel.
+__global__ __launch_bounds__(256, 2) void conv_wgrad_glds_kernel(WgradArgs a) {
+  constexpr int STAGE = 2 * WBM * WT;
+  __shared__ __attribute__((aligned(1024))) bf16_t lds[2 * STAGE];
+  __shared__ int2 tbl[3][WBM];
+  __shared__ float red[4][128];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wk = wave >> 1, wn = wave & 1;
+  const int tiles_n = (a.Ncol + WT - 1) / WT, tiles_k = (a.Kdim + WT - 1) / WT;
+  const int ntile = tiles_n * tiles_k;
+  // XCD-aware split-major order: workgroup L runs on XCD L & 7; all tiles of split s live on XCD s & 7 and are
+  // dispatched back to back, so the split's dy / x pixel rows come from HBM once per XCD and the other tiles of
+  // that split hit the XCD's L2 (tile-major order re-read them from HBM once per tile).
+  const int L = blockIdx.x, kq = L >> 3;
+  const int split = 8 * (kq / ntile) + (L & 7);
+  const int t = kq % ntile;
+  const int tk = t / tiles_n, tn = t % tiles_n;
+  const int n0 = tn * WT, k0 = tk * WT;
+  const int mbeg = split * a.m_per_split;
+  const int mend = min(a.M, mbeg + a.m_per_split);
+  if (split >= a.splits || mbeg >= mend) return;
+
+  // source granule of this lane (see wswz): rows 16i + 4*wave + (lane>>4)
+  const int Lg = lane >> 4;
+  const int f = (Lg << 1) | (((wave >> 1) & 1) << 3) | (wave & 1);
+  const int gsrc = (lane & 15) ^ f;
+  const int nn = n0 + gsrc * 8;
+  const bool nvalid = nn < a.Ncol;
+  const int kk = k0 + gsrc * 8;
+  const bool kvalid = kk < a.Kdim;
+  const int SC = a.S * a.Cs;
+  int r = 0, s = 0, c = 0;
+  if (kvalid) { r = kk / SC; const int rem = kk - r * SC; s = rem / a.Cs; c = rem - s * a.Cs; }
+  const int rdh = r * a.dh, sdw = s * a.dwl;
+  const int tapoff = rdh * a.Ws + sdw;
+
+  const int ohw = a.OH * a.OW;
+  auto build_table = [&](int mb, int slot) {
+    if (tid < WBM) {
+      const int m = mb + tid;
+      int2 e;
+      if (m < mend) {
+        const int nb = m / ohw, rem = m - nb * ohw;
+        const int oh = rem / a.OW, ow = rem - oh * a.OW;
+        const int hb = oh * a.sh - a.ph, wb = ow * a.sw - a.pw;
+        e.x = (nb * a.Hs + hb) * a.Ws + wb;
+        e.y = (hb << 16) | (wb & 0xffff);
+      } else {
+        e.x = 0;
+        e.y = (int)0x80008000;
+      }
+      tbl[slot][tid] = e;
+    }
+  };
+  auto issue = [&](int mb, int tslot, int buf) {
+    bf16_t* D = lds + buf * STAGE;
+    bf16_t* X = D + WBM * WT;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int rowblk = (i * 4 + wave) * 4;          // first of the 4 rows this instruction fills
+      const int row = rowblk + Lg;
+      const int m = mb + row;
+      const int2 e = tbl[tslot][row];
+      const int ih = (e.y >> 16) + rdh, iw = ((int)(short)(e.y & 0xffff)) + sdw;
+      // columns past Ncol / Kdim only feed discarded outputs: no DMA at all for those lanes
+      const bf16_t* pd = m < mend ? a.dy + (unsigned)(m * a.ldy + nn) : g_zero_granule;
+      const bool okx = (unsigned)ih < (unsigned)a.Hs && (unsigned)iw < (unsigned)a.Ws;
+      const bf16_t* px = okx ? a.src + (unsigned)((e.x + tapoff) * a.Cs + c) : g_zero_granule;
+      if (nvalid) glds16(pd, (LDS_PTR(void))(D + rowblk * WT));
+      if (kvalid) glds16(px, (LDS_PTR(void))(X + rowblk * WT));
+    }
+  };
+
+  v4f acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+  const bool do_bias = a.dbias != nullptr && tk == 0 && wk == 0;
+  float bsum[4] = {0.f, 0.f, 0.f, 0.f};
+
+  const int G = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+
+  build_table(mbeg, 0);
+  build_table(mbeg + WBM, 1);
+  __syncthreads();
+  issue(mbeg, 0, 0);
+  build_table(mbeg + 2 * WBM, 2);
+  __syncthreads();
+  int cur = 0, ts = 1;
+  for (int mb = mbeg; mb < mend; mb += WBM) {
+    const bool more = mb + WBM < mend;
+    if (more) issue(mb + WBM, ts, cur ^ 1);
+    const bf16_t* D = lds + cur * STAGE;
+    const bf16_t* X = D + WBM * WT;
+#pragma unroll
+    for (int ks = 0; ks < WBM / 32; ++ks) {
+      v8s fx[4], fd[4];
+      const int rbase = ks * 32 + 8 * G + q;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int col = wk * 64 + i * 16 + 4 * p;
+        v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(v4s))(X + wswz(rbase, col)));
+        v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(v4s))(X + wswz(rbase + 4, col)));
+        fx[i] = v8s{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int col = wn * 64 + j * 16 + 4 * p;
+        v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(v4s))(D + wswz(rbase, col)));
+        v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(v4s))(D + wswz(rbase + 4, col)));
+        fd[j] = v8s{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fx[i], fd[j], acc[i][j], 0, 0, 0);
+      if (do_bias) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (n0 + wn * 64 + j * 16 + (lane & 15) < a.Ncol) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) bsum[j] += bf2f((bf16_t)fd[j][e]);
+          }
+      }
+    }
+    // table of stage t+3 into the slot stage t used; then retire stage t+1's DMA (vmcnt(0)) before reuse
+    build_table(mb + 3 * WBM, (ts + 2) % 3);
+    __syncthreads();
+    cur ^= 1;
+    ts = ts == 2 ? 0 : ts + 1;
+  }
+
+  float* part = a.ws ? a.ws + (size_t)split * a.Ncol * a.Kdim : nullptr;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int kb = k0 + wk * 64 + i * 16 + 4 * (lane >> 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = n0 + wn * 64 + j * 16 + (lane & 15);
+      if (n < a.Ncol) {
+        if (part) {   // this split owns its partial tile: plain 16-byte stores (Kdim % 8 == 0)
+          if (kb < a.Kdim) *reinterpret_cast<v4f*>(part + (size_t)n * a.Kdim + kb) = acc[i][j];
+        } else {
+          float* o = a.dw + (size_t)n * a.Kdim + kb;
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (kb + e < a.Kdim) atomicAdd(o + e, acc[i][j][e]);
+        }
+      }
+    }
+  }
+  if (a.dbias != nullptr && tk == 0) {
+    // waves wk==0 (wn = 0, 1) hold, per lane, partial sums of column wn*64 + j*16 + (lane&15) over the rows of
+    // row-group G; reduce the 4 groups through LDS
+    if (do_bias) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) red[G][wn * 64 + j * 16 + (lane & 15)] = bsum[j];
+    }
+    __syncthreads();
+    if (tid < 128) {
+      const float tot = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
+      const int n = n0 + tid;
+      if (n < a.Ncol) atomicAdd(a.dbias + n, tot);
+    }
+  }
+}
+
+// dw += sum over splits of the workspace partials. Split group g (blockIdx.y) sums splits g, g+G, ... with two
+// independent accumulators; with G > 1 the groups meet in dw through fp32 atomics (G-way contention at most), so
+// tiny weights (64x64 with ~1000 splits) still spread the reduction over the whole chip.
+template <bool ALIGNED>
+__global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ ws, float* __restrict__ dw,
+                                                           long n4, int splits) {
+  const int g = blockIdx.y, G = gridDim.y;
+  const v4f* w4 = reinterpret_cast<const v4f*>(ws);
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+    v4f s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
+    int sp = g;
+    for (; sp + G < splits; sp += 2 * G) {
+      s0 += w4[(long)sp * n4 + i];
+      s1 += w4[(long)(sp + G) * n4 + i];
+    }
+    if (sp < splits) s0 += w4[(long)sp * n4 + i];
+    s0 += s1;
+    if (G > 1) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) unsafeAtomicAdd(dw + 4 * i + e, s0[e]);
+    } else if (ALIGNED) {
+      reinterpret_cast<v4f*>(dw)[i] += s0;
+    } else {   // dw is a view into the flat gradient buffer at a 4-byte-aligned offset
+#pragma unroll
+      for (int e = 0; e < 4; ++e) dw[4 * i + e] += s0[e];
+    }
+  }
+}
+
 __global__ void transpose_krsc_kernel(const bf16_t* __restrict__ w, bf16_t* __restrict__ wt, int K, int RS,
                                       int C) {
   // wt[c][rs][k] = w[k][rs][c]
@@ -850,9 +1054,44 @@ int bigdl_conv_nt(const ConvArgs* a, hipStream_t st) {
   return 0;
 }
 
+// 64-wide output-channel layers with a deep reduction (stem 7x7, 3x3 over 64 channels) run half-empty 128x128
+// tiles; the register-staged atomic kernel is faster there (measured per layer, profiles/r1_ab_wgrad.txt)
+static bool wgrad_prefers_atomic(const WgradArgs* a) { return a->Ncol <= 64 && a->Kdim > 256; }
+
+long bigdl_conv_wgrad_plan(WgradArgs* a) {
+  const int tiles = ((a->Ncol + WT - 1) / WT) * ((a->Kdim + WT - 1) / WT);
+  if (conv_impl() < 1 || wgrad_prefers_atomic(a)) { a->splits = 0; return 0; }
+  // workspace split-K: ~4 workgroups per CU (two resident waves of 2/CU), >= 4 LDS stages per split
+  int splits = (1024 + tiles - 1) / tiles;
+  const int maxsplit = (a->M + 8 * WBM - 1) / (8 * WBM);
+  if (splits > maxsplit) splits = maxsplit;
+  if (splits < 1) splits = 1;
+  int mps = (a->M + splits - 1) / splits;
+  mps = (mps + WBM - 1) / WBM * WBM;
+  splits = (a->M + mps - 1) / mps;
+  a->m_per_split = mps;
+  a->splits = splits;
+  return splits > 1 ? (long)splits * a->Ncol * a->Kdim : 0;
+}
+
 int bigdl_conv_wgrad(const WgradArgs* a_in, hipStream_t st) {
   WgradArgs a = *a_in;
   if (a.Cs % 8 != 0 || a.Ncol % 8 != 0 || a.Kdim % 8 != 0) return -1;
+  if (a.ws != nullptr && a.splits > 1 && conv_impl() >= 1) {
+    const int tiles = ((a.Ncol + WT - 1) / WT) * ((a.Kdim + WT - 1) / WT);
+    const int spad = (a.splits + 7) / 8 * 8;
+    conv_wgrad_glds_kernel<<<dim3(tiles * spad), dim3(256), 0, st>>>(a);
+    const long n4 = (long)a.Ncol * a.Kdim / 4;
+    const int blocks = (int)std::min<long>((n4 + 255) / 256, 8192);
+    // ~2048 reduce workgroups in total, >= 4 splits per group, <= 64-way atomic contention
+    const int groups = blocks >= 256 ? 1 : std::max(1, std::min({2048 / blocks, a.splits / 4, 64}));
+    const dim3 rgrid(blocks, groups);
+    if ((reinterpret_cast<uintptr_t>(a.dw) & 15) == 0) wgrad_reduce_kernel<true><<<rgrid, 256, 0, st>>>(a.ws, a.dw, n4, a.splits);
+    else wgrad_reduce_kernel<false><<<rgrid, 256, 0, st>>>(a.ws, a.dw, n4, a.splits);
+    HIP_LAUNCH_CHECK();
+    return 0;
+  }
+  a.ws = nullptr;
   const int tiles = ((a.Ncol + WT - 1) / WT) * ((a.Kdim + WT - 1) / WT);
   // ~2 workgroups per CU in one dispatch wave; every split adds a full fp32 atomic pass over its
   // tile, so also cap the atomic traffic (splits x |dW| x 4 B) at ~32 MB (~25 us at the chip rate).
@@ -867,8 +1106,10 @@ int bigdl_conv_wgrad(const WgradArgs* a_in, hipStream_t st) {
   mps = (mps + WBM - 1) / WBM * WBM;
   splits = (a.M + mps - 1) / mps;
   a.m_per_split = mps;
-  dim3 grid(tiles, splits), block(256);
-  conv_wgrad_kernel<<<grid, block, 0, st>>>(a);
+  a.splits = splits;
+  if (conv_impl() >= 1 && !wgrad_prefers_atomic(&a))
+    conv_wgrad_glds_kernel<<<dim3(tiles * ((splits + 7) / 8 * 8)), dim3(256), 0, st>>>(a);
+  else conv_wgrad_kernel<<<dim3(tiles, splits), dim3(256), 0, st>>>(a);
   HIP_LAUNCH_CHECK();
   return 0;
 }

@@ -36,11 +36,16 @@ struct WgradArgs {
   int sh, sw, ph, pw, dh, dwl;
   int M, Ncol, Kdim, ldy;
   int m_per_split;
+  float* ws;       // split-K partials [splits][Ncol][Kdim] (nullptr: fp32 atomics into dw)
+  int splits;
 };
 
 extern "C" {
 int bigdl_conv_nt(const ConvArgs* a, hipStream_t st);
 int bigdl_conv_wgrad(const WgradArgs* a, hipStream_t st);
+// Split-K plan for the weight gradient: fills m_per_split / splits; returns the workspace size in floats
+// (0 when the single-split path accumulates straight into dw).
+long bigdl_conv_wgrad_plan(WgradArgs* a);
 void bigdl_transpose_krsc(const uint16_t* w, uint16_t* wt, int K, int RS, int C, hipStream_t st);
 
 // batch norm (NHWC bf16, fp32 statistics). Statistics / backward-reduction buffers are
