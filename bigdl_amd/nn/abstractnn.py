@@ -30,6 +30,8 @@ def module_key(cls):
         return "keras." + cls.__name__
     if mod == "bigdl_amd.nn.tf_ops":
         return "ops." + cls.__name__
+    if mod in ("bigdl_amd.nn.ops", "bigdl_amd.nn.tf"):
+        return mod[len("bigdl_amd."):] + "." + cls.__name__
     return cls.__name__
 
 
@@ -495,9 +497,14 @@ class AbstractModule(metaclass=_RecordInit):
 
         node = Node(self)
         for n in nodes:
-            if isinstance(n, (list, tuple)):
+            if isinstance(n, tuple) and len(n) == 2 and isinstance(n[1], int):   # (node, fromIndex) edge
+                n[0].add_next(node, n[1])
+            elif isinstance(n, (list, tuple)):
                 for x in n:
-                    x.add_next(node)
+                    if isinstance(x, tuple):
+                        x[0].add_next(node, x[1])
+                    else:
+                        x.add_next(node)
             elif n is not None:
                 n.add_next(node)
         return node

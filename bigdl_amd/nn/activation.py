@@ -313,14 +313,26 @@ class Identity(TensorModule):
 
 
 class Echo(TensorModule):
-    """Prints activations and gradients passing through (debugging, reference Echo.scala)."""
+    """Prints activations and gradients passing through (debugging, reference Echo.scala); ``feval`` /
+    ``beval`` replace the printing with callbacks ``fn(module, tensor)``."""
+
+    def __init__(self, feval=None, beval=None):
+        super().__init__()
+        self.feval = feval
+        self.beval = beval
 
     def updateOutput(self, input):
-        print(f"{self.getName()} : Activation size is {_shape(input)}")
+        if self.feval is not None:
+            self.feval(self, input)
+        else:
+            print(f"{self.getName()} : Activation size is {_shape(input)}")
         return input
 
     def updateGradInput(self, input, gradOutput):
-        print(f"{self.getName()} : Gradient size is {_shape(gradOutput)}")
+        if self.beval is not None:
+            self.beval(self, gradOutput)
+        else:
+            print(f"{self.getName()} : Gradient size is {_shape(gradOutput)}")
         return gradOutput
 
 

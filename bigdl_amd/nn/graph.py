@@ -24,13 +24,27 @@ class Node:
         self.element = element
         self.prevs = []
         self.nexts = []
+        self.prev_index = []     # per incoming edge: None, or the 1-based slot of the predecessor's output Table
+        self.next_index = []     # the same edge seen from the predecessor
         Node._ids += 1
         self.id = Node._ids
 
-    def add_next(self, node):
+    def add_next(self, node, from_index=None):
+        """Edge ``self -> node``; ``from_index`` selects one entry of this node's Table output
+        (reference utils/DirectedGraph.scala Edge(fromIndex))."""
         self.nexts.append(node)
+        self.next_index.append(from_index)
         node.prevs.append(self)
+        node.prev_index.append(from_index)
         return node
+
+    def remove_prev(self, prev):
+        while prev in self.prevs:
+            i = self.prevs.index(prev)
+            del self.prevs[i], self.prev_index[i]
+        while self in prev.nexts:
+            j = prev.nexts.index(self)
+            del prev.nexts[j], prev.next_index[j]
 
     def __rshift__(self, node):
         return self.add_next(node)
@@ -73,6 +87,19 @@ def topo_sort(outputs):
     return order
 
 
+def edge_value(out, from_index):
+    return out if from_index is None else out[from_index]
+
+
+def add_edge_grad(acc, g, from_index):
+    """Accumulate the gradient arriving over one edge; an indexed edge contributes to one Table slot."""
+    if from_index is None:
+        return add_activity(acc, g)
+    acc = acc if acc is not None else Table()
+    acc[from_index] = add_activity(acc.get(from_index), g)
+    return acc
+
+
 class Graph(Container):
     """Static DAG model (reference StaticGraph)."""
 
@@ -106,15 +133,16 @@ class Graph(Container):
         return self
 
     def _node_input(self, n, outs, graph_input):
-        if n in self.inputs_nodes:
+        if n in self.inputs_nodes and not n.prevs:
             if len(self.inputs_nodes) == 1:
                 return graph_input
             return graph_input[self.inputs_nodes.index(n) + 1]
-        if len(n.prevs) == 1:
-            return outs[n.prevs[0].id]
+        vals = [edge_value(outs[p.id], k) for p, k in zip(n.prevs, n.prev_index)]
+        if len(vals) == 1:
+            return vals[0]
         t = Table()
-        for i, p in enumerate(n.prevs):
-            t[i + 1] = outs[p.id]
+        for i, v in enumerate(vals):
+            t[i + 1] = v
         return t
 
     def updateOutput(self, input):
@@ -165,10 +193,11 @@ class Graph(Container):
                 continue
             if len(n.prevs) == 1:
                 p = n.prevs[0]
-                grads[p.id] = add_activity(grads.get(p.id), gi)
+                grads[p.id] = add_edge_grad(grads.get(p.id), gi, n.prev_index[0])
             else:
                 for i, p in enumerate(n.prevs):
-                    grads[p.id] = add_activity(grads.get(p.id), gi[i + 1] if gi is not None else None)
+                    grads[p.id] = add_edge_grad(grads.get(p.id), gi[i + 1] if gi is not None else None,
+                                                n.prev_index[i])
         return gin
 
     def backward(self, input, gradOutput):
@@ -197,12 +226,115 @@ class Graph(Container):
         return f"Graph({len(self.order)} nodes)"
 
 
+    @staticmethod
+    def dynamic(inputs, outputs, variables=None, generateBackward=True):
+        """Reference Graph.dynamic (S/nn/Graph.scala:540): a DynamicGraph run by the Scheduler."""
+        return DynamicGraph(inputs, outputs, variables, generateBackward)
+
+
 StaticGraph = Graph
 
 
+def _all_nodes(outputs):
+    """Every node reachable backwards from ``outputs`` (cycles through NextIteration edges allowed)."""
+    seen, order, stack = set(), [], list(outputs)
+    while stack:
+        n = stack.pop()
+        if n.id in seen:
+            continue
+        seen.add(n.id)
+        order.append(n)
+        stack.extend(n.prevs)
+    return order
+
+
 class DynamicGraph(Graph):
-    """Graph whose execution order is decided at run time (control-flow ops); executes the same way here
-    because the nodes run eagerly."""
+    """Graph executed by a data-flow scheduler with TensorFlow-style control flow (Switch / Merge / Enter /
+    Exit / NextIteration / LoopCondition, see nn/tf.py). Reference: S/nn/DynamicGraph.scala:45-144,
+    S/nn/Scheduler.scala:36-294, S/nn/FrameManager.scala:31.
+
+    Forward runs whatever the scheduler makes ready: untaken Switch branches never run, loop bodies run once
+    per iteration, and Const sub-graphs run once per model lifetime. Backward (graphs without control ops
+    only, like the reference) walks the executed nodes in reverse.
+    """
+
+    def __init__(self, inputs, outputs, variables=None, generateBackward=True):
+        from .scheduler import Scheduler
+
+        inputs = list(inputs) if isinstance(inputs, (list, tuple)) else [inputs]
+        outputs = list(outputs) if isinstance(outputs, (list, tuple)) else [outputs]
+        Container.__init__(self)
+        self.inputs_nodes = inputs
+        self.output_nodes = outputs
+        nodes = _all_nodes(outputs + inputs)
+        nodes.sort(key=lambda n: n.id)
+        self.order = nodes
+        mods = [n.element for n in nodes]
+        if len({id(m) for m in mods}) != len(mods):
+            raise ValueError("DynamicGraph: a module instance appears in more than one node")
+        self.modules = mods
+        self._stop_grad = set()
+        self.variables = variables
+        self.generateBackward = generateBackward
+        from .tf import ControlOps
+        self._has_control = any(isinstance(m, ControlOps) for m in mods)
+        sources = [n for n in nodes if not n.prevs]
+        self.scheduler = Scheduler(sources, outputs)
+
+    def updateOutput(self, input):
+        outs = {}
+        self._node_inputs = {}
+        self._executed = []
+        sch = self.scheduler
+        sch.reset()
+        while not sch.finished():
+            n = sch.fetch()
+            if n is None:
+                break
+            x = self._node_input(n, _LiveOutputs(n), input)
+            self._node_inputs[n.id] = x
+            outs[n.id] = n.element.forward(x)
+            self._executed.append(n)
+            sch.schedule(n)
+        self._outs = outs
+        if len(self.output_nodes) == 1:
+            return self.output_nodes[0].element.output
+        t = Table()
+        for i, o in enumerate(self.output_nodes):
+            t[i + 1] = o.element.output
+        return t
+
+    def _run_backward(self, input, gradOutput, acc_params, upd_input):
+        if not self.generateBackward:
+            return None
+        if self._has_control:
+            raise RuntimeError("DynamicGraph: backward through control-flow ops is not supported (reference "
+                               "DynamicGraph.buildBackwardGraph)")
+        saved = self.order
+        seen, order = set(), []
+        for n in self._executed:
+            if n.id not in seen:
+                seen.add(n.id)
+                order.append(n)
+        self.order = order
+        try:
+            return Graph._run_backward(self, input, gradOutput, acc_params, upd_input)
+        finally:
+            self.order = saved
+
+    def __repr__(self):
+        return f"DynamicGraph({len(self.order)} nodes)"
+
+
+class _LiveOutputs:
+    """Output lookup for DynamicGraph input assembly: each predecessor's live module output (a Const node
+    that the scheduler skips on later forwards still holds its value)."""
+
+    def __init__(self, node):
+        self._by_id = {p.id: p.element for p in node.prevs}
+
+    def __getitem__(self, nid):
+        return self._by_id[nid].output
 
 
 def Model(inputs, outputs):

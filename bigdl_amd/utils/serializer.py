@@ -95,10 +95,12 @@ def encode_module(m, ctx):
     if isinstance(m, Graph):
         idx = {n.id: i for i, n in enumerate(m.order)}
         d["graph"] = {
-            "nodes": [{"module": encode_module(n.element, ctx), "prevs": [idx[p.id] for p in n.prevs]}
-                      for n in m.order],
+            "nodes": [{"module": encode_module(n.element, ctx), "prevs": [idx[p.id] for p in n.prevs],
+                       "prev_index": list(n.prev_index)} for n in m.order],
             "inputs": [idx[n.id] for n in m.inputs_nodes],
             "outputs": [idx[n.id] for n in m.output_nodes],
+            "dynamic": type(m).__name__ == "DynamicGraph",
+            "generateBackward": bool(getattr(m, "generateBackward", True)),
         }
     elif hasattr(m, "modules") and isinstance(m.modules, list) and not _init_has_modules(m):
         d["children"] = [encode_module(c, ctx) for c in m.modules]
@@ -164,11 +166,15 @@ def decode_module(d, tensors):
             n = Node(decode_module(nd["module"], tensors))
             nodes.append(n)
         for nd, n in zip(g["nodes"], nodes):
-            for p in nd["prevs"]:
-                nodes[p].add_next(n)
+            for p, k in zip(nd["prevs"], nd.get("prev_index") or [None] * len(nd["prevs"])):
+                nodes[p].add_next(n, k)
         for i in g["inputs"]:
             nodes[i]._is_input = True
-        m = Graph([nodes[i] for i in g["inputs"]], [nodes[i] for i in g["outputs"]])
+        if g.get("dynamic"):
+            m = Graph.dynamic([nodes[i] for i in g["inputs"]], [nodes[i] for i in g["outputs"]], None,
+                              g.get("generateBackward", True))
+        else:
+            m = Graph([nodes[i] for i in g["inputs"]], [nodes[i] for i in g["outputs"]])
     else:
         args = [_dec(a, tensors) for a in d["init"]["args"]]
         kw = {k: _dec(x, tensors) for k, x in d["init"]["kw"].items()}
