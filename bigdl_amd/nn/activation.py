@@ -226,8 +226,9 @@ class SoftMin(AutogradModule):
 
 class LogSoftMax(AutogradModule):
     def fn(self, x):
-        d = 0 if x.dim() == 1 else x.dim() - 1
-        return torch.log_softmax(x.float(), d).to(x.dtype)
+        from ..ops import nnk
+
+        return nnk.log_softmax(x).to(x.dtype)          # last dim; GPU: one wave per row (csrc/nn_misc.hip)
 
 
 class Exp(AutogradModule):

@@ -19,9 +19,16 @@ class Dropout(TensorModule):
         return self.p
 
     def updateOutput(self, input):
+        self._seed = None
         if not self.train or self.p == 0:
             self._mask = None
             return input
+        if input.is_cuda and input.dtype in (torch.float32, torch.bfloat16):
+            from ..ops import nnk      # Philox keep-mask, regenerated in backward (csrc/nn_misc.hip)
+
+            self._mask = None
+            self._seed = nnk.next_seed()
+            return nnk.dropout_gpu(input, self.p, self.scale, self._seed)
         keep = 1.0 - self.p
         mask = (torch.rand(input.shape, device=input.device) < keep).to(input.dtype)
         if self.scale:
@@ -30,6 +37,10 @@ class Dropout(TensorModule):
         return input * mask
 
     def updateGradInput(self, input, gradOutput):
+        if getattr(self, "_seed", None) is not None:
+            from ..ops import nnk
+
+            return nnk.dropout_gpu(gradOutput.to(input.dtype), self.p, self.scale, self._seed)
         if self._mask is None:
             return gradOutput
         return gradOutput * self._mask

@@ -251,6 +251,10 @@ class LookupTable(TensorModule):
                 scale = torch.where(n > self.maxNorm, self.maxNorm / (n + 1e-7), torch.ones_like(n))
                 self.weight[rows] = w * scale
         safe = idx.clamp_min(0)
+        if self.weight.is_cuda and self.weight.dtype == torch.float32:
+            from ..ops import nnk      # wave-per-row gather (csrc/nn_misc.hip); negative ids -> zero rows
+
+            return nnk.embedding_fwd_gpu(self.weight, idx if self.maskZero else safe)
         out = self.weight[safe]
         if self.maskZero:
             out = out * (idx >= 0).unsqueeze(-1).to(out.dtype)
@@ -265,6 +269,11 @@ class LookupTable(TensorModule):
         keep = idx >= 0
         if self.paddingValue != 0:
             keep = keep & (idx != int(self.paddingValue) - 1)
+        if self.gradWeight.is_cuda and not self.shouldScaleGradByFreq:
+            from ..ops import nnk      # fp32 atomic scatter-add straight into gradWeight
+
+            nnk.embedding_bwd_gpu(self.gradWeight, torch.where(keep, idx, torch.full_like(idx, -1)), g, self.scaleW)
+            return
         idx, g = idx[keep], g[keep]
         if self.shouldScaleGradByFreq:
             cnt = torch.bincount(idx, minlength=self.nIndex).float()

@@ -222,10 +222,12 @@ class SpatialCrossMapLRN(AutogradModule):
         self.size, self.alpha, self.beta, self.k, self.format = size, alpha, beta, k, format
 
     def fn(self, x):
+        from ..ops import nnk
+
         xf = x.float()
         if self.format == "NHWC":
             xf = xf.permute(0, 3, 1, 2)
-        y = F.local_response_norm(xf, self.size, self.alpha, self.beta, self.k)
+        y = nnk.lrn(xf, self.size, self.alpha, self.beta, self.k)     # GPU: csrc/nn_misc.hip lrn kernels
         if self.format == "NHWC":
             y = y.permute(0, 2, 3, 1)
         return y.to(x.dtype)

@@ -371,7 +371,9 @@ class ResizeBilinear(AutogradModule):
     def fn(self, x):
         if self.fmt == "NHWC":
             x = x.permute(0, 3, 1, 2)
-        y = F.interpolate(x.float(), size=self.size, mode="bilinear", align_corners=self.align)
+        from ..ops import nnk
+
+        y = nnk.resize_bilinear(x, self.size[0], self.size[1], self.align)   # TF-legacy sampling, GPU kernel
         if self.fmt == "NHWC":
             y = y.permute(0, 2, 3, 1)
         return y

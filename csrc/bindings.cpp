@@ -368,6 +368,74 @@ void image_augment(const Tensor& src, const Tensor& params, const Tensor& out, s
                       rgb ? 1 : 0, bf ? 1 : 0, stream());
 }
 
+// ------------------------------------------------------------------------------------------ misc NN (nn_misc.hip)
+void contig(const Tensor& t, const char* n) { TORCH_CHECK(t.is_contiguous(), n, " must be contiguous"); }
+
+void lrn_fwd(const Tensor& x, const Tensor& y, const Tensor& scale, int64_t size, double alpha, double beta, double k) {
+  contig(x, "x");
+  TORCH_CHECK(x.dim() == 4 && y.numel() == x.numel() && scale.numel() == x.numel(), "lrn_fwd: bad shapes");
+  bigdl_lrn_fwd(cf(x, "x"), mf(y, "y"), mf(scale, "scale"), x.size(0), x.size(1), x.size(2) * x.size(3), size, alpha,
+                beta, k, stream());
+}
+void lrn_bwd(const Tensor& x, const Tensor& y, const Tensor& scale, const Tensor& gy, const Tensor& gx, int64_t size,
+             double alpha, double beta) {
+  contig(x, "x"); contig(gy, "gy");
+  TORCH_CHECK(x.dim() == 4 && gy.numel() == x.numel() && gx.numel() == x.numel(), "lrn_bwd: bad shapes");
+  bigdl_lrn_bwd(cf(x, "x"), cf(y, "y"), cf(scale, "scale"), cf(gy, "gy"), mf(gx, "gx"), x.size(0), x.size(1),
+                x.size(2) * x.size(3), size, alpha, beta, stream());
+}
+void dropout(const Tensor& x, const Tensor& y, double p, double mul, int64_t seed) {
+  contig(x, "x"); contig(y, "y");
+  TORCH_CHECK(x.numel() == y.numel() && x.scalar_type() == y.scalar_type(), "dropout: x/y mismatch");
+  const bool bf = x.scalar_type() == at::kBFloat16;
+  TORCH_CHECK(bf || x.scalar_type() == at::kFloat, "dropout: fp32 or bf16 only");
+  TORCH_CHECK(x.is_cuda() && y.is_cuda(), "dropout: GPU tensors");
+  bigdl_dropout(x.data_ptr(), y.data_ptr(), bf ? 1 : 0, x.numel(), p, mul, (unsigned long long)seed, stream());
+}
+void embedding_fwd(const Tensor& W, const Tensor& idx, const Tensor& out) {
+  contig(W, "W"); contig(idx, "idx"); contig(out, "out");
+  TORCH_CHECK(W.dim() == 2 && idx.scalar_type() == at::kLong && idx.is_cuda(), "embedding_fwd: W 2-D, idx int64");
+  TORCH_CHECK(out.numel() == idx.numel() * W.size(1), "embedding_fwd: out size");
+  bigdl_embedding_fwd(cf(W, "W"), (const long*)idx.data_ptr(), mf(out, "out"), idx.numel(), W.size(1), W.size(0),
+                      stream());
+}
+void embedding_bwd(const Tensor& gout, const Tensor& idx, const Tensor& gW, double scale) {
+  contig(gout, "gout"); contig(idx, "idx"); contig(gW, "gW");
+  TORCH_CHECK(gW.dim() == 2 && idx.scalar_type() == at::kLong && idx.is_cuda(), "embedding_bwd: gW 2-D, idx int64");
+  TORCH_CHECK(gout.numel() == idx.numel() * gW.size(1), "embedding_bwd: gout size");
+  bigdl_embedding_bwd(cf(gout, "gout"), (const long*)idx.data_ptr(), mf(gW, "gW"), idx.numel(), gW.size(1), gW.size(0),
+                      scale, stream());
+}
+void resize_bilinear_fwd(const Tensor& x, const Tensor& y, double sh, double sw) {
+  contig(x, "x"); contig(y, "y");
+  TORCH_CHECK(x.dim() == 4 && y.dim() == 4 && x.size(0) * x.size(1) == y.size(0) * y.size(1), "resize: shapes");
+  bigdl_resize_bilinear_fwd(cf(x, "x"), mf(y, "y"), x.size(0) * x.size(1), x.size(2), x.size(3), y.size(2), y.size(3),
+                            sh, sw, stream());
+}
+void resize_bilinear_bwd(const Tensor& gy, const Tensor& gx, double sh, double sw) {
+  contig(gy, "gy"); contig(gx, "gx");
+  TORCH_CHECK(gy.dim() == 4 && gx.dim() == 4 && gx.size(0) * gx.size(1) == gy.size(0) * gy.size(1), "resize: shapes");
+  bigdl_resize_bilinear_bwd(cf(gy, "gy"), mf(gx, "gx"), gy.size(0) * gy.size(1), gx.size(2), gx.size(3), gy.size(2),
+                            gy.size(3), sh, sw, stream());
+}
+void log_softmax_fwd(const Tensor& x, const Tensor& y) {
+  contig(x, "x"); contig(y, "y");
+  TORCH_CHECK(x.numel() == y.numel() && x.dim() >= 1, "log_softmax_fwd: shapes");
+  const int64_t cols = x.size(-1);
+  bigdl_log_softmax_fwd(cf(x, "x"), mf(y, "y"), x.numel() / cols, cols, stream());
+}
+void log_softmax_bwd(const Tensor& y, const Tensor& gy, const Tensor& gx) {
+  contig(y, "y"); contig(gy, "gy"); contig(gx, "gx");
+  TORCH_CHECK(y.numel() == gy.numel() && gx.numel() == y.numel(), "log_softmax_bwd: shapes");
+  const int64_t cols = y.size(-1);
+  bigdl_log_softmax_bwd(cf(y, "y"), cf(gy, "gy"), mf(gx, "gx"), y.numel() / cols, cols, stream());
+}
+void f32_to_bf16_rtz(const Tensor& x, const Tensor& y) {
+  contig(x, "x"); contig(y, "y");
+  TORCH_CHECK(x.numel() == y.numel(), "f32_to_bf16_rtz: sizes");
+  bigdl_f32_to_bf16_rtz(cf(x, "x"), mbf(y, "y"), x.numel(), stream());
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -407,6 +475,16 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("roi_align_fwd", &roi_align_fwd);
   m.def("roi_pool_fwd", &roi_pool_fwd);
   m.def("roi_pool_bwd", &roi_pool_bwd);
+  m.def("lrn_fwd", &lrn_fwd);
+  m.def("lrn_bwd", &lrn_bwd);
+  m.def("dropout", &dropout);
+  m.def("embedding_fwd", &embedding_fwd);
+  m.def("embedding_bwd", &embedding_bwd);
+  m.def("resize_bilinear_fwd", &resize_bilinear_fwd);
+  m.def("resize_bilinear_bwd", &resize_bilinear_bwd);
+  m.def("log_softmax_fwd", &log_softmax_fwd);
+  m.def("log_softmax_bwd", &log_softmax_bwd);
+  m.def("f32_to_bf16_rtz", &f32_to_bf16_rtz);
   m.def("set_conv_impl", &bigdl_set_conv_impl);
   m.def("get_conv_impl", &bigdl_get_conv_impl);
   m.attr("arch") = "gfx950";

@@ -128,4 +128,24 @@ int bigdl_roi_pool_fwd(const float* x, const float* rois, float* out, int* argma
                        int PH, int PW, float scale, hipStream_t st);
 int bigdl_roi_pool_bwd(const float* gy, const int* argmax, const float* rois, float* gx, int R, int C, int H, int W,
                        int PH, int PW, hipStream_t st);
+
+// Misc NN kernels (csrc/nn_misc.hip): LRN across channels (NCHW fp32), Philox dropout (mask regenerated in
+// backward), embedding gather / atomic scatter-add, TF-style bilinear resize (NCHW fp32), row log-softmax,
+// fp32 -> bf16 round-toward-zero (FP16CompressedTensor parity).
+void bigdl_lrn_fwd(const float* x, float* y, float* scale, int N, int C, long HW, int size, float alpha, float beta,
+                   float k, hipStream_t st);
+void bigdl_lrn_bwd(const float* x, const float* y, const float* scale, const float* gy, float* gx, int N, int C, long HW,
+                   int size, float alpha, float beta, hipStream_t st);
+void bigdl_dropout(const void* x, void* y, int is_bf16, long n, float p, float mul, unsigned long long seed,
+                   hipStream_t st);
+void bigdl_embedding_fwd(const float* W, const long* idx, float* out, long rows, int D, long nIndex, hipStream_t st);
+void bigdl_embedding_bwd(const float* gout, const long* idx, float* gW, long rows, int D, long nIndex, float scale,
+                         hipStream_t st);
+void bigdl_resize_bilinear_fwd(const float* x, float* y, long NC, int H, int W, int OH, int OW, float sh, float sw,
+                               hipStream_t st);
+void bigdl_resize_bilinear_bwd(const float* gy, float* gx, long NC, int H, int W, int OH, int OW, float sh, float sw,
+                               hipStream_t st);
+void bigdl_log_softmax_fwd(const float* x, float* y, long rows, int cols, hipStream_t st);
+void bigdl_log_softmax_bwd(const float* y, const float* gy, float* gx, long rows, int cols, hipStream_t st);
+void bigdl_f32_to_bf16_rtz(const float* x, uint16_t* y, long n, hipStream_t st);
 }

@@ -236,3 +236,13 @@ def test_variable_assign_and_grad_ops():
     y = (xx - xx.mean((0, 1, 2))) / torch.sqrt(xx.var((0, 1, 2), unbiased=False) + 1e-3) * s2
     y.backward(dy)
     assert torch.allclose(dx, xx.grad, atol=1e-4) and torch.allclose(dsc, s2.grad, atol=1e-4)
+
+
+def test_resize_bilinear_reference_fixture():
+    """S/test/.../nn/ResizeBilinearSpec.scala 'double height' (TF-legacy sampling, NHWC)."""
+    x = torch.tensor([[[[1, 2, 3], [4, 5, 6]], [[7, 8, 9], [2, 3, 1]], [[4, 8, 2], [5, 3, 0]]]], dtype=torch.float32)
+    assert torch.equal(nn.ResizeBilinear(3, 2, dataFormat="NHWC").forward(x), x)
+    out = nn.ResizeBilinear(6, 2, dataFormat="NHWC").forward(x)
+    exp = torch.tensor([[[[1, 2, 3], [4, 5, 6]], [[4, 5, 6], [3, 4, 3.5]], [[7, 8, 9], [2, 3, 1]],
+                         [[5.5, 8, 5.5], [3.5, 3, 0.5]], [[4, 8, 2], [5, 3, 0]], [[4, 8, 2], [5, 3, 0]]]])
+    assert torch.allclose(out, exp)

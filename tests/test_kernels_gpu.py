@@ -278,3 +278,96 @@ def test_image_augment_kernel(nhwc):
     ref = augment_batch_ref(src, p, 32, 30, mean, std, True, nhwc)
     out = augment_batch(src.cuda(), p, 32, 30, mean, std, True, nhwc).cpu()
     assert torch.allclose(out.float(), ref.float(), atol=2e-2 if nhwc else 1e-5)
+
+
+# ---------------------------------------------------------------------------------------------- misc NN kernels
+def test_lrn_kernel_matches_fp32_reference():
+    from bigdl_amd.ops import nnk
+
+    torch.manual_seed(0)
+    for size in (5, 4):
+        x = torch.randn(3, 13, 7, 5)
+        ref_y = nnk.lrn_cpu(x.double(), size, 1e-2, 0.75, 2.0).float()
+        xr = x.clone().double().requires_grad_(True)
+        gy = torch.randn_like(x)
+        nnk.lrn_cpu(xr, size, 1e-2, 0.75, 2.0).backward(gy.double())
+        xg = x.cuda().requires_grad_(True)
+        y = nnk.lrn(xg, size, 1e-2, 0.75, 2.0)
+        y.backward(gy.cuda())
+        assert torch.allclose(y.cpu(), ref_y, atol=1e-5, rtol=1e-4)
+        assert torch.allclose(xg.grad.cpu(), xr.grad.float(), atol=1e-5, rtol=1e-4)
+    if True:   # odd size agrees with torch's LRN too
+        x = torch.randn(2, 9, 4, 4)
+        assert torch.allclose(nnk.lrn_cpu(x, 5, 1e-3, 0.75, 1.0),
+                              torch.nn.functional.local_response_norm(x, 5, 1e-3, 0.75, 1.0), atol=1e-6)
+
+
+def test_dropout_kernel_mask_regenerated():
+    from bigdl_amd import nn
+
+    torch.manual_seed(0)
+    for dt in (torch.float32, torch.bfloat16):
+        x = torch.randn(1001, 33, device="cuda").to(dt)
+        d = nn.Dropout(0.3)
+        y = d.forward(x)
+        keep = (y != 0)
+        frac = keep.float().mean().item()
+        assert abs(frac - 0.7) < 0.01
+        assert torch.allclose(y[keep].float(), (x[keep].float() / 0.7), rtol=1e-2)
+        g = d.backward(x, torch.ones_like(x))
+        assert torch.equal(g != 0, keep)
+        y2 = d.forward(x)
+        assert not torch.equal(y2 != 0, keep)          # a fresh mask each forward
+
+
+def test_embedding_kernels_match_reference():
+    from bigdl_amd import nn
+
+    torch.manual_seed(0)
+    lt = nn.LookupTable(50, 24)
+    idx = torch.randint(1, 51, (7, 9)).float()
+    ref = lt.weight[idx.long() - 1]
+    gy = torch.randn(7, 9, 24)
+    ref_g = torch.zeros(50, 24).index_add_(0, idx.long().reshape(-1) - 1, gy.reshape(-1, 24))
+    lt = lt.to(torch.device("cuda"))
+    out = lt.forward(idx.cuda())
+    lt.zeroGradParameters()
+    lt.backward(idx.cuda(), gy.cuda())
+    assert torch.allclose(out.cpu(), ref)
+    assert torch.allclose(lt.gradWeight.cpu(), ref_g, atol=1e-5)
+
+
+def test_resize_bilinear_and_log_softmax_kernels():
+    from bigdl_amd.ops import nnk
+
+    torch.manual_seed(0)
+    for align in (False, True):
+        x = torch.randn(2, 3, 5, 7)
+        gy = torch.randn(2, 3, 9, 4)
+        xr = x.clone().requires_grad_(True)
+        ref = nnk.resize_bilinear_cpu(xr, 9, 4, align)
+        ref.backward(gy)
+        xg = x.cuda().requires_grad_(True)
+        y = nnk.resize_bilinear(xg, 9, 4, align)
+        y.backward(gy.cuda())
+        assert torch.allclose(y.cpu(), ref.detach(), atol=1e-5)
+        assert torch.allclose(xg.grad.cpu(), xr.grad, atol=1e-5)
+    x = torch.randn(37, 1000) * 4
+    gy = torch.randn(37, 1000)
+    xr = x.clone().requires_grad_(True)
+    torch.log_softmax(xr, -1).backward(gy)
+    xg = x.cuda().requires_grad_(True)
+    y = nnk.log_softmax(xg)
+    y.backward(gy.cuda())
+    assert torch.allclose(y.cpu(), torch.log_softmax(x, -1), atol=1e-5)
+    assert torch.allclose(xg.grad.cpu(), xr.grad, atol=1e-5)
+
+
+def test_bf16_truncation_kernel():
+    from bigdl_amd.ops import nnk
+
+    x = torch.randn(4099) * 100
+    ref = nnk.f32_to_bf16_rtz(x)
+    got = nnk.f32_to_bf16_rtz(x.cuda()).cpu()
+    assert torch.equal(got.view(torch.int16), ref.view(torch.int16))
+    assert torch.all(got.float().abs() <= x.abs())         # toward zero
