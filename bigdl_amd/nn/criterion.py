@@ -342,9 +342,32 @@ class TimeDistributedCriterion(AbstractCriterion):
         self.critrn = critrn
         self.dimension = dimension
 
+    def _flat_ok(self, input, target):
+        """Criterions whose per-step value is a uniform mean (or sum) over the rows of the step can run once over
+        all (batch x time) rows: sum_t mean_b(l) == T * mean_{b,t}(l). Weighted / padded NLL is not uniform."""
+        c = self.critrn
+        if self.dimension != 2 or input.dim() < 3 or target.dim() < 2 or target.shape[:2] != input.shape[:2]:
+            return False
+        if isinstance(c, CrossEntropyCriterion):
+            return c.weights is None
+        if isinstance(c, ClassNLLCriterion):
+            return c.weights is None and c.paddingValue == -1
+        return isinstance(c, (MSECriterion, AbsCriterion))
+
+    def _flat(self, input, target):
+        n = input.shape[0] * input.shape[1]
+        x = input.reshape((n,) + tuple(input.shape[2:]))
+        y = target.reshape((n,) + tuple(target.shape[2:]))
+        return x, y
+
     def updateOutput(self, input, target):
         d = self.dimension - 1
         T = input.shape[d]
+        if self._flat_ok(input, target):       # one launch over B*T rows instead of T small ones
+            x, y = self._flat(input, target)
+            loss = self.critrn.forward(x, y)
+            loss = loss * T if self.critrn.sizeAverage else loss
+            return loss / T if self.sizeAverage else loss
         loss = 0.0
         for t in range(T):
             loss = loss + self.critrn.forward(input.select(d, t), target.select(d, t) if target.dim() > d else target)
@@ -353,6 +376,13 @@ class TimeDistributedCriterion(AbstractCriterion):
     def updateGradInput(self, input, target):
         d = self.dimension - 1
         T = input.shape[d]
+        if self._flat_ok(input, target):
+            x, y = self._flat(input, target)
+            if getattr(self.critrn, "_grad", None) is None:
+                self.critrn.forward(x, y)
+            g = self.critrn.backward(x, y).reshape(input.shape)
+            scale = (T if self.critrn.sizeAverage else 1.0) / (T if self.sizeAverage else 1.0)
+            return g * scale if scale != 1.0 else g
         gs = []
         for t in range(T):
             xi = input.select(d, t)

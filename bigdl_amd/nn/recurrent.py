@@ -264,9 +264,29 @@ class _LSTMSeq(torch.autograd.Function):
         dc_prev.copy_(dc * f)
 
     @staticmethod
+    def _fused_gpu(xg, U):
+        return xg.is_cuda and U.shape[1] % 32 == 0 and xg.dtype == torch.float32
+
+    @staticmethod
     def forward(ctx, xg, h0, c0, U):
         B, T, G = xg.shape
         H = G // 4
+        if _LSTMSeq._fused_gpu(xg, U):
+            # one fused launch per step (csrc/lstm.hip): bf16 MFMA recurrent GEMM + cell in its epilogue
+            C = ops.native.get()
+            W16 = U.detach().to(torch.bfloat16).contiguous()
+            out = xg.new_empty(B, T, H)
+            cs = xg.new_empty(T, B, H)
+            acts = xg.new_empty(T, B, G)
+            h16 = xg.new_empty(2, B, H, dtype=torch.bfloat16)
+            h16[0].copy_(h0)
+            c_prev = c0.contiguous()
+            for t in range(T):
+                C.lstm_fwd_step(W16, h16[t & 1], xg[:, t], c_prev, cs[t], out[:, t], h16[(t + 1) & 1], acts[t])
+                c_prev = cs[t]
+            ctx.save_for_backward(h0, c0, U, out, cs, acts)
+            ctx.fused = True
+            return out, out[:, -1].clone(), cs[-1].clone()
         hs = xg.new_empty(T, B, H)
         cs = xg.new_empty(T, B, H)
         acts = xg.new_empty(T, B, G)
@@ -277,10 +297,34 @@ class _LSTMSeq(torch.autograd.Function):
             _LSTMSeq._cell_fwd(g, c, cs[t], hs[t], acts[t])
             h, c = hs[t], cs[t]
         ctx.save_for_backward(h0, c0, U, hs, cs, acts)
+        ctx.fused = False
         return hs.transpose(0, 1).contiguous(), hs[-1].clone(), cs[-1].clone()
 
     @staticmethod
+    def _backward_fused(ctx, dout, dhT, dcT):
+        h0, c0, U, out, cs, acts = ctx.saved_tensors
+        B, T, H = out.shape
+        C = ops.native.get()
+        dout = dout.contiguous() if dout is not None else None
+        WT16 = U.detach().t().contiguous().to(torch.bfloat16)
+        dxg = out.new_empty(B, T, 4 * H)
+        dg16 = out.new_empty(2, B, 4 * H, dtype=torch.bfloat16)
+        dc = dcT.contiguous().clone() if dcT is not None else out.new_zeros(B, H)
+        dhT = dhT.contiguous() if dhT is not None else None
+        c0 = c0.contiguous()
+        for t in range(T - 1, -1, -1):
+            C.lstm_bwd_step(WT16, dg16[(t + 1) & 1] if t < T - 1 else None,
+                            dout[:, t] if dout is not None else None, dhT if t == T - 1 else None, acts[t],
+                            cs[t - 1] if t > 0 else c0, cs[t], dc, dxg[:, t], dg16[t & 1])
+        dh0 = dxg[:, 0] @ U
+        hprev = torch.cat([h0.unsqueeze(1), out[:, :-1]], 1).reshape(B * T, H)
+        dU = torch.matmul(dxg.reshape(B * T, 4 * H).t().to(torch.bfloat16), hprev.to(torch.bfloat16)).float()
+        return dxg, dh0, dc, dU
+
+    @staticmethod
     def backward(ctx, dout, dhT, dcT):
+        if ctx.fused:
+            return _LSTMSeq._backward_fused(ctx, dout, dhT, dcT)
         h0, c0, U, hs, cs, acts = ctx.saved_tensors
         T, B, H = hs.shape
         dgs = acts.new_empty(T, B, 4 * H)

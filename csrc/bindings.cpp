@@ -436,6 +436,46 @@ void f32_to_bf16_rtz(const Tensor& x, const Tensor& y) {
   bigdl_f32_to_bf16_rtz(cf(x, "x"), mbf(y, "y"), x.numel(), stream());
 }
 
+// ------------------------------------------------------------------------------------------ fused LSTM steps
+// Row-strided views (e.g. xg[:, t] of a [B, T, 4H] tensor) are passed with their batch-row stride.
+int64_t rowstride(const Tensor& t, int64_t inner, const char* n) {
+  TORCH_CHECK(t.dim() == 2 && t.stride(1) == 1 && t.size(1) == inner, n, ": expected [B, ", inner, "] with unit inner stride");
+  return t.stride(0);
+}
+void lstm_fwd_step(const Tensor& W16, const OptT& h16_prev, const Tensor& xg, const OptT& c_prev, const Tensor& c_out,
+                   const Tensor& h_out, const Tensor& h16_out, const Tensor& acts) {
+  const int64_t B = xg.size(0), H = W16.size(1);
+  TORCH_CHECK(W16.size(0) == 4 * H && W16.is_contiguous(), "lstm_fwd_step: W16 must be [4H, H] contiguous");
+  TORCH_CHECK(H % 32 == 0, "lstm_fwd_step: H must be a multiple of 32");
+  const int64_t ldx = rowstride(xg, 4 * H, "xg"), ldh = rowstride(h_out, H, "h_out"), lda = rowstride(acts, 4 * H, "acts");
+  TORCH_CHECK(h_out.size(0) == B && acts.size(0) == B && c_out.numel() == B * H && h16_out.numel() == B * H,
+              "lstm_fwd_step: batch mismatch");
+  TORCH_CHECK(c_out.is_contiguous() && h16_out.is_contiguous(), "lstm_fwd_step: c_out/h16_out contiguous");
+  if (h16_prev && h16_prev->defined()) TORCH_CHECK(h16_prev->numel() == B * H && h16_prev->is_contiguous(), "h16_prev");
+  if (c_prev && c_prev->defined()) TORCH_CHECK(c_prev->numel() == B * H && c_prev->is_contiguous(), "c_prev");
+  bigdl_lstm_fwd_step(cbf(W16, "W16"), ocbf(h16_prev, "h16_prev"), cf(xg, "xg"), ldx, ocf(c_prev, "c_prev"),
+                      mf(c_out, "c_out"), mf(h_out, "h_out"), ldh, mbf(h16_out, "h16_out"), mf(acts, "acts"), lda, B, H,
+                      stream());
+}
+void lstm_bwd_step(const Tensor& WT16, const OptT& dg16_next, const OptT& dout, const OptT& dh_ext, const Tensor& acts,
+                   const OptT& c_prev, const Tensor& c_t, const Tensor& dc, const Tensor& dg_out, const Tensor& dg16_out) {
+  const int64_t H = WT16.size(0), B = acts.size(0);
+  TORCH_CHECK(WT16.size(1) == 4 * H && WT16.is_contiguous(), "lstm_bwd_step: WT16 must be [H, 4H] contiguous");
+  TORCH_CHECK(H % 32 == 0, "lstm_bwd_step: H must be a multiple of 32");
+  const int64_t lda = rowstride(acts, 4 * H, "acts"), ldg = rowstride(dg_out, 4 * H, "dg_out");
+  int64_t ldd = 0;
+  if (dout && dout->defined()) { ldd = rowstride(*dout, H, "dout"); TORCH_CHECK(dout->size(0) == B, "dout batch"); }
+  TORCH_CHECK(dg_out.size(0) == B && c_t.numel() == B * H && dc.numel() == B * H && dg16_out.numel() == B * 4 * H,
+              "lstm_bwd_step: batch mismatch");
+  TORCH_CHECK(c_t.is_contiguous() && dc.is_contiguous() && dg16_out.is_contiguous(), "lstm_bwd_step: contiguity");
+  if (dg16_next && dg16_next->defined()) TORCH_CHECK(dg16_next->numel() == B * 4 * H && dg16_next->is_contiguous(), "dg16_next");
+  if (dh_ext && dh_ext->defined()) TORCH_CHECK(dh_ext->numel() == B * H && dh_ext->is_contiguous(), "dh_ext");
+  if (c_prev && c_prev->defined()) TORCH_CHECK(c_prev->numel() == B * H && c_prev->is_contiguous(), "c_prev");
+  bigdl_lstm_bwd_step(cbf(WT16, "WT16"), ocbf(dg16_next, "dg16_next"), ocf(dout, "dout"), ldd, ocf(dh_ext, "dh_ext"),
+                      cf(acts, "acts"), lda, ocf(c_prev, "c_prev"), cf(c_t, "c_t"), mf(dc, "dc"), mf(dg_out, "dg_out"),
+                      ldg, mbf(dg16_out, "dg16_out"), B, H, stream());
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -485,6 +525,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("log_softmax_fwd", &log_softmax_fwd);
   m.def("log_softmax_bwd", &log_softmax_bwd);
   m.def("f32_to_bf16_rtz", &f32_to_bf16_rtz);
+  m.def("lstm_fwd_step", &lstm_fwd_step);
+  m.def("lstm_bwd_step", &lstm_bwd_step);
   m.def("set_conv_impl", &bigdl_set_conv_impl);
   m.def("get_conv_impl", &bigdl_get_conv_impl);
   m.attr("arch") = "gfx950";

@@ -9,6 +9,7 @@
 // Every memory-bound kernel moves 16 bytes per lane (cdna_hip_programming.md Guideline 13).
 #include "common.h"
 #include "kernels.h"
+#include <algorithm>
 
 namespace {
 
@@ -249,34 +250,92 @@ __global__ void avgpool_bwd_kernel(const bf16_t* __restrict__ dy, bf16_t* __rest
 }
 
 // ---------------- fused log-softmax + NLL: one wave per row ----------------
+// Fused log-softmax + NLL (+ gradient). One wave per row, rows grid-strided; a single online max/sum pass
+// (running max with rescaled sum) over 16-byte loads, a second pass writes the gradient. Each block reduces its
+// rows' losses in LDS and issues ONE atomic (16k-row LM batches would otherwise serialise on one address).
+template <bool VEC>
 __global__ __launch_bounds__(256) void softmax_xent_kernel(const bf16_t* __restrict__ lb, const float* __restrict__ lf,
                                                            const float* __restrict__ labels, float* __restrict__ loss,
                                                            bf16_t* __restrict__ db, float* __restrict__ df, int B, int K,
                                                            float label_base, float grad_scale) {
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (row >= B) return;
-  auto ld = [&](int k) -> float { return lb ? bf2f(lb[(long)row * K + k]) : lf[(long)row * K + k]; };
-  float mx = -INFINITY;
-  for (int k = lane; k < K; k += 64) mx = fmaxf(mx, ld(k));
-  mx = wave_max(mx);
-  float se = 0.f;
-  for (int k = lane; k < K; k += 64) se += __expf(ld(k) - mx);
-  se = wave_sum(se);
-  const float lse = mx + __logf(se);
-  const int tgt = (int)(labels[row] - label_base);
-  if (lane == 0 && loss) {
-    const float xt = (tgt >= 0 && tgt < K) ? ld(tgt) : lse;
-    atomicAdd(loss, (lse - xt) * grad_scale);
-  }
-  if (db || df) {
-    const float inv = 1.f / se;
-    for (int k = lane; k < K; k += 64) {
-      float g = __expf(ld(k) - mx) * inv - (k == tgt ? 1.f : 0.f);
-      g *= grad_scale;
-      if (db) db[(long)row * K + k] = f2bf(g);
-      else df[(long)row * K + k] = g;
+  __shared__ float part[4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float my_loss = 0.f;
+  for (int row = blockIdx.x * 4 + wave; row < B; row += gridDim.x * 4) {
+    const long base = (long)row * K;
+    float mx = -INFINITY, se = 0.f;
+    auto acc = [&](float v) {
+      if (v > mx) { se = se * __expf(mx - v) + 1.f; mx = v; } else { se += __expf(v - mx); }
+    };
+    if (VEC && lb) {            // 8 bf16 per lane per load
+      const v4u* p = (const v4u*)(lb + base);
+      for (int q = lane; q < (K >> 3); q += 64) {
+        const v4u v = p[q];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { acc(lo_bf(v[e])); acc(hi_bf(v[e])); }
+      }
+    } else if (VEC) {           // 4 fp32 per lane per load
+      const float4* p = (const float4*)(lf + base);
+      for (int q = lane; q < (K >> 2); q += 64) {
+        const float4 v = p[q];
+        acc(v.x); acc(v.y); acc(v.z); acc(v.w);
+      }
+    } else {
+      for (int k = lane; k < K; k += 64) acc(lb ? bf2f(lb[base + k]) : lf[base + k]);
     }
+    const float m_all = wave_max(mx);
+    se = (mx == -INFINITY) ? 0.f : se * __expf(mx - m_all);
+    const float s_all = wave_sum(se);
+    const float lse = m_all + __logf(s_all);
+    const int tgt = (int)(labels[row] - label_base);
+    if (lane == 0) {
+      const float xt = (tgt >= 0 && tgt < K) ? (lb ? bf2f(lb[base + tgt]) : lf[base + tgt]) : lse;
+      my_loss += (lse - xt) * grad_scale;
+    }
+    if (db || df) {
+      const float inv = 1.f / s_all;
+      if (VEC && lb && db) {
+        const v4u* p = (const v4u*)(lb + base);
+        v4u* o = (v4u*)(db + base);
+        for (int q = lane; q < (K >> 3); q += 64) {
+          const v4u v = p[q];
+          v4u w;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int k = q * 8 + 2 * e;
+            const float g0 = (__expf(lo_bf(v[e]) - m_all) * inv - (k == tgt ? 1.f : 0.f)) * grad_scale;
+            const float g1 = (__expf(hi_bf(v[e]) - m_all) * inv - (k + 1 == tgt ? 1.f : 0.f)) * grad_scale;
+            w[e] = pack2bf(g0, g1);
+          }
+          o[q] = w;
+        }
+      } else if (VEC && !lb && df) {
+        const float4* p = (const float4*)(lf + base);
+        float4* o = (float4*)(df + base);
+        for (int q = lane; q < (K >> 2); q += 64) {
+          const float4 v = p[q];
+          const int k = q * 4;
+          float4 g;
+          g.x = (__expf(v.x - m_all) * inv - (k == tgt ? 1.f : 0.f)) * grad_scale;
+          g.y = (__expf(v.y - m_all) * inv - (k + 1 == tgt ? 1.f : 0.f)) * grad_scale;
+          g.z = (__expf(v.z - m_all) * inv - (k + 2 == tgt ? 1.f : 0.f)) * grad_scale;
+          g.w = (__expf(v.w - m_all) * inv - (k + 3 == tgt ? 1.f : 0.f)) * grad_scale;
+          o[q] = g;
+        }
+      } else {
+        for (int k = lane; k < K; k += 64) {
+          const float x = lb ? bf2f(lb[base + k]) : lf[base + k];
+          const float g = (__expf(x - m_all) * inv - (k == tgt ? 1.f : 0.f)) * grad_scale;
+          if (db) db[base + k] = f2bf(g);
+          else df[base + k] = g;
+        }
+      }
+    }
+  }
+  if (loss) {
+    if (lane == 0) part[wave] = my_loss;
+    __syncthreads();
+    if (threadIdx.x == 0) atomicAdd(loss, part[0] + part[1] + part[2] + part[3]);
   }
 }
 
@@ -445,7 +504,12 @@ void bigdl_avgpool_bwd(const uint16_t* dy, uint16_t* dx, int N, int H, int W, in
 }
 void bigdl_softmax_xent(const uint16_t* lb, const float* lf, const float* labels, float* loss, uint16_t* db, float* df,
                         int B, int K, float label_base, float grad_scale, hipStream_t st) {
-  softmax_xent_kernel<<<(B + 3) / 4, 256, 0, st>>>(lb, lf, labels, loss, db, df, B, K, label_base, grad_scale);
+  const int blocks = std::min((B + 3) / 4, 2048);
+  const bool vec = lb ? (K % 8 == 0) : (K % 4 == 0);   // rows start 16-byte aligned when K is a multiple
+  if (vec)
+    softmax_xent_kernel<true><<<blocks, 256, 0, st>>>(lb, lf, labels, loss, db, df, B, K, label_base, grad_scale);
+  else
+    softmax_xent_kernel<false><<<blocks, 256, 0, st>>>(lb, lf, labels, loss, db, df, B, K, label_base, grad_scale);
   HIP_LAUNCH_CHECK();
 }
 void bigdl_sgd_step(float* w, const float* g, float* mom, uint16_t* w16, long n, const float* lr_dev, float lr,

@@ -148,4 +148,13 @@ void bigdl_resize_bilinear_bwd(const float* gy, float* gx, long NC, int H, int W
 void bigdl_log_softmax_fwd(const float* x, float* y, long rows, int cols, hipStream_t st);
 void bigdl_log_softmax_bwd(const float* y, const float* gy, float* gx, long rows, int cols, hipStream_t st);
 void bigdl_f32_to_bf16_rtz(const float* x, uint16_t* y, long n, hipStream_t st);
+
+// Fused LSTM steps (csrc/lstm.hip). W16 [4H][H] bf16 (gate blocks i, g, f, o), WT16 = W^T [H][4H] bf16.
+// Row strides: xg/h_out/acts/dout/dg_out rows are batch rows (ldx, ldh, lda, ldd, ldg elements apart).
+int bigdl_lstm_fwd_step(const uint16_t* W16, const uint16_t* h16_prev, const float* xg, long ldx, const float* c_prev,
+                        float* c_out, float* h_out, long ldh, uint16_t* h16_out, float* acts, long lda, int B, int H,
+                        hipStream_t st);
+int bigdl_lstm_bwd_step(const uint16_t* WT16, const uint16_t* dg16_next, const float* dout, long ldd,
+                        const float* dh_ext, const float* acts, long lda, const float* c_prev, const float* c_t,
+                        float* dc, float* dg_out, long ldg, uint16_t* dg16_out, int B, int H, hipStream_t st);
 }

@@ -250,3 +250,25 @@ def test_regularizer_adds_decay():
     m.zeroGradParameters()
     m.backward(x, torch.zeros(4, 2))
     assert torch.allclose(m.gradWeight, 0.1 * m.weight)
+
+
+def test_time_distributed_criterion_flat_equals_per_step_loop():
+    """The batched (B*T rows) fast path must equal the reference per-time-step loop (TimeDistributedCriterion.scala)."""
+    torch.manual_seed(0)
+    for inner in [nn.CrossEntropyCriterion(), nn.ClassNLLCriterion(), nn.MSECriterion(),
+                  nn.CrossEntropyCriterion(sizeAverage=False)]:
+        for sa in (True, False):
+            x = torch.randn(3, 5, 7)
+            y = torch.randn(3, 5, 7) if isinstance(inner, nn.MSECriterion) else torch.randint(1, 8, (3, 5)).float()
+            if isinstance(inner, nn.ClassNLLCriterion):
+                x = torch.log_softmax(x, -1)
+            c = nn.TimeDistributedCriterion(inner, sa)
+            loss, g = c.forward(x, y), c.backward(x, y)
+            ref_l, ref_g = 0.0, []
+            for t in range(5):
+                ref_l = ref_l + inner.forward(x[:, t], y[:, t])
+                ref_g.append(inner.backward(x[:, t], y[:, t]))
+            ref_g = torch.stack(ref_g, 1)
+            if sa:
+                ref_l, ref_g = ref_l / 5, ref_g / 5
+            assert abs(float(loss - ref_l)) < 1e-5 and torch.allclose(g, ref_g, atol=1e-6)
