@@ -359,6 +359,16 @@ class DataSet:
         return ImageFrameDataSet(frame)
 
     @staticmethod
+    def SeqFileFolder():
+        from .seqfile import SeqFileFolder
+        return SeqFileFolder
+
+    @staticmethod
+    def ImageFolder():
+        from .seqfile import ImageFolder
+        return ImageFolder
+
+    @staticmethod
     def from_tensors(x, y=None, shuffle=True, distributed=False):
         samples = [Sample(x[i], None if y is None else y[i]) for i in range(x.shape[0])]
         return DataSet.rdd(samples, shuffle) if distributed else DataSet.array(samples, shuffle)

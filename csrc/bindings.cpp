@@ -478,7 +478,10 @@ void lstm_bwd_step(const Tensor& WT16, const OptT& dg16_next, const OptT& dout, 
 
 }  // namespace
 
+void register_host_runtime(pybind11::module& m);   // csrc/host_runtime.cpp
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  register_host_runtime(m);
   m.doc() = "bigdl_amd native HIP kernels for gfx950 (MI355X)";
   m.def("conv_nt", &conv_nt, py::arg("src"), py::arg("wt"), py::arg("out"), py::arg("bias"), py::arg("stats"),
         py::arg("geo"), py::arg("taps"), py::arg("relu"), py::arg("addend") = py::none());

@@ -56,7 +56,7 @@ class HipBuildExt(BuildExtension):
 
 ext = CppExtension(
     name="bigdl_amd._C",
-    sources=[os.path.join("csrc", "bindings.cpp")],
+    sources=[os.path.join("csrc", "bindings.cpp"), os.path.join("csrc", "host_runtime.cpp")],
     include_dirs=[os.path.join(HERE, "csrc"), os.path.join(ROCM, "include")],
     define_macros=[("__HIP_PLATFORM_AMD__", "1"), ("USE_ROCM", "1")],
     extra_compile_args=["-O3", "-std=c++17"],

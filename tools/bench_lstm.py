@@ -26,7 +26,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=64, help="per-GPU batch (sequences)")
+    ap.add_argument("--batch", type=int, default=128, help="per-GPU batch (sequences)")
     ap.add_argument("--seq", type=int, default=256)
     ap.add_argument("--hidden", type=int, default=1024)
     ap.add_argument("--vocab", type=int, default=10000)
