@@ -510,8 +510,14 @@ class AbstractModule(metaclass=_RecordInit):
         return node
 
     def toGraph(self, *startNodes):
+        """Graph over this module's leaf layers (containers flattened; reference Sequential/DynamicContainer
+        .toGraph). The layers are shared with this module, not copied."""
         from .graph import Graph, Input
 
+        if getattr(self, "modules", None):
+            from ..utils.intermediate import BlasToIR
+
+            return BlasToIR.convert(self).build("blas", share=True)
         inp = Input()
         out = self.inputs(inp)
         return Graph([inp], [out])

@@ -167,3 +167,23 @@ def test_zoo_models_gpu_match_cpu(name, shape):
     gpu.evaluate()
     x = torch.randn(*shape)
     assert _rel(gpu.forward(x.cuda()), cpu.forward(x)) < 5e-2
+
+
+def test_ir_dnn_inference_fusion_matches_cpu():
+    """IRToDnn: BN folded into conv weights + ReLU in the conv epilogue on the GPU engine vs the CPU model."""
+    from bigdl_amd.models.resnet import DatasetType, ResNet
+    from bigdl_amd.utils.intermediate import ConversionUtils
+
+    torch.manual_seed(0)
+    m = ResNet(10, 20, dataSet=DatasetType.CIFAR10)
+    for layer in m.flattened_layers():
+        if hasattr(layer, "runningMean"):
+            layer.runningMean.uniform_(-0.2, 0.2)
+            layer.runningVar.uniform_(0.8, 1.2)
+    m.evaluate()
+    x = torch.randn(8, 3, 32, 32)
+    ref = m.forward(x)
+    g = ConversionUtils.convert(m, "dnn", device="cuda", train=False)
+    out = g.forward(x.cuda()).float().cpu()
+    rel = ((out - ref).norm() / ref.norm()).item()
+    assert rel < 3e-2, rel
