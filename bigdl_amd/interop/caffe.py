@@ -507,15 +507,20 @@ def _layer_def(m, name, bottoms, tops):
         d["type"] = ["Pooling"]
         d["pooling_param"] = [{"pool": ["MAX" if isinstance(m, nn.SpatialMaxPooling) else "AVE"],
                                "kernel_h": [m.kH], "kernel_w": [m.kW], "stride_h": [m.dH], "stride_w": [m.dW],
-                               "pad_h": [m.padH], "pad_w": [m.padW]}]
+                               "pad_h": [m.padH], "pad_w": [m.padW],
+                               "round_mode": ["CEIL" if getattr(m, "ceilMode", False) else "FLOOR"]}]
     elif isinstance(m, nn.ReLU):
         d["type"] = ["ReLU"]
     elif isinstance(m, nn.Sigmoid):
         d["type"] = ["Sigmoid"]
     elif isinstance(m, nn.Tanh):
         d["type"] = ["TanH"]
-    elif isinstance(m, (nn.SoftMax, nn.LogSoftMax)):
+    elif isinstance(m, nn.SoftMax):
         d["type"] = ["Softmax"]
+    elif isinstance(m, nn.LogSoftMax):            # Softmax + Log (layer pair)
+        d["type"] = ["Softmax"]
+        log = {"name": [name + "_log"], "bottom": list(tops), "top": list(tops), "type": ["Log"]}
+        return [d, log]
     elif isinstance(m, nn.Dropout):
         d["type"] = ["Dropout"]
         d["dropout_param"] = [{"dropout_ratio": [float(m.p)]}]
@@ -525,7 +530,14 @@ def _layer_def(m, name, bottoms, tops):
     elif isinstance(m, nn.BatchNormalization):
         d["type"] = ["BatchNorm"]
         d["batch_norm_param"] = [{"eps": [float(m.eps)]}]
-        blobs = [m.runningMean, m.runningVar, torch.ones(1)]
+        d["blobs"] = [tensor_to_blob(b) for b in (m.runningMean, m.runningVar, torch.ones(1))]
+        if getattr(m, "weight", None) is None:
+            return d
+        # affine part as the Caffe-standard in-place Scale layer (gamma, beta)
+        sc = {"name": [name + "_scale"], "bottom": list(tops), "top": list(tops), "type": ["Scale"],
+              "scale_param": [{"bias_term": [m.bias is not None]}],
+              "blobs": [tensor_to_blob(b) for b in ([m.weight] + ([m.bias] if m.bias is not None else []))]}
+        return [d, sc]
     elif isinstance(m, nn.JoinTable):
         d["type"] = ["Concat"]
         d["concat_param"] = [{"axis": [m.dimension - 1]}]
@@ -547,29 +559,25 @@ def save_caffe(module, prototxtPath, modelPath, overwrite=False, input_shape=Non
         if os.path.exists(p) and not overwrite:
             raise FileExistsError(p)
     layers = []
-    if isinstance(module, nn.Graph):
-        names = {}
-        for n in module.order:
-            nm = n.element.getName()
-            names[n.id] = nm
-            if n in module.inputs_nodes and not n.prevs:
-                continue
-            d = _layer_def(n.element, nm, [names[p.id] for p in n.prevs], [nm])
-            if d is not None:
-                layers.append(d)
-        net_inputs = [names[n.id] for n in module.inputs_nodes]
-    else:
-        prev = "data"
-        net_inputs = ["data"]
-        for m in module.flattened_layers():
-            if m.modules_list():
-                continue
-            nm = m.getName()
-            d = _layer_def(m, nm, [prev], [nm])
-            if d is None:
-                continue
-            layers.append(d)
-            prev = nm
+    # containers (Sequential / ConcatTable / Concat / ...) are flattened into a graph of their leaf layers so
+    # branches keep their true bottoms (utils/intermediate BlasToIR)
+    g = module if isinstance(module, nn.Graph) else module.toGraph()
+    names = {}
+    for n in g.order:
+        nm = n.element.getName()
+        if n in g.inputs_nodes and not n.prevs:
+            names[n.id] = "data" if len(g.inputs_nodes) == 1 else nm
+            continue
+        bottoms = [names[p.id] for p in n.prevs]
+        d = _layer_def(n.element, nm, bottoms, [nm])
+        if d is None:
+            if len(bottoms) != 1:
+                raise ValueError(f"save_caffe: cannot express {n.element.getPrintName()} in Caffe")
+            names[n.id] = bottoms[0]            # pass-through (Identity, SelectTable of one input, ...)
+            continue
+        names[n.id] = nm
+        layers.extend(d if isinstance(d, list) else [d])
+    net_inputs = [names[n.id] for n in g.inputs_nodes]
     net = {"name": [module.getName()], "input": net_inputs, "layer": layers}
     if input_shape:
         net["input_dim"] = list(input_shape)

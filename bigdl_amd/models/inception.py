@@ -232,3 +232,113 @@ def Inception_v2(classNum):
     split2 = nn.Concat(2).add(out3).add(out2)
     split1 = nn.Concat(2).add(nn.Sequential().add(f2).add(split2)).add(out1)
     return nn.Sequential().add(f1).add(split1)
+
+
+# ---------------------------------------------------------------------------------------------- Inception-v3
+# Inception-v3 (Szegedy et al. 2015, "Rethinking the Inception Architecture"), the model of BASELINE config 4
+# (the reference ships v1 / v2 builders and loads v3 through its Caffe / TF importers). Every convolution is
+# conv (no bias) + BatchNorm(eps=1e-3) + ReLU; factorised 1x7 / 7x1 and 1x3 / 3x1 kernels run on the same
+# implicit-GEMM conv kernels as square ones. Input 3 x 299 x 299.
+def _cbr3(cin, cout, kh, kw, sh=1, sw=1, ph=0, pw=0, name=""):
+    s = nn.Sequential()
+    s.add(nn.SpatialConvolution(cin, cout, kw, kh, sw, sh, pw, ph, withBias=False)
+          .setInitMethod(nn.Xavier(), nn.Zeros()).setName(name + "conv"))
+    s.add(nn.SpatialBatchNormalization(cout, 1e-3).setName(name + "bn"))
+    s.add(nn.ReLU(True).setName(name + "relu"))
+    return s
+
+
+def _branch(*mods):
+    s = nn.Sequential()
+    for m in mods:
+        s.add(m)
+    return s
+
+
+def _inception_a(cin, pool_features, p):
+    c = nn.Concat(2)
+    c.add(_cbr3(cin, 64, 1, 1, name=p + "b1x1_"))
+    c.add(_branch(_cbr3(cin, 48, 1, 1, name=p + "b5x5_1_"), _cbr3(48, 64, 5, 5, ph=2, pw=2, name=p + "b5x5_2_")))
+    c.add(_branch(_cbr3(cin, 64, 1, 1, name=p + "b3x3dbl_1_"), _cbr3(64, 96, 3, 3, ph=1, pw=1, name=p + "b3x3dbl_2_"),
+                  _cbr3(96, 96, 3, 3, ph=1, pw=1, name=p + "b3x3dbl_3_")))
+    c.add(_branch(nn.SpatialAveragePooling(3, 3, 1, 1, 1, 1).setName(p + "pool"),
+                  _cbr3(cin, pool_features, 1, 1, name=p + "bpool_")))
+    return c.setName(p + "concat")
+
+
+def _inception_b(cin, p):
+    c = nn.Concat(2)
+    c.add(_cbr3(cin, 384, 3, 3, 2, 2, name=p + "b3x3_"))
+    c.add(_branch(_cbr3(cin, 64, 1, 1, name=p + "b3x3dbl_1_"), _cbr3(64, 96, 3, 3, ph=1, pw=1, name=p + "b3x3dbl_2_"),
+                  _cbr3(96, 96, 3, 3, 2, 2, name=p + "b3x3dbl_3_")))
+    c.add(nn.SpatialMaxPooling(3, 3, 2, 2).setName(p + "pool"))
+    return c.setName(p + "concat")
+
+
+def _inception_c(cin, c7, p):
+    c = nn.Concat(2)
+    c.add(_cbr3(cin, 192, 1, 1, name=p + "b1x1_"))
+    c.add(_branch(_cbr3(cin, c7, 1, 1, name=p + "b7x7_1_"), _cbr3(c7, c7, 1, 7, pw=3, name=p + "b7x7_2_"),
+                  _cbr3(c7, 192, 7, 1, ph=3, name=p + "b7x7_3_")))
+    c.add(_branch(_cbr3(cin, c7, 1, 1, name=p + "b7x7dbl_1_"), _cbr3(c7, c7, 7, 1, ph=3, name=p + "b7x7dbl_2_"),
+                  _cbr3(c7, c7, 1, 7, pw=3, name=p + "b7x7dbl_3_"), _cbr3(c7, c7, 7, 1, ph=3, name=p + "b7x7dbl_4_"),
+                  _cbr3(c7, 192, 1, 7, pw=3, name=p + "b7x7dbl_5_")))
+    c.add(_branch(nn.SpatialAveragePooling(3, 3, 1, 1, 1, 1).setName(p + "pool"),
+                  _cbr3(cin, 192, 1, 1, name=p + "bpool_")))
+    return c.setName(p + "concat")
+
+
+def _inception_d(cin, p):
+    c = nn.Concat(2)
+    c.add(_branch(_cbr3(cin, 192, 1, 1, name=p + "b3x3_1_"), _cbr3(192, 320, 3, 3, 2, 2, name=p + "b3x3_2_")))
+    c.add(_branch(_cbr3(cin, 192, 1, 1, name=p + "b7x7x3_1_"), _cbr3(192, 192, 1, 7, pw=3, name=p + "b7x7x3_2_"),
+                  _cbr3(192, 192, 7, 1, ph=3, name=p + "b7x7x3_3_"), _cbr3(192, 192, 3, 3, 2, 2, name=p + "b7x7x3_4_")))
+    c.add(nn.SpatialMaxPooling(3, 3, 2, 2).setName(p + "pool"))
+    return c.setName(p + "concat")
+
+
+def _inception_e(cin, p):
+    c = nn.Concat(2)
+    c.add(_cbr3(cin, 320, 1, 1, name=p + "b1x1_"))
+    b3 = nn.Sequential().add(_cbr3(cin, 384, 1, 1, name=p + "b3x3_1_"))
+    b3.add(nn.Concat(2).add(_cbr3(384, 384, 1, 3, pw=1, name=p + "b3x3_2a_"))
+           .add(_cbr3(384, 384, 3, 1, ph=1, name=p + "b3x3_2b_")))
+    c.add(b3)
+    bd = nn.Sequential().add(_cbr3(cin, 448, 1, 1, name=p + "b3x3dbl_1_"))
+    bd.add(_cbr3(448, 384, 3, 3, ph=1, pw=1, name=p + "b3x3dbl_2_"))
+    bd.add(nn.Concat(2).add(_cbr3(384, 384, 1, 3, pw=1, name=p + "b3x3dbl_3a_"))
+           .add(_cbr3(384, 384, 3, 1, ph=1, name=p + "b3x3dbl_3b_")))
+    c.add(bd)
+    c.add(_branch(nn.SpatialAveragePooling(3, 3, 1, 1, 1, 1).setName(p + "pool"),
+                  _cbr3(cin, 192, 1, 1, name=p + "bpool_")))
+    return c.setName(p + "concat")
+
+
+def Inception_v3(classNum=1000, hasDropout=True):
+    """Inception-v3 for 299 x 299 inputs (no auxiliary classifier). 2048-channel 8 x 8 final map."""
+    m = nn.Sequential()
+    m.add(_cbr3(3, 32, 3, 3, 2, 2, name="Conv2d_1a_3x3_"))
+    m.add(_cbr3(32, 32, 3, 3, name="Conv2d_2a_3x3_"))
+    m.add(_cbr3(32, 64, 3, 3, ph=1, pw=1, name="Conv2d_2b_3x3_"))
+    m.add(nn.SpatialMaxPooling(3, 3, 2, 2).setName("MaxPool_3a_3x3"))
+    m.add(_cbr3(64, 80, 1, 1, name="Conv2d_3b_1x1_"))
+    m.add(_cbr3(80, 192, 3, 3, name="Conv2d_4a_3x3_"))
+    m.add(nn.SpatialMaxPooling(3, 3, 2, 2).setName("MaxPool_5a_3x3"))
+    m.add(_inception_a(192, 32, "Mixed_5b_"))
+    m.add(_inception_a(256, 64, "Mixed_5c_"))
+    m.add(_inception_a(288, 64, "Mixed_5d_"))
+    m.add(_inception_b(288, "Mixed_6a_"))
+    m.add(_inception_c(768, 128, "Mixed_6b_"))
+    m.add(_inception_c(768, 160, "Mixed_6c_"))
+    m.add(_inception_c(768, 160, "Mixed_6d_"))
+    m.add(_inception_c(768, 192, "Mixed_6e_"))
+    m.add(_inception_d(768, "Mixed_7a_"))
+    m.add(_inception_e(1280, "Mixed_7b_"))
+    m.add(_inception_e(2048, "Mixed_7c_"))
+    m.add(nn.SpatialAveragePooling(8, 8, 1, 1).setName("AvgPool_1a_8x8"))
+    if hasDropout:
+        m.add(nn.Dropout(0.2).setName("Dropout_1b"))
+    m.add(nn.View(2048).setNumInputDims(3))
+    m.add(nn.Linear(2048, classNum).setName("Logits"))
+    m.add(nn.LogSoftMax().setName("Predictions"))
+    return m

@@ -442,7 +442,16 @@ class AbstractModule(metaclass=_RecordInit):
 
     # ------------------------------------------------------------------ cloning / structure
     def cloneModule(self):
-        return copy.deepcopy(self)
+        # graphs of a few hundred nodes (imported Caffe / TF models) are linked node -> node, which a recursive
+        # deepcopy walks depth-first: give it room instead of failing at Python's default depth
+        import sys
+
+        old = sys.getrecursionlimit()
+        sys.setrecursionlimit(max(old, 100000))
+        try:
+            return copy.deepcopy(self)
+        finally:
+            sys.setrecursionlimit(old)
 
     def clone(self):
         return self.cloneModule()

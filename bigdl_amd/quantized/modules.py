@@ -55,14 +55,19 @@ def quantize_per_sample_ref(x):
     return q, amax / QMAX
 
 
-def quantize_act_gpu(x_nhwc, C, Cp):
-    """x_nhwc: contiguous [N, ..., C] bf16/fp32 device tensor -> (q int8 [N, P, Cp], scale fp32 [N])."""
+def quantize_act_gpu(x_nhwc, C, Cp, static_amax=None):
+    """x_nhwc: contiguous [N, ..., C] bf16/fp32 device tensor -> (q int8 [N, P, Cp], scale fp32 [N]).
+    ``static_amax`` (a calibrated range, MklInt8Convertible-style) replaces the per-sample abs-max pass."""
     N = x_nhwc.shape[0]
     P = x_nhwc.numel() // (N * C)
     q = torch.empty((N, P, Cp), dtype=torch.int8, device=x_nhwc.device)
-    amax = torch.empty(N, dtype=torch.float32, device=x_nhwc.device)
     scale = torch.empty(N, dtype=torch.float32, device=x_nhwc.device)
-    native.get().quantize_act(x_nhwc, q, amax, scale, N, P, C, Cp)
+    if static_amax is not None:
+        amax = torch.full((N,), float(static_amax), dtype=torch.float32, device=x_nhwc.device)
+        native.get().quantize_act(x_nhwc, q, amax, scale, N, P, C, Cp, True)
+    else:
+        amax = torch.empty(N, dtype=torch.float32, device=x_nhwc.device)
+        native.get().quantize_act(x_nhwc, q, amax, scale, N, P, C, Cp, False)
     return q, scale
 
 
@@ -135,7 +140,7 @@ class QuantizedLinear(QuantizedModule):
         B = x.shape[0]
         if x.dtype not in (BF16, torch.float32):
             x = x.float()
-        q, sx = quantize_act_gpu(x.contiguous(), self.inputSize, self.Kp)
+        q, sx = quantize_act_gpu(x.contiguous(), self.inputSize, self.Kp, getattr(self, "inputAmax", None))
         out = torch.empty(B, self.outputSize, dtype=torch.float32, device=x.device)
         geo = [B, 1, 1, self.Kp, 1, 1, 1, 1, self.Kp, self.outputSize, self.outputSize, 1, 1, 1, 1, 0, 0]
         native.get().conv_i8(q, self.weight, out, self.bias, sx, self.weightScale, geo, [0, 0, 0], False)
@@ -241,7 +246,7 @@ class QuantizedSpatialConvolution(QuantizedModule):
         ys = []
         for g in range(G):
             xg = xn if G == 1 else xn[..., g * cin:(g + 1) * cin]
-            q, sx = quantize_act_gpu(xg.contiguous(), cin, self.Cp)
+            q, sx = quantize_act_gpu(xg.contiguous(), cin, self.Cp, getattr(self, "inputAmax", None))
             y = torch.empty((N, cout, OH, OW), dtype=BF16, device=x.device, memory_format=CL)
             geo = [N, H, W, self.Cp, OH, OW, self.strideH, self.strideW, R * S * self.Cp, cout, cout,
                    OH, OW, 1, 1, 0, 0]

@@ -14,7 +14,7 @@ import torch
 
 from ..nn.activation import ReLU
 from ..nn.containers import Container, Sequential
-from ..nn.conv import SpatialConvolution, SpatialDilatedConvolution
+from ..nn.conv import SpatialConvolution, SpatialDilatedConvolution, SpatialShareConvolution
 from ..nn.graph import Graph
 from ..nn.linear import Linear
 from ..nn.normalization import BatchNormalization
@@ -43,7 +43,8 @@ def _q_conv(m):
 
 
 # registry keyed by exact class (reference registers exact class names, Quantizer.scala:68-75)
-REGISTRY = {Linear: _q_linear, SpatialConvolution: _q_conv, SpatialDilatedConvolution: _q_conv}
+REGISTRY = {Linear: _q_linear, SpatialConvolution: _q_conv, SpatialShareConvolution: _q_conv,
+            SpatialDilatedConvolution: _q_conv}
 
 
 def register(cls, fn):
@@ -73,7 +74,8 @@ def _fold_bn_into(prev, bn):
 
 
 def _foldable(a, b):
-    return (type(a) in (SpatialConvolution, SpatialDilatedConvolution, Linear) and isinstance(b, BatchNormalization)
+    return (type(a) in (SpatialConvolution, SpatialShareConvolution, SpatialDilatedConvolution, Linear)
+            and isinstance(b, BatchNormalization)
             and getattr(a, "nGroup", 1) == 1 and a.weight.shape[0] == b.nOutput and b.runningMean is not None)
 
 
@@ -81,7 +83,10 @@ def quantize_module(m, fold_bn=True):
     """Substitute quantizable layers inside ``m`` (in place where possible); returns the new module."""
     fn = REGISTRY.get(type(m))
     if fn is not None:
-        return fn(m)
+        q = fn(m)
+        if getattr(m, "_calib_amax", None) is not None:
+            q.inputAmax = m._calib_amax
+        return q
     if isinstance(m, Graph):
         for n in m.order:
             new = quantize_module(n.element, fold_bn)
@@ -116,12 +121,50 @@ def quantize_module(m, fold_bn=True):
     return m
 
 
-def quantize(model, fold_bn=True):
-    """Clone ``model`` and return its int8 inference version (reference Quantization.quantize)."""
+def calibrate(model, sample):
+    """Record the abs-max of every quantizable layer's input over ``sample`` (reference MklInt8Convertible
+    .calcScales with input mask 0: one per-tensor range per layer). The quantized layers then quantize their
+    input with that fixed range instead of a per-sample abs-max pass."""
+    layers = [m for m in model.flattened_layers() if type(m) in REGISTRY]
+    saved = {}
+    for m in layers:
+        orig = m.updateOutput
+
+        def hook(inp, _m=m, _orig=orig):
+            a = float(inp.detach().abs().max()) if isinstance(inp, torch.Tensor) else None
+            if a is not None:
+                _m._calib_amax = max(a, getattr(_m, "_calib_amax", 0.0) or 0.0)
+            return _orig(inp)
+        saved[id(m)] = orig
+        m.updateOutput = hook
+    try:
+        model.evaluate()
+        with torch.no_grad():
+            model.forward(sample)
+    finally:
+        for m in layers:
+            del m.updateOutput
+    return model
+
+
+def quantize(model, fold_bn=True, calibration=None):
+    """Clone ``model`` and return its int8 inference version (reference Quantization.quantize).
+
+    A Graph (e.g. a model imported from Caffe / TF) is first lowered through the engine-neutral IR so BatchNorm
+    folds into the preceding convolution there too. ``calibration`` (a sample input batch) switches the
+    activations to calibrated static ranges (see ``calibrate``)."""
+    from ..utils.intermediate import BlasToIR, IRToDnn
+
     dev = getattr(model, "_device", None)
     cloned = model.cloneModule()
+    if isinstance(cloned, Graph) and fold_bn:
+        cloned = IRToDnn.fuse(BlasToIR.convert(cloned)).build("blas", train=False)
+    if calibration is not None:
+        calibrate(cloned, calibration.to(getattr(cloned, "_device", torch.device("cpu"))))
     q = quantize_module(cloned, fold_bn)
     q.evaluate()
     if dev is not None and dev.type == "cuda":
         q.to(dev)
+    if isinstance(q, Graph):
+        IRToDnn.relu_plan(q)
     return q

@@ -261,6 +261,7 @@ class IRToDnn:
         from ..nn.conv import SpatialConvolution
         from ..nn.linear import Linear
         from ..nn.normalization import BatchNormalization
+        from ..quantized.modules import QuantizedSpatialConvolution
 
         users = {}
         for n in g.order:
@@ -269,7 +270,7 @@ class IRToDnn:
         for n in g.order:
             if isinstance(n.element, ReLU) and len(n.prevs) == 1:
                 p = n.prevs[0]
-                if isinstance(p.element, (SpatialConvolution, Linear, BatchNormalization)) and \
+                if isinstance(p.element, (SpatialConvolution, Linear, BatchNormalization, QuantizedSpatialConvolution)) and \
                         hasattr(p.element, "fuse_relu") and len(users.get(p.id, [])) == 1:
                     p.element.fuse_relu = True
                     n.element.passthrough = True

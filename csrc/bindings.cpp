@@ -240,7 +240,7 @@ void lstm_cell_bwd(const Tensor& act, const OptT& c_prev, const Tensor& c, const
 
 // int8 path (csrc/quant.hip)
 void quantize_act(const Tensor& x, const Tensor& q, const Tensor& amax, const Tensor& scale, int64_t N, int64_t P,
-                  int64_t C, int64_t Cp) {
+                  int64_t C, int64_t Cp, bool static_amax) {
   TORCH_CHECK(x.is_cuda() && x.is_contiguous(), "quantize_act: x must be a contiguous device tensor");
   const bool bf = x.scalar_type() == at::kBFloat16;
   TORCH_CHECK(bf || x.scalar_type() == at::kFloat, "quantize_act: x must be bf16 or fp32");
@@ -249,7 +249,7 @@ void quantize_act(const Tensor& x, const Tensor& q, const Tensor& amax, const Te
               "quantize_act: q must be int8 [N][P][Cp], Cp % 16 == 0");
   TORCH_CHECK(amax.numel() >= N && scale.numel() >= N && amax.scalar_type() == at::kFloat, "quantize_act: amax/scale");
   bigdl_quantize_act(x.data_ptr(), bf ? 1 : 0, q.data_ptr<int8_t>(), amax.data_ptr<float>(), scale.data_ptr<float>(),
-                     (int)N, P, (int)C, (int)Cp, stream());
+                     (int)N, P, (int)C, (int)Cp, static_amax ? 1 : 0, stream());
 }
 
 void conv_i8(const Tensor& src, const Tensor& wt, const Tensor& out, const OptT& bias, const Tensor& xscale,
@@ -512,7 +512,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("lstm_cell_fwd", &lstm_cell_fwd);
   m.def("lstm_cell_bwd", &lstm_cell_bwd);
   m.def("image_augment", &image_augment);
-  m.def("quantize_act", &quantize_act);
+  m.def("quantize_act", &quantize_act, py::arg("x"), py::arg("q"), py::arg("amax"), py::arg("scale"), py::arg("N"),
+        py::arg("P"), py::arg("C"), py::arg("Cp"), py::arg("static_amax") = false);
   m.def("conv_i8", &conv_i8);
   m.def("nms", &nms);
   m.def("roi_align_fwd", &roi_align_fwd);

@@ -107,7 +107,7 @@ void bigdl_lstm_cell_bwd(const float* act, const float* c_prev, const float* c, 
 // Int8 inference: per-sample activation quantization (x [N][P][C] bf16 or fp32 -> int8 [N][P][Cp]) and the
 // dequantizing implicit-GEMM conv on the i8 MFMA (src/wt are int8 images; out bf16 or fp32).
 int bigdl_quantize_act(const void* x, int is_bf16, int8_t* q, float* amax, float* scale, int N, long P, int C,
-                       int Cp, hipStream_t st);
+                       int Cp, int static_amax, hipStream_t st);
 int bigdl_conv_i8(const ConvArgs* a, const float* xscale, const float* wscale, int out_f32, hipStream_t st);
 
 void bigdl_set_conv_impl(int impl);

@@ -30,13 +30,25 @@ template <>
 __device__ __forceinline__ float ldf<uint16_t>(const uint16_t* p, long i) { return bf2f(p[i]); }
 
 // amax per sample: grid (blocks_per_sample, N); positive floats order like their bit patterns.
+// bf16 rows whose length is a multiple of 8 are read 16 bytes per lane (the activations of a 256-image batch
+// are 100+ MB: a 2-byte-per-lane scan was the int8 path's largest kernel).
 template <typename T>
 __global__ void amax_kernel(const T* __restrict__ x, long per_sample, float* __restrict__ amax) {
   const int n = blockIdx.y;
   const T* xs = x + (long)n * per_sample;
   float m = 0.f;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < per_sample; i += (long)gridDim.x * blockDim.x)
-    m = fmaxf(m, fabsf(ldf<T>(xs, i)));
+  if (sizeof(T) == 2 && (per_sample & 7) == 0) {
+    const v4u* v = reinterpret_cast<const v4u*>(xs);
+    const long n8 = per_sample >> 3;
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
+      const v4u u = v[i];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) m = fmaxf(m, fmaxf(fabsf(lo_bf(u[e])), fabsf(hi_bf(u[e]))));
+    }
+  } else {
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < per_sample; i += (long)gridDim.x * blockDim.x)
+      m = fmaxf(m, fabsf(ldf<T>(xs, i)));
+  }
   m = wave_max(m);
   __shared__ float red[16];
   const int w = threadIdx.x >> 6;
@@ -63,6 +75,30 @@ __global__ void quantize_kernel(const T* __restrict__ x, int8_t* __restrict__ q,
     int v = 0;
     if (c < C) v = __float2int_rn(ldf<T>(x, pix * C + c) * inv);
     q[i] = (int8_t)max(-127, min(127, v));
+    if (i < N) scale[i] = amax[i] / 127.f;
+  }
+}
+
+// C == Cp, C % 8 == 0, bf16: 8 channels per lane, one 16-byte load and one 8-byte store.
+__global__ void quantize8_bf16_kernel(const v4u* __restrict__ x, v2u* __restrict__ q, const float* __restrict__ amax,
+                                      float* __restrict__ scale, long per8, int N) {
+  const long total = (long)N * per8;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int n = (int)(i / per8);
+    const float a = amax[n];
+    const float inv = a > 0.f ? 127.f / a : 0.f;
+    const v4u u = x[i];
+    unsigned packed[2] = {0u, 0u};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int v0 = max(-127, min(127, __float2int_rn(lo_bf(u[e]) * inv)));
+      const int v1 = max(-127, min(127, __float2int_rn(hi_bf(u[e]) * inv)));
+      packed[e >> 1] |= ((unsigned)(v0 & 0xff) | ((unsigned)(v1 & 0xff) << 8)) << (16 * (e & 1));
+    }
+    v2u o;
+    o[0] = packed[0];
+    o[1] = packed[1];
+    q[i] = o;
     if (i < N) scale[i] = amax[i] / 127.f;
   }
 }
@@ -215,13 +251,22 @@ __global__ __launch_bounds__(256, 2) void conv_i8_kernel(ConvArgs a, const float
 extern "C" {
 
 int bigdl_quantize_act(const void* x, int is_bf16, int8_t* q, float* amax, float* scale, int N, long P, int C,
-                       int Cp, hipStream_t st) {
-  (void)hipMemsetAsync(amax, 0, sizeof(float) * N, st);
+                       int Cp, int static_amax, hipStream_t st) {
   const long per = P * C;
-  const int bx = (int)std::min<long>((per + 255) / 256, 256);
-  dim3 g1(bx, N);
-  if (is_bf16) amax_kernel<uint16_t><<<g1, 256, 0, st>>>((const uint16_t*)x, per, amax);
-  else amax_kernel<float><<<g1, 256, 0, st>>>((const float*)x, per, amax);
+  if (!static_amax) {            // dynamic per-sample range; with static_amax the caller filled amax (calibrated)
+    (void)hipMemsetAsync(amax, 0, sizeof(float) * N, st);
+    const int bx = (int)std::min<long>((per / (is_bf16 && (per & 7) == 0 ? 8 : 1) + 255) / 256, 256);
+    dim3 g1(bx > 0 ? bx : 1, N);
+    if (is_bf16) amax_kernel<uint16_t><<<g1, 256, 0, st>>>((const uint16_t*)x, per, amax);
+    else amax_kernel<float><<<g1, 256, 0, st>>>((const float*)x, per, amax);
+  }
+  if (is_bf16 && C == Cp && (C & 7) == 0) {
+    const long per8 = per >> 3, total8 = (long)N * per8;
+    const int blocks = (int)std::min<long>((total8 + 255) / 256, 16384);
+    quantize8_bf16_kernel<<<blocks, 256, 0, st>>>((const v4u*)x, (v2u*)q, amax, scale, per8, N);
+    HIP_LAUNCH_CHECK();
+    return 0;
+  }
   const long total = (long)N * P * Cp;
   const int blocks = (int)std::min<long>((total + 255) / 256, 16384);
   if (is_bf16) quantize_kernel<uint16_t><<<blocks, 256, 0, st>>>((const uint16_t*)x, q, amax, scale, P, C, Cp, N);

@@ -187,3 +187,18 @@ def test_ir_dnn_inference_fusion_matches_cpu():
     out = g.forward(x.cuda()).float().cpu()
     rel = ((out - ref).norm() / ref.norm()).item()
     assert rel < 3e-2, rel
+
+
+def test_inception_v3_gpu_matches_cpu():
+    """Inception-v3 (factorised 1x7 / 7x1 / 1x3 / 3x1 kernels, avg-pool branches) on the GPU engine vs CPU fp32."""
+    from bigdl_amd.models.inception import Inception_v3
+
+    torch.manual_seed(0)
+    m = Inception_v3(100)
+    m.evaluate()
+    x = torch.randn(2, 3, 299, 299)
+    ref = m.forward(x)
+    g = copy.deepcopy(m).to("cuda")
+    out = g.forward(x.cuda()).float().cpu()
+    rel = ((out.exp() - ref.exp()).norm() / ref.exp().norm()).item()
+    assert rel < 3e-2, rel

@@ -141,3 +141,23 @@ def test_graph_quantize_and_serialize(tmp_path):
     from bigdl_amd.nn.module import Module
     q3 = Module.loadModule(p)
     assert torch.equal(q3.forward(x), y)
+
+
+def test_quantize_graph_folds_bn_and_calibrates():
+    """A Graph (e.g. Caffe-imported) quantizes with BN folded through the IR; calibration sets static ranges
+    (MklInt8Convertible.calcScales analogue) on every quantized layer."""
+    import torch
+    from bigdl_amd.models.resnet import DatasetType, ResNet
+    from bigdl_amd.quantized.quantizer import quantize
+
+    torch.manual_seed(0)
+    m = ResNet(10, 20, dataSet=DatasetType.CIFAR10)
+    m.evaluate()
+    x = torch.randn(4, 3, 32, 32)
+    ref = m.forward(x)
+    q = quantize(m.toGraph(), calibration=x)
+    qs = [l for l in q.flattened_layers() if "Quantized" in type(l).__name__]
+    assert len(qs) == 22 and all(getattr(l, "inputAmax", None) is not None for l in qs)
+    assert not any(type(l).__name__ == "SpatialBatchNormalization" for l in q.flattened_layers())
+    out = q.forward(x)
+    assert ((out - ref).norm() / ref.norm()).item() < 5e-2
