@@ -159,8 +159,10 @@ def quantize(model, fold_bn=True, calibration=None):
     cloned = model.cloneModule()
     if isinstance(cloned, Graph) and fold_bn:
         cloned = IRToDnn.fuse(BlasToIR.convert(cloned)).build("blas", train=False)
+        if dev is not None:
+            cloned.to(dev)            # rebuilt IR layers start on the CPU; kept general layers are on dev
     if calibration is not None:
-        calibrate(cloned, calibration.to(getattr(cloned, "_device", torch.device("cpu"))))
+        calibrate(cloned, calibration.to(dev if dev is not None else torch.device("cpu")))
     q = quantize_module(cloned, fold_bn)
     q.evaluate()
     if dev is not None and dev.type == "cuda":
