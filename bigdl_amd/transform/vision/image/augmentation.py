@@ -299,14 +299,19 @@ class Crop(FeatureTransformer):
     def transformMat(self, f):
         m = f.opencvMat()
         h, w = m.shape[:2]
-        x1, y1, x2, y2 = self.box(f)
+        x1, y1, x2, y2 = self._last_box = self.box(f)
         if self.normalized:
             x1, x2, y1, y2 = x1 * w, x2 * w, y1 * h, y2 * h
         if self.isClip:
             x1, x2 = max(0.0, min(x1, w)), max(0.0, min(x2, w))
             y1, y2 = max(0.0, min(y1, h)), max(0.0, min(y2, h))
-        x1, y1, x2, y2 = int(x1), int(y1), int(math.ceil(x2)), int(math.ceil(y2))
-        f[ImageFeature.mat] = m[y1:y2, x1:x2].contiguous()
+        # OpenCV Rect(x1, y1, width, height) with truncated float coordinates (Crop.scala transform)
+        rx, ry, rw, rh = int(x1), int(y1), int(x2 - x1), int(y2 - y1)
+        f[ImageFeature.mat] = m[ry:ry + rh, rx:rx + rw].contiguous()
+        if f.get(ImageFeature.label) is not None:      # the crop box, for RoiProject (Crop.scala:35-37)
+            from .roi import BoundingBox
+
+            f[ImageFeature.boundingBox] = BoundingBox(*self._last_box, normalized=self.normalized)
 
 
 class CenterCrop(Crop):
