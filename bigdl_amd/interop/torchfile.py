@@ -322,7 +322,10 @@ def from_module(m):
     if isinstance(m, (nn.Sequential, nn.ConcatTable, nn.Concat, nn.ParallelTable)):
         cls = {nn.Sequential: "nn.Sequential", nn.ConcatTable: "nn.ConcatTable", nn.Concat: "nn.Concat",
                nn.ParallelTable: "nn.ParallelTable"}[type(m)]
-        o = base(cls, modules={i + 1: from_module(c) for i, c in enumerate(m.modules)})
+        kids = list(m.modules)
+        if isinstance(m, nn.Sequential):
+            kids = _static_flattens(kids)
+        o = base(cls, modules={i + 1: from_module(c) for i, c in enumerate(kids)})
         if isinstance(m, nn.Concat):
             o["dimension"] = m.dimension
         return o
@@ -358,12 +361,53 @@ def from_module(m):
                     numInputDims=getattr(m, "numInputDims", None))
     if isinstance(m, nn.Reshape):
         return base("nn.Reshape", size=torch.tensor(list(m.size), dtype=torch.int64))
+    if isinstance(m, nn.InferReshape) and tuple(m.size) in ((0, -1), (-1,)) and (tuple(m.size) == (0, -1) or
+                                                                                 m.batchMode):
+        # Caffe Flatten of a [N, C, H, W] blob: per-sample flatten = nn.View(-1) over 3 input dims
+        return base("nn.View", size=torch.tensor([-1], dtype=torch.int64), numInputDims=3)
     raise ValueError(f"cannot save {type(m).__name__} to t7")
+
+
+def _first_linear(m):
+    while True:
+        if isinstance(m, nn.Linear):
+            return m
+        mods = getattr(m, "modules", None)
+        if not mods or isinstance(m, (nn.ConcatTable, nn.Concat, nn.ParallelTable)):
+            return None
+        m = mods[0]
+
+
+def _static_flattens(mods):
+    """Torch7 nn has no shape-inferring flatten: an InferReshape(0, -1) (Caffe Flatten / InnerProduct input)
+    whose consumer is a Linear becomes nn.Reshape(inputSize), which Torch7 applies per sample."""
+    out = list(mods)
+    for i, m in enumerate(out):
+        if isinstance(m, nn.InferReshape) and tuple(m.size) == (0, -1) and i + 1 < len(out):
+            lin = _first_linear(out[i + 1])
+            if lin is not None:
+                out[i] = nn.Reshape([lin.inputSize])
+    return out
+
+
+def _chain_to_sequential(g):
+    """A Graph that is a single chain (e.g. an imported Caffe net without branches) as a Sequential; Torch7 nn
+    has no graph container."""
+    seq = nn.Sequential()
+    for n in g.order:
+        if len(n.prevs) > 1 or len(n.nexts) > 1:
+            raise ValueError("cannot save a branching Graph to t7 (Torch7 nn has no graph container)")
+        if n in g.inputs_nodes and not n.prevs:
+            continue
+        seq.add(n.element)
+    return seq
 
 
 def save_torch(obj, path, overWrite=False):
     if os.path.exists(path) and not overWrite:
         raise FileExistsError(path)
+    if isinstance(obj, nn.Graph):
+        obj = _chain_to_sequential(obj)
     if isinstance(obj, nn.AbstractModule):
         obj = from_module(obj)
     write_t7(path, obj)
