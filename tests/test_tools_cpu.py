@@ -57,4 +57,5 @@ def test_logger_filter_routes_third_party_to_file(tmp_path, monkeypatch):
             lg.removeHandler(h)
             h.close()
         lg.propagate = True
+        lg.setLevel(logging.NOTSET)
     assert "third-party message" in text and "framework message" in text
