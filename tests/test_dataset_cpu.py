@@ -133,3 +133,15 @@ def test_text_pipeline():
     s = list(D.LabeledSentenceToSample(dic.getVocabSize(), fixDataLength=7, fixLabelLength=7)(iter(ls)))
     assert s[0].feature().shape == (7, 6) and s[0].label().shape == (7,)
     assert float(s[0].label().min()) >= 1
+
+
+def test_row_transformer_atomic_and_numeric():
+    import pandas as pd
+    from bigdl_amd.dataset.datamining import RowTransformer
+
+    df = pd.DataFrame({"name": ["a", "b"], "x": [1.0, 3.0], "y": [2, 4], "z": [0.5, 0.25]})
+    rows = [r for _, r in df.iterrows()]
+    t = list(RowTransformer.atomicWithNumeric(["name"], {"xy": ["x", "y"], "z": ["z"]}).apply(iter(rows)))
+    assert t[1]["name"] == ["b"] and t[1]["xy"].tolist() == [3.0, 4.0] and t[0]["z"].tolist() == [0.5]
+    allnum = list(RowTransformer.numeric().apply(iter([{"a": 1, "b": 2.5, "c": "s"}])))
+    assert allnum[0]["all"].tolist() == [1.0, 2.5]
