@@ -46,6 +46,7 @@ def main():
         print("bench.py: --gpus > 1 requires torch.distributed.run (one process per GPU)", file=sys.stderr)
         sys.exit(2)
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    local = local % max(1, torch.cuda.device_count())   # ranks > devices only in single-GPU rehearsals
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 

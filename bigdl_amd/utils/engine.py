@@ -69,6 +69,8 @@ class _Engine:
         if td.is_initialized():
             return
         backend = "nccl" if (self.engine_type == EngineType.GPU and torch.cuda.is_available()) else "gloo"
+        # test hook: BIGDL_DIST_BACKEND=gloo runs several ranks on one GPU (RCCL refuses duplicate devices)
+        backend = os.environ.get("BIGDL_DIST_BACKEND", backend)
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29500")
         if backend == "nccl":
