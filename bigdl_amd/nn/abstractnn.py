@@ -568,6 +568,25 @@ class AbstractModule(metaclass=_RecordInit):
 
         return Predictor(self, batchSize).predictClass(dataset)
 
+    # ------------------------------------------------------------------ int8 calibration (MklInt8Convertible)
+    def calcScales(self, sample):
+        """Record calibrated activation ranges of every quantizable layer over ``sample``
+        (S/nn/MklInt8Convertible.scala:53); a later ``quantize()`` uses them as static ranges."""
+        from ..quantized.quantizer import calibrate
+
+        calibrate(self, sample)
+        return self
+
+    def setInputDimMask(self, mask):
+        """Input scale granularity (0 = one per tensor, the only mode the int8 kernels use)."""
+        self._input_dim_mask = mask
+        return self
+
+    def setWeightDimMask(self, mask):
+        """Weight scale granularity (1 = per output channel, the only mode the int8 kernels use)."""
+        self._weight_dim_mask = mask
+        return self
+
     def quantize(self):
         from ..quantized.quantizer import quantize
 

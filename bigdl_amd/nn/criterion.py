@@ -463,4 +463,45 @@ class TransformerCriterion(AbstractCriterion):
         return self.it.backward(input, g) if self.it is not None else g
 
 
+
+
+def _regsplex(n):
+    """Vertices of a regular n-simplex (n+1 points in n dims, unit norm), ClassSimplexCriterion.regsplex."""
+    a = torch.zeros(n + 1, n, dtype=torch.float64)
+    for k in range(1, n + 1):
+        if k == 1:
+            a[0, 0] = 1.0
+        else:
+            v = a[k - 1, : k - 1].norm(2)
+            a[k - 1, k - 1] = torch.sqrt(1.0 - v * v)
+        c = (a[k - 1, k - 1] ** 2 - 1.0 - 1.0 / n) / a[k - 1, k - 1]
+        a[k:, k - 1] = c
+    return a
+
+
+class ClassSimplexCriterion(MSECriterion):
+    """MSE between the input and the class's vertex of a regular simplex embedding (reference
+    S/nn/ClassSimplexCriterion.scala: ``regsplex(nClasses - 1)`` padded to ``nClasses`` columns)."""
+
+    def __init__(self, nClasses):
+        super().__init__()
+        if nClasses <= 1:
+            raise ValueError("ClassSimplexCriterion: nClasses must be > 1")
+        self.nClasses = nClasses
+        simp = _regsplex(nClasses - 1)
+        self.simplex = torch.zeros(simp.shape[0], nClasses, dtype=torch.float64)
+        self.simplex[:, : simp.shape[1]] = simp
+
+    def _target(self, input, target):
+        t = target.reshape(-1).long() - 1
+        tb = self.simplex.to(input.device)[t].to(input.dtype)
+        if tb.numel() != input.numel():
+            raise ValueError(f"ClassSimplexCriterion: input has {input.numel()} elements, target embedding "
+                             f"{tb.numel()}")
+        return tb.reshape(input.shape)
+
+    def loss(self, input, target):
+        return super().loss(input, self._target(input, target))
+
+
 __all__ = [n for n in list(globals()) if n[0].isupper() and n not in ("F", "Table")]

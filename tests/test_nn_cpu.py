@@ -272,3 +272,43 @@ def test_time_distributed_criterion_flat_equals_per_step_loop():
             if sa:
                 ref_l, ref_g = ref_l / 5, ref_g / 5
             assert abs(float(loss - ref_l)) < 1e-5 and torch.allclose(g, ref_g, atol=1e-6)
+
+
+def test_class_simplex_criterion_embedding():
+    from bigdl_amd.nn.criterion import ClassSimplexCriterion
+
+    c = ClassSimplexCriterion(5)
+    emb = c.simplex
+    assert torch.allclose(emb.norm(dim=1), torch.ones(5, dtype=torch.float64))
+    gram = emb @ emb.t()
+    assert torch.allclose(gram[~torch.eye(5, dtype=torch.bool)], torch.full((20,), -0.25, dtype=torch.float64))
+    x, y = torch.randn(3, 5), torch.tensor([1.0, 3.0, 5.0])
+    loss = c.forward(x, y)
+    assert abs(float(loss) - float(((x.double() - emb[y.long() - 1]) ** 2).mean())) < 1e-6
+    assert c.backward(x, y).shape == x.shape
+
+
+def test_nn_primitive_im2col_vol2col_match_conv():
+    from bigdl_amd.nn import primitive as P
+
+    torch.manual_seed(0)
+    x, w = torch.randn(3, 7, 8), torch.randn(4, 3, 3, 3)
+    cols = P.im2col(x, 3, 3, 2, 1, 1, 1)
+    y = (w.reshape(4, -1) @ cols).reshape(4, P.out_size(7, 3, 1, 1), P.out_size(8, 3, 2, 1))
+    assert torch.allclose(y, torch.nn.functional.conv2d(x[None], w, stride=(1, 2), padding=1)[0], atol=1e-5)
+    r = torch.randn_like(cols)
+    assert torch.allclose((cols * r).sum(), (x * P.col2im(r, 3, 7, 8, 3, 3, 2, 1, 1, 1)).sum(), atol=1e-4)
+    v, wv = torch.randn(2, 4, 5, 6), torch.randn(5, 2, 2, 3, 3)
+    cv = P.vol2col(v, 2, 3, 3, 1, 1, 1, 0, 1, 1)
+    ref = torch.nn.functional.conv3d(v[None], wv, padding=(0, 1, 1))[0]
+    assert torch.allclose((wv.reshape(5, -1) @ cv).reshape(ref.shape), ref, atol=1e-4)
+
+
+def test_calc_scales_then_quantize_uses_static_ranges():
+    m = nn.Sequential().add(nn.SpatialConvolution(3, 8, 3, 3)).add(nn.ReLU()).add(nn.View(8 * 6 * 6)) \
+        .add(nn.Linear(288, 4))
+    x = torch.randn(2, 3, 8, 8)
+    m.calcScales(x)
+    q = m.quantize()
+    assert all(getattr(l, "inputAmax", None) is not None for l in q.flattened_layers()
+               if "Quantized" in type(l).__name__)
