@@ -108,10 +108,12 @@ class BatchNormalization(TensorModule):
             res = residual
             if res is not None and (res.dtype != BF16 or res.stride() != x.stride()):
                 res = res.to(BF16).contiguous(memory_format=CL if x.dim() == 4 else torch.contiguous_format)
-            y, sm, si = bnops.bn_forward_gpu(x, self.weight, self.bias, self.runningMean, self.runningVar, self.eps,
-                                              self.momentum, self.train, stats=stats, res=res,
-                                              relu=self.fuse_relu, sync_fn=self.sync_fn if self.train else None)
+            y, sm, si, aff = bnops.bn_forward_gpu(x, self.weight, self.bias, self.runningMean, self.runningVar,
+                                                   self.eps, self.momentum, self.train, stats=stats, res=res,
+                                                   relu=self.fuse_relu, sync_fn=self.sync_fn if self.train else None)
             self.saveMean, self.saveStd = sm, si
+            # without a residual the ReLU mask is a function of x: backward recomputes it from (scale, shift)
+            self._aff = aff if (self.fuse_relu and res is None) else None
             self._xin = x
             return self._from_nchw(y)
         xf = x.float()
@@ -135,13 +137,14 @@ class BatchNormalization(TensorModule):
         x = self._xin
         if gz.dtype != BF16 or gz.stride() != x.stride():
             gz = gz.to(BF16).contiguous(memory_format=CL if x.dim() == 4 else torch.contiguous_format)
-        z = self._to_nchw(self.output) if self.fuse_relu else None
+        aff = getattr(self, "_aff", None)
+        z = self._to_nchw(self.output) if (self.fuse_relu and aff is None) else None
         direct = self._direct_grads()
         dg = self.gradWeight if direct else (torch.zeros_like(self.runningMean) if self.affine else None)
         db = self.gradBias if direct else (torch.zeros_like(self.runningMean) if self.affine else None)
         dx, dres = bnops.bn_backward_gpu(gz, z, x, self.saveMean, self.saveStd, self.weight, dg, db,
                                          training=self.train, need_dres=need_dres,
-                                         sync_fn=self.sync_fn if self.train else None)
+                                         sync_fn=self.sync_fn if self.train else None, aff=aff)
         if not direct and self.affine and not self._frozen:
             self.gradWeight.add_(dg, alpha=self.scaleW)
             self.gradBias.add_(db, alpha=self.scaleB)

@@ -17,9 +17,40 @@ def stat_slots():
     return native.get().STAT_SLOTS
 
 
+class _StatsArena:
+    """One zeroed buffer per training step for every BN statistics / gradient-reduction slot array: a single
+    memset replaces ~100 small fills per ResNet-50 step. Slices are handed out in call order, so offsets are the
+    same every step (safe inside a captured HIP graph). Outside begin()/end() new_stats falls back to zeros."""
+
+    def __init__(self):
+        self.buf, self.off, self.active, self.need = None, 0, False, 0
+
+    def begin(self, device):
+        if self.need and (self.buf is None or self.buf.numel() < self.need or self.buf.device != device):
+            self.buf = torch.empty(self.need, dtype=torch.float32, device=device)
+        if self.buf is not None:
+            self.buf.zero_()
+        self.off, self.need, self.active = 0, 0, True
+
+    def end(self):
+        self.active = False
+
+    def take(self, n, device):
+        n_al = (n + 63) // 64 * 64
+        self.need += n_al
+        if self.active and self.buf is not None and self.buf.device == device and self.off + n_al <= self.buf.numel():
+            t = self.buf[self.off:self.off + n]
+            self.off += n_al
+            return t
+        return torch.zeros(n, dtype=torch.float32, device=device)
+
+
+ARENA = _StatsArena()
+
+
 def new_stats(C, device):
     """Zeroed [STAT_SLOTS][2][C] fp32 accumulation buffer (see csrc/batchnorm.hip)."""
-    return torch.zeros(stat_slots() * 2 * C, dtype=torch.float32, device=device)
+    return ARENA.take(stat_slots() * 2 * C, torch.device(device))
 
 
 def _reduce_slots_for_sync(buf, C, P, sync_fn):
@@ -31,7 +62,7 @@ def _reduce_slots_for_sync(buf, C, P, sync_fn):
 
 def bn_forward_gpu(x, gamma, beta, rmean, rvar, eps, momentum, training, stats=None, res=None, relu=False,
                    out=None, sync_fn=None):
-    """Returns (y, save_mean, save_invstd).
+    """Returns (y, save_mean, save_invstd, aff) with aff = [scale | shift] of the apply pass (fp32 [2C]).
 
     x: (N, C, H, W) bf16 channels_last (or (N, C) bf16 contiguous). ``stats`` may hold the slotted
     (sum, sumsq) already produced by the preceding conv epilogue; otherwise they are computed here.
@@ -43,8 +74,8 @@ def bn_forward_gpu(x, gamma, beta, rmean, rvar, eps, momentum, training, stats=N
     dev = x.device
     if out is None:
         out = torch.empty_like(x)
-    scale = torch.empty(C, dtype=torch.float32, device=dev)
-    shift = torch.empty(C, dtype=torch.float32, device=dev)
+    aff = torch.empty(2 * C, dtype=torch.float32, device=dev)
+    scale, shift = aff[:C], aff[C:]
     smean = torch.empty(C, dtype=torch.float32, device=dev)
     sinv = torch.empty(C, dtype=torch.float32, device=dev)
     nslots = stat_slots()
@@ -60,14 +91,15 @@ def bn_forward_gpu(x, gamma, beta, rmean, rvar, eps, momentum, training, stats=N
     C_.bn_finalize(stats, nslots, gamma, beta, rmean, rvar, smean, sinv, scale, shift, Ptot, C, float(eps),
                    float(momentum), bool(training))
     C_.bn_apply(x, scale, shift, res, out, P, C, bool(relu))
-    return out, smean, sinv
+    return out, smean, sinv, aff
 
 
 def bn_backward_gpu(dz, z, x, smean, sinv, gamma, dgamma, dbeta, training=True, need_dres=False, need_dx=True,
-                    sync_fn=None):
+                    sync_fn=None, aff=None):
     """Backward of y = relu?(bn(x) [+ res]).
 
-    dz: gradient w.r.t. the (post-relu) output; z: the forward output (ReLU mask) or None.
+    dz: gradient w.r.t. the (post-relu) output; z: the forward output (ReLU mask) or None. With z None and
+    ``aff`` (the forward's [scale | shift]) the ReLU mask is recomputed from x, so z is never read back.
     Returns (dx, dres) — dres is the gradient flowing into the residual branch (= masked dz).
     """
     C = x.shape[1]
@@ -76,14 +108,14 @@ def bn_backward_gpu(dz, z, x, smean, sinv, gamma, dgamma, dbeta, training=True, 
     red, nslots, Ptot = None, 0, P
     if training:
         red = new_stats(C, x.device)
-        C_.bn_bwd_reduce(dz, z, x, smean, red, P, C)
+        C_.bn_bwd_reduce(dz, z, x, smean, red, P, C, aff)
         nslots = stat_slots()
         if sync_fn is not None:
             red, nslots, Ptot = _reduce_slots_for_sync(red, C, P, sync_fn)
     coef = torch.empty(3 * C, dtype=torch.float32, device=x.device)
     dx = torch.empty_like(x) if need_dx else None
     dres = torch.empty_like(x) if need_dres else None
-    C_.bn_bwd_apply(dz, z, x, smean, sinv, gamma, red, nslots, coef, dx, dres, dgamma, dbeta, Ptot, C)
+    C_.bn_bwd_apply(dz, z, x, smean, sinv, gamma, red, nslots, coef, dx, dres, dgamma, dbeta, Ptot, C, aff)
     return dx, dres
 
 

@@ -141,9 +141,18 @@ class TrainStep:
                 self.comm.all_gather_weights(self.w)
 
     def step(self, x, y):
-        self.zero_grad()
-        loss = self.forward_backward(x, y)
-        self.sync_and_update(loss)
+        arena = None
+        if self.device.type == "cuda":
+            from ..ops.bn import ARENA as arena
+
+            arena.begin(self.device)
+        try:
+            self.zero_grad()
+            loss = self.forward_backward(x, y)
+            self.sync_and_update(loss)
+        finally:
+            if arena is not None:
+                arena.end()
         self.loss = loss
         return loss
 

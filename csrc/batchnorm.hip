@@ -20,10 +20,13 @@ namespace {
 // Generic per-channel reduction over P rows of C channels (C % 8 == 0).
 // MODE 0: stats     -> out[c] += x,          out[C+c] += x*x
 // MODE 1: bwd       -> out[c] += dy,         out[C+c] += dy*(x-mean)  with dy = dz * (z>0 ? 1 : 0 if z)
+// MODE 1 with z == nullptr and aff != nullptr: the ReLU mask is recomputed from x as x*scale + shift > 0 (the
+// exact fp32 expression of bn_apply_kernel), so the post-ReLU output is never read back (one pass less).
 template <int MODE>
 __global__ __launch_bounds__(256) void chan_reduce_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dz,
                                                           const bf16_t* __restrict__ z, const float* __restrict__ mean,
-                                                          float* __restrict__ out, long P, int C, long rows_per_block) {
+                                                          float* __restrict__ out, long P, int C, long rows_per_block,
+                                                          const float* __restrict__ aff) {
   __shared__ float sm[256 * 16];
   const int G = C >> 3;
   const int tid = threadIdx.x;
@@ -33,12 +36,17 @@ __global__ __launch_bounds__(256) void chan_reduce_kernel(const bf16_t* __restri
     const int gcount = min(256, G - gbase);
     const int rpi = 256 / gcount;          // rows per iteration
     const int g = gbase + tid % gcount, rsub = tid / gcount;
-    float a1[8], a2[8], mu[8];
+    float a1[8], a2[8], mu[8], sc[8], sh[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) { a1[e] = 0.f; a2[e] = 0.f; mu[e] = 0.f; }
+    for (int e = 0; e < 8; ++e) { a1[e] = 0.f; a2[e] = 0.f; mu[e] = 0.f; sc[e] = 0.f; sh[e] = 0.f; }
+    const bool xmask = MODE == 1 && z == nullptr && aff != nullptr;
     if (MODE == 1 && rsub < rpi) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) mu[e] = mean[g * 8 + e];
+      if (xmask) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { sc[e] = aff[g * 8 + e]; sh[e] = aff[C + g * 8 + e]; }
+      }
     }
     if (rsub < rpi) {
       for (long r = rbeg + rsub; r < rend; r += rpi) {
@@ -59,6 +67,10 @@ __global__ __launch_bounds__(256) void chan_reduce_kernel(const bf16_t* __restri
           for (int e = 0; e < 4; ++e) {
             float dl = lo_bf(vd[e]), dh = hi_bf(vd[e]);
             if (z) { if (!(lo_bf(vz[e]) > 0.f)) dl = 0.f; if (!(hi_bf(vz[e]) > 0.f)) dh = 0.f; }
+            if (xmask) {
+              if (!(lo_bf(vx[e]) * sc[2 * e] + sh[2 * e] > 0.f)) dl = 0.f;
+              if (!(hi_bf(vx[e]) * sc[2 * e + 1] + sh[2 * e + 1] > 0.f)) dh = 0.f;
+            }
             a1[2 * e] += dl; a1[2 * e + 1] += dh;
             a2[2 * e] += dl * (lo_bf(vx[e]) - mu[2 * e]);
             a2[2 * e + 1] += dh * (hi_bf(vx[e]) - mu[2 * e + 1]);
@@ -83,16 +95,36 @@ __global__ __launch_bounds__(256) void chan_reduce_kernel(const bf16_t* __restri
   }
 }
 
+// Slot sums for one channel by 32 lanes (one slot each) + shuffle reduction: the per-layer finalize / coefficient
+// kernels sit on the critical path between the big passes, and a serial 32-slot loop per thread made them
+// latency-bound (~12 us each, 100+ per ResNet-50 step). Two channels per wave, lanes 0-31 and 32-63.
+__device__ __forceinline__ void slot_sums(const float* __restrict__ red, int nslots, int C, int c, int sl, double& s1,
+                                          double& s2) {
+  s1 = 0.0;
+  s2 = 0.0;
+  for (int k = sl; k < nslots; k += 32) {
+    s1 += red[(size_t)k * 2 * C + c];
+    s2 += red[(size_t)k * 2 * C + C + c];
+  }
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) {
+    s1 += __shfl_xor(s1, o, 64);
+    s2 += __shfl_xor(s2, o, 64);
+  }
+}
+
 __global__ void bn_finalize_kernel(const float* __restrict__ stats, int nslots, const float* __restrict__ gamma,
                                    const float* __restrict__ beta, float* run_mean, float* run_var, float* save_mean,
                                    float* save_invstd, float* scale, float* shift, long P, int C, float eps,
                                    float momentum, int training) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  const int lane = threadIdx.x & 63, sl = lane & 31;
+  const int c = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 2 + (lane >> 5);
   if (c >= C) return;
   float mean, invstd;
   if (training) {
-    double s1 = 0.0, s2 = 0.0;
-    for (int k = 0; k < nslots; ++k) { s1 += stats[(size_t)k * 2 * C + c]; s2 += stats[(size_t)k * 2 * C + C + c]; }
+    double s1, s2;
+    slot_sums(stats, nslots, C, c, sl, s1, s2);
+    if (sl != 0) return;
     mean = (float)(s1 / (double)P);
     const float var = fmaxf((float)(s2 / (double)P - (double)mean * mean), 0.f);
     invstd = rsqrtf(var + eps);
@@ -104,6 +136,7 @@ __global__ void bn_finalize_kernel(const float* __restrict__ stats, int nslots, 
       run_var[c] = momentum * unbiased + (1.f - momentum) * run_var[c];
     }
   } else {
+    if (sl != 0) return;
     mean = run_mean[c];
     invstd = rsqrtf(run_var[c] + eps);
     if (save_mean) { save_mean[c] = mean; save_invstd[c] = invstd; }
@@ -113,19 +146,29 @@ __global__ void bn_finalize_kernel(const float* __restrict__ stats, int nslots, 
   shift[c] = b - mean * g * invstd;
 }
 
+// Channel-stationary mapping (also bn_bwd_apply_kernel): a thread owns one 8-channel group for its whole row
+// range, so its per-channel coefficients are loaded once instead of once per 16-byte granule, and the loop has
+// no 64-bit modulo. blockIdx.y walks channel groups in chunks of 256; rows of a block are [rbeg, rend).
 __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* __restrict__ x, const float* __restrict__ scale,
                                                        const float* __restrict__ shift, const bf16_t* __restrict__ res,
-                                                       bf16_t* __restrict__ y, long ngran, int C, int relu) {
+                                                       bf16_t* __restrict__ y, long P, int C, long rpb, int relu) {
   const int G = C >> 3;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < ngran; i += (long)gridDim.x * blockDim.x) {
-    const int c0 = (int)(i % G) * 8;
+  const int gbase = blockIdx.y * 256;
+  const int gcount = min(256, G - gbase);
+  const int rpi = 256 / gcount;
+  const int g = gbase + threadIdx.x % gcount, rsub = threadIdx.x / gcount;
+  if (rsub >= rpi) return;
+  const long rbeg = blockIdx.x * rpb, rend = min(P, rbeg + rpb);
+  const int c0 = g * 8;
+  const v4f s0 = *reinterpret_cast<const v4f*>(scale + c0), s1 = *reinterpret_cast<const v4f*>(scale + c0 + 4);
+  const v4f b0 = *reinterpret_cast<const v4f*>(shift + c0), b1 = *reinterpret_cast<const v4f*>(shift + c0 + 4);
+  const float sc[8] = {s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
+  const float sh[8] = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+  for (long r = rbeg + rsub; r < rend; r += rpi) {
+    const long i = r * G + g;
     const v4u vx = reinterpret_cast<const v4u*>(x)[i];
     v4u vr = {0u, 0u, 0u, 0u};
     if (res) vr = reinterpret_cast<const v4u*>(res)[i];
-    const v4f s0 = *reinterpret_cast<const v4f*>(scale + c0), s1 = *reinterpret_cast<const v4f*>(scale + c0 + 4);
-    const v4f b0 = *reinterpret_cast<const v4f*>(shift + c0), b1 = *reinterpret_cast<const v4f*>(shift + c0 + 4);
-    const float sc[8] = {s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
-    const float sh[8] = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
     v4u o;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -144,14 +187,16 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* __restrict_
 __global__ void bn_bwd_coeff_kernel(const float* __restrict__ red, int nslots, const float* __restrict__ mean,
                                     const float* __restrict__ invstd, const float* __restrict__ gamma,
                                     float* __restrict__ coef, float* dgamma, float* dbeta, long P, int C, int training) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  const int lane = threadIdx.x & 63, sl = lane & 31;
+  const int c = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 2 + (lane >> 5);
   if (c >= C) return;
+  double sdy = 0.0, sdyx = 0.0;
+  if (training) slot_sums(red, nslots, C, c, sl, sdy, sdyx);
+  if (sl != 0) return;
   const float is = invstd[c];
   const float g = gamma ? gamma[c] : 1.f;
   float A = g * is, B = 0.f, D = 0.f;
   if (training) {
-    double sdy = 0.0, sdyx = 0.0;
-    for (int k = 0; k < nslots; ++k) { sdy += red[(size_t)k * 2 * C + c]; sdyx += red[(size_t)k * 2 * C + C + c]; }
     const float mdy = (float)(sdy / (double)P);
     const float mdyx = (float)(sdyx / (double)P) * is;     // mean(dy * xhat)
     B = -g * is * is * mdyx;
@@ -177,24 +222,40 @@ __device__ __forceinline__ void load8(const float* p, float* v) {
 
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16_t* __restrict__ dz, const bf16_t* __restrict__ z,
                                                            const bf16_t* __restrict__ x, const float* __restrict__ coef,
-                                                           bf16_t* __restrict__ dx, bf16_t* __restrict__ dres, long ngran,
-                                                           int C) {
+                                                           bf16_t* __restrict__ dx, bf16_t* __restrict__ dres, long P,
+                                                           int C, long rpb, const float* __restrict__ aff) {
   const int G = C >> 3;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < ngran; i += (long)gridDim.x * blockDim.x) {
-    const int c0 = (int)(i % G) * 8;
+  const bool xmask = z == nullptr && aff != nullptr;   // ReLU mask from x*scale + shift (see chan_reduce_kernel)
+  const int gbase = blockIdx.y * 256;
+  const int gcount = min(256, G - gbase);
+  const int rpi = 256 / gcount;
+  const int g = gbase + threadIdx.x % gcount, rsub = threadIdx.x / gcount;
+  if (rsub >= rpi) return;
+  const long rbeg = blockIdx.x * rpb, rend = min(P, rbeg + rpb);
+  const int c0 = g * 8;
+  float A[8], B[8], D[8], S[8], T[8];
+  load8(coef + c0, A);
+  load8(coef + C + c0, B);
+  load8(coef + 2 * C + c0, D);
+  if (xmask) {
+    load8(aff + c0, S);
+    load8(aff + C + c0, T);
+  }
+  for (long r = rbeg + rsub; r < rend; r += rpi) {
+    const long i = r * G + g;
     const v4u vd = reinterpret_cast<const v4u*>(dz)[i];
     v4u vz = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
     if (z) vz = reinterpret_cast<const v4u*>(z)[i];
     const v4u vx = reinterpret_cast<const v4u*>(x)[i];
-    float A[8], B[8], D[8];
-    load8(coef + c0, A);
-    load8(coef + C + c0, B);
-    load8(coef + 2 * C + c0, D);
     v4u o, od;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       float d0 = lo_bf(vd[e]), d1 = hi_bf(vd[e]);
       if (z) { if (!(lo_bf(vz[e]) > 0.f)) d0 = 0.f; if (!(hi_bf(vz[e]) > 0.f)) d1 = 0.f; }
+      if (xmask) {
+        if (!(lo_bf(vx[e]) * S[2 * e] + T[2 * e] > 0.f)) d0 = 0.f;
+        if (!(hi_bf(vx[e]) * S[2 * e + 1] + T[2 * e + 1] > 0.f)) d1 = 0.f;
+      }
       const float r0 = A[2 * e] * d0 + B[2 * e] * lo_bf(vx[e]) + D[2 * e];
       const float r1 = A[2 * e + 1] * d1 + B[2 * e + 1] * hi_bf(vx[e]) + D[2 * e + 1];
       o[e] = pack2bf(r0, r1);
@@ -205,6 +266,23 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16_t* __restr
   }
 }
 
+// Grid of a channel-stationary elementwise pass: (row blocks, channel-group chunks); ~8 rows per thread.
+dim3 stationary_grid(long P, int C, long* rpb_out) {
+  const int G = C >> 3;
+  const int rpi = 256 / (G < 256 ? G : 256);
+  const int gy = (G + 255) / 256;
+  long rpb = (long)rpi * 8;
+  long bx = (P + rpb - 1) / rpb;
+  const long cap = 8192 / gy;
+  if (bx > cap) {
+    bx = cap;
+    rpb = (P + bx - 1) / bx;
+  }
+  if (bx < 1) bx = 1;
+  *rpb_out = rpb;
+  return dim3((unsigned)bx, (unsigned)gy);
+}
+
 int grid_for(long work, int per_block, int cap) {
   long g = (work + per_block - 1) / per_block;
   if (g > cap) g = cap;
@@ -213,7 +291,7 @@ int grid_for(long work, int per_block, int cap) {
 }
 
 void launch_reduce(int mode, const bf16_t* x, const bf16_t* dz, const bf16_t* z, const float* mean, float* out, long P,
-                   int C, hipStream_t st) {
+                   int C, hipStream_t st, const float* aff = nullptr) {
   const int G = C >> 3;
   const int rpi = 256 / (G < 256 ? G : 256);
   long blocks = (P + rpi * 16 - 1) / (rpi * 16);   // >= 16 rows per thread
@@ -221,8 +299,8 @@ void launch_reduce(int mode, const bf16_t* x, const bf16_t* dz, const bf16_t* z,
   if (blocks < 1) blocks = 1;
   const long rpb = (P + blocks - 1) / blocks;
   blocks = (P + rpb - 1) / rpb;
-  if (mode == 0) chan_reduce_kernel<0><<<(int)blocks, 256, 0, st>>>(x, dz, z, mean, out, P, C, rpb);
-  else chan_reduce_kernel<1><<<(int)blocks, 256, 0, st>>>(x, dz, z, mean, out, P, C, rpb);
+  if (mode == 0) chan_reduce_kernel<0><<<(int)blocks, 256, 0, st>>>(x, dz, z, mean, out, P, C, rpb, nullptr);
+  else chan_reduce_kernel<1><<<(int)blocks, 256, 0, st>>>(x, dz, z, mean, out, P, C, rpb, aff);
 }
 
 }  // namespace
@@ -237,8 +315,8 @@ void bigdl_bn_stats(const uint16_t* x, float* stats, long P, int C, hipStream_t 
 void bigdl_bn_finalize(const float* stats, int nslots, const float* gamma, const float* beta, float* run_mean,
                        float* run_var, float* save_mean, float* save_invstd, float* scale, float* shift, long P, int C,
                        float eps, float momentum, int training, hipStream_t st) {
-  bn_finalize_kernel<<<(C + 255) / 256, 256, 0, st>>>(stats, nslots, gamma, beta, run_mean, run_var, save_mean,
-                                                       save_invstd, scale, shift, P, C, eps, momentum, training);
+  bn_finalize_kernel<<<(C + 7) / 8, 256, 0, st>>>(stats, nslots, gamma, beta, run_mean, run_var, save_mean,
+                                                   save_invstd, scale, shift, P, C, eps, momentum, training);
   HIP_LAUNCH_CHECK();
 }
 
@@ -249,26 +327,29 @@ void bigdl_bn_slot_reduce(const float* in, int nslots, int C, float* out, hipStr
 
 void bigdl_bn_apply(const uint16_t* x, const float* scale, const float* shift, const uint16_t* res, uint16_t* y,
                     long P, int C, int relu, hipStream_t st) {
-  const long ngran = P * (C >> 3);
-  bn_apply_kernel<<<grid_for(ngran, 256, 8192), 256, 0, st>>>(x, scale, shift, res, y, ngran, C, relu);
+  long rpb = 0;
+  const dim3 grid = stationary_grid(P, C, &rpb);
+  bn_apply_kernel<<<grid, 256, 0, st>>>(x, scale, shift, res, y, P, C, rpb, relu);
   HIP_LAUNCH_CHECK();
 }
 
 void bigdl_bn_bwd_reduce(const uint16_t* dz, const uint16_t* z, const uint16_t* x, const float* mean, float* red,
-                         long P, int C, hipStream_t st) {
-  launch_reduce(1, x, dz, z, mean, red, P, C, st);
+                         long P, int C, const float* aff, hipStream_t st) {
+  launch_reduce(1, x, dz, z, mean, red, P, C, st, aff);
   HIP_LAUNCH_CHECK();
 }
 
 void bigdl_bn_bwd_apply(const uint16_t* dz, const uint16_t* z, const uint16_t* x, const float* mean,
                         const float* invstd, const float* gamma, const float* red, int nslots, float* coef,
                         uint16_t* dx, uint16_t* dres, float* dgamma, float* dbeta, long P, int C, int training,
-                        hipStream_t st) {
-  bn_bwd_coeff_kernel<<<(C + 255) / 256, 256, 0, st>>>(red, nslots, mean, invstd, gamma, coef, dgamma, dbeta, P, C,
-                                                        training);
-  const long ngran = P * (C >> 3);
-  if (dx || dres)
-    bn_bwd_apply_kernel<<<grid_for(ngran, 256, 8192), 256, 0, st>>>(dz, z, x, coef, dx, dres, ngran, C);
+                        const float* aff, hipStream_t st) {
+  bn_bwd_coeff_kernel<<<(C + 7) / 8, 256, 0, st>>>(red, nslots, mean, invstd, gamma, coef, dgamma, dbeta, P, C,
+                                                    training);
+  if (dx || dres) {
+    long rpb = 0;
+    const dim3 grid = stationary_grid(P, C, &rpb);
+    bn_bwd_apply_kernel<<<grid, 256, 0, st>>>(dz, z, x, coef, dx, dres, P, C, rpb, aff);
+  }
   HIP_LAUNCH_CHECK();
 }
 

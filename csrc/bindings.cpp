@@ -117,21 +117,23 @@ void bn_apply(const Tensor& x, const Tensor& scale, const Tensor& shift, const O
                  relu ? 1 : 0, stream());
 }
 void bn_bwd_reduce(const Tensor& dz, const OptT& z, const Tensor& x, const Tensor& mean, const Tensor& red, int64_t P,
-                   int64_t C) {
+                   int64_t C, const OptT& aff) {
   TORCH_CHECK(C % 8 == 0 && x.numel() == P * C && dz.numel() == P * C, "bn_bwd_reduce: shape");
   TORCH_CHECK(red.numel() >= BIGDL_STAT_SLOTS * 2 * C, "bn_bwd_reduce: red must hold STAT_SLOTS x 2C");
+  if (aff && aff->defined()) TORCH_CHECK(aff->numel() >= 2 * C && aff->is_contiguous(), "bn_bwd_reduce: aff is [2C]");
   bigdl_bn_bwd_reduce(cbf(dz, "dz"), ocbf(z, "z"), cbf(x, "x"), cf(mean, "mean"), mf(red, "red"), P, (int)C,
-                      stream());
+                      ocf(aff, "aff"), stream());
 }
 void bn_bwd_apply(const Tensor& dz, const OptT& z, const Tensor& x, const Tensor& mean, const Tensor& invstd,
                   const OptT& gamma, const OptT& red, int64_t nslots, const Tensor& coef, const OptT& dx,
-                  const OptT& dres, const OptT& dgamma, const OptT& dbeta, int64_t P, int64_t C) {
+                  const OptT& dres, const OptT& dgamma, const OptT& dbeta, int64_t P, int64_t C, const OptT& aff) {
   TORCH_CHECK(coef.numel() >= 3 * C, "bn_bwd_apply: coef size");
+  if (aff && aff->defined()) TORCH_CHECK(aff->numel() >= 2 * C && aff->is_contiguous(), "bn_bwd_apply: aff is [2C]");
   const bool training = red && red->defined();
   bigdl_bn_bwd_apply(cbf(dz, "dz"), ocbf(z, "z"), cbf(x, "x"), cf(mean, "mean"), cf(invstd, "invstd"),
                      ocf(gamma, "gamma"), ocf(red, "red"), (int)nslots, mf(coef, "coef"), ombf(dx, "dx"),
                      ombf(dres, "dres"), omf(dgamma, "dgamma"), omf(dbeta, "dbeta"), P, (int)C, training ? 1 : 0,
-                     stream());
+                     ocf(aff, "aff"), stream());
 }
 
 void relu_fwd(const Tensor& x, const Tensor& y) {
@@ -492,8 +494,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_apply", &bn_apply);
   m.def("bn_slot_reduce", &bn_slot_reduce);
   m.attr("STAT_SLOTS") = BIGDL_STAT_SLOTS;
-  m.def("bn_bwd_reduce", &bn_bwd_reduce);
-  m.def("bn_bwd_apply", &bn_bwd_apply);
+  m.def("bn_bwd_reduce", &bn_bwd_reduce, py::arg("dz"), py::arg("z"), py::arg("x"), py::arg("mean"), py::arg("red"),
+        py::arg("P"), py::arg("C"), py::arg("aff") = py::none());
+  m.def("bn_bwd_apply", &bn_bwd_apply, py::arg("dz"), py::arg("z"), py::arg("x"), py::arg("mean"), py::arg("invstd"),
+        py::arg("gamma"), py::arg("red"), py::arg("nslots"), py::arg("coef"), py::arg("dx"), py::arg("dres"),
+        py::arg("dgamma"), py::arg("dbeta"), py::arg("P"), py::arg("C"), py::arg("aff") = py::none());
   m.def("relu_fwd", &relu_fwd);
   m.def("relu_bwd", &relu_bwd);
   m.def("add_bf16", &add_bf16);

@@ -58,12 +58,13 @@ void bigdl_bn_finalize(const float* stats, int nslots, const float* gamma, const
 void bigdl_bn_slot_reduce(const float* in, int nslots, int C, float* out, hipStream_t st);
 void bigdl_bn_apply(const uint16_t* x, const float* scale, const float* shift, const uint16_t* res,
                     uint16_t* y, long P, int C, int relu, hipStream_t st);
+// aff (optional, [scale C | shift C] of the forward apply): with z == nullptr the ReLU mask is recomputed from x.
 void bigdl_bn_bwd_reduce(const uint16_t* dz, const uint16_t* z, const uint16_t* x, const float* mean,
-                         float* red, long P, int C, hipStream_t st);
+                         float* red, long P, int C, const float* aff, hipStream_t st);
 void bigdl_bn_bwd_apply(const uint16_t* dz, const uint16_t* z, const uint16_t* x, const float* mean,
                         const float* invstd, const float* gamma, const float* red, int nslots, float* coef,
                         uint16_t* dx, uint16_t* dres, float* dgamma, float* dbeta, long P, int C, int training,
-                        hipStream_t st);
+                        const float* aff, hipStream_t st);
 
 // elementwise
 void bigdl_relu_fwd(const uint16_t* x, uint16_t* y, long n, hipStream_t st);

@@ -136,7 +136,7 @@ def test_bn_fwd_bwd(res, relu):
     g = torch.rand(C, device=dev) + 0.5
     b = torch.randn(C, device=dev)
     rm, rv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
-    y, sm, si = bn.bn_forward_gpu(x, g, b, rm, rv, 1e-3, 0.1, True, res=r, relu=relu)
+    y, sm, si, aff = bn.bn_forward_gpu(x, g, b, rm, rv, 1e-3, 0.1, True, res=r, relu=relu)
     xr = x.float().requires_grad_(True)
     ref = F.batch_norm(xr, None, None, g, b, True, 0.1, 1e-3)
     if res:
@@ -159,6 +159,10 @@ def test_bn_fwd_bwd(res, relu):
         out2 = torch.relu(out2)
     out2.backward(gzb.float())
     assert _rel(dx, xr2.grad) < 2e-2
+    if relu and not res:       # mask recomputed from x*scale + shift instead of reading y back
+        dg2, db2 = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
+        dx2, _ = bn.bn_backward_gpu(gzb, None, x, sm, si, g, dg2, db2, aff=aff)
+        assert _rel(dx2, dx) < 1e-3 and _rel(dg2, dg) < 1e-3 and _rel(db2, dbt) < 1e-3
     if res:
         mask = (y.float() > 0).float() if relu else 1.0
         assert _rel(dres, gzb.float() * mask) < 1e-2
