@@ -1,6 +1,6 @@
 """bigdl_amd.nn — BigDL-style layers, containers, graphs and criterions (reference S/nn/**)."""
 from .abstractnn import (AbstractCriterion, AbstractModule, AutogradCriterion, AutogradModule,  # noqa: F401
-                         TensorCriterion, TensorModule, all_module_classes, module_class)
+                         MklInt8Convertible, TensorCriterion, TensorModule, all_module_classes, module_class)
 from .activation import *  # noqa: F401,F403
 from .containers import *  # noqa: F401,F403
 from .conv import *  # noqa: F401,F403
@@ -21,3 +21,4 @@ from .tree_lstm import *  # noqa: F401,F403
 from ..optim.regularizer import L1L2Regularizer, L1Regularizer, L2Regularizer  # noqa: F401
 from ..utils.table import T, Table  # noqa: F401
 from .module import Module  # noqa: F401
+from . import primitive as NNPrimitive  # noqa: E402,F401

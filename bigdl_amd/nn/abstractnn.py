@@ -105,7 +105,74 @@ def activity_apply(a, fn):
     return a
 
 
-class AbstractModule(metaclass=_RecordInit):
+class MklInt8Convertible:
+    """Int8 calibration state carried by every module (reference S/nn/MklInt8Convertible.scala:53-423):
+    ``calcScales`` records activation ranges over a sample batch, dim masks pick the scale granularity and the
+    scale getters / setters expose what a later ``quantize()`` consumes. Ranges are max-abs values; the int8
+    kernels use one input scale per tensor (mask 0) and one weight scale per output channel (mask 1)."""
+
+    def calcScales(self, sample):
+        from ..quantized.quantizer import calibrate
+
+        calibrate(self, sample)
+        return self
+
+    def _scales(self, key):
+        return self.__dict__.setdefault(key, [])
+
+    def getInputScales(self):
+        amax = self.__dict__.get("_calib_amax")
+        if amax is not None and not self._scales("_input_scales"):
+            return [[float(amax)]]
+        return self._scales("_input_scales")
+
+    def setInputScales(self, scales):
+        self._input_scales = [list(map(float, s)) for s in scales]
+        if self._input_scales and len(self._input_scales[0]) == 1:
+            self._calib_amax = self._input_scales[0][0]
+        return self
+
+    def getOutputScales(self):
+        return self._scales("_output_scales")
+
+    def setOutputScales(self, scales):
+        self._output_scales = [list(map(float, s)) for s in scales]
+        return self
+
+    def getWeightScales(self):
+        if not self._scales("_weight_scales"):
+            w = self.__dict__.get("weight")
+            if torch.is_tensor(w) and w.dim() >= 2:
+                return [w.detach().float().abs().reshape(w.shape[0], -1).amax(1).tolist()]
+        return self._scales("_weight_scales")
+
+    def setWeightScales(self, scales):
+        self._weight_scales = [list(map(float, s)) for s in scales]
+        return self
+
+    def getInputDimMask(self):
+        return self.__dict__.get("_input_dim_mask", 0)
+
+    def setInputDimMask(self, mask):
+        self._input_dim_mask = mask
+        return self
+
+    def getOutputDimMask(self):
+        return self.__dict__.get("_output_dim_mask", 0)
+
+    def setOutputDimMask(self, mask):
+        self._output_dim_mask = mask
+        return self
+
+    def getWeightDimMask(self):
+        return self.__dict__.get("_weight_dim_mask", 1)
+
+    def setWeightDimMask(self, mask):
+        self._weight_dim_mask = mask
+        return self
+
+
+class AbstractModule(MklInt8Convertible, metaclass=_RecordInit):
     """Base of every layer and container."""
 
     def __init__(self):
@@ -567,25 +634,6 @@ class AbstractModule(metaclass=_RecordInit):
         from ..optim.predictor import Predictor
 
         return Predictor(self, batchSize).predictClass(dataset)
-
-    # ------------------------------------------------------------------ int8 calibration (MklInt8Convertible)
-    def calcScales(self, sample):
-        """Record calibrated activation ranges of every quantizable layer over ``sample``
-        (S/nn/MklInt8Convertible.scala:53); a later ``quantize()`` uses them as static ranges."""
-        from ..quantized.quantizer import calibrate
-
-        calibrate(self, sample)
-        return self
-
-    def setInputDimMask(self, mask):
-        """Input scale granularity (0 = one per tensor, the only mode the int8 kernels use)."""
-        self._input_dim_mask = mask
-        return self
-
-    def setWeightDimMask(self, mask):
-        """Weight scale granularity (1 = per output channel, the only mode the int8 kernels use)."""
-        self._weight_dim_mask = mask
-        return self
 
     def quantize(self):
         from ..quantized.quantizer import quantize

@@ -182,27 +182,20 @@ class Optimizer:
         return TrainStep(self.model, self.criterion, self._optim_method(), device=self.device, comm=comm,
                          compress=self.compress, overlap=self._overlap)
 
-    def _clip(self, step):
-        g = step.g_shard
+    def _processors(self):
+        """Clipping as ParameterProcessors (reference ParameterOperations.scala), constant clipping first."""
+        from ..parallel.processors import ConstantClippingProcessor, L2NormClippingProcessor
+
+        out = []
         if self.constantClip is not None:
-            g.clamp_(self.constantClip[0], self.constantClip[1])
+            out.append(ConstantClippingProcessor(*self.constantClip))
         if self.l2NormClip is not None:
-            sq = torch.zeros(1, device=g.device)
-            if g.is_cuda:
-                from ..ops import native
+            out.append(L2NormClippingProcessor(self.l2NormClip))
+        return out
 
-                native.get().sumsq(g, sq)
-            else:
-                sq += (g * g).sum()
-            step.comm.all_reduce_scalar(sq)
-            norm = sq.sqrt()
-            scale = torch.clamp(self.l2NormClip / (norm + 1e-6), max=1.0)
-            if g.is_cuda:
-                from ..ops import native
-
-                native.get().scale_f32(g, scale, 1.0)
-            else:
-                g.mul_(scale)
+    def _clip(self, step):
+        for p in self._processors():
+            p(step.g_shard, step.comm)
 
     def _header(self, epoch, n, iteration, wall):
         return f"[Epoch {epoch} {n}/{self._epoch_size()}][Iteration {iteration}][Wall Clock {wall:.3f}s]"

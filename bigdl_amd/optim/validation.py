@@ -271,6 +271,31 @@ class _PRResult(ValidationResult):
         return auc, len(self.scores)
 
 
+class EvaluateMethods:
+    """Batch accuracy counters (reference S/optim/EvaluateMethods.scala:21): ``(correct, count)`` for a
+    [batch, classes] or [classes] score tensor against 1-based labels."""
+
+    @staticmethod
+    def _topk_hits(output, target, k):
+        if output.dim() == 1:
+            if target.numel() != 1:
+                raise ValueError("a single-sample output needs a single target")
+            output = output.unsqueeze(0)
+        elif output.dim() != 2:
+            raise ValueError("output must be 1-D or 2-D")
+        idx = output.float().topk(min(k, output.shape[1]), 1).indices + 1
+        t = target.reshape(-1, 1).to(idx.device).long()
+        return int((idx == t).any(1).sum()), output.shape[0]
+
+    @staticmethod
+    def calcAccuracy(output, target):
+        return EvaluateMethods._topk_hits(output, target, 1)
+
+    @staticmethod
+    def calcTop5Accuracy(output, target):
+        return EvaluateMethods._topk_hits(output, target, 5)
+
+
 __all__ = ["ValidationResult", "AccuracyResult", "LossResult", "ContiguousResult", "MAPResult", "ValidationMethod",
            "Top1Accuracy", "Top5Accuracy", "TreeNNAccuracy", "Loss", "MAE", "HitRatio", "NDCG",
-           "MeanAveragePrecision", "PrecisionRecallAUC"]
+           "MeanAveragePrecision", "PrecisionRecallAUC", "EvaluateMethods"]
