@@ -196,7 +196,10 @@ class SpatialConvolution(TensorModule):
         x, ph, pw, eh, ew = self._prep(x)
         if gy.is_cuda:
             gy = self._relu_mask(gy)
-            gi = self._dgrad_gpu(x, gy, ph, pw)
+            once = getattr(self, "_dgrad_bn_once", False)
+            self._dgrad_bn_once = False
+            bn_src = getattr(input, "_bn_bwd", None) if (getattr(self, "_dgrad_bn_ok", False) or once) else None
+            gi = self._dgrad_gpu(x, gy, ph, pw, None if (squeeze or eh or ew or self.format != "NCHW") else bn_src)
         else:
             gy = self._relu_mask(gy)
             gi = torch.nn.grad.conv2d_input(x.shape, self.weight, gy.float(), (self.strideH, self.strideW),
@@ -216,7 +219,7 @@ class SpatialConvolution(TensorModule):
             return ops.relu_bwd_gpu(gy.contiguous(memory_format=CL), self.output)
         return gy * (self.output > 0)
 
-    def _dgrad_gpu(self, x, gy, ph, pw):
+    def _dgrad_gpu(self, x, gy, ph, pw, bn_src=None):
         gy16 = gy if (gy.dtype == BF16 and gy.is_contiguous(memory_format=CL)) else gy.to(BF16, memory_format=CL)
         if self.nGroup == 1:
             w16 = self._w16_padded()
@@ -230,10 +233,17 @@ class SpatialConvolution(TensorModule):
             self._dgrad_addend = None
             if addend is not None and Cp != x.shape[1]:
                 raise RuntimeError("dgrad addend requires unpadded channels")
+            bn = None
+            if bn_src is not None and Cp == x.shape[1]:
+                # the input is a training BN's output: reduce that BN's backward statistics in our epilogue
+                bnmod, bx, bmean, baff, bz = bn_src
+                bn = {"x": bx, "z": bz, "mean": bmean, "aff": baff, "red": bnops.new_stats(Cp, gy16.device)}
             gi = cv.conv2d_dgrad(gy16, wt, xs, (self.strideH, self.strideW), (ph, pw),
-                                 (self.dilationH, self.dilationW), addend=addend)
+                                 (self.dilationH, self.dilationW), addend=addend, bn=bn)
             if Cp != x.shape[1]:
                 gi = gi[:, : x.shape[1]].contiguous(memory_format=CL)
+            elif bn is not None and bn.get("done"):
+                gi._bn_red = (bnmod, bn["red"])
             return gi
         G = self.nGroup
         cin, cout = self.nInputPlane // G, self.nOutputPlane // G

@@ -9,10 +9,15 @@ work the producer already did.
   conv -> BN          conv epilogue emits per-channel (sum, sumsq): BN skips its statistics pass
   BN -> ReLU          ReLU applied in the BN apply pass; backward mask from the BN output
   conv/Linear -> ReLU ReLU in the GEMM epilogue
+  BN -> ReLU -> conv  (opt-in, BIGDL_DGRAD_BN=1) backward: the conv's data-gradient epilogue reduces the BN's
+                      backward statistics (sum dy, sum dy * (x - mean) under the ReLU mask): BN skips its
+                      reduction pass
   ResNet block        Sequential[ConcatTable[branch(... BN), shortcut], CAddTable, ReLU]: the shortcut runs
                       first, its output is added inside the branch's last BN apply pass together with the
                       ReLU; backward emits the residual-branch gradient from the same pass.
 """
+import os
+
 from ..utils.table import Table
 from .activation import ReLU
 from .containers import ConcatTable, Sequential, add_activity
@@ -24,11 +29,19 @@ from .table_ops import CAddTable
 
 def _reset(m):
     for x in m.flattened_layers():
-        for attr, val in (("emit_stats", False), ("fuse_relu", False), ("passthrough", False)):
+        for attr, val in (("emit_stats", False), ("fuse_relu", False), ("passthrough", False),
+                          ("_dgrad_bn_ok", False)):
             if hasattr(x, attr):
                 setattr(x, attr, val)
         if isinstance(x, Sequential):
             x._residual_plan = None
+
+
+def _dgrad_bn_enabled():
+    """Off by default: measured on ResNet-50 b256 (profiles/r1_dgrad_bn_ab.txt) the extra x / z reads in the
+    dgrad epilogue cost the GEMM +2.7 ms/step while the skipped reduction pass saved 2.4 ms — the epilogue
+    runs at 2 workgroups per CU with nothing to overlap its reads, the separate pass streams at full bandwidth."""
+    return os.environ.get("BIGDL_DGRAD_BN", "0") == "1"
 
 
 def fuse_for_training(model):
@@ -67,6 +80,12 @@ def _fuse_sequential(seq):
         elif isinstance(a, BatchNormalization) and isinstance(b, ReLU):
             a.fuse_relu = True
             b.passthrough = True
+    # BN -> ReLU -> conv: the conv is the only consumer of the BN output, so its data-gradient GEMM
+    # produces the BN's complete output gradient and can reduce the BN backward statistics in its epilogue
+    for a, b, c in zip(mods[:-2], mods[1:-1], mods[2:]):
+        if (_dgrad_bn_enabled() and isinstance(a, BatchNormalization) and a.fuse_relu and isinstance(b, ReLU) and b.passthrough
+                and isinstance(c, SpatialConvolution) and c.nGroup == 1):
+            c._dgrad_bn_ok = True
         elif isinstance(a, (SpatialConvolution, Linear)) and isinstance(b, ReLU):
             a.fuse_relu = True
             b.passthrough = True
@@ -79,6 +98,8 @@ def residual_forward(seq, x):
     h = x
     for m in branch.modules[:-1]:
         h = m.forward(h)
+    if tuple(res.shape) != tuple(h.shape[:1]) + (bn.nOutput,) + tuple(h.shape[2:]):
+        raise ValueError(f"residual block: shortcut output {tuple(res.shape)} does not match the branch output")
     out = bn.updateOutput(h, residual=res)
     bn.output = out
     branch.output = out
@@ -105,5 +126,8 @@ def residual_backward(seq, x, gradOutput):
         inp = mods[i - 1].output if i > 0 else x
         if i == 0 and fold:
             first._dgrad_addend = gs
+            # with the shortcut gradient folded in, the dgrad output is the complete gradient of the block
+            # input: if that is the previous block's output, its last BN's reduction can run in the epilogue
+            first._dgrad_bn_once = _dgrad_bn_enabled()
         g = mods[i].backward(inp, g)
     return g if fold else add_activity(g, gs)

@@ -115,6 +115,9 @@ class BatchNormalization(TensorModule):
             # without a residual the ReLU mask is a function of x: backward recomputes it from (scale, shift)
             self._aff = aff if (self.fuse_relu and res is None) else None
             self._xin = x
+            if self.train and self.fuse_relu:
+                # lets a consuming conv reduce this BN's backward statistics in its dgrad epilogue (nn.fusion)
+                y._bn_bwd = (self, x, sm, self._aff, y if res is not None else None)
             return self._from_nchw(y)
         xf = x.float()
         y, mean, invstd = bnops.bn_forward_cpu(xf, self.weight, self.bias, self.runningMean, self.runningVar, self.eps,
@@ -142,9 +145,11 @@ class BatchNormalization(TensorModule):
         direct = self._direct_grads()
         dg = self.gradWeight if direct else (torch.zeros_like(self.runningMean) if self.affine else None)
         db = self.gradBias if direct else (torch.zeros_like(self.runningMean) if self.affine else None)
+        pre = getattr(gradOutput, "_bn_red", None)
+        red = pre[1] if (pre is not None and pre[0] is self and self.train) else None
         dx, dres = bnops.bn_backward_gpu(gz, z, x, self.saveMean, self.saveStd, self.weight, dg, db,
                                          training=self.train, need_dres=need_dres,
-                                         sync_fn=self.sync_fn if self.train else None, aff=aff)
+                                         sync_fn=self.sync_fn if self.train else None, aff=aff, red=red)
         if not direct and self.affine and not self._frozen:
             self.gradWeight.add_(dg, alpha=self.scaleW)
             self.gradBias.add_(db, alpha=self.scaleB)

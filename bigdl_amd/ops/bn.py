@@ -95,20 +95,24 @@ def bn_forward_gpu(x, gamma, beta, rmean, rvar, eps, momentum, training, stats=N
 
 
 def bn_backward_gpu(dz, z, x, smean, sinv, gamma, dgamma, dbeta, training=True, need_dres=False, need_dx=True,
-                    sync_fn=None, aff=None):
+                    sync_fn=None, aff=None, red=None):
     """Backward of y = relu?(bn(x) [+ res]).
 
     dz: gradient w.r.t. the (post-relu) output; z: the forward output (ReLU mask) or None. With z None and
     ``aff`` (the forward's [scale | shift]) the ReLU mask is recomputed from x, so z is never read back.
     Returns (dx, dres) — dres is the gradient flowing into the residual branch (= masked dz).
+    ``red``: the slotted backward reduction already accumulated by the producer of dz (a dgrad epilogue).
     """
     C = x.shape[1]
     P = _P(x)
     C_ = native.get()
-    red, nslots, Ptot = None, 0, P
-    if training:
+    nslots, Ptot = 0, P
+    if not training:
+        red = None
+    elif red is None:
         red = new_stats(C, x.device)
         C_.bn_bwd_reduce(dz, z, x, smean, red, P, C, aff)
+    if training:
         nslots = stat_slots()
         if sync_fn is not None:
             red, nslots, Ptot = _reduce_slots_for_sync(red, C, P, sync_fn)

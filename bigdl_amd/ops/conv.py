@@ -138,12 +138,17 @@ def dgrad_phases(H, W, R, S, stride, pad, dil):
     return res
 
 
-def conv2d_dgrad(dy, w16t, x_shape, stride, pad, dil=(1, 1), out=None, addend=None):
+def conv2d_dgrad(dy, w16t, x_shape, stride, pad, dil=(1, 1), out=None, addend=None, bn=None):
     """dx = conv_transpose(dy, w) [+ addend]. ``w16t`` is the (C, R, S, K)-ordered transposed weight.
 
     Stride > 1 runs one dense implicit GEMM per stride phase (no zero-insertion, no masked MFMAs).
     ``addend`` (same shape/layout as dx) is summed in the GEMM epilogue — used to fold the residual
     branch gradient of a ResNet block into the block-input gradient.
+
+    ``bn`` = {"x", "z", "mean", "aff", "red"}: dx is the gradient of a training BatchNorm's (ReLU-fused)
+    output, and the epilogue also accumulates that BN's backward reduction into ``red`` (the pass
+    bn_bwd_reduce would make over dx and x). Only when every pixel of dx is written by a GEMM phase (or the
+    uncovered pixels are zero); ``bn["done"]`` reports whether it ran.
     """
     N, C, H, W = x_shape
     _, K, OH, OW = dy.shape
@@ -166,9 +171,14 @@ def conv2d_dgrad(dy, w16t, x_shape, stride, pad, dil=(1, 1), out=None, addend=No
             out.zero_()
     C_ = native.get()
     ldw = R * S * K
+    bnk = {}
+    if bn is not None and (covered == H * W or addend is None) and bn["x"].shape == out.shape \
+            and bn["x"].stride() == out.stride():
+        bnk = dict(bn_x=bn["x"], bn_z=bn["z"], bn_mean=bn["mean"], bn_aff=bn["aff"], bn_red=bn["red"])
+        bn["done"] = True
     for (a, b, nI, nJ, taps) in phases:
         geo = [N, OH, OW, K, nI, nJ, 1, 1, ldw, C, C, H, W, stride[0], stride[1], a, b]
-        C_.conv_nt(dy, w16t, out, None, None, geo, taps, False, addend)
+        C_.conv_nt(dy, w16t, out, None, None, geo, taps, False, addend, **bnk)
     return out
 
 

@@ -32,7 +32,8 @@ float* omf(const OptT& t, const char* n) { return (t && t->defined()) ? mf(*t, n
 // geo = [Nb, Hs, Ws, Cs, OH, OW, mul_h, mul_w, ldw, Ncol, ldo, OHo, OWo, omul_h, omul_w, ooff_h, ooff_w]
 // taps = flat [tap_h0, tap_w0, tap_k0, tap_h1, ...]
 void conv_nt(const Tensor& src, const Tensor& wt, const Tensor& out, const OptT& bias, const OptT& stats,
-             std::vector<int64_t> geo, std::vector<int64_t> taps, bool relu, const OptT& addend) {
+             std::vector<int64_t> geo, std::vector<int64_t> taps, bool relu, const OptT& addend, const OptT& bn_x,
+             const OptT& bn_z, const OptT& bn_mean, const OptT& bn_aff, const OptT& bn_red) {
   TORCH_CHECK(geo.size() == 17, "conv_nt: bad geometry");
   if (stats && stats->defined())
     TORCH_CHECK(stats->numel() >= BIGDL_STAT_SLOTS * 2 * geo[9], "conv_nt: stats must hold STAT_SLOTS x 2Ncol");
@@ -42,6 +43,14 @@ void conv_nt(const Tensor& src, const Tensor& wt, const Tensor& out, const OptT&
   a.bias = ocf(bias, "bias"); a.stats = omf(stats, "stats");
   a.addend = ocbf(addend, "addend");
   if (a.addend) TORCH_CHECK(addend->numel() == out.numel(), "conv_nt: addend must match out");
+  a.bnx = ocbf(bn_x, "bn_x"); a.bnz = ocbf(bn_z, "bn_z"); a.bnmean = ocf(bn_mean, "bn_mean");
+  a.bnaff = ocf(bn_aff, "bn_aff"); a.bnred = omf(bn_red, "bn_red");
+  if (a.bnred) {
+    TORCH_CHECK(a.bnx && a.bnmean && bn_x->numel() == out.numel(), "conv_nt: bn_x must match out, bn_mean required");
+    TORCH_CHECK(!a.bnz || bn_z->numel() == out.numel(), "conv_nt: bn_z must match out");
+    TORCH_CHECK(bn_mean->numel() >= geo[9] && (!a.bnaff || bn_aff->numel() >= 2 * geo[9]), "conv_nt: bn vectors");
+    TORCH_CHECK(bn_red->numel() >= BIGDL_STAT_SLOTS * 2 * geo[9], "conv_nt: bn_red must hold STAT_SLOTS x 2Ncol");
+  }
   a.Nb = geo[0]; a.Hs = geo[1]; a.Ws = geo[2]; a.Cs = geo[3]; a.OH = geo[4]; a.OW = geo[5];
   a.mul_h = geo[6]; a.mul_w = geo[7]; a.ldw = geo[8]; a.Ncol = geo[9]; a.ldo = geo[10];
   a.OHo = geo[11]; a.OWo = geo[12]; a.omul_h = geo[13]; a.omul_w = geo[14]; a.ooff_h = geo[15]; a.ooff_w = geo[16];
@@ -267,6 +276,7 @@ void conv_i8(const Tensor& src, const Tensor& wt, const Tensor& out, const OptT&
   a.wt = reinterpret_cast<const uint16_t*>(wt.data_ptr<int8_t>());
   a.out = reinterpret_cast<uint16_t*>(out.data_ptr());
   a.bias = ocf(bias, "bias"); a.stats = nullptr; a.addend = nullptr;
+  a.bnx = nullptr; a.bnz = nullptr; a.bnmean = nullptr; a.bnaff = nullptr; a.bnred = nullptr;
   a.Nb = geo[0]; a.Hs = geo[1]; a.Ws = geo[2]; a.Cs = geo[3]; a.OH = geo[4]; a.OW = geo[5];
   a.mul_h = geo[6]; a.mul_w = geo[7]; a.ldw = geo[8]; a.Ncol = geo[9]; a.ldo = geo[10];
   a.OHo = geo[11]; a.OWo = geo[12]; a.omul_h = geo[13]; a.omul_w = geo[14]; a.ooff_h = geo[15]; a.ooff_w = geo[16];
@@ -486,7 +496,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   register_host_runtime(m);
   m.doc() = "bigdl_amd native HIP kernels for gfx950 (MI355X)";
   m.def("conv_nt", &conv_nt, py::arg("src"), py::arg("wt"), py::arg("out"), py::arg("bias"), py::arg("stats"),
-        py::arg("geo"), py::arg("taps"), py::arg("relu"), py::arg("addend") = py::none());
+        py::arg("geo"), py::arg("taps"), py::arg("relu"), py::arg("addend") = py::none(), py::arg("bn_x") = py::none(),
+        py::arg("bn_z") = py::none(), py::arg("bn_mean") = py::none(), py::arg("bn_aff") = py::none(),
+        py::arg("bn_red") = py::none());
   m.def("conv_wgrad", &conv_wgrad);
   m.def("transpose_krsc", &transpose_krsc);
   m.def("bn_stats", &bn_stats);

@@ -133,15 +133,6 @@ __device__ __forceinline__ void nt_epilogue_lds(const ConvArgs& a, v4f (&acc)[MI
   constexpr int PPI = 64 / LPR;         // pixels per read instruction
   static_assert(TN % 8 == 0 && 64 % LPR == 0, "tile");
   auto gpos = [](int p, int g) { return (p * GR + (g ^ (p & (GR - 1)))) * 4; };
-#pragma unroll
-  for (int i = 0; i < MI; ++i)
-#pragma unroll
-    for (int j = 0; j < NI; ++j) {
-      const int p = i * 16 + (lane & 15);
-      const int g = j * 4 + (lane >> 4);
-      *reinterpret_cast<v4f*>(wl + gpos(p, g)) = acc[i][j];
-    }
-  __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's LDS writes landed (wave-private slice)
   const int ohw = a.OH * a.OW;
   const int q = lane % LPR;              // this lane's 8-channel group within the wave tile
   const int n = nbase + q * 8;
@@ -152,24 +143,66 @@ __device__ __forceinline__ void nt_epilogue_lds(const ConvArgs& a, v4f (&acc)[MI
   float s1[8], s2[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) s1[e] = s2[e] = 0.f;
+  float bmu[8], bsc[8], bsh[8];
 #pragma unroll
-  for (int r = 0; r < TM / PPI; ++r) {
-    const int p = r * PPI + lane / LPR;
-    const int m = mbase + p;
-    const v4f lo = *reinterpret_cast<const v4f*>(wl + gpos(p, 2 * q));
-    const v4f hi = *reinterpret_cast<const v4f*>(wl + gpos(p, 2 * q + 1));
+  for (int e = 0; e < 8; ++e) {
+    const bool on = a.bnred && !a.stats && nok;
+    bmu[e] = on ? a.bnmean[n + e] : 0.f;
+    bsc[e] = (on && a.bnaff) ? a.bnaff[n + e] : 0.f;
+    bsh[e] = (on && a.bnaff) ? a.bnaff[a.Ncol + n + e] : 0.f;
+  }
+  // Phase 1: every global read of the epilogue (addend, consumer-BN x / z) is issued before the first store:
+  // `out` may alias them as far as the compiler knows, so loads left inside the store loop would be serialised
+  // one round trip per row group.
+  constexpr int NR = TM / PPI;
+  long orows[NR];
+  v4u pad[NR], px[NR], pz[NR];
+  const bool bnw = a.bnred && !a.stats;
+#pragma unroll
+  for (int r = 0; r < NR; ++r) {
+    const int m = mbase + r * PPI + lane / LPR;
+    long orow = -1;
     if (m < a.M && nok) {
-      long orow = m;
+      orow = m;
       if (!a.ident_out) {
         const int nb = m / ohw, rem = m - nb * ohw;
         const int oh = rem / a.OW, ow = rem - oh * a.OW;
         orow = ((long)nb * a.OHo + oh * a.omul_h + a.ooff_h) * a.OWo + ow * a.omul_w + a.ooff_w;
       }
+    }
+    orows[r] = orow;
+    const size_t off = (size_t)(orow < 0 ? 0 : orow) * a.ldo + n;
+    pad[r] = v4u{0u, 0u, 0u, 0u};
+    px[r] = v4u{0u, 0u, 0u, 0u};
+    pz[r] = v4u{0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
+    if (orow >= 0) {
+      if (a.addend) pad[r] = *reinterpret_cast<const v4u*>(a.addend + off);
+      if (bnw) {
+        px[r] = *reinterpret_cast<const v4u*>(a.bnx + off);
+        if (a.bnz) pz[r] = *reinterpret_cast<const v4u*>(a.bnz + off);
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int p = i * 16 + (lane & 15);
+      const int g = j * 4 + (lane >> 4);
+      *reinterpret_cast<v4f*>(wl + gpos(p, g)) = acc[i][j];
+    }
+  __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's LDS writes landed (wave-private slice)
+#pragma unroll
+  for (int r = 0; r < NR; ++r) {
+    const int p = r * PPI + lane / LPR;
+    const v4f lo = *reinterpret_cast<const v4f*>(wl + gpos(p, 2 * q));
+    const v4f hi = *reinterpret_cast<const v4f*>(wl + gpos(p, 2 * q + 1));
+    const long orow = orows[r];
+    if (orow >= 0) {
       float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       if (a.addend) {
-        const v4u ad = *reinterpret_cast<const v4u*>(a.addend + (size_t)orow * a.ldo + n);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) { v[2 * e] += lo_bf(ad[e]); v[2 * e + 1] += hi_bf(ad[e]); }
+        for (int e = 0; e < 4; ++e) { v[2 * e] += lo_bf(pad[r][e]); v[2 * e + 1] += hi_bf(pad[r][e]); }
       }
       v4u o;
 #pragma unroll
@@ -185,11 +218,28 @@ __device__ __forceinline__ void nt_epilogue_lds(const ConvArgs& a, v4f (&acc)[MI
           s1[2 * e] += y0; s2[2 * e] += y0 * y0;
           s1[2 * e + 1] += y1; s2[2 * e + 1] += y1 * y1;
         }
+      } else if (bnw) {
+        // consumer-BN backward reduction on the rounded gradient (what bn_bwd_reduce would read back)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float d0 = lo_bf(o[e]), d1 = hi_bf(o[e]);
+          const float x0 = lo_bf(px[r][e]), x1 = hi_bf(px[r][e]);
+          if (a.bnz) {
+            if (!(lo_bf(pz[r][e]) > 0.f)) d0 = 0.f;
+            if (!(hi_bf(pz[r][e]) > 0.f)) d1 = 0.f;
+          } else if (a.bnaff) {
+            if (!(x0 * bsc[2 * e] + bsh[2 * e] > 0.f)) d0 = 0.f;
+            if (!(x1 * bsc[2 * e + 1] + bsh[2 * e + 1] > 0.f)) d1 = 0.f;
+          }
+          s1[2 * e] += d0; s2[2 * e] += d0 * (x0 - bmu[2 * e]);
+          s1[2 * e + 1] += d1; s2[2 * e + 1] += d1 * (x1 - bmu[2 * e + 1]);
+        }
       }
       *reinterpret_cast<v4u*>(a.out + (size_t)orow * a.ldo + n) = o;
     }
   }
-  if (a.stats) {
+  float* const red = a.stats ? a.stats : a.bnred;
+  if (red) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
 #pragma unroll
@@ -199,7 +249,7 @@ __device__ __forceinline__ void nt_epilogue_lds(const ConvArgs& a, v4f (&acc)[MI
       }
     }
     if (lane < LPR && nok) {
-      float* sp = a.stats + (size_t)(bid & (BIGDL_STAT_SLOTS - 1)) * 2 * a.Ncol;
+      float* sp = red + (size_t)(bid & (BIGDL_STAT_SLOTS - 1)) * 2 * a.Ncol;
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         atomicAdd(sp + n + e, s1[e]);
@@ -1035,6 +1085,8 @@ int bigdl_get_conv_impl() { return conv_impl(); }
 // Forward or data-gradient implicit GEMM. Returns 0 on success, negative on unsupported shapes.
 int bigdl_conv_nt(const ConvArgs* a, hipStream_t st) {
   if (a->Cs % 8 != 0 || a->Kdim != a->ntaps * a->Cs || a->ntaps < 1 || a->ntaps > CONV_MAX_TAPS) return -1;
+  // the BN-backward reduction lives in the LDS-transposed epilogue only
+  if (a->bnred && (a->stats || a->bnx == nullptr || a->bnmean == nullptr || (a->Ncol & 7) || (a->ldo & 7))) return -2;
   if (a->M <= 0) return 0;
   const bool fastk = (a->Cs % BK) == 0;
   const int impl = conv_impl();

@@ -17,6 +17,14 @@ struct ConvArgs {
   const float* bias;
   float* stats;
   const uint16_t* addend;   // optional [rows][ldo] bf16 added in the epilogue (same placement as out)
+  // Optional BN-backward reduction of the consumer BatchNorm (data-gradient GEMMs only): with bnred set the
+  // epilogue accumulates sum(dm) and sum(dm * (x - mean)) per channel into [STAT_SLOTS][2][Ncol] slots, where
+  // dm = out masked by the fused ReLU (z > 0 when bnz is set, else x * aff[c] + aff[Ncol + c] > 0, else no mask)
+  const uint16_t* bnx;      // BN input x, same placement / ldo as out
+  const uint16_t* bnz;      // BN output (post residual + ReLU) or nullptr
+  const float* bnmean;      // [Ncol] batch mean
+  const float* bnaff;       // [2 Ncol] scale | shift or nullptr
+  float* bnred;
   int Nb, Hs, Ws, Cs;
   int OH, OW;
   int mul_h, mul_w;

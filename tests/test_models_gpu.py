@@ -202,3 +202,46 @@ def test_inception_v3_gpu_matches_cpu():
     out = g.forward(x.cuda()).float().cpu()
     rel = ((out.exp() - ref.exp()).norm() / ref.exp().norm()).item()
     assert rel < 3e-2, rel
+
+
+def test_dgrad_epilogue_bn_reduction_matches_separate_pass(monkeypatch):
+    """Two stacked bottlenecks: the BN backward reductions computed in the consumer conv's dgrad epilogue
+    (BN->ReLU->conv inside a branch, and the previous block's last BN through the folded residual dgrad)
+    match the separate bn_bwd_reduce pass, and that pass is skipped."""
+    from bigdl_amd import nn
+    from bigdl_amd.models.resnet import _Builder
+    from bigdl_amd.nn.fusion import fuse_for_training
+    from bigdl_amd.ops import native
+
+    b = _Builder("B", True)
+    b.iChannels = 64
+    cpu = nn.Sequential().add(b.bottleneck(64, 1)).add(b.bottleneck(128, 2))
+    _randomize_bn(cpu)
+    torch.manual_seed(0)
+    x = torch.randn(8, 64, 16, 16).to(torch.bfloat16).float().cuda()
+    C_ = native.get()
+    real = C_.bn_bwd_reduce
+    calls = []
+
+    def counting(*a, **k):
+        calls.append(1)
+        return real(*a, **k)
+
+    monkeypatch.setattr(C_, "bn_bwd_reduce", counting)
+    res = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("BIGDL_DGRAD_BN", mode)     # opt-in fusion (see nn/fusion.py)
+        m = copy.deepcopy(cpu).to("cuda")
+        fuse_for_training(m)
+        calls.clear()
+        out = m.forward(x)
+        gy = torch.randn(out.shape, generator=torch.Generator().manual_seed(1)).to(torch.bfloat16).cuda()
+        gx = m.backward(x, gy.to(out.dtype))
+        torch.cuda.synchronize()
+        res[mode] = (gx.float(), _weight_grads(m), len(calls))
+    n_bn = sum(isinstance(q, nn.BatchNormalization) for q in cpu.flattened_layers())
+    assert res["0"][2] == n_bn
+    # fused: 2 branch BNs per block + block 1's last BN (through block 2's folded conv1 dgrad)
+    assert res["1"][2] == n_bn - 5
+    assert _rel(res["1"][0], res["0"][0]) < 2e-2
+    assert _rel(res["1"][1], res["0"][1]) < 2e-2
