@@ -125,7 +125,7 @@ __device__ __forceinline__ void nt_epilogue(const ConvArgs& a, v4f (&acc)[MI][NI
 // are conflict-free — then re-reads it row-wise: a lane owns 8 channels of one pixel, so every store is
 // 16 B and one wave instruction writes 64/(TN/8) whole pixel rows of TN channels. bias / addend / ReLU /
 // BN statistics are applied in the row phase (the addend is read with the same 16-byte coalesced pattern).
-template <int MI, int NI, int TM, int TN>
+template <int MI, int NI, int TM, int TN, int NH = 1>
 __device__ __forceinline__ void nt_epilogue_lds(const ConvArgs& a, v4f (&acc)[MI][NI], int mbase, int nbase,
                                                 int lane, int bid, float* wl) {
   constexpr int GR = TN / 4;            // 16-byte fp32 granules per pixel row
@@ -183,18 +183,24 @@ __device__ __forceinline__ void nt_epilogue_lds(const ConvArgs& a, v4f (&acc)[MI
       }
     }
   }
+  // NH > 1: the accumulator tile goes through LDS in NH row chunks, so the wave slice is TM/NH x TN floats
+  constexpr int MIH = MI / NH, NRH = NR / NH;
+  static_assert(MI % NH == 0 && NR % NH == 0, "row chunks");
 #pragma unroll
-  for (int i = 0; i < MI; ++i)
+  for (int h = 0; h < NH; ++h) {
+#pragma unroll
+  for (int i = 0; i < MIH; ++i)
 #pragma unroll
     for (int j = 0; j < NI; ++j) {
       const int p = i * 16 + (lane & 15);
       const int g = j * 4 + (lane >> 4);
-      *reinterpret_cast<v4f*>(wl + gpos(p, g)) = acc[i][j];
+      *reinterpret_cast<v4f*>(wl + gpos(p, g)) = acc[h * MIH + i][j];
     }
   __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's LDS writes landed (wave-private slice)
 #pragma unroll
-  for (int r = 0; r < NR; ++r) {
-    const int p = r * PPI + lane / LPR;
+  for (int rr = 0; rr < NRH; ++rr) {
+    const int r = h * NRH + rr;
+    const int p = rr * PPI + lane / LPR;
     const v4f lo = *reinterpret_cast<const v4f*>(wl + gpos(p, 2 * q));
     const v4f hi = *reinterpret_cast<const v4f*>(wl + gpos(p, 2 * q + 1));
     const long orow = orows[r];
@@ -237,6 +243,7 @@ __device__ __forceinline__ void nt_epilogue_lds(const ConvArgs& a, v4f (&acc)[MI
       }
       *reinterpret_cast<v4u*>(a.out + (size_t)orow * a.ldo + n) = o;
     }
+  }
   }
   float* const red = a.stats ? a.stats : a.bnred;
   if (red) {
@@ -507,6 +514,135 @@ __global__ __launch_bounds__(256, 2) void conv_nt_glds_kernel(ConvArgs a) {
                                     reinterpret_cast<float*>(lds) + wave * TM * TN);
   else
     nt_epilogue<MI, NI, TM, TN>(a, acc, m0 + wm * TM, n0 + wn * TN, lane, bid);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Persistent LDS-DMA NT kernel: a grid of 2 workgroups per CU walks the tiles (tile = blockIdx + k * grid,
+// through the same XCD remap, so each XCD keeps its contiguous tile range). When a tile's K loop ends the
+// first K-slice of the NEXT tile is DMA'd into stage 0 before the epilogue runs, and the epilogue stages
+// its accumulators through stage 1 in two row chunks — so the next tile's load latency hides behind this
+// tile's epilogue (stores, statistics atomics). Aimed at the many-tile, short-K layers (1x1 convs over 64-256
+// channels: 1-4 K-slices per tile) where load -> MFMA -> epilogue run back to back. Measured on ResNet-50
+// b256 it is slower than the one-tile-per-workgroup kernel (33.3 vs 32.4 ms/step): the barrier opening each
+// tile waits on vmcnt(0), which now includes the previous epilogue's stores, while a retiring workgroup lets
+// its stores drain under the next workgroup's loads. Opt-in (BIGDL_CONV_IMPL=3) until the wait is counted.
+// ------------------------------------------------------------------------------------------------
+template <int BM, int BN, int WM>
+__global__ __launch_bounds__(256, 2) void conv_nt_pers_kernel(ConvArgs a) {
+  constexpr int WN = 4 / WM;
+  constexpr int TM = BM / WM, TN = BN / WN;
+  constexpr int MI = TM / 16, NI = TN / 16;
+  constexpr int AI = BM / 32, BI = BN / 32;
+  constexpr int STAGE = (BM + BN) * BK;
+  static_assert(4 * (TM / 2) * TN * 4 <= STAGE * 2, "epilogue chunk must fit one stage");
+  __shared__ __attribute__((aligned(1024))) bf16_t lds[2 * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WN, wn = wave % WN;
+  const int tiles_n = (a.Ncol + BN - 1) / BN;
+  const int tiles_m = (a.M + BM - 1) / BM;
+  const int nwg = tiles_m * tiles_n;
+  const int rsub = lane >> 3;
+  const int gsrc = (lane ^ rsub) & 7;
+  const int ohw = a.OH * a.OW;
+  const int nk = a.Kdim / BK;
+
+  int a_pix[AI], a_h[AI], a_w[AI];
+  const bf16_t* wrow[BI];
+  bool bvalid[BI];
+  auto setup = [&](int m0, int n0) {
+#pragma unroll
+    for (int i = 0; i < AI; ++i) {
+      const int m = m0 + (i * 4 + wave) * 8 + rsub;
+      if (m < a.M) {
+        const int nb = m / ohw, rem = m - nb * ohw;
+        const int oh = rem / a.OW, ow = rem - oh * a.OW;
+        a_pix[i] = nb * a.Hs * a.Ws;
+        a_h[i] = oh * a.mul_h;
+        a_w[i] = ow * a.mul_w;
+      } else {
+        a_pix[i] = 0; a_h[i] = -(1 << 28); a_w[i] = -(1 << 28);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < BI; ++i) {
+      const int n = n0 + (i * 4 + wave) * 8 + rsub;
+      bvalid[i] = n < a.Ncol;
+      wrow[i] = a.wt + (size_t)(bvalid[i] ? n : 0) * a.ldw + gsrc * 8;
+    }
+  };
+  auto issue = [&](int kt, int buf) {
+    const int k0 = kt * BK;
+    const int t = k0 / a.Cs;
+    const int c = k0 - t * a.Cs + gsrc * 8;
+    const int th = a.tap_h[t], tw = a.tap_w[t];
+    const int wk = a.tap_k[t] * a.Cs + (k0 - t * a.Cs);
+    bf16_t* A = lds + buf * STAGE;
+    bf16_t* B = A + BM * BK;
+#pragma unroll
+    for (int i = 0; i < AI; ++i) {
+      const int ch = a_h[i] + th, cw = a_w[i] + tw;
+      const bool ok = (unsigned)ch < (unsigned)a.Hs && (unsigned)cw < (unsigned)a.Ws;
+      const bf16_t* src = ok ? a.src + (unsigned)((a_pix[i] + ch * a.Ws + cw) * a.Cs + c) : g_zero_granule;
+      glds16(src, (LDS_PTR(void))(A + (i * 4 + wave) * 8 * BK));
+    }
+#pragma unroll
+    for (int i = 0; i < BI; ++i) {
+      const bf16_t* src = bvalid[i] ? wrow[i] + wk : g_zero_granule;
+      glds16(src, (LDS_PTR(void))(B + (i * 4 + wave) * 8 * BK));
+    }
+  };
+  auto swz = [](int row, int g) { return row * BK + ((g ^ (row & 7)) << 3); };
+
+  int t = blockIdx.x;
+  if (t >= nwg) return;
+  int bid = xcd_remap(t, nwg);
+  setup((bid / tiles_n) * BM, (bid % tiles_n) * BN);
+  issue(0, 0);
+  while (true) {
+    const int m0 = (bid / tiles_n) * BM, n0 = (bid % tiles_n) * BN;
+    v4f acc[MI][NI];
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+    __syncthreads();   // stage 0 of this tile landed; the previous epilogue is done with stage 1
+    for (int kt = 0; kt < nk; ++kt) {
+      // the tile's first slice is in stage 0; slice kt lives in stage kt & 1
+      const int cur = kt & 1;
+      if (kt + 1 < nk) issue(kt + 1, cur ^ 1);
+      const bf16_t* A = lds + cur * STAGE;
+      const bf16_t* B = A + BM * BK;
+#pragma unroll
+      for (int ks = 0; ks < BK / 32; ++ks) {
+        v8s fa[MI], fb[NI];
+        const int g = ks * 4 + (lane >> 4);
+#pragma unroll
+        for (int i = 0; i < MI; ++i) fa[i] = *reinterpret_cast<const v8s*>(A + swz(wm * TM + i * 16 + (lane & 15), g));
+#pragma unroll
+        for (int j = 0; j < NI; ++j) fb[j] = *reinterpret_cast<const v8s*>(B + swz(wn * TN + j * 16 + (lane & 15), g));
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < NI; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+      }
+      __syncthreads();
+    }
+    // next tile's first K-slice into stage 0 while this tile's epilogue runs out of stage 1
+    const int tn_next = t + gridDim.x;
+    const int bid_cur = bid;
+    if (tn_next < nwg) {
+      t = tn_next;
+      bid = xcd_remap(t, nwg);
+      setup((bid / tiles_n) * BM, (bid % tiles_n) * BN);
+      issue(0, 0);
+    }
+    nt_epilogue_lds<MI, NI, TM, TN, 2>(a, acc, m0 + wm * TM, n0 + wn * TN, lane, bid_cur,
+                                       reinterpret_cast<float*>(lds + STAGE) + wave * (TM / 2) * TN);
+    if (bid == bid_cur) break;
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1058,13 +1194,21 @@ void launch_nt_glds(const ConvArgs& a, hipStream_t st) {
   conv_nt_glds_kernel<BM, BN, WM><<<dim3(nwg), dim3(256), 0, st>>>(a);
 }
 
+template <int BM, int BN, int WM>
+void launch_nt_pers(const ConvArgs& a, hipStream_t st) {
+  const int nwg = ((a.M + BM - 1) / BM) * ((a.Ncol + BN - 1) / BN);
+  const int grid = std::min(nwg, 2 * 256);
+  conv_nt_pers_kernel<BM, BN, WM><<<dim3(grid), dim3(256), 0, st>>>(a);
+}
+
 template <int BN, int WGM, int WGN>
 void launch_nt_p3(const ConvArgs& a, hipStream_t st) {
   const int nwg = ((a.M + 255) / 256) * ((a.Ncol + BN - 1) / BN);
   conv_nt_p3_kernel<BN, WGM, WGN><<<dim3(nwg), dim3(512), 0, st>>>(a);
 }
 
-// BIGDL_CONV_IMPL: 2 = deep-pipelined 256-pixel kernel on grids that fill the chip,
+// BIGDL_CONV_IMPL: 3 = persistent LDS-DMA kernel (next tile's loads overlap the epilogue) on grids of more
+// than two tiles per CU, 2 = deep-pipelined 256-pixel kernel on grids that fill the chip,
 // 1 (default) = LDS-DMA kernel where Cs % 64 == 0, 0 = register-staged kernel everywhere.
 int g_conv_impl = -1;
 int conv_impl() {
@@ -1091,9 +1235,14 @@ int bigdl_conv_nt(const ConvArgs* a, hipStream_t st) {
   const bool fastk = (a->Cs % BK) == 0;
   const int impl = conv_impl();
   const long p3_tiles = (long)((a->M + 255) / 256) * ((a->Ncol + 127) / 128);
+  const long tiles128 = (long)((a->M + 127) / 128) * ((a->Ncol + (a->Ncol <= 64 ? 63 : 127)) / (a->Ncol <= 64 ? 64 : 128));
+  const bool aligned_out = (a->Ncol & 7) == 0 && (a->ldo & 7) == 0;   // the persistent kernel has no fallback epilogue
   if (fastk && impl == 2 && p3_tiles >= 256) {
     if (a->Ncol <= 64) launch_nt_p3<64, 8, 1>(*a, st);
     else launch_nt_p3<128, 4, 2>(*a, st);
+  } else if (fastk && impl == 3 && aligned_out && tiles128 > 2 * 256) {
+    if (a->Ncol <= 64) launch_nt_pers<128, 64, 2>(*a, st);
+    else launch_nt_pers<128, 128, 2>(*a, st);
   } else if (fastk && impl >= 1) {
     if (a->Ncol <= 64) launch_nt_glds<128, 64, 2>(*a, st);
     else launch_nt_glds<128, 128, 2>(*a, st);

@@ -79,14 +79,16 @@ BIG_CASES = [
     (32, 256, 56, 64, 1, 1, 0),
     (16, 128, 56, 256, 3, 2, 1),
     (8, 512, 28, 1000, 1, 1, 0),     # Ncol tail (1000 % 128 != 0)
+    (16, 64, 56, 200, 1, 1, 0),      # persistent kernel: 784 tiles, Ncol tail
+    (24, 64, 57, 128, 1, 1, 0),      # persistent kernel: M tail
 ]
 
 
-@pytest.mark.parametrize("impl", [0, 1, 2])
+@pytest.mark.parametrize("impl", [0, 1, 2, 3])
 @pytest.mark.parametrize("case", BIG_CASES)
 def test_conv_nt_variants_large(case, impl):
-    """Register-staged (0), LDS-DMA (1) and deep-pipelined 3-stage LDS-DMA (2) NT kernels, fwd (+stats) and
-    dgrad, vs fp32 torch."""
+    """Register-staged (0), LDS-DMA (1), deep-pipelined 3-stage LDS-DMA (2) and persistent LDS-DMA (3) NT
+    kernels, fwd (+stats) and dgrad, vs fp32 torch."""
     from bigdl_amd.ops import bn as bnops
     from bigdl_amd.ops import conv as cv
     from bigdl_amd.ops import native
