@@ -160,7 +160,7 @@ void add_bf16(const Tensor& a, const Tensor& b, const Tensor& y) {
 void nchw_to_nhwc(const Tensor& x, const Tensor& y, int64_t Cp) {
   TORCH_CHECK(x.dim() == 4 && x.is_contiguous(), "nchw_to_nhwc: x must be contiguous NCHW");
   const int N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
-  TORCH_CHECK(y.numel() == (int64_t)N * H * W * Cp && Cp >= C, "nchw_to_nhwc: y size");
+  TORCH_CHECK(y.numel() == (int64_t)N * H * W * Cp && Cp >= C && Cp % 8 == 0, "nchw_to_nhwc: y size / Cp % 8");
   bigdl_nchw_f32_to_nhwc_bf16(cf(x, "x"), mbf(y, "y"), N, C, H, W, (int)Cp, stream());
 }
 void cast_f32_bf16(const Tensor& x, const Tensor& y) {

@@ -1167,16 +1167,23 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
   }
 }
 
-__global__ void transpose_krsc_kernel(const bf16_t* __restrict__ w, bf16_t* __restrict__ wt, int K, int RS,
-                                      int C) {
-  // wt[c][rs][k] = w[k][rs][c]
-  const size_t total = (size_t)K * RS * C;
-  for (size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x; idx < total; idx += (size_t)gridDim.x * blockDim.x) {
-    const int k = idx % K;
-    const size_t t = idx / K;
-    const int rs = t % RS;
-    const int c = t / RS;
-    wt[idx] = w[((size_t)k * RS + rs) * C + c];
+// wt[c][rs][k] = w[k][rs][c]: per tap, a [K][C] -> [C][K] transpose through a 64 x 64 LDS tile (coalesced
+// 2-byte reads along c and writes along k; the +1 column pad keeps the column reads conflict-free).
+__global__ __launch_bounds__(256) void transpose_krsc_kernel(const bf16_t* __restrict__ w, bf16_t* __restrict__ wt,
+                                                             int K, int RS, int C) {
+  __shared__ bf16_t tile[64][65];
+  const int c0 = blockIdx.x * 64, k0 = blockIdx.y * 64, rs = blockIdx.z;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int k = k0 + ty + 4 * i, c = c0 + tx;
+    tile[ty + 4 * i][tx] = (k < K && c < C) ? w[((size_t)k * RS + rs) * C + c] : (bf16_t)0;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int c = c0 + ty + 4 * i, k = k0 + tx;
+    if (c < C && k < K) wt[((size_t)c * RS + rs) * K + k] = tile[tx][ty + 4 * i];
   }
 }
 
@@ -1316,10 +1323,8 @@ int bigdl_conv_wgrad(const WgradArgs* a_in, hipStream_t st) {
 }
 
 void bigdl_transpose_krsc(const bf16_t* w, bf16_t* wt, int K, int RS, int C, hipStream_t st) {
-  const size_t total = (size_t)K * RS * C;
-  int blocks = (int)((total + 255) / 256);
-  if (blocks > 4096) blocks = 4096;
-  transpose_krsc_kernel<<<blocks, 256, 0, st>>>(w, wt, K, RS, C);
+  if (RS > 65535) return;
+  transpose_krsc_kernel<<<dim3((C + 63) / 64, (K + 63) / 64, RS), 256, 0, st>>>(w, wt, K, RS, C);
   HIP_LAUNCH_CHECK();
 }
 

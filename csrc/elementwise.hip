@@ -63,18 +63,22 @@ __global__ void add_tail(const bf16_t* a, const bf16_t* b, bf16_t* y, long s, lo
   GRID_STRIDE(i, n - s) y[s + i] = f2bf(bf2f(a[s + i]) + bf2f(b[s + i]));
 }
 
-// NCHW fp32 (the user-facing BigDL layout) -> NHWC bf16 with channel padding to Cp (zeros)
-__global__ void nchw_to_nhwc_kernel(const float* __restrict__ x, bf16_t* __restrict__ y, int N, int C, int H, int W,
-                                    int Cp) {
-  const long total = (long)N * H * W * Cp;
-  GRID_STRIDE(i, total) {
-    const int c = i % Cp;
-    const long p = i / Cp;
-    const int w = p % W;
-    const long t = p / W;
-    const int h = t % H;
-    const int n = t / H;
-    y[i] = c < C ? f2bf(x[(((long)n * C + c) * H + h) * W + w]) : (bf16_t)0;
+// NCHW fp32 (the user-facing BigDL layout) -> NHWC bf16 with channel padding to Cp (zeros). One thread per
+// (pixel, 8-channel group): the C plane reads are coalesced along the pixel axis, the 8 bf16 channels leave
+// as one 16-byte store, and blockIdx.y = (image, group) keeps 64-bit division out of the loop.
+__global__ __launch_bounds__(256) void nchw_to_nhwc_kernel(const float* __restrict__ x, bf16_t* __restrict__ y,
+                                                           int N, int C, int H, int W, int Cp) {
+  const int HW = H * W, G = Cp >> 3;
+  const int hw = blockIdx.x * 256 + threadIdx.x;
+  if (hw >= HW) return;
+  for (int ng = blockIdx.y; ng < N * G; ng += gridDim.y) {
+    const int n = ng / G, g = ng - n * G;
+    const float* src = x + ((long)n * C + g * 8) * HW + hw;
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = (g * 8 + e < C) ? src[(long)e * HW] : 0.f;
+    *reinterpret_cast<v4u*>(y + ((long)n * HW + hw) * Cp + g * 8) =
+        v4u{pack2bf(v[0], v[1]), pack2bf(v[2], v[3]), pack2bf(v[4], v[5]), pack2bf(v[6], v[7])};
   }
 }
 __global__ void cast_f32_bf16_kernel(const float* __restrict__ x, bf16_t* __restrict__ y, long n) {
@@ -467,7 +471,9 @@ void bigdl_add_bf16(const uint16_t* a, const uint16_t* b, uint16_t* y, long n, h
   HIP_LAUNCH_CHECK();
 }
 void bigdl_nchw_f32_to_nhwc_bf16(const float* x, uint16_t* y, int N, int C, int H, int W, int Cp, hipStream_t st) {
-  nchw_to_nhwc_kernel<<<grid_cap((long)N * H * W * Cp), 256, 0, st>>>(x, y, N, C, H, W, Cp);
+  if (Cp % 8 != 0) return;   // the host pads channels to a multiple of 8
+  const dim3 grid((H * W + 255) / 256, std::min(N * (Cp / 8), 65535));
+  nchw_to_nhwc_kernel<<<grid, 256, 0, st>>>(x, y, N, C, H, W, Cp);
   HIP_LAUNCH_CHECK();
 }
 void bigdl_cast_f32_bf16(const float* x, uint16_t* y, long n, hipStream_t st) {

@@ -377,3 +377,27 @@ def test_bf16_truncation_kernel():
     got = nnk.f32_to_bf16_rtz(x.cuda()).cpu()
     assert torch.equal(got.view(torch.int16), ref.view(torch.int16))
     assert torch.all(got.float().abs() <= x.abs())         # toward zero
+
+
+@pytest.mark.parametrize("K,C,R", [(64, 8, 7), (200, 72, 3), (1000, 2048, 1), (3, 5, 2)])
+def test_transpose_krsc_exact(K, C, R):
+    from bigdl_amd.ops import conv as cv
+
+    dev = _dev()
+    w = torch.randn(K, C, R, R, device=dev).to(BF, memory_format=CL)
+    wt = cv.transpose_w(w)
+    ref = w.permute(1, 2, 3, 0).contiguous()      # (C, R, S, K)
+    assert torch.equal(wt, ref)
+
+
+@pytest.mark.parametrize("shape", [(3, 3, 17, 19), (2, 12, 5, 7), (4, 3, 224, 224)])
+def test_nchw_to_nhwc_bf16_exact(shape):
+    from bigdl_amd.ops import conv as cv
+
+    dev = _dev()
+    x = torch.randn(*shape, device=dev)
+    y = cv.to_nhwc_bf16(x)
+    C = shape[1]
+    assert y.shape[1] % 8 == 0 and y.is_contiguous(memory_format=CL)
+    assert torch.equal(y[:, :C].float(), x.to(BF).float())
+    assert not y[:, C:].float().any()
