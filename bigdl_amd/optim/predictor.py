@@ -4,14 +4,13 @@ Reference: S/optim/Predictor.scala:35-257 (distributed predict / predictClass / 
 LocalPredictor.scala:33-197, PredictionService.scala:56-354 (pool of model clones, ``predict(Activity)``
 :79 and ``predict(bytes)`` :128 with (de)serialized activities).
 
-On MI355X the "pool of clones" is one resident model per GPU plus a lock-protected request path; requests
-are batched on the device stream. ``predict(bytes)`` uses a small self-describing tensor wire format
+On MI355X the "pool of clones" is a pool of replicas that share one copy of the weights, each with its own
+HIP stream, so concurrent requests overlap on the device. ``predict(bytes)`` uses a small self-describing tensor wire format
 (JSON header + raw little-endian payload) instead of the reference's protobuf Activity message.
 """
 import io
 import json
 import struct
-import threading
 
 import torch
 
@@ -130,13 +129,40 @@ def deserialize_activity(b):
     return dec(header)
 
 
+def _share_weights(src, dst):
+    """Point the parameters and buffers of the clone ``dst`` at the tensors of ``src`` (replicas differ only in
+    their activation buffers)."""
+    for a, b in zip(src.flattened_layers(), dst.flattened_layers()):
+        for w, _ in getattr(a, "_params", ()):
+            t = getattr(a, w, None)
+            if t is not None:
+                setattr(b, w, t)
+        for name in getattr(a, "_buffers", ()):
+            t = getattr(a, name, None)
+            if t is not None:
+                setattr(b, name, t)
+
+
 class PredictionService:
-    """Thread-safe serving of one model (reference PredictionService.scala:56-354)."""
+    """Thread-safe serving (reference PredictionService.scala:56-354): a pool of ``numThreads`` model replicas
+    sharing one copy of the weights; on the GPU each replica owns a HIP stream, so concurrent requests run
+    concurrently on the device instead of queueing behind one lock."""
 
     def __init__(self, model, numThreads=1):
+        import queue
+
         self.model = model.evaluate()
-        self._lock = threading.Lock()
-        self.numThreads = numThreads
+        self.numThreads = max(1, int(numThreads))
+        dev = getattr(self.model, "device", torch.device("cpu"))
+        self._pool = queue.Queue()
+        for i in range(self.numThreads):
+            m = self.model
+            if i > 0:
+                m = self.model.cloneModule()
+                _share_weights(self.model, m)
+                m.evaluate()
+            stream = torch.cuda.Stream(device=dev) if dev.type == "cuda" else None
+            self._pool.put((m, stream))
 
     def predict(self, request):
         if isinstance(request, (bytes, bytearray, memoryview)):
@@ -149,10 +175,16 @@ class PredictionService:
         return self._run(request)
 
     def _run(self, act):
-        dev = self.model.device
-        act = act.to(dev) if hasattr(act, "to") else act
-        with self._lock, torch.no_grad():
-            out = self.model.forward(act)
-            if isinstance(out, torch.Tensor):
-                return out.float().cpu()
-            return out.to("cpu")
+        import contextlib
+
+        model, stream = self._pool.get()
+        try:
+            dev = getattr(model, "device", torch.device("cpu"))
+            ctx = torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()
+            with ctx, torch.no_grad():
+                act = act.to(dev) if hasattr(act, "to") else act
+                out = model.forward(act)
+                out = out.float().cpu() if isinstance(out, torch.Tensor) else out.to("cpu")
+            return out
+        finally:
+            self._pool.put((model, stream))

@@ -221,6 +221,27 @@ def test_prediction_service_bytes_roundtrip():
     assert torch.equal(t[2], torch.arange(3))
 
 
+def test_prediction_service_replica_pool_concurrent():
+    from concurrent.futures import ThreadPoolExecutor
+
+    model = _mlp()
+    svc = O.PredictionService(model, numThreads=3)
+    assert svc._pool.qsize() == 3
+    replicas = [svc._pool.get() for _ in range(3)]
+    for r in replicas:
+        svc._pool.put(r)
+    def first_weight(m):
+        return [q for q in m.flattened_layers() if getattr(q, "weight", None) is not None][0].weight
+
+    # replicas share the weight tensors, not copies
+    assert all(first_weight(r[0]) is first_weight(model) for r in replicas)
+    xs = [torch.randn(5, 4) for _ in range(12)]
+    with ThreadPoolExecutor(4) as ex:
+        outs = list(ex.map(svc.predict, xs))
+    for x, o in zip(xs, outs):
+        assert torch.allclose(o, model.forward(x), atol=1e-6)
+
+
 def test_optim_method_save_load(tmp_path):
     sgd = O.SGD(0.1, momentum=0.9)
     x = torch.tensor([1.0, 2.0])
