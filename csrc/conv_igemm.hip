@@ -1167,23 +1167,27 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
   }
 }
 
-// wt[c][rs][k] = w[k][rs][c]: per tap, a [K][C] -> [C][K] transpose through a 64 x 64 LDS tile (coalesced
-// 2-byte reads along c and writes along k; the +1 column pad keeps the column reads conflict-free).
+// wt[c][rs][k] = w[k][rs][c]: per tap, a [K][C] -> [C][K] transpose through a 32 x 32 LDS tile (coalesced
+// reads along c and writes along k, +1 column pad against bank conflicts). Small tiles keep >= 4 workgroups on
+// the 64 x 64 layers: most of the 53 per-step launches are latency-, not bandwidth-bound.
 __global__ __launch_bounds__(256) void transpose_krsc_kernel(const bf16_t* __restrict__ w, bf16_t* __restrict__ wt,
                                                              int K, int RS, int C) {
-  __shared__ bf16_t tile[64][65];
-  const int c0 = blockIdx.x * 64, k0 = blockIdx.y * 64, rs = blockIdx.z;
-  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  __shared__ bf16_t tile[32][33];
+  const int c0 = blockIdx.x * 32, k0 = blockIdx.y * 32, rs = blockIdx.z;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  bf16_t v[4];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int k = k0 + ty + 4 * i, c = c0 + tx;
-    tile[ty + 4 * i][tx] = (k < K && c < C) ? w[((size_t)k * RS + rs) * C + c] : (bf16_t)0;
+  for (int i = 0; i < 4; ++i) {
+    const int k = k0 + ty + 8 * i, c = c0 + tx;
+    v[i] = (k < K && c < C) ? w[((size_t)k * RS + rs) * C + c] : (bf16_t)0;
   }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) tile[ty + 8 * i][tx] = v[i];
   __syncthreads();
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int c = c0 + ty + 4 * i, k = k0 + tx;
-    if (c < C && k < K) wt[((size_t)c * RS + rs) * K + k] = tile[tx][ty + 4 * i];
+  for (int i = 0; i < 4; ++i) {
+    const int c = c0 + ty + 8 * i, k = k0 + tx;
+    if (c < C && k < K) wt[((size_t)c * RS + rs) * K + k] = tile[tx][ty + 8 * i];
   }
 }
 
@@ -1324,7 +1328,7 @@ int bigdl_conv_wgrad(const WgradArgs* a_in, hipStream_t st) {
 
 void bigdl_transpose_krsc(const bf16_t* w, bf16_t* wt, int K, int RS, int C, hipStream_t st) {
   if (RS > 65535) return;
-  transpose_krsc_kernel<<<dim3((C + 63) / 64, (K + 63) / 64, RS), 256, 0, st>>>(w, wt, K, RS, C);
+  transpose_krsc_kernel<<<dim3((C + 31) / 32, (K + 31) / 32, RS), 256, 0, st>>>(w, wt, K, RS, C);
   HIP_LAUNCH_CHECK();
 }
 
