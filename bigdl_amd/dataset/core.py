@@ -376,3 +376,9 @@ class DataSet:
 
 def batches_per_epoch(size, batch):
     return int(math.ceil(size / float(batch)))
+
+
+# reference names (S/dataset/DataSet.scala, MiniBatch.scala): one local dataset type and one dense mini-batch type
+LocalDataSet = AbstractDataSet
+CachedDistriDataSet = DistributedDataSet
+ArrayTensorMiniBatch = MiniBatch

@@ -527,7 +527,8 @@ def save_tf(model, inputs, path, byteOrder=None, dataFormat="NHWC"):
     return out
 
 
-__all__ = ["load_tf", "save_tf", "read_graph", "parse_graph", "attrs_of", "tensor_of", "SCHEMA"]
+__all__ = ["load_tf", "save_tf", "read_graph", "parse_graph", "attrs_of", "tensor_of", "SCHEMA", "TensorflowLoader",
+           "TensorflowSaver", "TensorflowToBigDL", "BigDLToTensorflow"]
 
 
 class Session:
@@ -550,3 +551,22 @@ class Session:
         model.evaluate()
         with torch.no_grad():
             return model.forward(x)
+
+
+class TensorflowLoader:
+    """Reference S/utils/tf/TensorflowLoader.scala:55 ``load(graphFile, inputs, outputs, byteOrder, binFile)``."""
+
+    load = staticmethod(load_tf)
+    parse = staticmethod(parse_graph)
+
+
+class TensorflowSaver:
+    """Reference S/utils/tf/TensorflowSaver.scala:36 ``saveGraph(model, inputs, path, byteOrder, dataFormat)``."""
+
+    @staticmethod
+    def saveGraph(model, inputs, path, byteOrder=None, dataFormat="NHWC"):
+        return save_tf(model, inputs, path, byteOrder, dataFormat)
+
+
+TensorflowToBigDL = TensorflowLoader     # op-by-op conversion lives in the loader (TensorflowToBigDL.scala:41)
+BigDLToTensorflow = TensorflowSaver      # module-by-module emission lives in the saver (BigDLToTensorflow.scala:33)

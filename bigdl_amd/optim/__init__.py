@@ -3,7 +3,7 @@ from .evaluator import DistriValidator, Evaluator, LocalValidator, Validator  # 
 from .methods import *  # noqa: F401,F403
 from .metrics import Metrics  # noqa: F401
 from .optim_method import OptimMethod  # noqa: F401
-from .optimizer import DistriOptimizer, LocalOptimizer, Optimizer, ParallelOptimizer  # noqa: F401
+from .optimizer import AbstractOptimizer, DistriOptimizer, LocalOptimizer, Optimizer, ParallelOptimizer  # noqa: F401
 from .predictor import LocalPredictor, PredictionService, Predictor  # noqa: F401
 from .regularizer import L1L2Regularizer, L1Regularizer, L2Regularizer, Regularizer  # noqa: F401
 from .sgd import *  # noqa: F401,F403

@@ -402,3 +402,6 @@ def create(model, training_set, criterion, end_trigger=None, batch_size=32, opti
 
 
 Optimizer.create = staticmethod(create)
+
+
+AbstractOptimizer = Optimizer   # reference AbstractOptimizer.scala:33 — shared validate / checkpoint / summary logic

@@ -242,3 +242,26 @@ def load_module(path, weightPath=None):
         wp = weightPath or os.path.join(os.path.dirname(path), meta["weights"])
         tensors.update(load_file(wp))
     return decode_module(doc["module"], tensors)
+
+
+class ModuleSerializer:
+    """Reference S/utils/serializer/ModuleSerializer.scala:36 (serialize / load of one module)."""
+
+    serialize = staticmethod(encode_module)
+    load = staticmethod(decode_module)
+
+
+class ModuleLoader:
+    """Reference ModuleLoader.scala:37 ``loadFromFile(path, weightPath)``."""
+
+    @staticmethod
+    def loadFromFile(modelPath, weightPath=None):
+        return load_module(modelPath, weightPath)
+
+
+class ModulePersister:
+    """Reference ModuleLoader.scala:230 ``saveToFile(path, weightPath, module, overwrite)``."""
+
+    @staticmethod
+    def saveToFile(modelPath, weightPath, module, overwrite=False):
+        return save_module(module, modelPath, weightPath, overwrite)

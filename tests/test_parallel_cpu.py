@@ -122,3 +122,44 @@ def test_bucketed_overlap_equals_plain_zero1():
     b = run_distributed(_plain_job, 2, ((X, Y), 4))
     assert torch.allclose(a[0], a[1], atol=1e-6)
     assert torch.allclose(a[0], b[0], atol=1e-5)
+
+
+def _bcast_worker(rank, world, port, q):
+    import os
+
+    import torch
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bigdl_amd.nn as nn
+    from bigdl_amd.parallel.broadcast import ModelBroadcast
+
+    torch.manual_seed(rank)
+    m = nn.Sequential().add(nn.Linear(4, 3)).add(nn.BatchNormalization(3))
+    with torch.no_grad():
+        m.modules[1].runningMean.fill_(float(rank))
+    ModelBroadcast().broadcast(m)
+    q.put((rank, m.modules[0].weight.clone(), m.modules[1].runningMean.clone()))
+    dist.destroy_process_group()
+
+
+def test_model_broadcast_gloo():
+    import multiprocessing as mp
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_bcast_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = dict((r, (w, rm)) for r, w, rm in (q.get(timeout=120) for _ in ps))
+    for p in ps:
+        p.join(60)
+    assert torch.equal(res[0][0], res[1][0])
+    assert torch.equal(res[1][1], torch.zeros(3))

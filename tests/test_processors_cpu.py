@@ -41,3 +41,18 @@ def test_int8_convertible_scales():
     seq.calcScales(torch.randn(2, 3, 8, 8))
     assert seq.modules[0].getInputScales()[0][0] > 0
     assert callable(nn.NNPrimitive.im2col)
+
+
+def test_reference_named_entry_points(tmp_path):
+    import bigdl_amd.dataset as D
+    import bigdl_amd.optim as O
+    from bigdl_amd.interop.tensorflow import BigDLToTensorflow, TensorflowLoader, TensorflowSaver, TensorflowToBigDL
+    from bigdl_amd.utils.serializer import ModuleLoader, ModulePersister
+
+    assert D.ArrayTensorMiniBatch is D.MiniBatch and O.AbstractOptimizer is O.Optimizer
+    assert TensorflowToBigDL is TensorflowLoader and BigDLToTensorflow is TensorflowSaver
+    m = nn.Sequential().add(nn.Linear(3, 2))
+    p = str(tmp_path / "m.bigdl")
+    ModulePersister.saveToFile(p, None, m, True)
+    x = torch.randn(2, 3)
+    assert torch.allclose(ModuleLoader.loadFromFile(p).forward(x), m.forward(x))
