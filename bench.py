@@ -33,6 +33,7 @@ def parse():
     ap.add_argument("--depth", type=int, default=50)
     ap.add_argument("--compress", default=None, choices=[None, "bf16"])
     ap.add_argument("--graph", type=int, default=1, help="capture the training step in a HIP graph")
+    ap.add_argument("--bucket", type=int, default=8, help="gradient bucket size, M elements (N > 1)")
     ap.add_argument("--profile-steps", type=int, default=0)
     return ap.parse_args()
 
@@ -64,7 +65,7 @@ def main():
     model = ResNet(1000, args.depth, dataSet=DatasetType.ImageNet)
     crit = nn.CrossEntropyCriterion()
     optim = SGD(learningRate=0.1, momentum=0.9, dampening=0.0)
-    step = TrainStep(model, crit, optim, device=dev, compress=args.compress)
+    step = TrainStep(model, crit, optim, device=dev, compress=args.compress, bucket_elems=args.bucket << 20)
 
     B = args.batch
     g = torch.Generator(device=dev)
@@ -79,29 +80,23 @@ def main():
             dist.barrier()
 
     run = lambda: step.step(x, y)  # noqa: E731
-    for _ in range(max(args.warmup, 2)):
-        run()
-    torch.cuda.synchronize()
     graph = None
-    if args.graph and world == 1:
+    if args.graph:
+        from bigdl_amd.optim.graphed import GraphedTrainStep
+
         try:
-            s = torch.cuda.Stream()
-            s.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(s):
-                run()
-            torch.cuda.current_stream().wait_stream(s)
-            torch.cuda.synchronize()
-            graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graph):
-                run()
-            graph.replay()
-            torch.cuda.synchronize()
+            graph = GraphedTrainStep(step, x, y, warmup=max(args.warmup, 2))
             run = graph.replay  # noqa: F811
+            for _ in range(2):
+                run()
         except Exception as e:  # fall back to eager launches
             print(f"[bench] HIP graph capture failed ({type(e).__name__}: {e}); running eager", file=sys.stderr)
             graph = None
             run = lambda: step.step(x, y)  # noqa: E731
-            torch.cuda.synchronize()
+    else:
+        for _ in range(max(args.warmup, 2)):
+            run()
+    torch.cuda.synchronize()
 
     barrier()
     torch.cuda.synchronize()
@@ -118,6 +113,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt = float(t.item())
     loss = float(step.loss.item()) if step.loss is not None else float("nan")
+    step.flush()
     ms = dt / args.steps * 1e3
     ips = B * world * args.steps / dt
     if rank == 0:
@@ -137,7 +133,8 @@ def main():
             "config": {"model": f"ResNet-{args.depth} v1.5 (BigDL ImageNet builder)", "global_batch": B * world,
                        "per_gpu_batch": B, "seq_len": None, "image": args.image, "parallelism": f"dp{world}",
                        "optimizer": "SGD momentum 0.9 + L2 1e-4 (ZeRO-1 sharded over RCCL)",
-                       "hip_graph": graph is not None, "final_loss": round(loss, 4)},
+                       "hip_graph": graph is not None, "bucketed_overlap": step.bucketed is not None,
+                       "grad_compress": args.compress, "final_loss": round(loss, 4)},
         }), flush=True)
     Engine.shutdown()
 

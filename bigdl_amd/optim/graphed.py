@@ -1,0 +1,69 @@
+"""A training step captured once into a HIP graph and replayed (runtime counterpart of the reference's
+per-iteration task launch, S/optim/DistriOptimizer.scala:204-396 — here the whole iteration, including the
+RCCL reduce-scatter / all-gather, is ONE ``hipGraphLaunch``).
+
+Capture rules this wrapper enforces:
+  * warm-up steps run eagerly first (kernel plans, workspaces, momentum buffers and RCCL communicators are
+    created outside the capture; the SGD "first step" branch is never captured);
+  * the input batch lives in static device buffers: ``replay(x, y)`` copies the new batch into them;
+  * the learning-rate schedule keeps advancing: every captured SGD reads its rate from a device scalar that
+    ``replay`` refreshes on the host side of the graph (``SGD.graph_prologue``) — methods whose update
+    depends on host values that change per step (Adam bias correction, LARS) are refused;
+  * nothing in the step synchronises with the host (TrainStep guarantees it), so capture succeeds with the
+    collectives inside.
+"""
+import torch
+
+from .sgd import SGD
+
+
+class GraphedTrainStep:
+    def __init__(self, step, x, y, warmup=2):
+        self.step = step
+        for p in step.plan:
+            if type(p.method) is not SGD:
+                raise TypeError(f"GraphedTrainStep: {type(p.method).__name__} updates depend on per-step host "
+                                "values; use the eager TrainStep")
+        self.x = x.clone()
+        self.y = y.clone()
+        for _ in range(max(warmup, 1)):
+            step.step(self.x, self.y)
+        torch.cuda.synchronize()
+        methods = []
+        for p in step.plan:
+            if getattr(p.method, "_lr_dev", None) is None:
+                p.method._lr_dev = torch.zeros(1, device=step.device)
+            methods.append(p.method)
+        self.methods = methods
+        self._prologue()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):          # one more eager step on the capture stream (allocator warm-up)
+            step.step(self.x, self.y)
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        self._prologue()
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.loss = step.step(self.x, self.y)
+        self._fresh = True                  # capture did not execute: the first replay uses this prologue
+
+    def _prologue(self):
+        for m in self.methods:
+            m.graph_prologue()
+
+    def replay(self, x=None, y=None):
+        if x is not None:
+            self.x.copy_(x, non_blocking=True)
+        if y is not None:
+            self.y.copy_(y, non_blocking=True)
+        if not self._fresh:
+            self._prologue()
+        self._fresh = False
+        self.graph.replay()
+        return self.loss
+
+    def release(self):
+        for m in self.methods:
+            m._lr_dev = None
+        self.graph = None

@@ -279,13 +279,20 @@ class LarsSGD(SGD):
         self.learningRateSchedule.updateHyperParameter(self)
         global_lr = -self.learningRateSchedule.currentRate * self.trust
         if self._calculated_scale is not None:
-            scale = self._calculated_scale
+            scale = self._calculated_scale          # layer-global scale from LarsProcessor (device tensor ok)
             self._calculated_scale = None
         else:
             nw = float(x.norm())
             ng = float(g.norm())
-            scale = (ng + self.weightDecay * nw) / nw if nw > 0 else 1.0
-        rate = global_lr / scale if scale != 0 else global_lr
+            scale = (ng + self.weightDecay * nw) / nw if nw > 0 else float("inf")
+            # reference getGradientScale guards (LarsSGD.scala:100-112)
+            if math.isinf(scale):
+                scale = 10000.0
+            elif math.isnan(scale):
+                scale = 1.0
+            elif abs(scale) < 1e-4:
+                scale = 1e-4
+        rate = global_lr / scale
         v.mul_(self.momentum).add_((g + self.weightDecay * x) * rate)
         x.sub_(v)
         _sync_shadow(self, x)

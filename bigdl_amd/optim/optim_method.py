@@ -7,7 +7,6 @@ in place. On the GPU engine ``x`` / ``dfdx`` are the flat fp32 master buffers pr
 pass (``attach_shadow``).
 """
 import copy
-import pickle
 
 import torch
 
@@ -59,32 +58,31 @@ class OptimMethod:
         return c
 
     def save(self, path, overWrite=False):
+        """Persist this method (hyper-parameters, schedule, state table) as a safetensors file with a JSON
+        structure header (utils/safe_state.py): nothing in the file is executed when it is loaded."""
         import os
+
+        from ..utils import safe_state
 
         if os.path.exists(path) and not overWrite:
             raise FileExistsError(path)
-        with open(path, "wb") as f:
-            pickle.dump(self._to_portable(), f)
+        sh = self._shadow16
+        self._shadow16 = None
+        try:
+            safe_state.save(self, path)
+        finally:
+            self._shadow16 = sh
         return self
-
-    def _to_portable(self):
-        d = {}
-        for k, v in self.__dict__.items():
-            if k == "_shadow16":
-                continue
-            d[k] = _cpu(v)
-        return {"class": type(self).__name__, "module": type(self).__module__, "dict": d}
 
     @staticmethod
     def load(path):
-        """Load an OptimMethod saved by ``save`` (files written by this framework only)."""
-        import importlib
+        """Load an OptimMethod saved by ``save``; only OptimMethod / schedule classes of this package are
+        instantiated."""
+        from ..utils import safe_state
 
-        with open(path, "rb") as f:
-            obj = pickle.load(f)  # noqa: S301 - own checkpoint format
-        cls = getattr(importlib.import_module(obj["module"]), obj["class"])
-        m = cls.__new__(cls)
-        m.__dict__.update(obj["dict"])
+        m = safe_state.load(path)
+        if not isinstance(m, OptimMethod):
+            raise ValueError(f"{path} does not hold an OptimMethod")
         m._shadow16 = None
         return m
 

@@ -172,15 +172,16 @@ class Optimizer:
 
     # ---------------------------------------------------------------- core loop
     _overlap = False
+    _expand = False
+    _priorities = None
 
     def _optim_method(self):
-        if len(self.optimMethods) != 1:
-            raise NotImplementedError("per-submodule optim methods: use ParallelOptimizer")
         return next(iter(self.optimMethods.values()))
 
     def _make_step(self, comm=None):
-        return TrainStep(self.model, self.criterion, self._optim_method(), device=self.device, comm=comm,
-                         compress=self.compress, overlap=self._overlap)
+        return TrainStep(self.model, self.criterion, dict(self.optimMethods), device=self.device, comm=comm,
+                         compress=self.compress, overlap=self._overlap, processors=self._processors(),
+                         expand_methods=self._expand, priorities=self._priorities)
 
     def _processors(self):
         """Clipping as ParameterProcessors (reference ParameterOperations.scala), constant clipping first."""
@@ -193,10 +194,6 @@ class Optimizer:
             out.append(L2NormClippingProcessor(self.l2NormClip))
         return out
 
-    def _clip(self, step):
-        for p in self._processors():
-            p(step.g_shard, step.comm)
-
     def _header(self, epoch, n, iteration, wall):
         return f"[Epoch {epoch} {n}/{self._epoch_size()}][Iteration {iteration}][Wall Clock {wall:.3f}s]"
 
@@ -204,49 +201,94 @@ class Optimizer:
         return self.dataset.size()
 
     def optimize(self):
+        """Train until ``endWhen``; returns the model holding the exact trained weights on every rank.
+
+        Failure policy (reference DistriOptimizer.scala:881-963): argument errors propagate; any other error is
+        retried from the latest checkpoint (model + per-method state, each method's history cleared) up to
+        ``bigdl.failure.retryTimes``. In a multi-rank job a failing rank cannot re-enter the collectives of the
+        others, so the error propagates and the launcher (torch.distributed.run --max-restarts) restarts the
+        whole job, which resumes from the same checkpoint through ``bigdl.failure.resume``."""
         retries = 0
+        if self.checkpointPath is not None and Engine.getProperty("bigdl.failure.resume", None) and \
+                self._restore_latest():
+            logger.info("resumed from the latest checkpoint in %s", self.checkpointPath)
+        if self._step is None and not getattr(self, "_resumed", False):
+            for om in self.optimMethods.values():      # reference optimize(): fresh optimizer history
+                om.clearHistory()
         while True:
             try:
                 return self._optimize_once()
-            except KeyboardInterrupt:
+            except (KeyboardInterrupt, ValueError, TypeError):
                 raise
             except Exception:
                 retries += 1
-                if retries > self.retryTimes or self.checkpointPath is None:
+                if retries > self.retryTimes or self.checkpointPath is None or Engine.world_size() > 1:
                     raise
                 logger.exception("training failed; retrying from the last checkpoint (%d/%d)", retries,
                                  self.retryTimes)
-                self._restore_latest()
+                if self._restore_latest():
+                    for om in self.optimMethods.values():   # reference :946 newOptimMethod.clearHistory()
+                        om.clearHistory()
+
+    @staticmethod
+    def _latest(path, prefix):
+        best, best_n = None, -1
+        for f in os.listdir(path):
+            if not f.startswith(prefix + "."):
+                continue
+            suf = f[len(prefix) + 1:]
+            n = int(suf) if suf.isdigit() else (10 ** 12 if suf == "latest" else -1)
+            if n > best_n:
+                best, best_n = f, n
+        return best
 
     def _restore_latest(self):
+        """Reload the newest model and every method from ``checkpointPath`` (history cleared like the
+        reference). Returns True when a model snapshot was found."""
         from ..utils.serializer import load_module
         from .optim_method import OptimMethod
 
-        files = [f for f in os.listdir(self.checkpointPath) if f.startswith("model.")]
-        if not files:
-            return
-        last = max(files, key=lambda f: int(f.split(".")[1]) if f.split(".")[1].isdigit() else -1)
-        suffix = last.split(".", 1)[1]
+        last = self._latest(self.checkpointPath, "model")
+        if last is None:
+            return False
         m = load_module(os.path.join(self.checkpointPath, last))
+        old = self.model
         self.model = m
-        om = os.path.join(self.checkpointPath, f"optimMethod.{suffix}")
-        if os.path.exists(om):
-            self.optimMethods = {m.getName(): OptimMethod.load(om)}
+        methods = {}
+        for name, om in self.optimMethods.items():
+            key = m.getName() if name == old.getName() else name
+            f = self._latest(self.checkpointPath, f"optimMethod-{name}")
+            nm = OptimMethod.load(os.path.join(self.checkpointPath, f)) if f else om
+            methods[key] = nm
+        self.optimMethods = methods
+        first = next(iter(methods.values()))
+        for k in ("epoch", "neval"):
+            if first.state.get(k) is not None:
+                self.state[k] = first.state[k]
+        self._resumed = True
         self._step = None
+        return True
+
+    def _sync_states(self, st):
+        for om in self.optimMethods.values():
+            om.state["epoch"] = st["epoch"]
+            om.state["neval"] = st["neval"]
+            if "Loss" in st.keys():
+                om.state["Loss"] = st["Loss"]
+            if "score" in st.keys():
+                om.state["score"] = st["score"]
 
     def _optimize_once(self):
         st = self.state
         st["epoch"] = st.get("epoch", 1)
         st["neval"] = st.get("neval", 1)
         st["recordsProcessedThisEpoch"] = st.get("recordsProcessedThisEpoch", 0)
-        om = self._optim_method()
-        om.state["epoch"] = st["epoch"]
-        om.state["neval"] = st["neval"]
+        self._sync_states(st)
         if self._step is None:
             self._step = self._make_step()
         step = self._step
         world = step.comm.world
-        rank = step.comm.rank
+        drop = _StragglerDrop(self, world) if self.dropPercentage > 0 else None
         it = iter(self.dataset.data(train=True))
         wall0 = time.perf_counter()
         pending = []  # (iteration, loss tensor, records)
@@ -254,39 +296,48 @@ class Optimizer:
             t0 = time.perf_counter()
             batch = next(it)
             batch = batch.to(step.device, non_blocking=True)
-            self.metrics.add("data fetch time", time.perf_counter() - t0)
+            fetch = time.perf_counter() - t0
+            self.metrics.add("data fetch time", fetch)
             t1 = time.perf_counter()
-            step.zero_grad()
-            loss = step.forward_backward(batch.getInput(), batch.getTarget())
-            if step.bucketed is not None:          # ParallelOptimizer: buckets already in flight
-                self._clip(step)
-                step.bucketed.update(loss)
+            finished = None
+            if drop is not None and drop.timed_out(fetch):
+                # straggler: the deadline passed before compute could start — contribute nothing this iteration
+                loss = torch.zeros((), device=step.device)
+                finished = 0.0
             else:
-                step.comm.reduce_scatter_gradients(step.g, out=step.g_shard)
-                if self.constantClip is not None or self.l2NormClip is not None:
-                    self._clip(step)
-                om.optimize(lambda _: (loss, step.g_shard), step.w_shard)
-                if world > 1:
-                    step.comm.all_gather_weights(step.w16 if step.w16 is not None else step.w)
+                step.zero_grad()
+                loss = step.forward_backward(batch.getInput(), batch.getTarget())
+                if drop is not None:
+                    finished = drop.finished(time.perf_counter() - t0)
+            if finished is not None:
+                step.min_finished = world * (1.0 - self.maxDropPercentage)
+                n_ok = drop.record(step.sync_and_update(loss, finished=finished), finished)
+            else:
+                step.sync_and_update(loss)
+                n_ok = 1
             self.metrics.add("computing time", time.perf_counter() - t1)
             records = batch.size() * world
             pending.append((st["neval"], loss.detach() if torch.is_tensor(loss) else torch.tensor(float(loss)),
                             records))
             st["neval"] += 1
-            om.state["neval"] = st["neval"]
             st["recordsProcessedThisEpoch"] += records
+            self._sync_states(st)
+            if drop is not None:
+                drop.maybe_update_threshold(step, st["neval"] - 1)
             need_loss = (self.logInterval > 0 and (st["neval"] - 1) % self.logInterval == 0)
             if need_loss or self.endWhen(st) or isinstance(self.endWhen, Trigger.minLoss(0).__class__):
                 self._flush_losses(step, pending, wall0)
                 pending = []
             if st["recordsProcessedThisEpoch"] >= self._epoch_size():
                 st["epoch"] += 1
-                om.state["epoch"] = st["epoch"]
                 st["recordsProcessedThisEpoch"] = 0
+                self._sync_states(st)
             self._validate(step)
             self._checkpoint(step)
+            del n_ok
         if pending:
             self._flush_losses(step, pending, wall0)
+        step.gather_model()
         if self.device.type == "cuda":
             torch.cuda.synchronize()
         return self.model
@@ -343,6 +394,7 @@ class Optimizer:
             return
         from .evaluator import evaluate_dataset
 
+        step.flush()
         results = evaluate_dataset(self.model, self.validationDataSet, self.validationMethods, device=step.device)
         self.model.training()
         for r, m in zip(results, self.validationMethods):
@@ -355,20 +407,88 @@ class Optimizer:
         self._last_validation = results
 
     def _checkpoint(self, step):
+        """Reference AbstractOptimizer.checkpoint: the gathered model (getModel) as ``model.<neval>`` and every
+        method as ``optimMethod-<name>.<neval>`` with its FULL optimizer state (gathered from every rank's
+        shard pieces, so a checkpoint restores on any number of ranks). Collective."""
         if self.checkpointTrigger is None or self.checkpointPath is None:
             return
         if not self.checkpointTrigger(self.state):
             return
-        if step.comm.world > 1 and step.w16 is None:
-            pass  # fp32 weights already all-gathered each iteration
-        suffix = "" if self.isOverWrite else f".{self.state['neval'] - 1}"
+        step.gather_model()
+        methods = step.gather_optim_state()
+        neval = self.state["neval"] - 1
+        suffix = ".latest" if self.isOverWrite else f".{neval}"
         if step.comm.rank == 0:
-            self.model.saveModule(os.path.join(self.checkpointPath, f"model{suffix or '.latest'}"), overWrite=True)
-            self._optim_method().save(os.path.join(self.checkpointPath, f"optimMethod{suffix or '.latest'}"),
-                                      overWrite=True)
+            self.model.saveModule(os.path.join(self.checkpointPath, f"model{suffix}"), overWrite=True)
+            for name, om in methods.items():
+                om.state["epoch"] = self.state["epoch"]
+                om.state["neval"] = self.state["neval"]
+                om.save(os.path.join(self.checkpointPath, f"optimMethod-{name}{suffix}"), overWrite=True)
         d = _dist()
         if d is not None:
             d.barrier()
+
+
+class _StragglerDrop:
+    """Straggler drop (reference DistriOptimizer.scala:171-178, 241-246, 343, 421-449).
+
+    Every rank is one "sub-model". After ``warmupIterationNum`` iterations, every ``computeThresholdbatchSize``
+    iterations the per-iteration times of all ranks are gathered and the threshold is set to the k-th largest
+    (k = dropPercentage · batch · ranks, less the drops already seen). A rank whose iteration exceeds the
+    threshold contributes a zero gradient with weight 0; the gradient is averaged over the ranks that finished
+    and the update is skipped when fewer than (1 - maxDropPercentage) of the ranks did."""
+
+    def __init__(self, opt, world):
+        self.opt = opt
+        self.world = world
+        self.times = []
+        self.threshold = float("inf")
+        self.dropped = 0
+        self.iteration = 0
+
+    def timed_out(self, elapsed):
+        return elapsed > self.threshold
+
+    def finished(self, elapsed):
+        if self.opt.device.type == "cuda" and self.threshold != float("inf"):
+            torch.cuda.synchronize()
+        self.times.append(elapsed)
+        return 0.0 if elapsed > self.threshold else 1.0
+
+    def record(self, updated, finished):
+        self.iteration += 1
+        if not finished:
+            self.dropped += 1
+        return updated
+
+    def maybe_update_threshold(self, step, iteration):
+        o = self.opt
+        if iteration <= o.warmupIterationNum or iteration % o.computeThresholdbatchSize != 0:
+            return
+        local = torch.tensor(self.times[-o.computeThresholdbatchSize:] or [0.0], dtype=torch.float64)
+        d = _dist()
+        if d is not None and self.world > 1:
+            n = torch.tensor([local.numel()], dtype=torch.int64, device=step.device)
+            d.all_reduce(n, op=d.ReduceOp.MAX)
+            buf = torch.zeros(int(n.item()), dtype=torch.float64, device=step.device)
+            buf[:local.numel()] = local.to(step.device)
+            allt = [torch.zeros_like(buf) for _ in range(self.world)]
+            d.all_gather(allt, buf)
+            times = torch.cat(allt).cpu()
+            dropped = torch.tensor([float(self.dropped)], device=step.device)
+            d.all_reduce(dropped)
+            dropped = int(dropped.item())
+        else:
+            times, dropped = local, self.dropped
+        k = int(o.dropPercentage * o.computeThresholdbatchSize * self.world)
+        if k > dropped:
+            vals = sorted(times.tolist(), reverse=True)
+            self.threshold = vals[min(k - dropped, len(vals)) - 1]
+        else:
+            self.threshold = self.threshold * 1.01
+        logger.info("threshold: %s", self.threshold)
+        self.times = []
+        self.dropped = 0
 
 
 class LocalOptimizer(Optimizer):
@@ -383,17 +503,22 @@ class DistriOptimizer(Optimizer):
 
 
 class ParallelOptimizer(DistriOptimizer):
-    """Data-parallel training with layer-wise bucketed gradient reduce-scatter overlapped with backward
-    (reference ParallelOptimizer.scala:42-791; mechanism in parallel/bucketed.py)."""
+    """Data-parallel training with layer-wise bucketed gradient reduce-scatter overlapped with backward and the
+    weight all-gather deferred into the next forward (reference ParallelOptimizer.scala:42-791; mechanism in
+    parallel/bucketed.py). Every leaf layer without its own OptimMethod inherits its parent's
+    (expandOptimMethods :642-670); layers are synchronised in priority order, default = execution order
+    (defaultPrioritize :675-683); gradient clipping reduces the whole gradient before any layer updates."""
 
     _overlap = True
+    _expand = True
 
     def __new__(cls, *args, **kw):
         return object.__new__(cls)
 
-    def _clip(self, step):
-        if self.constantClip is not None or self.l2NormClip is not None:
-            raise NotImplementedError("gradient clipping needs the whole gradient; use DistriOptimizer")
+    def setPriorities(self, priorities):
+        """{layer name: priority}; higher priorities are synchronised first."""
+        self._priorities = dict(priorities)
+        return self
 
 
 def create(model, training_set, criterion, end_trigger=None, batch_size=32, optim_method=None, **kw):

@@ -266,8 +266,16 @@ class SGD(OptimMethod):
     def getHyperParameter(self):
         return f"Current learning rate is {-self.learningRateSchedule.currentRate}. "
 
-    def optimize(self, feval, x):
+    def graph_prologue(self):
+        """HIP-graph replay support (optim/graphed.py): advance the schedule on the host and publish the rate
+        to the device scalar the captured kernel reads."""
         self.updateHyperParameter()
+        self._lr_dev.fill_(-self.learningRateSchedule.currentRate)
+
+    def optimize(self, feval, x):
+        graphed = getattr(self, "_lr_dev", None) is not None
+        if not graphed:
+            self.updateHyperParameter()
         if self.dampening == _MAXD:
             self.dampening = self.momentum
         wd, mom, damp, nest = self.weightDecay, self.momentum, self.dampening, self.nesterov
@@ -282,7 +290,8 @@ class SGD(OptimMethod):
                 self.state["dfdx"] = buf
             seg = getattr(self, "_wd_segments", None)
             native.get().sgd_step(x, dfdx, buf if mom != 0 else None, self._shadow16, float(-clr), float(wd),
-                                  float(mom), float(damp), bool(nest), bool(first), None,
+                                  float(mom), float(damp), bool(nest), bool(first),
+                                  self._lr_dev if graphed else None,
                                   seg[0] if seg else None, seg[1] if seg else None,
                                   int(getattr(self, "_seg_base", 0)))
             return x, [fx]

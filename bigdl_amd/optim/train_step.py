@@ -2,21 +2,32 @@
 
 This is the per-rank core that the reference spreads over DistriOptimizer's two Spark jobs per iteration
 (S/optim/DistriOptimizer.scala:204-396): getWeights → forward/backward → putGradients → aggregate shard →
-optimize shard → sendWeightPartition. On MI355X it is:
+parameter processors → optimize shard (per sub-module OptimMethod, :370-389) → sendWeightPartition.
+On MI355X it is:
 
   zero grads (one memset of the flat fp32 gradient buffer)
   forward / criterion / backward through the BigDL module protocol (HIP kernels, bf16 NHWC activations)
-  reduce-scatter of the flat gradients over RCCL (ZeRO-1 shard per rank)            [N > 1]
-  fused optimizer kernel on this rank's fp32 master shard, writing the bf16 compute shard
-  all-gather of the bf16 compute weights over RCCL                                   [N > 1]
+  reduce-scatter of the flat gradients over RCCL (ZeRO-1 shard per rank)                      [N > 1]
+  parameter processors on the shard (clipping, LARS layer norms: one small all-reduce each)
+  fused optimizer kernel per (owned range ∩ sub-module split), writing the bf16 compute shard
+  all-gather of the updated weights over RCCL (exact fp32 master on every rank, or bf16)      [N > 1]
+
+With ``overlap`` (ParallelOptimizer) the flat buffer is cut into buckets: each bucket's reduce-scatter is
+launched as soon as backward has produced it, and the all-gather of the updated weights is deferred to the
+start of the NEXT step where each bucket is waited for only right before the first layer that reads it
+(reference: update deferred to the next forward, S/nn/abstractnn/AbstractModule.scala:1184-1199; layers
+synchronised in priority order, S/optim/ParallelOptimizer.scala:675-683). ``flush()`` completes a pending
+all-gather (before a checkpoint, validation or the end of training).
 
 Layer regularizers (L1/L2) are folded into the optimizer kernel as per-segment decay (identical maths:
 the reference adds lambda*w inside accGradParameters before the gradient average, which equals adding it
-after the average). The whole step can be captured into a HIP graph once buffers are warm.
+after the average). Nothing in ``step`` synchronises with the host, so the whole step — including the RCCL
+collectives — can be captured into a HIP graph once buffers are warm (``optim/graphed.py``).
 """
+import copy
+
 import torch
 
-from .. import nn
 from ..optim.regularizer import L1L2Regularizer
 from ..parallel.allreduce_parameter import AllReduceParameter
 
@@ -59,15 +70,151 @@ def fold_regularizers(model, total, device):
     return (torch.tensor(mo, dtype=torch.int64, device=device), torch.tensor(mv, dtype=torch.float32, device=device))
 
 
+# --------------------------------------------------------------------------------------------- splits
+def find_module(model, name):
+    for m in model.flattened_layers():
+        if m.getName() == name:
+            return m
+    return None
+
+
+def _param_range(model, sub, fw):
+    """[lo, hi) of ``sub``'s parameters inside the flat weight buffer ``fw`` (they are contiguous)."""
+    p = sub.parameters()
+    if not p:
+        return None
+    base = fw.data_ptr()
+    es = fw.element_size()
+    lo = min((w.data_ptr() - base) // es for w in p[0])
+    hi = max((w.data_ptr() - base) // es + w.numel() for w in p[0])
+    return int(lo), int(hi)
+
+
+def parameter_splits(model, methods, fw, total, expand=False):
+    """Map each OptimMethod to the flat range of the sub-module it is registered for.
+
+    Reference DistriOptimizer.scala:816-853: one method for the whole model, or one per named sub-module whose
+    ranges must tile the whole parameter vector. With ``expand`` (ParallelOptimizer.expandOptimMethods,
+    ParallelOptimizer.scala:642-670) every leaf layer without an explicit method inherits its nearest
+    ancestor's (consecutive leaves inheriting the same method share one split — element-wise methods make that
+    identical to per-layer clones).
+    Returns a list of (name, lo, hi, method) sorted by lo.
+    """
+    if len(methods) == 1 and not expand:
+        name, m = next(iter(methods.items()))
+        if name != model.getName() and find_module(model, name) is None:
+            raise ValueError(f"{name} doesn't have corresponding sub-module in {model.getName()}")
+        sub = model if name == model.getName() else find_module(model, name)
+        rng = (0, total) if sub is model else _param_range(model, sub, fw)
+        if rng != (0, total):
+            raise ValueError(f"DistriOptimizer: All subModules should have an OptimMethod ({name} covers "
+                             f"{rng} of {total})")
+        return [(name, 0, total, m)]
+    if expand:
+        out = []
+
+        def walk(mod, inherited):
+            meth = methods.get(mod.getName(), inherited)
+            kids = mod.modules_list()
+            if not kids:
+                rng = _param_range(model, mod, fw)
+                if rng is not None:
+                    if meth is None:
+                        raise ValueError(f"{mod.getName()}'s parent optim method should not be null")
+                    out.append((mod.getName(), rng[0], rng[1], meth))
+                return
+            for k in kids:
+                walk(k, meth)
+
+        walk(model, methods.get(model.getName()))
+        out.sort(key=lambda t: t[1])
+        merged = []
+        for s in out:
+            if merged and merged[-1][3] is s[3] and merged[-1][2] == s[1]:
+                merged[-1] = (merged[-1][0], merged[-1][1], s[2], s[3])
+            else:
+                merged.append(s)
+        out = merged
+    else:
+        out = []
+        for name, m in methods.items():
+            sub = model if name == model.getName() else find_module(model, name)
+            if sub is None:
+                raise ValueError(f"Optimizer couldn't find {name} in {model.getName()}")
+            rng = _param_range(model, sub, fw)
+            if rng is None:
+                continue
+            out.append((name, rng[0], rng[1], m))
+        out.sort(key=lambda t: t[1])
+    pos = 0
+    for name, lo, hi, _ in out:
+        if lo != pos:
+            raise ValueError(f"DistriOptimizer: All subModules should have an OptimMethod (gap at {pos}, "
+                             f"next split {name} starts at {lo})")
+        pos = hi
+    if pos != total:
+        raise ValueError(f"DistriOptimizer: All subModules should have an OptimMethod (covered {pos} of {total})")
+    return out
+
+
+class UpdatePiece:
+    """One optimizer call per step: ``method`` on flat range [lo, hi) owned by this rank."""
+
+    __slots__ = ("name", "lo", "hi", "method", "split_lo", "split_hi", "primary")
+
+    def __init__(self, name, lo, hi, method, split_lo, split_hi, primary):
+        self.name, self.lo, self.hi, self.method = name, lo, hi, method
+        self.split_lo, self.split_hi, self.primary = split_lo, split_hi, primary
+
+    def __repr__(self):
+        return f"UpdatePiece({self.name}, [{self.lo},{self.hi}), {type(self.method).__name__})"
+
+
+def build_update_plan(owned, splits, w16, seg):
+    """Intersect this rank's owned ranges with the method splits. The first piece of every split uses the
+    registered method object itself; further pieces use clones (per-piece optimizer state, like the reference's
+    per-partition OptimMethod copies)."""
+    plan = []
+    seen, used = set(), set()
+    for (a, b) in owned:
+        for name, lo, hi, m in splits:
+            x, y = max(a, lo), min(b, hi)
+            if y <= x:
+                continue
+            primary = name not in seen
+            seen.add(name)
+            meth = m if id(m) not in used else _clone_method(m)
+            used.add(id(meth))
+            if seg is not None:
+                meth._wd_segments = seg
+                meth._seg_base = x
+            if w16 is not None:
+                meth.attach_shadow(w16[x:y])
+            plan.append(UpdatePiece(name, x, y, meth, lo, hi, primary))
+    return plan
+
+
+def _clone_method(m):
+    sh = m._shadow16
+    m._shadow16 = None
+    try:
+        c = copy.deepcopy(m)
+    finally:
+        m._shadow16 = sh
+    return c
+
+
+# --------------------------------------------------------------------------------------------- TrainStep
 class TrainStep:
     def __init__(self, model, criterion, optim_method, device=None, comm=None, compress=None, fuse=True,
-                 overlap=None, bucket_elems=8 << 20):
+                 overlap=None, bucket_elems=8 << 20, processors=None, expand_methods=False, priorities=None):
         from ..utils.engine import Engine
 
         self.device = torch.device(device) if device is not None else Engine.device()
         self.model = model
         self.criterion = criterion
-        self.optim = optim_method
+        self.methods = dict(optim_method) if isinstance(optim_method, dict) else {model.getName(): optim_method}
+        self.optim = next(iter(self.methods.values()))
         model.to(self.device)
         criterion.to(self.device)
         if fuse and self.device.type == "cuda":
@@ -76,8 +223,9 @@ class TrainStep:
             fuse_for_training(model)
         ws, _ = model.parameters() or ([], [])
         total = sum(w.numel() for w in ws)
+        self.total = total
         self.comm = comm if comm is not None else AllReduceParameter(total, compress=compress)
-        self.w, self.g = model.getParameters(pad_multiple=max(self.comm.padded // max(total, 1), 1) if False else 1)
+        self.w, self.g = model.getParameters()
         if self.w.numel() != self.comm.padded:
             # re-flatten into a padded buffer so every rank's shard has the same size
             pw = torch.zeros(self.comm.padded, device=self.device)
@@ -91,35 +239,46 @@ class TrainStep:
             self.w16 = torch.empty(self.comm.padded, dtype=torch.bfloat16, device=self.device)
             self.w16.copy_(self.w)
             model.attach_bf16_shadow(self.w16)
-        seg = fold_regularizers(model, total, self.device) if self.device.type == "cuda" else None
+        self.seg = fold_regularizers(model, total, self.device) if self.device.type == "cuda" else None
         self.w_shard = self.comm.shard_of(self.w)
         self.g_shard = self.comm.shard_of(self.g)
-        if seg is not None:
-            optim_method._wd_segments = seg
-            optim_method._seg_base = self.comm.start
-        if self.w16 is not None:
-            optim_method.attach_shadow(self.comm.shard_of(self.w16))
+        self.splits = parameter_splits(model, self.methods, self.w, total, expand=expand_methods)
+        self.processors = list(processors or [])
+        from ..optim.methods import LarsSGD
+
+        lars = [s for s in self.splits if isinstance(s[3], LarsSGD)]
+        if lars:
+            from ..parallel.processors import LarsProcessor
+
+            self.processors.append(LarsProcessor(lars[0][3].weightDecay))
         self.loss = None
-        self._graph = None
         # ParallelOptimizer-style bucketed reduce-scatter overlapped with backward (parallel/bucketed.py)
         from ..nn.containers import Sequential
 
         if overlap is None:
-            overlap = self.comm.world > 1 and isinstance(model, Sequential) and compress is None
+            overlap = self.comm.active and isinstance(model, Sequential)
         self.bucketed = None
-        if overlap and self.comm.world > 1:
+        if overlap and self.comm.active:
             from ..parallel.bucketed import BucketedGradSync
 
-            self.bucketed = BucketedGradSync(model, self.w, self.g, self.w16, optim_method, self.comm.world,
-                                             self.comm.rank, self.comm.group, bucket_elems, total)
+            self.bucketed = BucketedGradSync(self, bucket_elems, priorities)
+            owned = self.bucketed.owned_ranges()
+        else:
+            owned = [(self.comm.start, self.comm.end)]
+        self.plan = build_update_plan(owned, self.splits, self.w16, self.seg)
+        self._pending_gather = False
 
+    # ------------------------------------------------------------------ pieces
     def zero_grad(self):
         self.g.zero_()
 
     def forward_backward(self, x, y):
         m, c = self.model, self.criterion
         m.training()
-        out = m.forward(x)
+        if self.bucketed is not None:
+            out = self.bucketed.forward(x)
+        else:
+            out = m.forward(x)
         loss = c.forward(out, y)
         gout = c.backward(out, y)
         if self.bucketed is not None:
@@ -128,17 +287,77 @@ class TrainStep:
             m.backward(x, gout)
         return loss
 
-    def sync_and_update(self, loss):
+    def _lockstep(self):
+        """Keep every method clone's iteration/epoch counters equal to its primary's."""
+        prim = {p.name: p.method for p in self.plan if p.primary}
+        for p in self.plan:
+            if not p.primary:
+                lead = prim[p.name].state
+                for k in ("neval", "epoch", "Loss", "score"):
+                    if k in lead.keys():
+                        p.method.state[k] = lead[k]
+
+    def apply_processors(self):
+        for proc in self.processors:
+            proc(self)
+
+    def optimize_pieces(self, loss, pieces=None):
+        self._lockstep()
+        for p in (self.plan if pieces is None else pieces):
+            gs = self.g[p.lo:p.hi]
+            p.method.optimize(lambda _x, _g=gs: (loss, _g), self.w[p.lo:p.hi])
+
+    def sync_and_update(self, loss, finished=None):
+        """Reduce gradients, run processors and the sharded update, publish the weights.
+
+        ``finished`` (straggler drop, DistriOptimizer.scala:421-449): this rank's 0/1 contribution weight; the
+        gradient is averaged over the ranks that finished and the update is skipped when fewer than
+        ``min_finished`` did. Returns False when the update was skipped."""
+        if finished is not None:
+            return self._sync_and_update_weighted(loss, finished)
         if self.bucketed is not None:
             self.bucketed.update(loss)
-            return
+            self._pending_gather = True
+            return True
         self.comm.reduce_scatter_gradients(self.g, out=self.g_shard)
-        self.optim.optimize(lambda _: (loss, self.g_shard), self.w_shard)
-        if self.comm.world > 1:
-            if self.w16 is not None:
-                self.comm.all_gather_weights(self.w16)
-            else:
-                self.comm.all_gather_weights(self.w)
+        self.apply_processors()
+        self.optimize_pieces(loss)
+        self.comm.all_gather_weights(self.w, self.w16)
+        return True
+
+    min_finished = 0.0
+
+    def _sync_and_update_weighted(self, loss, finished):
+        self.flush()
+        cnt = torch.tensor([float(finished)], device=self.device)
+        self.comm.all_reduce_scalar(cnt)
+        n = float(cnt.item())
+        if not finished:
+            self.g.zero_()
+        self.comm.reduce_scatter_gradients(self.g, out=self.g_shard, average=False)
+        if n <= 0 or n < self.min_finished:
+            return False
+        self.g_shard.mul_(1.0 / n)
+        self.apply_processors()
+        self.optimize_pieces(loss)
+        self.comm.all_gather_weights(self.w, self.w16)
+        return True
+
+    def flush(self):
+        """Complete a deferred (bucketed) weight all-gather: afterwards every rank holds the current weights."""
+        if self._pending_gather:
+            self.bucketed.gather_all()
+            self._pending_gather = False
+
+    def gather_model(self):
+        """Reference DistriOptimizer.getModel: exact fp32 weights everywhere and rank 0's extra state (BN
+        running statistics) on every rank. Collective: every rank must call it."""
+        self.flush()
+        self.comm.gather_master(self.w)
+        if self.comm.active:
+            for t in self.model.getExtraParameter() or []:
+                self.comm.broadcast(t, 0)
+        return self.model
 
     def step(self, x, y):
         arena = None
@@ -155,6 +374,62 @@ class TrainStep:
                 arena.end()
         self.loss = loss
         return loss
+
+    # ------------------------------------------------------------------ optimizer state (checkpoints)
+    def gather_optim_state(self):
+        """Full-size optimizer state per split, identical on every rank (collective).
+
+        Every per-element state tensor of a piece (same length as the piece) is placed at its offset inside a
+        split-sized zero tensor, and the disjoint pieces of all ranks are summed with one all-reduce. Scalars
+        and schedules come from the primary piece. Returns {split name: OptimMethod with full-size state}."""
+        out = {}
+        for name, lo, hi, meth in self.splits:
+            full = _clone_method(meth)
+            full._shadow16 = None
+            keys = {}
+            for p in self.plan:
+                if p.name != name:
+                    continue
+                for k, v in p.method.state.items():
+                    if torch.is_tensor(v) and v.dim() == 1 and v.numel() == p.hi - p.lo:
+                        if k not in keys:
+                            keys[k] = torch.zeros(hi - lo, dtype=v.dtype, device=v.device)
+                        keys[k][p.lo - lo:p.hi - lo].copy_(v)
+            # ranks may own no piece of a split: agree on the key set first
+            names = sorted(_all_keys(self.comm, name, list(keys)))
+            for k in names:
+                t = keys.get(k)
+                if t is None:
+                    t = torch.zeros(hi - lo, dtype=torch.float32, device=self.device)
+                self.comm.all_reduce_scalar(t)
+                full.state[k] = t
+            out[name] = full
+        return out
+
+    def load_optim_state(self, methods):
+        """Inverse of ``gather_optim_state``: slice full-size state into this rank's pieces."""
+        for p in self.plan:
+            src = methods.get(p.name)
+            if src is None:
+                continue
+            for k, v in src.state.items():
+                if torch.is_tensor(v) and v.dim() == 1 and v.numel() == p.split_hi - p.split_lo:
+                    p.method.state[k] = v[p.lo - p.split_lo:p.hi - p.split_lo].to(self.device).clone()
+                elif not torch.is_tensor(v):
+                    p.method.state[k] = v
+
+
+def _all_keys(comm, name, keys):
+    if comm.world == 1:
+        return set(keys)
+    import torch.distributed as dist
+
+    got = [None] * comm.world
+    dist.all_gather_object(got, keys, group=comm.group)
+    s = set()
+    for g in got:
+        s.update(g)
+    return s
 
 
 def _reflatten(model, fw, fg):

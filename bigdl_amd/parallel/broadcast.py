@@ -23,6 +23,17 @@ def _tensors(model):
     return out
 
 
+def _refresh_bf16(model):
+    """Rewrite the bf16 compute copies (GPU engine) from the broadcast fp32 weights, so kernels that read the
+    shadow see the new values too."""
+    for m in model.flattened_layers():
+        if getattr(m, "_w16_managed", False):
+            for name, t16 in m._w16.items():
+                w = getattr(m, name, None)
+                if torch.is_tensor(w):
+                    t16.copy_(w)
+
+
 class ModelBroadcast:
     def __init__(self, applyProtoBuffer=False, group=None, src=0):
         self.group, self.src = group, src
@@ -44,6 +55,7 @@ class ModelBroadcast:
                 n = t.numel()
                 t.data.copy_(flat[off:off + n].view_as(t))
                 off += n
+        _refresh_bf16(model)
         return self
 
     def value(self, initGradient=False, shareWeight=True):

@@ -1,0 +1,141 @@
+"""Multi-rank training on the GPU engine (bf16 shadow weights, fused HIP optimizer), on ONE MI355X:
+
+* 2 ranks over gloo sharing cuda:0 (RCCL refuses two ranks on one device) — the ZeRO-1 bf16-shadow path:
+  after several steps the bf16 compute weights are bit-equal on both ranks, the fp32 masters agree to 1e-6,
+  and both match one rank at twice the batch; the checkpoint written by rank 0 reloads to those weights.
+* 1 rank over RCCL with BIGDL_FORCE_COLLECTIVES=1 — the in-place reduce-scatter / all-gather and the bucketed
+  overlap path captured in a HIP graph must reproduce the eager steps.
+"""
+import os
+
+import pytest
+import torch
+
+from bigdl_amd.utils.testing import run_distributed
+
+pytestmark = pytest.mark.gpu
+
+
+def _cnn(bn):
+    from bigdl_amd import nn
+    from bigdl_amd.utils.random_generator import RNG
+
+    RNG.setSeed(11)
+    m = nn.Sequential().setName("cnn")
+    m.add(nn.SpatialConvolution(8, 32, 3, 3, 1, 1, 1, 1))
+    if bn:
+        m.add(nn.SpatialBatchNormalization(32))
+    m.add(nn.ReLU())
+    m.add(nn.SpatialConvolution(32, 64, 3, 3, 2, 2, 1, 1))
+    if bn:
+        m.add(nn.SpatialBatchNormalization(64))
+    m.add(nn.ReLU())
+    m.add(nn.SpatialAveragePooling(8, 8, 1, 1)).add(nn.View(64)).add(nn.Linear(64, 10))
+    return m
+
+
+def _batch(n):
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(n, 8, 16, 16, generator=g)
+    y = torch.randint(1, 11, (n,), generator=g).float()
+    return x, y
+
+
+def _gpu_train(rank, world, overlap, compress, bn, iters):
+    from bigdl_amd import nn
+    from bigdl_amd import optim as O
+    from bigdl_amd.optim.train_step import TrainStep
+
+    dev = torch.device("cuda", 0)
+    model = _cnn(bn)
+    step = TrainStep(model, nn.CrossEntropyCriterion(), O.SGD(0.05, momentum=0.9, dampening=0.0), device=dev,
+                     compress=compress, overlap=overlap, bucket_elems=4096)
+    X, Y = _batch(32)
+    n = 32 // world
+    xs, ys = X[rank * n:(rank + 1) * n].to(dev), Y[rank * n:(rank + 1) * n].to(dev)
+    for _ in range(iters):
+        step.step(xs, ys)
+    step.gather_model()
+    torch.cuda.synchronize()
+    return step.w[:step.total].clone(), step.w16[:step.total].clone(), step.bucketed is not None
+
+
+@pytest.mark.parametrize("overlap,compress", [(False, None), (True, None), (True, "bf16")])
+def test_two_gloo_ranks_on_one_gpu_match(overlap, compress):
+    two = run_distributed(_gpu_train, 2, (overlap, compress, False, 3), engine="gpu")
+    (w0, h0, b0), (w1, h1, _) = two
+    assert b0 == overlap
+    assert torch.equal(h0, h1), "bf16 compute weights differ between ranks"
+    assert torch.allclose(w0, w1, atol=1e-6, rtol=0), (w0 - w1).abs().max()
+    one = run_distributed(_gpu_train, 1, (False, None, False, 3), engine="gpu")
+    rel = float((w0 - one[0][0]).norm() / one[0][0].norm())
+    assert rel < (2e-2 if compress else 5e-3), rel
+
+
+def test_two_gloo_ranks_with_bn_stay_identical():
+    two = run_distributed(_gpu_train, 2, (True, None, True, 3), engine="gpu")
+    assert torch.equal(two[0][1], two[1][1])
+    assert torch.allclose(two[0][0], two[1][0], atol=1e-6, rtol=0)
+
+
+def _gpu_optimizer(rank, world, path):
+    from bigdl_amd import nn
+    from bigdl_amd import optim as O
+    from bigdl_amd.dataset.core import DataSet, Sample
+
+    model = _cnn(True)
+    X, Y = _batch(64)
+    ds = DataSet.rdd([Sample(X[i], Y[i]) for i in range(64)], shuffle=False)
+    opt = O.Optimizer(model, ds, nn.CrossEntropyCriterion(), batchSize=16,
+                      optimMethod=O.SGD(0.05, momentum=0.9, dampening=0.0), endTrigger=O.Trigger.maxIteration(4))
+    opt.setCheckpoint(path, O.Trigger.severalIteration(4))
+    m = opt.optimize()
+    return m.getParameters()[0][:opt._step.total].clone()
+
+
+def test_gpu_distri_optimizer_checkpoint_reloads(tmp_path):
+    from bigdl_amd.utils.serializer import load_module
+
+    res = run_distributed(_gpu_optimizer, 2, (str(tmp_path),), engine="gpu")
+    assert torch.equal(res[0], res[1])
+    m = load_module(os.path.join(tmp_path, "model.4"))
+    w = m.getParameters()[0][:res[0].numel()].cpu()
+    assert torch.equal(w, res[0])
+
+
+def _rccl_graph(rank, world, overlap, compress):
+    from bigdl_amd import nn
+    from bigdl_amd import optim as O
+    from bigdl_amd.optim.graphed import GraphedTrainStep
+    from bigdl_amd.optim.train_step import TrainStep
+
+    dev = torch.device("cuda", 0)
+    X, Y = _batch(16)
+    X, Y = X.to(dev), Y.to(dev)
+    outs = []
+    for graphed in (False, True):
+        model = _cnn(True)
+        step = TrainStep(model, nn.CrossEntropyCriterion(), O.SGD(0.05, momentum=0.9, dampening=0.0,
+                                                                  learningRateDecay=0.01),
+                         device=dev, compress=compress, overlap=overlap, bucket_elems=4096)
+        assert step.comm.active
+        if graphed:
+            g = GraphedTrainStep(step, X, Y, warmup=2)      # 2 warm-up + 1 side-stream step run eagerly
+            for _ in range(3):
+                g.replay()
+        else:
+            for _ in range(6):
+                step.step(X, Y)
+        step.gather_model()
+        torch.cuda.synchronize()
+        outs.append((step.w[:step.total].clone(), step.w16[:step.total].clone(), float(step.loss)))
+    return outs
+
+
+@pytest.mark.parametrize("overlap,compress", [(False, None), (True, None), (True, "bf16")])
+def test_rccl_step_captured_in_hip_graph_matches_eager(overlap, compress):
+    res = run_distributed(_rccl_graph, 1, (overlap, compress), engine="gpu", backend="nccl",
+                          env={"BIGDL_FORCE_COLLECTIVES": "1"})[0]
+    (we, he, le), (wg, hg, lg) = res
+    assert torch.allclose(we, wg, atol=1e-5, rtol=1e-4), (we - wg).abs().max()
+    assert abs(le - lg) < 1e-3 * max(1.0, abs(le))

@@ -89,6 +89,7 @@ def _bucketed_job(rank, world, data, iters, bucket):
     n = X.shape[0] // world
     for i in range(iters):
         step.step(X[rank * n:(rank + 1) * n], Y[rank * n:(rank + 1) * n])
+    step.gather_model()      # the weight all-gather of the last update is deferred to the next forward
     w, _ = model.getParameters()
     return w[:model._flat_total].clone()
 
