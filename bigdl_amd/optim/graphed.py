@@ -1,6 +1,10 @@
-"""A training step captured once into a HIP graph and replayed (runtime counterpart of the reference's
-per-iteration task launch, S/optim/DistriOptimizer.scala:204-396 — here the whole iteration, including the
-RCCL reduce-scatter / all-gather, is ONE ``hipGraphLaunch``).
+"""A training step captured once into HIP graphs and replayed (runtime counterpart of the reference's
+per-iteration task launch, S/optim/DistriOptimizer.scala:204-396).
+
+On one rank the whole iteration is ONE ``hipGraphLaunch``. With collectives the step is recorded as a chain of
+single-stream graphs cut at every RCCL launch / wait (parallel/graph_segments.py): the collectives are re-issued
+between the graph launches, so the bucketed reduce-scatter still overlaps backward and the deferred weight
+all-gather still overlaps the next forward, while no captured graph ever forks onto RCCL's stream.
 
 Capture rules this wrapper enforces:
   * warm-up steps run eagerly first (kernel plans, workspaces, momentum buffers and RCCL communicators are
@@ -12,8 +16,11 @@ Capture rules this wrapper enforces:
   * nothing in the step synchronises with the host (TrainStep guarantees it), so capture succeeds with the
     collectives inside.
 """
+import warnings
+
 import torch
 
+from ..parallel.graph_segments import SegmentedGraph
 from .sgd import SGD
 
 
@@ -43,9 +50,10 @@ class GraphedTrainStep:
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
         self._prologue()
-        self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
-            self.loss = step.step(self.x, self.y)
+        self.graph = SegmentedGraph()
+        with warnings.catch_warnings():
+            warnings.filterwarnings("ignore", message=".*CUDA Graph is empty.*")
+            self.loss = self.graph.record(lambda: step.step(self.x, self.y))
         self._fresh = True                  # capture did not execute: the first replay uses this prologue
 
     def _prologue(self):

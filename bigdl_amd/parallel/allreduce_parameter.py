@@ -25,6 +25,8 @@ The flat buffers are padded so every rank's shard has the same size (a multiple 
 import torch
 import torch.distributed as dist
 
+from .graph_segments import issue as _issue
+
 
 def dist_ready():
     return dist.is_available() and dist.is_initialized()
@@ -78,7 +80,10 @@ class AllReduceParameter:
     # ------------------------------------------------------------------------- collectives on a range
     def _rs(self, out_shard, full, op, async_op=False):
         if self._inplace:
-            return dist.reduce_scatter_tensor(out_shard, full, op=op, group=self.group, async_op=async_op)
+            w = _issue(lambda: dist.reduce_scatter_tensor(out_shard, full, op=op, group=self.group, async_op=True))
+            if not async_op:
+                _wait(w)
+            return w
         tmp = torch.empty_like(out_shard)
         w = dist.reduce_scatter_tensor(tmp, full, op=op, group=self.group)
         out_shard.copy_(tmp)
@@ -86,7 +91,10 @@ class AllReduceParameter:
 
     def _ag(self, full, my_shard, async_op=False):
         if self._inplace:
-            return dist.all_gather_into_tensor(full, my_shard, group=self.group, async_op=async_op)
+            w = _issue(lambda: dist.all_gather_into_tensor(full, my_shard, group=self.group, async_op=True))
+            if not async_op:
+                _wait(w)
+            return w
         w = dist.all_gather_into_tensor(full, my_shard.clone(), group=self.group)
         return _Done() if async_op else w
 
@@ -167,12 +175,13 @@ class AllReduceParameter:
     # -- C7: global scalar reductions (gradient norm clipping, loss averaging, LARS norms, finished counts)
     def all_reduce_scalar(self, t, op="sum"):
         if self.active:
-            dist.all_reduce(t, op=dist.ReduceOp.SUM if op == "sum" else dist.ReduceOp.MAX, group=self.group)
+            rop = dist.ReduceOp.SUM if op == "sum" else dist.ReduceOp.MAX
+            _wait(_issue(lambda: dist.all_reduce(t, op=rop, group=self.group, async_op=True)))
         return t
 
     def broadcast(self, t, src=0):
         if self.active:
-            dist.broadcast(t, src, group=self.group)
+            _wait(_issue(lambda: dist.broadcast(t, src, group=self.group, async_op=True)))
         return t
 
 

@@ -1,0 +1,142 @@
+"""Segmented HIP-graph capture: a training step recorded as a chain of single-stream HIP graphs cut at every
+collective launch / wait, with the RCCL calls themselves re-issued eagerly between the graph launches.
+
+Why not one graph with the collectives inside: a capture that forks onto RCCL's stream (async reduce-scatter in
+flight while the next layers' backward kernels are captured on the compute stream) replays with corrupted
+results on this ROCm 7 / PyTorch 2.10 stack — measured by ``tools/diag_overlap*.py``: an in-flight side-stream
+branch, even a trivial ``mul_(1.0)`` on a disjoint range, made the kernels captured after the fork produce wrong
+gradients (and NaNs), while eager execution with the same overlap and a capture whose collectives are joined
+immediately were bit-exact. Cutting the step at the collectives keeps every captured graph a single stream;
+overlap still happens because a collective issued between two graph launches runs on RCCL's stream while the
+next graph runs on the compute stream.
+
+Replay cost is one ``hipGraphLaunch`` per segment plus the eager collective calls (a few µs each, all async): for
+ResNet-50 with 8M-element buckets that is ~15 launches per step instead of ~1,400 kernel launches.
+
+Usage (optim/graphed.py): ``rec = SegmentedGraph(); rec.record(lambda: step.step(x, y))``; code on the step's
+path announces collective boundaries with ``boundary(fn)`` / ``issue(fn)`` (no-ops outside a recording).
+"""
+import torch
+
+_ACTIVE = None
+
+
+def active():
+    """The recorder currently capturing, or None."""
+    return _ACTIVE
+
+
+def boundary(fn):
+    """Run ``fn`` (a host-issued collective launch or stream wait). Inside a recording the current graph segment
+    is closed first, ``fn`` runs eagerly and is kept for replay, and a new segment is opened."""
+    rec = _ACTIVE
+    if rec is None:
+        return fn()
+    return rec.boundary(fn)
+
+
+class _Cell:
+    """Handle of a collective issued through ``issue`` during a recording: replays re-issue the collective and
+    store the fresh work object here, so a recorded ``wait`` always waits for the current step's collective."""
+
+    def __init__(self):
+        self.h = None
+
+    def wait(self):
+        boundary(lambda: _raw_wait(self.h))
+        return True
+
+    def is_completed(self):
+        return False
+
+
+def _raw_wait(h):
+    if h is not None:
+        h.wait()
+
+
+def issue(fn):
+    """Launch a collective: ``fn()`` returns a work handle (or None). Inside a recording the launch becomes a
+    replayed boundary and a ``_Cell`` proxy is returned."""
+    rec = _ACTIVE
+    if rec is None:
+        return fn()
+    cell = _Cell()
+
+    def run():
+        cell.h = fn()
+
+    rec.boundary(run)
+    return cell
+
+
+class SegmentedGraph:
+    def __init__(self):
+        self.items = []          # ("g", CUDAGraph) | ("f", callable)
+        self.pool = None
+        self._g = None
+        self.n_graphs = 0
+        self.n_calls = 0
+
+    # ------------------------------------------------------------------ recording
+    def _begin(self):
+        self._g = torch.cuda.CUDAGraph()
+        self._g.capture_begin(pool=self.pool)
+
+    def _end(self):
+        g = self._g
+        self._g = None
+        g.capture_end()
+        self.items.append(("g", g))
+        self.n_graphs += 1
+
+    def boundary(self, fn):
+        self._end()
+        try:
+            out = fn()
+        finally:
+            self.items.append(("f", fn))
+            self.n_calls += 1
+            self._begin()
+        return out
+
+    def record(self, fn):
+        """Record ``fn()`` (one training step) on a private capture stream; returns its result (tensors in the
+        graphs' pool, refreshed by every replay)."""
+        global _ACTIVE
+        if _ACTIVE is not None:
+            raise RuntimeError("nested segmented capture")
+        torch.cuda.synchronize()
+        self.pool = torch.cuda.graph_pool_handle()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            _ACTIVE = self
+            try:
+                self._begin()
+                out = fn()
+                self._end()
+            except BaseException:
+                if self._g is not None:
+                    try:
+                        self._g.capture_end()
+                    except Exception:  # noqa: BLE001 - the original error is the one to report
+                        pass
+                    self._g = None
+                raise
+            finally:
+                _ACTIVE = None
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        return out
+
+    # ------------------------------------------------------------------ replay
+    def replay(self):
+        for kind, x in self.items:
+            if kind == "g":
+                x.replay()
+            else:
+                x()
+
+    def __len__(self):
+        return len(self.items)
