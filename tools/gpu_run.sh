@@ -8,6 +8,7 @@
 #   prof[=ARGS]       rocprofv3 --kernel-trace --stats of bench.py (eager) -> gpurun_out/prof/
 #   pmc=COUNTERS      rocprofv3 --pmc COUNTERS of bench.py (one pass)      -> gpurun_out/pmc_N/
 #   py=SCRIPT[:ARGS]  python SCRIPT ARGS                           -> gpurun_out/<script>.log
+#   dist[=ARGS]       2 ranks of bench.py on the one GPU over gloo (multi-rank rehearsal) -> gpurun_out/dist.log
 set -o pipefail
 export PYTHONPATH=$PWD
 ROOT=$PWD
@@ -45,6 +46,11 @@ for s in "$@"; do
       log=gpurun_out/$(basename "$scr" .py).log
       timeout -k 10 600 python -u $scr $a > "$log" 2>&1; rc=$?
       tail -20 "$log"; [ $rc -eq 0 ] || exit $rc ;;
+    dist)
+      a=${val:-"--steps 3 --warmup 2 --batch 64"}
+      BIGDL_DIST_BACKEND=gloo timeout -k 10 500 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+        --master-addr 127.0.0.1 --master-port 29611 bench.py --gpus 2 $a > gpurun_out/dist.log 2>&1; rc=$?
+      tail -3 gpurun_out/dist.log; [ $rc -eq 0 ] || exit $rc ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
