@@ -10,3 +10,12 @@ from .sgd import *  # noqa: F401,F403
 from .train_step import TrainStep  # noqa: F401
 from .trigger import Trigger  # noqa: F401
 from .validation import *  # noqa: F401,F403
+from .detection_map import (MAPMultiIOUValidationResult, MAPValidationResult,  # noqa: F401,E402
+                            MeanAveragePrecisionObjectDetection, cocoBBox, cocoSegmentation, pascalVOC)
+from .validation import MeanAveragePrecision as _MAP  # noqa: E402
+
+# reference `object MeanAveragePrecision` factories (S/optim/ValidationMethod.scala:761-840)
+_MAP.pascalVOC = staticmethod(pascalVOC)
+_MAP.cocoBBox = staticmethod(cocoBBox)
+_MAP.cocoSegmentation = staticmethod(cocoSegmentation)
+_MAP.classification = staticmethod(lambda nClasses, topK=-1: _MAP(topK, nClasses))

@@ -1,6 +1,7 @@
 """Batch inference and the thread-safe prediction service.
 
-Reference: S/optim/Predictor.scala:35-257 (distributed predict / predictClass / predictImage),
+Reference: S/optim/Predictor.scala:35-257 (distributed predict / predictClass / predictImage: batches are
+spread over the ranks and gathered back in order),
 LocalPredictor.scala:33-197, PredictionService.scala:56-354 (pool of model clones, ``predict(Activity)``
 :79 and ``predict(bytes)`` :128 with (de)serialized activities).
 
@@ -18,7 +19,58 @@ from ..dataset.core import AbstractDataSet, DataSet, MiniBatch, Sample, SampleTo
 from ..utils.table import Table
 
 
+def _dist_world():
+    import torch.distributed as dist
+
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        return dist, dist.get_world_size(), dist.get_rank()
+    return None, 1, 0
+
+
+def _gather_ordered(dist, world, rank, mine, dev):
+    """All-gather every rank's ``[(batch index, output)]`` and return the outputs of ALL batches in batch order
+    (the reference's ordered ``mapPartitions(...).collect()``). Tensor outputs go through one padded tensor
+    all-gather (RCCL on the GPU engine); Tables / other activities through ``all_gather_object``."""
+    tensors = all(isinstance(o, torch.Tensor) for _, o in mine)
+    flag = torch.tensor([1.0 if tensors else 0.0], device=dev)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    if flag.item() < 1.0:
+        got = [None] * world
+        dist.all_gather_object(got, [(i, o.to("cpu") if hasattr(o, "to") else o) for i, o in mine])
+        allb = sorted((b for g in got for b in g), key=lambda t: t[0])
+        return [o for _, o in allb]
+    # shapes / batch indices of every rank, then one all-gather of the concatenated (padded) payloads
+    meta = [(i, tuple(o.shape), str(o.dtype).split(".")[-1]) for i, o in mine]
+    metas = [None] * world
+    dist.all_gather_object(metas, meta)
+    dtype = next((getattr(torch, m[0][2]) for m in metas if m), torch.float32)
+    flat = torch.cat([o.reshape(-1).to(dtype) for _, o in mine]) if mine else torch.empty(0, dtype=dtype)
+    sizes = [sum(int(torch.Size(sh).numel()) for _, sh, _ in m) for m in metas]
+    cap = max(sizes) if sizes else 0
+    buf = torch.zeros(cap, dtype=dtype, device=dev)
+    buf[:flat.numel()].copy_(flat.to(dev))
+    out = torch.empty(world * cap, dtype=dtype, device=dev)
+    dist.all_gather_into_tensor(out, buf)
+    out = out.cpu()
+    allb = []
+    for r, m in enumerate(metas):
+        off = r * cap
+        for i, sh, _ in m:
+            n = int(torch.Size(sh).numel())
+            allb.append((i, out[off:off + n].reshape(sh)))
+            off += n
+    allb.sort(key=lambda t: t[0])
+    return [o for _, o in allb]
+
+
 class Predictor:
+    """Batch inference (reference S/optim/Predictor.scala:152-180 + LocalPredictor.scala).
+
+    Distributed (``torch.distributed`` initialised with more than one rank): the model is already replicated
+    (every rank holds the broadcast weights), batch ``b`` of the input is predicted by rank ``b % world`` — the
+    analogue of one Spark partition per executor — and the per-rank outputs are gathered back in input order on
+    every rank. ``gather=False`` returns only this rank's outputs (``(batch index, output)`` pairs)."""
+
     def __init__(self, model, batchSize=-1, batchPerPartition=4):
         self.model = model
         self.batchSize = batchSize if batchSize and batchSize > 0 else 32 * batchPerPartition
@@ -44,18 +96,39 @@ class Predictor:
         if buf:
             yield samples_to_minibatch(buf).getInput()
 
-    def predict(self, data):
+    def predict(self, data, gather=True):
+        dist, world, rank = _dist_world()
+        # a rank-sharded dataset (DataSet.rdd: rank r owns global elements r, r+world, ...) is already split:
+        # predict the whole local shard and re-interleave the rows after the gather
+        sharded = dist is not None and isinstance(data, AbstractDataSet) and data.isDistributed()
         was = self.model.isTraining()
         self.model.evaluate()
         dev = self.model.device
-        outs = []
+        mine = []
         with torch.no_grad():
-            for x in self._batches(data):
-                x = x.to(dev) if isinstance(x, torch.Tensor) else x.to(dev)
+            for b, x in enumerate(self._batches(data)):
+                if not sharded and b % world != rank:
+                    continue
+                x = x.to(dev)
                 y = self.model.forward(x)
-                outs.append(y.float().cpu() if isinstance(y, torch.Tensor) else y)
+                mine.append((b, y.float() if isinstance(y, torch.Tensor) else y))
         if was:
             self.model.training()
+        if not gather:
+            return [(b, y.cpu() if isinstance(y, torch.Tensor) else y) for b, y in mine]
+        if dist is None:
+            outs = [y.cpu() if isinstance(y, torch.Tensor) else y for _, y in mine]
+        else:
+            cdev = dev if dist.get_backend() == "nccl" else torch.device("cpu")
+            if sharded:
+                local = torch.cat([y for _, y in mine], 0) if mine else torch.empty(0)
+                parts = _gather_ordered(dist, world, rank, [(rank, local)], cdev)
+                n = sum(p.shape[0] for p in parts)
+                out = torch.empty((n,) + tuple(parts[0].shape[1:]), dtype=parts[0].dtype)
+                for r, p in enumerate(parts):
+                    out[r::world][:p.shape[0]] = p
+                return out
+            outs = _gather_ordered(dist, world, rank, mine, cdev)
         if outs and isinstance(outs[0], torch.Tensor):
             return torch.cat(outs, 0)
         return outs

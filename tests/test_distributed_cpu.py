@@ -195,3 +195,31 @@ def test_distri_optimizer_straggler_drop_runs(tmp_path):
     res = run_distributed(_optimizer_job, 2, (str(tmp_path), True))
     assert torch.equal(res[0], res[1])
     assert torch.isfinite(res[0]).all()
+
+
+def _predict(rank, world):
+    from bigdl_amd import nn
+    from bigdl_amd.dataset.core import DataSet, Sample
+    from bigdl_amd.optim.predictor import Predictor
+
+    model = _model()
+    x, _ = _data(37)
+    p = Predictor(model, batchSize=5)
+    full = p.predict(x)
+    cls = p.predictClass(x)
+    ds = DataSet.rdd([Sample(x[i], torch.tensor([1.0])) for i in range(37)], shuffle=False)
+    sh = p.predict(ds)
+    mine = p.predict(x, gather=False)
+    return full, cls, sh, [b for b, _ in mine]
+
+
+def test_distributed_predictor_shards_batches_and_gathers_in_order():
+    """Reference Predictor.predict (S/optim/Predictor.scala:152-180): partitions predicted where they live,
+    results collected in input order."""
+    ref = run_distributed(_predict, 1)[0]
+    two = run_distributed(_predict, 2)
+    for r in two:
+        assert torch.allclose(r[0], ref[0], atol=1e-6)
+        assert torch.equal(r[1], ref[1])
+        assert torch.allclose(r[2], ref[0], atol=1e-6)
+    assert two[0][3] == [0, 2, 4, 6] and two[1][3] == [1, 3, 5, 7]
