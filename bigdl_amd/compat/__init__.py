@@ -1,0 +1,35 @@
+"""Reference-compatible Python API (``bigdl.*`` module layout of P/ = pyspark/bigdl) over the bigdl_amd engine.
+
+    from bigdl_amd.compat.nn.layer import *          # Sequential, Linear, SpatialConvolution, Model, ...
+    from bigdl_amd.compat.nn.criterion import *      # ClassNLLCriterion, ...
+    from bigdl_amd.compat.optim.optimizer import *   # Optimizer, SGD, MaxEpoch, Top1Accuracy, ...
+    from bigdl_amd.compat.util.common import *       # Sample, init_engine, SparkContext, ...
+
+or, for unmodified reference scripts, ``bigdl_amd.compat.install()`` registers these modules under the
+``bigdl.*`` names so ``from bigdl.nn.layer import *`` resolves to them.
+"""
+import importlib
+import sys
+
+_MODULES = {
+    "bigdl": "bigdl_amd.compat",
+    "bigdl.util": "bigdl_amd.compat.util",
+    "bigdl.util.common": "bigdl_amd.compat.util.common",
+    "bigdl.nn": "bigdl_amd.compat.nn",
+    "bigdl.nn.layer": "bigdl_amd.compat.nn.layer",
+    "bigdl.nn.criterion": "bigdl_amd.compat.nn.criterion",
+    "bigdl.optim": "bigdl_amd.compat.optim",
+    "bigdl.optim.optimizer": "bigdl_amd.compat.optim.optimizer",
+    "bigdl.dataset": "bigdl_amd.compat.dataset",
+    "bigdl.dataset.transformer": "bigdl_amd.compat.dataset.transformer",
+    "bigdl.dataset.mnist": "bigdl_amd.compat.dataset.mnist",
+}
+
+
+def install():
+    """Alias the facade as the reference's ``bigdl`` package (only if no real ``bigdl`` is imported)."""
+    for name, target in _MODULES.items():
+        if name in sys.modules and not sys.modules[name].__name__.startswith("bigdl_amd"):
+            raise RuntimeError(f"a different {name!r} is already imported")
+        sys.modules[name] = importlib.import_module(target)
+    return sys.modules["bigdl"]

@@ -1,0 +1,148 @@
+"""Reference-style Python scripts run against the bigdl_amd facade (reference P/models/lenet/lenet5.py +
+utils.py, P/optim/optimizer.py, P/nn/layer.py, P/util/common.py). The LeNet script body below is the
+reference's build_model / preprocess / Optimizer / set_validation / set_checkpoint / optimize / Model.load /
+evaluate flow with ``from bigdl.* import *`` imports, on synthetic MNIST-shaped data (no downloads)."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+
+@pytest.fixture
+def bigdl():
+    import bigdl_amd.compat as compat
+
+    saved = {k: sys.modules.get(k) for k in compat._MODULES}
+    compat.install()
+    yield
+    for k, v in saved.items():
+        if v is None:
+            sys.modules.pop(k, None)
+        else:
+            sys.modules[k] = v
+
+
+LENET = '''
+from bigdl.dataset import mnist
+from bigdl.dataset.transformer import *
+from bigdl.nn.layer import *
+from bigdl.nn.criterion import *
+from bigdl.optim.optimizer import *
+from bigdl.util.common import *
+
+
+def build_model(class_num):
+    model = Sequential()
+    model.add(Reshape([1, 28, 28]))
+    model.add(SpatialConvolution(1, 6, 5, 5))
+    model.add(Tanh())
+    model.add(SpatialMaxPooling(2, 2, 2, 2))
+    model.add(SpatialConvolution(6, 12, 5, 5))
+    model.add(Tanh())
+    model.add(SpatialMaxPooling(2, 2, 2, 2))
+    model.add(Reshape([12 * 4 * 4]))
+    model.add(Linear(12 * 4 * 4, 100))
+    model.add(Tanh())
+    model.add(Linear(100, class_num))
+    model.add(LogSoftMax())
+    return model
+
+
+def get_mnist(sc, images, labels):
+    images = sc.parallelize(images)
+    labels = sc.parallelize(labels + 1)  # Target start from 1 in BigDL
+    return images.zip(labels)
+
+
+def run(images, labels, ckpt):
+    sc = SparkContext(appName="lenet5", conf=create_spark_conf())
+    redire_spark_logs(log_path=ckpt + "/bigdl.log")
+    show_bigdl_info_logs()
+    init_engine()
+    train_data = get_mnist(sc, images, labels)\\
+        .map(lambda rec_tuple: (normalizer(rec_tuple[0], mnist.TRAIN_MEAN, mnist.TRAIN_STD), rec_tuple[1]))\\
+        .map(lambda t: Sample.from_ndarray(t[0], t[1]))
+    test_data = train_data
+    optimizer = Optimizer(
+        model=build_model(10),
+        training_rdd=train_data,
+        criterion=ClassNLLCriterion(),
+        optim_method=SGD(learningrate=0.05, learningrate_decay=0.0002),
+        end_trigger=MaxEpoch(3),
+        batch_size=16)
+    optimizer.set_validation(batch_size=16, val_rdd=test_data, trigger=EveryEpoch(), val_method=[Top1Accuracy()])
+    optimizer.set_checkpoint(EveryEpoch(), ckpt)
+    trained_model = optimizer.optimize()
+    parameters = trained_model.parameters()
+    model = Model.load(ckpt + "/model.latest")
+    results = model.evaluate(test_data, 16, [Top1Accuracy()])
+    sc.stop()
+    return trained_model, parameters, results
+'''
+
+
+def test_reference_lenet_script_trains_checkpoints_and_evaluates(bigdl, tmp_path):
+    rng = np.random.RandomState(0)
+    labels = rng.randint(0, 10, size=96).astype(np.float32)
+    # learnable synthetic digits: a class-dependent bright bar on noise
+    images = rng.randint(0, 60, size=(96, 28, 28, 1)).astype(np.float32)
+    for i, l in enumerate(labels.astype(int)):
+        images[i, 2 * l + 3:2 * l + 6, 4:24, 0] = 250
+    ns = {}
+    exec(compile(LENET, "lenet5_reference_style.py", "exec"), ns)
+    model, params, results = ns["run"](images.reshape(96, 784), labels, str(tmp_path))
+    assert os.path.exists(tmp_path / "model.latest")
+    assert set(params) and all("weight" in v for v in params.values())
+    acc = results[0].result
+    assert results[0].total_num == 96 and acc > 0.5, acc
+    # the trained model predicts with the ndarray API
+    pred = model.predict_class(images.reshape(96, 784))
+    assert pred.shape == (96,) and pred.min() >= 1
+
+
+def test_local_optimizer_and_layer_ndarray_api(bigdl):
+    from bigdl.nn.criterion import MSECriterion
+    from bigdl.nn.layer import Linear, Model, Input, ReLU, Sequential
+    from bigdl.optim.optimizer import Adam, MaxIteration, Optimizer
+    from bigdl.util.common import JTensor, Sample
+
+    rng = np.random.RandomState(1)
+    X = rng.randn(64, 4).astype(np.float32)
+    W = rng.randn(4, 2).astype(np.float32)
+    Y = X @ W
+    inp = Input()
+    out = Linear(4, 2, with_bias=False)(inp)
+    model = Model([inp], [out])
+    opt = Optimizer.create(model, (X, Y), MSECriterion(), MaxIteration(300), 16, Adam(learningrate=0.05))
+    trained = opt.optimize()
+    assert np.abs(trained.forward(X) - Y).mean() < 0.05
+    seq = Sequential().add(Linear(4, 3)).add(ReLU())
+    w = [np.ones((3, 4), np.float32), np.zeros(3, np.float32)]
+    seq.set_weights(w)
+    assert np.allclose(seq.get_weights()[0], 1.0)
+    seq.forward(X[:2])
+    g = seq.backward(X[:2], np.ones((2, 3), np.float32))
+    assert g.shape == (2, 4)
+    seq.zero_grad_parameters()
+    s = Sample.from_ndarray(np.arange(6).reshape(2, 3), np.array([1.0]))
+    assert s.feature.to_ndarray().shape == (2, 3)
+    assert np.allclose(JTensor.sparse(np.array([1.0, 2.0]), np.array([0, 1, 1, 2]), [2, 3]).to_ndarray(),
+                       [[0, 1, 0], [0, 0, 2]])
+
+
+def test_snake_case_keywords_map_to_engine_arguments(bigdl):
+    from bigdl.nn.layer import SpatialConvolution, Linear
+    from bigdl.optim.optimizer import SGD, Plateau, SequentialSchedule, Warmup, Poly
+
+    conv = SpatialConvolution(n_input_plane=3, n_output_plane=4, kernel_w=3, kernel_h=3, stride_w=2, pad_w=1,
+                              pad_h=1, with_bias=False, bigdl_type="float")
+    assert conv.value.nInputPlane == 3 and conv.value.strideW == 2 and conv.value.bias is None
+    lin = Linear(2, 3, init_weight=np.ones((3, 2), np.float32), init_bias=np.zeros(3, np.float32))
+    assert np.allclose(lin.get_weights()[0], 1.0)
+    with pytest.raises(TypeError):
+        Linear(2, 3, no_such_argument=1)
+    sched = SequentialSchedule(5).add(Warmup(0.1), 3).add(Poly(0.5, 100), 100)
+    sgd = SGD(learningrate=0.1, momentum=0.9, leaningrate_schedule=sched)
+    assert sgd.value.momentum == 0.9 and sgd.value.learningRateSchedule is sched.value
+    assert Plateau("score").value is not None
