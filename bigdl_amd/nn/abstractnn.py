@@ -599,11 +599,15 @@ class AbstractModule(MklInt8Convertible, metaclass=_RecordInit):
         return Graph([inp], [out])
 
     # ------------------------------------------------------------------ persistence / inference
-    def saveModule(self, path, weightPath=None, overWrite=False):
+    def saveModule(self, path, weightPath=None, overWrite=False, format=None):
         from ..utils.serializer import save_module
 
-        save_module(self, path, weightPath, overWrite)
+        save_module(self, path, weightPath, overWrite, format)
         return self
+
+    def saveBigDL(self, path, weightPath=None, overWrite=False):
+        """Write the reference's bigdl.proto ``BigDLModule`` format (utils/bigdl_proto.py)."""
+        return self.saveModule(path, weightPath, overWrite, format="bigdl")
 
     def save(self, path, overWrite=False):
         return self.saveModule(path, overWrite=overWrite)

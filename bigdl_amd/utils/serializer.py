@@ -210,8 +210,21 @@ def decode_module(d, tensors):
     return m
 
 
-def save_module(module, path, weightPath=None, overWrite=False):
+def save_module(module, path, weightPath=None, overWrite=False, format=None):
+    """``format``: "safetensors" (default; engine-native, every attribute) or "bigdl" (the reference's
+    bigdl.proto ``BigDLModule``, utils/bigdl_proto.py). The default follows the ``bigdl.modelFormat`` engine
+    property."""
     from safetensors.torch import save_file
+
+    if format is None:
+        from .engine import Engine
+
+        format = Engine.getProperty("bigdl.modelFormat", "safetensors")
+    if format in ("bigdl", "protobuf", "proto"):
+        from .bigdl_proto import save_bigdl
+
+        save_bigdl(module, path, weightPath, overWrite)
+        return path
 
     for p in (path, weightPath):
         if p is not None and os.path.exists(p) and not overWrite:
@@ -229,8 +242,15 @@ def save_module(module, path, weightPath=None, overWrite=False):
 
 
 def load_module(path, weightPath=None):
+    """Loads either format: safetensors files written by this package, or bigdl.proto ``BigDLModule`` files
+    (reference ModuleLoader.loadFromFile)."""
     from safetensors import safe_open
     from safetensors.torch import load_file
+
+    from .bigdl_proto import is_bigdl_proto, load_bigdl
+
+    if is_bigdl_proto(path):
+        return load_bigdl(path, weightPath)
 
     with safe_open(path, framework="pt") as f:
         meta = f.metadata() or {}

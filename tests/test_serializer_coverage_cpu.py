@@ -1,0 +1,204 @@
+"""Every registered module class round-trips through BOTH persistence formats — the engine's safetensors format
+and the reference's bigdl.proto ``BigDLModule`` (reference T/utils/serializer/SerializerSpec.scala:38-285
+enumerates every module and requires a save/load round trip). Classes are enumerated from the module
+registry, so a new module without serialization support fails here instead of at a user's save time."""
+import importlib
+import inspect
+
+import pytest
+import torch
+
+import bigdl_amd.keras  # noqa: F401  (registers the keras-style layers)
+import bigdl_amd.nn as nn
+import bigdl_amd.quantized  # noqa: F401
+from bigdl_amd.nn.abstractnn import AbstractCriterion, all_module_classes
+from bigdl_amd.utils.serializer import load_module
+
+for _m in ("bigdl_amd.nn.tf", "bigdl_amd.nn.ops", "bigdl_amd.nn.tf_ops"):
+    importlib.import_module(_m)
+
+
+def _lin():
+    return nn.Linear(3, 2)
+
+
+# constructor arguments for classes without an all-default constructor (reference SerializerSpec's table)
+ARGS = {
+    "ActivityRegularization": (0.1, 0.2), "Add": (4,), "AddConstant": (1.5,), "Attention": (8, 2, 0.0),
+    "BatchNormalization": (4,), "BifurcateSplitTable": (1,), "Bilinear": (3, 4, 2), "BinaryTreeLSTM": (3, 4),
+    "Bottle": (_lin,), "BoxHead": (8,), "BoxPostProcessor": (0.05, 0.5, 10, 3), "CAdd": ([1, 4],),
+    "CMul": ([1, 4],), "Clamp": (-1.0, 1.0), "Concat": (2,), "ConvLSTMPeephole": (3, 4, 3, 3),
+    "ConvLSTMPeephole3D": (3, 4, 3, 3), "Cosine": (3, 2), "Cropping2D": ([1, 1], [1, 1]),
+    "Cropping3D": ([1, 1], [1, 1], [1, 1]), "Euclidean": (3, 2), "ExpandSize": ([2, 3],), "FPN": ([4, 8], 4),
+    "FeedForwardNetwork": (8, 16, 0.0), "GRU": (3, 4), "GaussianDropout": (0.1,), "GaussianNoise": (0.1,),
+    "Highway": (4,), "Index": (1,), "InferReshape": ([-1, 2],), "JoinTable": (2, 2), "L1Penalty": (0.1,),
+    "LSTM": (3, 4), "LSTMPeephole": (3, 4), "LayerNormalization": (8,), "Linear": (3, 2),
+    "LocallyConnected1D": (6, 3, 2, 3), "LocallyConnected2D": (2, 6, 6, 3, 3, 3),
+    "LookupTable": (10, 4), "LookupTableSparse": (10, 4), "MaskHead": (8,), "Maxout": (3, 2, 2),
+    "MulConstant": (2.0,), "Narrow": (1, 1, 2), "NarrowTable": (1, 2), "NormalizeScale": (2.0, 20.0, [1, 4, 1, 1]),
+    "Pack": (1,), "Padding": (1, 2, 2), "Pooler": (7, [0.25], 2), "Power": (2.0,), "PriorBox": ([30.0],),
+    "Proposal": (100, 10, [0.5, 1.0, 2.0], [8.0, 16.0]), "RecurrentDecoder": (3,), "RegionProposal": (8,),
+    "Replicate": (3,), "Reshape": ([2, 3],), "ResizeBilinear": (4, 4), "RoiAlign": (0.25, 2, 7, 7),
+    "RoiPooling": (7, 7, 0.25), "SReLU": ([4],), "Scale": ([1, 4, 1, 1],), "Select": (1, 1), "SelectTable": (1,),
+    "SequenceBeamSearch": (20, 2, 0.6, 5, 1, 0.0, 1, 8), "SparseJoinTable": (2,), "SparseLinear": (10, 3),
+    "SpatialAveragePooling": (2, 2), "SpatialBatchNormalization": (4,), "SpatialConvolution": (3, 4, 3, 3),
+    "SpatialConvolutionMap": (lambda: nn.SpatialConvolutionMap.full(2, 3), 3, 3),
+    "QuantizedLinear": (3, 2), "QuantizedSpatialConvolution": (3, 4, 3, 3),
+    "QuantizedSpatialDilatedConvolution": (3, 4, 3, 3), "SpatialDilatedConvolution": (3, 4, 3, 3),
+    "SpatialFullConvolution": (3, 4, 3, 3), "SpatialMaxPooling": (2, 2),
+    "SpatialSeparableConvolution": (4, 8, 1, 3, 3), "SpatialShareConvolution": (3, 4, 3, 3),
+    "SpatialZeroPadding": (1, 1, 1, 1), "SplitTable": (1,), "SplitTensor": (1, 2),
+    "TableOperation": (lambda: nn.CMulTable(),), "TemporalConvolution": (3, 4, 2), "TemporalMaxPooling": (2,),
+    "TimeDistributed": (_lin,), "Transformer": (20, 8, 2, 16, 1, 0.0, 0.0, 0.0), "Transpose": ([(1, 2)],),
+    "TreeLSTM": (3,), "Unsqueeze": (1,), "UpSampling1D": (2,), "UpSampling2D": ([2, 2],),
+    "UpSampling3D": ([2, 2, 2],), "VolumetricAveragePooling": (2, 2, 2), "VolumetricConvolution": (2, 3, 2, 2, 2),
+    "VolumetricFullConvolution": (2, 3, 2, 2, 2), "VolumetricMaxPooling": (2, 2, 2),
+    "MultiRNNCell": (lambda: [nn.LSTM(3, 3), nn.LSTM(3, 3)],),
+    # keras-style layers
+    "keras.Activation": ("relu",), "keras.AtrousConvolution1D": (4, 3), "keras.AtrousConvolution2D": (4, 3, 3),
+    "keras.Bidirectional": (lambda: bigdl_amd.keras.layers.LSTM(4),), "keras.ConvLSTM2D": (4, 3),
+    "keras.Convolution1D": (4, 3), "keras.Convolution2D": (4, 3, 3), "keras.Convolution3D": (4, 2, 2, 2),
+    "keras.Deconvolution2D": (4, 3, 3), "keras.Dense": (4,), "keras.Dropout": (0.5,), "keras.Embedding": (10, 4),
+    "keras.GRU": (4,), "keras.GaussianDropout": (0.2,), "keras.GaussianNoise": (0.1,), "keras.InputLayer": ([3],),
+    "keras.KerasIdentityWrapper": (_lin,), "keras.KerasLayerWrapper": (_lin,), "keras.LSTM": (4,),
+    "keras.LocallyConnected1D": (4, 3), "keras.LocallyConnected2D": (4, 3, 3), "keras.MaxoutDense": (4,),
+    "keras.Permute": ([2, 1],), "keras.Recurrent": (4,), "keras.RepeatVector": (3,), "keras.Reshape": ([2, 3],),
+    "keras.SeparableConvolution2D": (4, 3, 3), "keras.SimpleRNN": (4,),
+    "keras.TimeDistributed": (lambda: bigdl_amd.keras.layers.Dense(3),),
+    # TF-graph operations
+    "nn.ops.BucketizedCol": ([0.0, 1.0],), "nn.ops.CategoricalColHashBucket": (10,),
+    "nn.ops.CategoricalColVocaList": (["a", "b"],), "nn.ops.CrossCol": (10,),
+    "nn.ops.Dilation2D": ([1, 1, 1, 1], [1, 1, 1, 1], "SAME"), "nn.ops.InTopK": (1,), "nn.ops.IndicatorCol": (5,),
+    "nn.ops.ModuleToOperation": (_lin,), "nn.ops.TopK": (2,), "nn.tf.AvgPoolGrad": (2, 2, 1, 1),
+    "nn.tf.Const": (lambda: torch.ones(2, 3),), "nn.tf.Conv2D": (1, 1), "nn.tf.Conv2DBackFilter": (1, 1, 0, 0),
+    "nn.tf.Conv2DTranspose": (1, 1), "nn.tf.Conv3D": (1, 1, 1), "nn.tf.Conv3DBackpropFilter": (1, 1, 1),
+    "nn.tf.Conv3DBackpropFilterV2": (1, 1, 1), "nn.tf.Conv3DBackpropInput": (1, 1, 1),
+    "nn.tf.Conv3DBackpropInputV2": (1, 1, 1), "nn.tf.Enter": ("frame",), "nn.tf.MaxPoolGrad": (2, 2, 1, 1),
+    "nn.tf.SplitAndSelect": (1, 1, 2), "nn.tf.StridedSlice": ([(1, 1, 2, 1)],),
+    "nn.tf.Variable": (lambda: torch.ones(3),),
+}
+
+# containers that are built by adding their cell / body (reference SerializerSpec builds them the same way)
+BUILD = {
+    "Recurrent": lambda: nn.Recurrent().add(nn.LSTM(3, 4)),
+    "BiRecurrent": lambda: nn.BiRecurrent().add(nn.GRU(3, 4)),
+    "RecurrentDecoder": lambda: nn.RecurrentDecoder(3).add(nn.LSTM(4, 4)),
+}
+
+# classes that cannot be built standalone (need a live graph / data-flow context or are abstract bases),
+# each with the reason; they are covered by the graph / TF-import tests instead
+SKIP = {
+    "Graph": "built from nodes: covered by test_graph_round_trips_both_formats",
+    "DynamicGraph": "built from nodes: covered by test_graph_round_trips_both_formats",
+    "Cell": "abstract recurrent-cell base", "keras.Recurrent": "abstract keras recurrent base",
+    "nn.ops.TensorOp": "wraps a Python callable (not serializable by design in either format)",
+    "ops.TFOp": "wraps a Python callable (TF import creates it with the op's closure)",
+    "nn.tf.AssignGrad": "aliases a live variable buffer", "nn.tf.TensorArrayGrad": "aliases a live TensorArray",
+    "nn.tf.ParseExample": "takes TF dtype objects", "nn.tf.ParseSingleExample": "takes TF dtype objects",
+    "nn.tf.TensorModuleWrapper": "wraps a Python callable",
+    "BaseModule": "abstract base of the detection heads", "QuantizedModule": "abstract quantized base",
+}
+
+
+def _args(key):
+    a = ARGS.get(key, ())
+    return tuple(x() if callable(x) and not isinstance(x, type) else x for x in a)
+
+
+def _classes():
+    out = []
+    for key, cls in sorted(all_module_classes().items()):
+        if issubclass(cls, AbstractCriterion) or key.startswith("_") or key in SKIP:
+            continue
+        if inspect.isabstract(cls):
+            continue
+        out.append((key, cls))
+    return out
+
+
+def _state(m):
+    ws = m.parameters()
+    ws = [w.detach().float().clone() for w in ws[0]] if ws else []
+    bufs = [getattr(m, b).detach().float().clone() for b in getattr(m, "_buffers", ())
+            if isinstance(getattr(m, b, None), torch.Tensor)]
+    return ws, bufs
+
+
+@pytest.mark.parametrize("fmt", ["safetensors", "bigdl"])
+def test_every_registered_module_round_trips(fmt, tmp_path):
+    failures, n = [], 0
+    for key, cls in _classes():
+        try:
+            m = BUILD[key]() if key in BUILD else cls(*_args(key))
+        except Exception as e:  # noqa: BLE001
+            failures.append(f"{key}: cannot construct with the test table args: {type(e).__name__}: {e}")
+            continue
+        path = str(tmp_path / f"{key}.model")
+        try:
+            m.saveModule(path, overWrite=True, format=fmt)
+            m2 = load_module(path)
+        except Exception as e:  # noqa: BLE001
+            failures.append(f"{key}: {type(e).__name__}: {e}")
+            continue
+        n += 1
+        if type(m2) is not type(m):
+            failures.append(f"{key}: loaded as {type(m2).__name__}")
+            continue
+        (w1, b1), (w2, b2) = _state(m), _state(m2)
+        if len(w1) != len(w2) or any(a.shape != b.shape or not torch.equal(a, b) for a, b in zip(w1, w2)):
+            failures.append(f"{key}: parameters differ after the round trip")
+        if len(b1) != len(b2) or any(a.shape != b.shape or not torch.equal(a, b) for a, b in zip(b1, b2)):
+            failures.append(f"{key}: buffers differ after the round trip")
+    assert not failures, f"{len(failures)} of {n + len(failures)} modules fail ({fmt}):\n" + "\n".join(failures)
+    assert n > 250
+
+
+@pytest.mark.parametrize("fmt", ["safetensors", "bigdl"])
+def test_graph_round_trips_both_formats(fmt, tmp_path):
+    i = nn.Input()
+    a = nn.Linear(4, 3)(i)
+    b = nn.Tanh()(a)
+    c = nn.CAddTable()(a, b)
+    s = nn.SplitTable(2)(c)
+    d = nn.SelectTable(2)(s)
+    g = nn.Graph([i], [c, d])
+    x = torch.randn(2, 4)
+    y = g.forward(x)
+    g.saveModule(str(tmp_path / "g.model"), overWrite=True, format=fmt)
+    g2 = load_module(str(tmp_path / "g.model"))
+    y2 = g2.forward(x)
+    assert torch.equal(y[1], y2[1]) and torch.equal(y[2], y2[2])
+
+
+def test_bigdl_proto_separate_weight_file_and_shared_weights(tmp_path):
+    lin = nn.Linear(4, 4)
+    m = nn.Sequential().add(lin).add(nn.ReLU()).add(lin)        # the same module twice (shared weights)
+    x = torch.randn(3, 4)
+    y = m.forward(x)
+    m.saveBigDL(str(tmp_path / "m.model"), str(tmp_path / "m.bin"))
+    m2 = load_module(str(tmp_path / "m.model"), str(tmp_path / "m.bin"))
+    assert m2.modules[0] is m2.modules[2]                      # module identity survives (BigDLModule.id)
+    assert torch.equal(m2.forward(x), y)
+    raw = bytearray((tmp_path / "m.bin").read_bytes())
+    raw[20] ^= 0xFF
+    (tmp_path / "bad.bin").write_bytes(bytes(raw))
+    with pytest.raises(ValueError):
+        load_module(str(tmp_path / "m.model"), str(tmp_path / "bad.bin"))
+
+
+def test_bigdl_proto_field_layout_is_the_reference_schema(tmp_path):
+    """Decode our file with a schema built independently from RES/serialization/bigdl.proto field numbers."""
+    from bigdl_amd.utils import pbwire as pb
+
+    m = nn.Sequential().add(nn.Linear(2, 3).setName("fc"))
+    m.saveBigDL(str(tmp_path / "m.model"))
+    root = pb.Msg((tmp_path / "m.model").read_bytes())
+    assert root.str(7) == "com.intel.analytics.bigdl.nn.Sequential"          # moduleType = 7
+    sub = root.msgs(2)[0]                                                      # subModules = 2
+    assert sub.str(7) == "com.intel.analytics.bigdl.nn.Linear" and sub.str(1) == "fc"
+    assert sub.bool(15)                                                        # hasParameters = 15
+    params = sub.msgs(16)                                                      # parameters = 16
+    assert [p.ints(2) for p in params] == [[3, 2], [3]]                        # BigDLTensor.size = 2
+    attrs = {e.str(1): e.msg(2) for e in sub.msgs(8)}                          # attr map<string, AttrValue> = 8
+    assert attrs["inputSize"].int(3) == 2 and attrs["outputSize"].int(3) == 3  # int32Value = 3
+    assert "global_storage" in {e.str(1) for e in root.msgs(8)}
