@@ -14,8 +14,12 @@ import bigdl_amd.quantized  # noqa: F401
 from bigdl_amd.nn.abstractnn import AbstractCriterion, all_module_classes
 from bigdl_amd.utils.serializer import load_module
 
-for _m in ("bigdl_amd.nn.tf", "bigdl_amd.nn.ops", "bigdl_amd.nn.tf_ops"):
-    importlib.import_module(_m)
+import pkgutil  # noqa: E402
+
+import bigdl_amd  # noqa: E402
+
+for _m in pkgutil.walk_packages(bigdl_amd.__path__, "bigdl_amd."):
+    importlib.import_module(_m.name)   # the complete registry, whatever other tests imported first
 
 
 def _lin():
@@ -53,7 +57,7 @@ ARGS = {
     "TreeLSTM": (3,), "Unsqueeze": (1,), "UpSampling1D": (2,), "UpSampling2D": ([2, 2],),
     "UpSampling3D": ([2, 2, 2],), "VolumetricAveragePooling": (2, 2, 2), "VolumetricConvolution": (2, 3, 2, 2, 2),
     "VolumetricFullConvolution": (2, 3, 2, 2, 2), "VolumetricMaxPooling": (2, 2, 2),
-    "MultiRNNCell": (lambda: [nn.LSTM(3, 3), nn.LSTM(3, 3)],),
+    "MultiRNNCell": (lambda: [nn.LSTM(3, 3), nn.LSTM(3, 3)],), "MaskRCNN": (8, 8),
     # keras-style layers
     "keras.Activation": ("relu",), "keras.AtrousConvolution1D": (4, 3), "keras.AtrousConvolution2D": (4, 3, 3),
     "keras.Bidirectional": (lambda: bigdl_amd.keras.layers.LSTM(4),), "keras.ConvLSTM2D": (4, 3),
@@ -96,6 +100,7 @@ SKIP = {
     "nn.tf.AssignGrad": "aliases a live variable buffer", "nn.tf.TensorArrayGrad": "aliases a live TensorArray",
     "nn.tf.ParseExample": "takes TF dtype objects", "nn.tf.ParseSingleExample": "takes TF dtype objects",
     "nn.tf.TensorModuleWrapper": "wraps a Python callable",
+    "OnnxOp": "wraps the importer's op closure (covered by the ONNX import tests)",
     "BaseModule": "abstract base of the detection heads", "QuantizedModule": "abstract quantized base",
 }
 
