@@ -235,6 +235,20 @@ class RnnCell(Cell):
         return h, [h]
 
 
+def _rnn_param_grads(dg16, h16, U, WT16):
+    """Native MFMA GEMMs closing a fused recurrent backward sweep (no library GEMM):
+    dU = sum_t dg_t^T h_{t-1} over all T*B rows (the conv weight-gradient kernel on a 1x1 'image' of T*B pixels:
+    split-K over rows, fp32 accumulation) and dh0 = dg_0 . U (the conv forward kernel, 1x1)."""
+    from ..ops import conv as cv
+
+    T, B, G = dg16.shape
+    H = U.shape[1]
+    dU = torch.zeros(G, H, 1, 1, device=dg16.device)
+    cv.conv2d_wgrad(dg16.view(T * B, G, 1, 1), h16[:T].view(T * B, H, 1, 1), dU, None, (1, 1), (0, 0))
+    dh0 = cv.conv2d_fwd(dg16[0].view(B, G, 1, 1), WT16.view(H, G, 1, 1), None, (1, 1), (0, 0))
+    return dh0.view(B, H).float(), dU.view(G, H)
+
+
 class _LSTMSeq(torch.autograd.Function):
     """Whole-sequence LSTM (gate order i, g, f, o) with the fused HIP cell kernels on the GPU engine."""
 
@@ -278,13 +292,15 @@ class _LSTMSeq(torch.autograd.Function):
             out = xg.new_empty(B, T, H)
             cs = xg.new_empty(T, B, H)
             acts = xg.new_empty(T, B, G)
-            h16 = xg.new_empty(2, B, H, dtype=torch.bfloat16)
+            # time-major bf16 states h_{-1..T-1}: step t's GEMM operand, and (rows t*B + b) the B operand of the
+            # weight-gradient GEMM after the backward sweep
+            h16 = xg.new_empty(T + 1, B, H, dtype=torch.bfloat16)
             h16[0].copy_(h0)
             c_prev = c0.contiguous()
             for t in range(T):
-                C.lstm_fwd_step(W16, h16[t & 1], xg[:, t], c_prev, cs[t], out[:, t], h16[(t + 1) & 1], acts[t])
+                C.lstm_fwd_step(W16, h16[t], xg[:, t], c_prev, cs[t], out[:, t], h16[t + 1], acts[t])
                 c_prev = cs[t]
-            ctx.save_for_backward(h0, c0, U, out, cs, acts)
+            ctx.save_for_backward(h0, c0, U, out, cs, acts, h16)
             ctx.fused = True
             return out, out[:, -1].clone(), cs[-1].clone()
         hs = xg.new_empty(T, B, H)
@@ -302,23 +318,21 @@ class _LSTMSeq(torch.autograd.Function):
 
     @staticmethod
     def _backward_fused(ctx, dout, dhT, dcT):
-        h0, c0, U, out, cs, acts = ctx.saved_tensors
+        h0, c0, U, out, cs, acts, h16 = ctx.saved_tensors
         B, T, H = out.shape
         C = ops.native.get()
         dout = dout.contiguous() if dout is not None else None
         WT16 = U.detach().t().contiguous().to(torch.bfloat16)
         dxg = out.new_empty(B, T, 4 * H)
-        dg16 = out.new_empty(2, B, 4 * H, dtype=torch.bfloat16)
+        dg16 = out.new_empty(T, B, 4 * H, dtype=torch.bfloat16)      # time-major: rows t*B + b
         dc = dcT.contiguous().clone() if dcT is not None else out.new_zeros(B, H)
         dhT = dhT.contiguous() if dhT is not None else None
         c0 = c0.contiguous()
         for t in range(T - 1, -1, -1):
-            C.lstm_bwd_step(WT16, dg16[(t + 1) & 1] if t < T - 1 else None,
+            C.lstm_bwd_step(WT16, dg16[t + 1] if t < T - 1 else None,
                             dout[:, t] if dout is not None else None, dhT if t == T - 1 else None, acts[t],
-                            cs[t - 1] if t > 0 else c0, cs[t], dc, dxg[:, t], dg16[t & 1])
-        dh0 = dxg[:, 0] @ U
-        hprev = torch.cat([h0.unsqueeze(1), out[:, :-1]], 1).reshape(B * T, H)
-        dU = torch.matmul(dxg.reshape(B * T, 4 * H).t().to(torch.bfloat16), hprev.to(torch.bfloat16)).float()
+                            cs[t - 1] if t > 0 else c0, cs[t], dc, dxg[:, t], dg16[t])
+        dh0, dU = _rnn_param_grads(dg16, h16, U, WT16)
         return dxg, dh0, dc, dU
 
     @staticmethod
@@ -341,6 +355,66 @@ class _LSTMSeq(torch.autograd.Function):
         hprev = torch.cat([h0.unsqueeze(0), hs[:-1]], 0).reshape(T * B, H)
         dU = dgs.reshape(T * B, 4 * H).t() @ hprev
         return dgs.transpose(0, 1), dh_next, dc_next, dU
+
+
+class _GRUSeq(torch.autograd.Function):
+    """Whole-sequence GRU (preTopology order r, z, n) on the fused HIP step kernels (csrc/gru.hip): two MFMA
+    launches per step forward (r/z, then n and h) and two per step backward, then the recurrent weight gradients
+    as two native GEMMs over all T*B rows."""
+
+    @staticmethod
+    def usable(x, H):
+        return x.is_cuda and H % 32 == 0 and x.dtype == torch.float32
+
+    @staticmethod
+    def forward(ctx, xg, h0, Urz, Un):
+        B, T, G = xg.shape
+        H = G // 3
+        C = ops.native.get()
+        bf = torch.bfloat16
+        Wrz, Wn = Urz.detach().to(bf).contiguous(), Un.detach().to(bf).contiguous()
+        out = xg.new_empty(B, T, H)
+        gates = xg.new_empty(3, T, B, H)                 # r, z, n per step
+        h16 = xg.new_empty(T + 1, B, H, dtype=bf)         # h_{t-1} operands, time-major
+        rh16 = xg.new_empty(T, B, H, dtype=bf)            # (r * h_{t-1}) operands, time-major
+        h16[0].copy_(h0)
+        h0 = h0.contiguous()
+        for t in range(T):
+            hp = h0 if t == 0 else out[:, t - 1]
+            C.gru_step(0, h16[t], Wrz, B, H, xg=xg[:, t], hprev=hp, r=gates[0, t], z=gates[1, t], rh16=rh16[t])
+            C.gru_step(1, rh16[t], Wn, B, H, xg=xg[:, t], hprev=hp, z=gates[1, t], n=gates[2, t], hout=out[:, t],
+                       h16out=h16[t + 1])
+        ctx.save_for_backward(h0, Urz, Un, out, gates, h16, rh16)
+        return out, out[:, -1].clone()
+
+    @staticmethod
+    def backward(ctx, dout, dhT):
+        from ..ops import conv as cv
+
+        h0, Urz, Un, out, gates, h16, rh16 = ctx.saved_tensors
+        B, T, H = out.shape
+        C = ops.native.get()
+        bf = torch.bfloat16
+        UrzT = Urz.detach().t().contiguous().to(bf)       # [H, 2H]: D = drz . U_rz
+        UnT = Un.detach().t().contiguous().to(bf)         # [H, H]:  D = dn . U_n
+        dout = dout.contiguous() if dout is not None else None
+        dx = out.new_empty(B, T, 3 * H)
+        dn16 = out.new_empty(T, B, H, dtype=bf)
+        drz16 = out.new_empty(T, B, 2 * H, dtype=bf)
+        dhp = dhT.contiguous().clone() if dhT is not None else out.new_zeros(B, H)
+        for t in range(T - 1, -1, -1):
+            hp = h0 if t == 0 else out[:, t - 1]
+            C.gru_step(2, drz16[t + 1] if t < T - 1 else None, UrzT, B, H, hprev=hp, z=gates[1, t], n=gates[2, t],
+                       dout=dout[:, t] if dout is not None else None, dhp=dhp, dx=dx[:, t], dn16=dn16[t],
+                       drz16=drz16[t])
+            C.gru_step(3, dn16[t], UnT, B, H, hprev=hp, r=gates[0, t], dhp=dhp, dx=dx[:, t], drz16=drz16[t])
+        dh0 = out.new_empty(B, H)
+        C.gru_step(4, drz16[0], UrzT, B, H, dhp=dhp, dh0=dh0)
+        dUrz = torch.zeros(2 * H, H, 1, 1, device=out.device)
+        cv.conv2d_wgrad(drz16.view(T * B, 2 * H, 1, 1), h16[:T].view(T * B, H, 1, 1), dUrz, None, (1, 1), (0, 0))
+        dUn = torch.zeros(H, H, 1, 1, device=out.device)
+        cv.conv2d_wgrad(dn16.view(T * B, H, 1, 1), rh16.view(T * B, H, 1, 1), dUn, None, (1, 1), (0, 0))
+        return dx, dh0, dUrz.view(2 * H, H), dUn.view(H, H)
 
 
 class LSTM(Cell):
@@ -452,6 +526,15 @@ class GRU(Cell):
         n = act(x[:, 2 * H:] + F.linear(self._drop(r * h), self.h2n.weight))
         h2 = (1 - z) * n + z * h
         return h2, [h2]
+
+    def _fused_ok(self):
+        return self.p == 0 and _is(self.activation, Tanh) and _is(self.innerActivation, Sigmoid)
+
+    def sequence(self, x2, hid, mask=None):
+        if mask is None and self._fused_ok() and _GRUSeq.usable(x2, self.outputSize):
+            out, h = _GRUSeq.apply(x2.contiguous(), hid[0], self.h2g.weight, self.h2n.weight)
+            return out, [h]
+        return super().sequence(x2, hid, mask)
 
 
 class _ConvLSTMBase(Cell):

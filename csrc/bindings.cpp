@@ -488,6 +488,46 @@ void lstm_bwd_step(const Tensor& WT16, const OptT& dg16_next, const OptT& dout, 
                       ldg, mbf(dg16_out, "dg16_out"), B, H, stream());
 }
 
+int64_t rows_of(const OptT& t, int64_t B, int64_t cols, const char* name) {
+  if (!(t && t->defined())) return 0;
+  TORCH_CHECK(t->dim() == 2 && t->size(0) == B && t->size(1) >= cols && t->stride(1) == 1, name,
+              ": expected [B, >=", cols, "] rows with unit inner stride");
+  return t->stride(0);
+}
+void need_flat(const OptT& t, int64_t n, const char* name) {
+  if (t && t->defined()) TORCH_CHECK(t->is_contiguous() && t->numel() == n, name, ": expected ", n, " contiguous elements");
+}
+void gru_step(int64_t mode, const OptT& A, const Tensor& W, int64_t B, int64_t H, const OptT& xg, const OptT& hprev,
+              const OptT& r, const OptT& z, const OptT& n, const OptT& rh16, const OptT& hout, const OptT& h16out,
+              const OptT& dout, const OptT& dhp, const OptT& dx, const OptT& dn16, const OptT& drz16, const OptT& dh0) {
+  TORCH_CHECK(W.dim() == 2 && W.is_contiguous(), "gru_step: W must be [N, K] contiguous");
+  const int64_t N = W.size(0), K = W.size(1);
+  TORCH_CHECK(H % 32 == 0 && K % 32 == 0 && N % 16 == 0 && B > 0, "gru_step: H, K multiples of 32, N of 16");
+  TORCH_CHECK(mode >= 0 && mode <= 4, "gru_step: bad mode");
+  TORCH_CHECK(N == (mode == 0 ? 2 * H : H) && K == (mode == 2 || mode == 4 ? 2 * H : H), "gru_step: W shape vs mode");
+  GruStepArgs a{};
+  a.mode = (int)mode; a.B = (int)B; a.H = (int)H; a.K = (int)K; a.N = (int)N;
+  a.W = cbf(W, "W");
+  if (A && A->defined()) { a.lda = rows_of(A, B, K, "A"); a.A = cbf(*A, "A"); }
+  need_flat(r, B * H, "r"); need_flat(z, B * H, "z"); need_flat(n, B * H, "n"); need_flat(rh16, B * H, "rh16");
+  need_flat(h16out, B * H, "h16out"); need_flat(dhp, B * H, "dhp"); need_flat(dn16, B * H, "dn16");
+  need_flat(drz16, B * 2 * H, "drz16"); need_flat(dh0, B * H, "dh0");
+  a.ldx = rows_of(xg, B, 3 * H, "xg"); a.ldhp = rows_of(hprev, B, H, "hprev"); a.ldho = rows_of(hout, B, H, "hout");
+  a.ldd = rows_of(dout, B, H, "dout"); a.lddx = rows_of(dx, B, 3 * H, "dx");
+  a.xg = ocf(xg, "xg"); a.hprev = ocf(hprev, "hprev"); a.r = omf(r, "r"); a.z = omf(z, "z"); a.n = omf(n, "n");
+  a.rh16 = ombf(rh16, "rh16"); a.hout = omf(hout, "hout"); a.h16out = ombf(h16out, "h16out"); a.dout = ocf(dout, "dout");
+  a.dhp = omf(dhp, "dhp"); a.dx = omf(dx, "dx"); a.dn16 = ombf(dn16, "dn16"); a.drz16 = ombf(drz16, "drz16");
+  a.dh0 = omf(dh0, "dh0");
+  switch (mode) {
+    case 0: TORCH_CHECK(a.xg && a.r && a.z && a.rh16, "gru_step fwd r/z: xg, r, z, rh16 required"); break;
+    case 1: TORCH_CHECK(a.A && a.xg && a.z && a.n && a.hout && a.h16out, "gru_step fwd n: A, xg, z, n, hout, h16out required"); break;
+    case 2: TORCH_CHECK(a.z && a.n && a.dhp && a.dx && a.dn16 && a.drz16, "gru_step bwd h: z, n, dhp, dx, dn16, drz16 required"); break;
+    case 3: TORCH_CHECK(a.A && a.r && a.dhp && a.dx && a.drz16, "gru_step bwd r: A, r, dhp, dx, drz16 required"); break;
+    default: TORCH_CHECK(a.dhp && a.dh0, "gru_step bwd h0: dhp, dh0 required"); break;
+  }
+  TORCH_CHECK(bigdl_gru_step(&a, stream()) == 0, "gru_step: unsupported shape");
+}
+
 }  // namespace
 
 void register_host_runtime(pybind11::module& m);   // csrc/host_runtime.cpp
@@ -548,6 +588,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("f32_to_bf16_rtz", &f32_to_bf16_rtz);
   m.def("lstm_fwd_step", &lstm_fwd_step);
   m.def("lstm_bwd_step", &lstm_bwd_step);
+  m.def("gru_step", &gru_step, py::arg("mode"), py::arg("A"), py::arg("W"), py::arg("B"), py::arg("H"),
+        py::arg("xg") = py::none(), py::arg("hprev") = py::none(), py::arg("r") = py::none(), py::arg("z") = py::none(),
+        py::arg("n") = py::none(), py::arg("rh16") = py::none(), py::arg("hout") = py::none(),
+        py::arg("h16out") = py::none(), py::arg("dout") = py::none(), py::arg("dhp") = py::none(),
+        py::arg("dx") = py::none(), py::arg("dn16") = py::none(), py::arg("drz16") = py::none(),
+        py::arg("dh0") = py::none());
   m.def("set_conv_impl", &bigdl_set_conv_impl);
   m.def("get_conv_impl", &bigdl_get_conv_impl);
   m.attr("arch") = "gfx950";

@@ -166,4 +166,15 @@ int bigdl_lstm_fwd_step(const uint16_t* W16, const uint16_t* h16_prev, const flo
 int bigdl_lstm_bwd_step(const uint16_t* WT16, const uint16_t* dg16_next, const float* dout, long ldd,
                         const float* dh_ext, const float* acts, long lda, const float* c_prev, const float* c_t,
                         float* dc, float* dg_out, long ldg, uint16_t* dg16_out, int B, int H, hipStream_t st);
+
+// Fused GRU steps (csrc/gru.hip). mode: 0 fwd r/z, 1 fwd n + h, 2 bwd dh_t + dn/dz, 3 bwd dr + r-path, 4 bwd dh_0.
+// GEMM D[b][n] = sum_k A[b][k] W[n][k] (A rows lda apart; W [N][K] contiguous); row strides of the fp32 per-step
+// views (xg, hprev, hout, dout, dx) are in elements; every other buffer is a contiguous [B][H] ([B][2H] drz16).
+typedef struct {
+  const uint16_t* A; long lda; const uint16_t* W; int B, H, K, N, mode;
+  const float* xg; long ldx; const float* hprev; long ldhp; float* r; float* z; float* n; uint16_t* rh16;
+  float* hout; long ldho; uint16_t* h16out; const float* dout; long ldd; float* dhp; float* dx; long lddx;
+  uint16_t* dn16; uint16_t* drz16; float* dh0;
+} GruStepArgs;
+int bigdl_gru_step(const GruStepArgs* a, hipStream_t st);
 }
