@@ -191,12 +191,53 @@ def transpose_w(w16, out=None):
     return out
 
 
+def _gemm_shaped(dy, x, dw32, stride, pad, dil):
+    """A 1x1 / stride-1 / unpadded weight gradient is a plain GEMM dW[K][C] = sum_p dy[p][K] x[p][C]."""
+    K, C = dy.shape[1], x.shape[1]
+    return (dw32.shape[2] == 1 and dw32.shape[3] == 1 and tuple(stride) == (1, 1) and tuple(pad) == (0, 0)
+            and dy.shape[2:] == x.shape[2:] and dw32.is_contiguous() and C % 8 == 0 and K % 8 == 0
+            and dy.is_contiguous(memory_format=CL) and x.is_contiguous(memory_format=CL))
+
+
+def _rows_T64(t2d):
+    """(P, C) bf16 rows -> (C, P64) bf16, P zero-padded to a multiple of 64 (the LDS-DMA GEMM's K step)."""
+    P, C = t2d.shape
+    P64 = -(-P // 64) * 64
+    if P64 != P:
+        pad = torch.zeros((P64, C), dtype=BF16, device=t2d.device)
+        pad[:P].copy_(t2d)
+        t2d = pad
+    out = torch.empty((C, P64), dtype=BF16, device=t2d.device)
+    native.get().transpose_krsc(t2d, out, P64, 1, C)
+    return out
+
+
+def gemm_wgrad_nt(dy2d, x2d, dw32, dbias32=None):
+    """dW (fp32 [K][C]) += dy^T x over P rows on the NT MFMA GEMM kernel: both operands are transposed once (LDS
+    tiles) so the reduction runs along contiguous rows, and the epilogue accumulates fp32 straight into dW. For
+    large outputs this is ~2-5x the split-K weight-gradient kernel (which exists for small outputs / deep
+    reductions, where it fills the chip by splitting P)."""
+    P, K = dy2d.shape
+    C = x2d.shape[1]
+    dyT, xT = _rows_T64(dy2d), _rows_T64(x2d)
+    P64 = dyT.shape[1]
+    geo = [K, 1, 1, P64, 1, 1, 1, 1, P64, C, C, 1, 1, 1, 1, 0, 0]
+    native.get().conv_nt(dyT, xT, dw32.view(K, C), None, None, geo, [0, 0, 0], False, accumulate=True)
+    if dbias32 is not None:
+        native.get().colsum_bf16(dy2d, dbias32)
+
+
 def conv2d_wgrad(dy, x, dw32, dbias32, stride, pad, dil=(1, 1)):
     """dW (fp32, (K, C, R, S) channels_last buffer) += conv weight gradient; dbias += sum(dy)."""
     N, C, H, W = x.shape
     _, K, OH, OW = dy.shape
     Kw, Cw, R, S = dw32.shape
     assert Kw == K and Cw == C
+    P = N * OH * OW
+    if (P >= 512 and ((K + 127) // 128) * ((C + 127) // 128) >= 192 and _gemm_shaped(dy, x, dw32, stride, pad, dil)):
+        gemm_wgrad_nt(dy.reshape(P, K) if dy.is_contiguous() else dy.permute(0, 2, 3, 1).reshape(P, K),
+                      x.reshape(P, C) if x.is_contiguous() else x.permute(0, 2, 3, 1).reshape(P, C), dw32, dbias32)
+        return
     sh, sw = stride
     ph, pw = pad
     dh, dw = dil

@@ -33,13 +33,16 @@ float* omf(const OptT& t, const char* n) { return (t && t->defined()) ? mf(*t, n
 // taps = flat [tap_h0, tap_w0, tap_k0, tap_h1, ...]
 void conv_nt(const Tensor& src, const Tensor& wt, const Tensor& out, const OptT& bias, const OptT& stats,
              std::vector<int64_t> geo, std::vector<int64_t> taps, bool relu, const OptT& addend, const OptT& bn_x,
-             const OptT& bn_z, const OptT& bn_mean, const OptT& bn_aff, const OptT& bn_red) {
+             const OptT& bn_z, const OptT& bn_mean, const OptT& bn_aff, const OptT& bn_red, bool accumulate) {
   TORCH_CHECK(geo.size() == 17, "conv_nt: bad geometry");
   if (stats && stats->defined())
     TORCH_CHECK(stats->numel() >= BIGDL_STAT_SLOTS * 2 * geo[9], "conv_nt: stats must hold STAT_SLOTS x 2Ncol");
   TORCH_CHECK(taps.size() % 3 == 0 && !taps.empty() && taps.size() / 3 <= CONV_MAX_TAPS, "conv_nt: bad taps");
   ConvArgs a;
-  a.src = cbf(src, "src"); a.wt = cbf(wt, "wt"); a.out = mbf(out, "out");
+  a.src = cbf(src, "src"); a.wt = cbf(wt, "wt");
+  a.out = nullptr; a.out32 = nullptr; a.accum32 = accumulate ? 1 : 0;
+  if (out.scalar_type() == at::kFloat) a.out32 = mf(out, "out");   // fp32 GEMM output (weight gradients)
+  else a.out = mbf(out, "out");
   a.bias = ocf(bias, "bias"); a.stats = omf(stats, "stats");
   a.addend = ocbf(addend, "addend");
   if (a.addend) TORCH_CHECK(addend->numel() == out.numel(), "conv_nt: addend must match out");
@@ -70,7 +73,8 @@ void conv_nt(const Tensor& src, const Tensor& wt, const Tensor& out, const OptT&
   TORCH_CHECK((a.OH - 1) * a.omul_h + a.ooff_h < a.OHo && (a.OW - 1) * a.omul_w + a.ooff_w < a.OWo,
               "conv_nt: output placement out of range");
   const int rc = bigdl_conv_nt(&a, stream());
-  TORCH_CHECK(rc == 0, "conv_nt: unsupported shape (channels must be a multiple of 8)");
+  TORCH_CHECK(rc == 0, "conv_nt: unsupported shape (channels must be a multiple of 8; fp32 output needs Ncol % 8 "
+              "== 0 and no fused stats / BN / ReLU / addend)");
 }
 
 // geo = [Nb, Hs, Ws, Cs, OH, OW, R, S, sh, sw, ph, pw, dh, dw, M, Ncol, Kdim, ldy]
@@ -275,7 +279,7 @@ void conv_i8(const Tensor& src, const Tensor& wt, const Tensor& out, const OptT&
   a.src = reinterpret_cast<const uint16_t*>(src.data_ptr<int8_t>());
   a.wt = reinterpret_cast<const uint16_t*>(wt.data_ptr<int8_t>());
   a.out = reinterpret_cast<uint16_t*>(out.data_ptr());
-  a.bias = ocf(bias, "bias"); a.stats = nullptr; a.addend = nullptr;
+  a.bias = ocf(bias, "bias"); a.stats = nullptr; a.addend = nullptr; a.out32 = nullptr; a.accum32 = 0;
   a.bnx = nullptr; a.bnz = nullptr; a.bnmean = nullptr; a.bnaff = nullptr; a.bnred = nullptr;
   a.Nb = geo[0]; a.Hs = geo[1]; a.Ws = geo[2]; a.Cs = geo[3]; a.OH = geo[4]; a.OW = geo[5];
   a.mul_h = geo[6]; a.mul_w = geo[7]; a.ldw = geo[8]; a.Ncol = geo[9]; a.ldo = geo[10];
@@ -488,6 +492,11 @@ void lstm_bwd_step(const Tensor& WT16, const OptT& dg16_next, const OptT& dout, 
                       ldg, mbf(dg16_out, "dg16_out"), B, H, stream());
 }
 
+void colsum_bf16(const Tensor& x, const Tensor& out) {
+  TORCH_CHECK(x.dim() == 2 && x.is_contiguous() && x.size(1) % 8 == 0, "colsum_bf16: x must be [P, K] contiguous, K % 8 == 0");
+  TORCH_CHECK(out.is_contiguous() && out.numel() == x.size(1), "colsum_bf16: out must hold K floats");
+  bigdl_colsum_bf16(cbf(x, "x"), mf(out, "out"), x.size(0), (int)x.size(1), stream());
+}
 int64_t rows_of(const OptT& t, int64_t B, int64_t cols, const char* name) {
   if (!(t && t->defined())) return 0;
   TORCH_CHECK(t->dim() == 2 && t->size(0) == B && t->size(1) >= cols && t->stride(1) == 1, name,
@@ -538,7 +547,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_nt", &conv_nt, py::arg("src"), py::arg("wt"), py::arg("out"), py::arg("bias"), py::arg("stats"),
         py::arg("geo"), py::arg("taps"), py::arg("relu"), py::arg("addend") = py::none(), py::arg("bn_x") = py::none(),
         py::arg("bn_z") = py::none(), py::arg("bn_mean") = py::none(), py::arg("bn_aff") = py::none(),
-        py::arg("bn_red") = py::none());
+        py::arg("bn_red") = py::none(), py::arg("accumulate") = false);
   m.def("conv_wgrad", &conv_wgrad);
   m.def("transpose_krsc", &transpose_krsc);
   m.def("bn_stats", &bn_stats);
@@ -588,6 +597,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("f32_to_bf16_rtz", &f32_to_bf16_rtz);
   m.def("lstm_fwd_step", &lstm_fwd_step);
   m.def("lstm_bwd_step", &lstm_bwd_step);
+  m.def("colsum_bf16", &colsum_bf16);
   m.def("gru_step", &gru_step, py::arg("mode"), py::arg("A"), py::arg("W"), py::arg("B"), py::arg("H"),
         py::arg("xg") = py::none(), py::arg("hprev") = py::none(), py::arg("r") = py::none(), py::arg("z") = py::none(),
         py::arg("n") = py::none(), py::arg("rh16") = py::none(), py::arg("hout") = py::none(),

@@ -204,6 +204,18 @@ __device__ __forceinline__ void nt_epilogue_lds(const ConvArgs& a, v4f (&acc)[MI
     const v4f lo = *reinterpret_cast<const v4f*>(wl + gpos(p, 2 * q));
     const v4f hi = *reinterpret_cast<const v4f*>(wl + gpos(p, 2 * q + 1));
     const long orow = orows[r];
+    if (orow >= 0 && a.out32) {        // fp32 GEMM output (+ bias), optionally accumulated: 2 x 16-byte stores
+      float* o32 = a.out32 + (size_t)orow * a.ldo + n;
+      v4f p0 = {lo[0] + bs[0], lo[1] + bs[1], lo[2] + bs[2], lo[3] + bs[3]};
+      v4f p1 = {hi[0] + bs[4], hi[1] + bs[5], hi[2] + bs[6], hi[3] + bs[7]};
+      if (a.accum32) {
+        p0 += *reinterpret_cast<const v4f*>(o32);
+        p1 += *reinterpret_cast<const v4f*>(o32 + 4);
+      }
+      *reinterpret_cast<v4f*>(o32) = p0;
+      *reinterpret_cast<v4f*>(o32 + 4) = p1;
+      continue;
+    }
     if (orow >= 0) {
       float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       if (a.addend) {
@@ -1242,6 +1254,8 @@ int bigdl_conv_nt(const ConvArgs* a, hipStream_t st) {
   if (a->Cs % 8 != 0 || a->Kdim != a->ntaps * a->Cs || a->ntaps < 1 || a->ntaps > CONV_MAX_TAPS) return -1;
   // the BN-backward reduction lives in the LDS-transposed epilogue only
   if (a->bnred && (a->stats || a->bnx == nullptr || a->bnmean == nullptr || (a->Ncol & 7) || (a->ldo & 7))) return -2;
+  // fp32 output exists in the LDS-transposed epilogue only (aligned columns), without stats / BN / ReLU / addend
+  if (a->out32 && ((a->Ncol & 7) || (a->ldo & 7) || a->stats || a->bnred || a->relu || a->addend)) return -3;
   if (a->M <= 0) return 0;
   const bool fastk = (a->Cs % BK) == 0;
   const int impl = conv_impl();

@@ -81,6 +81,34 @@ __global__ __launch_bounds__(256) void nchw_to_nhwc_kernel(const float* __restri
         v4u{pack2bf(v[0], v[1]), pack2bf(v[2], v[3]), pack2bf(v[4], v[5]), pack2bf(v[6], v[7])};
   }
 }
+// Column sums of a [P][K] bf16 matrix into fp32 out[K] (+=): bias gradients of GEMM-shaped layers. A lane owns 8
+// consecutive columns (one 16-byte load per row), the 4 waves of a block take interleaved rows of the block's row
+// chunk, partials meet in LDS and one atomic per column per block lands in out.
+__global__ void __launch_bounds__(256) colsum_bf16_kernel(const bf16_t* __restrict__ x, float* __restrict__ out,
+                                                         long P, int K, long rows_per_block) {
+  __shared__ float part[4][64][9];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c0 = (blockIdx.x * 64 + lane) * 8;
+  const long r0 = (long)blockIdx.y * rows_per_block;
+  const long r1 = r0 + rows_per_block < P ? r0 + rows_per_block : P;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (c0 < K) {
+    for (long r = r0 + wave; r < r1; r += 4) {
+      const v4u q = *reinterpret_cast<const v4u*>(x + r * K + c0);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { acc[2 * e] += lo_bf(q[e]); acc[2 * e + 1] += hi_bf(q[e]); }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) part[wave][lane][e] = acc[e];
+  __syncthreads();
+  if (wave == 0 && c0 < K) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) atomicAdd(out + c0 + e, part[0][lane][e] + part[1][lane][e] + part[2][lane][e] +
+                                                        part[3][lane][e]);
+  }
+}
+
 __global__ void cast_f32_bf16_kernel(const float* __restrict__ x, bf16_t* __restrict__ y, long n) {
   const long n4 = n >> 2;
   GRID_STRIDE(i, n4) {
@@ -476,6 +504,16 @@ void bigdl_nchw_f32_to_nhwc_bf16(const float* x, uint16_t* y, int N, int C, int 
   nchw_to_nhwc_kernel<<<grid, 256, 0, st>>>(x, y, N, C, H, W, Cp);
   HIP_LAUNCH_CHECK();
 }
+void bigdl_colsum_bf16(const uint16_t* x, float* out, long P, int K, hipStream_t st) {
+  const int bx = (K / 8 + 63) / 64;
+  long by = (P + 255) / 256;                   // >= 64 rows per wave, ~2048 blocks at most
+  if ((long)bx * by > 2048) by = (2048 + bx - 1) / bx;
+  if (by < 1) by = 1;
+  const long rpb = (P + by - 1) / by;
+  colsum_bf16_kernel<<<dim3(bx, (unsigned)by), 256, 0, st>>>(x, out, P, K, rpb);
+  HIP_LAUNCH_CHECK();
+}
+
 void bigdl_cast_f32_bf16(const float* x, uint16_t* y, long n, hipStream_t st) {
   cast_f32_bf16_kernel<<<grid_cap(n / 4 + 1), 256, 0, st>>>(x, y, n);
   HIP_LAUNCH_CHECK();

@@ -33,6 +33,10 @@ struct ConvArgs {
   int OHo, OWo, omul_h, omul_w, ooff_h, ooff_w, ident_out;
   int relu;
   short tap_h[CONV_MAX_TAPS], tap_w[CONV_MAX_TAPS], tap_k[CONV_MAX_TAPS];
+  // fp32 output instead of bf16 (same placement / ldo), += into it when accum32: weight gradients of GEMM-shaped
+  // layers computed as an NT GEMM over transposed operands (LDS-transposed epilogue only; no stats / bn / relu)
+  float* out32;
+  int accum32;
 };
 
 struct WgradArgs {
@@ -81,6 +85,7 @@ void bigdl_add_bf16(const uint16_t* a, const uint16_t* b, uint16_t* y, long n, h
 void bigdl_nchw_f32_to_nhwc_bf16(const float* x, uint16_t* y, int N, int C, int H, int W, int Cp,
                                  hipStream_t st);
 void bigdl_cast_f32_bf16(const float* x, uint16_t* y, long n, hipStream_t st);
+void bigdl_colsum_bf16(const uint16_t* x, float* out, long P, int K, hipStream_t st);
 void bigdl_cast_bf16_f32(const uint16_t* x, float* y, long n, hipStream_t st);
 
 // pooling (NHWC bf16)

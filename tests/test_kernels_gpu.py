@@ -401,3 +401,23 @@ def test_nchw_to_nhwc_bf16_exact(shape):
     assert y.shape[1] % 8 == 0 and y.is_contiguous(memory_format=CL)
     assert torch.equal(y[:, :C].float(), x.to(BF).float())
     assert not y[:, C:].float().any()
+
+
+@pytest.mark.parametrize("P,K,C,bias", [(16384, 1000, 1024, True), (300, 2048, 512, False), (4096, 4096, 1024, False)])
+def test_gemm_shaped_wgrad_on_nt_kernel_matches_fp32(P, K, C, bias):
+    """Large 1x1 / Linear weight gradients run as an NT MFMA GEMM over transposed operands with an fp32
+    accumulating epilogue (ops/conv.gemm_wgrad_nt); compare against the fp32 torch product."""
+    from bigdl_amd.ops import conv as cv
+
+    torch.manual_seed(0)
+    dy = torch.randn(P, K, device="cuda").to(torch.bfloat16)
+    x = torch.randn(P, C, device="cuda").to(torch.bfloat16)
+    dw = torch.randn(K, C, 1, 1, device="cuda")
+    db = torch.randn(K, device="cuda") if bias else None
+    ref = dw.view(K, C) + dy.float().t() @ x.float()
+    refb = db + dy.float().sum(0) if bias else None
+    cv.conv2d_wgrad(dy.view(P, K, 1, 1), x.view(P, C, 1, 1), dw, db, (1, 1), (0, 0))
+    err = ((dw.view(K, C) - ref).norm() / ref.norm()).item()
+    assert err < 1e-3, err
+    if bias:
+        assert torch.allclose(db, refb, rtol=1e-3, atol=1e-2)
