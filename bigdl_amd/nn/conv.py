@@ -20,6 +20,7 @@ import torch.nn.functional as F
 from .. import ops
 from ..ops import bn as bnops
 from ..ops import conv as cv
+from ..ops import conv_fn
 from .abstractnn import AutogradModule, TensorModule
 from .init_methods import RandomUniform, Zeros
 
@@ -360,6 +361,9 @@ class SpatialFullConvolution(AutogradModule):
         else:  # Table(input, sizeTensor)
             x = x[1]
             adj = (self.adjH, self.adjW)
+        if x.is_cuda and self.nGroup == 1:     # the native data-gradient kernel (ops/conv_fn.py)
+            return conv_fn.conv_transpose2d(x.float(), self.weight, self.bias, (self.dH, self.dW),
+                                            (self.padH, self.padW), adj)
         return F.conv_transpose2d(x.to(self.weight.dtype), self.weight, self.bias, (self.dH, self.dW),
                                   (self.padH, self.padW), adj, self.nGroup)
 
@@ -388,7 +392,7 @@ class SpatialSeparableConvolution(AutogradModule):
         if self.dataFormat == "NHWC":
             x = x.permute(0, 3, 1, 2)
         y = F.conv2d(x.to(self.depthWeight.dtype), self.depthWeight, None, self.s, self.p, groups=self.cin)
-        y = F.conv2d(y, self.pointWeight, self.bias)
+        y = conv_fn.conv2d(y, self.pointWeight, self.bias)        # pointwise half on the MFMA GEMM
         return y.permute(0, 2, 3, 1) if self.dataFormat == "NHWC" else y
 
 
@@ -429,7 +433,7 @@ class SpatialConvolutionMap(AutogradModule):
         idx_o = self.connTable[:, 1].to(self.weight.device) - 1
         idx_i = self.connTable[:, 0].to(self.weight.device) - 1
         W = W.index_put((idx_o, idx_i), self.weight)
-        return F.conv2d(x.to(W.dtype), W, self.bias, (self.dH, self.dW), (self.padH, self.padW))
+        return conv_fn.conv2d(x.to(W.dtype), W, self.bias, (self.dH, self.dW), (self.padH, self.padW))
 
 
 class VolumetricConvolution(AutogradModule):
@@ -459,7 +463,9 @@ class VolumetricConvolution(AutogradModule):
             p = 0
         else:
             p = self.p
-        return F.conv3d(x.to(self.weight.dtype), self.weight, self.bias, self.s, p)
+        if isinstance(p, int):
+            p = (p, p, p)
+        return conv_fn.conv3d(x.to(self.weight.dtype), self.weight, self.bias, self.s, p)
 
 
 class VolumetricFullConvolution(AutogradModule):
@@ -505,7 +511,7 @@ class TemporalConvolution(AutogradModule):
         if squeeze:
             x = x.unsqueeze(0)
         w = self.weight.view(self.outputFrameSize, self.kernelW, self.inputFrameSize).permute(0, 2, 1)
-        y = F.conv1d(x.to(w.dtype).transpose(1, 2), w, self.bias, self.strideW).transpose(1, 2)
+        y = conv_fn.conv1d(x.to(w.dtype).transpose(1, 2), w, self.bias, self.strideW).transpose(1, 2)
         return y.squeeze(0) if squeeze else y
 
 

@@ -1,0 +1,70 @@
+"""Conv-family layers on the native implicit-GEMM kernels (ops/conv_fn.py) vs the fp32 CPU engine: transposed,
+temporal, connection-table, separable (pointwise half) and volumetric convolution, forward and all gradients."""
+import copy
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    a, b = a.float().cpu(), b.float().cpu()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+def _case(name):
+    from bigdl_amd import nn
+
+    if name == "full":
+        return nn.SpatialFullConvolution(12, 20, 3, 3, 2, 2, 1, 1, 1, 1), (2, 12, 9, 9)
+    if name == "full_nopad":
+        return nn.SpatialFullConvolution(8, 16, 4, 4, 2, 2, 0, 0), (3, 8, 7, 6)
+    if name == "temporal":
+        return nn.TemporalConvolution(24, 40, 3, 2), (4, 17, 24)
+    if name == "map":
+        return nn.SpatialConvolutionMap(nn.SpatialConvolutionMap.full(6, 10), 3, 3, 1, 1, 1, 1), (2, 6, 11, 11)
+    if name == "separable":
+        return nn.SpatialSeparableConvolution(8, 24, 2, 3, 3, 1, 1, 1, 1), (2, 8, 10, 10)
+    if name == "volumetric":
+        return nn.VolumetricConvolution(6, 16, 3, 3, 3, 1, 2, 2, 1, 1, 1), (2, 6, 7, 9, 9)
+    raise KeyError(name)
+
+
+@pytest.mark.parametrize("name", ["full", "full_nopad", "temporal", "map", "separable", "volumetric"])
+def test_conv_family_native_matches_cpu(name):
+    from bigdl_amd.utils.random_generator import RNG
+
+    RNG.setSeed(5)
+    cpu, shape = _case(name)
+    gpu = copy.deepcopy(cpu).to("cuda")
+    x = torch.randn(*shape).to(torch.bfloat16).float()
+    yc = cpu.forward(x)
+    yg = gpu.forward(x.cuda())
+    assert yg.shape == yc.shape
+    assert _rel(yg, yc) < 1e-2, _rel(yg, yc)
+    gy = torch.randn_like(yc)
+    gc = cpu.backward(x, gy)
+    gg = gpu.backward(x.cuda(), gy.cuda())
+    assert _rel(gg, gc) < 2e-2, _rel(gg, gc)
+    for a, b in zip(gpu.parameters()[1], cpu.parameters()[1]):
+        assert _rel(a, b) < 2e-2, (a.shape, _rel(a, b))
+
+
+def test_conv_family_uses_no_vendor_conv(monkeypatch):
+    """The GPU path must not reach torch's (MIOpen) convolutions for these layers."""
+    import torch.nn.functional as F
+
+    def boom(*a, **k):
+        raise AssertionError("vendor convolution called on the GPU path")
+
+    for fn in ("conv2d", "conv1d", "conv3d", "conv_transpose2d"):
+        monkeypatch.setattr(F, fn, boom)
+    from bigdl_amd.utils.random_generator import RNG
+
+    RNG.setSeed(1)
+    for name in ("full", "temporal", "map", "volumetric"):
+        m, shape = _case(name)
+        m = m.to("cuda")
+        y = m.forward(torch.randn(*shape, device="cuda"))
+        m.backward(torch.randn(*shape, device="cuda"), torch.ones_like(y))
