@@ -492,6 +492,29 @@ void lstm_bwd_step(const Tensor& WT16, const OptT& dg16_next, const OptT& dout, 
                       ldg, mbf(dg16_out, "dg16_out"), B, H, stream());
 }
 
+void layernorm_fwd(const Tensor& x, const OptT& g, const OptT& b, const Tensor& y, const Tensor& mean,
+                   const Tensor& rstd, double eps) {
+  TORCH_CHECK(x.is_contiguous() && y.is_contiguous() && x.numel() == y.numel() && x.dim() >= 1, "layernorm_fwd: x/y");
+  const int64_t D = x.size(-1), rows = x.numel() / D;
+  TORCH_CHECK(mean.numel() == rows && rstd.numel() == rows, "layernorm_fwd: mean/rstd must hold one value per row");
+  if (g && g->defined()) TORCH_CHECK(g->numel() == D && g->is_contiguous(), "layernorm_fwd: gamma");
+  if (b && b->defined()) TORCH_CHECK(b->numel() == D && b->is_contiguous(), "layernorm_fwd: beta");
+  TORCH_CHECK(bigdl_layernorm_fwd(cf(x, "x"), ocf(g, "g"), ocf(b, "b"), mf(y, "y"), mf(mean, "mean"), mf(rstd, "rstd"),
+                                  rows, (int)D, (float)eps, stream()) == 0, "layernorm_fwd: hidden size > 4096");
+}
+void layernorm_bwd(const Tensor& dy, const Tensor& x, const OptT& g, const Tensor& mean, const Tensor& rstd,
+                   const OptT& dx, const OptT& dg, const OptT& db) {
+  TORCH_CHECK(dy.is_contiguous() && x.is_contiguous() && dy.numel() == x.numel(), "layernorm_bwd: dy/x");
+  const int64_t D = x.size(-1), rows = x.numel() / D;
+  TORCH_CHECK(mean.numel() == rows && rstd.numel() == rows, "layernorm_bwd: mean/rstd");
+  if (dx && dx->defined()) TORCH_CHECK(dx->is_contiguous() && dx->numel() == x.numel(), "layernorm_bwd: dx");
+  if (g && g->defined()) TORCH_CHECK(g->numel() == D, "layernorm_bwd: gamma");
+  if (dg && dg->defined()) TORCH_CHECK(dg->numel() == D && dg->is_contiguous(), "layernorm_bwd: dgamma");
+  if (db && db->defined()) TORCH_CHECK(db->numel() == D && db->is_contiguous(), "layernorm_bwd: dbeta");
+  TORCH_CHECK(bigdl_layernorm_bwd(cf(dy, "dy"), cf(x, "x"), ocf(g, "g"), cf(mean, "mean"), cf(rstd, "rstd"),
+                                  omf(dx, "dx"), omf(dg, "dg"), omf(db, "db"), rows, (int)D, stream()) == 0,
+              "layernorm_bwd: hidden size > 4096");
+}
 void colsum_bf16(const Tensor& x, const Tensor& out) {
   TORCH_CHECK(x.dim() == 2 && x.is_contiguous() && x.size(1) % 8 == 0, "colsum_bf16: x must be [P, K] contiguous, K % 8 == 0");
   TORCH_CHECK(out.is_contiguous() && out.numel() == x.size(1), "colsum_bf16: out must hold K floats");
@@ -598,6 +621,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("lstm_fwd_step", &lstm_fwd_step);
   m.def("lstm_bwd_step", &lstm_bwd_step);
   m.def("colsum_bf16", &colsum_bf16);
+  m.def("layernorm_fwd", &layernorm_fwd);
+  m.def("layernorm_bwd", &layernorm_bwd);
   m.def("gru_step", &gru_step, py::arg("mode"), py::arg("A"), py::arg("W"), py::arg("B"), py::arg("H"),
         py::arg("xg") = py::none(), py::arg("hprev") = py::none(), py::arg("r") = py::none(), py::arg("z") = py::none(),
         py::arg("n") = py::none(), py::arg("rh16") = py::none(), py::arg("hout") = py::none(),

@@ -182,4 +182,10 @@ typedef struct {
   uint16_t* dn16; uint16_t* drz16; float* dh0;
 } GruStepArgs;
 int bigdl_gru_step(const GruStepArgs* a, hipStream_t st);
+
+// Layer normalisation over the last dimension (csrc/layernorm.hip), D <= 4096, fp32 rows.
+int bigdl_layernorm_fwd(const float* x, const float* g, const float* b, float* y, float* mean, float* rstd, long rows,
+                        int D, float eps, hipStream_t st);
+int bigdl_layernorm_bwd(const float* dy, const float* x, const float* g, const float* mean, const float* rstd,
+                        float* dx, float* dg, float* db, long rows, int D, hipStream_t st);
 }

@@ -68,3 +68,23 @@ def test_conv_family_uses_no_vendor_conv(monkeypatch):
         m = m.to("cuda")
         y = m.forward(torch.randn(*shape, device="cuda"))
         m.backward(torch.randn(*shape, device="cuda"), torch.ones_like(y))
+
+
+@pytest.mark.parametrize("shape", [(4, 7, 512), (33, 1000), (2, 3, 4096), (5, 96)])
+def test_layernorm_native_matches_fp32(shape):
+    from bigdl_amd.ops.norm import layer_norm
+
+    torch.manual_seed(0)
+    D = shape[-1]
+    x = torch.randn(*shape) * 3 + 1
+    g, b = torch.randn(D), torch.randn(D)
+    dy = torch.randn(*shape)
+    leaves = [t.clone().requires_grad_(True) for t in (x, g, b)]
+    ref = torch.nn.functional.layer_norm(leaves[0], (D,), leaves[1], leaves[2], 1e-6)
+    ref.backward(dy)
+    dev = [t.cuda().requires_grad_(True) for t in (x, g, b)]
+    y = layer_norm(dev[0], dev[1], dev[2], 1e-6)
+    y.backward(dy.cuda())
+    assert _rel(y, ref) < 1e-5
+    for a, r in zip(dev, leaves):
+        assert _rel(a.grad, r.grad) < 1e-4
