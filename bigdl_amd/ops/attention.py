@@ -1,7 +1,8 @@
 """Scaled-dot-product attention core: softmax(q k^T + bias) v over [B, heads, L, depth] tensors.
 
 Reference: the MM(transB) -> CAddTable(bias) -> SoftMax -> Dropout -> MM chain of S/nn/Attention.scala:90-103.
-Math path (CPU engine, and any shape the fused kernel does not cover): explicit GEMMs + softmax under autograd
+GPU engine: the fused flash kernel (ops/flash_attention.py -> csrc/attention.hip) for head dims 64 / 128.
+Math path (CPU engine, attention dropout, other head dims): explicit GEMMs + softmax under autograd
 (q is pre-scaled by depth^-0.5 as in SplitHeads(mul=true), Attention.scala:256-275).
 """
 import torch
@@ -10,12 +11,14 @@ from . import native
 
 
 def _flash_ok(q, k, v, bias, dropout_p):
+    """The fused kernel (csrc/attention.hip) covers head dims 64 / 128 without attention dropout; a bias that
+    needs a gradient (anything but a constant mask) keeps the math path."""
     if not q.is_cuda or dropout_p > 0.0:
         return False
-    if not native.available() or not hasattr(native.get(), "flash_attn_fwd"):
+    if bias is not None and bias.requires_grad and not getattr(bias, "_bigdl_mask", True):
         return False
     d = q.shape[-1]
-    return d in (64, 128) and q.shape[-2] >= 1 and k.shape[-2] >= 1
+    return d in (64, 128) and q.shape[-2] >= 1 and k.shape[-2] >= 1 and (bias is None or bias.dim() <= 4)
 
 
 def attention_math(q, k, v, bias=None, dropout_p=0.0, training=False):

@@ -515,6 +515,48 @@ void layernorm_bwd(const Tensor& dy, const Tensor& x, const OptT& g, const Tenso
                                   omf(dx, "dx"), omf(dg, "dg"), omf(db, "db"), rows, (int)D, stream()) == 0,
               "layernorm_bwd: hidden size > 4096");
 }
+AttnCall attn_call(const Tensor& q, const Tensor& k, const Tensor& v, const OptT& bias, int64_t H, bool causal) {
+  TORCH_CHECK(q.dim() == 3 && k.dim() == 3 && v.dim() == 3, "attention: q/k/v must be [B*H, L, D]");
+  TORCH_CHECK(q.is_contiguous() && k.is_contiguous() && v.is_contiguous(), "attention: contiguous q/k/v");
+  TORCH_CHECK(k.sizes() == v.sizes() && q.size(0) == k.size(0) && q.size(2) == k.size(2), "attention: shapes");
+  AttnCall c{};
+  c.q = cbf(q, "q"); c.k = cbf(k, "k"); c.v = cbf(v, "v");
+  c.BH = (int)q.size(0); c.H = (int)H; c.Lq = (int)q.size(1); c.Lk = (int)k.size(1); c.D = (int)q.size(2);
+  TORCH_CHECK(c.D == 64 || c.D == 128, "attention: head dim must be 64 or 128");
+  TORCH_CHECK(H > 0 && c.BH % H == 0, "attention: heads");
+  c.causal = causal ? 1 : 0;
+  if (bias && bias->defined()) {
+    TORCH_CHECK(bias->dim() == 4, "attention: bias must be 4-D (broadcast over batch, head, query, key)");
+    const int64_t B = c.BH / H;
+    TORCH_CHECK((bias->size(0) == B || bias->size(0) == 1) && (bias->size(1) == H || bias->size(1) == 1) &&
+                (bias->size(2) == c.Lq || bias->size(2) == 1) && (bias->size(3) == c.Lk || bias->size(3) == 1),
+                "attention: bias not broadcastable to [B, H, Lq, Lk]");
+    c.bias = cf(*bias, "bias");
+    c.sb = bias->size(0) == 1 ? 0 : bias->stride(0); c.sh = bias->size(1) == 1 ? 0 : bias->stride(1);
+    c.sq = bias->size(2) == 1 ? 0 : bias->stride(2); c.sk = bias->size(3) == 1 ? 0 : bias->stride(3);
+  }
+  return c;
+}
+void attn_fwd(const Tensor& q, const Tensor& k, const Tensor& v, const OptT& bias, int64_t H, bool causal,
+              const Tensor& o, const Tensor& lse) {
+  AttnCall c = attn_call(q, k, v, bias, H, causal);
+  TORCH_CHECK(o.is_contiguous() && o.numel() == q.numel() && lse.numel() == (int64_t)c.BH * c.Lq, "attn_fwd: o/lse");
+  c.o = mf(o, "o"); c.lse = mf(lse, "lse");
+  TORCH_CHECK(bigdl_attn_fwd(&c, stream()) == 0, "attn_fwd: unsupported shape");
+}
+void attn_bwd(const Tensor& q, const Tensor& k, const Tensor& v, const OptT& bias, int64_t H, bool causal,
+              const Tensor& o, const Tensor& lse, const Tensor& dout, const Tensor& dq, const Tensor& dk,
+              const Tensor& dv, const Tensor& delta_ws) {
+  AttnCall c = attn_call(q, k, v, bias, H, causal);
+  TORCH_CHECK(o.is_contiguous() && dout.is_contiguous() && o.numel() == q.numel() && dout.numel() == q.numel(),
+              "attn_bwd: o/dout");
+  TORCH_CHECK(dq.is_contiguous() && dq.numel() == q.numel() && dk.numel() == k.numel() && dv.numel() == v.numel() &&
+              dk.is_contiguous() && dv.is_contiguous(), "attn_bwd: gradient buffers");
+  TORCH_CHECK(lse.numel() == (int64_t)c.BH * c.Lq && delta_ws.numel() == (int64_t)c.BH * c.Lq, "attn_bwd: lse/delta");
+  c.o = mf(o, "o"); c.lse = mf(lse, "lse"); c.dout = cf(dout, "dout");
+  c.dq = mf(dq, "dq"); c.dk = mf(dk, "dk"); c.dv = mf(dv, "dv");
+  TORCH_CHECK(bigdl_attn_bwd(&c, mf(delta_ws, "delta"), stream()) == 0, "attn_bwd: unsupported shape");
+}
 void colsum_bf16(const Tensor& x, const Tensor& out) {
   TORCH_CHECK(x.dim() == 2 && x.is_contiguous() && x.size(1) % 8 == 0, "colsum_bf16: x must be [P, K] contiguous, K % 8 == 0");
   TORCH_CHECK(out.is_contiguous() && out.numel() == x.size(1), "colsum_bf16: out must hold K floats");
@@ -622,6 +664,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("lstm_bwd_step", &lstm_bwd_step);
   m.def("colsum_bf16", &colsum_bf16);
   m.def("layernorm_fwd", &layernorm_fwd);
+  m.def("attn_fwd", &attn_fwd);
+  m.def("attn_bwd", &attn_bwd);
   m.def("layernorm_bwd", &layernorm_bwd);
   m.def("gru_step", &gru_step, py::arg("mode"), py::arg("A"), py::arg("W"), py::arg("B"), py::arg("H"),
         py::arg("xg") = py::none(), py::arg("hprev") = py::none(), py::arg("r") = py::none(), py::arg("z") = py::none(),

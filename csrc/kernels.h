@@ -188,4 +188,14 @@ int bigdl_layernorm_fwd(const float* x, const float* g, const float* b, float* y
                         int D, float eps, hipStream_t st);
 int bigdl_layernorm_bwd(const float* dy, const float* x, const float* g, const float* mean, const float* rstd,
                         float* dx, float* dg, float* db, long rows, int D, hipStream_t st);
+
+// Fused attention (csrc/attention.hip). q/k/v bf16 [BH][L][D] (D = 64 or 128), bias fp32 through element strides
+// (sb, sh, sq, sk) or nullptr, o / dq / dk / dv / dout fp32, lse / delta fp32 [BH][Lq].
+typedef struct {
+  const uint16_t* q; const uint16_t* k; const uint16_t* v; const float* bias; long sb, sh, sq, sk;
+  float* o; float* lse; const float* dout; const float* delta; float* dq; float* dk; float* dv;
+  int BH, H, Lq, Lk, D, causal;
+} AttnCall;
+int bigdl_attn_fwd(const AttnCall* c, hipStream_t st);
+int bigdl_attn_bwd(const AttnCall* c, float* delta_ws, hipStream_t st);
 }

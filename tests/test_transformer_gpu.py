@@ -29,3 +29,39 @@ def test_transformer_lm_gpu_matches_cpu():
     wc = torch.cat([g.reshape(-1) for g in cpu.parameters()[1]])
     wg = torch.cat([g.float().cpu().reshape(-1) for g in gpu.parameters()[1]])
     assert _rel(wg, wc) < 5e-2
+
+
+@pytest.mark.parametrize("B,H,Lq,Lk,D,mode", [(2, 4, 128, 128, 64, "none"), (1, 2, 100, 77, 128, "pad"),
+                                              (2, 2, 130, 130, 64, "causal"), (3, 1, 64, 200, 128, "full"),
+                                              (1, 8, 1, 50, 64, "pad")])
+def test_fused_attention_matches_fp32(B, H, Lq, Lk, D, mode):
+    """csrc/attention.hip forward and backward vs the fp32 softmax(q k^T + bias) v reference."""
+    from bigdl_amd.ops.flash_attention import flash_attention
+
+    torch.manual_seed(0)
+    q = (torch.randn(B, H, Lq, D) * D ** -0.5).to(torch.bfloat16).float()
+    k = torch.randn(B, H, Lk, D).to(torch.bfloat16).float()
+    v = torch.randn(B, H, Lk, D).to(torch.bfloat16).float()
+    bias, causal = None, False
+    if mode == "pad":
+        bias = torch.zeros(B, 1, 1, Lk)
+        bias[..., Lk - Lk // 4:] = -1e9
+    elif mode == "full":
+        bias = torch.randn(B, H, Lq, Lk)
+    elif mode == "causal":
+        causal = True
+    leaves = [t.clone().double().requires_grad_(True) for t in (q, k, v)]
+    s = leaves[0] @ leaves[1].transpose(-1, -2)
+    if bias is not None:
+        s = s + bias.double()
+    if causal:
+        s = s + torch.triu(torch.full((Lq, Lk), -1e9, dtype=torch.float64), 1)
+    ref = torch.softmax(s, -1) @ leaves[2]
+    go = torch.randn_like(ref)
+    ref.backward(go)
+    dev = [t.cuda().requires_grad_(True) for t in (q, k, v)]
+    o = flash_attention(dev[0], dev[1], dev[2], bias.cuda() if bias is not None else None, causal)
+    o.backward(go.float().cuda())
+    assert _rel(o, ref) < 1e-2, _rel(o, ref)
+    for d, r in zip(dev, leaves):
+        assert _rel(d.grad, r.grad) < 2e-2, (d.shape, _rel(d.grad, r.grad))
