@@ -22,6 +22,8 @@ reverse sweep instead of T small ones.
 import torch
 import torch.nn.functional as F
 
+from ..ops.conv_fn import linear as _linear
+
 __all__ = ["Cell", "RnnCell", "RNN", "LSTM", "LSTMPeephole", "GRU", "ConvLSTMPeephole", "ConvLSTMPeephole3D", "MultiRNNCell",
            "Recurrent", "RecurrentDecoder", "BiRecurrent", "TimeDistributed"]
 
@@ -163,7 +165,7 @@ class Cell(Container):
         if p is None:
             return x
         if isinstance(p, Linear):
-            return F.linear(x, p.weight, p.bias)
+            return _linear(x, p.weight, p.bias)
         raise ValueError(f"unsupported preTopology {type(p).__name__}")
 
     def step(self, x, hid):
@@ -231,7 +233,7 @@ class RnnCell(Cell):
         self.modules.append(self.h2h)
 
     def step(self, x, hid):
-        h = _act(self.activation)(x + F.linear(hid[0], self.h2h.weight, self.h2h.bias))
+        h = _act(self.activation)(x + _linear(hid[0], self.h2h.weight, self.h2h.bias))
         return h, [h]
 
 
@@ -449,7 +451,7 @@ class LSTM(Cell):
             if self.h2g.bias is not None:
                 hg = hg + self.h2g.bias
             return x + hg
-        return x + F.linear(h, self.h2g.weight, self.h2g.bias)
+        return x + _linear(h, self.h2g.weight, self.h2g.bias)
 
     def step(self, x, hid):
         h, c = hid
@@ -485,7 +487,7 @@ class LSTMPeephole(Cell):
     def step(self, x, hid):
         h, c = hid
         H = self.hiddenSize
-        g = x + F.linear(h, self.h2g.weight)
+        g = x + _linear(h, self.h2g.weight)
         i = torch.sigmoid(g[:, :H] + self.peepI.weight * c)
         f = torch.sigmoid(g[:, H:2 * H] + self.peepF.weight * c)
         gg = torch.tanh(g[:, 2 * H:3 * H])
@@ -521,9 +523,9 @@ class GRU(Cell):
         h = hid[0]
         H = self.outputSize
         sig, act = _act(self.innerActivation), _act(self.activation)
-        rz = sig(x[:, :2 * H] + F.linear(self._drop(h), self.h2g.weight))
+        rz = sig(x[:, :2 * H] + _linear(self._drop(h), self.h2g.weight))
         r, z = rz[:, :H], rz[:, H:]
-        n = act(x[:, 2 * H:] + F.linear(self._drop(r * h), self.h2n.weight))
+        n = act(x[:, 2 * H:] + _linear(self._drop(r * h), self.h2n.weight))
         h2 = (1 - z) * n + z * h
         return h2, [h2]
 

@@ -22,6 +22,8 @@ import math
 import torch
 import torch.nn.functional as F
 
+from ..ops.conv_fn import linear as _linear
+
 from ..ops.attention import attention as attention_core
 from ..utils.table import Table
 from .abstractnn import AbstractModule, TensorModule
@@ -173,9 +175,9 @@ class Attention(Container):
         return t.view(B, L, self.numHeads, self.hiddenSize // self.numHeads).transpose(1, 2)
 
     def _forward(self, x, y, bias, cache, causal):
-        q = F.linear(x, self.queryLayer.weight)
-        k = F.linear(y, self.keyLayer.weight)
-        v = F.linear(y, self.valueLayer.weight)
+        q = _linear(x, self.queryLayer.weight)
+        k = _linear(y, self.keyLayer.weight)
+        v = _linear(y, self.valueLayer.weight)
         if cache is not None:
             kn, vn = self.getName() + "_k", self.getName() + "_v"
             ck, cv = cache.get(kn), cache.get(vn)
@@ -191,7 +193,7 @@ class Attention(Container):
                            dropout_p=1.0 - self.attentionDropout, training=self.train, causal=causal)
         B, _, L, _ = o.shape
         o = o.transpose(1, 2).reshape(B, L, self.hiddenSize)
-        return F.linear(o, self.outputLayer.weight)
+        return _linear(o, self.outputLayer.weight)
 
     def updateOutput(self, input):
         x, y, b = input[1], input[2], input[3]

@@ -135,6 +135,17 @@ def conv_transpose2d(x, w, b=None, stride=(1, 1), pad=(0, 0), adj=(0, 0)):
     return _ConvT2d.apply(x, w, b, tuple(stride), tuple(pad), tuple(adj))
 
 
+def linear(x, w, b=None):
+    """y = x W^T + b over the last dimension on the MFMA GEMM kernels (a 1x1 convolution over the rows): the
+    projections of layers written as autograd functions (attention, generic recurrent cells). CPU: torch."""
+    if not x.is_cuda:
+        return F.linear(x, w, b)
+    lead = x.shape[:-1]
+    rows = x.reshape(-1, x.shape[-1])
+    y = conv2d(rows.view(rows.shape[0], rows.shape[1], 1, 1), w.view(w.shape[0], w.shape[1], 1, 1), b)
+    return y.view(*lead, w.shape[0])
+
+
 def conv1d(x, w, b=None, stride=1):
     """x: [N, C, L], w: [K, C, kW] -> [N, K, L'] as a 2-D convolution over a height-1 image."""
     if not x.is_cuda:
