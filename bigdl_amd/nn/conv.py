@@ -169,9 +169,30 @@ class SpatialConvolution(TensorModule):
         self._geom = (x.shape, ph, pw)
         return y
 
+    def _direct_groups(self):
+        """Groups with <= 16 input channels (depthwise, ResNeXt-style) run the direct grouped kernels
+        (csrc/grouped_conv.hip): one launch per pass for all groups."""
+        return self.nGroup > 1 and self.nInputPlane // self.nGroup <= 16
+
+    def _geo_g(self, ph, pw):
+        return [self.strideH, self.strideW, ph, pw, self.dilationH, self.dilationW, self.nGroup]
+
     def _fwd_gpu_grouped(self, x, ph, pw):
         G = self.nGroup
         cin, cout = self.nInputPlane // G, self.nOutputPlane // G
+        if self._direct_groups():
+            xf = x.float().contiguous()
+            OH = cv.out_size(x.shape[2], self.kernelH, self.strideH, ph, self.dilationH)
+            OW = cv.out_size(x.shape[3], self.kernelW, self.strideW, pw, self.dilationW)
+            y = xf.new_empty(x.shape[0], self.nOutputPlane, OH, OW)
+            ops.native.get().gconv(0, xf, self.weight.float().contiguous(),
+                                   self.bias.float().contiguous() if self.bias is not None else None, y,
+                                   self._geo_g(ph, pw))
+            if self.fuse_relu:
+                y.relu_()
+            self._xf = xf
+            self._geom = (x.shape, ph, pw)
+            return y.to(BF16).contiguous(memory_format=CL)
         outs = []
         w = self.weight
         self._x16 = cv.to_nhwc_bf16(x) if x.shape[1] % 8 == 0 else None
@@ -248,6 +269,11 @@ class SpatialConvolution(TensorModule):
             return gi
         G = self.nGroup
         cin, cout = self.nInputPlane // G, self.nOutputPlane // G
+        if self._direct_groups():
+            gyf = gy.float().contiguous()
+            dx = torch.empty(x.shape[0], self.nInputPlane, x.shape[2], x.shape[3], device=gy.device)
+            ops.native.get().gconv(1, dx, self.weight.float().contiguous(), None, gyf, self._geo_g(ph, pw))
+            return dx.to(BF16).contiguous(memory_format=CL)
         parts = []
         for g in range(G):
             wg = cv.pad_dim(cv.weight_krsc_bf16(self.weight[g * cout:(g + 1) * cout]), 0)
@@ -281,6 +307,17 @@ class SpatialConvolution(TensorModule):
         if x16 is None or x16.shape[0] != x.shape[0] or x16.shape[2:] != x.shape[2:]:
             x16 = cv.to_nhwc_bf16(x)
         st, pd, dl = (self.strideH, self.strideW), (ph, pw), (self.dilationH, self.dilationW)
+        if self.nGroup != 1 and self._direct_groups():
+            xf = getattr(self, "_xf", None)
+            if xf is None or xf.shape != x.shape:
+                xf = x.float().contiguous()
+            dw = torch.zeros(self.weight.shape, device=x.device)
+            db = torch.zeros(self.nOutputPlane, device=x.device) if self.bias is not None else None
+            ops.native.get().gconv(2, xf, dw, db, gy.float().contiguous(), self._geo_g(pd[0], pd[1]))
+            self.gradWeight.add_(dw, alpha=self.scaleW)
+            if db is not None:
+                self.gradBias.add_(db, alpha=self.scaleB)
+            return
         if self.nGroup != 1:
             G = self.nGroup
             cin, cout = self.nInputPlane // G, self.nOutputPlane // G
@@ -391,7 +428,9 @@ class SpatialSeparableConvolution(AutogradModule):
     def fn(self, x):
         if self.dataFormat == "NHWC":
             x = x.permute(0, 3, 1, 2)
-        y = F.conv2d(x.to(self.depthWeight.dtype), self.depthWeight, None, self.s, self.p, groups=self.cin)
+        # depthwise half on the direct grouped kernel, pointwise half on the MFMA GEMM
+        y = conv_fn.group_conv2d(x.to(self.depthWeight.dtype), self.depthWeight, None, self.s, self.p,
+                                 groups=self.cin)
         y = conv_fn.conv2d(y, self.pointWeight, self.bias)        # pointwise half on the MFMA GEMM
         return y.permute(0, 2, 3, 1) if self.dataFormat == "NHWC" else y
 

@@ -146,6 +146,58 @@ def linear(x, w, b=None):
     return y.view(*lead, w.shape[0])
 
 
+class _GroupConv(torch.autograd.Function):
+    """Grouped / depthwise convolution in one launch per pass (csrc/grouped_conv.hip), fp32 NCHW."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, stride, pad, dil, groups):
+        from . import native
+
+        x, w = x.float().contiguous(), w.float().contiguous()
+        N, C, H, W = x.shape
+        K, _, R, S = w.shape
+        OH = (H + 2 * pad[0] - dil[0] * (R - 1) - 1) // stride[0] + 1
+        OW = (W + 2 * pad[1] - dil[1] * (S - 1) - 1) // stride[1] + 1
+        y = x.new_empty(N, K, OH, OW)
+        geo = [stride[0], stride[1], pad[0], pad[1], dil[0], dil[1], groups]
+        native.get().gconv(0, x, w, b.float().contiguous() if b is not None else None, y, geo)
+        ctx.save_for_backward(x, w)
+        ctx.geo, ctx.has_b = geo, b is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        from . import native
+
+        x, w = ctx.saved_tensors
+        gy = gy.float().contiguous()
+        gx = gw = gb = None
+        if ctx.needs_input_grad[0]:
+            gx = torch.empty_like(x)
+            native.get().gconv(1, gx, w, None, gy, ctx.geo)
+        if ctx.needs_input_grad[1] or (ctx.has_b and ctx.needs_input_grad[2]):
+            gw = torch.zeros_like(w)
+            gb = torch.zeros(w.shape[0], device=x.device) if ctx.has_b else None
+            native.get().gconv(2, x, gw, gb, gy, ctx.geo)
+        return gx, gw, gb, None, None, None, None
+
+
+def group_conv2d(x, w, b=None, stride=(1, 1), pad=(0, 0), dil=(1, 1), groups=1):
+    """Grouped convolution: direct kernel when groups carry little reduction depth (depthwise, <= 16 input
+    channels per group), else the implicit-GEMM conv per group writing its channel slice."""
+    if not x.is_cuda:
+        return F.conv2d(x, w, b, stride, pad, dil, groups)
+    if groups == 1:
+        return conv2d(x, w, b, stride, pad, dil)
+    cin_g = x.shape[1] // groups
+    if cin_g <= 16:
+        return _GroupConv.apply(x, w, b, tuple(stride), tuple(pad), tuple(dil), groups)
+    cout_g = w.shape[0] // groups
+    outs = [conv2d(x[:, g * cin_g:(g + 1) * cin_g], w[g * cout_g:(g + 1) * cout_g],
+                   b[g * cout_g:(g + 1) * cout_g] if b is not None else None, stride, pad, dil) for g in range(groups)]
+    return torch.cat(outs, 1)
+
+
 def conv1d(x, w, b=None, stride=1):
     """x: [N, C, L], w: [K, C, kW] -> [N, K, L'] as a 2-D convolution over a height-1 image."""
     if not x.is_cuda:

@@ -557,6 +557,30 @@ void attn_bwd(const Tensor& q, const Tensor& k, const Tensor& v, const OptT& bia
   c.dq = mf(dq, "dq"); c.dk = mf(dk, "dk"); c.dv = mf(dv, "dv");
   TORCH_CHECK(bigdl_attn_bwd(&c, mf(delta_ws, "delta"), stream()) == 0, "attn_bwd: unsupported shape");
 }
+// geo = [stride_h, stride_w, pad_h, pad_w, dil_h, dil_w, groups]
+void gconv(int64_t pass, const Tensor& x_or_dx, const Tensor& w_or_dw, const OptT& b_or_db, const Tensor& y_or_dy,
+           std::vector<int64_t> geo) {
+  TORCH_CHECK(geo.size() == 7, "gconv: geo = [sh, sw, ph, pw, dh, dw, groups]");
+  const Tensor& x = x_or_dx;
+  const Tensor& w = w_or_dw;
+  const Tensor& y = y_or_dy;
+  TORCH_CHECK(x.dim() == 4 && w.dim() == 4 && y.dim() == 4 && x.is_contiguous() && w.is_contiguous() &&
+              y.is_contiguous(), "gconv: contiguous NCHW x / y and KCRS weight");
+  GConvCall c{};
+  c.N = (int)x.size(0); c.C = (int)x.size(1); c.H = (int)x.size(2); c.W = (int)x.size(3);
+  c.K = (int)y.size(1); c.OH = (int)y.size(2); c.OW = (int)y.size(3); c.R = (int)w.size(2); c.S = (int)w.size(3);
+  c.sh = (int)geo[0]; c.sw = (int)geo[1]; c.ph = (int)geo[2]; c.pw = (int)geo[3]; c.dh = (int)geo[4]; c.dw = (int)geo[5];
+  c.G = (int)geo[6];
+  TORCH_CHECK(y.size(0) == c.N && w.size(0) == c.K && c.G > 0 && c.C % c.G == 0 && c.K % c.G == 0 &&
+              w.size(1) == c.C / c.G, "gconv: shapes (weight [K, C/groups, R, S])");
+  TORCH_CHECK((c.OH - 1) * c.sh - c.ph + (c.R - 1) * c.dh < c.H + c.ph + c.sh &&
+              (c.OW - 1) * c.sw - c.pw + (c.S - 1) * c.dw < c.W + c.pw + c.sw, "gconv: output size inconsistent");
+  if (b_or_db && b_or_db->defined()) TORCH_CHECK(b_or_db->numel() == c.K && b_or_db->is_contiguous(), "gconv: bias");
+  if (pass == 0) { c.x = cf(x, "x"); c.w = cf(w, "w"); c.b = ocf(b_or_db, "b"); c.y = mf(y, "y"); }
+  else if (pass == 1) { c.dx = mf(x, "dx"); c.w = cf(w, "w"); c.dy = cf(y, "dy"); }
+  else { c.x = cf(x, "x"); c.dwt = mf(w, "dw"); c.db = omf(b_or_db, "db"); c.dy = cf(y, "dy"); }
+  TORCH_CHECK(bigdl_gconv(&c, (int)pass, stream()) == 0, "gconv: bad geometry");
+}
 void colsum_bf16(const Tensor& x, const Tensor& out) {
   TORCH_CHECK(x.dim() == 2 && x.is_contiguous() && x.size(1) % 8 == 0, "colsum_bf16: x must be [P, K] contiguous, K % 8 == 0");
   TORCH_CHECK(out.is_contiguous() && out.numel() == x.size(1), "colsum_bf16: out must hold K floats");
@@ -665,6 +689,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("colsum_bf16", &colsum_bf16);
   m.def("layernorm_fwd", &layernorm_fwd);
   m.def("attn_fwd", &attn_fwd);
+  m.def("gconv", &gconv);
   m.def("attn_bwd", &attn_bwd);
   m.def("layernorm_bwd", &layernorm_bwd);
   m.def("gru_step", &gru_step, py::arg("mode"), py::arg("A"), py::arg("W"), py::arg("B"), py::arg("H"),

@@ -198,4 +198,12 @@ typedef struct {
 } AttnCall;
 int bigdl_attn_fwd(const AttnCall* c, hipStream_t st);
 int bigdl_attn_bwd(const AttnCall* c, float* delta_ws, hipStream_t st);
+
+// Direct grouped / depthwise convolution, fp32 NCHW (csrc/grouped_conv.hip). pass 0 forward (x, w, b -> y),
+// 1 data gradient (dy, w -> dx), 2 weight / bias gradient (dy, x -> dwt, db accumulated).
+typedef struct {
+  const float* x; const float* w; const float* b; float* y; const float* dy; float* dx; float* dwt; float* db;
+  int N, C, H, W, K, OH, OW, R, S, sh, sw, ph, pw, dh, dw, G;
+} GConvCall;
+int bigdl_gconv(const GConvCall* c, int pass, hipStream_t st);
 }

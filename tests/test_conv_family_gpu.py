@@ -26,12 +26,19 @@ def _case(name):
         return nn.SpatialConvolutionMap(nn.SpatialConvolutionMap.full(6, 10), 3, 3, 1, 1, 1, 1), (2, 6, 11, 11)
     if name == "separable":
         return nn.SpatialSeparableConvolution(8, 24, 2, 3, 3, 1, 1, 1, 1), (2, 8, 10, 10)
+    if name == "grouped":
+        return nn.SpatialConvolution(16, 32, 3, 3, 1, 1, 1, 1, nGroup=4), (2, 16, 12, 12)
+    if name == "depthwise":
+        return nn.SpatialConvolution(24, 48, 3, 3, 2, 2, 1, 1, nGroup=24), (2, 24, 13, 13)
+    if name == "grouped_wide":
+        return nn.SpatialConvolution(64, 64, 3, 3, 1, 1, 1, 1, nGroup=2), (2, 64, 8, 8)
     if name == "volumetric":
         return nn.VolumetricConvolution(6, 16, 3, 3, 3, 1, 2, 2, 1, 1, 1), (2, 6, 7, 9, 9)
     raise KeyError(name)
 
 
-@pytest.mark.parametrize("name", ["full", "full_nopad", "temporal", "map", "separable", "volumetric"])
+@pytest.mark.parametrize("name", ["full", "full_nopad", "temporal", "map", "separable", "volumetric", "grouped",
+                                  "depthwise", "grouped_wide"])
 def test_conv_family_native_matches_cpu(name):
     from bigdl_amd.utils.random_generator import RNG
 
@@ -63,7 +70,7 @@ def test_conv_family_uses_no_vendor_conv(monkeypatch):
     from bigdl_amd.utils.random_generator import RNG
 
     RNG.setSeed(1)
-    for name in ("full", "temporal", "map", "volumetric"):
+    for name in ("full", "temporal", "map", "volumetric", "separable", "grouped", "depthwise"):
         m, shape = _case(name)
         m = m.to("cuda")
         y = m.forward(torch.randn(*shape, device="cuda"))
