@@ -12,6 +12,7 @@
 // [2][C] fp32 stats buffer is all-reduced over RCCL by the Python layer.
 #include "common.h"
 #include "kernels.h"
+#include <stdlib.h>
 
 #define STAT_SLOTS BIGDL_STAT_SLOTS
 
@@ -22,7 +23,7 @@ namespace {
 // MODE 1: bwd       -> out[c] += dy,         out[C+c] += dy*(x-mean)  with dy = dz * (z>0 ? 1 : 0 if z)
 // MODE 1 with z == nullptr and aff != nullptr: the ReLU mask is recomputed from x as x*scale + shift > 0 (the
 // exact fp32 expression of bn_apply_kernel), so the post-ReLU output is never read back (one pass less).
-template <int MODE>
+template <int MODE, int U>
 __global__ __launch_bounds__(256) void chan_reduce_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dz,
                                                           const bf16_t* __restrict__ z, const float* __restrict__ mean,
                                                           float* __restrict__ out, long P, int C, long rows_per_block,
@@ -49,31 +50,45 @@ __global__ __launch_bounds__(256) void chan_reduce_kernel(const bf16_t* __restri
       }
     }
     if (rsub < rpi) {
-      for (long r = rbeg + rsub; r < rend; r += rpi) {
-        const size_t off = (size_t)r * C + g * 8;
-        const v4u vx = *reinterpret_cast<const v4u*>(x + off);
-        if (MODE == 0) {
+      // U rows per trip, all loads issued before the first use: a lane keeps U (x, dz[, z]) granules in flight,
+      // which is what lets a streaming reduction approach HBM bandwidth (one load in flight per lane is
+      // latency-bound at ~2.5 TB/s). Rows past the block end re-read row rbeg and contribute zero.
+      for (long r0 = rbeg + rsub; r0 < rend; r0 += (long)U * rpi) {
+        v4u vx[U], vd[U], vz[U];
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float l = lo_bf(vx[e]), h = hi_bf(vx[e]);
-            a1[2 * e] += l; a1[2 * e + 1] += h;
-            a2[2 * e] += l * l; a2[2 * e + 1] += h * h;
+        for (int u = 0; u < U; ++u) {
+          const long r = r0 + (long)u * rpi;
+          const size_t off = (size_t)(r < rend ? r : rbeg) * C + g * 8;
+          vx[u] = *reinterpret_cast<const v4u*>(x + off);
+          if (MODE == 1) {
+            vd[u] = *reinterpret_cast<const v4u*>(dz + off);
+            if (z) vz[u] = *reinterpret_cast<const v4u*>(z + off);
           }
-        } else {
-          const v4u vd = *reinterpret_cast<const v4u*>(dz + off);
-          v4u vz = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
-          if (z) vz = *reinterpret_cast<const v4u*>(z + off);
+        }
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            float dl = lo_bf(vd[e]), dh = hi_bf(vd[e]);
-            if (z) { if (!(lo_bf(vz[e]) > 0.f)) dl = 0.f; if (!(hi_bf(vz[e]) > 0.f)) dh = 0.f; }
-            if (xmask) {
-              if (!(lo_bf(vx[e]) * sc[2 * e] + sh[2 * e] > 0.f)) dl = 0.f;
-              if (!(hi_bf(vx[e]) * sc[2 * e + 1] + sh[2 * e + 1] > 0.f)) dh = 0.f;
+        for (int u = 0; u < U; ++u) {
+          const bool ok = r0 + (long)u * rpi < rend;
+          if (MODE == 0) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float l = ok ? lo_bf(vx[u][e]) : 0.f, h = ok ? hi_bf(vx[u][e]) : 0.f;
+              a1[2 * e] += l; a1[2 * e + 1] += h;
+              a2[2 * e] += l * l; a2[2 * e + 1] += h * h;
             }
-            a1[2 * e] += dl; a1[2 * e + 1] += dh;
-            a2[2 * e] += dl * (lo_bf(vx[e]) - mu[2 * e]);
-            a2[2 * e + 1] += dh * (hi_bf(vx[e]) - mu[2 * e + 1]);
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              float dl = ok ? lo_bf(vd[u][e]) : 0.f, dh = ok ? hi_bf(vd[u][e]) : 0.f;
+              const float xl = lo_bf(vx[u][e]), xh = hi_bf(vx[u][e]);
+              if (z) { if (!(lo_bf(vz[u][e]) > 0.f)) dl = 0.f; if (!(hi_bf(vz[u][e]) > 0.f)) dh = 0.f; }
+              if (xmask) {
+                if (!(xl * sc[2 * e] + sh[2 * e] > 0.f)) dl = 0.f;
+                if (!(xh * sc[2 * e + 1] + sh[2 * e + 1] > 0.f)) dh = 0.f;
+              }
+              a1[2 * e] += dl; a1[2 * e + 1] += dh;
+              a2[2 * e] += dl * (xl - mu[2 * e]);
+              a2[2 * e + 1] += dh * (xh - mu[2 * e + 1]);
+            }
           }
         }
       }
@@ -93,6 +108,16 @@ __global__ __launch_bounds__(256) void chan_reduce_kernel(const bf16_t* __restri
     }
     __syncthreads();
   }
+}
+
+// Row unroll of the streaming BN passes (BIGDL_BN_UNROLL=1|2|4|8 for A/B runs; default 4).
+int bn_unroll() {
+  static int u = [] {
+    const char* e = getenv("BIGDL_BN_UNROLL");
+    const int v = e ? atoi(e) : 4;
+    return (v == 1 || v == 2 || v == 8) ? v : 4;
+  }();
+  return u;
 }
 
 // Slot sums for one channel by 32 lanes (one slot each) + shuffle reduction: the per-layer finalize / coefficient
@@ -149,6 +174,7 @@ __global__ void bn_finalize_kernel(const float* __restrict__ stats, int nslots, 
 // Channel-stationary mapping (also bn_bwd_apply_kernel): a thread owns one 8-channel group for its whole row
 // range, so its per-channel coefficients are loaded once instead of once per 16-byte granule, and the loop has
 // no 64-bit modulo. blockIdx.y walks channel groups in chunks of 256; rows of a block are [rbeg, rend).
+template <int U>
 __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* __restrict__ x, const float* __restrict__ scale,
                                                        const float* __restrict__ shift, const bf16_t* __restrict__ res,
                                                        bf16_t* __restrict__ y, long P, int C, long rpb, int relu) {
@@ -164,21 +190,30 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* __restrict_
   const v4f b0 = *reinterpret_cast<const v4f*>(shift + c0), b1 = *reinterpret_cast<const v4f*>(shift + c0 + 4);
   const float sc[8] = {s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
   const float sh[8] = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
-  for (long r = rbeg + rsub; r < rend; r += rpi) {
-    const long i = r * G + g;
-    const v4u vx = reinterpret_cast<const v4u*>(x)[i];
-    v4u vr = {0u, 0u, 0u, 0u};
-    if (res) vr = reinterpret_cast<const v4u*>(res)[i];
-    v4u o;
+  for (long r0 = rbeg + rsub; r0 < rend; r0 += (long)U * rpi) {
+    v4u vx[U], vr[U];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      float l = lo_bf(vx[e]) * sc[2 * e] + sh[2 * e];
-      float h = hi_bf(vx[e]) * sc[2 * e + 1] + sh[2 * e + 1];
-      if (res) { l += lo_bf(vr[e]); h += hi_bf(vr[e]); }
-      if (relu) { l = fmaxf(l, 0.f); h = fmaxf(h, 0.f); }
-      o[e] = pack2bf(l, h);
+    for (int u = 0; u < U; ++u) {     // all U rows' loads in flight before the first store
+      const long r = r0 + (long)u * rpi;
+      const long i = (r < rend ? r : rbeg) * G + g;
+      vx[u] = reinterpret_cast<const v4u*>(x)[i];
+      vr[u] = v4u{0u, 0u, 0u, 0u};
+      if (res) vr[u] = reinterpret_cast<const v4u*>(res)[i];
     }
-    reinterpret_cast<v4u*>(y)[i] = o;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long r = r0 + (long)u * rpi;
+      v4u o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float l = lo_bf(vx[u][e]) * sc[2 * e] + sh[2 * e];
+        float h = hi_bf(vx[u][e]) * sc[2 * e + 1] + sh[2 * e + 1];
+        if (res) { l += lo_bf(vr[u][e]); h += hi_bf(vr[u][e]); }
+        if (relu) { l = fmaxf(l, 0.f); h = fmaxf(h, 0.f); }
+        o[e] = pack2bf(l, h);
+      }
+      if (r < rend) reinterpret_cast<v4u*>(y)[r * G + g] = o;
+    }
   }
 }
 
@@ -220,6 +255,7 @@ __device__ __forceinline__ void load8(const float* p, float* v) {
   v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3]; v[4] = b[0]; v[5] = b[1]; v[6] = b[2]; v[7] = b[3];
 }
 
+template <int U>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16_t* __restrict__ dz, const bf16_t* __restrict__ z,
                                                            const bf16_t* __restrict__ x, const float* __restrict__ coef,
                                                            bf16_t* __restrict__ dx, bf16_t* __restrict__ dres, long P,
@@ -241,28 +277,40 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16_t* __restr
     load8(aff + c0, S);
     load8(aff + C + c0, T);
   }
-  for (long r = rbeg + rsub; r < rend; r += rpi) {
-    const long i = r * G + g;
-    const v4u vd = reinterpret_cast<const v4u*>(dz)[i];
-    v4u vz = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
-    if (z) vz = reinterpret_cast<const v4u*>(z)[i];
-    const v4u vx = reinterpret_cast<const v4u*>(x)[i];
-    v4u o, od;
+  for (long r0 = rbeg + rsub; r0 < rend; r0 += (long)U * rpi) {
+    v4u vd[U], vz[U], vx[U];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      float d0 = lo_bf(vd[e]), d1 = hi_bf(vd[e]);
-      if (z) { if (!(lo_bf(vz[e]) > 0.f)) d0 = 0.f; if (!(hi_bf(vz[e]) > 0.f)) d1 = 0.f; }
-      if (xmask) {
-        if (!(lo_bf(vx[e]) * S[2 * e] + T[2 * e] > 0.f)) d0 = 0.f;
-        if (!(hi_bf(vx[e]) * S[2 * e + 1] + T[2 * e + 1] > 0.f)) d1 = 0.f;
-      }
-      const float r0 = A[2 * e] * d0 + B[2 * e] * lo_bf(vx[e]) + D[2 * e];
-      const float r1 = A[2 * e + 1] * d1 + B[2 * e + 1] * hi_bf(vx[e]) + D[2 * e + 1];
-      o[e] = pack2bf(r0, r1);
-      od[e] = pack2bf(d0, d1);
+    for (int u = 0; u < U; ++u) {
+      const long r = r0 + (long)u * rpi;
+      const long i = (r < rend ? r : rbeg) * G + g;
+      vd[u] = reinterpret_cast<const v4u*>(dz)[i];
+      vz[u] = v4u{0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
+      if (z) vz[u] = reinterpret_cast<const v4u*>(z)[i];
+      vx[u] = reinterpret_cast<const v4u*>(x)[i];
     }
-    if (dx) reinterpret_cast<v4u*>(dx)[i] = o;
-    if (dres) reinterpret_cast<v4u*>(dres)[i] = od;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long r = r0 + (long)u * rpi;
+      v4u o, od;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float d0 = lo_bf(vd[u][e]), d1 = hi_bf(vd[u][e]);
+        const float x0 = lo_bf(vx[u][e]), x1 = hi_bf(vx[u][e]);
+        if (z) { if (!(lo_bf(vz[u][e]) > 0.f)) d0 = 0.f; if (!(hi_bf(vz[u][e]) > 0.f)) d1 = 0.f; }
+        if (xmask) {
+          if (!(x0 * S[2 * e] + T[2 * e] > 0.f)) d0 = 0.f;
+          if (!(x1 * S[2 * e + 1] + T[2 * e + 1] > 0.f)) d1 = 0.f;
+        }
+        const float r0v = A[2 * e] * d0 + B[2 * e] * x0 + D[2 * e];
+        const float r1v = A[2 * e + 1] * d1 + B[2 * e + 1] * x1 + D[2 * e + 1];
+        o[e] = pack2bf(r0v, r1v);
+        od[e] = pack2bf(d0, d1);
+      }
+      if (r < rend) {
+        if (dx) reinterpret_cast<v4u*>(dx)[r * G + g] = o;
+        if (dres) reinterpret_cast<v4u*>(dres)[r * G + g] = od;
+      }
+    }
   }
 }
 
@@ -299,8 +347,15 @@ void launch_reduce(int mode, const bf16_t* x, const bf16_t* dz, const bf16_t* z,
   if (blocks < 1) blocks = 1;
   const long rpb = (P + blocks - 1) / blocks;
   blocks = (P + rpb - 1) / rpb;
-  if (mode == 0) chan_reduce_kernel<0><<<(int)blocks, 256, 0, st>>>(x, dz, z, mean, out, P, C, rpb, nullptr);
-  else chan_reduce_kernel<1><<<(int)blocks, 256, 0, st>>>(x, dz, z, mean, out, P, C, rpb, aff);
+#define BN_RED(M, U) chan_reduce_kernel<M, U><<<(int)blocks, 256, 0, st>>>(x, dz, z, mean, out, P, C, rpb, aff)
+  if (mode == 0) aff = nullptr;
+  switch (bn_unroll()) {
+    case 1: if (mode == 0) BN_RED(0, 1); else BN_RED(1, 1); break;
+    case 2: if (mode == 0) BN_RED(0, 2); else BN_RED(1, 2); break;
+    case 8: if (mode == 0) BN_RED(0, 8); else BN_RED(1, 8); break;
+    default: if (mode == 0) BN_RED(0, 4); else BN_RED(1, 4); break;
+  }
+#undef BN_RED
 }
 
 }  // namespace
@@ -329,7 +384,12 @@ void bigdl_bn_apply(const uint16_t* x, const float* scale, const float* shift, c
                     long P, int C, int relu, hipStream_t st) {
   long rpb = 0;
   const dim3 grid = stationary_grid(P, C, &rpb);
-  bn_apply_kernel<<<grid, 256, 0, st>>>(x, scale, shift, res, y, P, C, rpb, relu);
+  switch (bn_unroll()) {
+    case 1: bn_apply_kernel<1><<<grid, 256, 0, st>>>(x, scale, shift, res, y, P, C, rpb, relu); break;
+    case 2: bn_apply_kernel<2><<<grid, 256, 0, st>>>(x, scale, shift, res, y, P, C, rpb, relu); break;
+    case 8: bn_apply_kernel<8><<<grid, 256, 0, st>>>(x, scale, shift, res, y, P, C, rpb, relu); break;
+    default: bn_apply_kernel<4><<<grid, 256, 0, st>>>(x, scale, shift, res, y, P, C, rpb, relu); break;
+  }
   HIP_LAUNCH_CHECK();
 }
 
@@ -348,7 +408,12 @@ void bigdl_bn_bwd_apply(const uint16_t* dz, const uint16_t* z, const uint16_t* x
   if (dx || dres) {
     long rpb = 0;
     const dim3 grid = stationary_grid(P, C, &rpb);
-    bn_bwd_apply_kernel<<<grid, 256, 0, st>>>(dz, z, x, coef, dx, dres, P, C, rpb, aff);
+    switch (bn_unroll()) {
+      case 1: bn_bwd_apply_kernel<1><<<grid, 256, 0, st>>>(dz, z, x, coef, dx, dres, P, C, rpb, aff); break;
+      case 2: bn_bwd_apply_kernel<2><<<grid, 256, 0, st>>>(dz, z, x, coef, dx, dres, P, C, rpb, aff); break;
+      case 8: bn_bwd_apply_kernel<8><<<grid, 256, 0, st>>>(dz, z, x, coef, dx, dres, P, C, rpb, aff); break;
+      default: bn_bwd_apply_kernel<4><<<grid, 256, 0, st>>>(dz, z, x, coef, dx, dres, P, C, rpb, aff); break;
+    }
   }
   HIP_LAUNCH_CHECK();
 }

@@ -421,7 +421,9 @@ __device__ __forceinline__ void glds16(const void* g, LDS_PTR(void) l) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g, l, 16, 0, 0);
 }
 
-template <int BM, int BN, int WM>
+// FASTK = false (Cs % 64 != 0, e.g. the 7x7 stem over 8 padded channels): a K stage spans several taps, so each
+// lane resolves its own granule's tap (kk = k0 + 8 * gsrc) and zero-fills past Kdim.
+template <int BM, int BN, int WM, bool FASTK = true>
 __global__ __launch_bounds__(256, 2) void conv_nt_glds_kernel(ConvArgs a) {
   constexpr int WN = 4 / WM;
   constexpr int TM = BM / WM, TN = BN / WN;
@@ -465,27 +467,39 @@ __global__ __launch_bounds__(256, 2) void conv_nt_glds_kernel(ConvArgs a) {
   for (int i = 0; i < BI; ++i) {
     const int n = n0 + (i * 4 + wave) * 8 + rsub;
     bvalid[i] = n < a.Ncol;
-    wrow[i] = a.wt + (size_t)(bvalid[i] ? n : 0) * a.ldw + gsrc * 8;
+    wrow[i] = a.wt + (size_t)(bvalid[i] ? n : 0) * a.ldw;
   }
 
   auto issue = [&](int kt, int buf) {
     const int k0 = kt * BK;
-    const int t = k0 / a.Cs;
-    const int c = k0 - t * a.Cs + gsrc * 8;
-    const int th = a.tap_h[t], tw = a.tap_w[t];
-    const int wk = a.tap_k[t] * a.Cs + (k0 - t * a.Cs);
+    int th, tw, c, wk;
+    bool kv = true;
+    if constexpr (FASTK) {                  // the whole stage lies in one tap
+      const int t = k0 / a.Cs;
+      c = k0 - t * a.Cs + gsrc * 8;
+      th = a.tap_h[t]; tw = a.tap_w[t];
+      wk = a.tap_k[t] * a.Cs + c;
+    } else {                                // per-lane tap of granule kk
+      const int kk = k0 + gsrc * 8;
+      kv = kk < a.Kdim;
+      const int kc = kv ? kk : 0;
+      const int t = kc / a.Cs;
+      c = kc - t * a.Cs;
+      th = a.tap_h[t]; tw = a.tap_w[t];
+      wk = a.tap_k[t] * a.Cs + c;
+    }
     bf16_t* A = lds + buf * STAGE;
     bf16_t* B = A + BM * BK;
 #pragma unroll
     for (int i = 0; i < AI; ++i) {
       const int ch = a_h[i] + th, cw = a_w[i] + tw;
-      const bool ok = (unsigned)ch < (unsigned)a.Hs && (unsigned)cw < (unsigned)a.Ws;
+      const bool ok = kv && (unsigned)ch < (unsigned)a.Hs && (unsigned)cw < (unsigned)a.Ws;
       const bf16_t* src = ok ? a.src + (unsigned)((a_pix[i] + ch * a.Ws + cw) * a.Cs + c) : g_zero_granule;
       glds16(src, (LDS_PTR(void))(A + (i * 4 + wave) * 8 * BK));
     }
 #pragma unroll
     for (int i = 0; i < BI; ++i) {
-      const bf16_t* src = bvalid[i] ? wrow[i] + wk : g_zero_granule;
+      const bf16_t* src = (bvalid[i] && kv) ? wrow[i] + wk : g_zero_granule;
       glds16(src, (LDS_PTR(void))(B + (i * 4 + wave) * 8 * BK));
     }
   };
@@ -497,7 +511,7 @@ __global__ __launch_bounds__(256, 2) void conv_nt_glds_kernel(ConvArgs a) {
 #pragma unroll
     for (int j = 0; j < NI; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = a.Kdim / BK;
+  const int nk = (a.Kdim + BK - 1) / BK;
   issue(0, 0);
   __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
@@ -1211,10 +1225,16 @@ void launch_nt(const ConvArgs& a, bool fastk, hipStream_t st) {
   else conv_nt_kernel<BM, BN, WM, false><<<grid, block, 0, st>>>(a);
 }
 
-template <int BM, int BN, int WM>
+template <int BM, int BN, int WM, bool FASTK = true>
 void launch_nt_glds(const ConvArgs& a, hipStream_t st) {
   const int nwg = ((a.M + BM - 1) / BM) * ((a.Ncol + BN - 1) / BN);
-  conv_nt_glds_kernel<BM, BN, WM><<<dim3(nwg), dim3(256), 0, st>>>(a);
+  conv_nt_glds_kernel<BM, BN, WM, FASTK><<<dim3(nwg), dim3(256), 0, st>>>(a);
+}
+
+// LDS-DMA path for Cs % 64 != 0 (BIGDL_CONV_GLDS_SLOWK=0 restores the register-staged kernel there)
+static bool glds_slowk() {
+  static int v = [] { const char* e = getenv("BIGDL_CONV_GLDS_SLOWK"); return e ? atoi(e) : 1; }();
+  return v != 0;
 }
 
 template <int BM, int BN, int WM>
@@ -1271,6 +1291,9 @@ int bigdl_conv_nt(const ConvArgs* a, hipStream_t st) {
   } else if (fastk && impl >= 1) {
     if (a->Ncol <= 64) launch_nt_glds<128, 64, 2>(*a, st);
     else launch_nt_glds<128, 128, 2>(*a, st);
+  } else if (!fastk && impl >= 1 && glds_slowk()) {
+    if (a->Ncol <= 64) launch_nt_glds<128, 64, 2, false>(*a, st);
+    else launch_nt_glds<128, 128, 2, false>(*a, st);
   } else if (a->Ncol <= 64) {
     launch_nt<128, 64, 2>(*a, fastk, st);
   } else {

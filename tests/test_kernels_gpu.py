@@ -116,6 +116,36 @@ def test_conv_nt_variants_large(case, impl):
         C_.set_conv_impl(old)
 
 
+WGRAD_CASES = [
+    # N, C, H, K, R, stride, pad: split-K workspace and atomic paths, incl. 64-column layers and the stem
+    (16, 64, 56, 64, 3, 1, 1),
+    (16, 256, 56, 64, 1, 1, 0),
+    (8, 8, 224, 64, 7, 2, 3),
+    (16, 64, 56, 256, 1, 1, 0),
+    (8, 40, 30, 48, 3, 1, 1),       # Ncol < 64 and Kdim tails
+]
+
+
+@pytest.mark.parametrize("case", WGRAD_CASES)
+def test_conv_wgrad_large(case):
+    """Weight gradient (+bias) at ResNet-like sizes (split-K LDS-DMA and atomic kernels) vs fp32 torch."""
+    from bigdl_amd.ops import conv as cv
+
+    N, C, H, K, R, st, pd = case
+    torch.manual_seed(2)
+    dev = _dev()
+    x = torch.randn(N, C, H, H, device=dev).to(BF, memory_format=CL)
+    w = (torch.randn(K, C, R, R, device=dev) * (1.0 / (C * R * R) ** 0.5)).to(BF, memory_format=CL)
+    yr = F.conv2d(x.float(), w.float(), None, stride=st, padding=pd)
+    gy = torch.randn_like(yr).to(BF, memory_format=CL)
+    dw = torch.zeros(K, C, R, R, device=dev).contiguous(memory_format=CL)
+    db = torch.zeros(K, device=dev)
+    cv.conv2d_wgrad(gy, x, dw, db, (st, st), (pd, pd))
+    dwr = torch.nn.grad.conv2d_weight(x.float(), w.shape, gy.float(), stride=st, padding=pd)
+    assert _rel(dw, dwr) < 1e-2
+    assert _rel(db, gy.float().sum(dim=(0, 2, 3))) < 1e-2
+
+
 def test_linear_as_conv1x1():
     from bigdl_amd.ops import conv as cv
 
