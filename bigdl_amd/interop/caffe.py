@@ -538,6 +538,15 @@ def _layer_def(m, name, bottoms, tops):
               "scale_param": [{"bias_term": [m.bias is not None]}],
               "blobs": [tensor_to_blob(b) for b in ([m.weight] + ([m.bias] if m.bias is not None else []))]}
         return [d, sc]
+    elif isinstance(m, (nn.Scale, nn.CMul)) and m.weight.numel() == max(m.weight.shape):
+        # per-channel affine / multiply ([1, C, 1, 1] parameters) as the Caffe Scale layer
+        d["type"] = ["Scale"]
+        has_b = isinstance(m, nn.Scale)
+        d["scale_param"] = [{"bias_term": [has_b]}]
+        blobs = [m.weight.reshape(-1)] + ([m.bias.reshape(-1)] if has_b else [])
+    elif isinstance(m, nn.CAdd) and m.bias.numel() == max(m.bias.shape):
+        d["type"] = ["Bias"]
+        blobs = [m.bias.reshape(-1)]
     elif isinstance(m, nn.JoinTable):
         d["type"] = ["Concat"]
         d["concat_param"] = [{"axis": [m.dimension - 1]}]
@@ -551,6 +560,9 @@ def _layer_def(m, name, bottoms, tops):
     if blobs:
         d["blobs"] = [tensor_to_blob(b) for b in blobs]
     return d
+
+
+_CAFFE_PASSTHROUGH = ("Identity", "Contiguous", "SelectTable", "Echo", "Squeeze", "Unsqueeze", "FlattenTable")
 
 
 def save_caffe(module, prototxtPath, modelPath, overwrite=False, input_shape=None):
@@ -571,7 +583,9 @@ def save_caffe(module, prototxtPath, modelPath, overwrite=False, input_shape=Non
         bottoms = [names[p.id] for p in n.prevs]
         d = _layer_def(n.element, nm, bottoms, [nm])
         if d is None:
-            if len(bottoms) != 1:
+            # only layout / identity layers may vanish from the Caffe net; anything that computes must not be
+            # dropped silently
+            if len(bottoms) != 1 or type(n.element).__name__ not in _CAFFE_PASSTHROUGH:
                 raise ValueError(f"save_caffe: cannot express {n.element.getPrintName()} in Caffe")
             names[n.id] = bottoms[0]            # pass-through (Identity, SelectTable of one input, ...)
             continue

@@ -53,6 +53,7 @@ class SpatialConvolution(TensorModule):
         self.wRegularizer, self.bRegularizer = wRegularizer, bRegularizer
         self.emit_stats = False      # set by nn.fusion when a BatchNorm consumes this conv's output
         self.fuse_relu = False
+        self._fuse_out = self._fuse_addend = None
         self.register_parameter("weight", "gradWeight",
                                 torch.empty(nOutputPlane, nInputPlane // nGroup, kernelH, kernelW))
         if withBias:
@@ -162,8 +163,13 @@ class SpatialConvolution(TensorModule):
         stats = None
         if self.emit_stats and self.train and self.nOutputPlane % 8 == 0:
             stats = bnops.new_stats(self.nOutputPlane, x.device)
+        # inference graph fusion (nn.fusion.fuse_graph_for_inference): output straight into a concat slice
+        # and / or a residual addend summed in the epilogue; set by the graph right before this call
+        out, addend = getattr(self, "_fuse_out", None), getattr(self, "_fuse_addend", None)
+        self._fuse_out = self._fuse_addend = None
         y = cv.conv2d_fwd(x16, w16, self.bias, (self.strideH, self.strideW), (ph, pw),
-                          (self.dilationH, self.dilationW), relu=self.fuse_relu, stats=stats)
+                          (self.dilationH, self.dilationW), relu=self.fuse_relu, stats=stats, out=out,
+                          addend=addend)
         if stats is not None:
             y._bn_stats = stats
         self._geom = (x.shape, ph, pw)

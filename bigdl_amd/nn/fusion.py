@@ -131,3 +131,227 @@ def residual_backward(seq, x, gradOutput):
             first._dgrad_bn_once = _dgrad_bn_enabled()
         g = mods[i].backward(inp, g)
     return g if fold else add_activity(g, gs)
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# Graph-form inference fusion (nn.Graph on the GPU engine: models imported from Caffe / TF / ONNX and every model
+# lowered through the IR by ConversionUtils.convert(model, "dnn")). Reference: the MKL-DNN graph compile
+# (S/nn/mkldnn/DnnGraph.scala:396-409 fusion at compile, Fusion.scala:60-217 conv+relu / conv+sum,
+# JoinTable.scala:54 concat into the consumer's memory). Flags that depend on run-time shapes are decided in
+# per-node hooks that nn.Graph.updateOutput calls right before the node runs (``node.fuse_pre``).
+# ---------------------------------------------------------------------------------------------------------------
+def _graph_users(g):
+    users = {}
+    for n in g.order:
+        for p in n.prevs:
+            users.setdefault(p.id, []).append(n)
+    return users
+
+
+def _conv_fusable(n):
+    m = n.element
+    return (type(m).__name__ in ("SpatialConvolution", "SpatialShareConvolution", "SpatialDilatedConvolution")
+            and isinstance(m, SpatialConvolution) and m.nGroup == 1 and m.format == "NCHW")
+
+
+def _conv_out_shape(conv, x):
+    from ..ops.conv import out_size
+
+    N, _, H, W = x.shape
+    ph, pw = conv._pads(H, W)
+    return (N, conv.nOutputPlane, out_size(H, conv.kernelH, conv.strideH, ph, conv.dilationH),
+            out_size(W, conv.kernelW, conv.strideW, pw, conv.dilationW))
+
+
+def _topo_with_deps(g, extra):
+    """Topological order of ``g`` where node ``k`` also waits for every node in ``extra[k.id]`` (iterative DFS)."""
+    order, state = [], {}
+    for root in list(g.output_nodes) + list(g.inputs_nodes):
+        stack = [(root, False)]
+        while stack:
+            n, done = stack.pop()
+            if done:
+                if state.get(n.id) != 2:
+                    state[n.id] = 2
+                    order.append(n)
+                continue
+            st = state.get(n.id)
+            if st == 2:
+                continue
+            if st == 1:
+                raise ValueError("inference fusion created a cycle")
+            state[n.id] = 1
+            stack.append((n, True))
+            for p in reversed(list(n.prevs) + extra.get(n.id, [])):
+                if state.get(p.id) != 2:
+                    if state.get(p.id) == 1:
+                        raise ValueError("inference fusion created a cycle")
+                    stack.append((p, False))
+    return order
+
+
+class _ResidualLink:
+    """conv -> CAddTable(conv, other) [-> ReLU]: the add (and ReLU) run in the conv's epilogue when ``other`` is
+    a dense bf16 NHWC tensor of the conv's output shape; otherwise every node runs unfused."""
+
+    def __init__(self, conv, other_id, add, idx, relu):
+        self.conv, self.other_id, self.add, self.idx, self.relu = conv, other_id, add, idx, relu
+        self.used = False
+
+    def pre_conv(self, outs, x):
+        import torch
+
+        a = outs[self.other_id]
+        self.used = (isinstance(a, torch.Tensor) and x.is_cuda and a.dtype == torch.bfloat16 and a.dim() == 4
+                     and a.is_contiguous(memory_format=torch.channels_last)
+                     and tuple(a.shape) == _conv_out_shape(self.conv, x))
+        self.conv._fuse_addend = a if self.used else None
+        self.conv.fuse_relu = self.used and self.relu is not None
+
+    def pre_add(self, outs, x):
+        self.add.passthrough = self.used
+        self.add._pass_index = self.idx
+
+    def pre_relu(self, outs, x):
+        self.relu.passthrough = self.used
+
+
+class _ConcatLink:
+    """JoinTable over channels whose conv producers write their channel slice of one NHWC buffer. Widths of the
+    non-producer inputs are read at run time (they are scheduled before the first producer)."""
+
+    def __init__(self, join, prevs, producer_convs):
+        self.join, self.prevs, self.conv_of = join, prevs, producer_convs   # conv_of: prev id -> conv module
+        self.buf = None
+
+    def _width(self, p, outs):
+        c = self.conv_of.get(p.id)
+        return c.nOutputPlane if c is not None else outs[p.id].shape[1]
+
+    def pre_conv(self, pid, outs, x):
+        import torch
+
+        conv = self.conv_of[pid]
+        if not x.is_cuda:
+            return
+        N, K, OH, OW = _conv_out_shape(conv, x)
+        off = 0
+        for p in self.prevs:
+            if p.id == pid:
+                break
+            off += self._width(p, outs)
+        if self.buf is None:
+            ctot = sum(self._width(p, outs) for p in self.prevs)
+            self.buf = torch.empty((N, ctot, OH, OW), dtype=torch.bfloat16, device=x.device,
+                                   memory_format=torch.channels_last)
+        b = self.buf
+        if off % 8 == 0 and b.shape[0] == N and b.shape[2] == OH and b.shape[3] == OW:
+            conv._fuse_out = b[:, off:off + K]
+
+    def pre_join(self, outs, x):
+        self.join._fuse_buf, self.buf = self.buf, None
+
+
+def _chain(hooks):
+    def run(outs, x):
+        for h in hooks:
+            h(outs, x)
+    return run
+
+
+def fuse_graph_for_inference(g):
+    """Compile-time inference fusion of an nn.Graph for the GPU engine:
+
+      ReLU      a ReLU whose only producer is a conv / Linear / BN that feeds nothing else runs in its epilogue
+      residual  CAddTable(conv, other) [-> ReLU]: the conv (single consumer) adds ``other`` in its epilogue and
+                applies the ReLU; the add and the ReLU pass through. ``other`` is scheduled before the conv.
+      concat    JoinTable over channels: convs (through a fused ReLU) that feed only the JoinTable write their
+                channel slice of the concat buffer; the JoinTable copies only its other inputs, which are
+                scheduled before the first producer conv so the buffer's width is known.
+    Inference only: the graph's backward is not valid after this pass (``unfuse_graph`` resets it).
+    """
+    from ..quantized.modules import QuantizedSpatialConvolution
+    from .table_ops import JoinTable
+    from .shape_ops import _bdim
+    import torch
+
+    unfuse_graph(g)
+    users = _graph_users(g)
+    single = lambda n: len(users.get(n.id, [])) == 1  # noqa: E731
+    # ReLU into producer epilogues
+    for n in g.order:
+        if isinstance(n.element, ReLU) and len(n.prevs) == 1:
+            p = n.prevs[0]
+            if isinstance(p.element, (SpatialConvolution, Linear, BatchNormalization, QuantizedSpatialConvolution)) \
+                    and hasattr(p.element, "fuse_relu") and single(p):
+                p.element.fuse_relu = True
+                n.element.passthrough = True
+    hooks, extra = {}, {}
+    res_convs = set()
+    # residual adds into the conv epilogue
+    for n in g.order:
+        m = n.element
+        if not (isinstance(m, CAddTable) and len(n.prevs) == 2 and all(k is None for k in n.prev_index)):
+            continue
+        for ci in (0, 1):
+            c, o = n.prevs[ci], n.prevs[1 - ci]
+            if c is o or not _conv_fusable(c) or not single(c) or c.element.fuse_relu:
+                continue
+            us = users.get(n.id, [])
+            relu_n = us[0] if (len(us) == 1 and isinstance(us[0].element, ReLU) and len(us[0].prevs) == 1) else None
+            link = _ResidualLink(c.element, o.id, m, ci + 1, relu_n.element if relu_n is not None else None)
+            hooks.setdefault(c.id, []).append(link.pre_conv)
+            hooks.setdefault(n.id, []).append(link.pre_add)
+            if relu_n is not None:
+                hooks.setdefault(relu_n.id, []).append(link.pre_relu)
+            extra.setdefault(c.id, []).append(o)
+            res_convs.add(c.id)
+            break
+    # concat written in place by its producer convs
+    for n in g.order:
+        m = n.element
+        if not (isinstance(m, JoinTable) and len(n.prevs) >= 2 and all(k is None for k in n.prev_index)):
+            continue
+        if _bdim(m.dimension, torch.empty((0, 0, 0, 0)), m.nInputDims if m.nInputDims > 0 else None) != 1:
+            continue
+        if len({p.id for p in n.prevs}) != len(n.prevs):
+            continue
+        conv_of, conv_node, dyn = {}, {}, []
+        for p in n.prevs:
+            c = p
+            if isinstance(p.element, ReLU) and p.element.passthrough and len(p.prevs) == 1 and single(p):
+                c = p.prevs[0]
+            if (_conv_fusable(c) and single(c) and c.id not in res_convs and single(p)
+                    and c.element.nOutputPlane % 8 == 0):
+                conv_of[p.id] = c.element
+                conv_node[p.id] = c
+            else:
+                dyn.append(p)
+        if not conv_of:
+            continue
+        link = _ConcatLink(m, list(n.prevs), conv_of)
+        for pid, c in conv_node.items():
+            hooks.setdefault(c.id, []).append(lambda outs, x, _p=pid, _l=link: _l.pre_conv(_p, outs, x))
+            extra.setdefault(c.id, []).extend(dyn)
+        hooks.setdefault(n.id, []).append(link.pre_join)
+    for n in g.order:
+        hs = hooks.get(n.id)
+        n.fuse_pre = _chain(hs) if hs else None
+    if extra:
+        g.order = _topo_with_deps(g, extra)
+        g.modules = [n.element for n in g.order]
+    g._inference_fused = True
+    return g
+
+
+def unfuse_graph(g):
+    """Undo fuse_graph_for_inference / relu planning on an nn.Graph (flags, hooks)."""
+    for n in g.order:
+        n.fuse_pre = None
+        m = n.element
+        for attr, val in (("fuse_relu", False), ("passthrough", False), ("_fuse_out", None),
+                          ("_fuse_addend", None), ("_fuse_buf", None)):
+            if hasattr(m, attr):
+                setattr(m, attr, val)
+    g._inference_fused = False
+    return g

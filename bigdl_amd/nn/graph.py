@@ -151,6 +151,9 @@ class Graph(Container):
         for n in self.order:
             x = self._node_input(n, outs, input)
             self._node_inputs[n.id] = x
+            pre = getattr(n, "fuse_pre", None)   # inference fusion hook (nn.fusion.fuse_graph_for_inference)
+            if pre is not None:
+                pre(outs, x)
             outs[n.id] = n.element.forward(x)
         self._outs = outs
         if len(self.output_nodes) == 1:

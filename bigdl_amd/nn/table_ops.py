@@ -19,8 +19,8 @@ class CAddTable(TensorModule):
         self.passthrough = False    # set by nn.fusion when the residual add is folded into a BatchNorm
 
     def updateOutput(self, input):
-        if self.passthrough:
-            return input[1]
+        if self.passthrough:   # the sum was produced in place by input[_pass_index]'s producer
+            return input[getattr(self, "_pass_index", 1)]
         ts = input.toSeq()
         out = ts[0]
         for t in ts[1:]:
@@ -105,6 +105,18 @@ class JoinTable(TensorModule):
         d = _bdim(self.dimension, ts[0], self.nInputDims if self.nInputDims > 0 else None)
         self._d = d
         self._sizes = [t.shape[d] for t in ts]
+        buf = getattr(self, "_fuse_buf", None)
+        if buf is not None:
+            # concat written in place (nn.fusion.fuse_graph_for_inference): producers already wrote their channel
+            # slices of ``buf``; inputs that did not (e.g. a pooling branch) are copied into theirs
+            self._fuse_buf = None
+            off = 0
+            for t in ts:
+                sl = buf.narrow(d, off, t.shape[d])
+                if t.data_ptr() != sl.data_ptr() or t.stride() != sl.stride():
+                    sl.copy_(t)
+                off += t.shape[d]
+            return buf
         out = torch.cat(ts, dim=d)
         if out.is_cuda and out.dim() == 4:
             out = out.contiguous(memory_format=torch.channels_last)

@@ -66,10 +66,13 @@ def pad_dim(t, dim, mult=8):
     return out
 
 
-def conv2d_fwd(x, w16, bias, stride, pad, dil=(1, 1), relu=False, stats=None, out=None):
-    """y = conv(x, w) + bias (+ReLU); optionally accumulate per-channel (sum, sumsq) of y into ``stats``.
+def conv2d_fwd(x, w16, bias, stride, pad, dil=(1, 1), relu=False, stats=None, out=None, addend=None):
+    """y = conv(x, w) + bias [+ addend] (+ReLU); optionally accumulate per-channel (sum, sumsq) of y into ``stats``.
 
     x: (N, C, H, W) bf16 channels_last (C % 8 == 0); w16: (K, C, R, S) bf16 channels_last.
+    ``out`` may be a channel slice ``buf[:, c0:c0 + K]`` of a channels_last (N, Ctot, OH, OW) buffer (a concat
+    written in place: row stride Ctot); ``addend`` (same shape as y, channels_last) is summed in the epilogue
+    before the ReLU (a residual add).
     """
     N, C, H, W = x.shape
     K, Cw, R, S = w16.shape
@@ -78,10 +81,18 @@ def conv2d_fwd(x, w16, bias, stride, pad, dil=(1, 1), relu=False, stats=None, ou
     ph, pw = pad
     dh, dw = dil
     OH, OW = out_size(H, R, sh, ph, dh), out_size(W, S, sw, pw, dw)
+    ldo = K
     if out is None:
         out = torch.empty((N, K, OH, OW), dtype=BF16, device=x.device, memory_format=CL)
-    native.get().conv_nt(x, w16, out, bias, stats, _fwd_geo(N, H, W, C, OH, OW, sh, sw, R * S * C, K),
-                         _fwd_taps(R, S, ph, pw, dh, dw), relu)
+    else:
+        assert tuple(out.shape) == (N, K, OH, OW) and out.stride(1) == 1, "conv2d_fwd: out must be NHWC (N, K, OH, OW)"
+        ldo = out.stride(3) if OW > 1 else out.stride(2) // max(OW, 1)
+    if addend is not None:
+        assert ldo == K and addend.shape == out.shape and addend.is_contiguous(memory_format=CL), \
+            "conv2d_fwd: a residual addend needs a dense NHWC output"
+    geo = _fwd_geo(N, H, W, C, OH, OW, sh, sw, R * S * C, K)
+    geo[10] = ldo
+    native.get().conv_nt(x, w16, out, bias, stats, geo, _fwd_taps(R, S, ph, pw, dh, dw), relu, addend)
     return out
 
 

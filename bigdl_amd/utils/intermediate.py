@@ -225,19 +225,73 @@ def _fold_bn_into_conv(conv_e, bn_e):
     return new
 
 
+def _channel_affine(e, nout):
+    """(scale, shift) per output channel of a Caffe-style Scale / CMul / CAdd element with a [1, C, 1, 1] (or [C])
+    parameter, or None when the element is not a per-channel affine map over ``nout`` channels."""
+    m = e.module if e.general else e.source
+    if m is None:
+        return None
+    w = getattr(m, "weight", None) if e.op in ("Scale", "CMul") else None
+    b = getattr(m, "bias", None) if e.op in ("Scale", "CAdd") else None
+    out = []
+    for t in (w, b):
+        if t is None:
+            out.append(None)
+            continue
+        t = t.detach().float().cpu()
+        shape = [d for d in t.shape]
+        if t.numel() != nout or (len(shape) == 4 and (shape[0] != 1 or shape[2] != 1 or shape[3] != 1)) \
+                or len(shape) not in (1, 4):
+            return None
+        out.append(t.reshape(nout))
+    if out[0] is None and out[1] is None:
+        return None
+    return (out[0] if out[0] is not None else torch.ones(nout)), (out[1] if out[1] is not None else torch.zeros(nout))
+
+
+def _fold_affine_into_conv(conv_e, scale, shift):
+    """conv -> per-channel affine (Caffe Scale after BatchNorm): W' = W * s, b' = b * s + t."""
+    w = conv_e.weights["weight"]
+    out_ch = w.shape[0]
+    b = conv_e.weights.get("bias")
+    new = IRElement(conv_e.op, conv_e.args, dict(conv_e.kwargs), dict(conv_e.weights), conv_e.name,
+                    attrs=conv_e.attrs)
+    new.weights["weight"] = w * scale.view((out_ch,) + (1,) * (w.dim() - 1))
+    new.weights["bias"] = (b if b is not None else torch.zeros(out_ch)) * scale + shift
+    if len(new.args) > 16:
+        new.args = new.args[:16] + (True,) + new.args[17:]
+    else:
+        new.kwargs["withBias"] = True
+    return new
+
+
 class IRToDnn:
     """GPU-engine lowering with the inference fusion passes."""
 
     CONV = ("SpatialConvolution", "SpatialShareConvolution", "SpatialDilatedConvolution")
+    AFFINE = ("Scale", "CMul", "CAdd")
 
     @staticmethod
-    def fuse(graph):
-        """conv -> BN folding and conv/BN -> ReLU fusion on a copy of the IR (inference only)."""
+    def _nexts(graph):
         nodes = graph.nodes()
         nexts = {n.id: [] for n in nodes}
         for n in nodes:
             for p in n.prevs:
                 nexts[p.id].append(n)
+        return nodes, nexts
+
+    @staticmethod
+    def _replace(graph, nodes, replaced):
+        for n in nodes:
+            n.prevs = [replaced.get(p.id, p) for p in n.prevs]
+        graph.outputs = [replaced.get(o.id, o) for o in graph.outputs]
+
+    @staticmethod
+    def fuse(graph):
+        """conv -> BN folding, then conv -> per-channel affine (Caffe BatchNorm + Scale pairs) folding, on a copy of
+        the IR (inference only). ReLU / residual / concat fusion runs on the built graph
+        (nn.fusion.fuse_graph_for_inference)."""
+        nodes, nexts = IRToDnn._nexts(graph)
         replaced = {}
         for n in nodes:
             e = n.element
@@ -248,33 +302,29 @@ class IRToDnn:
                         and "runningMean" in e.weights):
                     p.element = _fold_bn_into_conv(pe, e)
                     replaced[n.id] = p
-        for n in nodes:
-            n.prevs = [replaced.get(p.id, p) for p in n.prevs]
-        graph.outputs = [replaced.get(o.id, o) for o in graph.outputs]
+        IRToDnn._replace(graph, nodes, replaced)
+        nodes, nexts = IRToDnn._nexts(graph)
+        replaced = {}
+        for n in nodes:      # chains conv -> Scale -> CAdd fold one after the other (nodes are in topo order)
+            e = n.element
+            if e.op in IRToDnn.AFFINE and len(n.prevs) == 1:
+                p = replaced.get(n.prevs[0].id, n.prevs[0])
+                pe = p.element
+                if pe.op in IRToDnn.CONV and not pe.general and len(nexts[n.prevs[0].id]) == 1:
+                    aff = _channel_affine(e, pe.weights["weight"].shape[0])
+                    if aff is not None:
+                        p.element = _fold_affine_into_conv(pe, *aff)
+                        replaced[n.id] = p
+        IRToDnn._replace(graph, nodes, replaced)
         return graph
 
     @staticmethod
     def relu_plan(g):
-        """Set fuse_relu / passthrough flags on a built nn.Graph: a ReLU whose only producer is a conv, Linear or
-        BN that feeds nothing else runs inside that producer's epilogue."""
-        from ..nn.activation import ReLU
-        from ..nn.conv import SpatialConvolution
-        from ..nn.linear import Linear
-        from ..nn.normalization import BatchNormalization
-        from ..quantized.modules import QuantizedSpatialConvolution
+        """Inference fusion of a built nn.Graph for the GPU engine (ReLU into producer epilogues, residual adds and
+        concats in place): see nn.fusion.fuse_graph_for_inference."""
+        from ..nn.fusion import fuse_graph_for_inference
 
-        users = {}
-        for n in g.order:
-            for p in n.prevs:
-                users.setdefault(p.id, []).append(n)
-        for n in g.order:
-            if isinstance(n.element, ReLU) and len(n.prevs) == 1:
-                p = n.prevs[0]
-                if isinstance(p.element, (SpatialConvolution, Linear, BatchNormalization, QuantizedSpatialConvolution)) and \
-                        hasattr(p.element, "fuse_relu") and len(users.get(p.id, [])) == 1:
-                    p.element.fuse_relu = True
-                    n.element.passthrough = True
-        return g
+        return fuse_graph_for_inference(g)
 
 
 class IRConverter:

@@ -69,7 +69,11 @@ void conv_nt(const Tensor& src, const Tensor& wt, const Tensor& out, const OptT&
   }
   TORCH_CHECK(src.numel() >= (int64_t)a.Nb * a.Hs * a.Ws * a.Cs, "conv_nt: src too small");
   TORCH_CHECK(wt.numel() >= (int64_t)(a.Ncol - 1) * a.ldw + (int64_t)(max_tk + 1) * a.Cs, "conv_nt: weight too small");
-  TORCH_CHECK(out.numel() >= ((int64_t)a.Nb * a.OHo * a.OWo - 1) * a.ldo + a.Ncol, "conv_nt: out too small");
+  // `out` may be a channel-slice view of a wider NHWC buffer (concat written in place): bound by its storage
+  const int64_t out_avail = (int64_t)(out.storage().nbytes() / out.element_size()) - out.storage_offset();
+  TORCH_CHECK(a.ldo >= a.Ncol && out_avail >= ((int64_t)a.Nb * a.OHo * a.OWo - 1) * a.ldo + a.Ncol,
+              "conv_nt: out too small");
+  if (a.addend) TORCH_CHECK(a.ldo == a.Ncol, "conv_nt: an addend needs a dense output (ldo == Ncol)");
   TORCH_CHECK((a.OH - 1) * a.omul_h + a.ooff_h < a.OHo && (a.OW - 1) * a.omul_w + a.ooff_w < a.OWo,
               "conv_nt: output placement out of range");
   const int rc = bigdl_conv_nt(&a, stream());

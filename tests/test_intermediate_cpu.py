@@ -53,3 +53,32 @@ def test_container_to_graph_shares_layers():
     g.forward(x)
     gi_g = g.backward(x, gy)
     assert torch.allclose(gi_g, gi_seq, atol=1e-6) and torch.allclose(lin.gradWeight, gw_seq, atol=1e-6)
+
+
+def test_graph_inference_fusion_plan_cpu():
+    """Caffe-style BN + Scale pairs fold into the conv at the IR level; the graph fusion pass schedules a concat's
+    non-conv inputs before its producer convs and the residual shortcut before the residual conv, and the fused
+    graph computes the same function (on the CPU the run-time hooks leave every node unfused)."""
+    import os
+    import sys
+
+    sys.path.insert(0, os.path.dirname(__file__))
+    from test_graph_fusion_gpu import _inception_residual_graph
+
+    from bigdl_amd.nn.fusion import fuse_graph_for_inference
+    from bigdl_amd.utils.intermediate import BlasToIR, IRToDnn
+
+    g = _inception_residual_graph()
+    x = torch.randn(2, 3, 16, 16)
+    ref = g.forward(x).clone()
+    cg = IRToDnn.fuse(BlasToIR.convert(g)).build("blas", train=False)
+    names = [type(n.element).__name__ for n in cg.order]
+    assert "Scale" not in names and "SpatialBatchNormalization" not in names
+    fuse_graph_for_inference(cg)
+    order = [type(n.element).__name__ for n in cg.order]
+    pos = {n.id: i for i, n in enumerate(cg.order)}
+    join = [n for n in cg.order if names and type(n.element).__name__ == "JoinTable"][0]
+    pool = [p for p in join.prevs if type(p.element).__name__ == "SpatialMaxPooling"][0]
+    convs = [n for n in cg.order if n.fuse_pre is not None and type(n.element).__name__ == "SpatialConvolution"]
+    assert convs and all(pos[pool.id] < pos[c.id] for c in convs if c.id != cg.order[1].id), order
+    assert torch.allclose(cg.forward(x), ref, atol=1e-5)
