@@ -154,7 +154,8 @@ class Graph(Container):
             pre = getattr(n, "fuse_pre", None)   # inference fusion hook (nn.fusion.fuse_graph_for_inference)
             if pre is not None:
                 pre(outs, x)
-            outs[n.id] = n.element.forward(x)
+            run = getattr(n, "fuse_run", None)   # planned runner (quantized.int8_graph) replacing forward
+            outs[n.id] = run(x) if run is not None else n.element.forward(x)
         self._outs = outs
         if len(self.output_nodes) == 1:
             return outs[self.output_nodes[0].id]

@@ -147,12 +147,13 @@ def calibrate(model, sample):
     return model
 
 
-def quantize(model, fold_bn=True, calibration=None):
+def quantize(model, fold_bn=True, calibration=None, plan=True):
     """Clone ``model`` and return its int8 inference version (reference Quantization.quantize).
 
     A Graph (e.g. a model imported from Caffe / TF) is first lowered through the engine-neutral IR so BatchNorm
-    folds into the preceding convolution there too. ``calibration`` (a sample input batch) switches the
-    activations to calibrated static ranges (see ``calibrate``)."""
+    (and Caffe Scale) folds into the preceding convolution there too. ``calibration`` (a sample input batch)
+    switches the activations to calibrated static ranges (see ``calibrate``); for a Graph on the GPU it also
+    attaches the static int8 execution plan (``plan``; quantized/int8_graph.py)."""
     from ..utils.intermediate import BlasToIR, IRToDnn
 
     dev = getattr(model, "_device", None)
@@ -169,4 +170,10 @@ def quantize(model, fold_bn=True, calibration=None):
         q.to(dev)
     if isinstance(q, Graph):
         IRToDnn.relu_plan(q)
+        if plan and calibration is not None and dev is not None and dev.type == "cuda":
+            # static int8 execution plan: int8 activations between layers, requantizing epilogues, in-place
+            # concats, int8 pooling (quantized/int8_graph.py)
+            from .int8_graph import plan_int8
+
+            plan_int8(q, calibration.to(dev))
     return q

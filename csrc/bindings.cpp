@@ -271,13 +271,18 @@ void quantize_act(const Tensor& x, const Tensor& q, const Tensor& amax, const Te
                      (int)N, P, (int)C, (int)Cp, static_amax ? 1 : 0, stream());
 }
 
-void conv_i8(const Tensor& src, const Tensor& wt, const Tensor& out, const OptT& bias, const Tensor& xscale,
-             const Tensor& wscale, std::vector<int64_t> geo, std::vector<int64_t> taps, bool relu) {
+// xscale: [N] per-sample scales, or None with xs_const (a static per-tensor scale); out bf16 / fp32 / int8 (int8:
+// requantized with out_scale). `out` may be a channel slice of a wider NHWC buffer (rows geo[10] = ldo apart).
+void conv_i8(const Tensor& src, const Tensor& wt, const Tensor& out, const OptT& bias, const OptT& xscale,
+             const Tensor& wscale, std::vector<int64_t> geo, std::vector<int64_t> taps, bool relu, double xs_const,
+             double out_scale) {
   TORCH_CHECK(geo.size() == 17, "conv_i8: bad geometry");
   TORCH_CHECK(src.scalar_type() == at::kChar && wt.scalar_type() == at::kChar && src.is_cuda() && wt.is_cuda() &&
                   src.is_contiguous() && wt.is_contiguous(), "conv_i8: src/wt must be contiguous int8 device tensors");
-  const bool f32 = out.scalar_type() == at::kFloat;
-  TORCH_CHECK(f32 || out.scalar_type() == at::kBFloat16, "conv_i8: out bf16 or fp32");
+  const int mode = out.scalar_type() == at::kFloat ? 1 : out.scalar_type() == at::kChar ? 2 : 0;
+  TORCH_CHECK(mode != 0 || out.scalar_type() == at::kBFloat16, "conv_i8: out bf16, fp32 or int8");
+  TORCH_CHECK(mode != 2 || out_scale > 0, "conv_i8: int8 output needs out_scale > 0");
+  TORCH_CHECK(out.is_cuda(), "conv_i8: out must be a device tensor");
   TORCH_CHECK(taps.size() % 3 == 0 && !taps.empty() && taps.size() / 3 <= CONV_MAX_TAPS, "conv_i8: bad taps");
   ConvArgs a;
   a.src = reinterpret_cast<const uint16_t*>(src.data_ptr<int8_t>());
@@ -300,11 +305,51 @@ void conv_i8(const Tensor& src, const Tensor& wt, const Tensor& out, const OptT&
   }
   TORCH_CHECK(src.numel() >= (int64_t)a.Nb * a.Hs * a.Ws * a.Cs, "conv_i8: src too small");
   TORCH_CHECK(wt.numel() >= (int64_t)(a.Ncol - 1) * a.ldw + (int64_t)(max_tk + 1) * a.Cs, "conv_i8: weight too small");
-  TORCH_CHECK(out.numel() >= (int64_t)(a.M - 1) * a.ldo + a.Ncol, "conv_i8: out too small");
-  TORCH_CHECK(xscale.numel() >= a.Nb && wscale.numel() >= a.Ncol && xscale.scalar_type() == at::kFloat &&
-                  wscale.scalar_type() == at::kFloat, "conv_i8: scales");
-  const int rc = bigdl_conv_i8(&a, xscale.data_ptr<float>(), wscale.data_ptr<float>(), f32 ? 1 : 0, stream());
+  const int64_t out_avail = (int64_t)(out.storage().nbytes() / out.element_size()) - out.storage_offset();
+  TORCH_CHECK(a.ldo >= a.Ncol && out_avail >= (int64_t)(a.M - 1) * a.ldo + a.Ncol, "conv_i8: out too small");
+  const bool has_xs = xscale && xscale->defined();
+  TORCH_CHECK(!has_xs || (xscale->numel() >= a.Nb && xscale->scalar_type() == at::kFloat && xscale->is_cuda()),
+              "conv_i8: xscale must hold N fp32 scales");
+  TORCH_CHECK(wscale.numel() >= a.Ncol && wscale.scalar_type() == at::kFloat, "conv_i8: wscale");
+  const int rc = bigdl_conv_i8(&a, has_xs ? xscale->data_ptr<float>() : nullptr, (float)xs_const,
+                               wscale.data_ptr<float>(), mode, mode == 2 ? (float)(1.0 / out_scale) : 0.f, stream());
   TORCH_CHECK(rc == 0, "conv_i8: unsupported shape (channels must be a multiple of 16)");
+}
+
+void pool_i8(const Tensor& x, const Tensor& y, std::vector<int64_t> g, bool avg, bool count_pad) {
+  // g = [N, H, W, Cp, OH, OW, kh, kw, sh, sw, ph, pw, ldo]
+  TORCH_CHECK(g.size() == 13 && x.scalar_type() == at::kChar && y.scalar_type() == at::kChar && x.is_cuda() &&
+                  y.is_cuda() && x.is_contiguous(), "pool_i8: int8 device tensors, 13 geometry values");
+  TORCH_CHECK(g[3] % 16 == 0 && x.numel() >= g[0] * g[1] * g[2] * g[3], "pool_i8: x is [N][H][W][Cp], Cp % 16 == 0");
+  const int64_t y_avail = (int64_t)y.storage().nbytes() - y.storage_offset();
+  TORCH_CHECK(g[12] >= g[3] && y_avail >= (g[0] * g[4] * g[5] - 1) * g[12] + g[3] && (y.storage_offset() % 16) == 0,
+              "pool_i8: y too small or misaligned");
+  bigdl_pool_i8(x.data_ptr<int8_t>(), y.data_ptr<int8_t>(), g[0], g[1], g[2], g[3], g[4], g[5], g[6], g[7], g[8], g[9],
+                g[10], g[11], avg ? 1 : 0, count_pad ? 1 : 0, g[12], stream());
+}
+
+void quantize_nchw_f32(const Tensor& x, const Tensor& q, int64_t Cp, double scale) {
+  TORCH_CHECK(x.dim() == 4 && x.is_contiguous() && x.scalar_type() == at::kFloat && x.is_cuda(),
+              "quantize_nchw_f32: x fp32 contiguous NCHW");
+  const int64_t N = x.size(0), C = x.size(1), HW = x.size(2) * x.size(3);
+  TORCH_CHECK(Cp % 16 == 0 && Cp >= C && q.scalar_type() == at::kChar && q.numel() >= N * HW * Cp && q.is_contiguous(),
+              "quantize_nchw_f32: q is int8 [N][H][W][Cp]");
+  bigdl_quantize_nchw_f32(x.data_ptr<float>(), q.data_ptr<int8_t>(), N, C, HW, Cp, (float)(1.0 / scale), stream());
+}
+
+void quantize_rows_bf16(const Tensor& x, const Tensor& q, int64_t P, int64_t C, int64_t ldq, double scale) {
+  TORCH_CHECK(C % 8 == 0 && x.numel() == P * C && x.scalar_type() == at::kBFloat16 && q.scalar_type() == at::kChar,
+              "quantize_rows_bf16: x bf16 [P][C], C % 8 == 0");
+  const int64_t q_avail = (int64_t)q.storage().nbytes() - q.storage_offset();
+  TORCH_CHECK(ldq >= C && q_avail >= (P - 1) * ldq + C && (q.storage_offset() % 8) == 0, "quantize_rows_bf16: q");
+  bigdl_quantize_rows_bf16((const uint16_t*)x.data_ptr(), q.data_ptr<int8_t>(), P, C, ldq, (float)(1.0 / scale),
+                           stream());
+}
+
+void dequantize_rows(const Tensor& q, const Tensor& y, int64_t P, int64_t C, int64_t ld, double scale) {
+  TORCH_CHECK(q.scalar_type() == at::kChar && y.scalar_type() == at::kBFloat16 && y.numel() == P * C &&
+                  q.numel() >= (P - 1) * ld + C, "dequantize_rows: shapes");
+  bigdl_dequantize_rows(q.data_ptr<int8_t>(), (uint16_t*)y.data_ptr(), P, C, ld, (float)scale, stream());
 }
 
 // detection (csrc/detection.hip)
@@ -673,7 +718,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("image_augment", &image_augment);
   m.def("quantize_act", &quantize_act, py::arg("x"), py::arg("q"), py::arg("amax"), py::arg("scale"), py::arg("N"),
         py::arg("P"), py::arg("C"), py::arg("Cp"), py::arg("static_amax") = false);
-  m.def("conv_i8", &conv_i8);
+  m.def("conv_i8", &conv_i8, py::arg("src"), py::arg("wt"), py::arg("out"), py::arg("bias"), py::arg("xscale"),
+        py::arg("wscale"), py::arg("geo"), py::arg("taps"), py::arg("relu"), py::arg("xs_const") = 0.0,
+        py::arg("out_scale") = 0.0);
+  m.def("pool_i8", &pool_i8);
+  m.def("quantize_nchw_f32", &quantize_nchw_f32);
+  m.def("quantize_rows_bf16", &quantize_rows_bf16);
+  m.def("dequantize_rows", &dequantize_rows);
   m.def("nms", &nms);
   m.def("roi_align_fwd", &roi_align_fwd);
   m.def("roi_pool_fwd", &roi_pool_fwd);

@@ -122,7 +122,17 @@ void bigdl_lstm_cell_bwd(const float* act, const float* c_prev, const float* c, 
 // dequantizing implicit-GEMM conv on the i8 MFMA (src/wt are int8 images; out bf16 or fp32).
 int bigdl_quantize_act(const void* x, int is_bf16, int8_t* q, float* amax, float* scale, int N, long P, int C,
                        int Cp, int static_amax, hipStream_t st);
-int bigdl_conv_i8(const ConvArgs* a, const float* xscale, const float* wscale, int out_f32, hipStream_t st);
+// xscale: [N] per-sample activation scales or nullptr (xs_const for the whole tensor); out_mode 0 bf16, 1 fp32,
+// 2 int8 requantized with out_inv = 1 / out_scale. Output rows are a->ldo elements apart.
+int bigdl_conv_i8(const ConvArgs* a, const float* xscale, float xs_const, const float* wscale, int out_mode,
+                  float out_inv, hipStream_t st);
+// int8 NHWC pooling (max or average, same scale in and out; output rows ldo apart), graph-input quantizer
+// (fp32 NCHW -> int8 NHWC, static scale), bf16 rows -> int8 rows at a channel offset, int8 rows -> bf16.
+void bigdl_pool_i8(const int8_t* x, int8_t* y, int N, int H, int W, int Cp, int OH, int OW, int kh, int kw, int sh,
+                   int sw, int ph, int pw, int avg, int count_pad, long ldo, hipStream_t st);
+void bigdl_quantize_nchw_f32(const float* x, int8_t* q, int N, int C, int HW, int Cp, float inv, hipStream_t st);
+void bigdl_quantize_rows_bf16(const uint16_t* x, int8_t* q, long P, int C, long ldq, float inv, hipStream_t st);
+void bigdl_dequantize_rows(const int8_t* q, uint16_t* y, long P, int C, long ld, float scale, hipStream_t st);
 
 void bigdl_set_conv_impl(int impl);
 int bigdl_get_conv_impl();

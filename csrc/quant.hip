@@ -104,35 +104,62 @@ __global__ void quantize8_bf16_kernel(const v4u* __restrict__ x, v2u* __restrict
 }
 
 // ---------------------------------------------------------------------------------- int8 conv
-__device__ __forceinline__ v4u qload16(const uint8_t* p, bool ok) {
-  return *reinterpret_cast<const v4u*>(ok ? p : g_zero16);
+// LDS-DMA implicit GEMM on v_mfma_i32_16x16x64_i8. The LDS image, fragment reads and XOR swizzle are byte-for-byte
+// those of the bf16 conv_nt_glds_kernel (conv_igemm.hip): a 16-byte granule is 16 int8 channels instead of 8 bf16,
+// a 128-byte K stage is 128 int8 taps*channels instead of 64, and one i8 MFMA consumes a 16-byte fragment per lane
+// exactly like the bf16 one — so the int8 kernel moves half the operand bytes per MAC and issues half the MFMAs.
+// Operands go global -> LDS with global_load_lds_dwordx4 (no VGPR staging); a K stage lies in one tap when
+// Cs % 128 == 0 (FASTK), otherwise every lane resolves the tap of its own granule.
+// Epilogue (through the idle staging LDS, one pixel row of 8 channels per lane): y = acc * s_x * s_w[n] + bias
+// (+ReLU), stored as bf16 / fp32, or requantized to int8 with the consumer's static scale (y * out_inv, round,
+// clamp +-127) — the int8 output path lets the next quantized layer (or a concat slice it reads) consume it
+// directly, with no separate quantize pass. Output rows are `ldo` apart, so a concat slice is just an offset.
+__device__ __forceinline__ void glds16(const void* g, LDS_PTR(void) l) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g, l, 16, 0, 0);
 }
 
-template <int BM, int BN>
-__global__ __launch_bounds__(256, 2) void conv_i8_kernel(ConvArgs a, const float* __restrict__ xscale,
-                                                         const float* __restrict__ wscale, int out_f32) {
-  constexpr int WM = 2, WN = 2;
+struct I8Epi {
+  const float* xscale;   // [N] per-sample scale, or nullptr -> xs_const
+  float xs_const;
+  const float* wscale;   // [Ncol]
+  int out_mode;          // 0 bf16, 1 fp32, 2 int8
+  float out_inv;         // int8 output: 1 / out_scale
+};
+
+//
+// Tiles: 128 x 128 (2 x 2 waves) by default; narrow layers (Ncol <= 64 / <= 32 — the 147x147 / 73x73 stem convs
+// and the 64-, 48-, 32-channel branch convs of Inception) use 256 x 64 / 256 x 32 tiles with the four waves stacked
+// along M, so no MFMA is spent on the empty half (or three quarters) of a 128-wide tile.
+template <int BM, int BN, int WM, bool FASTK>
+__global__ __launch_bounds__(256, 2) void conv_i8_glds_kernel(ConvArgs a, I8Epi ep) {
+  constexpr int WN = 4 / WM;
   constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int MI = TM / 16, NI = TN / 16;
-  constexpr int AROWS = BM / 32, BROWS = BN / 32;
-  constexpr int STAGE = (BM + BN) * QBK;        // bytes per stage
-  __shared__ __attribute__((aligned(16))) uint8_t lds[2 * STAGE];
+  constexpr int AI = BM / 32, BI = BN / 32;
+  constexpr int STAGE = (BM + BN) * QBK;          // bytes
+  __shared__ __attribute__((aligned(1024))) uint8_t lds[2 * STAGE];
   const uint8_t* src = reinterpret_cast<const uint8_t*>(a.src);
   const uint8_t* wt = reinterpret_cast<const uint8_t*>(a.wt);
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WN, wn = wave % WN;
   const int tiles_n = (a.Ncol + BN - 1) / BN;
-  const int nwg = ((a.M + BM - 1) / BM) * tiles_n;
+  const int tiles_m = (a.M + BM - 1) / BM;
+  const int nwg = tiles_m * tiles_n;
   const int bid = xcd_remap(blockIdx.x, nwg);
   const int tm = bid / tiles_n, tn = bid % tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
-  const int lrow = tid >> 3, lg = tid & 7;
+
+  // DMA lane geometry (as conv_nt_glds_kernel): instruction i of wave w fills rows (i*4 + w)*8 .. +8; lane ->
+  // row += lane>>3, LDS slot lane&7 holds source granule (lane ^ (lane>>3)) & 7.
+  const int rsub = lane >> 3;
+  const int gsrc = (lane ^ rsub) & 7;
+  int a_pix[AI], a_h[AI], a_w[AI];
   const int ohw = a.OH * a.OW;
-  int a_pix[AROWS], a_h[AROWS], a_w[AROWS];
 #pragma unroll
-  for (int i = 0; i < AROWS; ++i) {
-    const int m = m0 + lrow + 32 * i;
+  for (int i = 0; i < AI; ++i) {
+    const int m = m0 + (i * 4 + wave) * 8 + rsub;
     if (m < a.M) {
       const int nb = m / ohw, rem = m - nb * ohw;
       const int oh = rem / a.OW, ow = rem - oh * a.OW;
@@ -143,47 +170,60 @@ __global__ __launch_bounds__(256, 2) void conv_i8_kernel(ConvArgs a, const float
       a_pix[i] = 0; a_h[i] = -(1 << 28); a_w[i] = -(1 << 28);
     }
   }
-  v4u ra[AROWS], rb[BROWS];
-  auto gload = [&](int kt) {
-    const int kk = kt * QBK + lg * 16;
-    const bool kvalid = kk < a.Kdim;
-    const int kc = kvalid ? kk : 0;
-    const int t = kc / a.Cs, c = kc - t * a.Cs;
-    const int th = a.tap_h[t], tw = a.tap_w[t];
-    const int wk = a.tap_k[t] * a.Cs + c;
+  const uint8_t* wrow[BI];
+  bool bvalid[BI];
 #pragma unroll
-    for (int i = 0; i < AROWS; ++i) {
-      const int ch = a_h[i] + th, cw = a_w[i] + tw;
-      const bool ok = kvalid && (unsigned)ch < (unsigned)a.Hs && (unsigned)cw < (unsigned)a.Ws;
-      ra[i] = qload16(src + (size_t)(a_pix[i] + ch * a.Ws + cw) * a.Cs + c, ok);
+  for (int i = 0; i < BI; ++i) {
+    const int n = n0 + (i * 4 + wave) * 8 + rsub;
+    bvalid[i] = n < a.Ncol;
+    wrow[i] = wt + (size_t)(bvalid[i] ? n : 0) * a.ldw;
+  }
+  auto issue = [&](int kt, int buf) {
+    const int k0 = kt * QBK;
+    int th, tw, c, wk;
+    bool kv = true;
+    if constexpr (FASTK) {
+      const int t = k0 / a.Cs;
+      c = k0 - t * a.Cs + gsrc * 16;
+      th = a.tap_h[t]; tw = a.tap_w[t];
+      wk = a.tap_k[t] * a.Cs + c;
+    } else {
+      const int kk = k0 + gsrc * 16;
+      kv = kk < a.Kdim;
+      const int kc = kv ? kk : 0;
+      const int t = kc / a.Cs;
+      c = kc - t * a.Cs;
+      th = a.tap_h[t]; tw = a.tap_w[t];
+      wk = a.tap_k[t] * a.Cs + c;
     }
-#pragma unroll
-    for (int i = 0; i < BROWS; ++i) {
-      const int n = n0 + lrow + 32 * i;
-      rb[i] = qload16(wt + (size_t)(n < a.Ncol ? n : 0) * a.ldw + wk, kvalid && n < a.Ncol);
-    }
-  };
-  auto swz = [](int row, int g) { return row * QBK + ((g ^ (row & 7)) << 4); };
-  auto swrite = [&](int buf) {
     uint8_t* A = lds + buf * STAGE;
     uint8_t* B = A + BM * QBK;
 #pragma unroll
-    for (int i = 0; i < AROWS; ++i) *reinterpret_cast<v4u*>(A + swz(lrow + 32 * i, lg)) = ra[i];
+    for (int i = 0; i < AI; ++i) {
+      const int ch = a_h[i] + th, cw = a_w[i] + tw;
+      const bool ok = kv && (unsigned)ch < (unsigned)a.Hs && (unsigned)cw < (unsigned)a.Ws;
+      const uint8_t* g = ok ? src + (size_t)(a_pix[i] + ch * a.Ws + cw) * a.Cs + c : g_zero16;
+      glds16(g, (LDS_PTR(void))(A + (i * 4 + wave) * 8 * QBK));
+    }
 #pragma unroll
-    for (int i = 0; i < BROWS; ++i) *reinterpret_cast<v4u*>(B + swz(lrow + 32 * i, lg)) = rb[i];
+    for (int i = 0; i < BI; ++i) {
+      const uint8_t* g = (bvalid[i] && kv) ? wrow[i] + wk : g_zero16;
+      glds16(g, (LDS_PTR(void))(B + (i * 4 + wave) * 8 * QBK));
+    }
   };
+  auto swz = [](int row, int g) { return row * QBK + ((g ^ (row & 7)) << 4); };
+
   v4i acc[MI][NI];
 #pragma unroll
   for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int j = 0; j < NI; ++j) acc[i][j] = v4i{0, 0, 0, 0};
   const int nk = (a.Kdim + QBK - 1) / QBK;
-  gload(0);
-  swrite(0);
+  issue(0, 0);
   __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
-    if (kt + 1 < nk) gload(kt + 1);
+    if (kt + 1 < nk) issue(kt + 1, cur ^ 1);
     const uint8_t* A = lds + cur * STAGE;
     const uint8_t* B = A + BM * QBK;
 #pragma unroll
@@ -200,49 +240,227 @@ __global__ __launch_bounds__(256, 2) void conv_i8_kernel(ConvArgs a, const float
         for (int j = 0; j < NI; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fb[j], fa[i], acc[i][j], 0, 0, 0);
     }
-    if (kt + 1 < nk) swrite(cur ^ 1);
-    __syncthreads();
+    __syncthreads();   // retires the stage-(k+1) DMA and the stage-k fragment reads
   }
-  // epilogue: lane owns channels 4*(lane>>4)+e of pixel lane&15 (weights were the MFMA A operand)
+
+  // ---- epilogue: park the wave's int32 tile (as fp32, exact to 2^24 relative rounding) in its LDS slice,
+  // XOR-swizzled by pixel, then re-read one pixel row of 8 channels per lane.
+  constexpr int GR = TN / 4, LPR = TN / 8, PPI = 64 / LPR, NR = TM / PPI;
+  float* wl = reinterpret_cast<float*>(lds) + wave * TM * TN;
+  auto gpos = [](int p, int g) { return (p * GR + (g ^ (p & (GR - 1)))) * 4; };
 #pragma unroll
-  for (int j = 0; j < NI; ++j) {
-    const int nb = n0 + wn * TN + j * 16 + (lane >> 4) * 4;
-    float ws[4], bs[4];
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const bool ok = nb + e < a.Ncol;
-      ws[e] = ok ? wscale[nb + e] : 0.f;
-      bs[e] = (ok && a.bias) ? a.bias[nb + e] : 0.f;
+    for (int j = 0; j < NI; ++j) {
+      const v4i v = acc[i][j];
+      *reinterpret_cast<v4f*>(wl + gpos(i * 16 + (lane & 15), j * 4 + (lane >> 4))) =
+          v4f{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
     }
+  __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's LDS writes landed (wave-private slice)
+  const int q = lane % LPR;
+  const int mbase = m0 + wm * TM, n = n0 + wn * TN + q * 8;
+  if (n >= a.Ncol) return;
+  const bool full8 = n + 8 <= a.Ncol;
+  float wsc[8], bs[8];
 #pragma unroll
-    for (int i = 0; i < MI; ++i) {
-      const int m = m0 + wm * TM + i * 16 + (lane & 15);
-      if (m >= a.M) continue;
-      const int img = m / ohw;
-      const float xs = xscale[img];
-      float v[4];
+  for (int e = 0; e < 8; ++e) {
+    const bool ok = n + e < a.Ncol;
+    wsc[e] = ok ? ep.wscale[n + e] : 0.f;
+    bs[e] = (ok && a.bias) ? a.bias[n + e] : 0.f;
+  }
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float t = (float)acc[i][j][e] * xs * ws[e] + bs[e];
-        if (a.relu) t = fmaxf(t, 0.f);
-        v[e] = t;
+  for (int r = 0; r < NR; ++r) {
+    const int p = r * PPI + lane / LPR;
+    const int m = mbase + p;
+    if (m >= a.M) continue;
+    const v4f lo = *reinterpret_cast<const v4f*>(wl + gpos(p, 2 * q));
+    const v4f hi = *reinterpret_cast<const v4f*>(wl + gpos(p, 2 * q + 1));
+    const float xs = ep.xscale ? ep.xscale[m / ohw] : ep.xs_const;
+    float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      v[e] = v[e] * xs * wsc[e] + bs[e];
+      if (a.relu) v[e] = fmaxf(v[e], 0.f);
+    }
+    const size_t off = (size_t)m * a.ldo + n;
+    if (ep.out_mode == 2) {
+      int8_t* o = reinterpret_cast<int8_t*>(a.out) + off;
+      unsigned pk[2] = {0u, 0u};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int qv = max(-127, min(127, __float2int_rn(v[e] * ep.out_inv)));
+        pk[e >> 2] |= (unsigned)(qv & 0xff) << (8 * (e & 3));
       }
-      if (out_f32) {
-        float* o = reinterpret_cast<float*>(a.out) + (size_t)m * a.ldo + nb;
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          if (nb + e < a.Ncol) o[e] = v[e];
+      if (full8 && (off & 7) == 0) {
+        *reinterpret_cast<v2u*>(o) = v2u{pk[0], pk[1]};
       } else {
-        bf16_t* o = a.out + (size_t)m * a.ldo + nb;
-        if ((a.ldo & 3) == 0 && nb + 3 < a.Ncol) {
-          *reinterpret_cast<v2u*>(o) = v2u{pack2bf(v[0], v[1]), pack2bf(v[2], v[3])};
-        } else {
 #pragma unroll
-          for (int e = 0; e < 4; ++e)
-            if (nb + e < a.Ncol) o[e] = f2bf(v[e]);
+        for (int e = 0; e < 8; ++e)
+          if (n + e < a.Ncol) o[e] = (int8_t)((pk[e >> 2] >> (8 * (e & 3))) & 0xff);
+      }
+    } else if (ep.out_mode == 1) {
+      float* o = reinterpret_cast<float*>(a.out) + off;
+      if (full8 && (off & 3) == 0) {
+        *reinterpret_cast<v4f*>(o) = v4f{v[0], v[1], v[2], v[3]};
+        *reinterpret_cast<v4f*>(o + 4) = v4f{v[4], v[5], v[6], v[7]};
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (n + e < a.Ncol) o[e] = v[e];
+      }
+    } else {
+      bf16_t* o = a.out + off;
+      if (full8 && (off & 7) == 0) {
+        *reinterpret_cast<v4u*>(o) = v4u{pack2bf(v[0], v[1]), pack2bf(v[2], v[3]), pack2bf(v[4], v[5]), pack2bf(v[6], v[7])};
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (n + e < a.Ncol) o[e] = f2bf(v[e]);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------- int8 pooling / quantize
+// NHWC int8 max / average pooling over [N][H][W][Cp] -> [N][OH][OW][ldo] (rows `ldo` apart, so a pooling branch
+// of an int8 concat writes its slice in place). One lane = 16 channels of one output pixel (16-byte loads); the
+// scale is unchanged (max of int8 values / rounded mean stay in [-127, 127]). Average: count_pad selects whether
+// padded taps count in the divisor (Caffe / BigDL default) or not.
+// K3 (3x3 windows, Inception's branch pools and reductions): the nine window granules are loaded unconditionally
+// (out-of-image taps read a zero granule) before any is used, so a lane keeps nine L2/HBM requests in flight
+// instead of nine dependent round trips.
+template <bool K3>
+__global__ void pool_i8_kernel(const int8_t* __restrict__ x, int8_t* __restrict__ y, int N, int H, int W, int Cp,
+                               int OH, int OW, int kh, int kw, int sh, int sw, int ph, int pw, int avg, int count_pad,
+                               long ldo) {
+  const int G = Cp >> 4;
+  if constexpr (K3) {
+    const long total = (long)N * OH * OW * G;
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+      const int g = (int)(i % G);
+      const long pix = i / G;
+      const int ow = (int)(pix % OW), oh = (int)((pix / OW) % OH), nb = (int)(pix / ((long)OW * OH));
+      const int h0 = oh * sh - ph, w0 = ow * sw - pw;
+      v4u u[9];
+      int cnt = 0;
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int hh = h0 + t / 3, ww = w0 + t % 3;
+        const bool inb = (unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W;
+        cnt += (avg && count_pad) ? (hh < H + ph && ww < W + pw) : inb;
+        const int8_t* src = inb ? x + (((size_t)nb * H + hh) * W + ww) * Cp + g * 16
+                                : reinterpret_cast<const int8_t*>(g_zero16);
+        u[t] = *reinterpret_cast<const v4u*>(src);
+        if (!avg && !inb) u[t] = v4u{0x80808080u, 0x80808080u, 0x80808080u, 0x80808080u};   // -128: never the max
+      }
+      v4u o = {0u, 0u, 0u, 0u};
+      const float inv = cnt > 0 ? 1.f / (float)cnt : 0.f;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        int acc = avg ? 0 : -128;
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+          const int v = (int)(int8_t)((u[t][e >> 2] >> (8 * (e & 3))) & 0xff);
+          acc = avg ? acc + v : max(acc, v);
+        }
+        int v = avg ? __float2int_rn((float)acc * inv) : (cnt > 0 ? acc : 0);
+        v = max(-127, min(127, v));
+        o[e >> 2] |= (unsigned)(v & 0xff) << (8 * (e & 3));
+      }
+      *reinterpret_cast<v4u*>(y + pix * ldo + g * 16) = o;
+    }
+    return;
+  }
+  const long total = (long)N * OH * OW * G;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int g = (int)(i % G);
+    const long pix = i / G;
+    const int ow = (int)(pix % OW), oh = (int)((pix / OW) % OH), nb = (int)(pix / ((long)OW * OH));
+    const int h0 = oh * sh - ph, w0 = ow * sw - pw;
+    int acc[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[e] = avg ? 0 : -128;
+    int cnt = 0;
+    for (int r = 0; r < kh; ++r) {
+      const int hh = h0 + r;
+      for (int s = 0; s < kw; ++s) {
+        const int ww = w0 + s;
+        const bool inb = (unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W;
+        if (avg && count_pad) {
+          if (hh < H + ph && ww < W + pw) ++cnt;
+        } else if (inb) {
+          ++cnt;
+        }
+        if (!inb) continue;
+        const v4u u = *reinterpret_cast<const v4u*>(x + (((size_t)nb * H + hh) * W + ww) * Cp + g * 16);
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int v = (int)(int8_t)((u[e >> 2] >> (8 * (e & 3))) & 0xff);
+          acc[e] = avg ? acc[e] + v : max(acc[e], v);
         }
       }
     }
+    v4u o = {0u, 0u, 0u, 0u};
+    const float inv = cnt > 0 ? 1.f / (float)cnt : 0.f;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      int v = avg ? __float2int_rn((float)acc[e] * inv) : (cnt > 0 ? acc[e] : 0);
+      v = max(-127, min(127, v));
+      o[e >> 2] |= (unsigned)(v & 0xff) << (8 * (e & 3));
+    }
+    *reinterpret_cast<v4u*>(y + pix * ldo + g * 16) = o;
+  }
+}
+
+// fp32 NCHW image batch -> int8 NHWC [N][H][W][Cp] with a static scale (graph input of an int8 plan); pad channels 0.
+__global__ void quantize_nchw_f32_kernel(const float* __restrict__ x, int8_t* __restrict__ q, int N, int C, int HW,
+                                         int Cp, float inv) {
+  const long total = (long)N * HW;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long nb = i / HW, p = i - nb * HW;
+    const float* xs = x + nb * C * (long)HW + p;
+    int8_t* o = q + i * Cp;
+    for (int c0 = 0; c0 < Cp; c0 += 16) {
+      v4u u = {0u, 0u, 0u, 0u};
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int c = c0 + e;
+        const int v = c < C ? max(-127, min(127, __float2int_rn(xs[(long)c * HW] * inv))) : 0;
+        u[e >> 2] |= (unsigned)(v & 0xff) << (8 * (e & 3));
+      }
+      *reinterpret_cast<v4u*>(o + c0) = u;
+    }
+  }
+}
+
+// bf16 NHWC [P][C] -> int8 [P][ldq] (written at a channel offset of a wider int8 buffer), static scale
+__global__ void quantize_rows_bf16_kernel(const bf16_t* __restrict__ x, int8_t* __restrict__ q, long P, int C,
+                                          long ldq, float inv) {
+  const int G = C >> 3;
+  const long total = P * G;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long p = i / G;
+    const int g = (int)(i - p * G);
+    const v4u u = *reinterpret_cast<const v4u*>(x + p * C + g * 8);
+    unsigned pk[2] = {0u, 0u};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int v0 = max(-127, min(127, __float2int_rn(lo_bf(u[e]) * inv)));
+      const int v1 = max(-127, min(127, __float2int_rn(hi_bf(u[e]) * inv)));
+      pk[e >> 1] |= ((unsigned)(v0 & 0xff) | ((unsigned)(v1 & 0xff) << 8)) << (16 * (e & 1));
+    }
+    *reinterpret_cast<v2u*>(q + p * ldq + g * 8) = v2u{pk[0], pk[1]};
+  }
+}
+
+// int8 NHWC [P][ld] -> bf16 [P][C] (dequantize, for a float consumer of an int8 tensor)
+__global__ void dequantize_rows_kernel(const int8_t* __restrict__ q, bf16_t* __restrict__ y, long P, int C, long ld,
+                                       float scale) {
+  const long total = P * C;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long p = i / C;
+    const int c = (int)(i - p * C);
+    y[i] = f2bf((float)q[p * ld + c] * scale);
   }
 }
 
@@ -275,13 +493,62 @@ int bigdl_quantize_act(const void* x, int is_bf16, int8_t* q, float* amax, float
   return 0;
 }
 
-int bigdl_conv_i8(const ConvArgs* a, const float* xscale, const float* wscale, int out_f32, hipStream_t st) {
+int bigdl_conv_i8(const ConvArgs* a, const float* xscale, float xs_const, const float* wscale, int out_mode,
+                  float out_inv, hipStream_t st) {
   if (a->Cs % 16 != 0 || a->Kdim != a->ntaps * a->Cs || a->ntaps < 1 || a->ntaps > CONV_MAX_TAPS) return -1;
   if (a->M <= 0) return 0;
   const int nwg = ((a->M + 127) / 128) * ((a->Ncol + 127) / 128);
-  conv_i8_kernel<128, 128><<<nwg, 256, 0, st>>>(*a, xscale, wscale, out_f32);
+  const I8Epi ep{xscale, xs_const, wscale, out_mode, out_inv};
+  const bool fk = a->Cs % QBK == 0;
+  if (a->Ncol <= 32) {
+    const int g = ((a->M + 255) / 256) * ((a->Ncol + 31) / 32);
+    if (fk) conv_i8_glds_kernel<256, 32, 4, true><<<g, 256, 0, st>>>(*a, ep);
+    else conv_i8_glds_kernel<256, 32, 4, false><<<g, 256, 0, st>>>(*a, ep);
+  } else if (a->Ncol <= 64) {
+    const int g = ((a->M + 255) / 256) * ((a->Ncol + 63) / 64);
+    if (fk) conv_i8_glds_kernel<256, 64, 4, true><<<g, 256, 0, st>>>(*a, ep);
+    else conv_i8_glds_kernel<256, 64, 4, false><<<g, 256, 0, st>>>(*a, ep);
+  } else if (fk) {
+    conv_i8_glds_kernel<128, 128, 2, true><<<nwg, 256, 0, st>>>(*a, ep);
+  } else {
+    conv_i8_glds_kernel<128, 128, 2, false><<<nwg, 256, 0, st>>>(*a, ep);
+  }
   HIP_LAUNCH_CHECK();
   return 0;
+}
+
+void bigdl_pool_i8(const int8_t* x, int8_t* y, int N, int H, int W, int Cp, int OH, int OW, int kh, int kw, int sh,
+                   int sw, int ph, int pw, int avg, int count_pad, long ldo, hipStream_t st) {
+  const long total = (long)N * OH * OW * (Cp >> 4);
+  const int blocks = (int)std::min<long>((total + 255) / 256, 16384);
+  if (kh == 3 && kw == 3)
+    pool_i8_kernel<true><<<blocks > 0 ? blocks : 1, 256, 0, st>>>(x, y, N, H, W, Cp, OH, OW, kh, kw, sh, sw, ph, pw,
+                                                                  avg, count_pad, ldo);
+  else
+    pool_i8_kernel<false><<<blocks > 0 ? blocks : 1, 256, 0, st>>>(x, y, N, H, W, Cp, OH, OW, kh, kw, sh, sw, ph, pw,
+                                                                   avg, count_pad, ldo);
+  HIP_LAUNCH_CHECK();
+}
+
+void bigdl_quantize_nchw_f32(const float* x, int8_t* q, int N, int C, int HW, int Cp, float inv, hipStream_t st) {
+  const long total = (long)N * HW;
+  const int blocks = (int)std::min<long>((total + 255) / 256, 16384);
+  quantize_nchw_f32_kernel<<<blocks > 0 ? blocks : 1, 256, 0, st>>>(x, q, N, C, HW, Cp, inv);
+  HIP_LAUNCH_CHECK();
+}
+
+void bigdl_quantize_rows_bf16(const uint16_t* x, int8_t* q, long P, int C, long ldq, float inv, hipStream_t st) {
+  const long total = P * (C >> 3);
+  const int blocks = (int)std::min<long>((total + 255) / 256, 16384);
+  quantize_rows_bf16_kernel<<<blocks > 0 ? blocks : 1, 256, 0, st>>>(x, q, P, C, ldq, inv);
+  HIP_LAUNCH_CHECK();
+}
+
+void bigdl_dequantize_rows(const int8_t* q, uint16_t* y, long P, int C, long ld, float scale, hipStream_t st) {
+  const long total = P * C;
+  const int blocks = (int)std::min<long>((total + 255) / 256, 16384);
+  dequantize_rows_kernel<<<blocks > 0 ? blocks : 1, 256, 0, st>>>(q, y, P, C, ld, scale);
+  HIP_LAUNCH_CHECK();
 }
 
 }  // extern "C"

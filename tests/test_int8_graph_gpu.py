@@ -1,0 +1,115 @@
+"""Static int8 inference plan (quantized/int8_graph.py) and its kernels (csrc/quant.hip): requantizing conv
+epilogue into concat slices, int8 max / average pooling, graph-input quantizer, and whole-graph numerics of the
+planned int8 Graph against the float model."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from bigdl_amd import nn
+from bigdl_amd.ops import native
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    a, b = a.float().cpu(), b.float().cpu()
+    return float((a - b).norm() / (b.norm() + 1e-12))
+
+
+def test_conv_i8_requantized_output_into_slice():
+    """int8 output written at a channel offset of a wider buffer equals round(clamp(y / s_out)) of the fp32 result."""
+    from bigdl_amd.ops.conv import _fwd_taps, out_size
+
+    N, C, H, W, K, R = 2, 48, 10, 9, 40, 3
+    g = torch.Generator().manual_seed(3)
+    x = torch.randint(-127, 128, (N, H, W, C), generator=g, dtype=torch.int8)
+    w = torch.randint(-127, 128, (K, R, R, C), generator=g, dtype=torch.int8)
+    xs, ws = 0.02, torch.rand(K, generator=g) * 0.01 + 0.001
+    bias = torch.randn(K, generator=g)
+    OH, OW = out_size(H, R, 1, 1), out_size(W, R, 1, 1)
+    ref = F.conv2d(x.permute(0, 3, 1, 2).double(), w.permute(0, 3, 1, 2).double(), None, 1, 1)
+    ref = ref * xs * ws.double().view(1, K, 1, 1) + bias.double().view(1, K, 1, 1)
+    ref = torch.relu(ref).permute(0, 2, 3, 1)
+    s_out = float(ref.abs().max()) / 127
+    buf = torch.full((N, OH, OW, 64), 99, dtype=torch.int8, device="cuda")
+    sl = buf[..., 16:16 + K]
+    geo = [N, H, W, C, OH, OW, 1, 1, R * R * C, K, 64, OH, OW, 1, 1, 0, 0]
+    native.get().conv_i8(x.cuda(), w.cuda(), sl, bias.cuda(), None, ws.cuda(), geo, _fwd_taps(R, R, 1, 1, 1, 1), True,
+                         xs, s_out)
+    got = buf.cpu()
+    exp = torch.clamp(torch.round(ref / s_out), -127, 127).to(torch.int8)
+    assert (got[..., 16:16 + K].int() - exp.int()).abs().max() <= 1
+    assert torch.all(got[..., :16] == 99) and torch.all(got[..., 16 + K:] == 99)
+
+
+@pytest.mark.parametrize("avg,k,s,p,count_pad", [(False, 3, 2, 0, False), (False, 3, 1, 1, False),
+                                                (True, 3, 1, 1, True), (True, 3, 1, 1, False), (True, 8, 8, 0, True)])
+def test_pool_i8_matches_reference(avg, k, s, p, count_pad):
+    from bigdl_amd.ops.conv import out_size
+
+    N, H, W, C = 2, 17, 17, 32
+    g = torch.Generator().manual_seed(4)
+    x = torch.randint(-127, 128, (N, H, W, C), generator=g, dtype=torch.int8)
+    OH, OW = out_size(H, k, s, p), out_size(W, k, s, p)
+    y = torch.zeros((N, OH, OW, C), dtype=torch.int8, device="cuda")
+    native.get().pool_i8(x.cuda(), y, [N, H, W, C, OH, OW, k, k, s, s, p, p, C], avg, count_pad)
+    xf = x.permute(0, 3, 1, 2).double()
+    if avg:
+        ref = torch.round(F.avg_pool2d(xf, k, s, p, count_include_pad=count_pad))
+    else:
+        ref = F.max_pool2d(xf, k, s, p)
+    ref = ref.permute(0, 2, 3, 1)
+    assert (y.cpu().double() - ref).abs().max() <= 1
+
+
+def test_quantize_nchw_input():
+    x = torch.randn(2, 3, 7, 5, device="cuda")
+    q = torch.zeros((2, 7, 5, 16), dtype=torch.int8, device="cuda")
+    s = float(x.abs().max()) / 127
+    native.get().quantize_nchw_f32(x, q, 16, s)
+    ref = torch.clamp(torch.round(x.permute(0, 2, 3, 1) / s), -127, 127).to(torch.int8)
+    assert (q[..., :3].int() - ref.int()).abs().max() <= 1 and torch.all(q[..., 3:] == 0)
+
+
+def _small_inception():
+    torch.manual_seed(0)
+    inp = nn.Input()
+    x = nn.ReLU()(nn.SpatialConvolution(3, 32, 3, 3, 2, 2)(inp))
+    x = nn.ReLU()(nn.SpatialConvolution(32, 48, 3, 3, 1, 1, 1, 1)(x))
+    x = nn.SpatialMaxPooling(3, 3, 2, 2)(x)
+    a = nn.ReLU()(nn.SpatialConvolution(48, 32, 1, 1)(x))
+    b = nn.ReLU()(nn.SpatialConvolution(48, 16, 1, 1)(x))
+    b = nn.ReLU()(nn.SpatialConvolution(16, 32, 3, 3, 1, 1, 1, 1)(b))
+    c = nn.SpatialAveragePooling(3, 3, 1, 1, 1, 1)(x)
+    c = nn.ReLU()(nn.SpatialConvolution(48, 16, 1, 1)(c))
+    d = nn.SpatialMaxPooling(3, 3, 1, 1, 1, 1)(x)
+    j = nn.JoinTable(2, 0)(a, b, c, d)                                       # 32 + 32 + 16 + 48 = 128
+    y = nn.ReLU()(nn.SpatialConvolution(128, 64, 1, 1)(j))
+    y = nn.SpatialAveragePooling(7, 7, 1, 1)(y)
+    y = nn.View(64).setNumInputDims(3)(y)
+    y = nn.Linear(64, 10)(y)
+    g = nn.Graph([inp], [y])
+    g.evaluate()
+    return g
+
+
+def test_int8_plan_graph_matches_float():
+    from bigdl_amd.quantized.int8_graph import I8Act
+    from bigdl_amd.quantized.quantizer import quantize
+
+    g = _small_inception()
+    x = torch.randn(8, 3, 33, 33)
+    ref = g.forward(x).clone()
+    dev = torch.device("cuda:0")
+    gd = g.cloneModule().to(dev)
+    q = quantize(gd, calibration=x.to(dev))
+    plan = q._int8_plan
+    assert plan is not None and sum(plan.int8.values()) >= 8, plan.int8
+    y = q.forward(x.to(dev))
+    assert y.dtype == torch.float32 and y.shape == ref.shape
+    assert _rel(y, ref) < 0.08
+    # every conv produced int8 (requantizing epilogue) and the concat stayed int8
+    n8 = sum(isinstance(v, I8Act) for v in q._outs.values())
+    assert n8 >= 8
+    y2 = q.forward(x.to(dev))
+    assert _rel(y2, y) < 1e-6
