@@ -118,6 +118,7 @@ class Int8GraphPlan:
             for p in n.prevs:
                 self.users.setdefault(p.id, []).append(n)
         self.amax = self._calibrate(calibration)
+        self._find_residuals()
         self.int8 = {}
         self._classify()
         self._scales()
@@ -136,10 +137,34 @@ class Int8GraphPlan:
         self.g._outs = {}
         return amax
 
+    def _find_residuals(self):
+        """CAddTable(conv, other) [-> ReLU] where the conv feeds only the add: the int8 conv epilogue adds the
+        shortcut (int8, its own scale) and applies the ReLU (reference Fusion.scala conv + sum)."""
+        self.res, self.res_conv, self.res_relu = {}, {}, {}
+        for n in self.g.order:
+            if not (type(n.element).__name__ == "CAddTable" and len(n.prevs) == 2
+                    and all(k is None for k in n.prev_index)):
+                continue
+            for ci in (0, 1):
+                c, o = n.prevs[ci], n.prevs[1 - ci]
+                if c is o or not _conv_ok(c.element) or len(self.users.get(c.id, [])) != 1 or c.element.fuse_relu:
+                    continue
+                us = self.users.get(n.id, [])
+                r = us[0] if (len(us) == 1 and isinstance(us[0].element, ReLU) and len(us[0].prevs) == 1) else None
+                self.res[n.id] = (c, o, r, ci + 1)
+                self.res_conv[c.id] = n.id
+                if r is not None:
+                    self.res_relu[r.id] = n.id
+                break
+
     def _consumer_ok(self, n, c):
         m = c.element
         if any(k is not None for k in c.prev_index):
             return False
+        if c.id in self.res:              # a planned residual add takes its conv and an int8 shortcut
+            return True
+        if c.id in self.res_relu:
+            return True
         if _conv_ok(m) or _pool_ok(m) or _pass_ok(m):
             return len(c.prevs) == 1
         if isinstance(m, JoinTable):
@@ -156,6 +181,17 @@ class Int8GraphPlan:
         outs = {o.id for o in g.output_nodes}
         for n in g.order:
             m = n.element
+            if n.id in self.int8:          # set with its residual conv
+                continue
+            if n.id in self.res_conv:      # conv -> add [-> ReLU]: the block output decides for all three
+                add = self.res_conv[n.id]
+                c, o, r, _ = self.res[add]
+                f = r if r is not None else [x for x in g.order if x.id == add][0]
+                us = self.users.get(f.id, [])
+                cap = f.id not in outs and bool(us) and all(self._consumer_ok(f, u) for u in us)
+                for nid in (n.id, add) + ((r.id,) if r is not None else ()):
+                    self.int8[nid] = cap
+                continue
             us = self.users.get(n.id, [])
             if n.id in outs or not us or not all(self._consumer_ok(n, c) for c in us):
                 self.int8[n.id] = False
@@ -179,7 +215,14 @@ class Int8GraphPlan:
                 continue
             uf.find(n.id)
             m = n.element
-            if (_pool_ok(m) or _pass_ok(m) or _is_flatten(m)) and n.prevs:
+            if n.id in self.res:
+                c, o, r, _ = self.res[n.id]
+                uf.union(n.id, c.id)
+                if r is not None:
+                    uf.union(r.id, n.id)
+            elif n.id in self.res_relu:
+                pass
+            elif (_pool_ok(m) or _pass_ok(m) or _is_flatten(m)) and n.prevs:
                 uf.union(n.id, n.prevs[0].id)
             elif isinstance(m, JoinTable):
                 for p in n.prevs:
@@ -208,10 +251,22 @@ class Int8GraphPlan:
                     if isinstance(p.element, ReLU) and p.element.passthrough and len(p.prevs) == 1 \
                             and len(self.users.get(p.prevs[0].id, [])) == 1:
                         self.join_of[p.prevs[0].id] = (link, p)     # conv -> fused ReLU -> concat
+        self.stash, self.fused = {}, {}
+        extra = {}
+        for add_id, (c, o, r, idx) in self.res.items():
+            extra.setdefault(c.id, []).append(o)
         for n in g.order:
             m = n.element
             run = None
-            if n in g.inputs_nodes and not n.prevs:
+            n.fuse_pre = None
+            if n.id in self.res_conv:
+                o = self.res[self.res_conv[n.id]][1]
+                n.fuse_pre = (lambda outs, x, _c=n.id, _o=o.id: self.stash.__setitem__(_c, outs[_o]))
+            if n.id in self.res:
+                run = self._add_runner(n)
+            elif n.id in self.res_relu:
+                run = self._res_relu_runner(n)
+            elif n in g.inputs_nodes and not n.prevs:
                 if self.int8[n.id]:
                     run = self._input_runner(n)
             elif _conv_ok(m):
@@ -227,6 +282,11 @@ class Int8GraphPlan:
             else:
                 run = self._float_runner(n)
             n.fuse_run = run
+        if extra:
+            from ..nn.fusion import _topo_with_deps
+
+            g.order = _topo_with_deps(g, extra)
+            g.modules = [n.element for n in g.order]
         g._int8_plan = self
 
     def join_of_self(self, n):
@@ -260,10 +320,51 @@ class Int8GraphPlan:
             return I8Act(q, C, scale)
         return run
 
+    def _residual_addend(self, n, N, OH, OW, K):
+        """The int8 shortcut of a residual conv (quantized here when it arrived as a float tensor), or None."""
+        a = self.stash.pop(n.id, None)
+        add_id = self.res_conv[n.id]
+        self.fused[add_id] = False
+        if a is None or tuple(a.shape) != (N, K, OH, OW):
+            return None
+        if not isinstance(a, I8Act):
+            if not (isinstance(a, torch.Tensor) and a.is_cuda and K % 8 == 0):
+                return None
+            o = self.res[add_id][1]
+            sc = (self.amax.get(o.id, 0.0) or float(a.abs().max()) or 1.0) / 127.0
+            q = (torch.empty if _ceil16(K) == K else torch.zeros)((N, OH, OW, _ceil16(K)), dtype=torch.int8,
+                                                                   device=a.device)
+            _quantize_into(a, q[..., :K], q.shape[3], sc)
+            a = I8Act(q, K, sc)
+        self.fused[add_id] = True
+        return a
+
+    def _add_runner(self, n):
+        m = n.element
+        idx = self.res[n.id][3]
+
+        def run(x):
+            if self.fused.get(n.id):
+                return x[idx]
+            return m.forward(_as_float(x))
+        return run
+
+    def _res_relu_runner(self, n):
+        m = n.element
+        add_id = self.res_relu[n.id]
+
+        def run(x):
+            if self.fused.get(add_id):
+                return x
+            return m.forward(_as_float(x))
+        return run
+
     def _conv_runner(self, n):
         m = n.element
         out8 = self.int8[n.id]
         oscale = self.scale.get(n.id)
+        residual = n.id in self.res_conv
+        res_relu = residual and self.res[self.res_conv[n.id]][2] is not None
 
         def run(x):
             if not (isinstance(x, I8Act) or (isinstance(x, torch.Tensor) and x.is_cuda and x.dim() == 4)):
@@ -283,14 +384,17 @@ class Int8GraphPlan:
             K = m.nOutputPlane
             taps = _fwd_taps(R, S, ph, pw, m.dilationH, m.dilationW)
             geo = [N, H, W, m.Cp, OH, OW, m.strideH, m.strideW, R * S * m.Cp, K, K, OH, OW, 1, 1, 0, 0]
-            if out8:
+            add = self._residual_addend(n, N, OH, OW, K) if residual else None
+            relu = m.fuse_relu or (add is not None and res_relu)
+            ad, asc = (add.data, float(add.scale)) if add is not None else (None, 0.0)
+            if out8 and (add is not None or not residual):
                 dst, _ = self._dest(n, N, OH, OW, K, q.device)
                 geo[10] = dst.stride(2)
-                native.get().conv_i8(q, m.weight, dst, m.bias, xs, m.weightScale, geo, taps, m.fuse_relu, xsc,
-                                     float(oscale))
+                native.get().conv_i8(q, m.weight, dst, m.bias, xs, m.weightScale, geo, taps, relu, xsc,
+                                     float(oscale), ad, asc)
                 return I8Act(dst, K, oscale)
             y = torch.empty((N, K, OH, OW), dtype=BF16, device=q.device, memory_format=CL)
-            native.get().conv_i8(q, m.weight, y, m.bias, xs, m.weightScale, geo, taps, m.fuse_relu, xsc, 0.0)
+            native.get().conv_i8(q, m.weight, y, m.bias, xs, m.weightScale, geo, taps, relu, xsc, 0.0, ad, asc)
             return y
         return run
 

@@ -275,7 +275,7 @@ void quantize_act(const Tensor& x, const Tensor& q, const Tensor& amax, const Te
 // requantized with out_scale). `out` may be a channel slice of a wider NHWC buffer (rows geo[10] = ldo apart).
 void conv_i8(const Tensor& src, const Tensor& wt, const Tensor& out, const OptT& bias, const OptT& xscale,
              const Tensor& wscale, std::vector<int64_t> geo, std::vector<int64_t> taps, bool relu, double xs_const,
-             double out_scale) {
+             double out_scale, const OptT& addend, double add_scale) {
   TORCH_CHECK(geo.size() == 17, "conv_i8: bad geometry");
   TORCH_CHECK(src.scalar_type() == at::kChar && wt.scalar_type() == at::kChar && src.is_cuda() && wt.is_cuda() &&
                   src.is_contiguous() && wt.is_contiguous(), "conv_i8: src/wt must be contiguous int8 device tensors");
@@ -311,8 +311,20 @@ void conv_i8(const Tensor& src, const Tensor& wt, const Tensor& out, const OptT&
   TORCH_CHECK(!has_xs || (xscale->numel() >= a.Nb && xscale->scalar_type() == at::kFloat && xscale->is_cuda()),
               "conv_i8: xscale must hold N fp32 scales");
   TORCH_CHECK(wscale.numel() >= a.Ncol && wscale.scalar_type() == at::kFloat, "conv_i8: wscale");
+  const int8_t* add8 = nullptr;
+  long add_ld = 0;
+  if (addend && addend->defined()) {
+    TORCH_CHECK(addend->scalar_type() == at::kChar && addend->is_cuda() && addend->dim() == 4 &&
+                    addend->size(0) * addend->size(1) * addend->size(2) == (int64_t)a.M && addend->size(3) >= a.Ncol &&
+                    addend->stride(3) == 1 && addend->stride(1) == addend->size(2) * addend->stride(2) &&
+                    addend->stride(0) == addend->size(1) * addend->stride(1),
+                "conv_i8: addend must be int8 [N][OH][OW][>= Ncol] rows of one stride");
+    add8 = addend->data_ptr<int8_t>();
+    add_ld = addend->stride(2);
+  }
   const int rc = bigdl_conv_i8(&a, has_xs ? xscale->data_ptr<float>() : nullptr, (float)xs_const,
-                               wscale.data_ptr<float>(), mode, mode == 2 ? (float)(1.0 / out_scale) : 0.f, stream());
+                               wscale.data_ptr<float>(), mode, mode == 2 ? (float)(1.0 / out_scale) : 0.f, add8,
+                               (float)add_scale, add_ld, stream());
   TORCH_CHECK(rc == 0, "conv_i8: unsupported shape (channels must be a multiple of 16)");
 }
 
@@ -720,7 +732,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("P"), py::arg("C"), py::arg("Cp"), py::arg("static_amax") = false);
   m.def("conv_i8", &conv_i8, py::arg("src"), py::arg("wt"), py::arg("out"), py::arg("bias"), py::arg("xscale"),
         py::arg("wscale"), py::arg("geo"), py::arg("taps"), py::arg("relu"), py::arg("xs_const") = 0.0,
-        py::arg("out_scale") = 0.0);
+        py::arg("out_scale") = 0.0, py::arg("addend") = py::none(), py::arg("add_scale") = 0.0);
   m.def("pool_i8", &pool_i8);
   m.def("quantize_nchw_f32", &quantize_nchw_f32);
   m.def("quantize_rows_bf16", &quantize_rows_bf16);

@@ -124,8 +124,9 @@ int bigdl_quantize_act(const void* x, int is_bf16, int8_t* q, float* amax, float
                        int Cp, int static_amax, hipStream_t st);
 // xscale: [N] per-sample activation scales or nullptr (xs_const for the whole tensor); out_mode 0 bf16, 1 fp32,
 // 2 int8 requantized with out_inv = 1 / out_scale. Output rows are a->ldo elements apart.
+// add8 (optional): int8 residual addend [M][add_ld] with scale add_scale, summed before the ReLU.
 int bigdl_conv_i8(const ConvArgs* a, const float* xscale, float xs_const, const float* wscale, int out_mode,
-                  float out_inv, hipStream_t st);
+                  float out_inv, const int8_t* add8, float add_scale, long add_ld, hipStream_t st);
 // int8 NHWC pooling (max or average, same scale in and out; output rows ldo apart), graph-input quantizer
 // (fp32 NCHW -> int8 NHWC, static scale), bf16 rows -> int8 rows at a channel offset, int8 rows -> bf16.
 void bigdl_pool_i8(const int8_t* x, int8_t* y, int N, int H, int W, int Cp, int OH, int OW, int kh, int kw, int sh,

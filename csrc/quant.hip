@@ -124,6 +124,9 @@ struct I8Epi {
   const float* wscale;   // [Ncol]
   int out_mode;          // 0 bf16, 1 fp32, 2 int8
   float out_inv;         // int8 output: 1 / out_scale
+  const int8_t* add8;    // optional int8 residual addend [M][add_ld] (dequantized with add_scale, before the ReLU)
+  float add_scale;
+  long add_ld;
 };
 
 //
@@ -277,9 +280,21 @@ __global__ __launch_bounds__(256, 2) void conv_i8_glds_kernel(ConvArgs a, I8Epi 
     const v4f hi = *reinterpret_cast<const v4f*>(wl + gpos(p, 2 * q + 1));
     const float xs = ep.xscale ? ep.xscale[m / ohw] : ep.xs_const;
     float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    float ad[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (ep.add8) {          // residual (conv + sum, then ReLU): the shortcut's int8 tensor in its own scale
+      const int8_t* ap = ep.add8 + (size_t)m * ep.add_ld + n;
+      if (full8 && ((reinterpret_cast<uintptr_t>(ap) & 7) == 0)) {
+        const v2u u = *reinterpret_cast<const v2u*>(ap);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) ad[e] = (float)(int8_t)((u[e >> 2] >> (8 * (e & 3))) & 0xff) * ep.add_scale;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) ad[e] = n + e < a.Ncol ? (float)ap[e] * ep.add_scale : 0.f;
+      }
+    }
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      v[e] = v[e] * xs * wsc[e] + bs[e];
+      v[e] = v[e] * xs * wsc[e] + bs[e] + ad[e];
       if (a.relu) v[e] = fmaxf(v[e], 0.f);
     }
     const size_t off = (size_t)m * a.ldo + n;
@@ -494,11 +509,11 @@ int bigdl_quantize_act(const void* x, int is_bf16, int8_t* q, float* amax, float
 }
 
 int bigdl_conv_i8(const ConvArgs* a, const float* xscale, float xs_const, const float* wscale, int out_mode,
-                  float out_inv, hipStream_t st) {
+                  float out_inv, const int8_t* add8, float add_scale, long add_ld, hipStream_t st) {
   if (a->Cs % 16 != 0 || a->Kdim != a->ntaps * a->Cs || a->ntaps < 1 || a->ntaps > CONV_MAX_TAPS) return -1;
   if (a->M <= 0) return 0;
   const int nwg = ((a->M + 127) / 128) * ((a->Ncol + 127) / 128);
-  const I8Epi ep{xscale, xs_const, wscale, out_mode, out_inv};
+  const I8Epi ep{xscale, xs_const, wscale, out_mode, out_inv, add8, add_scale, add_ld};
   const bool fk = a->Cs % QBK == 0;
   if (a->Ncol <= 32) {
     const int g = ((a->M + 255) / 256) * ((a->Ncol + 31) / 32);

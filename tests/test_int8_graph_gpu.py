@@ -113,3 +113,25 @@ def test_int8_plan_graph_matches_float():
     assert n8 >= 8
     y2 = q.forward(x.to(dev))
     assert _rel(y2, y) < 1e-6
+
+
+def test_int8_plan_residual_conv_sum_fused():
+    """conv -> BN -> Scale -> CAddTable(shortcut) -> ReLU: BN / Scale fold into the conv, the int8 epilogue adds the
+    int8 shortcut and applies the ReLU; numerics vs the float graph."""
+    import os
+    import sys
+
+    sys.path.insert(0, os.path.dirname(__file__))
+    from test_graph_fusion_gpu import _inception_residual_graph
+
+    from bigdl_amd.quantized.quantizer import quantize
+
+    g = _inception_residual_graph()
+    x = torch.randn(8, 3, 16, 16)
+    ref = g.forward(x).clone()
+    dev = torch.device("cuda:0")
+    q = quantize(g.cloneModule().to(dev), calibration=x.to(dev))
+    y = q.forward(x.to(dev))
+    assert _rel(y, ref) < 0.08
+    plan = q._int8_plan
+    assert plan.res and all(plan.fused.get(a) for a in plan.res), "residual add was not fused into the int8 conv"
