@@ -292,6 +292,21 @@ class Optimizer:
         it = iter(self.dataset.data(train=True))
         wall0 = time.perf_counter()
         pending = []  # (iteration, loss tensor, records)
+        # liveness: a rank stuck (dead peer in a collective, hung kernel) exits instead of hanging the job
+        from ..utils.affinity import StepWatchdog
+        wd_s = float(Engine.getProperty("bigdl.step.timeout", 0) or 0)
+        watchdog = StepWatchdog(wd_s).start() if wd_s > 0 else None
+        try:
+            self._train_iterations(st, step, world, drop, it, wall0, pending, watchdog)
+        finally:
+            if watchdog is not None:
+                watchdog.stop()
+        step.gather_model()
+        if self.device.type == "cuda":
+            torch.cuda.synchronize()
+        return self.model
+
+    def _train_iterations(self, st, step, world, drop, it, wall0, pending, watchdog):
         while not self.endWhen(st):
             t0 = time.perf_counter()
             batch = next(it)
@@ -335,12 +350,10 @@ class Optimizer:
             self._validate(step)
             self._checkpoint(step)
             del n_ok
+            if watchdog is not None:
+                watchdog.kick()
         if pending:
             self._flush_losses(step, pending, wall0)
-        step.gather_model()
-        if self.device.type == "cuda":
-            torch.cuda.synchronize()
-        return self.model
 
     def _flush_losses(self, step, pending, wall0):
         if not pending:

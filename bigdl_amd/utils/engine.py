@@ -58,6 +58,15 @@ class _Engine:
             self.engine_type = engine_type
             if dist is None:
                 dist = world > 1
+            if (engine_type == EngineType.GPU and torch.cuda.is_available()
+                    and str(self.getProperty("bigdl.affinity", "1")) != "0"):
+                # pin this rank's host threads to its GPU's NUMA node before any pool thread exists
+                from .affinity import bind_to_gpu_numa
+
+                try:
+                    self.cpus = bind_to_gpu_numa(self.local_rank())
+                except OSError:
+                    self.cpus = None
             if dist:
                 self._init_dist()
             self._initialized = True
@@ -73,11 +82,17 @@ class _Engine:
         backend = os.environ.get("BIGDL_DIST_BACKEND", backend)
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29500")
+        # collective timeout (reference bigdl.network.timeout): with async error handling a rank whose peer died
+        # gets an error from RCCL instead of blocking forever
+        import datetime
+
+        timeout = datetime.timedelta(seconds=float(self.getProperty("bigdl.network.timeout", 1800)))
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
         if backend == "nccl":
             torch.cuda.set_device(self.local_rank())
-            td.init_process_group(backend, device_id=torch.device("cuda", self.local_rank()))
+            td.init_process_group(backend, device_id=torch.device("cuda", self.local_rank()), timeout=timeout)
         else:
-            td.init_process_group(backend)
+            td.init_process_group(backend, timeout=timeout)
         self._pg_owned = True
 
     def shutdown(self):

@@ -142,7 +142,8 @@ def _bcast_worker(rank, world, port, q):
     with torch.no_grad():
         m.modules[1].runningMean.fill_(float(rank))
     ModelBroadcast().broadcast(m)
-    q.put((rank, m.modules[0].weight.clone(), m.modules[1].runningMean.clone()))
+    # plain numpy payloads: a tensor would travel as a shared-memory handle that vanishes when this worker exits
+    q.put((rank, m.modules[0].weight.detach().clone().numpy(), m.modules[1].runningMean.clone().numpy()))
     dist.destroy_process_group()
 
 
@@ -159,7 +160,7 @@ def test_model_broadcast_gloo():
     ps = [ctx.Process(target=_bcast_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in ps:
         p.start()
-    res = dict((r, (w, rm)) for r, w, rm in (q.get(timeout=120) for _ in ps))
+    res = dict((r, (torch.from_numpy(w), torch.from_numpy(rm))) for r, w, rm in (q.get(timeout=120) for _ in ps))
     for p in ps:
         p.join(60)
     assert torch.equal(res[0][0], res[1][0])
