@@ -1,0 +1,54 @@
+"""Example applications (bigdl_amd.examples, reference S/example/**) run end to end on small synthetic data."""
+import pytest
+
+from bigdl_amd import examples
+
+
+def _run(name, argv):
+    m = examples.get(name)
+    return m.run(m.build_parser().parse_args(argv + ["--device", "cpu"] if "--device" in
+                                             m.build_parser().format_help() else argv))
+
+
+def test_text_classification_learns():
+    r = _run("textclassification", ["--maxEpoch", "6", "--maxSequenceLength", "72", "--embeddingDim", "32",
+                                     "--learningRate", "0.05"])
+    assert r["val_top1"] >= 0.8
+
+
+def test_ptb_lstm_language_model_perplexity_drops():
+    r = _run("languagemodel", ["--vocabSize", "50", "--hiddenSize", "32", "--numSteps", "10", "--batchSize", "16",
+                               "--maxEpoch", "3", "--syntheticWords", "6000"])
+    assert r["val_perplexity"] < 0.5 * r["val_perplexity_before"]
+
+
+def test_tree_lstm_sentiment_learns():
+    r = _run("treelstm", ["--hiddenSize", "48", "--epoch", "8", "--p", "0.1", "--synthetic", "400"])
+    assert r["root_accuracy"] >= 0.8
+
+
+def test_udf_predictor_query():
+    r = _run("udfpredictor", [])
+    assert r["rows"] == 60 and r["accuracy"] >= 0.8 and 0 < r["query_rows"] < 60
+
+
+def test_image_predictor_pipeline():
+    r = _run("imagepredictor", [])
+    assert r["images"] == 6 and all(1 <= p <= 10 for _, p in r["predictions"])
+
+
+def test_tf_load_and_save_roundtrip():
+    r = _run("tfloadandsave", [])
+    assert r["max_abs_diff"] < 1e-5
+
+
+@pytest.mark.parametrize("fmt", ["caffe", "bigdl", "torch"])
+def test_model_validator_loads_every_format(fmt):
+    r = _run("loadmodel", ["--modelType", fmt, "--model", "resnet50", "--classNum", "10", "--limit", "4",
+                           "--batchSize", "2", "--engine", "blas"])
+    assert r["images"] == 4 and 0.0 <= r["top5"] <= 1.0
+
+
+def test_examples_cli_lists_examples(capsys):
+    assert examples.main([]) == 2
+    assert "textclassification" in capsys.readouterr().out
