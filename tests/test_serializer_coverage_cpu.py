@@ -19,6 +19,8 @@ import pkgutil  # noqa: E402
 import bigdl_amd  # noqa: E402
 
 for _m in pkgutil.walk_packages(bigdl_amd.__path__, "bigdl_amd."):
+    if _m.name.endswith(".__main__"):    # CLI entry points run on import
+        continue
     importlib.import_module(_m.name)   # the complete registry, whatever other tests imported first
 
 
