@@ -170,6 +170,8 @@ def _split_ref(ref):
 _ACT = {"Relu": nn.ReLU, "Tanh": nn.Tanh, "Sigmoid": nn.Sigmoid, "Relu6": nn.ReLU6, "Elu": nn.ELU,
         "Softplus": nn.SoftPlus, "Softsign": nn.SoftSign}
 _PASSTHROUGH = {"Identity", "StopGradient", "Snapshot", "CheckNumerics"}
+_DATA_INPUT_OPS = ("Placeholder", "PlaceholderWithDefault", "QueueDequeueV2", "QueueDequeueManyV2",
+                   "QueueDequeueUpToV2", "ReaderReadV2")
 
 
 class _Loader:
@@ -187,6 +189,8 @@ class _Loader:
         self.gnodes = {}          # (name, port) -> graph Node
         self.layer_cache = {}     # shared-weight conversions keyed by the weight node
         self.input_nodes = []
+        self.context = {}         # variable name -> value (checkpoint bin file, tf_session.checkpoints)
+        self.var_bindings = []    # (variable name, module, attribute, layout) of variables that became parameters
 
     # -- helpers
     def op(self, name):
@@ -232,7 +236,10 @@ class _Loader:
         return v
 
     def _variable_init(self, name):
-        """Initial value of a VariableV2 from its Assign(var, const) initializer, if any."""
+        """Value of a VariableV2: the session context (checkpoint) when it holds the name, else the constant of
+        its Assign(var, const) initializer, if any."""
+        if name in self.context:
+            return torch.as_tensor(self.context[name]).clone()
         for n, node in self.nodes.items():
             if self.op(n) == "Assign":
                 ins = self.data_inputs(n)
@@ -241,10 +248,29 @@ class _Loader:
         return None
 
     # -- conversion
+    def _multi(self, name):
+        """Ops whose output is a Table of several tensors (every port, 0 included, is selected from it)."""
+        if name not in self.nodes:
+            return False
+        op = self.op(name)
+        if op in MULTI_OUTPUT:
+            return True
+        if op in ("QueueDequeueV2", "QueueDequeueManyV2", "QueueDequeueUpToV2"):
+            return len(attrs_of(self.nodes[name]).get("component_types") or []) > 1
+        return False
+
     def node_for(self, ref):
         name, port = ref
         if (name, port) in self.gnodes:
             return self.gnodes[(name, port)]
+        if self._multi(name):
+            base = self.gnodes.get((name, "*"))
+            if base is None:
+                base = self._convert(name)
+                self.gnodes[(name, "*")] = base
+            sel = nn.SelectTable(port + 1).setName(f"{name}:{port}").inputs(base)
+            self.gnodes[(name, port)] = sel
+            return sel
         if (name, 0) in self.gnodes and port:
             base = self.gnodes[(name, 0)]
             sel = nn.SelectTable(port + 1).setName(f"{name}:{port}").inputs(base)
@@ -260,9 +286,11 @@ class _Loader:
         feed = None
         for i, (iname, _) in enumerate(self.inputs):
             if name == iname:
-                feed = nn.Input(name if self.op(name) in ("Placeholder", "PlaceholderWithDefault") else name + "/input")
+                # placeholders and data-pipeline ops (queue dequeues, readers: Session.scala inputOp) ARE the input
+                data_op = self.op(name) in _DATA_INPUT_OPS
+                feed = nn.Input(name if data_op else name + "/input")
                 self.input_nodes.append((i, feed))
-                if self.op(name) in ("Placeholder", "PlaceholderWithDefault"):
+                if data_op:
                     return feed
         op = self.op(name)
         at = attrs_of(self.nodes[name])
@@ -295,6 +323,28 @@ class _Loader:
         v = self.const_value(ref)
         return v if isinstance(v, torch.Tensor) and v.is_floating_point() else None
 
+    def _var_of(self, ref):
+        """Name of the VariableV2 behind a weight reference (through Identity / 'read' nodes), or None."""
+        name = ref[0]
+        for _ in range(8):
+            if name not in self.nodes:
+                return None
+            op = self.op(name)
+            if op in ("VariableV2", "Variable"):
+                return name
+            if op not in _PASSTHROUGH:
+                return None
+            ins = self.data_inputs(name)
+            if not ins:
+                return None
+            name = ins[0][0]
+        return None
+
+    def _bind(self, ref, module, attr, layout):
+        var = self._var_of(ref)
+        if var is not None:
+            self.var_bindings.append((var, module, attr, layout))
+
     def _share(self, layer, key):
         """Layers converted from the same weight node share one weight tensor (reference: shared variables)."""
         first = self.layer_cache.get(key)
@@ -321,6 +371,7 @@ class _Loader:
                     layer, refs = inner
                     layer.bias = b.clone().float()
                     layer.gradBias = torch.zeros_like(layer.bias)
+                    self._bind(ins[1], layer, "bias", "id")
                     if ("bias", "gradBias") not in layer._params:
                         layer._params.append(("bias", "gradBias"))
                     if hasattr(layer, "withBias"):
@@ -336,6 +387,7 @@ class _Loader:
             lin = nn.Linear(W.shape[1], W.shape[0], withBias=False)
             lin.weight.data.copy_(W)
             self._share(lin, ("mm", ins[1][0], bool(at.get("transpose_b", False))))
+            self._bind(ins[1], lin, "weight", "id" if at.get("transpose_b", False) else "t")
             return lin, ins[:1]
         if op in ("Conv2D",) and len(ins) == 2:
             w = self._weight(ins[1])
@@ -352,13 +404,16 @@ class _Loader:
                                          dilationW=dw, dilationH=dh)
             conv.weight.data.copy_(w.permute(3, 2, 0, 1))
             self._share(conv, ("conv", ins[1][0]))
+            self._bind(ins[1], conv, "weight", "hwio")
             return conv, ins[:1]
         if op in ("BiasAdd", "BiasAddV1") and len(ins) == 2:
             b = self._weight(ins[1])
             if b is None:
                 return None
             fmt = at.get("data_format", "NHWC")
-            return _TFBias(b, fmt), ins[:1]
+            tb = _TFBias(b, fmt)
+            self._bind(ins[1], tb, "bias", "id")
+            return tb, ins[:1]
         if op in ("MaxPool", "AvgPool"):
             fmt = at.get("data_format", "NHWC")
             k, s = at["ksize"], at["strides"]
@@ -408,9 +463,15 @@ class _TFBias(nn.AutogradModule):
 
 
 def load_tf(graphFile, inputs, outputs, byteOrder=None, binFile=None, generatedBackward=True):
-    """Load a TensorFlow GraphDef into a bigdl_amd Graph (reference TensorflowLoader.load)."""
+    """Load a TensorFlow GraphDef into a bigdl_amd Graph (reference TensorflowLoader.load); ``binFile`` (a name ->
+    tensor file written by Session.saveParameters) supplies the variable values."""
     nodes = read_graph(graphFile)
-    return _Loader(nodes, list(inputs), list(outputs)).build()
+    loader = _Loader(nodes, list(inputs), list(outputs))
+    if binFile:
+        from .tf_session import load_bin
+
+        loader.context = load_bin(binFile)
+    return loader.build()
 
 
 def parse_graph(graphFile):
@@ -532,32 +593,51 @@ __all__ = ["load_tf", "save_tf", "read_graph", "parse_graph", "attrs_of", "tenso
 
 
 class Session:
-    """Train / run an imported TensorFlow graph (reference utils/tf/Session.scala BigDLSessionImpl.train/predict).
-    The graph is loaded between ``inputs`` and the given endpoints and optimised with the bigdl_amd Optimizer on
-    a bigdl_amd DataSet (TF input-queue sub-graphs are not executed: feed data through DataSet instead)."""
+    """Train / run an imported TensorFlow graph (reference utils/tf/Session.scala BigDLSessionImpl): placeholder-fed
+    training on a DataSet, or queue-fed training / prediction over the graph's own input pipeline
+    (interop/tf_session.py)."""
 
-    def __init__(self, graphFile, inputs):
-        self.graphFile, self.inputs = graphFile, list(inputs)
+    def __init__(self, graphFile, inputs=None, context=None):
+        from .tf_session import BigDLSession
 
-    def train(self, outputs, dataset, optMethod, criterion, endWhen, batchSize=None):
-        from ..optim import Optimizer
-        model = load_tf(self.graphFile, self.inputs, outputs)
-        opt = Optimizer(model=model, dataset=dataset, criterion=criterion, batchSize=batchSize)
-        opt.setOptimMethod(optMethod).setEndWhen(endWhen)
-        return opt.optimize()
+        self._s = BigDLSession(graphFile, inputs, context)
+        self.graphFile, self.inputs = graphFile, list(inputs or [])
 
-    def predict(self, outputs, x):
+    def train(self, outputs, dataset=None, optMethod=None, criterion=None, endWhen=None, batchSize=None,
+              isDataBatch=False, loss=None):
+        return self._s.train(outputs, dataset, optMethod, criterion, endWhen, batchSize, isDataBatch, loss)
+
+    def predict(self, outputs, x=None, isDataBatch=False, batchSize=32):
+        if x is None:
+            return self._s.predict(outputs, isDataBatch, batchSize)
         model = load_tf(self.graphFile, self.inputs, outputs)
         model.evaluate()
         with torch.no_grad():
             return model.forward(x)
 
+    def saveParameters(self, binFile):
+        self._s.saveParameters(binFile)
+        return self
+
+    def variables(self):
+        return self._s.variables()
+
 
 class TensorflowLoader:
-    """Reference S/utils/tf/TensorflowLoader.scala:55 ``load(graphFile, inputs, outputs, byteOrder, binFile)``."""
+    """Reference S/utils/tf/TensorflowLoader.scala:55 ``load(graphFile, inputs, outputs, byteOrder, binFile)``,
+    :88 ``checkpoints(graphFile, binFile)``."""
 
     load = staticmethod(load_tf)
     parse = staticmethod(parse_graph)
+
+    @staticmethod
+    def checkpoints(graphFile, binFile, byteOrder=None):
+        from .tf_session import checkpoints
+
+        s = Session.__new__(Session)
+        s._s = checkpoints(graphFile, binFile)
+        s.graphFile, s.inputs = graphFile, []
+        return s
 
 
 class TensorflowSaver:

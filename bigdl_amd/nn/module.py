@@ -37,6 +37,13 @@ class Module:
         return load_tf(path, inputs, outputs, byteOrder, binFile, generatedBackward)
 
     @staticmethod
+    def tensorflowCheckpoints(graphFile, binFile, byteOrder=None):
+        """A TensorFlow Session whose variables come from ``binFile`` (reference Module.scala:108)."""
+        from ..interop.tensorflow import TensorflowLoader
+
+        return TensorflowLoader.checkpoints(graphFile, binFile, byteOrder)
+
+    @staticmethod
     def loadONNX(path):
         from ..interop.onnx import load_onnx
 
