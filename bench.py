@@ -81,6 +81,13 @@ def main():
 
     run = lambda: step.step(x, y)  # noqa: E731
     graph = None
+    if args.graph and world > 1:
+        import torch.distributed as dist
+
+        if dist.get_backend() != "nccl":
+            # gloo collectives (single-GPU multi-rank rehearsal) run on the host: nothing to capture
+            print("[bench] non-RCCL backend: eager launches", file=sys.stderr)
+            args.graph = 0
     if args.graph:
         from bigdl_amd.optim.graphed import GraphedTrainStep
 
