@@ -53,7 +53,10 @@ def main():
 
     from bigdl_amd.utils.engine import Engine
 
-    Engine.init(master=f"local[{world}]", dist=world > 1)
+    # BIGDL_FORCE_COLLECTIVES=1 (under torch.distributed.run) runs the full multi-GPU step on one rank: RCCL
+    # reduce-scatter / all-gather, bucketed overlap and the segmented HIP graph, to price their overhead
+    force = os.environ.get("BIGDL_FORCE_COLLECTIVES") == "1" and "MASTER_PORT" in os.environ
+    Engine.init(master=f"local[{world}]", dist=world > 1 or force)
 
     from bigdl_amd import nn
     from bigdl_amd.models.resnet import DatasetType, ResNet
@@ -81,7 +84,7 @@ def main():
 
     run = lambda: step.step(x, y)  # noqa: E731
     graph = None
-    if args.graph and world > 1:
+    if args.graph and (world > 1 or force):
         import torch.distributed as dist
 
         if dist.get_backend() != "nccl":
