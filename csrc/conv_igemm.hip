@@ -1311,7 +1311,9 @@ long bigdl_conv_wgrad_plan(WgradArgs* a) {
   const int tiles = ((a->Ncol + WT - 1) / WT) * ((a->Kdim + WT - 1) / WT);
   if (conv_impl() < 1 || wgrad_prefers_atomic(a)) { a->splits = 0; return 0; }
   // workspace split-K: ~4 workgroups per CU (two resident waves of 2/CU), >= 4 LDS stages per split
-  int splits = (1024 + tiles - 1) / tiles;
+  // (BIGDL_WGRAD_WGS overrides the workgroup target for A/B runs: fewer splits = fewer partials to reduce)
+  static const int target = [] { const char* e = getenv("BIGDL_WGRAD_WGS"); return e ? atoi(e) : 1024; }();
+  int splits = (target + tiles - 1) / tiles;
   const int maxsplit = (a->M + 8 * WBM - 1) / (8 * WBM);
   if (splits > maxsplit) splits = maxsplit;
   if (splits < 1) splits = 1;

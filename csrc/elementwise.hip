@@ -405,6 +405,49 @@ __global__ void sgd_kernel(float* __restrict__ w, const float* __restrict__ g, f
   }
 }
 
+// 4 elements per lane (16-byte fp32 loads / stores, 8-byte bf16 shadow store); the weight-decay segment is found by
+// one binary search per 4 elements and then stepped forward (segments span thousands of elements).
+__global__ void sgd4_kernel(float* __restrict__ w, const float* __restrict__ g, float* __restrict__ mom,
+                            bf16_t* __restrict__ w16, long n4, const float* __restrict__ lr_dev, float lr, float wd,
+                            float momentum, float dampening, int nesterov, int first, const long* __restrict__ seg_off,
+                            const float* __restrict__ seg_wd, int nseg, long base) {
+  const float rate = lr_dev ? lr_dev[0] : lr;
+  GRID_STRIDE(i, n4) {
+    const v4f wv = reinterpret_cast<const v4f*>(w)[i];
+    const v4f gv = reinterpret_cast<const v4f*>(g)[i];
+    v4f mv = {0.f, 0.f, 0.f, 0.f};
+    if (momentum != 0.f && !first) mv = reinterpret_cast<const v4f*>(mom)[i];
+    float dec[4] = {wd, wd, wd, wd};
+    if (nseg) {
+      const long g0 = base + 4 * i;
+      int lo = 0, hi = nseg - 1;
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (seg_off[mid] <= g0) lo = mid; else hi = mid - 1;
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        while (lo + 1 < nseg && seg_off[lo + 1] <= g0 + e) ++lo;
+        dec[e] += seg_wd[lo];
+      }
+    }
+    v4f wo, mo;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float d = gv[e] + dec[e] * wv[e];
+      if (momentum != 0.f) {
+        const float b = first ? d : momentum * mv[e] + (1.f - dampening) * d;
+        mo[e] = b;
+        d = nesterov ? d + momentum * b : b;
+      }
+      wo[e] = wv[e] - rate * d;
+    }
+    reinterpret_cast<v4f*>(w)[i] = wo;
+    if (momentum != 0.f) reinterpret_cast<v4f*>(mom)[i] = mo;
+    if (w16) reinterpret_cast<v2u*>(w16)[i] = v2u{pack2bf(wo[0], wo[1]), pack2bf(wo[2], wo[3])};
+  }
+}
+
 __global__ void adam_kernel(float* __restrict__ w, const float* __restrict__ g, float* __restrict__ m,
                             float* __restrict__ v, bf16_t* __restrict__ w16, long n, float lr, float b1, float b2,
                             float eps, float wd, float bc1, float bc2) {
@@ -559,8 +602,15 @@ void bigdl_softmax_xent(const uint16_t* lb, const float* lf, const float* labels
 void bigdl_sgd_step(float* w, const float* g, float* mom, uint16_t* w16, long n, const float* lr_dev, float lr,
                     float wd, float momentum, float dampening, int nesterov, int first, const long* seg_off,
                     const float* seg_wd, int nseg, long base, hipStream_t st) {
-  sgd_kernel<<<grid_cap(n), 256, 0, st>>>(w, g, mom, w16, n, lr_dev, lr, wd, momentum, dampening, nesterov, first,
-                                          seg_off, seg_wd, nseg, base);
+  const bool vec = (n & 3) == 0 && ((reinterpret_cast<uintptr_t>(w) | reinterpret_cast<uintptr_t>(g) |
+                                      reinterpret_cast<uintptr_t>(mom)) & 15) == 0 &&
+                   (reinterpret_cast<uintptr_t>(w16) & 7) == 0;
+  if (vec)
+    sgd4_kernel<<<grid_cap(n / 4), 256, 0, st>>>(w, g, mom, w16, n / 4, lr_dev, lr, wd, momentum, dampening, nesterov,
+                                                 first, seg_off, seg_wd, nseg, base);
+  else
+    sgd_kernel<<<grid_cap(n), 256, 0, st>>>(w, g, mom, w16, n, lr_dev, lr, wd, momentum, dampening, nesterov, first,
+                                            seg_off, seg_wd, nseg, base);
   HIP_LAUNCH_CHECK();
 }
 void bigdl_adam_step(float* w, const float* g, float* m, float* v, uint16_t* w16, long n, float lr, float beta1,
