@@ -245,3 +245,47 @@ def test_dgrad_epilogue_bn_reduction_matches_separate_pass(monkeypatch):
     assert res["1"][2] == n_bn - 5
     assert _rel(res["1"][0], res["0"][0]) < 2e-2
     assert _rel(res["1"][1], res["0"][1]) < 2e-2
+
+
+def test_resnet50_every_layer_matches_fp32_on_its_own_input():
+    """Pins every conv and BatchNorm of the full (fused) ResNet-50 training forward: each layer's bf16 GPU output
+    is compared with the fp32 CPU layer applied to the SAME (GPU-produced) input, so a systematic per-layer error
+    anywhere in the 50-layer network cannot hide behind the loose whole-network tolerance above."""
+    from bigdl_amd import nn
+    from bigdl_amd.models.resnet import ResNet
+    from bigdl_amd.nn.fusion import fuse_for_training
+    from bigdl_amd.utils.random_generator import RNG
+
+    RNG.setSeed(7)
+    cpu = ResNet(1000, 50, dataSet="ImageNet")
+    gpu = copy.deepcopy(cpu).to("cuda")
+    fuse_for_training(gpu)
+    resid_bns = {id(m._residual_plan[2]) for m in gpu.flattened_layers()
+                 if isinstance(m, nn.Sequential) and getattr(m, "_residual_plan", None)}
+    pairs = [(g, c) for g, c in zip(gpu.flattened_layers(), cpu.flattened_layers())
+             if isinstance(g, (nn.SpatialConvolution, nn.BatchNormalization)) and id(g) not in resid_bns]
+    seen = []
+    for g, c in pairs:
+        orig = g.updateOutput
+
+        def hook(inp, _g=g, _c=c, _orig=orig):
+            out = _orig(inp)
+            seen.append((_g, _c, inp.detach().float().cpu().clone(), out.detach().float().cpu().clone()))
+            return out
+        g.updateOutput = hook
+    torch.manual_seed(0)
+    gpu.forward(torch.randn(4, 3, 224, 224).cuda())
+    for g, _ in pairs:
+        del g.updateOutput
+    assert len(seen) == len(pairs) >= 60
+    worst = 0.0
+    for g, c, inp, out in seen:
+        c.training()
+        with torch.no_grad():
+            ref = c.forward(inp.contiguous())
+        if getattr(g, "fuse_relu", False):
+            ref = torch.relu(ref)
+        r = _rel(out, ref)
+        worst = max(worst, r)
+        assert r < 2e-2, (type(g).__name__, g.getName(), r)
+    assert worst < 2e-2
