@@ -6,7 +6,8 @@ HardShrink, LogSigmoid, SoftMax, SoftMin, LogSoftMax, Exp, Log, Sqrt, Square, Ab
 AddConstant, MulConstant, Negative, GradientReversal, Mul, Add, CMul, CAdd, Scale.
 
 ReLU has an explicit native path (csrc/elementwise.hip, and is fused into the producing conv / BN on the
-GPU engine — see nn/fusion.py); the rest derive their backward from a functional forward.
+GPU engine — see nn/fusion.py); the point-wise activations below run native forward / backward kernels on the GPU
+(csrc/activation.hip, ``_NativeActivation``); the rest derive their backward from a functional forward.
 """
 import torch
 import torch.nn.functional as F
@@ -45,7 +46,61 @@ def _dense(t):
     return t.is_contiguous() or (t.dim() == 4 and t.is_contiguous(memory_format=CL))
 
 
-class Threshold(AutogradModule):
+# kind codes of csrc/activation.hip
+_NATIVE_KIND = {"Tanh": 0, "Sigmoid": 1, "ELU": 2, "LeakyReLU": 3, "ReLU6": 4, "SoftPlus": 5, "SoftSign": 6,
+                "HardTanh": 7, "HardSigmoid": 8, "LogSigmoid": 9, "TanhShrink": 10, "SoftShrink": 11,
+                "HardShrink": 12, "Threshold": 13, "Exp": 14, "Log": 15, "Sqrt": 16, "Square": 17, "Abs": 18}
+
+
+class _NativeActivation(AutogradModule):
+    """Point-wise layer with a native GPU forward / backward (csrc/activation.hip) for dense bf16 / fp32 device
+    tensors; anything else (CPU, other dtypes, strided views) takes the autograd path of ``fn``."""
+
+    _kind = None
+
+    def _native_args(self):
+        return 0.0, 0.0
+
+    def _native_ok(self, x):
+        return (isinstance(x, torch.Tensor) and x.is_cuda and x.dtype in (BF16, torch.float32) and _dense(x)
+                and self._kind is not None)
+
+    def updateOutput(self, input):
+        if self._native_ok(input):
+            from ..ops import native
+
+            a, b = self._native_args()
+            y = torch.empty_like(input)
+            native.get().act_fwd(input, y, _NATIVE_KIND[self._kind], float(a), float(b))
+            self._ag = None
+            self._native_x = input
+            return y
+        self._native_x = None
+        return super().updateOutput(input)
+
+    def updateGradInput(self, input, gradOutput):
+        x = getattr(self, "_native_x", None)
+        if x is not None:
+            from ..ops import native
+
+            a, b = self._native_args()
+            y = self.output
+            g = gradOutput.to(x.dtype)
+            if g.stride() != x.stride():
+                g = g.contiguous(memory_format=CL) if x.dim() == 4 and not x.is_contiguous() else g.contiguous()
+            dx = torch.empty_like(x)
+            native.get().act_bwd(x, y, g, dx, _NATIVE_KIND[self._kind], float(a), float(b))
+            self._pending_param_grads = None
+            return dx
+        return super().updateGradInput(input, gradOutput)
+
+
+class Threshold(_NativeActivation):
+    _kind = "Threshold"
+
+    def _native_args(self):
+        return self.threshold, self.value
+
     def __init__(self, th=1e-6, v=0.0, ip=False):
         super().__init__()
         self.threshold, self.value, self.inplace = th, v, ip
@@ -63,7 +118,9 @@ class BinaryThreshold(AutogradModule):
         return (x > self.threshold).to(x.dtype)
 
 
-class ReLU6(AutogradModule):
+class ReLU6(_NativeActivation):
+    _kind = "ReLU6"
+
     def __init__(self, inplace=False):
         super().__init__()
 
@@ -71,7 +128,12 @@ class ReLU6(AutogradModule):
         return torch.clamp(x, 0.0, 6.0)
 
 
-class LeakyReLU(AutogradModule):
+class LeakyReLU(_NativeActivation):
+    _kind = "LeakyReLU"
+
+    def _native_args(self):
+        return self.negval, 0.0
+
     def __init__(self, negval=0.01, inplace=False):
         super().__init__()
         self.negval = negval
@@ -80,7 +142,12 @@ class LeakyReLU(AutogradModule):
         return F.leaky_relu(x, self.negval)
 
 
-class ELU(AutogradModule):
+class ELU(_NativeActivation):
+    _kind = "ELU"
+
+    def _native_args(self):
+        return self.alpha, 0.0
+
     def __init__(self, alpha=1.0, inplace=False):
         super().__init__()
         self.alpha = alpha
@@ -133,22 +200,33 @@ class SReLU(AutogradModule):
         return torch.where(x <= tl, tl + al * (x - tl), y)
 
 
-class Sigmoid(AutogradModule):
+class Sigmoid(_NativeActivation):
+    _kind = "Sigmoid"
+
     def fn(self, x):
         return torch.sigmoid(x)
 
 
-class HardSigmoid(AutogradModule):
+class HardSigmoid(_NativeActivation):
+    _kind = "HardSigmoid"
+
     def fn(self, x):
         return torch.clamp(0.2 * x + 0.5, 0.0, 1.0)
 
 
-class Tanh(AutogradModule):
+class Tanh(_NativeActivation):
+    _kind = "Tanh"
+
     def fn(self, x):
         return torch.tanh(x)
 
 
-class HardTanh(AutogradModule):
+class HardTanh(_NativeActivation):
+    _kind = "HardTanh"
+
+    def _native_args(self):
+        return self.minValue, self.maxValue
+
     def __init__(self, minValue=-1.0, maxValue=1.0, inplace=False):
         super().__init__()
         self.minValue, self.maxValue = minValue, maxValue
@@ -162,12 +240,19 @@ class Clamp(HardTanh):
         super().__init__(min, max)
 
 
-class TanhShrink(AutogradModule):
+class TanhShrink(_NativeActivation):
+    _kind = "TanhShrink"
+
     def fn(self, x):
         return x - torch.tanh(x)
 
 
-class SoftPlus(AutogradModule):
+class SoftPlus(_NativeActivation):
+    _kind = "SoftPlus"
+
+    def _native_args(self):
+        return self.beta, 0.0
+
     def __init__(self, beta=1.0):
         super().__init__()
         self.beta = beta
@@ -176,12 +261,19 @@ class SoftPlus(AutogradModule):
         return F.softplus(x, self.beta, 20.0)
 
 
-class SoftSign(AutogradModule):
+class SoftSign(_NativeActivation):
+    _kind = "SoftSign"
+
     def fn(self, x):
         return x / (1 + x.abs())
 
 
-class SoftShrink(AutogradModule):
+class SoftShrink(_NativeActivation):
+    _kind = "SoftShrink"
+
+    def _native_args(self):
+        return self.lambd, 0.0
+
     def __init__(self, lambd=0.5):
         super().__init__()
         self.lambd = lambd
@@ -190,7 +282,12 @@ class SoftShrink(AutogradModule):
         return F.softshrink(x, self.lambd)
 
 
-class HardShrink(AutogradModule):
+class HardShrink(_NativeActivation):
+    _kind = "HardShrink"
+
+    def _native_args(self):
+        return self.lambd, 0.0
+
     def __init__(self, lambd=0.5):
         super().__init__()
         self.lambd = lambd
@@ -199,7 +296,9 @@ class HardShrink(AutogradModule):
         return F.hardshrink(x, self.lambd)
 
 
-class LogSigmoid(AutogradModule):
+class LogSigmoid(_NativeActivation):
+    _kind = "LogSigmoid"
+
     def fn(self, x):
         return F.logsigmoid(x)
 
@@ -231,27 +330,37 @@ class LogSoftMax(AutogradModule):
         return nnk.log_softmax(x).to(x.dtype)          # last dim; GPU: one wave per row (csrc/nn_misc.hip)
 
 
-class Exp(AutogradModule):
+class Exp(_NativeActivation):
+    _kind = "Exp"
+
     def fn(self, x):
         return torch.exp(x)
 
 
-class Log(AutogradModule):
+class Log(_NativeActivation):
+    _kind = "Log"
+
     def fn(self, x):
         return torch.log(x)
 
 
-class Sqrt(AutogradModule):
+class Sqrt(_NativeActivation):
+    _kind = "Sqrt"
+
     def fn(self, x):
         return torch.sqrt(x)
 
 
-class Square(AutogradModule):
+class Square(_NativeActivation):
+    _kind = "Square"
+
     def fn(self, x):
         return x * x
 
 
-class Abs(AutogradModule):
+class Abs(_NativeActivation):
+    _kind = "Abs"
+
     def fn(self, x):
         return x.abs()
 

@@ -1,9 +1,9 @@
 """Optimization methods beyond SGD (reference S/optim/: Adam.scala:36, ParallelAdam.scala:38, Adagrad.scala,
 Adadelta.scala, Adamax.scala, RMSprop.scala, Ftrl.scala:39, LBFGS.scala:48, LineSearch.scala, LarsSGD.scala:47).
 
-All operate on the flat parameter tensor (or this rank's ZeRO-1 shard). Adam uses the fused native kernel on
-GPU (csrc/elementwise.hip adam_kernel, writing the bf16 compute copy in the same pass); the others are short
-sequences of vectorised tensor ops over the flat buffer.
+All operate on the flat parameter tensor (or this rank's ZeRO-1 shard). On the GPU, Adam (csrc/elementwise.hip
+adam_kernel) and Adagrad / RMSprop / Adadelta / Adamax / Ftrl (csrc/optim.hip) are single fused passes that also
+write the bf16 compute copy of the weights; on the CPU they are short sequences of tensor ops over the flat buffer.
 """
 import math
 
@@ -80,9 +80,13 @@ class Adagrad(OptimMethod):
         fx, g = feval(x)
         n = self.state.get("evalCounter", 0)
         clr = self.learningRate / (1 + n * self.learningRateDecay)
+        var = _state(self, "paramVariance", x)
+        if native_ok(x, g, var):
+            native.get().optim_step(0, x, g, var, None, self._shadow16, clr, self.weightDecay, 0.0, 0.0, 0.0)
+            self.state["evalCounter"] = n + 1
+            return x, [fx]
         if self.weightDecay:
             g = g + self.weightDecay * x
-        var = _state(self, "paramVariance", x)
         var.addcmul_(g, g)
         x.addcdiv_(g, var.sqrt().add_(1e-10), value=-clr)
         self.state["evalCounter"] = n + 1
@@ -100,6 +104,10 @@ class Adadelta(OptimMethod):
         rho, eps = self.decayRate, self.Epsilon
         var = _state(self, "paramVariance", x)
         acc = _state(self, "accDelta", x)
+        if native_ok(x, g, var, acc):
+            native.get().optim_step(2, x, g, var, acc, self._shadow16, rho, eps, 0.0, 0.0, 0.0)
+            self.state["evalCounter"] = self.state.get("evalCounter", 0) + 1
+            return x, [fx]
         var.mul_(rho).addcmul_(g, g, value=1 - rho)
         delta = (acc + eps).sqrt().div_((var + eps).sqrt()).mul_(g)
         x.sub_(delta)
@@ -120,6 +128,10 @@ class Adamax(OptimMethod):
         self.state["evalCounter"] = t
         m = _state(self, "m", x)
         u = _state(self, "u", x)
+        if native_ok(x, g, m, u):
+            native.get().optim_step(3, x, g, m, u, self._shadow16, self.learningRate / (1 - self.beta1 ** t),
+                                    self.beta1, self.beta2, self.Epsilon, 0.0)
+            return x, [fx]
         m.mul_(self.beta1).add_(g, alpha=1 - self.beta1)
         torch.maximum(u * self.beta2, g.abs() + self.Epsilon, out=u)
         x.addcdiv_(m, u, value=-self.learningRate / (1 - self.beta1 ** t))
@@ -138,6 +150,10 @@ class RMSprop(OptimMethod):
         n = self.state.get("evalCounter", 0)
         clr = self.learningRate / (1 + n * self.learningRateDecay)
         ms = _state(self, "sumSquare", x)
+        if native_ok(x, g, ms):
+            native.get().optim_step(1, x, g, ms, None, self._shadow16, clr, self.decayRate, self.Epsilon, 0.0, 0.0)
+            self.state["evalCounter"] = n + 1
+            return x, [fx]
         ms.mul_(self.decayRate).addcmul_(g, g, value=1 - self.decayRate)
         x.addcdiv_(g, ms.sqrt().add_(self.Epsilon), value=-clr)
         self.state["evalCounter"] = n + 1
@@ -161,6 +177,10 @@ class Ftrl(OptimMethod):
         lr, p = self.learningRate, self.learningRatePower
         accum = _state(self, "accum", x, self.initialAccumulatorValue)
         linear = _state(self, "linear", x)
+        if native_ok(x, g, accum, linear):
+            native.get().optim_step(4, x, g, accum, linear, self._shadow16, lr, p, self.l1, self.l2, self.l2s)
+            self.state["evalCounter"] = self.state.get("evalCounter", 0) + 1
+            return x, [fx]
         gs = g + 2 * self.l2s * x if self.l2s > 0 else g
         acc_new = accum + g * g
         if p == -0.5:

@@ -241,6 +241,15 @@ void adam_step(const Tensor& w, const Tensor& g, const Tensor& m, const Tensor& 
   bigdl_adam_step(mf(w, "w"), cf(g, "g"), mf(m, "m"), mf(v, "v"), ombf(w16, "w16"), w.numel(), (float)lr, (float)b1,
                   (float)b2, (float)eps, (float)wd, (float)bc1, (float)bc2, stream());
 }
+void optim_step(int64_t method, const Tensor& x, const Tensor& g, const Tensor& s1, const OptT& s2, const OptT& w16,
+                double a, double b, double c, double d, double e) {
+  TORCH_CHECK(g.numel() == x.numel() && s1.numel() == x.numel() && (!s2 || !s2->defined() || s2->numel() == x.numel())
+                  && (!w16 || !w16->defined() || w16->numel() >= x.numel()), "optim_step: buffer sizes");
+  for (const Tensor* t : {&x, &g, &s1}) TORCH_CHECK(t->is_contiguous(), "optim_step: contiguous buffers");
+  const OptimHP hp{(float)a, (float)b, (float)c, (float)d, (float)e};
+  TORCH_CHECK(bigdl_optim_step((int)method, &hp, mf(x, "x"), cf(g, "g"), mf(s1, "s1"), omf(s2, "s2"),
+                               ombf(w16, "w16"), x.numel(), stream()) == 0, "optim_step: unknown method");
+}
 void sumsq(const Tensor& x, const Tensor& out) { bigdl_sumsq(cf(x, "x"), mf(out, "out"), x.numel(), stream()); }
 void scale_f32(const Tensor& x, const OptT& sdev, double s) {
   bigdl_scale_f32(mf(x, "x"), x.numel(), ocf(sdev, "scale"), (float)s, stream());
@@ -362,6 +371,28 @@ void dequantize_rows(const Tensor& q, const Tensor& y, int64_t P, int64_t C, int
   TORCH_CHECK(q.scalar_type() == at::kChar && y.scalar_type() == at::kBFloat16 && y.numel() == P * C &&
                   q.numel() >= (P - 1) * ld + C, "dequantize_rows: shapes");
   bigdl_dequantize_rows(q.data_ptr<int8_t>(), (uint16_t*)y.data_ptr(), P, C, ld, (float)scale, stream());
+}
+
+// point-wise activations (csrc/activation.hip)
+static bool act_dense(const Tensor& t) {
+  return t.is_contiguous() || (t.dim() == 4 && t.is_contiguous(at::MemoryFormat::ChannelsLast));
+}
+void act_fwd(const Tensor& x, const Tensor& y, int64_t kind, double a, double b) {
+  const bool bf = x.scalar_type() == at::kBFloat16;
+  TORCH_CHECK(x.is_cuda() && (bf || x.scalar_type() == at::kFloat) && y.scalar_type() == x.scalar_type() &&
+                  y.numel() == x.numel() && act_dense(x) && x.strides() == y.strides(),
+              "act_fwd: x / y dense bf16 or fp32 device tensors of one layout");
+  TORCH_CHECK(bigdl_act_fwd(x.data_ptr(), y.data_ptr(), x.numel(), bf ? 1 : 0, (int)kind, (float)a, (float)b,
+                            stream()) == 0, "act_fwd: unknown kind");
+}
+void act_bwd(const Tensor& x, const Tensor& y, const Tensor& dy, const Tensor& dx, int64_t kind, double a, double b) {
+  const bool bf = x.scalar_type() == at::kBFloat16;
+  TORCH_CHECK(x.is_cuda() && (bf || x.scalar_type() == at::kFloat) && act_dense(x), "act_bwd: x");
+  for (const Tensor* t : {&y, &dy, &dx})
+    TORCH_CHECK(t->scalar_type() == x.scalar_type() && t->numel() == x.numel() && t->strides() == x.strides(),
+                "act_bwd: y / dy / dx must match x (dtype, size, layout)");
+  TORCH_CHECK(bigdl_act_bwd(x.data_ptr(), y.data_ptr(), dy.data_ptr(), dx.data_ptr(), x.numel(), bf ? 1 : 0,
+                            (int)kind, (float)a, (float)b, stream()) == 0, "act_bwd: unknown kind");
 }
 
 // detection (csrc/detection.hip)
@@ -723,6 +754,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("softmax_xent", &softmax_xent);
   m.def("sgd_step", &sgd_step, py::arg("w"), py::arg("g"), py::arg("mom"), py::arg("w16"), py::arg("lr"), py::arg("wd"), py::arg("momentum"), py::arg("dampening"), py::arg("nesterov"), py::arg("first"), py::arg("lr_dev") = py::none(), py::arg("seg_off") = py::none(), py::arg("seg_wd") = py::none(), py::arg("base") = 0);
   m.def("adam_step", &adam_step);
+  m.def("optim_step", &optim_step);
   m.def("sumsq", &sumsq);
   m.def("scale_f32", &scale_f32);
   m.def("lstm_cell_fwd", &lstm_cell_fwd);
@@ -734,6 +766,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("wscale"), py::arg("geo"), py::arg("taps"), py::arg("relu"), py::arg("xs_const") = 0.0,
         py::arg("out_scale") = 0.0, py::arg("addend") = py::none(), py::arg("add_scale") = 0.0);
   m.def("pool_i8", &pool_i8);
+  m.def("act_fwd", &act_fwd);
+  m.def("act_bwd", &act_bwd);
   m.def("quantize_nchw_f32", &quantize_nchw_f32);
   m.def("quantize_rows_bf16", &quantize_rows_bf16);
   m.def("dequantize_rows", &dequantize_rows);

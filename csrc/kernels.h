@@ -210,6 +210,20 @@ typedef struct {
 int bigdl_attn_fwd(const AttnCall* c, hipStream_t st);
 int bigdl_attn_bwd(const AttnCall* c, float* delta_ws, hipStream_t st);
 
+// Adaptive OptimMethod updates on flat fp32 buffers (csrc/optim.hip): method 0 Adagrad (a = lr, b = weight decay),
+// 1 RMSprop (a = lr, b = decay rate, c = eps), 2 Adadelta (a = decay rate, b = eps), 3 Adamax (a = lr / (1 - b1^t),
+// b = b1, c = b2, d = eps), 4 Ftrl (a = lr, b = lr power, c = l1, d = l2, e = l2 shrinkage); s1 / s2 are the state
+// buffers (s2 may be null for Adagrad / RMSprop); w16 (optional) receives the bf16 copy of the updated weights.
+typedef struct { float a, b, c, d, e; } OptimHP;
+int bigdl_optim_step(int method, const OptimHP* hp, float* x, const float* g, float* s1, float* s2, uint16_t* w16,
+                     long n, hipStream_t st);
+
+// Point-wise activations (csrc/activation.hip): kind codes in bigdl_amd/nn/activation.py _NATIVE_KIND; x, y, dy, dx
+// are contiguous bf16 (bf16 = 1) or fp32 buffers of n elements; returns -1 for an unknown kind.
+int bigdl_act_fwd(const void* x, void* y, long n, int bf16, int kind, float a, float b, hipStream_t st);
+int bigdl_act_bwd(const void* x, const void* y, const void* dy, void* dx, long n, int bf16, int kind, float a,
+                  float b, hipStream_t st);
+
 // Direct grouped / depthwise convolution, fp32 NCHW (csrc/grouped_conv.hip). pass 0 forward (x, w, b -> y),
 // 1 data gradient (dy, w -> dx), 2 weight / bias gradient (dy, x -> dwt, db accumulated).
 typedef struct {
