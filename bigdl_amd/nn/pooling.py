@@ -1,10 +1,12 @@
 """Pooling layers. Reference: S/nn/SpatialMaxPooling.scala:62, SpatialAveragePooling.scala:62,
 VolumetricMaxPooling.scala, VolumetricAveragePooling.scala, TemporalMaxPooling.scala; primitives in
-NNPrimitive.scala:654-1051. GPU engine: NHWC kernels in csrc/elementwise.hip."""
+NNPrimitive.scala:654-1051. GPU engine: 2D NHWC kernels in csrc/elementwise.hip, 3D / temporal pooling on the
+N-d window kernels of csrc/pool_nd.hip."""
 import torch
 import torch.nn.functional as F
 
 from ..ops import pool as P
+from ..ops import pool_nd as PN
 from .abstractnn import AutogradModule, TensorModule
 
 BF16 = torch.bfloat16
@@ -57,6 +59,9 @@ class SpatialMaxPooling(TensorModule):
         ph, pw = self._pads(x.shape[2], x.shape[3])
         if _gpu_ok(x):
             y, self._idx = P.maxpool_fwd_gpu(_prep(x), self.kH, self.kW, self.dH, self.dW, ph, pw, self.ceilMode)
+        elif x.is_cuda:       # any channel count / dtype / layout: N-d window kernel over N*C planes
+            geo, osh = PN.pool2d_geo(x.shape, self.kH, self.kW, self.dH, self.dW, ph, pw, self.ceilMode)
+            y, self._idx = PN.pool_nd_fwd(x.contiguous(), osh, geo, True)
         else:
             y, self._idx = F.max_pool2d(x, (self.kH, self.kW), (self.dH, self.dW), (ph, pw),
                                         ceil_mode=self.ceilMode, return_indices=True)
@@ -72,6 +77,9 @@ class SpatialMaxPooling(TensorModule):
         ph, pw = self._pads(x.shape[2], x.shape[3])
         if _gpu_ok(x):
             gi = P.maxpool_bwd_gpu(_prep(g), self._idx, x.shape, self.kH, self.kW, self.dH, self.dW, ph, pw)
+        elif x.is_cuda:
+            geo, _ = PN.pool2d_geo(x.shape, self.kH, self.kW, self.dH, self.dW, ph, pw, self.ceilMode)
+            gi = PN.pool_nd_bwd(g, self._idx, x.shape, geo, True, dtype=x.dtype)
         else:
             # overlapping windows must SUM their gradients (max_unpool2d would overwrite): use autograd
             xr = x.detach().float().requires_grad_(True)
@@ -118,6 +126,11 @@ class SpatialAveragePooling(TensorModule):
         kh, kw, sh, sw, ph, pw = self._geom(x)
         if _gpu_ok(x) and self.divide:
             y = P.avgpool_fwd_gpu(_prep(x), kh, kw, sh, sw, ph, pw, self.ceilMode, self.countIncludePad)
+        elif x.is_cuda:
+            geo, osh = PN.pool2d_geo(x.shape, kh, kw, sh, sw, ph, pw, self.ceilMode)
+            y, _ = PN.pool_nd_fwd(x.contiguous(), osh, geo, False, self.countIncludePad)
+            if not self.divide:
+                y = y * (kh * kw)
         else:
             y = F.avg_pool2d(x, (kh, kw), (sh, sw), (ph, pw), self.ceilMode, self.countIncludePad)
             if not self.divide:
@@ -134,6 +147,10 @@ class SpatialAveragePooling(TensorModule):
         kh, kw, sh, sw, ph, pw = self._geom(x)
         if _gpu_ok(x) and self.divide:
             gi = P.avgpool_bwd_gpu(_prep(g), x.shape, kh, kw, sh, sw, ph, pw, self.countIncludePad)
+        elif x.is_cuda:
+            geo, _ = PN.pool2d_geo(x.shape, kh, kw, sh, sw, ph, pw, self.ceilMode)
+            gi = PN.pool_nd_bwd(g * (kh * kw) if not self.divide else g, None, x.shape, geo, False,
+                                self.countIncludePad, dtype=x.dtype)
         else:
             xr = x.detach().float().requires_grad_(True)
             with torch.enable_grad():
@@ -158,7 +175,7 @@ class VolumetricMaxPooling(AutogradModule):
         return self
 
     def fn(self, x):
-        return F.max_pool3d(x, self.k, self.s, self.p, ceil_mode=self.ceilMode)
+        return PN.pool3d(x, self.k, self.s, self.p, self.ceilMode, max_mode=True)
 
 
 class VolumetricAveragePooling(AutogradModule):
@@ -171,7 +188,7 @@ class VolumetricAveragePooling(AutogradModule):
         self.countIncludePad, self.ceilMode = countIncludePad, ceilMode
 
     def fn(self, x):
-        return F.avg_pool3d(x, self.k, self.s, self.p, self.ceilMode, self.countIncludePad)
+        return PN.pool3d(x, self.k, self.s, self.p, self.ceilMode, max_mode=False, count_pad=self.countIncludePad)
 
 
 class TemporalMaxPooling(AutogradModule):
@@ -182,11 +199,7 @@ class TemporalMaxPooling(AutogradModule):
         self.kW, self.dW = kW, dW if dW is not None else kW
 
     def fn(self, x):
-        sq = x.dim() == 2
-        if sq:
-            x = x.unsqueeze(0)
-        y = F.max_pool1d(x.transpose(1, 2), self.kW, self.dW).transpose(1, 2)
-        return y.squeeze(0) if sq else y
+        return PN.temporal_max_pool(x, self.kW, self.dW)
 
 
 __all__ = ["SpatialMaxPooling", "SpatialAveragePooling", "VolumetricMaxPooling", "VolumetricAveragePooling",

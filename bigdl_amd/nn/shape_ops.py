@@ -338,7 +338,9 @@ class UpSampling1D(AutogradModule):
         self.length = length
 
     def fn(self, x):
-        return x.repeat_interleave(self.length, dim=1)
+        from ..ops.pool_nd import upsample_nearest
+
+        return upsample_nearest(x, (self.length,), sequence=True)     # GPU: csrc/pool_nd.hip
 
 
 class UpSampling2D(AutogradModule):
@@ -347,9 +349,9 @@ class UpSampling2D(AutogradModule):
         self.size, self.format = tuple(size), format
 
     def fn(self, x):
-        if self.format == "NHWC":
-            return x.repeat_interleave(self.size[0], 1).repeat_interleave(self.size[1], 2)
-        return x.repeat_interleave(self.size[0], 2).repeat_interleave(self.size[1], 3)
+        from ..ops.pool_nd import upsample_nearest
+
+        return upsample_nearest(x, self.size, channels_last=self.format == "NHWC")
 
 
 class UpSampling3D(AutogradModule):
@@ -358,9 +360,9 @@ class UpSampling3D(AutogradModule):
         self.size = tuple(size)
 
     def fn(self, x):
-        for i, s in enumerate(self.size):
-            x = x.repeat_interleave(s, 2 + i)
-        return x
+        from ..ops.pool_nd import upsample_nearest
+
+        return upsample_nearest(x, self.size)
 
 
 class ResizeBilinear(AutogradModule):

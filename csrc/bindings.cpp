@@ -395,6 +395,63 @@ void act_bwd(const Tensor& x, const Tensor& y, const Tensor& dy, const Tensor& d
                             (int)kind, (float)a, (float)b, stream()) == 0, "act_bwd: unknown kind");
 }
 
+
+// N-d pooling / nearest up-sampling (csrc/pool_nd.hip): dense [B][D][H][W][C] views, geo = the 17 PoolNdGeo ints
+static PoolNdGeo nd_geo(const std::vector<int64_t>& v) {
+  TORCH_CHECK(v.size() == 17, "pool_nd geo: 17 ints (B D H W C OD OH OW kd kh kw sd sh sw pd ph pw)");
+  PoolNdGeo g;
+  int* f = &g.B;
+  for (int i = 0; i < 17; ++i) {
+    TORCH_CHECK(v[i] >= 0 && v[i] < (1ll << 31), "pool_nd geo out of range");
+    f[i] = (int)v[i];
+  }
+  return g;
+}
+static bool nd_dtype(const Tensor& a, const Tensor& b, const char* what) {
+  const bool bf = a.scalar_type() == at::kBFloat16;
+  TORCH_CHECK(a.is_cuda() && (bf || a.scalar_type() == at::kFloat) && b.scalar_type() == a.scalar_type() &&
+                  a.is_contiguous() && b.is_contiguous(), what, ": contiguous bf16 or fp32 device tensors of one dtype");
+  return bf;
+}
+void poolnd_fwd(const Tensor& x, const Tensor& y, const c10::optional<Tensor>& idx, std::vector<int64_t> geo,
+                bool max_mode, bool count_pad) {
+  const PoolNdGeo g = nd_geo(geo);
+  const bool bf = nd_dtype(x, y, "poolnd_fwd");
+  TORCH_CHECK(x.numel() == (int64_t)g.B * g.D * g.H * g.W * g.C && y.numel() == (int64_t)g.B * g.OD * g.OH * g.OW * g.C,
+              "poolnd_fwd: sizes do not match the geometry");
+  int* ip = nullptr;
+  if (idx && idx->defined()) {
+    TORCH_CHECK(idx->scalar_type() == at::kInt && idx->is_contiguous() && idx->numel() == y.numel(), "poolnd_fwd: idx");
+    ip = idx->data_ptr<int>();
+  }
+  TORCH_CHECK(bigdl_poolnd_fwd(x.data_ptr(), y.data_ptr(), ip, &g, max_mode, count_pad, bf, stream()) == 0,
+              "poolnd_fwd: unsupported geometry");
+}
+void poolnd_bwd(const Tensor& dy, const c10::optional<Tensor>& idx, const Tensor& dx, std::vector<int64_t> geo,
+                bool max_mode, bool count_pad) {
+  const PoolNdGeo g = nd_geo(geo);
+  const bool bf = nd_dtype(dy, dx, "poolnd_bwd");
+  TORCH_CHECK(dx.numel() == (int64_t)g.B * g.D * g.H * g.W * g.C && dy.numel() == (int64_t)g.B * g.OD * g.OH * g.OW * g.C,
+              "poolnd_bwd: sizes do not match the geometry");
+  const int* ip = nullptr;
+  if (max_mode) {
+    TORCH_CHECK(idx && idx->defined() && idx->scalar_type() == at::kInt && idx->is_contiguous() &&
+                    idx->numel() == dy.numel(), "poolnd_bwd: max pooling needs the int32 index tensor");
+    ip = idx->data_ptr<int>();
+  }
+  TORCH_CHECK(bigdl_poolnd_bwd(dy.data_ptr(), ip, dx.data_ptr(), &g, max_mode, count_pad, bf, stream()) == 0,
+              "poolnd_bwd: unsupported geometry");
+}
+void upsample_nearest(const Tensor& src, const Tensor& dst, std::vector<int64_t> geo, bool backward) {
+  const PoolNdGeo g = nd_geo(geo);
+  const bool bf = nd_dtype(src, dst, "upsample_nearest");
+  const int64_t small = (int64_t)g.B * g.D * g.H * g.W * g.C, big = (int64_t)g.B * g.OD * g.OH * g.OW * g.C;
+  TORCH_CHECK(src.numel() == (backward ? big : small) && dst.numel() == (backward ? small : big),
+              "upsample_nearest: sizes do not match the geometry");
+  TORCH_CHECK(bigdl_upsample_nearest(src.data_ptr(), dst.data_ptr(), &g, backward, bf, stream()) == 0,
+              "upsample_nearest: output extent must be input x factor");
+}
+
 // detection (csrc/detection.hip)
 static void check_f32(const Tensor& t, const char* n) {
   TORCH_CHECK(t.is_cuda() && t.is_contiguous() && t.scalar_type() == at::kFloat, n, ": contiguous fp32 device tensor");
@@ -768,6 +825,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("pool_i8", &pool_i8);
   m.def("act_fwd", &act_fwd);
   m.def("act_bwd", &act_bwd);
+  m.def("poolnd_fwd", &poolnd_fwd);
+  m.def("poolnd_bwd", &poolnd_bwd);
+  m.def("upsample_nearest", &upsample_nearest);
   m.def("quantize_nchw_f32", &quantize_nchw_f32);
   m.def("quantize_rows_bf16", &quantize_rows_bf16);
   m.def("dequantize_rows", &dequantize_rows);

@@ -224,6 +224,16 @@ int bigdl_act_fwd(const void* x, void* y, long n, int bf16, int kind, float a, f
 int bigdl_act_bwd(const void* x, const void* y, const void* dy, void* dx, long n, int bf16, int kind, float a,
                   float b, hipStream_t st);
 
+// N-d window pooling / nearest up-sampling (csrc/pool_nd.hip) over a dense [B][D][H][W][C] view (C innermost):
+// input D x H x W, output OD x OH x OW, window (kd, kh, kw), stride, padding (for up-sampling kd / kh / kw are the
+// integer scale factors and stride / padding are unused). idx (max pooling) holds the input position (d*H+h)*W+w.
+typedef struct { int B, D, H, W, C, OD, OH, OW, kd, kh, kw, sd, sh, sw, pd, ph, pw; } PoolNdGeo;
+int bigdl_poolnd_fwd(const void* x, void* y, int* idx, const PoolNdGeo* g, int max_mode, int count_pad, int bf16,
+                     hipStream_t st);
+int bigdl_poolnd_bwd(const void* dy, const int* idx, void* dx, const PoolNdGeo* g, int max_mode, int count_pad,
+                     int bf16, hipStream_t st);
+int bigdl_upsample_nearest(const void* src, void* dst, const PoolNdGeo* g, int backward, int bf16, hipStream_t st);
+
 // Direct grouped / depthwise convolution, fp32 NCHW (csrc/grouped_conv.hip). pass 0 forward (x, w, b -> y),
 // 1 data gradient (dy, w -> dx), 2 weight / bias gradient (dy, x -> dwt, db accumulated).
 typedef struct {
