@@ -529,6 +529,8 @@ class VolumetricFullConvolution(AutogradModule):
             RandomUniform(-stdv, stdv).init(self.bias)
 
     def fn(self, x):
+        if x.is_cuda and self.g == 1:           # native 2-D transposed conv per temporal tap (ops/conv_fn.py)
+            return conv_fn.conv_transpose3d(x.float(), self.weight, self.bias, self.s, self.p, self.adj)
         return F.conv_transpose3d(x.to(self.weight.dtype), self.weight, self.bias, self.s, self.p, self.adj, self.g)
 
 

@@ -15,6 +15,7 @@ import torch.nn.functional as F
 
 from .. import ops
 from ..ops import conv as cv
+from ..ops import conv_fn
 from .abstractnn import AutogradModule, TensorModule
 from .init_methods import RandomUniform
 
@@ -360,7 +361,7 @@ class Cosine(AutogradModule):
 
     def fn(self, x):
         xs = x if x.dim() > 1 else x.unsqueeze(0)
-        y = F.normalize(xs.float(), dim=1, eps=1e-12) @ F.normalize(self.weight, dim=1, eps=1e-12).t()
+        y = conv_fn.linear(F.normalize(xs.float(), dim=1, eps=1e-12), F.normalize(self.weight, dim=1, eps=1e-12))
         return y if x.dim() > 1 else y.squeeze(0)
 
 
@@ -404,7 +405,7 @@ class Maxout(AutogradModule):
         RandomUniform(-stdv, stdv).init(self.bias)
 
     def fn(self, x):
-        y = F.linear(x.float(), self.weight, self.bias)
+        y = conv_fn.linear(x.float(), self.weight, self.bias)          # GPU: MFMA GEMM
         return y.view(y.shape[0], self.outputSize, self.k).max(dim=2).values
 
 
@@ -419,7 +420,7 @@ class Highway(AutogradModule):
         RandomUniform(-stdv, stdv).init(self.weight)
 
     def fn(self, x):
-        y = F.linear(x.float(), self.weight, self.bias)
+        y = conv_fn.linear(x.float(), self.weight, self.bias)
         t = torch.sigmoid(y[:, : self.size])
         h = y[:, self.size:]
         h = torch.tanh(h) if self.activation is None else _act_fn(self.activation, h)

@@ -250,7 +250,14 @@ class SpatialWithinChannelLRN(AutogradModule):
 
     def fn(self, x):
         xf = x.float()
-        sq = F.avg_pool2d(xf * xf, self.size, 1, (self.size - 1) // 2, count_include_pad=True)
+        p = (self.size - 1) // 2
+        if xf.is_cuda and xf.dim() == 4:          # GPU: N-d window kernel (csrc/pool_nd.hip)
+            from ..ops.pool_nd import pool2d_explicit
+
+            oh, ow = xf.shape[2] + 2 * p - self.size + 1, xf.shape[3] + 2 * p - self.size + 1
+            sq = pool2d_explicit(xf * xf, (self.size, self.size), (1, 1), (p, p), (oh, ow), False, True)
+        else:
+            sq = F.avg_pool2d(xf * xf, self.size, 1, p, count_include_pad=True)
         return (xf / (1 + self.alpha * sq) ** self.beta).to(x.dtype)
 
 
@@ -303,9 +310,11 @@ class SpatialSubtractiveNormalization(AutogradModule):
         k = self.kernel.to(xf.device)
         kh, kw = k.shape
         w = k.expand(1, self.nInputPlane, kh, kw)
-        m = F.conv2d(xf, w, padding=(kh // 2, kw // 2))
+        from ..ops import conv_fn
+
+        m = conv_fn.conv2d(xf, w, None, (1, 1), (kh // 2, kw // 2))        # GPU: native implicit GEMM
         ones = torch.ones(1, self.nInputPlane, xf.shape[2], xf.shape[3], device=xf.device)
-        coef = F.conv2d(ones, w, padding=(kh // 2, kw // 2))
+        coef = conv_fn.conv2d(ones, w, None, (1, 1), (kh // 2, kw // 2))
         return m / coef
 
     def fn(self, x):

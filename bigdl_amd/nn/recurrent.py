@@ -571,7 +571,9 @@ class _ConvLSTMBase(Cell):
             self.modules += [self.peepI, self.peepF, self.peepO]
 
     def _conv(self, x, conv, k):
-        fn = F.conv2d if self._nd == 2 else F.conv3d
+        from ..ops import conv_fn
+
+        fn = conv_fn.conv2d if self._nd == 2 else conv_fn.conv3d      # native implicit GEMM on the GPU
         w = conv.weight
         if self.padding == -1:
             pads = []
@@ -581,7 +583,8 @@ class _ConvLSTMBase(Cell):
             pad = 0
         else:
             pad = self.padding
-        return fn(x, w, conv.bias, self.stride, pad)
+        st = (self.stride,) * self._nd
+        return fn(x, w, conv.bias, st, (pad,) * self._nd)
 
     def init_hidden(self, B, x_t):
         spatial = []

@@ -791,6 +791,10 @@ class MaxPoolGrad(Operation):
         pw = _tf_pads(x.shape[3], self.k[1], self.s[1], self.same)
 
         def f(t):
+            if t.is_cuda:
+                from .tf_ops import tf_pool2d
+
+                return tf_pool2d(t, "max", self.k, self.s, self.same)
             t = F.pad(t, (pw[0], pw[1], ph[0], ph[1]), value=-math.inf)
             return F.max_pool2d(t, self.k, self.s)
         return _back(_autograd_grad(f, x.float(), _nchw(input[3], self.fmt).float()), self.fmt)
@@ -805,11 +809,15 @@ class AvgPoolGrad(Operation):
 
     def updateOutput(self, input):
         shape = [int(v) for v in input[1].reshape(-1).tolist()]
-        x = _nchw(torch.zeros(shape), self.fmt)
+        x = _nchw(torch.zeros(shape, device=input[2].device), self.fmt)
         ph = _tf_pads(x.shape[2], self.k[0], self.s[0], self.same)
         pw = _tf_pads(x.shape[3], self.k[1], self.s[1], self.same)
 
         def f(t):
+            if t.is_cuda:
+                from .tf_ops import tf_pool2d
+
+                return tf_pool2d(t, "avg", self.k, self.s, self.same)
             ones = F.pad(torch.ones_like(t), (pw[0], pw[1], ph[0], ph[1]))
             t = F.pad(t, (pw[0], pw[1], ph[0], ph[1]))
             return F.avg_pool2d(t, self.k, self.s) / F.avg_pool2d(ones, self.k, self.s)
@@ -886,7 +894,10 @@ class Conv2DBackFilter(Operation):
         ph = _tf_pads(x.shape[2], fs[0], self.s[0], self.same)
         pw = _tf_pads(x.shape[3], fs[1], self.s[1], self.same)
         xp = F.pad(x, (pw[0], pw[1], ph[0], ph[1]))
-        g = _autograd_grad(lambda wt: F.conv2d(xp, wt, stride=self.s), w, _nchw(input[3].float(), self.fmt))
+        from ..ops import conv_fn
+
+        w = w.to(xp.device)
+        g = _autograd_grad(lambda wt: conv_fn.conv2d(xp, wt, None, self.s), w, _nchw(input[3].float(), self.fmt))
         return g.permute(2, 3, 1, 0).contiguous()
 
 
@@ -924,7 +935,9 @@ def _conv3d(x, w, strides, same, fmt):
     pads = []
     for i in (2, 1, 0):
         pads += list(_tf_pads(x.shape[2 + i], wt.shape[2 + i], strides[i], same))
-    y = F.conv3d(F.pad(x, pads), wt, stride=tuple(strides))
+    from ..ops import conv_fn
+
+    y = conv_fn.conv3d(F.pad(x, pads).float(), wt.float(), None, tuple(strides)).to(x.dtype)   # GPU: native
     return y.permute(0, 2, 3, 4, 1) if fmt == "NDHWC" else y
 
 

@@ -136,7 +136,12 @@ def _conv2d(x, at):
         ph = _same_pads(xi.shape[2], wt.shape[2], sh, dh)
         pw = _same_pads(xi.shape[3], wt.shape[3], sw, dw)
         xi = F.pad(xi, (pw[0], pw[1], ph[0], ph[1]))
-    y = F.conv2d(xi, wt, None, (sh, sw), 0, (dh, dw))
+    if xi.is_cuda:                                     # native implicit GEMM (ops/conv_fn.py)
+        from ..ops import conv_fn
+
+        y = conv_fn.conv2d(xi.float(), wt.float(), None, (sh, sw), (0, 0), (dh, dw)).to(xi.dtype)
+    else:
+        y = F.conv2d(xi, wt, None, (sh, sw), 0, (dh, dw))
     return _back(y, fmt)
 
 
@@ -150,6 +155,10 @@ def _depthwise(x, at):
     if at.get("padding", "VALID") == "SAME":
         ph, pw = _same_pads(xi.shape[2], kh, sh), _same_pads(xi.shape[3], kw, sw)
         xi = F.pad(xi, (pw[0], pw[1], ph[0], ph[1]))
+    if xi.is_cuda:                                     # one-launch grouped / depthwise kernel
+        from ..ops import conv_fn
+
+        return _back(conv_fn.group_conv2d(xi.float(), wt.float(), None, (sh, sw), (0, 0), (1, 1), cin).to(xi.dtype), fmt)
     return _back(F.conv2d(xi, wt, None, (sh, sw), 0, 1, cin), fmt)
 
 
@@ -169,9 +178,36 @@ def _conv2d_transpose(x, at):
     Hp, Wp = H + ph[0] + ph[1], W + pw[0] + pw[1]
     oh = Hp - ((g.shape[2] - 1) * sh + kh)
     ow = Wp - ((g.shape[3] - 1) * sw + kw)
-    y = F.conv_transpose2d(g, wt, None, (sh, sw), 0, (oh, ow))
+    if g.is_cuda:                                      # the native data-gradient kernel
+        from ..ops import conv_fn
+
+        y = conv_fn.conv_transpose2d(g.float(), wt.float(), None, (sh, sw), (0, 0), (oh, ow)).to(g.dtype)
+    else:
+        y = F.conv_transpose2d(g, wt, None, (sh, sw), 0, (oh, ow))
     y = y[:, :, ph[0]: ph[0] + H, pw[0]: pw[0] + W]
     return _back(y, fmt)
+
+
+def tf_pool2d(xi, kind, k, s, same):
+    """TF max / avg pooling of an NCHW tensor (SAME: output ceil(H/s), leading pad (total)//2, averages exclude
+    the padding). GPU: the N-d window kernel with explicit leading pads (csrc/pool_nd.hip); CPU: torch."""
+    H, W = xi.shape[2], xi.shape[3]
+    if same:
+        ph, pw = _same_pads(H, k[0], s[0]), _same_pads(W, k[1], s[1])
+        oh, ow = -(-H // s[0]), -(-W // s[1])
+    else:
+        ph, pw = (0, 0), (0, 0)
+        oh, ow = (H - k[0]) // s[0] + 1, (W - k[1]) // s[1] + 1
+    if xi.is_cuda:
+        from ..ops.pool_nd import pool2d_explicit
+
+        return pool2d_explicit(xi, k, s, (ph[0], pw[0]), (oh, ow), kind == "max", False)
+    pads = (pw[0], pw[1], ph[0], ph[1])
+    if kind == "max":
+        return F.max_pool2d(F.pad(xi, pads, value=float("-inf")), k, s)
+    num = F.avg_pool2d(F.pad(xi, pads), k, s)
+    den = F.avg_pool2d(F.pad(torch.ones_like(xi[:, :1]), pads), k, s)
+    return num / den
 
 
 def _pool(kind):
@@ -180,6 +216,8 @@ def _pool(kind):
         kh, kw = _hw(at["ksize"], fmt)
         sh, sw = _hw(at["strides"], fmt)
         xi = _nchw(x[0], fmt)
+        if xi.is_cuda:
+            return _back(tf_pool2d(xi, kind, (kh, kw), (sh, sw), at.get("padding", "VALID") == "SAME"), fmt)
         if at.get("padding", "VALID") == "SAME":
             ph, pw = _same_pads(xi.shape[2], kh, sh), _same_pads(xi.shape[3], kw, sw)
             pads = (pw[0], pw[1], ph[0], ph[1])

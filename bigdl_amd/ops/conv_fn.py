@@ -205,6 +205,33 @@ def conv1d(x, w, b=None, stride=1):
     return conv2d(x.unsqueeze(2), w.unsqueeze(2), b, (1, stride), (0, 0)).squeeze(2)
 
 
+def conv_transpose3d(x, w, b=None, stride=(1, 1, 1), pad=(0, 0, 0), adj=(0, 0, 0)):
+    """x: [N, Cin, T, H, W], w: [Cin, Cout, kT, kH, kW]. Input frame t feeds output frames t*sT + kt - pT: each
+    temporal tap kt is a native 2-D transposed convolution of all frames (folded into the batch), scattered into
+    the output frames with index_add (the adjoint of conv3d's depth gather)."""
+    if not x.is_cuda:
+        return F.conv_transpose3d(x, w, b, stride, pad, adj)
+    N, Cin, T, H, W = x.shape
+    _, Cout, kT, kH, kW = w.shape
+    sT, sH, sW = stride
+    pT, pH, pW = pad
+    OT = (T - 1) * sT - 2 * pT + kT + adj[0]
+    L = max((T - 1) * sT + kT, pT + OT)                 # padded temporal extent
+    xs = x.permute(0, 2, 1, 3, 4).reshape(N * T, Cin, H, W)
+    y = None
+    for kt in range(kT):
+        part = conv_transpose2d(xs, w[:, :, kt], None, (sH, sW), (pH, pW), (adj[1], adj[2]))
+        OH, OW = part.shape[2], part.shape[3]
+        if y is None:
+            y = part.new_zeros(N, L, Cout, OH, OW)
+        idx = torch.arange(T, device=x.device) * sT + kt
+        y = y.index_add(1, idx, part.view(N, T, Cout, OH, OW))
+    y = y[:, pT:pT + OT].permute(0, 2, 1, 3, 4)
+    if b is not None:
+        y = y + b.view(1, -1, 1, 1, 1)
+    return y.contiguous()
+
+
 def conv3d(x, w, b=None, stride=(1, 1, 1), pad=(0, 0, 0)):
     """x: [N, C, T, H, W], w: [K, C, kT, kH, kW]. Each temporal tap kt is a 2-D convolution of the depth slices
     t*sT + kt - pT (zero outside) folded into the batch; the kT partial outputs are summed."""

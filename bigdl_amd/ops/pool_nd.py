@@ -86,6 +86,14 @@ def pool2d_geo(x_shape, kh, kw, sh, sw, ph, pw, ceil=False):
     return [N * C, 1, H, W, 1, 1, OH, OW, 1, kh, kw, 1, sh, sw, 0, ph, pw], (N, C, OH, OW)
 
 
+def pool2d_explicit(x, k, s, pad_begin, out_hw, max_mode, count_pad):
+    """Differentiable 2D pooling of an NCHW CUDA tensor with explicit output size and leading pads (windows are
+    clipped to the input, so trailing / asymmetric padding needs no copy): TF SAME / VALID pooling."""
+    N, C, H, W = x.shape
+    geo = [N * C, 1, H, W, 1, 1, out_hw[0], out_hw[1], 1, k[0], k[1], 1, s[0], s[1], 0, pad_begin[0], pad_begin[1]]
+    return _PoolNdFn.apply(x.contiguous(), (N, C, out_hw[0], out_hw[1]), geo, max_mode, count_pad)
+
+
 def pool3d(x, k, s, p, ceil=False, max_mode=True, count_pad=True):
     """Max / average pooling of an NCDHW (or CDHW) tensor; k, s, p are (t, h, w) triples."""
     if not _native_ok(x):
@@ -155,4 +163,4 @@ def upsample_nearest(x, factors, channels_last=False, sequence=False):
     return _UpsampleFn.apply(x, out_shape, geo)
 
 
-__all__ = ["pool_nd_fwd", "pool_nd_bwd", "pool2d_geo", "pool3d", "temporal_max_pool", "upsample_nearest"]
+__all__ = ["pool_nd_fwd", "pool_nd_bwd", "pool2d_geo", "pool2d_explicit", "pool3d", "temporal_max_pool", "upsample_nearest"]
