@@ -123,6 +123,14 @@ class QuantizedLinear(QuantizedModule):
     def dequantized_weight(self):
         return self.weight[:, : self.inputSize].float() * self.weightScale[:, None]
 
+    def quantized_weight(self):
+        """The int8 weight as a QuantizedTensor (reference ``weight: QuantizedTensor``), sharing the kernel's bytes."""
+        from ..tensor.quantized import QuantizedTensor
+
+        return QuantizedTensor.from_scaled(self.weight[:, : self.inputSize], self.weightScale,
+                                           {"kind": "LinearWeight", "outputSize": self.outputSize,
+                                            "inputSize": self.inputSize})
+
     def updateOutput(self, input):
         assert input.dim() in (1, 2), "quantized.Linear: input must be a vector or a batch of vectors"
         x = input.unsqueeze(0) if input.dim() == 1 else input
@@ -187,6 +195,14 @@ class QuantizedSpatialConvolution(QuantizedModule):
         self.bias = (torch.as_tensor(b).float().reshape(-1) if b is not None
                      else torch.zeros(self.nOutputPlane)).to(dev)
         return self
+
+    def quantized_weight(self):
+        """The int8 weight [nOutputPlane, kH, kW, nInputPlane / nGroup] (NHWC order, as the i8 kernels read it) as a
+        QuantizedTensor sharing the kernel's bytes."""
+        from ..tensor.quantized import QuantizedTensor
+
+        cin = self.nInputPlane // self.nGroup
+        return QuantizedTensor.from_scaled(self.weight[..., :cin], self.weightScale, {"kind": "ConvWeight"})
 
     def dequantized_weight(self):
         cin = self.nInputPlane // self.nGroup
