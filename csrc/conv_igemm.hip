@@ -151,16 +151,21 @@ __device__ __forceinline__ void nt_epilogue_lds(const ConvArgs& a, v4f (&acc)[MI
     bsc[e] = (on && a.bnaff) ? a.bnaff[n + e] : 0.f;
     bsh[e] = (on && a.bnaff) ? a.bnaff[a.Ncol + n + e] : 0.f;
   }
-  // Phase 1: every global read of the epilogue (addend, consumer-BN x / z) is issued before the first store:
-  // `out` may alias them as far as the compiler knows, so loads left inside the store loop would be serialised
-  // one round trip per row group.
+  // NH > 1: the accumulator tile goes through LDS in NH row chunks, so the wave slice is TM/NH x TN floats
   constexpr int NR = TM / PPI;
-  long orows[NR];
-  v4u pad[NR], px[NR], pz[NR];
+  constexpr int MIH = MI / NH, NRH = NR / NH;
+  static_assert(MI % NH == 0 && NR % NH == 0, "row chunks");
   const bool bnw = a.bnred && !a.stats;
 #pragma unroll
-  for (int r = 0; r < NR; ++r) {
-    const int m = mbase + r * PPI + lane / LPR;
+  for (int h = 0; h < NH; ++h) {
+  // Phase 1: every global read of the chunk (addend, consumer-BN x / z) is issued before its first store:
+  // `out` may alias them as far as the compiler knows, so loads left inside the store loop would be serialised
+  // one round trip per row group.
+  long orows[NRH];
+  v4u pad[NRH], px[NRH], pz[NRH];
+#pragma unroll
+  for (int rr = 0; rr < NRH; ++rr) {
+    const int m = mbase + (h * NRH + rr) * PPI + lane / LPR;
     long orow = -1;
     if (m < a.M && nok) {
       orow = m;
@@ -170,24 +175,19 @@ __device__ __forceinline__ void nt_epilogue_lds(const ConvArgs& a, v4f (&acc)[MI
         orow = ((long)nb * a.OHo + oh * a.omul_h + a.ooff_h) * a.OWo + ow * a.omul_w + a.ooff_w;
       }
     }
-    orows[r] = orow;
+    orows[rr] = orow;
     const size_t off = (size_t)(orow < 0 ? 0 : orow) * a.ldo + n;
-    pad[r] = v4u{0u, 0u, 0u, 0u};
-    px[r] = v4u{0u, 0u, 0u, 0u};
-    pz[r] = v4u{0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
+    pad[rr] = v4u{0u, 0u, 0u, 0u};
+    px[rr] = v4u{0u, 0u, 0u, 0u};
+    pz[rr] = v4u{0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
     if (orow >= 0) {
-      if (a.addend) pad[r] = *reinterpret_cast<const v4u*>(a.addend + off);
+      if (a.addend) pad[rr] = *reinterpret_cast<const v4u*>(a.addend + off);
       if (bnw) {
-        px[r] = *reinterpret_cast<const v4u*>(a.bnx + off);
-        if (a.bnz) pz[r] = *reinterpret_cast<const v4u*>(a.bnz + off);
+        px[rr] = *reinterpret_cast<const v4u*>(a.bnx + off);
+        if (a.bnz) pz[rr] = *reinterpret_cast<const v4u*>(a.bnz + off);
       }
     }
   }
-  // NH > 1: the accumulator tile goes through LDS in NH row chunks, so the wave slice is TM/NH x TN floats
-  constexpr int MIH = MI / NH, NRH = NR / NH;
-  static_assert(MI % NH == 0 && NR % NH == 0, "row chunks");
-#pragma unroll
-  for (int h = 0; h < NH; ++h) {
 #pragma unroll
   for (int i = 0; i < MIH; ++i)
 #pragma unroll
@@ -199,7 +199,7 @@ __device__ __forceinline__ void nt_epilogue_lds(const ConvArgs& a, v4f (&acc)[MI
   __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's LDS writes landed (wave-private slice)
 #pragma unroll
   for (int rr = 0; rr < NRH; ++rr) {
-    const int r = h * NRH + rr;
+    const int r = rr;
     const int p = rr * PPI + lane / LPR;
     const v4f lo = *reinterpret_cast<const v4f*>(wl + gpos(p, 2 * q));
     const v4f hi = *reinterpret_cast<const v4f*>(wl + gpos(p, 2 * q + 1));
@@ -423,14 +423,18 @@ __device__ __forceinline__ void glds16(const void* g, LDS_PTR(void) l) {
 
 // FASTK = false (Cs % 64 != 0, e.g. the 7x7 stem over 8 padded channels): a K stage spans several taps, so each
 // lane resolves its own granule's tap (kk = k0 + 8 * gsrc) and zero-fills past Kdim.
-template <int BM, int BN, int WM, bool FASTK = true>
-__global__ __launch_bounds__(256, 2) void conv_nt_glds_kernel(ConvArgs a) {
+// NST = 1: single-K-stage layers (Kdim == BK, the 1x1 convolutions over 64 channels): one LDS stage and a two-chunk
+// epilogue (NH = 2) fit the workgroup in 32 KB, so 3 workgroups share a CU (launch bound 3: 168 registers, no spills) and one workgroup's
+// operand DMA overlaps the others' epilogue stores on these store-bound layers.
+template <int BM, int BN, int WM, bool FASTK = true, int NST = 2>
+__global__ __launch_bounds__(256, NST == 1 ? 3 : 2) void conv_nt_glds_kernel(ConvArgs a) {
   constexpr int WN = 4 / WM;
   constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int MI = TM / 16, NI = TN / 16;
   constexpr int AI = BM / 32, BI = BN / 32;       // DMA instructions per thread per stage (8 rows each x 4 waves)
   constexpr int STAGE = (BM + BN) * BK;
-  __shared__ __attribute__((aligned(1024))) bf16_t lds[2 * STAGE];
+  static_assert(NST == 2 || (NST == 1 && TM * TN * 4 * 2 <= STAGE * 2), "one-stage epilogue must fit the stage");
+  __shared__ __attribute__((aligned(1024))) bf16_t lds[NST * STAGE];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -511,12 +515,12 @@ __global__ __launch_bounds__(256, 2) void conv_nt_glds_kernel(ConvArgs a) {
 #pragma unroll
     for (int j = 0; j < NI; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = (a.Kdim + BK - 1) / BK;
+  const int nk = NST == 1 ? 1 : (a.Kdim + BK - 1) / BK;
   issue(0, 0);
   __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) issue(kt + 1, cur ^ 1);
+    const int cur = NST == 1 ? 0 : (kt & 1);
+    if (NST == 2 && kt + 1 < nk) issue(kt + 1, cur ^ 1);
     const bf16_t* A = lds + cur * STAGE;
     const bf16_t* B = A + BM * BK;
 #pragma unroll
@@ -535,11 +539,16 @@ __global__ __launch_bounds__(256, 2) void conv_nt_glds_kernel(ConvArgs a) {
     }
     __syncthreads();   // retires the stage-(k+1) DMA (vmcnt(0)) and the stage-k fragment reads
   }
-  if ((a.Ncol & 7) == 0 && (a.ldo & 7) == 0)
+  if constexpr (NST == 1) {   // launched for aligned outputs only (bigdl_conv_nt)
+    constexpr int NH = NI >= 4 ? 4 : 2;   // row chunks: fewer live epilogue registers on the wide tile
+    nt_epilogue_lds<MI, NI, TM, TN, NH>(a, acc, m0 + wm * TM, n0 + wn * TN, lane, bid,
+                                        reinterpret_cast<float*>(lds) + wave * (TM / NH) * TN);
+  } else if ((a.Ncol & 7) == 0 && (a.ldo & 7) == 0) {
     nt_epilogue_lds<MI, NI, TM, TN>(a, acc, m0 + wm * TM, n0 + wn * TN, lane, bid,
                                     reinterpret_cast<float*>(lds) + wave * TM * TN);
-  else
+  } else {
     nt_epilogue<MI, NI, TM, TN>(a, acc, m0 + wm * TM, n0 + wn * TN, lane, bid);
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1225,10 +1234,16 @@ void launch_nt(const ConvArgs& a, bool fastk, hipStream_t st) {
   else conv_nt_kernel<BM, BN, WM, false><<<grid, block, 0, st>>>(a);
 }
 
-template <int BM, int BN, int WM, bool FASTK = true>
+template <int BM, int BN, int WM, bool FASTK = true, int NST = 2>
 void launch_nt_glds(const ConvArgs& a, hipStream_t st) {
   const int nwg = ((a.M + BM - 1) / BM) * ((a.Ncol + BN - 1) / BN);
-  conv_nt_glds_kernel<BM, BN, WM, FASTK><<<dim3(nwg), dim3(256), 0, st>>>(a);
+  conv_nt_glds_kernel<BM, BN, WM, FASTK, NST><<<dim3(nwg), dim3(256), 0, st>>>(a);
+}
+
+// single-stage kernel for Kdim == BK (BIGDL_CONV_ONESTAGE=0 disables it for A/B runs)
+static bool conv_onestage() {
+  static int v = [] { const char* e = getenv("BIGDL_CONV_ONESTAGE"); return e ? atoi(e) : 1; }();
+  return v != 0;
 }
 
 // LDS-DMA path for Cs % 64 != 0 (BIGDL_CONV_GLDS_SLOWK=0 restores the register-staged kernel there)
@@ -1288,6 +1303,9 @@ int bigdl_conv_nt(const ConvArgs* a, hipStream_t st) {
   } else if (fastk && impl == 3 && aligned_out && tiles128 > 2 * 256) {
     if (a->Ncol <= 64) launch_nt_pers<128, 64, 2>(*a, st);
     else launch_nt_pers<128, 128, 2>(*a, st);
+  } else if (fastk && impl >= 1 && a->Kdim == BK && aligned_out && conv_onestage()) {
+    if (a->Ncol <= 64) launch_nt_glds<128, 64, 2, true, 1>(*a, st);
+    else launch_nt_glds<128, 128, 2, true, 1>(*a, st);
   } else if (fastk && impl >= 1) {
     if (a->Ncol <= 64) launch_nt_glds<128, 64, 2>(*a, st);
     else launch_nt_glds<128, 128, 2>(*a, st);
