@@ -502,6 +502,44 @@ void roi_pool_bwd(const Tensor& gy, const Tensor& argmax, const Tensor& rois, co
                      (int)gy.size(3), stream());
 }
 
+// packed variable-size batch (csrc/image.hip image_pipeline_kernel): src uint8 flat, offs int64 [N], prm fp32 [N, 16]
+void image_pipeline(const Tensor& src, const Tensor& offs, const Tensor& prm, const Tensor& out, std::vector<double> mean,
+                    std::vector<double> std, bool rgb) {
+  TORCH_CHECK(src.is_cuda() && src.scalar_type() == at::kByte && src.is_contiguous(), "image_pipeline: src uint8 device");
+  TORCH_CHECK(offs.is_cuda() && offs.scalar_type() == at::kLong && offs.is_contiguous() && offs.dim() == 1,
+              "image_pipeline: offs int64 [N] device");
+  const int N = (int)offs.size(0);
+  TORCH_CHECK(prm.is_cuda() && prm.scalar_type() == at::kFloat && prm.is_contiguous() && prm.dim() == 2 &&
+                  prm.size(0) == N && prm.size(1) == 16, "image_pipeline: prm fp32 [N, 16] device");
+  TORCH_CHECK(mean.size() == 3 && std.size() == 3, "image_pipeline: mean/std need 3 entries");
+  const bool bf = out.scalar_type() == at::kBFloat16;
+  int OH, OW;
+  if (bf) {
+    TORCH_CHECK(out.dim() == 4 && out.size(3) == 3 && out.is_contiguous() && out.size(0) == N, "image_pipeline: bf16 out is [N, OH, OW, 3]");
+    OH = (int)out.size(1); OW = (int)out.size(2);
+  } else {
+    TORCH_CHECK(out.scalar_type() == at::kFloat && out.dim() == 4 && out.size(1) == 3 && out.is_contiguous() &&
+                    out.size(0) == N, "image_pipeline: fp32 out is [N, 3, OH, OW]");
+    OH = (int)out.size(2); OW = (int)out.size(3);
+  }
+  // bounds are validated on the host copy of the parameters (the kernel trusts them)
+  auto pc = prm.cpu(), oc = offs.cpu();
+  const float* p = pc.data_ptr<float>();
+  const int64_t* o = oc.data_ptr<int64_t>();
+  for (int n = 0; n < N; ++n) {
+    const float* q = p + 16 * n;
+    const int64_t H = (int64_t)q[0], W = (int64_t)q[1], y0 = (int64_t)q[2], x0 = (int64_t)q[3], ch = (int64_t)q[4],
+                  cw = (int64_t)q[5];
+    TORCH_CHECK(H > 0 && W > 0 && ch > 0 && cw > 0 && y0 >= 0 && x0 >= 0 && y0 + ch <= H && x0 + cw <= W,
+                "image_pipeline: crop box out of bounds for image ", n);
+    TORCH_CHECK(o[n] >= 0 && o[n] + H * W * 3 <= src.numel(), "image_pipeline: image ", n, " exceeds the buffer");
+    TORCH_CHECK(q[7] >= 0 && q[7] <= 4, "image_pipeline: at most 4 colour ops");
+  }
+  const float m[3] = {(float)mean[0], (float)mean[1], (float)mean[2]};
+  const float inv[3] = {(float)(1.0 / std[0]), (float)(1.0 / std[1]), (float)(1.0 / std[2])};
+  bigdl_image_pipeline(src.data_ptr<uint8_t>(), reinterpret_cast<const long*>(offs.data_ptr<int64_t>()),
+                       prm.data_ptr<float>(), out.data_ptr(), N, OH, OW, m, inv, rgb ? 1 : 0, bf ? 1 : 0, stream());
+}
 void image_augment(const Tensor& src, const Tensor& params, const Tensor& out, std::vector<double> mean,
                    std::vector<double> std, bool rgb) {
   TORCH_CHECK(src.is_cuda() && src.scalar_type() == at::kByte && src.dim() == 4 && src.size(3) == 3 &&
@@ -824,6 +862,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("out_scale") = 0.0, py::arg("addend") = py::none(), py::arg("add_scale") = 0.0);
   m.def("pool_i8", &pool_i8);
   m.def("act_fwd", &act_fwd);
+  m.def("image_pipeline", &image_pipeline);
   m.def("act_bwd", &act_bwd);
   m.def("poolnd_fwd", &poolnd_fwd);
   m.def("poolnd_bwd", &poolnd_bwd);

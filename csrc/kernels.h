@@ -142,6 +142,10 @@ int bigdl_get_conv_impl();
 // params: int32 [N][3] = (y0, x0, flip). Output fp32 NCHW [N, 3, OH, OW] or bf16 NHWC [N, OH, OW, 3].
 void bigdl_image_augment(const uint8_t* src, const int* params, void* out, int N, int H, int W, int OH, int OW,
                          const float* mean, const float* inv_std, int rgb, int nhwc_bf16, hipStream_t st);
+// variable-size batch: resized crop + flip + colour jitter + normalise (csrc/image.hip image_pipeline_kernel);
+// offs = int64 byte offset of each image, prm = 16 floats per image (layout in image.hip)
+void bigdl_image_pipeline(const uint8_t* src, const long* offs, const float* prm, void* out, int N, int OH, int OW,
+                          const float* mean, const float* inv_std, int rgb, int nhwc_bf16, hipStream_t st);
 
 // Detection (csrc/detection.hip): greedy NMS over score-sorted boxes (mask_ws: n * ceil(n/64) uint64),
 // RoiAlign forward, RoiPooling forward (argmax) / backward.

@@ -1,0 +1,62 @@
+"""Device image pipeline (csrc/image.hip image_pipeline_kernel) vs the host transformer chain on the same draws:
+variable-size BGR uint8 images -> random-resized crop (bilinear) -> flip -> colour jitter (brightness, contrast,
+saturation, hue in ColorJitter order) -> ChannelNormalize -> RGB, fp32 NCHW and bf16 NHWC outputs."""
+import pytest
+import torch
+
+from bigdl_amd.dataset.device_pipeline import BRIGHTNESS, CONTRAST, HUE, SATURATION, DeviceImagePipeline, ImageParams
+from bigdl_amd.utils.random_generator import RNG
+
+pytestmark = pytest.mark.gpu
+
+MEAN, STD = (123.68, 116.78, 103.94), (58.4, 57.1, 57.4)
+JITTER = dict(brightnessProb=1.0, contrastProb=1.0, saturationProb=1.0, hueProb=1.0)
+
+
+def _images():
+    g = torch.Generator().manual_seed(0)
+    return [torch.randint(0, 256, shp, dtype=torch.uint8, generator=g)
+            for shp in [(37, 53, 3), (120, 90, 3), (64, 64, 3), (200, 151, 3), (31, 300, 3)]]
+
+
+@pytest.mark.parametrize("fmt", ["NCHW", "NHWC_BF16"])
+def test_device_pipeline_matches_host_chain(fmt):
+    RNG.setSeed(11)
+    imgs = _images()
+    pipe = DeviceImagePipeline(48, 40, MEAN, STD, out_format=fmt)
+    params = pipe.random_params([im.shape for im in imgs], jitter=JITTER)
+    assert all(len(p.ops) == 4 for p in params)
+    out = pipe(imgs, params).float().cpu()
+    tol = 2e-3 if fmt == "NCHW" else 2e-2
+    for i, (im, p) in enumerate(zip(imgs, params)):
+        ref = pipe.host_reference(im, p)
+        err = (out[i] - ref).abs().flatten()
+        # HSV branch choices (which channel is the max) can flip where the float interpolation orders differ by
+        # one ulp; require 99.5 % of the values to agree tightly and the mean error to stay small
+        assert float(err.kthvalue(int(0.995 * err.numel())).values) < tol, (i, p)
+        assert float(err.mean()) < tol / 4, (i, p)
+
+
+def test_device_pipeline_geometry_only_is_exact_for_identity_resize():
+    img = torch.randint(0, 256, (20, 30, 3), dtype=torch.uint8)
+    pipe = DeviceImagePipeline(10, 12, out_format="NCHW", to_rgb=False)
+    out = pipe([img], [ImageParams(5, 7, 10, 12, flip=True)]).cpu()
+    ref = img[5:15, 7:19].flip(1).permute(2, 0, 1).float()
+    assert torch.equal(out[0], ref)
+
+
+def test_device_pipeline_rejects_out_of_bounds_crop():
+    img = torch.zeros(10, 10, 3, dtype=torch.uint8)
+    pipe = DeviceImagePipeline(4, 4)
+    with pytest.raises(RuntimeError):
+        pipe([img], [ImageParams(8, 0, 5, 5)])
+
+
+def test_op_codes_cover_each_transform():
+    img = torch.randint(0, 256, (16, 16, 3), dtype=torch.uint8)
+    pipe = DeviceImagePipeline(16, 16, out_format="NCHW")
+    for op in [(BRIGHTNESS, 20.0), (CONTRAST, 1.3), (SATURATION, 0.6), (HUE, 10.0)]:
+        p = ImageParams(0, 0, 16, 16, ops=[op])
+        out = pipe([img], [p]).cpu()[0]
+        ref = pipe.host_reference(img, p)
+        assert float((out - ref).abs().mean()) < 1e-3, op
