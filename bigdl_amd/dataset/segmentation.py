@@ -8,9 +8,11 @@ RLE convention (COCO "uncompressed" RLE): run lengths over the column-major flat
 starting with a run of zeros. All functions are host-side numpy: masks are produced once per detection and
 serialised, the GPU never sees them.
 """
+import glob
 import json
 import math
 import os
+import struct
 
 import numpy as np
 import torch
@@ -406,3 +408,160 @@ class COCODataset:
         masks = [a.segmentation.toRLE() for a in anns]
         crowd = torch.tensor([1.0 if a.isCrowd else 0.0 for a in anns])
         return boxes, cls, masks, crowd
+
+
+# ------------------------------------------------------------------------------------------ COCO sequence files
+COCO_MAGIC = 0x1F3D4E5A
+
+
+class COCOSerializeContext:
+    """Big-endian record writer of the COCO sequence-file key (reference COCODataset.scala:29-77)."""
+
+    def __init__(self):
+        self.buf = bytearray()
+
+    def clear(self):
+        self.buf = bytearray()
+
+    def dump_int(self, v):
+        self.buf += struct.pack(">i", int(v))
+
+    def dump_float(self, v):
+        self.buf += struct.pack(">f", float(v))
+
+    def dump_bool(self, v):
+        self.buf += b"\x01" if v else b"\x00"
+
+    def dump_bytes(self, b):
+        self.dump_int(len(b))
+        self.buf += bytes(b)
+
+    def dump_string(self, s):
+        self.dump_bytes(s.encode("utf-8"))
+
+    def toByteArray(self):
+        return bytes(self.buf)
+
+
+def dump_image_meta(ctx, image, dataset):
+    """fileName, height, width, then per annotation: category index, area, bbox (4 floats, inclusive x1 y1 x2 y2),
+    isCrowd, and the RLE counts (crowd) or polygons (reference COCOImage / COCOAnotationOD / COCORLE / COCOPoly
+    dumpTo), closed by the magic number."""
+    ctx.dump_string(image.fileName)
+    ctx.dump_int(image.height)
+    ctx.dump_int(image.width)
+    ctx.dump_int(len(image.annotations))
+    for a in image.annotations:
+        ctx.dump_int(dataset.categoryId2Idx(a.categoryId))
+        ctx.dump_float(a.area)
+        for v in a.bbox:
+            ctx.dump_float(v)
+        ctx.dump_bool(a.isCrowd)
+        seg = a.segmentation
+        if isinstance(seg, RLEMasks):
+            ctx.dump_int(len(seg.counts))
+            for c in seg.counts:
+                ctx.dump_int(c if c < 2 ** 31 else c - 2 ** 32)
+        else:
+            ctx.dump_int(len(seg.poly))
+            for p in seg.poly:
+                ctx.dump_int(len(p))
+                for v in p:
+                    ctx.dump_float(v)
+    ctx.dump_int(COCO_MAGIC)
+
+
+class COCODeserializer:
+    """Reader of the record key (reference COCODeserializer, COCODataset.scala:80-136)."""
+
+    def __init__(self, buf):
+        self.b, self.p = bytes(buf), 0
+
+    def _u(self, fmt, n):
+        (v,) = struct.unpack_from(fmt, self.b, self.p)
+        self.p += n
+        return v
+
+    def getInt(self):
+        return self._u(">i", 4)
+
+    def getFloat(self):
+        return self._u(">f", 4)
+
+    def getBoolean(self):
+        v = self.b[self.p] != 0
+        self.p += 1
+        return v
+
+    def getString(self):
+        n = self.getInt()
+        s = self.b[self.p:self.p + n].decode("utf-8")
+        self.p += n
+        return s
+
+    def getAnnotations(self):
+        h, w, n = self.getInt(), self.getInt(), self.getInt()
+        anns = []
+        for _ in range(n):
+            cat, area = self.getInt(), self.getFloat()
+            bbox = tuple(self.getFloat() for _ in range(4))
+            crowd = self.getBoolean()
+            if crowd:
+                counts = [self.getInt() & 0xFFFFFFFF for _ in range(self.getInt())]
+                masks = RLEMasks(counts, h, w)
+            else:
+                polys = []
+                for _ in range(self.getInt()):
+                    polys.append([self.getFloat() for _ in range(self.getInt())])
+                masks = PolyMasks(polys, h, w)
+            anns.append({"categoryId": cat, "area": area, "bbox": bbox, "isCrowd": crowd, "masks": masks})
+        return h, w, anns
+
+
+def generate_coco_seq_files(meta_path, image_root, out_dir, blockSize=12800, prefix="coco-seq"):
+    """COCO instances json + image folder -> ``{prefix}-{block}.seq`` files of (metadata key, encoded image bytes)
+    BytesWritable records (reference models/utils/COCOSeqFileGenerator.scala; written uncompressed here rather than
+    BZip2 block-compressed). Images whose file is missing are skipped with a warning, as in the reference."""
+    from .seqfile import _BYTES, SequenceFileWriter
+
+    meta = COCODataset.load(meta_path, image_root)
+    imgs = [im for im in meta.images if os.path.isfile(im.path)]
+    os.makedirs(out_dir, exist_ok=True)
+    ctx = COCOSerializeContext()
+    paths = []
+    for blk in range(0, len(imgs), blockSize):
+        path = os.path.join(out_dir, f"{prefix}-{blk // blockSize}.seq")
+        with SequenceFileWriter(path, _BYTES, _BYTES) as w:
+            for im in imgs[blk:blk + blockSize]:
+                ctx.clear()
+                dump_image_meta(ctx, im, meta)
+                w.append(ctx.toByteArray(), im.data())
+        paths.append(path)
+    return paths
+
+
+def read_coco_seq_files(folder):
+    """Yield one detection sample per record: {"fileName", "image" (uint8 BGR H x W x 3 tensor), "classes" (n),
+    "bboxes" (n, 4), "isCrowd" (n), "masks" [SegmentationMasks], "originalSize"} (reference
+    DataSet.SeqFileFolder.filesToRoiImageFrame)."""
+    import io
+
+    from PIL import Image
+
+    from .seqfile import read_sequence_file
+
+    for path in sorted(glob.glob(os.path.join(folder, "*.seq"))):
+        for key, value in read_sequence_file(path):
+            d = COCODeserializer(key)
+            name = d.getString()
+            h, w, anns = d.getAnnotations()
+            if d.getInt() != COCO_MAGIC:
+                raise ValueError(f"{path}: corrupted metadata for {name}")
+            rgb = np.asarray(Image.open(io.BytesIO(value)).convert("RGB"))
+            if rgb.shape[0] != h or rgb.shape[1] != w:
+                raise ValueError(f"{path}: {name} decodes to {rgb.shape[:2]}, metadata says {(h, w)}")
+            yield {"fileName": name, "image": torch.from_numpy(rgb[..., ::-1].copy()),
+                   "classes": torch.tensor([a["categoryId"] for a in anns], dtype=torch.float32),
+                   "bboxes": torch.tensor([a["bbox"] for a in anns], dtype=torch.float32).reshape(-1, 4),
+                   "isCrowd": torch.tensor([1.0 if a["isCrowd"] else 0.0 for a in anns]),
+                   "masks": [a["masks"] for a in anns], "originalSize": (h, w, 3)}

@@ -22,6 +22,7 @@ from .core import LocalArrayDataSet, MiniBatch, Transformer
 from .image import ByteRecord, LocalImageFiles, LocalLabeledImagePath, encode_bgr_record, read_image
 
 _TEXT = "org.apache.hadoop.io.Text"
+_BYTES = "org.apache.hadoop.io.BytesWritable"
 SYNC_INTERVAL = 100 * 20          # Hadoop SequenceFile.SYNC_INTERVAL (bytes between sync markers)
 
 
@@ -65,18 +66,29 @@ def _text(b):
 
 
 # ---------------------------------------------------------------------------------------------- writer / reader
-class SequenceFileWriter:
-    """Uncompressed SequenceFile (version 6) of Text key/value pairs."""
+def _writable(cls, b):
+    """Hadoop serialisation of one key / value: Text = vlong length + UTF-8, BytesWritable = int32 length + bytes."""
+    if cls == _BYTES:
+        b = bytes(b)
+        return struct.pack(">i", len(b)) + b
+    return _text(b)
 
-    def __init__(self, path):
+
+class SequenceFileWriter:
+    """Uncompressed SequenceFile (version 6); keys / values are Text (default) or BytesWritable (``_BYTES``, the
+    COCO generator's record type)."""
+
+    def __init__(self, path, key_class=_TEXT, value_class=_TEXT):
         self.f = open(path, "wb")
         self.sync = os.urandom(16)
-        hdr = b"SEQ" + bytes([6]) + _text(_TEXT) + _text(_TEXT) + b"\x00\x00" + struct.pack(">i", 0) + self.sync
+        self.key_class, self.value_class = key_class, value_class
+        hdr = (b"SEQ" + bytes([6]) + _text(key_class) + _text(value_class) + b"\x00\x00" + struct.pack(">i", 0)
+               + self.sync)
         self.f.write(hdr)
         self._last_sync = self.f.tell()
 
     def append(self, key, value):
-        k, v = _text(key), _text(value)
+        k, v = _writable(self.key_class, key), _writable(self.value_class, value)
         if self.f.tell() >= self._last_sync + SYNC_INTERVAL:
             self.f.write(struct.pack(">i", -1) + self.sync)
             self._last_sync = self.f.tell()
@@ -93,7 +105,7 @@ class SequenceFileWriter:
 
 
 def read_sequence_file(path):
-    """Yield (key bytes, value bytes) of an uncompressed Text/Text SequenceFile."""
+    """Yield (key bytes, value bytes) of an uncompressed SequenceFile of Text / BytesWritable pairs."""
     with open(path, "rb") as f:
         buf = f.read()
     if buf[:3] != b"SEQ":
@@ -131,9 +143,15 @@ def read_sequence_file(path):
         kb = buf[pos:pos + key_len]
         vb = buf[pos + key_len:pos + rec_len]
         pos += rec_len
-        kn, kp = read_vlong(kb, 0)
-        vn, vp = read_vlong(vb, 0)
-        yield kb[kp:kp + kn], vb[vp:vp + vn]
+        yield _unwritable(names[0], kb), _unwritable(names[1], vb)
+
+
+def _unwritable(cls, b):
+    if cls == _BYTES:
+        (n,) = struct.unpack_from(">i", b, 0)
+        return b[4:4 + n]
+    n, p = read_vlong(b, 0)
+    return b[p:p + n]
 
 
 def read_label(key):

@@ -16,6 +16,18 @@
                          (S/example/imageclassification)
     tfloadandsave        TensorFlow interop: save a model as a TF GraphDef, load it back and compare
                          (S/example/tensorflow/loadandsave)
+    tftransferlearning   TensorFlow GraphDef as a frozen feature extractor + a newly trained head
+                         (S/example/tensorflow/transferlearning)
+    lenetlocal           LeNet-5 train / test / predict on MNIST idx files in one process (S/example/lenetLocal)
+    mlpipeline           DLClassifier / DLEstimator DataFrame pipelines: LeNet, logistic regression, multi-label
+                         linear regression (S/example/MLPipeline)
+    imagetransferlearning  DataFrame image embeddings from a pre-trained net + DLClassifier
+                         (S/example/dlframes/imageTransferLearning)
+    keras                Keras-style LeNet: Sequential / compile / fit / evaluate / predict (S/example/keras)
+    int8                 calibrated int8 scales (calcScales -> JSON) and int8 inference vs fp32
+                         (S/example/mkldnn/int8/GenerateInt8Scales, ImageNetInference)
+    seqfile              ImageNet / COCO Hadoop SequenceFile generators (S/models/utils/*SeqFileGenerator)
+    perf                 ResNet-50 / VGG-16 / Inception training or fused-inference throughput (S/nn/mkldnn/Perf)
 
 Every example runs on synthetic data when no data directory is given (no network access for datasets).
 """
@@ -30,6 +42,14 @@ EXAMPLES = {
     "udfpredictor": "udf_predictor",
     "imagepredictor": "image_predictor",
     "tfloadandsave": "tf_load_and_save",
+    "tftransferlearning": "tf_transfer_learning",
+    "lenetlocal": "lenet_local",
+    "mlpipeline": "ml_pipeline",
+    "imagetransferlearning": "image_transfer_learning",
+    "keras": "keras_lenet",
+    "int8": "int8_inference",
+    "seqfile": "seqfile_generator",
+    "perf": "perf",
 }
 
 

@@ -13,6 +13,7 @@ MFMA-friendly NHWC physical layout) and the hot layers dispatch to the gfx950 HI
 ``bigdl_amd.ops``. On CPU every layer computes in fp32 with torch reference math.
 """
 import copy
+import itertools
 import time
 
 import torch
@@ -72,6 +73,8 @@ def _has_nonleaf(v):
         return any(_has_nonleaf(x) for x in v)
     return False
 
+
+_NAME_SEQ = itertools.count(1)
 
 class _RecordInit(type):
     """Records the constructor arguments of every module (used by the serializer and cloneModule)."""
@@ -204,7 +207,9 @@ class AbstractModule(MklInt8Convertible, metaclass=_RecordInit):
 
     def getName(self):
         if self._name is None:
-            self._name = f"{type(self).__name__}{id(self) % 100000:05d}"
+            # unique per process (the reference appends a random 32-bit hex): an object-id-derived suffix collides
+            # inside large models and breaks name-matched weight loading (Caffe / TF / serializer)
+            self._name = f"{type(self).__name__}{next(_NAME_SEQ):08x}"
         return self._name
 
     def hasName(self):

@@ -52,3 +52,49 @@ def test_model_validator_loads_every_format(fmt):
 def test_examples_cli_lists_examples(capsys):
     assert examples.main([]) == 2
     assert "textclassification" in capsys.readouterr().out
+
+
+def test_lenet_local_train_test_predict():
+    r = _run("lenetlocal", ["--maxEpoch", "2"])
+    assert r["top1"] >= 0.9 and r["predicted"] == r["labels"]
+
+
+@pytest.mark.parametrize("task,key,bound", [("logreg", "train_accuracy", 0.9), ("multilabel", "mse", 1e-3),
+                                            ("lenet", "test_accuracy", 0.7)])
+def test_ml_pipeline_tasks(task, key, bound):
+    r = _run("mlpipeline", ["--task", task, "--maxEpoch", "5"])
+    assert (r[key] >= bound) if key != "mse" else (r[key] <= bound)
+
+
+def test_keras_lenet_trains():
+    r = _run("keras", ["--maxEpoch", "3"])
+    assert r["test_accuracy"] >= 0.9 and r["predict_shape"] == [8, 10]
+
+
+def test_int8_scales_then_inference():
+    r = _run("int8", ["--imageSize", "32", "--valSize", "16", "--calibSize", "8"])
+    assert r["layers_with_scales"] > 10 and r["top1_agreement"] >= 0.8 and r["rel_output_error"] < 0.1
+
+
+def test_tf_transfer_learning_trains_head_only():
+    r = _run("tftransferlearning", ["--maxEpoch", "4"])
+    assert r["extractor_frozen"] and r["test_accuracy"] >= 0.9
+
+
+def test_image_transfer_learning():
+    r = _run("imagetransferlearning", [])
+    assert r["images"] == 16 and r["test_accuracy"] >= 0.75
+
+
+@pytest.mark.parametrize("mode", ["imagenet", "coco"])
+def test_seqfile_generators(mode):
+    r = _run("seqfile", ["--mode", mode, "--blockSize", "2"])
+    assert r["records"] == (12 if mode == "imagenet" else 3)
+    if mode == "coco":
+        assert r["annotations"] == 6
+
+
+def test_perf_inference_cpu():
+    r = _run("perf", ["--model", "resnet50", "--batchSize", "1", "--iteration", "1", "--training", "0",
+                      "--classNum", "10"])
+    assert r["images_per_s"] > 0
