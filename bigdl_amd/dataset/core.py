@@ -268,7 +268,18 @@ class AbstractDataSet:
         return False
 
 
-class LocalArrayDataSet(AbstractDataSet):
+class LocalDataSet(AbstractDataSet):
+    """A dataset iterated in this process (reference LocalDataSet, DataSet.scala:134-153): ``data`` yields the
+    elements, ``toLocal`` is the identity, it is never distributed."""
+
+    def toLocal(self):
+        return self
+
+    def isDistributed(self):
+        return False
+
+
+class LocalArrayDataSet(LocalDataSet):
     """In-memory dataset; training iteration is an infinite stream reshuffled every epoch starting at a
     random offset (reference DataSet.scala:247-324)."""
 
@@ -317,6 +328,50 @@ class DistributedDataSet(LocalArrayDataSet):
 
     def originRDD(self):
         return self.buffer
+
+
+class CachedDistriDataSet(DistributedDataSet):
+    """Rank-local partition held in memory with an index permutation (reference CachedDistriDataSet,
+    DataSet.scala:247-321).
+
+    ``data(True)`` is an endless stream over this rank's elements in index order starting at a random offset
+    (``RNG.uniform(0, n - (groupSize - 1))``); ``data(False)`` walks them once in order. ``shuffle`` draws a new
+    permutation unless ``isInOrder`` (sequence data whose consecutive ``groupSize`` records form one batch).
+    ``cache`` / ``unpersist`` toggle ``isCached``; ``originRDD`` is the partition buffer."""
+
+    def __init__(self, buffer, isInOrder=False, groupSize=1, rank=None, world=None):
+        super().__init__(buffer, shuffle=False, rank=rank, world=world)
+        self.isInOrder, self.groupSize = bool(isInOrder), int(groupSize)
+        self.indexes = list(range(len(self.buffer)))
+        self.isCached = False
+
+    def data(self, train):
+        from ..utils.random_generator import RNG
+
+        n = len(self.buffer)
+        if not train:
+            for i in range(n):
+                yield self.buffer[self.indexes[i]]
+            return
+        if n == 0:
+            return
+        group = self.groupSize if self.isInOrder else 1
+        span = max(1, n - (group - 1))
+        i = int(RNG.uniform(0, span))
+        while True:
+            yield self.buffer[self.indexes[i % n]]
+            i += 1
+
+    def shuffle(self):
+        if not self.isInOrder:
+            perm = torch.randperm(len(self.buffer), generator=self._gen).tolist()
+            self.indexes = perm
+
+    def cache(self):
+        self.isCached = True
+
+    def unpersist(self):
+        self.isCached = False
 
 
 class TransformedDataSet(AbstractDataSet):
@@ -378,7 +433,17 @@ def batches_per_epoch(size, batch):
     return int(math.ceil(size / float(batch)))
 
 
-# reference names (S/dataset/DataSet.scala, MiniBatch.scala): one local dataset type and one dense mini-batch type
-LocalDataSet = AbstractDataSet
-CachedDistriDataSet = DistributedDataSet
-ArrayTensorMiniBatch = MiniBatch
+class ArrayTensorMiniBatch(MiniBatch):
+    """Dense mini-batch built from per-sample tensors (reference ArrayTensorMiniBatch, MiniBatch.scala:92): stacks
+    ``inputData`` / ``targetData`` (lists of equally shaped tensors, or of tensor lists for multi-input samples)
+    into batch tensors (a Table for several inputs)."""
+
+    def __init__(self, inputData, targetData=None):
+        def stack(col):
+            if col is None or len(col) == 0:
+                return None
+            if isinstance(col[0], (list, tuple)):
+                return Table(*[torch.stack([c[j] for c in col]) for j in range(len(col[0]))])
+            return torch.stack(list(col))
+
+        super().__init__(stack(inputData), stack(targetData))

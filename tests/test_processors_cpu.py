@@ -49,7 +49,7 @@ def test_reference_named_entry_points(tmp_path):
     from bigdl_amd.interop.tensorflow import BigDLToTensorflow, TensorflowLoader, TensorflowSaver, TensorflowToBigDL
     from bigdl_amd.utils.serializer import ModuleLoader, ModulePersister
 
-    assert D.ArrayTensorMiniBatch is D.MiniBatch and O.AbstractOptimizer is O.Optimizer
+    assert issubclass(D.ArrayTensorMiniBatch, D.MiniBatch) and O.AbstractOptimizer is O.Optimizer
     assert TensorflowToBigDL is TensorflowLoader and BigDLToTensorflow is TensorflowSaver
     m = nn.Sequential().add(nn.Linear(3, 2))
     p = str(tmp_path / "m.bigdl")
