@@ -205,6 +205,108 @@ __global__ void maxpool_bwd_kernel(const bf16_t* __restrict__ dy, const uint8_t*
   }
 }
 
+// Fixed K x K / stride-S windows (the 3x3 / 2 stem pools of ResNet and Inception): 32-bit index math (the host
+// checks the element counts) and every window load issued before the first compare, so a lane keeps K*K
+// 16-byte loads in flight instead of walking the window one dependent branch at a time.
+template <int K, int S>
+__global__ __launch_bounds__(256) void maxpool_fwd_fixed_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
+                                                                uint8_t* __restrict__ idx, int N, int H, int W, int C,
+                                                                int OH, int OW, int ph, int pw) {
+  const int G = C >> 3;
+  const int total = N * OH * OW * G;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
+    const int g = i % G;
+    int p = i / G;
+    const int ow = p % OW; p /= OW;
+    const int oh = p % OH;
+    const int n = p / OH;
+    const int h0 = oh * S - ph, w0 = ow * S - pw;
+    v4u v[K * K];
+    bool ok[K * K];
+#pragma unroll
+    for (int r = 0; r < K; ++r)
+#pragma unroll
+      for (int s = 0; s < K; ++s) {
+        const int ih = h0 + r, iw = w0 + s;
+        const bool in = (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+        ok[r * K + s] = in;
+        const long off = in ? (long)((n * H + ih) * W + iw) * C + g * 8 : (long)g * 8;
+        v[r * K + s] = *reinterpret_cast<const v4u*>(x + off);
+      }
+    float best[8];
+    uint8_t bi[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { best[e] = -INFINITY; bi[e] = 0; }
+#pragma unroll
+    for (int t = 0; t < K * K; ++t) {
+      if (!ok[t]) continue;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float l = lo_bf(v[t][e]), h = hi_bf(v[t][e]);
+        if (l > best[2 * e] || (l != l)) { best[2 * e] = l; bi[2 * e] = (uint8_t)t; }
+        if (h > best[2 * e + 1] || (h != h)) { best[2 * e + 1] = h; bi[2 * e + 1] = (uint8_t)t; }
+      }
+    }
+    v4u o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = pack2bf(best[2 * e], best[2 * e + 1]);
+    reinterpret_cast<v4u*>(y)[i] = o;
+    uint2 packed;
+    packed.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | ((unsigned)bi[3] << 24);
+    packed.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | ((unsigned)bi[7] << 24);
+    reinterpret_cast<uint2*>(idx)[i] = packed;
+  }
+}
+
+// gather-form backward of the fixed window: an input pixel is covered by at most ceil(K/S) outputs per axis
+template <int K, int S>
+__global__ __launch_bounds__(256) void maxpool_bwd_fixed_kernel(const bf16_t* __restrict__ dy,
+                                                                const uint8_t* __restrict__ idx,
+                                                                bf16_t* __restrict__ dx, int N, int H, int W, int C,
+                                                                int OH, int OW, int ph, int pw) {
+  constexpr int M = (K + S - 1) / S;
+  const int G = C >> 3;
+  const int total = N * H * W * G;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
+    const int g = i % G;
+    int p = i / G;
+    const int iw = p % W; p /= W;
+    const int ih = p % H;
+    const int n = p / H;
+    const int ohh = (ih + ph) / S, owh = (iw + pw) / S;
+    uint2 ix[M * M];
+    v4u d[M * M];
+    int widx[M * M];
+#pragma unroll
+    for (int a = 0; a < M; ++a)
+#pragma unroll
+      for (int b = 0; b < M; ++b) {
+        const int oh = ohh - a, ow = owh - b;
+        const int r = ih + ph - oh * S, s = iw + pw - ow * S;
+        const bool in = oh >= 0 && oh < OH && ow >= 0 && ow < OW && r < K && s < K;
+        const int o = in ? ((n * OH + oh) * OW + ow) * G + g : g;
+        ix[a * M + b] = reinterpret_cast<const uint2*>(idx)[o];
+        d[a * M + b] = reinterpret_cast<const v4u*>(dy)[o];
+        widx[a * M + b] = in ? r * K + s : -1;
+      }
+    float acc[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+#pragma unroll
+    for (int t = 0; t < M * M; ++t) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int b = (int)(((e < 4 ? ix[t].x : ix[t].y) >> ((e & 3) * 8)) & 0xff);
+        if (b == widx[t]) acc[e] += (e & 1) ? hi_bf(d[t][e >> 1]) : lo_bf(d[t][e >> 1]);
+      }
+    }
+    v4u out;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) out[e] = pack2bf(acc[2 * e], acc[2 * e + 1]);
+    reinterpret_cast<v4u*>(dx)[i] = out;
+  }
+}
+
 __device__ __forceinline__ int pool_count(int oh, int ow, int H, int W, int kh, int kw, int sh, int sw, int ph, int pw,
                                           int count_pad) {
   int hs = oh * sh - ph, ws = ow * sw - pw;
@@ -567,14 +669,20 @@ void bigdl_cast_bf16_f32(const uint16_t* x, float* y, long n, hipStream_t st) {
 }
 void bigdl_maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* idx, int N, int H, int W, int C, int OH, int OW,
                        int kh, int kw, int sh, int sw, int ph, int pw, hipStream_t st) {
-  maxpool_fwd_kernel<<<grid_cap((long)N * OH * OW * (C / 8)), 256, 0, st>>>(x, y, idx, N, H, W, C, OH, OW, kh, kw, sh,
-                                                                            sw, ph, pw);
+  const long outs = (long)N * OH * OW * (C / 8), ins = (long)N * H * W * C;
+  if (kh == 3 && kw == 3 && sh == 2 && sw == 2 && outs < (1l << 31) && ins < (1l << 31))
+    maxpool_fwd_fixed_kernel<3, 2><<<grid_cap(outs), 256, 0, st>>>(x, y, idx, N, H, W, C, OH, OW, ph, pw);
+  else
+    maxpool_fwd_kernel<<<grid_cap(outs), 256, 0, st>>>(x, y, idx, N, H, W, C, OH, OW, kh, kw, sh, sw, ph, pw);
   HIP_LAUNCH_CHECK();
 }
 void bigdl_maxpool_bwd(const uint16_t* dy, const uint8_t* idx, uint16_t* dx, int N, int H, int W, int C, int OH,
                        int OW, int kh, int kw, int sh, int sw, int ph, int pw, hipStream_t st) {
-  maxpool_bwd_kernel<<<grid_cap((long)N * H * W * (C / 8)), 256, 0, st>>>(dy, idx, dx, N, H, W, C, OH, OW, kh, kw, sh,
-                                                                          sw, ph, pw);
+  const long ins = (long)N * H * W * (C / 8), outs = (long)N * OH * OW * C;
+  if (kh == 3 && kw == 3 && sh == 2 && sw == 2 && ins < (1l << 31) && outs < (1l << 31))
+    maxpool_bwd_fixed_kernel<3, 2><<<grid_cap(ins), 256, 0, st>>>(dy, idx, dx, N, H, W, C, OH, OW, ph, pw);
+  else
+    maxpool_bwd_kernel<<<grid_cap(ins), 256, 0, st>>>(dy, idx, dx, N, H, W, C, OH, OW, kh, kw, sh, sw, ph, pw);
   HIP_LAUNCH_CHECK();
 }
 void bigdl_avgpool_fwd(const uint16_t* x, uint16_t* y, int N, int H, int W, int C, int OH, int OW, int kh, int kw,

@@ -223,6 +223,25 @@ def test_maxpool_avgpool():
     assert _rel(da, xr.grad) < 1e-2
 
 
+@pytest.mark.parametrize("shape,k,s,p,ceil", [((2, 64, 15, 15), 3, 2, 1, False), ((3, 24, 16, 13), 3, 2, 0, True),
+                                                ((2, 8, 112, 112), 3, 2, 1, False), ((2, 16, 9, 9), 3, 1, 1, False),
+                                                ((2, 32, 10, 11), 2, 2, 0, False)])
+def test_maxpool_window_variants(shape, k, s, p, ceil):
+    """The fixed 3x3/2 kernels and the generic ones against torch (values exact, gradients summed per winner)."""
+    from bigdl_amd.ops import pool
+
+    torch.manual_seed(0)
+    x = torch.randn(*shape, device=_dev()).to(BF, memory_format=CL)
+    y, idx = pool.maxpool_fwd_gpu(x, k, k, s, s, p, p, ceil)
+    xr = x.float().requires_grad_(True)
+    yr = F.max_pool2d(xr, k, s, p, ceil_mode=ceil)
+    assert y.shape == yr.shape and torch.equal(y.float(), yr)
+    gy = torch.randn_like(yr).to(BF, memory_format=CL)
+    dx = pool.maxpool_bwd_gpu(gy, idx, x.shape, k, k, s, s, p, p)
+    yr.backward(gy.float())
+    assert _rel(dx, xr.grad) < 1e-2
+
+
 def test_softmax_xent():
     from bigdl_amd import ops
 
