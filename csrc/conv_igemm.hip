@@ -125,9 +125,12 @@ __device__ __forceinline__ void nt_epilogue(const ConvArgs& a, v4f (&acc)[MI][NI
 // are conflict-free — then re-reads it row-wise: a lane owns 8 channels of one pixel, so every store is
 // 16 B and one wave instruction writes 64/(TN/8) whole pixel rows of TN channels. bias / addend / ReLU /
 // BN statistics are applied in the row phase (the addend is read with the same 16-byte coalesced pattern).
-template <int MI, int NI, int TM, int TN, int NH = 1>
+// PAIR > 0: the workgroup's two pixel-half waves (wm = 0 / 1) that share a channel range combine their BN
+// statistics through LDS (PAIR = float offset from the wm = 0 wave's slice to its partner's) and only the wm = 0
+// wave issues the atomics: half the atomic traffic into the statistics slots.
+template <int MI, int NI, int TM, int TN, int NH = 1, int PAIR = 0>
 __device__ __forceinline__ void nt_epilogue_lds(const ConvArgs& a, v4f (&acc)[MI][NI], int mbase, int nbase,
-                                                int lane, int bid, float* wl) {
+                                                int lane, int bid, float* wl, int wm = 0) {
   constexpr int GR = TN / 4;            // 16-byte fp32 granules per pixel row
   constexpr int LPR = TN / 8;           // lanes per pixel row in the read phase
   constexpr int PPI = 64 / LPR;         // pixels per read instruction
@@ -265,6 +268,19 @@ __device__ __forceinline__ void nt_epilogue_lds(const ConvArgs& a, v4f (&acc)[MI
       for (int o = LPR; o < 64; o <<= 1) {
         s1[e] += __shfl_xor(s1[e], o, 64);
         s2[e] += __shfl_xor(s2[e], o, 64);
+      }
+    }
+    if constexpr (PAIR > 0) {
+      // the wm = 1 wave's own slice is free (its row phase has consumed it): park the sums there
+      if (wm == 1 && lane < LPR) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { wl[lane * 16 + e] = s1[e]; wl[lane * 16 + 8 + e] = s2[e]; }
+      }
+      __syncthreads();
+      if (wm == 1) return;
+      if (lane < LPR) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { s1[e] += wl[PAIR + lane * 16 + e]; s2[e] += wl[PAIR + lane * 16 + 8 + e]; }
       }
     }
     if (lane < LPR && nok) {
@@ -541,11 +557,13 @@ __global__ __launch_bounds__(256, NST == 1 ? 3 : 2) void conv_nt_glds_kernel(Con
   }
   if constexpr (NST == 1) {   // launched for aligned outputs only (bigdl_conv_nt)
     constexpr int NH = NI >= 4 ? 4 : 2;   // row chunks: fewer live epilogue registers on the wide tile
-    nt_epilogue_lds<MI, NI, TM, TN, NH>(a, acc, m0 + wm * TM, n0 + wn * TN, lane, bid,
-                                        reinterpret_cast<float*>(lds) + wave * (TM / NH) * TN);
+    constexpr int SL = (TM / NH) * TN;
+    nt_epilogue_lds<MI, NI, TM, TN, NH, WM == 2 ? WN * SL : 0>(a, acc, m0 + wm * TM, n0 + wn * TN, lane, bid,
+                                                               reinterpret_cast<float*>(lds) + wave * SL, wm);
   } else if ((a.Ncol & 7) == 0 && (a.ldo & 7) == 0) {
-    nt_epilogue_lds<MI, NI, TM, TN>(a, acc, m0 + wm * TM, n0 + wn * TN, lane, bid,
-                                    reinterpret_cast<float*>(lds) + wave * TM * TN);
+    nt_epilogue_lds<MI, NI, TM, TN, 1, WM == 2 ? WN * TM * TN : 0>(a, acc, m0 + wm * TM, n0 + wn * TN, lane, bid,
+                                                                   reinterpret_cast<float*>(lds) + wave * TM * TN,
+                                                                   wm);
   } else {
     nt_epilogue<MI, NI, TM, TN>(a, acc, m0 + wm * TM, n0 + wn * TN, lane, bid);
   }

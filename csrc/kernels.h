@@ -62,7 +62,7 @@ void bigdl_transpose_krsc(const uint16_t* w, uint16_t* wt, int K, int RS, int C,
 
 // batch norm (NHWC bf16, fp32 statistics). Statistics / backward-reduction buffers are
 // [BIGDL_STAT_SLOTS][2][C] fp32, zeroed by the caller; producers add into slot (block id % slots).
-#define BIGDL_STAT_SLOTS 32
+#define BIGDL_STAT_SLOTS 128
 void bigdl_bn_stats(const uint16_t* x, float* stats, long P, int C, hipStream_t st);
 void bigdl_bn_finalize(const float* stats, int nslots, const float* gamma, const float* beta, float* run_mean,
                        float* run_var, float* save_mean, float* save_invstd, float* scale, float* shift,
