@@ -9,7 +9,7 @@ work the producer already did.
   conv -> BN          conv epilogue emits per-channel (sum, sumsq): BN skips its statistics pass
   BN -> ReLU          ReLU applied in the BN apply pass; backward mask from the BN output
   conv/Linear -> ReLU ReLU in the GEMM epilogue
-  BN -> ReLU -> conv  (opt-in, BIGDL_DGRAD_BN=1) backward: the conv's data-gradient epilogue reduces the BN's
+  BN -> ReLU -> conv  (default; BIGDL_DGRAD_BN=0 disables) backward: the conv's data-gradient epilogue reduces the BN's
                       backward statistics (sum dy, sum dy * (x - mean) under the ReLU mask): BN skips its
                       reduction pass
   ResNet block        Sequential[ConcatTable[branch(... BN), shortcut], CAddTable, ReLU]: the shortcut runs
@@ -38,10 +38,10 @@ def _reset(m):
 
 
 def _dgrad_bn_enabled():
-    """Off by default: measured on ResNet-50 b256 (profiles/r1_dgrad_bn_ab.txt) the extra x / z reads in the
-    dgrad epilogue cost the GEMM +2.7 ms/step while the skipped reduction pass saved 2.4 ms — the epilogue
-    runs at 2 workgroups per CU with nothing to overlap its reads, the separate pass streams at full bandwidth."""
-    return os.environ.get("BIGDL_DGRAD_BN", "0") == "1"
+    """On by default since the statistics epilogue pairs its two waves' sums in LDS and spreads the atomics over
+    128 slots: ResNet-50 b256 30.6 -> 30.2 ms/step (profiles/r2_dgrad_bn_ab.txt). With 32 slots and one atomic
+    per wave it lost (+2.7 ms GEMM vs -2.4 ms reduction pass, profiles/r1_dgrad_bn_ab.txt)."""
+    return os.environ.get("BIGDL_DGRAD_BN", "1") == "1"
 
 
 def fuse_for_training(model):

@@ -230,7 +230,7 @@ def test_dgrad_epilogue_bn_reduction_matches_separate_pass(monkeypatch):
     monkeypatch.setattr(C_, "bn_bwd_reduce", counting)
     res = {}
     for mode in ("0", "1"):
-        monkeypatch.setenv("BIGDL_DGRAD_BN", mode)     # opt-in fusion (see nn/fusion.py)
+        monkeypatch.setenv("BIGDL_DGRAD_BN", mode)     # fusion on / off (see nn/fusion.py)
         m = copy.deepcopy(cpu).to("cuda")
         fuse_for_training(m)
         calls.clear()
