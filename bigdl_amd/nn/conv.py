@@ -254,7 +254,10 @@ class SpatialConvolution(TensorModule):
             if gy16.shape[1] % 8:   # output channels not a multiple of 8: zero-pad K for the GEMM
                 gy16 = cv.pad_dim(gy16, 1)
                 w16 = cv.pad_dim(w16, 0)
-            wt = cv.transpose_w(w16)
+            wt = getattr(self, "_wt_cache", None)
+            if getattr(self, "_wt_stamp", None) != cv.WT_STAMP[0] or wt is None or \
+                    tuple(wt.shape) != (w16.shape[1], w16.shape[2], w16.shape[3], w16.shape[0]):
+                wt = cv.transpose_w(w16)        # not batched by TrainStep this step (or padded K)
             Cp = w16.shape[1]
             xs = (x.shape[0], Cp, x.shape[2], x.shape[3])
             addend = getattr(self, "_dgrad_addend", None)

@@ -193,6 +193,60 @@ def conv2d_dgrad(dy, w16t, x_shape, stride, pad, dil=(1, 1), out=None, addend=No
     return out
 
 
+# Batched weight transposes for the data-gradient GEMMs: TrainStep transposes every eligible conv's bf16 weight in
+# one launch right before backward and stamps the modules; a conv whose stamp matches WT_STAMP reuses that buffer.
+WT_STAMP = [0]
+_DESC_CACHE = {}
+DESC_BUILDS = [0]            # descriptor tables built (one per distinct set of weight / buffer addresses)
+
+
+def prepare_dgrad_weights(convs):
+    """Transpose the (K, C, R, S) bf16 weights of ``convs`` (modules with ``_w16_padded``) into their
+    ``_wt_cache`` (C, R, S, K) buffers with one kernel launch (csrc/conv_igemm.hip transpose_krsc_batched_kernel).
+    Only layers whose bf16 weight is the persistent managed view (C % 8 == 0, K % 8 == 0) take part, so the
+    descriptor table is built once (before any HIP-graph capture) and reused."""
+    WT_STAMP[0] += 1
+    rows, mods, tile = [], [], 0
+    for m in convs:
+        if not getattr(m, "_w16_managed", False):      # per-call bf16 casts have no stable address
+            continue
+        wf = getattr(m, "weight", None)
+        if wf is None or wf.dim() != 4 or wf.shape[0] % 8 or wf.shape[1] % 8:
+            continue                                    # channel-padded weights are rebuilt per call
+        w16 = m._w16_padded()
+        K, C, R, S = w16.shape
+        if K % 8 or C % 8 or not w16.is_cuda or not w16.is_contiguous(memory_format=CL):
+            continue
+        wt = getattr(m, "_wt_cache", None)
+        if wt is None or tuple(wt.shape) != (C, R, S, K) or wt.device != w16.device:
+            wt = torch.empty((C, R, S, K), dtype=BF16, device=w16.device)
+            m._wt_cache = wt
+        rows.append((w16.data_ptr(), wt.data_ptr(), K, R * S, C, tile))
+        tile += ((C + 31) // 32) * ((K + 31) // 32) * R * S
+        mods.append(m)
+    if not rows:
+        return 0
+    key = tuple(rows)
+    desc = _DESC_CACHE.get(key)
+    if desc is None:
+        if torch.cuda.is_current_stream_capturing():
+            return 0                 # no host->device copy inside a graph capture: per-layer transposes instead
+        if len(_DESC_CACHE) > 8:
+            _DESC_CACHE.clear()
+        desc = torch.tensor(rows, dtype=torch.int64).to(mods[0]._wt_cache.device)
+        _DESC_CACHE[key] = desc
+        DESC_BUILDS[0] += 1
+    native.get().transpose_krsc_batched(desc, len(rows), tile)
+    for m in mods:
+        m._wt_stamp = WT_STAMP[0]
+    return len(rows)
+
+
+def end_dgrad_weights():
+    """Invalidate the batched transposes (the optimizer is about to change the weights)."""
+    WT_STAMP[0] += 1
+
+
 def transpose_w(w16, out=None):
     """(K, C, R, S) channels_last bf16 -> contiguous (C, R, S, K) bf16 for the data-gradient GEMM."""
     K, C, R, S = w16.shape

@@ -281,11 +281,32 @@ class TrainStep:
             out = m.forward(x)
         loss = c.forward(out, y)
         gout = c.backward(out, y)
-        if self.bucketed is not None:
-            self.bucketed.backward(x, gout)
-        else:
-            m.backward(x, gout)
+        convs = self._dgrad_convs()
+        if convs:
+            from ..ops import conv as cv
+
+            cv.prepare_dgrad_weights(convs)       # every conv weight transposed for its dgrad in one launch
+        try:
+            if self.bucketed is not None:
+                self.bucketed.backward(x, gout)
+            else:
+                m.backward(x, gout)
+        finally:
+            if convs:
+                cv.end_dgrad_weights()
         return loss
+
+    def _dgrad_convs(self):
+        """Convolutions whose backward runs the native data-gradient GEMM (GPU engine, one group)."""
+        if getattr(self, "_dgrad_conv_list", None) is None:
+            from ..nn.conv import SpatialConvolution
+
+            dev = getattr(self, "device", None)
+            ok = dev is not None and torch.device(dev).type == "cuda"
+            self._dgrad_conv_list = [q for q in self.model.flattened_layers()
+                                     if ok and isinstance(q, SpatialConvolution) and getattr(q, "nGroup", 1) == 1
+                                     and hasattr(q, "_dgrad_gpu") and hasattr(q, "_w16_padded")]
+        return self._dgrad_conv_list
 
     def _lockstep(self):
         """Keep every method clone's iteration/epoch counters equal to its primary's."""

@@ -452,6 +452,15 @@ void upsample_nearest(const Tensor& src, const Tensor& dst, std::vector<int64_t>
               "upsample_nearest: output extent must be input x factor");
 }
 
+// batched KRSC -> CRSK weight transposes (one launch for all conv layers): desc built by ops/conv.py
+void transpose_krsc_batched(const Tensor& desc, int64_t n, int64_t total_tiles) {
+  TORCH_CHECK(desc.is_cuda() && desc.scalar_type() == at::kLong && desc.is_contiguous() && desc.numel() == 6 * n,
+              "transpose_krsc_batched: desc must be a device int64 [n, 6] tensor");
+  TORCH_CHECK(n >= 0 && n < (1 << 16) && total_tiles >= 0 && total_tiles < (1ll << 31), "transpose_krsc_batched: size");
+  bigdl_transpose_krsc_batched(reinterpret_cast<const long*>(desc.data_ptr<int64_t>()), (int)n, (int)total_tiles,
+                               stream());
+}
+
 // detection (csrc/detection.hip)
 static void check_f32(const Tensor& t, const char* n) {
   TORCH_CHECK(t.is_cuda() && t.is_contiguous() && t.scalar_type() == at::kFloat, n, ": contiguous fp32 device tensor");
@@ -862,6 +871,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("out_scale") = 0.0, py::arg("addend") = py::none(), py::arg("add_scale") = 0.0);
   m.def("pool_i8", &pool_i8);
   m.def("act_fwd", &act_fwd);
+  m.def("transpose_krsc_batched", &transpose_krsc_batched);
   m.def("image_pipeline", &image_pipeline);
   m.def("act_bwd", &act_bwd);
   m.def("poolnd_fwd", &poolnd_fwd);

@@ -1244,6 +1244,45 @@ __global__ __launch_bounds__(256) void transpose_krsc_kernel(const bf16_t* __res
   }
 }
 
+// All conv weights of a model transposed for the data-gradient GEMMs in ONE launch (once per training step, after
+// the optimizer has rewritten the bf16 weights) instead of one small launch per layer. desc[i] = {w, wt, K, RS, C,
+// first tile}: workgroup b handles 32 x 32 tile (b - first tile) of the last layer whose first tile is <= b.
+__global__ __launch_bounds__(256) void transpose_krsc_batched_kernel(const long* __restrict__ desc, int n) {
+  __shared__ bf16_t tile[32][33];
+  __shared__ int li;
+  const int b = blockIdx.x;
+  if (threadIdx.x == 0) {
+    int i = 0;
+    while (i + 1 < n && desc[(i + 1) * 6 + 5] <= b) ++i;
+    li = i;
+  }
+  __syncthreads();
+  const long* d = desc + li * 6;
+  const bf16_t* w = reinterpret_cast<const bf16_t*>(d[0]);
+  bf16_t* wt = reinterpret_cast<bf16_t*>(d[1]);
+  const int K = (int)d[2], RS = (int)d[3], C = (int)d[4];
+  int t = b - (int)d[5];
+  const int tc = (C + 31) / 32, tk = (K + 31) / 32;
+  const int c0 = (t % tc) * 32;
+  t /= tc;
+  const int k0 = (t % tk) * 32, rs = t / tk;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  bf16_t v[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int k = k0 + ty + 8 * i, c = c0 + tx;
+    v[i] = (k < K && c < C) ? w[((size_t)k * RS + rs) * C + c] : (bf16_t)0;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) tile[ty + 8 * i][tx] = v[i];
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = c0 + ty + 8 * i, k = k0 + tx;
+    if (c < C && k < K) wt[((size_t)c * RS + rs) * K + k] = tile[tx][ty + 8 * i];
+  }
+}
+
 template <int BM, int BN, int WM>
 void launch_nt(const ConvArgs& a, bool fastk, hipStream_t st) {
   const int nwg = ((a.M + BM - 1) / BM) * ((a.Ncol + BN - 1) / BN);
@@ -1407,6 +1446,12 @@ int bigdl_conv_wgrad(const WgradArgs* a_in, hipStream_t st) {
 void bigdl_transpose_krsc(const bf16_t* w, bf16_t* wt, int K, int RS, int C, hipStream_t st) {
   if (RS > 65535) return;
   transpose_krsc_kernel<<<dim3((C + 31) / 32, (K + 31) / 32, RS), 256, 0, st>>>(w, wt, K, RS, C);
+  HIP_LAUNCH_CHECK();
+}
+
+void bigdl_transpose_krsc_batched(const long* desc, int n, int total_tiles, hipStream_t st) {
+  if (n <= 0 || total_tiles <= 0) return;
+  transpose_krsc_batched_kernel<<<dim3(total_tiles), 256, 0, st>>>(desc, n);
   HIP_LAUNCH_CHECK();
 }
 

@@ -59,6 +59,8 @@ int bigdl_conv_wgrad(const WgradArgs* a, hipStream_t st);
 // (0 when the single-split path accumulates straight into dw).
 long bigdl_conv_wgrad_plan(WgradArgs* a);
 void bigdl_transpose_krsc(const uint16_t* w, uint16_t* wt, int K, int RS, int C, hipStream_t st);
+// batched form: desc = device int64 [n][6] {w ptr, wt ptr, K, RS, C, first tile}, tiles of 32 x 32 per (rs)
+void bigdl_transpose_krsc_batched(const long* desc, int n, int total_tiles, hipStream_t st);
 
 // batch norm (NHWC bf16, fp32 statistics). Statistics / backward-reduction buffers are
 // [BIGDL_STAT_SLOTS][2][C] fp32, zeroed by the caller; producers add into slot (block id % slots).

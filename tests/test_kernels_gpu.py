@@ -470,3 +470,61 @@ def test_gemm_shaped_wgrad_on_nt_kernel_matches_fp32(P, K, C, bias):
     assert err < 1e-3, err
     if bias:
         assert torch.allclose(db, refb, rtol=1e-3, atol=1e-2)
+
+
+def test_batched_weight_transpose_matches_per_layer():
+    """transpose_krsc_batched (one launch for every conv of a step) equals the per-layer transpose."""
+    from bigdl_amd.ops import conv as cv
+
+    class _Fake:
+        _w16_managed = True
+
+        def __init__(self, w):
+            self.w = w
+            self.weight = w
+
+        def _w16_padded(self):
+            return self.w
+
+    torch.manual_seed(0)
+    mods = [_Fake(torch.randn(k, c, r, r, device=_dev()).to(BF, memory_format=CL))
+            for k, c, r in [(64, 8, 7), (256, 64, 1), (64, 64, 3), (512, 1024, 1), (40, 24, 3)]]
+    n = cv.prepare_dgrad_weights(mods)
+    assert n == 5
+    for m in mods:
+        assert m._wt_stamp == cv.WT_STAMP[0]
+        assert torch.equal(m._wt_cache, cv.transpose_w(m.w))
+    cv.end_dgrad_weights()
+    assert all(m._wt_stamp != cv.WT_STAMP[0] for m in mods)
+
+
+def test_train_step_with_batched_transposes_matches_per_layer(monkeypatch):
+    """A ResNet training step gives the same weight gradients whether the dgrad weights come from the batched
+    pre-transpose or from per-layer transposes."""
+    import copy
+
+    from bigdl_amd import nn
+    from bigdl_amd.models.resnet import ResNet
+    from bigdl_amd.ops import conv as cv
+    from bigdl_amd.optim.sgd import SGD
+    from bigdl_amd.optim.train_step import TrainStep
+    from bigdl_amd.utils.random_generator import RNG
+
+    RNG.setSeed(3)
+    base = ResNet(10, 20, dataSet="CIFAR10")
+    x = torch.randn(16, 3, 32, 32, device=_dev())
+    y = torch.randint(1, 11, (16,), device=_dev()).float()
+    grads = {}
+    for mode in ("batched", "per_layer"):
+        if mode == "per_layer":
+            monkeypatch.setattr(cv, "prepare_dgrad_weights", lambda convs: cv.WT_STAMP.__setitem__(0, cv.WT_STAMP[0] + 1))
+        step = TrainStep(copy.deepcopy(base), nn.CrossEntropyCriterion(), SGD(learningRate=0.0), device=_dev())
+        builds = cv.DESC_BUILDS[0]
+        for _ in range(3):
+            step.zero_grad()
+            step.forward_backward(x, y)
+        torch.cuda.synchronize()
+        grads[mode] = step.g.clone()
+        if mode == "batched":
+            assert cv.DESC_BUILDS[0] - builds == 1      # one descriptor table for all steps (graph-capture safe)
+    assert _rel(grads["batched"], grads["per_layer"]) < 1e-6
