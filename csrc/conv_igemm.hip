@@ -1426,7 +1426,8 @@ int bigdl_conv_wgrad(const WgradArgs* a_in, hipStream_t st) {
   // tile, so also cap the atomic traffic (splits x |dW| x 4 B) at ~32 MB (~25 us at the chip rate).
   int splits = (512 + tiles - 1) / tiles;
   const long tile_bytes = (long)tiles * WT * WT * 4;
-  const int cap_atomic = (int)((32l << 20) / tile_bytes);
+  static const long atomic_mb = [] { const char* e = getenv("BIGDL_WGRAD_ATOMIC_MB"); return e ? atol(e) : 32l; }();
+  const int cap_atomic = (int)((atomic_mb << 20) / tile_bytes);
   if (splits > cap_atomic) splits = cap_atomic;
   const int maxsplit = (a.M + 4 * WBM - 1) / (4 * WBM);   // >= 4 LDS stages per split
   if (splits > maxsplit) splits = maxsplit;
