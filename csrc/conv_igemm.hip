@@ -128,7 +128,7 @@ __device__ __forceinline__ void nt_epilogue(const ConvArgs& a, v4f (&acc)[MI][NI
 // PAIR > 0: the workgroup's two pixel-half waves (wm = 0 / 1) that share a channel range combine their BN
 // statistics through LDS (PAIR = float offset from the wm = 0 wave's slice to its partner's) and only the wm = 0
 // wave issues the atomics: half the atomic traffic into the statistics slots.
-template <int MI, int NI, int TM, int TN, int NH = 1, int PAIR = 0>
+template <int MI, int NI, int TM, int TN, int NH = 1, int PAIR = 0, int NWM = 2>
 __device__ __forceinline__ void nt_epilogue_lds(const ConvArgs& a, v4f (&acc)[MI][NI], int mbase, int nbase,
                                                 int lane, int bid, float* wl, int wm = 0) {
   constexpr int GR = TN / 4;            // 16-byte fp32 granules per pixel row
@@ -271,16 +271,22 @@ __device__ __forceinline__ void nt_epilogue_lds(const ConvArgs& a, v4f (&acc)[MI
       }
     }
     if constexpr (PAIR > 0) {
-      // the wm = 1 wave's own slice is free (its row phase has consumed it): park the sums there
-      if (wm == 1 && lane < LPR) {
+      // the wm > 0 waves' own slices are free (their row phase has consumed them): park the sums there; the
+      // wm = 0 wave of the channel range adds the NWM - 1 partners (PAIR floats apart) and issues the atomics
+      if (wm > 0 && lane < LPR) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) { wl[lane * 16 + e] = s1[e]; wl[lane * 16 + 8 + e] = s2[e]; }
       }
       __syncthreads();
-      if (wm == 1) return;
+      if (wm > 0) return;
       if (lane < LPR) {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) { s1[e] += wl[PAIR + lane * 16 + e]; s2[e] += wl[PAIR + lane * 16 + 8 + e]; }
+        for (int k = 1; k < NWM; ++k)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            s1[e] += wl[k * PAIR + lane * 16 + e];
+            s2[e] += wl[k * PAIR + lane * 16 + 8 + e];
+          }
       }
     }
     if (lane < LPR && nok) {
@@ -829,8 +835,8 @@ __global__ __launch_bounds__(512, 1) void conv_nt_p3_kernel(ConvArgs a) {
     cur = cur == 2 ? 0 : cur + 1;
   }
   if ((a.Ncol & 7) == 0 && (a.ldo & 7) == 0)
-    nt_epilogue_lds<MI, NI, TM, TN>(a, acc, m0 + wm * TM, n0 + wn * TN, lane, bid,
-                                    reinterpret_cast<float*>(lds) + wave * TM * TN);
+    nt_epilogue_lds<MI, NI, TM, TN, 1, WGN * TM * TN, WGM>(a, acc, m0 + wm * TM, n0 + wn * TN, lane, bid,
+                                                          reinterpret_cast<float*>(lds) + wave * TM * TN, wm);
   else
     nt_epilogue<MI, NI, TM, TN>(a, acc, m0 + wm * TM, n0 + wn * TN, lane, bid);
 }
