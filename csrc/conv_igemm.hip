@@ -1360,7 +1360,11 @@ int bigdl_conv_nt(const ConvArgs* a, hipStream_t st) {
   const long p3_tiles = (long)((a->M + 255) / 256) * ((a->Ncol + 127) / 128);
   const long tiles128 = (long)((a->M + 127) / 128) * ((a->Ncol + (a->Ncol <= 64 ? 63 : 127)) / (a->Ncol <= 64 ? 64 : 128));
   const bool aligned_out = (a->Ncol & 7) == 0 && (a->ldo & 7) == 0;   // the persistent kernel has no fallback epilogue
-  if (fastk && impl == 2 && p3_tiles >= 256) {
+  // deep-K layers on small pixel grids (ResNet stages 4-5: <= 50k output pixels, K >= 1024) run faster on the
+  // 8-wave deep-pipelined kernel (tools/bench_conv.py, impl 1 vs 2); BIGDL_CONV_P3AUTO=0 keeps them on impl 1
+  static const bool p3auto = [] { const char* e = getenv("BIGDL_CONV_P3AUTO"); return e ? atoi(e) != 0 : true; }();
+  const bool p3_pick = impl == 2 || (impl == 1 && p3auto && a->M <= 50176 && a->Kdim >= 1024);
+  if (fastk && p3_pick && p3_tiles >= 256) {
     if (a->Ncol <= 64) launch_nt_p3<64, 8, 1>(*a, st);
     else launch_nt_p3<128, 4, 2>(*a, st);
   } else if (fastk && impl == 3 && aligned_out && tiles128 > 2 * 256) {
