@@ -1391,8 +1391,9 @@ int bigdl_conv_nt(const ConvArgs* a, hipStream_t st) {
 // 64-wide output-channel layers with a deep reduction (stem 7x7, 3x3 over 64 channels) run half-empty 128x128
 // tiles; the register-staged atomic kernel is faster there (measured per layer, profiles/r1_ab_wgrad.txt)
 static bool wgrad_prefers_atomic(const WgradArgs* a) {
+  // BIGDL_WGRAD_ATOMIC: 1 (default) this rule, 0 never, 2 always (per-layer A/B runs)
   static const int on = [] { const char* e = getenv("BIGDL_WGRAD_ATOMIC"); return e ? atoi(e) : 1; }();
-  return on && a->Ncol <= 64 && a->Kdim > 256;
+  return on == 2 || (on == 1 && a->Ncol <= 64 && a->Kdim > 256);
 }
 
 long bigdl_conv_wgrad_plan(WgradArgs* a) {
