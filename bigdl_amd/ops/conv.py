@@ -217,6 +217,8 @@ def prepare_dgrad_weights(convs):
         K, C, R, S = w16.shape
         if K % 8 or C % 8 or not w16.is_cuda or not w16.is_contiguous(memory_format=CL):
             continue
+        if mods and w16.device != mods[0]._wt_cache.device:     # one descriptor table per device
+            continue
         wt = getattr(m, "_wt_cache", None)
         if wt is None or tuple(wt.shape) != (C, R, S, K) or wt.device != w16.device:
             wt = torch.empty((C, R, S, K), dtype=BF16, device=w16.device)
