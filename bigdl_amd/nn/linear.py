@@ -319,6 +319,32 @@ class MM(AutogradModule):
         return a @ b
 
 
+class Gemm(AutogradModule):
+    """y = alpha * op(A) * op(B) + beta * C (ONNX Gemm; reference S/nn/onnx/Gemm.scala:25-80, P/nn/layer.py Gemm).
+
+    Input is A with B and C given at construction (``matrixB`` / ``matrixC``, as the ONNX importer builds it), or a
+    Table(A, B, C). 2-D operands on the GPU engine run on the native MFMA GEMM (``ops/conv_fn.linear``)."""
+
+    def __init__(self, alpha=1.0, beta=1.0, transA=False, transB=False, matrixB=None, matrixC=None):
+        super().__init__()
+        self.alpha, self.beta, self.transA, self.transB = float(alpha), float(beta), bool(transA), bool(transB)
+        self.matrixB = None if matrixB is None else torch.as_tensor(matrixB, dtype=torch.float32)
+        self.matrixC = None if matrixC is None else torch.as_tensor(matrixC, dtype=torch.float32)
+
+    def fn(self, x):
+        if isinstance(x, torch.Tensor):
+            a, b, c = x, self.matrixB.to(x.device), self.matrixC.to(x.device)
+        else:
+            a, b, c = x[1], x[2], x[3]
+        a = a.transpose(-1, -2) if self.transA else a
+        b = b.transpose(-1, -2) if self.transB else b
+        if a.dim() == 2 and b.dim() == 2:
+            ab = conv_fn.linear(a.float(), b.float().t().contiguous())     # a @ b
+        else:
+            ab = a.float() @ b.float()
+        return self.alpha * ab + self.beta * c.float()
+
+
 class MV(AutogradModule):
     def __init__(self, trans=False):
         super().__init__()
@@ -427,7 +453,7 @@ class Highway(AutogradModule):
         return t * h + (1 - t) * x.float()
 
 
-__all__ = ["Linear", "SparseLinear", "Bilinear", "LookupTable", "LookupTableSparse", "MM", "MV", "DotProduct",
+__all__ = ["Linear", "SparseLinear", "Bilinear", "LookupTable", "LookupTableSparse", "MM", "Gemm", "MV", "DotProduct",
            "CosineDistance", "PairwiseDistance", "Cosine", "Euclidean", "CrossProduct", "Maxout", "Highway"]
 
 

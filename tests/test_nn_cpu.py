@@ -312,3 +312,27 @@ def test_calc_scales_then_quantize_uses_static_ranges():
     q = m.quantize()
     assert all(getattr(l, "inputAmax", None) is not None for l in q.flattened_layers()
                if "Quantized" in type(l).__name__)
+
+
+def test_gemm_layer_matches_reference_formula():
+    """nn.Gemm (ONNX Gemm, reference S/nn/onnx/Gemm.scala): alpha * op(A) op(B) + beta * C, constants or Table."""
+    import torch as _t
+
+    from bigdl_amd import nn as _nn
+    from bigdl_amd.utils.table import T as _T
+
+    g = _t.Generator().manual_seed(0)
+    a, b, c = _t.randn(4, 3, generator=g), _t.randn(5, 3, generator=g), _t.randn(4, 5, generator=g)
+    m = _nn.Gemm(0.5, 2.0, False, True, matrixB=b, matrixC=c)
+    assert _t.allclose(m.forward(a), 0.5 * a @ b.t() + 2.0 * c, atol=1e-5)
+    m2 = _nn.Gemm(1.0, 1.0, True, False)
+    y = m2.forward(_T(a.t().contiguous(), b.t().contiguous(), c))
+    assert _t.allclose(y, a @ b.t() + c, atol=1e-5)
+    gi = m2.backward(_T(a.t().contiguous(), b.t().contiguous(), c), _t.ones(4, 5))
+    assert gi[3].shape == c.shape
+
+
+def test_compat_gemm_wrapper():
+    from bigdl_amd.compat.nn.layer import Gemm
+
+    assert Gemm(1.0, 1.0, False, False) is not None
