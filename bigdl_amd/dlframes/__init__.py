@@ -45,12 +45,47 @@ class _Params:
         return "\n".join(f"{k}: {v!r}" for k, v in sorted(self._params.items()))
 
 
+class HasBatchSize(_Params):
+    """Param mixin (reference P/dlframes/dl_classifier.py HasBatchSize)."""
+
+    def setBatchSize(self, v):
+        return self.set("batchSize", int(v))
+
+    def getBatchSize(self):
+        return self.get("batchSize")
+
+
+class HasMaxEpoch(_Params):
+    def setMaxEpoch(self, v):
+        return self.set("maxEpoch", int(v))
+
+    def getMaxEpoch(self):
+        return self.get("maxEpoch")
+
+
+class HasLearningRate(_Params):
+    def setLearningRate(self, v):
+        return self.set("learningRate", float(v))
+
+    def getLearningRate(self):
+        return self.get("learningRate")
+
+
+class HasFeatureSize(_Params):
+    def setFeatureSize(self, v):
+        self.featureSize = list(v)
+        return self
+
+    def getFeatureSize(self):
+        return self.featureSize
+
+
 def _row_tensor(v, size):
     t = torch.as_tensor(np.asarray(v, dtype=np.float32))
     return t.reshape(size) if size else t
 
 
-class DLEstimator(_Params):
+class DLEstimator(HasBatchSize, HasMaxEpoch, HasLearningRate, HasFeatureSize):
     def __init__(self, model, criterion, featureSize, labelSize=(1,)):
         super().__init__(featuresCol="features", labelCol="label", predictionCol="prediction", batchSize=1,
                          maxEpoch=50, learningRate=1e-3, learningRateDecay=0.0, optimMethod=None, endWhen=None)
@@ -153,7 +188,7 @@ class DLEstimator(_Params):
             .setPredictionCol(self.get("predictionCol")).setBatchSize(self.get("batchSize"))
 
 
-class DLModel(_Params):
+class DLModel(HasBatchSize, HasFeatureSize):
     def __init__(self, model, featureSize):
         super().__init__(featuresCol="features", predictionCol="prediction", batchSize=4)
         self.model = model
@@ -281,5 +316,5 @@ class DLImageTransformer(_Params):
         return out_df
 
 
-__all__ = ["DLEstimator", "DLModel", "DLClassifier", "DLClassifierModel", "DLImageReader", "DLImageTransformer",
+__all__ = ["HasBatchSize", "HasMaxEpoch", "HasLearningRate", "HasFeatureSize", "DLEstimator", "DLModel", "DLClassifier", "DLClassifierModel", "DLImageReader", "DLImageTransformer",
            "image_row_to_tensor"]

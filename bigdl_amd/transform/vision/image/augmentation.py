@@ -224,21 +224,47 @@ class Resize(FeatureTransformer):
         f[ImageFeature.mat] = _resize(f.opencvMat(), self.w, self.h, mode)
 
 
+def aspect_scale_hw(h, w, scaleTo, maxSize, scaleMultipleOf=1, minScale=None):
+    """(height, width) after scaling the short side to ``scaleTo`` with the long side capped at ``maxSize`` and
+    both sides floored to multiples of ``scaleMultipleOf`` (reference AspectScale.getHeightWidthAfterRatioScale,
+    S/transform/vision/image/augmentation/Resize.scala:117-141; Java Math.round = floor(x + 0.5))."""
+    lo, hi = min(h, w), max(h, w)
+    s = float(scaleTo) / lo
+    if minScale is not None:
+        s = max(minScale, s)
+    if math.floor(s * hi + 0.5) > maxSize:
+        s = maxSize / float(hi)
+    sh = sw = s
+    if scaleMultipleOf > 1:
+        sh = math.floor(h * s / scaleMultipleOf) * scaleMultipleOf / h
+        sw = math.floor(w * s / scaleMultipleOf) * scaleMultipleOf / w
+    return int(math.floor(sh * h + 0.5)), int(math.floor(sw * w + 0.5))
+
+
 class AspectScale(FeatureTransformer):
     """Resize so the short side equals ``scale`` with the long side capped at ``maxSize``."""
 
-    def __init__(self, scale, scaleMultipleOf=1, maxSize=1000, resizeMode=INTER_LINEAR):
+    def __init__(self, scale, scaleMultipleOf=1, maxSize=1000, resizeMode=INTER_LINEAR, minScale=None):
         self.scale, self.mult, self.maxSize, self.mode = scale, scaleMultipleOf, maxSize, resizeMode
+        self.minScale = minScale
 
     def transformMat(self, f):
         m = f.opencvMat()
-        h, w = m.shape[:2]
-        s = self.scale / min(h, w)
-        if round(s * max(h, w)) > self.maxSize:
-            s = self.maxSize / max(h, w)
-        nh = int(math.floor(h * s / self.mult) * self.mult)
-        nw = int(math.floor(w * s / self.mult) * self.mult)
+        nh, nw = aspect_scale_hw(m.shape[0], m.shape[1], self.scale, self.maxSize, self.mult, self.minScale)
         f[ImageFeature.mat] = _resize(m, nw, nh, self.mode)
+
+
+class RandomAspectScale(FeatureTransformer):
+    """AspectScale to a scale drawn uniformly from ``scales`` (reference Resize.scala:151-160)."""
+
+    def __init__(self, scales, scaleMultipleOf=1, maxSize=1000):
+        self.scales, self.mult, self.maxSize = list(scales), scaleMultipleOf, maxSize
+
+    def transformMat(self, f):
+        m = f.opencvMat()
+        scale = self.scales[min(int(RNG.uniform(0, len(self.scales))), len(self.scales) - 1)]
+        nh, nw = aspect_scale_hw(m.shape[0], m.shape[1], scale, self.maxSize, self.mult)
+        f[ImageFeature.mat] = _resize(m, nw, nh)
 
 
 class RandomResize(FeatureTransformer):
@@ -407,6 +433,43 @@ class RandomAlterAspect(FeatureTransformer):
         s = min(h, w)
         y, x = (h - s) // 2, (w - s) // 2
         f[ImageFeature.mat] = _resize(m[y:y + s, x:x + s], self.L, self.L, self.mode)
+
+
+class FixExpand(FeatureTransformer):
+    """Place the image in the centre of a zero ``expandHeight`` x ``expandWidth`` canvas and record the placed box
+    (reference Expand.scala:102-129)."""
+
+    def __init__(self, expandHeight, expandWidth):
+        self.eh, self.ew = expandHeight, expandWidth
+
+    def transformMat(self, f):
+        from .roi import BoundingBox
+
+        m = f.opencvMat()
+        h, w = m.shape[:2]
+        assert w <= self.ew and h <= self.eh, f"image {h}x{w} larger than the {self.eh}x{self.ew} canvas"
+        top, left = (self.eh - h) // 2, (self.ew - w) // 2
+        out = torch.zeros((self.eh, self.ew) + tuple(m.shape[2:]), dtype=m.dtype, device=m.device)
+        out[top:top + h, left:left + w] = m
+        f[ImageFeature.mat] = out
+        f[ImageFeature.boundingBox] = BoundingBox(float(left), float(top), float(left + w), float(top + h))
+
+
+class PixelNormalize(PixelNormalizer):
+    """Reference name (P/transform/vision/image.py PixelNormalize) of PixelNormalizer: data(i) - mean(i)."""
+
+
+class Pipeline(FeatureTransformer):
+    """A list of FeatureTransformers applied in order (reference image.py Pipeline)."""
+
+    def __init__(self, transformers):
+        assert all(isinstance(t, FeatureTransformer) for t in transformers), "Pipeline takes FeatureTransformers"
+        self.transformers = list(transformers)
+
+    def transform(self, f):
+        for t in self.transformers:
+            f = t.transform(f)
+        return f
 
 
 class Expand(FeatureTransformer):

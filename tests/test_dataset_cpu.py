@@ -145,3 +145,40 @@ def test_row_transformer_atomic_and_numeric():
     assert t[1]["name"] == ["b"] and t[1]["xy"].tolist() == [3.0, 4.0] and t[0]["z"].tolist() == [0.5]
     allnum = list(RowTransformer.numeric().apply(iter([{"a": 1, "b": 2.5, "c": "s"}])))
     assert allnum[0]["all"].tolist() == [1.0, 2.5]
+
+
+def test_reference_named_vision_transforms(tmp_path):
+    """FixExpand (Expand.scala:102), RandomAspectScale / AspectScale sizing (Resize.scala:117-160), Pipeline,
+    PixelNormalize, the ROI transforms and SeqFileFolder.files_to_image_frame under the reference's names."""
+    import os
+
+    import torch
+
+    import bigdl_amd.transform.vision.image as V
+    from bigdl_amd.dataset.seqfile import generate_seq_files
+    from bigdl_amd.examples.seqfile_generator import _synthetic_imagenet
+    from bigdl_amd.transform.vision.image.augmentation import aspect_scale_hw
+    from bigdl_amd.transform.vision.image.feature import ImageFeature
+
+    f = ImageFeature()
+    f[ImageFeature.mat] = torch.ones(10, 20, 3)
+    V.FixExpand(30, 40).transform(f)
+    m, bb = f[ImageFeature.mat], f[ImageFeature.boundingBox]
+    assert m.shape == (30, 40, 3) and float(m.sum()) == 600.0 and float(m[10:20, 10:30].sum()) == 600.0
+    assert (bb.x1, bb.y1, bb.x2, bb.y2) == (10.0, 10.0, 30.0, 20.0)
+    assert aspect_scale_hw(375, 500, 600, 1000) == (600, 800)
+    assert aspect_scale_hw(375, 500, 600, 1000, 32) == (576, 800)
+    assert aspect_scale_hw(300, 2000, 600, 1000) == (150, 1000)
+    g = ImageFeature()
+    g[ImageFeature.mat] = torch.rand(375, 500, 3) * 255
+    V.Pipeline([V.RandomAspectScale([600], 32, 1000), V.HFlip()]).transform(g)
+    assert tuple(g[ImageFeature.mat].shape) == (576, 800, 3)
+    p = ImageFeature()
+    p[ImageFeature.mat] = torch.full((2, 2, 3), 5.0)
+    V.PixelNormalize(torch.ones(12).tolist()).transform(p)
+    assert float(p[ImageFeature.mat].sum()) == 48.0
+    _synthetic_imagenet(str(tmp_path / "train"))
+    generate_seq_files(str(tmp_path / "train"), str(tmp_path / "seq"), blockSize=5)
+    frame = V.SeqFileFolder.files_to_image_frame(str(tmp_path / "seq"), 2)
+    assert len(frame.array) == 8 and all(float(x[ImageFeature.label][0]) <= 2 for x in frame.array)
+    assert all(hasattr(V, n) for n in ("RoiHFlip", "RoiNormalize", "RoiProject", "RoiResize", "RandomSampler"))
