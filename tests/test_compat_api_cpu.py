@@ -146,3 +146,32 @@ def test_snake_case_keywords_map_to_engine_arguments(bigdl):
     sgd = SGD(learningrate=0.1, momentum=0.9, leaningrate_schedule=sched)
     assert sgd.value.momentum == 0.9 and sgd.value.learningRateSchedule is sched.value
     assert Plateau("score").value is not None
+
+
+def test_initialization_method_and_dataset_base_modules(tmp_path, capsys):
+    import torch
+
+    from bigdl_amd.compat.dataset.base import Progbar, display_table, maybe_download
+    from bigdl_amd.compat.nn import initialization_method as im
+
+    w = torch.empty(100, 50)
+    im.RandomUniform(0.5, -0.5).init(w)           # reference order: (upper, lower)
+    assert float(w.min()) >= -0.5 and float(w.max()) <= 0.5 and float(w.max()) > 0.4
+    im.ConstInitMethod(3.0).init(w)
+    assert float(w.mean()) == 3.0
+    for cls in (im.Zeros, im.Ones, im.Xavier, im.MsraFiller, im.BilinearFiller):
+        assert isinstance(cls(), im.InitializationMethod)
+    assert isinstance(im.RandomNormal(0.0, 1.0), im.InitializationMethod)
+    p = Progbar(10)
+    p.update(5, [("loss", 1.0)])
+    p.add(5, [("loss", 3.0)])
+    display_table([["a", "b"]], [5, 10])
+    out = capsys.readouterr().out
+    assert "10/10" in out and "loss: 2.0000" in out and out.rstrip().endswith("b")
+    (tmp_path / "f.bin").write_bytes(b"x")
+    assert maybe_download("f.bin", str(tmp_path)) == str(tmp_path / "f.bin")
+    try:
+        maybe_download("missing.bin", str(tmp_path), "http://example")
+        raise AssertionError("expected FileNotFoundError")
+    except FileNotFoundError:
+        pass
