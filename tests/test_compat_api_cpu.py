@@ -175,3 +175,26 @@ def test_initialization_method_and_dataset_base_modules(tmp_path, capsys):
         raise AssertionError("expected FileNotFoundError")
     except FileNotFoundError:
         pass
+
+
+def test_reference_dataset_helper_modules(tmp_path):
+    import numpy as np
+
+    from bigdl_amd.compat.dataset import movielens, news20, sentence
+
+    root = tmp_path / "20news-18828"
+    for i, grp in enumerate(["alt.atheism", "comp.graphics"]):
+        (root / grp).mkdir(parents=True)
+        (root / grp / "101").write_text(f"text {i}", encoding="latin-1")
+        (root / grp / "notes.txt").write_text("skip")
+    texts = news20.get_news20(str(tmp_path))
+    assert texts == [("text 0", 1), ("text 1", 2)]
+    (tmp_path / "glove.6B").mkdir()
+    (tmp_path / "glove.6B" / "glove.6B.2d.txt").write_text("the 0.5 -1\ncat 1 2\n")
+    assert news20.get_glove_w2v(str(tmp_path), 2)["cat"] == [1.0, 2.0]
+    (tmp_path / "ml-1m").mkdir()
+    (tmp_path / "ml-1m" / "ratings.dat").write_text("1::10::5::999\n2::20::3::998\n")
+    assert np.array_equal(movielens.get_id_ratings(str(tmp_path)), np.array([[1, 10, 5], [2, 20, 3]]))
+    assert sentence.sentences_split("Hello there. How are you?") == ["Hello there.", "How are you?"]
+    assert sentence.sentence_tokenizer("Hi, you.") == ["Hi", ",", "you", "."]
+    assert sentence.sentences_bipadding("a b") == "SENTENCESTART a b SENTENCEEND"
