@@ -298,9 +298,14 @@ def _pads2(at, k):
 
 
 def load_onnx(path):
-    """ONNX file -> bigdl_amd Graph (reference onnx_loader.load_model_proto)."""
+    """ONNX file -> bigdl_amd Graph (reference onnx_loader.load)."""
     with open(path, "rb") as f:
-        model = SCHEMA.decode("ModelProto", f.read())
+        return load_onnx_bytes(f.read())
+
+
+def load_onnx_bytes(data):
+    """Serialized ModelProto bytes -> bigdl_amd Graph (reference onnx_loader.load_model_proto)."""
+    model = SCHEMA.decode("ModelProto", bytes(data))
     opset = max([int(_first(o, "version", 13)) for o in model.get("opset_import", [])] or [13])
     g = model["graph"][0]
     inits = {_first(t, "name"): tensor_of(t) for t in g.get("initializer", [])}
@@ -552,4 +557,4 @@ def save_onnx(model, input_shape, path, input_name="input", opset=11):
     return out
 
 
-__all__ = ["load_onnx", "save_onnx", "OnnxOp", "SCHEMA"]
+__all__ = ["load_onnx", "load_onnx_bytes", "save_onnx", "OnnxOp", "SCHEMA"]

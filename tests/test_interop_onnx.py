@@ -71,3 +71,22 @@ def test_reference_op_set(tmp_path):
     r = torch.relu(x @ w.t())
     assert torch.allclose(out[1], torch.cat([r, r], 1), atol=1e-5)
     assert torch.allclose(out[2], torch.softmax(3 * r, 1), atol=1e-5)
+
+
+def test_reference_contrib_onnx_loader(tmp_path):
+    """bigdl.contrib.onnx.load / load_model_proto / calc_output_shape under the reference names."""
+    import torch
+
+    from bigdl_amd import nn
+    from bigdl_amd.compat.contrib import onnx as conx
+    from bigdl_amd.interop.onnx import save_onnx
+
+    m = nn.Sequential().add(nn.SpatialConvolution(3, 4, 3, 3, 1, 1, 1, 1)).add(nn.ReLU())
+    p = str(tmp_path / "m.onnx")
+    save_onnx(m, [1, 3, 8, 8], p)
+    x = torch.randn(1, 3, 8, 8)
+    a = conx.load(p).value.forward(x)
+    with open(p, "rb") as f:
+        b = conx.load_model_proto(f.read()).value.forward(x)
+    assert torch.allclose(a, m.forward(x), atol=1e-5) and torch.allclose(b, a)
+    assert conx.calc_output_shape(224, 3, 1, 2) == 112 and conx.calc_output_shape(7, 2, 0, 2, ceil_mode=True) == 4
