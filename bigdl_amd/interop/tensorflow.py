@@ -588,7 +588,39 @@ def save_tf(model, inputs, path, byteOrder=None, dataFormat="NHWC"):
     return out
 
 
-__all__ = ["load_tf", "save_tf", "read_graph", "parse_graph", "attrs_of", "tensor_of", "SCHEMA", "TensorflowLoader",
+def freeze_graph_with_variables(graph_file, values, output_node_names, output_graph):
+    """Replace every variable node (VariableV2 / Variable / VarHandleOp) named in ``values`` by a Const holding that
+    value, drop the nodes the outputs do not depend on (Assign / initialisers / savers) and write a binary GraphDef:
+    the freezing step of the reference tf_utils.merge_checkpoint, without TensorFlow."""
+    nodes = read_graph(graph_file)
+    by_name = {_first(n, "name"): n for n in nodes}
+    keep, stack = set(), [o.split(":")[0] for o in output_node_names]
+    while stack:
+        nm = stack.pop()
+        if nm in keep or nm not in by_name:
+            continue
+        keep.add(nm)
+        if _first(by_name[nm], "op") in ("VariableV2", "Variable", "VarHandleOp") and nm in values:
+            continue
+        for i in by_name[nm].get("input", []):
+            stack.append(i.lstrip("^").split(":")[0])
+    out = []
+    for n in nodes:
+        nm = _first(n, "name")
+        if nm not in keep:
+            continue
+        if _first(n, "op") in ("VariableV2", "Variable", "VarHandleOp") and nm in values:
+            t = torch.as_tensor(values[nm])
+            tp = _tensor_proto(t)
+            n = {"name": [nm], "op": ["Const"], "attr": [_attr("dtype", type=[tp["dtype"][0]]),
+                                                          _attr("value", tensor=[tp])]}
+        out.append(n)
+    with open(output_graph, "wb") as f:
+        f.write(SCHEMA.encode("GraphDef", {"node": out, "versions": [{"producer": [21]}]}))
+    return output_graph
+
+
+__all__ = ["load_tf", "save_tf", "read_graph", "freeze_graph_with_variables", "parse_graph", "attrs_of", "tensor_of", "SCHEMA", "TensorflowLoader",
            "TensorflowSaver", "TensorflowToBigDL", "BigDLToTensorflow"]
 
 

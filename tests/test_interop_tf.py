@@ -120,3 +120,40 @@ def test_tf_ops_semantics():
     assert run_op("ConcatV2", [x, x, torch.tensor(-1)], {}).shape == (2, 3, 8)
     parts = run_op("Split", [torch.tensor(1), x], {"num_split": 3})
     assert len(parts) == 3 and parts[0].shape == (2, 1, 4)
+
+
+def test_reference_tf_utils_save_variables_and_merge_checkpoint(tmp_path):
+    """bigdl.util.tf_utils: save_variable_bigdl + merge_checkpoint freeze a graph's variables into Consts (no
+    TensorFlow needed), and the frozen graph loads and computes x @ w."""
+    import numpy as np
+    import torch
+
+    from bigdl_amd.compat.util import tf_utils
+    from bigdl_amd.interop.tensorflow import SCHEMA, _attr
+    from bigdl_amd.nn.module import Module
+
+    f32 = {"type": ["DT_FLOAT"]}
+    nodes = [
+        {"name": ["x"], "op": ["Placeholder"], "attr": [_attr("dtype", **f32)]},
+        {"name": ["w"], "op": ["VariableV2"], "attr": [_attr("dtype", **f32)]},
+        {"name": ["w/read"], "op": ["Identity"], "input": ["w"], "attr": [_attr("T", **f32)]},
+        {"name": ["w/init"], "op": ["Const"], "attr": [_attr("dtype", **f32)]},
+        {"name": ["w/Assign"], "op": ["Assign"], "input": ["w", "w/init"], "attr": [_attr("T", **f32)]},
+        {"name": ["y"], "op": ["MatMul"], "input": ["x", "w/read"], "attr": [_attr("T", **f32)]},
+    ]
+    g = str(tmp_path / "g.pb")
+    with open(g, "wb") as fh:
+        fh.write(SCHEMA.encode("GraphDef", {"node": nodes}))
+    w = np.arange(6, dtype=np.float32).reshape(3, 2)
+    ck = str(tmp_path / "vars.bin")
+    tf_utils.save_variable_bigdl({"w": w}, ck)
+    out = str(tmp_path / "frozen.pb")
+    tf_utils.merge_checkpoint(g, ck, ["y"], out)
+    m = Module.loadTF(out, ["x"], ["y"])
+    x = torch.randn(4, 3)
+    assert torch.allclose(m.forward(x), x @ torch.from_numpy(w), atol=1e-5)
+    try:
+        tf_utils.export_checkpoint("ckpt")
+        raise AssertionError("expected ImportError")
+    except ImportError:
+        pass
