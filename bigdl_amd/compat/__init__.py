@@ -23,6 +23,21 @@ _MODULES = {
     "bigdl.dataset": "bigdl_amd.compat.dataset",
     "bigdl.dataset.transformer": "bigdl_amd.compat.dataset.transformer",
     "bigdl.dataset.mnist": "bigdl_amd.compat.dataset.mnist",
+    "bigdl.dataset.base": "bigdl_amd.compat.dataset.base",
+    "bigdl.dataset.news20": "bigdl_amd.compat.dataset.news20",
+    "bigdl.dataset.movielens": "bigdl_amd.compat.dataset.movielens",
+    "bigdl.dataset.sentence": "bigdl_amd.compat.dataset.sentence",
+    "bigdl.nn.onnx": "bigdl_amd.compat.nn.onnx",
+    "bigdl.nn.onnx.layer": "bigdl_amd.compat.nn.onnx.layer",
+    "bigdl.nn.initialization_method": "bigdl_amd.compat.nn.initialization_method",
+    "bigdl.util.tf_utils": "bigdl_amd.compat.util.tf_utils",
+    "bigdl.util.engine": "bigdl_amd.compat.util.engine",
+    "bigdl.version": "bigdl_amd.compat.version",
+    "bigdl.contrib": "bigdl_amd.compat.contrib",
+    "bigdl.contrib.onnx": "bigdl_amd.compat.contrib.onnx",
+    "bigdl.models": "bigdl_amd.compat.models",
+    "bigdl.models.utils": "bigdl_amd.compat.models.utils",
+    "bigdl.models.utils.model_broadcast": "bigdl_amd.compat.models.utils.model_broadcast",
 }
 
 

@@ -31,7 +31,7 @@ def module_key(cls):
         return "keras." + cls.__name__
     if mod == "bigdl_amd.nn.tf_ops":
         return "ops." + cls.__name__
-    if mod in ("bigdl_amd.nn.ops", "bigdl_amd.nn.tf"):
+    if mod in ("bigdl_amd.nn.ops", "bigdl_amd.nn.tf", "bigdl_amd.nn.onnx"):
         return mod[len("bigdl_amd."):] + "." + cls.__name__
     return cls.__name__
 

@@ -198,3 +198,75 @@ def test_reference_dataset_helper_modules(tmp_path):
     assert sentence.sentences_split("Hello there. How are you?") == ["Hello there.", "How are you?"]
     assert sentence.sentence_tokenizer("Hi, you.") == ["Hi", ",", "you", "."]
     assert sentence.sentences_bipadding("a b") == "SENTENCESTART a b SENTENCEEND"
+
+
+def test_reference_engine_version_and_model_broadcast(tmp_path, monkeypatch):
+    """bigdl.util.engine version helpers / prepare_env, bigdl.version, and bigdl.models.utils.model_broadcast:
+    a broadcast handle pickles to its saved path and loads an independent copy with the same outputs."""
+    import pickle
+    import sys
+
+    import numpy as np
+
+    from bigdl_amd import compat
+
+    compat.install()
+    from bigdl.models.utils.model_broadcast import broadcast_model
+    from bigdl.nn.layer import Linear, Sequential, ReLU
+    from bigdl.util.common import SparkContext
+    from bigdl.util.engine import compare_version, get_bigdl_classpath, is_spark_below_2_2, prepare_env
+    from bigdl.version import __version__
+
+    assert compare_version("2.10", "2.2") == 1 and compare_version("1.6", "2.2") == -1
+    assert compare_version("2.2.0", "2.2") == 0 and __version__.startswith("0.")
+    assert is_spark_below_2_2() is False and get_bigdl_classpath() == ""
+    monkeypatch.setenv("BIGDL_PACKAGES", str(tmp_path))
+    monkeypatch.setattr(sys, "path", list(sys.path))
+    prepare_env()
+    assert sys.path[0] == str(tmp_path)
+
+    model = Sequential().add(Linear(4, 3)).add(ReLU())
+    bc = broadcast_model(SparkContext(), model)
+    assert bc.value is model
+    remote = pickle.loads(pickle.dumps(bc))            # what a task would receive
+    x = np.random.RandomState(0).randn(2, 4).astype(np.float32)
+    got = remote.value
+    assert got is not model
+    np.testing.assert_allclose(got.forward(x), model.forward(x), rtol=1e-6, atol=1e-6)
+    bc.unpersist()
+
+
+def test_reference_onnx_layers():
+    """bigdl.nn.onnx.layer (P/nn/onnx/layer.py) over nn.onnx Shape / Reshape (S/nn/onnx/*.scala), nn.Gemm,
+    tf Const and Gather: ONNX semantics (0 copies a size, shape from a Table input, float sizes)."""
+    import numpy as np
+    import torch
+
+    from bigdl_amd import compat
+    from bigdl_amd.nn import onnx as nn_onnx
+    from bigdl_amd.utils.table import T
+
+    compat.install()
+    from bigdl.nn.onnx.layer import Constant, Gather, Gemm, Reshape, Shape
+
+    x = np.random.RandomState(0).rand(2, 3, 4).astype(np.float32)
+    assert Shape().forward(x).tolist() == [2.0, 3.0, 4.0]
+    assert Reshape([0, -1]).forward(x).shape == (2, 12)
+    np.testing.assert_array_equal(Constant(np.ones((2, 2))).forward(x), np.ones((2, 2)))
+    b, c = np.random.RandomState(1).rand(5, 4), np.random.RandomState(2).rand(3, 5)
+    a = np.random.RandomState(3).rand(3, 4).astype(np.float32)
+    np.testing.assert_allclose(Gemm(b, c, 0.5, 2.0, 0, 1).forward(a), 0.5 * a @ b.T + 2.0 * c, rtol=1e-5)
+    got = Gather().forward([np.arange(12, dtype=np.float32).reshape(4, 3), np.array([2, 0], dtype=np.int32)])
+    np.testing.assert_array_equal(got, [[6, 7, 8], [0, 1, 2]])
+
+    r = nn_onnx.Reshape()
+    data = torch.arange(24.0).reshape(2, 3, 4)
+    y = r.forward(T(data, torch.tensor([4.0, 6.0])))
+    assert y.shape == (4, 6) and r.shape == [4, 6]
+    gi = r.backward(T(data, torch.tensor([4.0, 6.0])), torch.ones(4, 6))
+    assert gi[1].shape == (2, 3, 4)
+    try:
+        nn_onnx.Reshape().forward(data)
+        raise AssertionError("expected ValueError")
+    except ValueError:
+        pass

@@ -51,11 +51,15 @@ def _case(name):
         return nn.SpatialSubtractiveNormalization(3, torch.ones(5, 5)), (2, 3, 9, 9)
     if name == "wclrn":
         return nn.SpatialWithinChannelLRN(5, 1.0, 0.75), (2, 3, 8, 8)
+    if name == "gemm":
+        g = torch.Generator().manual_seed(3)
+        return nn.Gemm(0.5, 2.0, False, True, matrixB=torch.randn(10, 24, generator=g),
+                       matrixC=torch.randn(6, 10, generator=g)), (6, 24)
     raise KeyError(name)
 
 
 ALL = ["full", "full_nopad", "temporal", "map", "separable", "volumetric", "grouped", "depthwise", "grouped_wide",
-       "full3d", "convlstm", "maxout", "highway", "cosine", "subnorm", "wclrn"]
+       "full3d", "convlstm", "maxout", "highway", "cosine", "subnorm", "wclrn", "gemm"]
 
 
 @pytest.mark.parametrize("name", ALL)
@@ -91,7 +95,7 @@ def test_conv_family_uses_no_vendor_conv(monkeypatch):
 
     RNG.setSeed(1)
     for name in ("full", "temporal", "map", "volumetric", "separable", "grouped", "depthwise", "full3d", "convlstm",
-                 "maxout", "highway", "cosine", "subnorm", "wclrn"):
+                 "maxout", "highway", "cosine", "subnorm", "wclrn", "gemm"):
         m, shape = _case(name)
         m = m.to("cuda")
         y = m.forward(torch.randn(*shape, device="cuda"))
