@@ -27,6 +27,12 @@ _MODULES = {
     "bigdl.dataset.news20": "bigdl_amd.compat.dataset.news20",
     "bigdl.dataset.movielens": "bigdl_amd.compat.dataset.movielens",
     "bigdl.dataset.sentence": "bigdl_amd.compat.dataset.sentence",
+    "bigdl.transform": "bigdl_amd.compat.transform",
+    "bigdl.transform.vision": "bigdl_amd.compat.transform.vision",
+    "bigdl.transform.vision.image": "bigdl_amd.compat.transform.vision.image",
+    "bigdl.nn.keras": "bigdl_amd.compat.nn.keras",
+    "bigdl.nn.keras.layer": "bigdl_amd.compat.nn.keras.layer",
+    "bigdl.nn.keras.topology": "bigdl_amd.compat.nn.keras.topology",
     "bigdl.nn.onnx": "bigdl_amd.compat.nn.onnx",
     "bigdl.nn.onnx.layer": "bigdl_amd.compat.nn.onnx.layer",
     "bigdl.nn.initialization_method": "bigdl_amd.compat.nn.initialization_method",

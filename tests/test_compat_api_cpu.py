@@ -270,3 +270,59 @@ def test_reference_onnx_layers():
         raise AssertionError("expected ValueError")
     except ValueError:
         pass
+
+
+def test_reference_keras_layer_and_topology():
+    """bigdl.nn.keras.layer / topology (P/nn/keras/*.py): snake_case keywords (input_dim, W_regularizer,
+    batch_size, nb_epoch) over the engine's keras layers; Sequential and functional Model train / predict."""
+    import numpy as np
+
+    from bigdl_amd import compat
+
+    compat.install()
+    from bigdl.nn.keras.layer import Activation, Dense
+    from bigdl.nn.keras.topology import Input, Model, Sequential
+
+    rs = np.random.RandomState(0)
+    x = rs.rand(64, 4).astype(np.float32)
+    y = np.eye(3)[rs.randint(0, 3, 64)].astype(np.float32)
+    m = Sequential().add(Dense(8, input_dim=4, activation="relu", W_regularizer=None)).add(Dense(3)) \
+        .add(Activation("softmax"))
+    m.compile("sgd", "categorical_crossentropy")
+    m.fit(x, y, batch_size=16, nb_epoch=2)
+    p = m.predict(x)
+    assert p.shape == (64, 3) and np.allclose(p.sum(1), 1.0, atol=1e-5)
+    assert m.get_output_shape()[-1] == 3
+
+    inp = Input(shape=(4,))
+    out = Dense(2)(inp)
+    fm = Model(inp, out)
+    assert fm.predict(x).shape == (64, 2)
+
+
+def test_reference_vision_image_facade():
+    """bigdl.transform.vision.image (P/transform/vision/image.py): snake_case transformer constructors over the
+    engine transformers, LocalImageFrame from ndarrays, get_image (CHW) / get_label, same values as the engine."""
+    import numpy as np
+    import torch
+
+    from bigdl_amd import compat
+    from bigdl_amd.transform.vision import image as eng
+
+    compat.install()
+    from bigdl.transform.vision.image import ChannelNormalize, LocalImageFrame, MatToTensor, Resize
+
+    rs = np.random.RandomState(0)
+    imgs = [(rs.rand(20, 30, 3) * 255).astype(np.float32) for _ in range(2)]
+    frame = LocalImageFrame(imgs, [np.array([1.0]), np.array([2.0])])
+    for t in (Resize(resize_h=10, resize_w=12), ChannelNormalize(100.0, 110.0, 120.0), MatToTensor(to_rgb=False)):
+        frame = frame.transform(t)
+    got = frame.get_image()
+    assert frame.is_local() and [g.shape for g in got] == [(3, 10, 12)] * 2
+    assert [l.tolist() for l in frame.get_label()] == [[1.0], [2.0]]
+    f = eng.ImageFeature()
+    f[eng.ImageFeature.mat] = torch.as_tensor(imgs[0])
+    f[eng.ImageFeature.originalSize] = imgs[0].shape
+    for t in (eng.Resize(10, 12), eng.ChannelNormalize(100.0, 110.0, 120.0), eng.MatToTensor(toRGB=False)):
+        f = t.transform(f)
+    np.testing.assert_allclose(got[0], f[eng.ImageFeature.imageTensor].numpy(), rtol=1e-6, atol=1e-5)
