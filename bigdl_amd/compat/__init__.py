@@ -27,6 +27,10 @@ _MODULES = {
     "bigdl.dataset.news20": "bigdl_amd.compat.dataset.news20",
     "bigdl.dataset.movielens": "bigdl_amd.compat.dataset.movielens",
     "bigdl.dataset.sentence": "bigdl_amd.compat.dataset.sentence",
+    "bigdl.dlframes": "bigdl_amd.compat.dlframes",
+    "bigdl.dlframes.dl_classifier": "bigdl_amd.compat.dlframes.dl_classifier",
+    "bigdl.dlframes.dl_image_reader": "bigdl_amd.compat.dlframes.dl_image_reader",
+    "bigdl.dlframes.dl_image_transformer": "bigdl_amd.compat.dlframes.dl_image_transformer",
     "bigdl.transform": "bigdl_amd.compat.transform",
     "bigdl.transform.vision": "bigdl_amd.compat.transform.vision",
     "bigdl.transform.vision.image": "bigdl_amd.compat.transform.vision.image",

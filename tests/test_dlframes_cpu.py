@@ -54,3 +54,19 @@ def test_image_reader_and_transformer(tmp_path):
     assert t.shape == (3, 4, 5)
     bgr = arr[..., ::-1].astype(np.float32)
     assert np.allclose(t[0], bgr[..., 0] - 30.0) or np.allclose(t[0], bgr[..., 0] - 10.0)
+
+
+def test_reference_dlframes_facade_takes_layer_handles():
+    """bigdl.dlframes.dl_classifier (P/dlframes/dl_classifier.py) with the facade's Layer / Criterion handles."""
+    from bigdl_amd import compat
+
+    compat.install()
+    from bigdl.dlframes.dl_classifier import DLClassifier as RefDLClassifier
+    from bigdl.nn.criterion import ClassNLLCriterion
+    from bigdl.nn.layer import Linear, LogSoftMax, ReLU, Sequential
+
+    RNG.setSeed(1)
+    model = Sequential().add(Linear(4, 8)).add(ReLU()).add(Linear(8, 2)).add(LogSoftMax())
+    est = RefDLClassifier(model, ClassNLLCriterion(), [4]).setBatchSize(20).setMaxEpoch(10).setLearningRate(0.1)
+    out = est.fit(_blobs()).transform(_blobs(100, seed=1))
+    assert (out["prediction"] == out["label"]).mean() > 0.95
