@@ -87,8 +87,55 @@ class _RecordInit(type):
 
     def __init__(cls, name, bases, ns):
         super().__init__(name, bases, ns)
+        if getattr(cls, "_SYNC_HOOKS", False):
+            for kind in ("forward", "backward"):
+                if kind in ns:
+                    setattr(cls, kind, _sync_wrap(kind, ns[kind]))
         if not name.startswith("_"):
             _REGISTRY[module_key(cls)] = cls
+
+
+def _sync_wrap(kind, f):
+    """Per-module synchroniser hooks (reference AbstractModule.scala:282-297 / 1184-1199): every module class's
+    own ``forward`` / ``backward`` — including overrides in containers, Graph, BN, recurrent layers — calls
+    ``self._sync.before_forward(self)`` before its forward and ``self._sync.after_backward(self)`` after its
+    backward when a synchroniser is installed (ParallelOptimizer, parallel/bucketed.py). A depth counter makes an
+    override that calls ``super().forward/backward`` fire once."""
+    if getattr(f, "_sync_wrapped", False):
+        return f
+    key = "_sync_fd" if kind == "forward" else "_sync_bd"
+
+    if kind == "forward":
+        def wrapped(self, *args, **kw):
+            s = self.__dict__.get("_sync")
+            if s is None:
+                return f(self, *args, **kw)
+            d = self.__dict__.get(key, 0)
+            self.__dict__[key] = d + 1
+            try:
+                if d == 0:
+                    s.before_forward(self)
+                return f(self, *args, **kw)
+            finally:
+                self.__dict__[key] = d
+    else:
+        def wrapped(self, *args, **kw):
+            s = self.__dict__.get("_sync")
+            if s is None:
+                return f(self, *args, **kw)
+            d = self.__dict__.get(key, 0)
+            self.__dict__[key] = d + 1
+            try:
+                out = f(self, *args, **kw)
+            finally:
+                self.__dict__[key] = d
+            if d == 0:
+                s.after_backward(self)
+            return out
+    wrapped.__name__, wrapped.__qualname__, wrapped.__doc__ = f.__name__, f.__qualname__, f.__doc__
+    wrapped.__wrapped__ = f
+    wrapped._sync_wrapped = True
+    return wrapped
 
 
 def to_device_tensor(t, device):
@@ -178,6 +225,8 @@ class MklInt8Convertible:
 class AbstractModule(MklInt8Convertible, metaclass=_RecordInit):
     """Base of every layer and container."""
 
+    _SYNC_HOOKS = True
+
     def __init__(self):
         self.output = None
         self.gradInput = None
@@ -229,8 +278,6 @@ class AbstractModule(MklInt8Convertible, metaclass=_RecordInit):
         t0 = time.perf_counter_ns()
         if getattr(input, "_is_bigdl_tensor", False):     # bigdl_amd.tensor.Tensor -> its torch tensor
             input = input._t
-        if self._sync is not None:
-            self._sync.before_forward(self)
         try:
             self.output = self.updateOutput(input)
         except Exception as e:  # reference wraps errors with the module path (AbstractModule.scala:260-266)
@@ -255,8 +302,6 @@ class AbstractModule(MklInt8Convertible, metaclass=_RecordInit):
             self.accGradParameters(input, gradOutput)
             self._apply_regularizers()
         self.backward_time += time.perf_counter_ns() - t0
-        if self._sync is not None:
-            self._sync.after_backward(self)
         return self.gradInput
 
     def __call__(self, *nodes):
@@ -563,8 +608,8 @@ class AbstractModule(MklInt8Convertible, metaclass=_RecordInit):
         new = cls.__new__(cls)
         memo[id(self)] = new
         for k, v in self.__dict__.items():
-            if k in ("output", "gradInput", "_flat", "_flat_views", "_w16", "_sync"):
-                setattr(new, k, None if k != "_w16" else {})
+            if k in ("output", "gradInput", "_flat", "_flat_views", "_w16", "_sync", "_sync_fd", "_sync_bd"):
+                setattr(new, k, {} if k == "_w16" else (0 if k in ("_sync_fd", "_sync_bd") else None))
             elif isinstance(v, torch.Tensor):
                 setattr(new, k, v.detach().clone(memory_format=torch.preserve_format))
             else:   # cached autograd activations (non-leaf tensors) are copied as plain data

@@ -167,8 +167,6 @@ class BatchNormalization(TensorModule):
             if not self._frozen:
                 self.accGradParameters(input, gradOutput)
         self.backward_time += time.perf_counter_ns() - t0
-        if self._sync is not None:
-            self._sync.after_backward(self)
         return self.gradInput
 
     def _cpu_grads(self, gradOutput):

@@ -12,6 +12,7 @@ in one small collective at logging / validation points instead of per-iteration 
 """
 import logging
 import math
+import copy
 import os
 import time
 
@@ -179,9 +180,12 @@ class Optimizer:
         return next(iter(self.optimMethods.values()))
 
     def _make_step(self, comm=None):
+        # gradient bucket size for the bucketed overlap (reference property bigdl.parallelOptimizer.parameterBlocks
+        # counts blocks; buckets here are sized in elements: 8M fp32 = 32 MB runs the xGMI links near their rate)
+        bucket = int(Engine.getProperty("bigdl.parallelOptimizer.bucketElems", 8 << 20) or (8 << 20))
         return TrainStep(self.model, self.criterion, dict(self.optimMethods), device=self.device, comm=comm,
                          compress=self.compress, overlap=self._overlap, processors=self._processors(),
-                         expand_methods=self._expand, priorities=self._priorities)
+                         expand_methods=self._expand, priorities=self._priorities, bucket_elems=bucket)
 
     def _processors(self):
         """Clipping as ParameterProcessors (reference ParameterOperations.scala), constant clipping first."""
@@ -229,6 +233,7 @@ class Optimizer:
                 if self._restore_latest():
                     for om in self.optimMethods.values():   # reference :946 newOptimMethod.clearHistory()
                         om.clearHistory()
+                    self._resume_state = None
 
     @staticmethod
     def _latest(path, prefix):
@@ -260,6 +265,16 @@ class Optimizer:
             f = self._latest(self.checkpointPath, f"optimMethod-{name}")
             nm = OptimMethod.load(os.path.join(self.checkpointPath, f)) if f else om
             methods[key] = nm
+        # the checkpoint holds each method's FULL per-element state (gather_optim_state); the TrainStep built next
+        # slices it into this rank's pieces on its device (load_optim_state), so the method objects it owns start
+        # without per-element tensors
+        full = {}
+        for key, nm in methods.items():
+            full[key] = copy.deepcopy(nm)
+            for k in list(nm.state.keys()):
+                if torch.is_tensor(nm.state[k]) and nm.state[k].dim() >= 1:
+                    del nm.state[k]
+        self._resume_state = full
         self.optimMethods = methods
         first = next(iter(methods.values()))
         for k in ("epoch", "neval"):
@@ -286,9 +301,13 @@ class Optimizer:
         self._sync_states(st)
         if self._step is None:
             self._step = self._make_step()
+            if getattr(self, "_resume_state", None):
+                self._step.load_optim_state(self._resume_state)
+                self._resume_state = None
         step = self._step
         world = step.comm.world
         drop = _StragglerDrop(self, world) if self.dropPercentage > 0 else None
+        step.defer_sync = drop is not None
         it = iter(self.dataset.data(train=True))
         wall0 = time.perf_counter()
         pending = []  # (iteration, loss tensor, records)

@@ -128,9 +128,13 @@ def parameter_splits(model, methods, fw, total, expand=False):
 
         walk(model, methods.get(model.getName()))
         out.sort(key=lambda t: t[1])
+        # LarsSGD is not element-wise (one trust ratio per split): every leaf keeps its own split, as the
+        # reference's per-layer clones do
+        from .methods import LarsSGD
+
         merged = []
         for s in out:
-            if merged and merged[-1][3] is s[3] and merged[-1][2] == s[1]:
+            if merged and merged[-1][3] is s[3] and merged[-1][2] == s[1] and not isinstance(s[3], LarsSGD):
                 merged[-1] = (merged[-1][0], merged[-1][1], s[2], s[3])
             else:
                 merged.append(s)
@@ -253,10 +257,8 @@ class TrainStep:
             self.processors.append(LarsProcessor(lars[0][3].weightDecay))
         self.loss = None
         # ParallelOptimizer-style bucketed reduce-scatter overlapped with backward (parallel/bucketed.py)
-        from ..nn.containers import Sequential
-
         if overlap is None:
-            overlap = self.comm.active and isinstance(model, Sequential)
+            overlap = self.comm.active
         self.bucketed = None
         if overlap and self.comm.active:
             from ..parallel.bucketed import BucketedGradSync
@@ -275,10 +277,12 @@ class TrainStep:
     def forward_backward(self, x, y):
         m, c = self.model, self.criterion
         m.training()
-        if self.bucketed is not None:
-            out = self.bucketed.forward(x)
-        else:
-            out = m.forward(x)
+        bk = self.bucketed
+        if bk is not None:
+            bk.begin_step()
+        out = m.forward(x)
+        if bk is not None:
+            bk.end_forward()
         loss = c.forward(out, y)
         gout = c.backward(out, y)
         convs = self._dgrad_convs()
@@ -287,10 +291,9 @@ class TrainStep:
 
             cv.prepare_dgrad_weights(convs)       # every conv weight transposed for its dgrad in one launch
         try:
-            if self.bucketed is not None:
-                self.bucketed.backward(x, gout)
-            else:
-                m.backward(x, gout)
+            if bk is not None:
+                bk.begin_backward()
+            m.backward(x, gout)
         finally:
             if convs:
                 cv.end_dgrad_weights()
@@ -347,6 +350,9 @@ class TrainStep:
         return True
 
     min_finished = 0.0
+    # straggler drop: no collective may start inside backward (a late rank skips it), so the bucketed hooks only
+    # record and ``_sync_and_update_weighted`` reduces once every rank has voted
+    defer_sync = False
 
     def _sync_and_update_weighted(self, loss, finished):
         self.flush()
@@ -355,13 +361,30 @@ class TrainStep:
         n = float(cnt.item())
         if not finished:
             self.g.zero_()
-        self.comm.reduce_scatter_gradients(self.g, out=self.g_shard, average=False)
-        if n <= 0 or n < self.min_finished:
-            return False
-        self.g_shard.mul_(1.0 / n)
+        if self.bucketed is not None:
+            # the update plan is per bucket (this rank owns one chunk of every bucket, not [start, end)):
+            # reduce each bucket into its owned chunk and average those chunks over the finished ranks
+            chunks = []
+            for (b0, b1) in self.bucketed.bounds:
+                work, chunk = self.comm.reduce_scatter_range(self.g, b0, b1, average=False)
+                if work is not None:
+                    work.wait()
+                chunks.append(chunk)
+            if n <= 0 or n < self.min_finished:
+                return False
+            for c in chunks:
+                c.mul_(1.0 / n)
+        else:
+            self.comm.reduce_scatter_gradients(self.g, out=self.g_shard, average=False)
+            if n <= 0 or n < self.min_finished:
+                return False
+            self.g_shard.mul_(1.0 / n)
         self.apply_processors()
         self.optimize_pieces(loss)
-        self.comm.all_gather_weights(self.w, self.w16)
+        if self.bucketed is not None:
+            self.bucketed.gather_all()
+        else:
+            self.comm.all_gather_weights(self.w, self.w16)
         return True
 
     def flush(self):
@@ -397,47 +420,80 @@ class TrainStep:
         return loss
 
     # ------------------------------------------------------------------ optimizer state (checkpoints)
+    def _method_layout(self):
+        """{registered method name: (method, [(split name, split lo, split hi, offset in the method's state)])}.
+
+        A registered OptimMethod may cover several splits (``expand``: one split per run of leaves inheriting it);
+        its checkpointed per-element state is the concatenation of those splits in flat-buffer order, so the saved
+        layout depends only on the model and the registration, not on the rank count or the bucket layout."""
+        out = {}
+        for mname, meth in self.methods.items():
+            segs, off = [], 0
+            for sname, lo, hi, m in self.splits:
+                if m is meth:
+                    segs.append((sname, lo, hi, off))
+                    off += hi - lo
+            out[mname] = (meth, segs, off)
+        return out
+
     def gather_optim_state(self):
-        """Full-size optimizer state per split, identical on every rank (collective).
+        """Full-size optimizer state per registered method, identical on every rank (collective).
 
         Every per-element state tensor of a piece (same length as the piece) is placed at its offset inside a
-        split-sized zero tensor, and the disjoint pieces of all ranks are summed with one all-reduce. Scalars
-        and schedules come from the primary piece. Returns {split name: OptimMethod with full-size state}."""
+        zero tensor as long as everything the method covers, and the disjoint pieces of all ranks are summed with
+        one all-reduce. Scalars and schedules come from the method object. Returns {method name: OptimMethod}."""
         out = {}
-        for name, lo, hi, meth in self.splits:
+        for mname, (meth, segs, size) in self._method_layout().items():
             full = _clone_method(meth)
             full._shadow16 = None
+            seg_of = {s[0]: s for s in segs}
             keys = {}
             for p in self.plan:
-                if p.name != name:
+                sg = seg_of.get(p.name)
+                if sg is None:
                     continue
+                base = sg[3] + (p.lo - sg[1])
                 for k, v in p.method.state.items():
                     if torch.is_tensor(v) and v.dim() == 1 and v.numel() == p.hi - p.lo:
                         if k not in keys:
-                            keys[k] = torch.zeros(hi - lo, dtype=v.dtype, device=v.device)
-                        keys[k][p.lo - lo:p.hi - lo].copy_(v)
-            # ranks may own no piece of a split: agree on the key set first
-            names = sorted(_all_keys(self.comm, name, list(keys)))
+                            keys[k] = torch.zeros(size, dtype=v.dtype, device=v.device)
+                        keys[k][base:base + (p.hi - p.lo)].copy_(v)
+            for k in list(full.state.keys()):
+                if torch.is_tensor(full.state[k]) and full.state[k].dim() == 1:
+                    del full.state[k]
+            # ranks may own no piece of a method: agree on the key set first
+            names = sorted(_all_keys(self.comm, mname, list(keys)))
             for k in names:
                 t = keys.get(k)
                 if t is None:
-                    t = torch.zeros(hi - lo, dtype=torch.float32, device=self.device)
+                    t = torch.zeros(size, dtype=torch.float32, device=self.device)
                 self.comm.all_reduce_scalar(t)
                 full.state[k] = t
-            out[name] = full
+            out[mname] = full
         return out
 
     def load_optim_state(self, methods):
-        """Inverse of ``gather_optim_state``: slice full-size state into this rank's pieces."""
-        for p in self.plan:
-            src = methods.get(p.name)
-            if src is None:
+        """Inverse of ``gather_optim_state``: slice each method's full-size state into this rank's pieces (on
+        this rank's device); scalar state (counters, schedules) is copied to every piece."""
+        layout = self._method_layout()
+        for mname, src in methods.items():
+            if mname not in layout:
                 continue
-            for k, v in src.state.items():
-                if torch.is_tensor(v) and v.dim() == 1 and v.numel() == p.split_hi - p.split_lo:
-                    p.method.state[k] = v[p.lo - p.split_lo:p.hi - p.split_lo].to(self.device).clone()
-                elif not torch.is_tensor(v):
-                    p.method.state[k] = v
+            _, segs, size = layout[mname]
+            seg_of = {s[0]: s for s in segs}
+            for p in self.plan:
+                sg = seg_of.get(p.name)
+                if sg is None:
+                    continue
+                base = sg[3] + (p.lo - sg[1])
+                for k, v in src.state.items():
+                    if torch.is_tensor(v) and v.dim() == 1:
+                        if v.numel() != size:
+                            raise ValueError(f"optimizer state {mname}.{k}: {v.numel()} elements, the model "
+                                             f"needs {size}")
+                        p.method.state[k] = v[base:base + (p.hi - p.lo)].to(device=self.device).clone()
+                    elif not torch.is_tensor(v):
+                        p.method.state[k] = v
 
 
 def _all_keys(comm, name, keys):

@@ -11,42 +11,41 @@ layer first, defaultPrioritize :675-683) before the layer's next forward (Abstra
 MI355X mapping (one process per GPU, RCCL over xGMI):
   * buckets are contiguous ranges of the padded flat fp32 gradient buffer whose sizes are multiples of
     64 x world, so every bucket reduce-scatters into equal per-rank chunks (ZeRO-1 per bucket);
-  * the training step runs the model's backward unit by unit (top-level layers, recursing into plain
-    Sequential containers; fused residual blocks are one unit) and launches an in-place
-    ``reduce_scatter_tensor(async_op=True)`` for every bucket the finished units complete — RCCL runs it on its
-    own stream while the next units' HIP kernels run on the compute stream (fp32, or bf16-compressed);
+  * model-agnostic per-module hooks, as in the reference: every module of the tree (Sequential, Graph, any
+    container, fused residual blocks) carries this synchroniser in ``_sync``; ``AbstractModule`` calls
+    ``before_forward`` / ``after_backward`` around every forward / backward (also for subclasses that override
+    them, see ``abstractnn._sync_wrap``). When a module's backward returns, the parameters of every leaf under it
+    are final (unless a leaf is still owed a backward from a second use in the same step); a bucket whose
+    leaves are all final launches its in-place ``reduce_scatter_tensor(async_op=True)`` right there, so RCCL
+    runs it on its own stream while the remaining layers' HIP kernels run on the compute stream;
   * after backward each rank updates its chunk of every bucket (fused HIP optimizer kernel, fp32 master ->
     bf16 shadow) bucket by bucket as the reduce-scatters land;
   * the all-gather of the updated chunks is deferred: the next step issues every bucket's all-gather in
-    priority order before its forward and waits for a bucket only right before the first unit that reads it,
-    so weight distribution overlaps the forward pass. ``gather_all`` finishes it at any sync point.
+    priority order before its forward and waits for a bucket only right before the first module that reads it
+    (a leaf with parameters, or a fused container that runs its children's kernels itself), so weight
+    distribution overlaps the forward pass. ``gather_all`` finishes it at any sync point.
 Buckets default to ~8M elements (32 MB fp32): large enough to run the xGMI links near their per-link rate,
-small enough that the last bucket's reduce-scatter hides behind a few layers of backward.
+small enough that the last bucket's reduce-scatter hides behind a few layers of backward. Every rank executes
+the same module sequence, so every rank launches the buckets in the same order (an RCCL requirement).
 """
 import torch
 
 
-def backward_units(model):
-    """Leaf units of the backward schedule, in forward order: top-level children, recursing into plain
-    Sequential containers (a Sequential with a fused residual plan is a single unit)."""
-    from ..nn.containers import Sequential
-
-    units = []
-
-    def rec(m):
-        if type(m) is Sequential and m._residual_plan is None and m.modules:
-            for c in m.modules:
-                rec(c)
-        else:
-            units.append(m)
-
-    rec(model)
-    return units
+def _own_ranges(m, base, es):
+    """[lo, hi) element ranges of ``m``'s OWN parameters inside the flat buffer starting at ``base``."""
+    out = []
+    for wname, _ in getattr(m, "_params", ()):
+        t = getattr(m, wname, None)
+        if isinstance(t, torch.Tensor) and t.numel():
+            lo = (t.data_ptr() - base) // es
+            out.append((int(lo), int(lo) + t.numel()))
+    return out
 
 
-def _nparams(m):
-    p = m.parameters()
-    return sum(t.numel() for t in p[0]) if p else 0
+def _bypasses_children(m):
+    """Containers whose forward runs (some of) their children's kernels without calling the children's forward:
+    the fused ResNet block (nn/fusion.py residual plan) reads the last BN's weights inside its own forward."""
+    return getattr(m, "_residual_plan", None) is not None
 
 
 class BucketedGradSync:
@@ -66,48 +65,95 @@ class BucketedGradSync:
             b1 = min(padded, b0 + bucket_elems)
             self.bounds.append((b0, b1))
             b0 = b1
-        self.units = backward_units(self.model)
-        offs, off = [], 0
-        for u in self.units:
-            offs.append(off)
-            off += _nparams(u)
-        self.unit_off = offs
-        total = step.total
-        nb, nu = len(self.bounds), len(self.units)
-        # the first unit index that touches each bucket: the bucket's gradient is complete once that unit's
-        # backward ran (units run backward last-to-first); the same unit is the first forward reader
-        self.first_unit = []
-        self.last_unit = []
-        for (b0, b1) in self.bounds:
-            fu, lu = nu - 1, 0
-            touched = [i for i, (o, u) in enumerate(zip(offs, self.units))
-                       if _nparams(u) and o < b1 and o + _nparams(u) > b0]
-            if touched:
-                fu, lu = touched[0], touched[-1]
-            if b0 >= total:       # pure padding bucket: ready immediately
-                fu, lu = nu, nu
-            self.first_unit.append(fu)
-            self.last_unit.append(lu)
-        # buckets a unit must wait for before its forward
-        self.unit_needs = [[b for b in range(nb) if self.first_unit[b] <= i <= self.last_unit[b]]
-                           for i in range(nu)]
         self.chunks = [(b1 - b0) // world for (b0, b1) in self.bounds]
+        self._index_modules(step.total)
         self.order = self._priority_order(priorities)
         self.works = {}
         self.ag_works = {}
+        self._fwd = {}
+        self._done = set()
+        self._rem = list(self._rem0)
+        self.launch_log = []          # bucket ids in launch order, for tests / diagnostics
+        self.install()
+
+    # ---------------------------------------------------------------------------------------- module index
+    def _index_modules(self, total):
+        base, es = self.w.data_ptr(), self.w.element_size()
+        mods, seen = [], set()
+
+        def rec(m):
+            if id(m) in seen:
+                return
+            seen.add(id(m))
+            mods.append(m)
+            for c in m.modules_list() or []:
+                rec(c)
+
+        rec(self.model)
+        self.modules = mods
+        # leaves = modules owning parameters, in flat-buffer order (= module order of the parameter vector)
+        leaves = [(r, m) for m in mods for r in [_own_ranges(m, base, es)] if r]
+        leaves.sort(key=lambda t: t[0][0][0])
+        self.leaves = [m for _, m in leaves]
+        self.leaf_index = {id(m): i for i, m in enumerate(self.leaves)}
+        nb = len(self.bounds)
+        self.leaf_buckets = []
+        for rngs, _ in leaves:
+            bs = sorted({b for (lo, hi) in rngs for b, (b0, b1) in enumerate(self.bounds) if lo < b1 and hi > b0})
+            self.leaf_buckets.append(bs)
+        self._rem0 = [0] * nb
+        for bs in self.leaf_buckets:
+            for b in bs:
+                self._rem0[b] += 1
+        # every module -> the leaves under it (itself included)
+        self.sub_leaves = {}
+
+        def leaves_of(m, memo):
+            k = id(m)
+            if k in memo:
+                return memo[k]
+            memo[k] = []           # cycle guard (shared sub-trees)
+            out = []
+            if k in self.leaf_index:
+                out.append(self.leaf_index[k])
+            for c in m.modules_list() or []:
+                out.extend(leaves_of(c, memo))
+            memo[k] = sorted(set(out))
+            return memo[k]
+
+        memo = {}
+        for m in mods:
+            self.sub_leaves[id(m)] = leaves_of(m, memo)
+        # buckets a module must have gathered before its forward reads weights
+        self.fwd_buckets = {}
+        for m in mods:
+            if id(m) in self.leaf_index:
+                self.fwd_buckets[id(m)] = self.leaf_buckets[self.leaf_index[id(m)]]
+            elif _bypasses_children(m):
+                self.fwd_buckets[id(m)] = sorted({b for li in self.sub_leaves[id(m)] for b in self.leaf_buckets[li]})
+        self._pad_buckets = [b for b in range(nb) if self._rem0[b] == 0]
+
+    def install(self):
+        for m in self.modules:
+            m._sync = self
+
+    def uninstall(self):
+        for m in self.modules:
+            if getattr(m, "_sync", None) is self:
+                m._sync = None
 
     def _priority_order(self, priorities):
         """Bucket all-gather issue order: highest priority first; default = forward execution order
-        (reference defaultPrioritize: priority = len - execution index)."""
+        (reference defaultPrioritize: priority = number of layers - execution index)."""
         nb = len(self.bounds)
         if not priorities:
             return list(range(nb))
-        pr = []
-        for b in range(nb):
-            best = float("-inf")
-            for i in range(min(self.first_unit[b], len(self.units) - 1), min(self.last_unit[b], len(self.units) - 1) + 1):
-                best = max(best, priorities.get(self.units[i].getName(), len(self.units) - i))
-            pr.append(best)
+        nl = len(self.leaves)
+        pr = [float("-inf")] * nb
+        for li, (m, bs) in enumerate(zip(self.leaves, self.leaf_buckets)):
+            p = priorities.get(m.getName(), nl - li)
+            for b in bs:
+                pr[b] = max(pr[b], p)
         return sorted(range(nb), key=lambda b: (-pr[b], b))
 
     def owned_ranges(self):
@@ -131,54 +177,76 @@ class BucketedGradSync:
             self.start_gather()
         self._wait_ag(list(self.ag_works))
 
-    def forward(self, x):
-        """Forward unit by unit, waiting for each bucket's weight all-gather only before its first reader."""
+    def begin_step(self):
+        """Called once per training step before the forward: issue the deferred all-gathers, reset the
+        per-step backward bookkeeping."""
         if self.step._pending_gather:
             self.start_gather()
             self.step._pending_gather = False
-        out = x
-        for i, u in enumerate(self.units):
-            if self.ag_works:
-                self._wait_ag(self.unit_needs[i])
-            out = u.forward(out)
+        self.works = {}
+        self._fwd = {}
+        self._done = set()
+        self._rem = list(self._rem0)
+        self.launch_log = []
+
+    def before_forward(self, m):
+        k = id(m)
+        self._fwd[k] = self._fwd.get(k, 0) + 1
+        if self.ag_works:
+            bs = self.fwd_buckets.get(k)
+            if bs:
+                self._wait_ag(bs)
+
+    def end_forward(self):
         self._wait_ag(list(self.ag_works))
-        self.model.output = out
-        return out
 
     # ---------------------------------------------------------------------------------------- backward
     def _launch(self, b):
+        if b in self.works:
+            return
         b0, b1 = self.bounds[b]
+        self.launch_log.append(b)
         self.works[b] = self.comm.reduce_scatter_range(self.g, b0, b1, async_op=True)[0]
 
-    def unit_done(self, ui):
-        for b in range(len(self.bounds) - 1, -1, -1):
-            if b not in self.works and self.first_unit[b] >= ui:
-                self._launch(b)
+    def after_backward(self, m):
+        if self.step.defer_sync:   # straggler drop: every rank reduces after the finished vote (TrainStep)
+            return
+        k = id(m)
+        n = self._fwd.get(k, 0)
+        if n > 1:                  # used again earlier in the forward: its gradient is not final yet
+            self._fwd[k] = n - 1
+            return
+        self._fwd[k] = 0
+        for li in self.sub_leaves.get(k, ()):
+            if li in self._done:
+                continue
+            leaf = self.leaves[li]
+            if self._fwd.get(id(leaf), 0) > 0 and leaf is not m:
+                continue           # the leaf still owes a backward of its own (shared elsewhere)
+            self._done.add(li)
+            for b in self.leaf_buckets[li]:
+                self._rem[b] -= 1
+                if self._rem[b] == 0:
+                    self._launch(b)
 
-    def backward(self, input, gradOutput):
-        """Run the model's backward unit by unit, firing bucket reduce-scatters as they complete."""
-        self.works = {}
-        for b in range(len(self.bounds)):
-            if self.first_unit[b] >= len(self.units):
+    def begin_backward(self):
+        if self.step.defer_sync:
+            return
+        for b in self._pad_buckets:          # pure padding buckets: nothing to wait for
+            self._launch(b)
+
+    def end_backward(self):
+        for b in range(len(self.bounds) - 1, -1, -1):
+            if b not in self.works:
                 self._launch(b)
-        g = gradOutput
-        outs = [u.output for u in self.units]
-        for i in range(len(self.units) - 1, -1, -1):
-            inp = outs[i - 1] if i > 0 else input
-            g = self.units[i].backward(inp, g)
-            self.unit_done(i)
-        self.model.gradInput = g
-        return g
 
     # ---------------------------------------------------------------------------------------- update
     def update(self, loss):
-        for b in range(len(self.bounds)):
-            if b not in self.works:
-                self._launch(b)
+        self.end_backward()
         step = self.step
         if step.processors:
             # processors (clipping, LARS) need the whole reduced gradient first
-            for b in range(len(self.bounds)):
+            for b in list(self.launch_log):
                 h = self.works.pop(b)
                 if h is not None:
                     h.wait()
@@ -186,7 +254,7 @@ class BucketedGradSync:
             step.optimize_pieces(loss)
             return
         step._lockstep()
-        for b in range(len(self.bounds) - 1, -1, -1):     # buckets completed first were launched first
+        for b in list(self.launch_log):                   # in launch order: the earliest collectives land first
             h = self.works.pop(b)
             if h is not None:
                 h.wait()

@@ -401,8 +401,13 @@ def save_bigdl(module, path, weightPath=None, overWrite=False):
     return module
 
 
-_DT_ID = {"INT32": 0, "INT64": 1, "FLOAT": 2, "DOUBLE": 3, "BOOL": 5, "SHORT": 7}
-_DT_FMT = {0: ">i4", 1: ">i8", 2: ">f4", 3: ">f8", 5: ">u1", 7: ">i2"}
+# The weight file keys storages by the Scala ``BigDLDataType`` enumeration (serializer/Types.scala:49-52:
+# FLOAT, DOUBLE, CHAR, BOOL, STRING, INT, SHORT, LONG, BYTESTRING, BYTE = 0..9), NOT by the protobuf DataType
+# numbering used inside TensorStorage messages. Element encodings follow DataReaderWriter.scala (big-endian
+# DataOutputStream: writeFloat / writeDouble / writeChar (u16) / writeBoolean (u8) / writeInt / writeShort /
+# writeLong / raw bytes).
+_DT_ID = {"FLOAT": 0, "DOUBLE": 1, "CHAR": 2, "BOOL": 3, "INT32": 5, "SHORT": 6, "INT64": 7, "BYTE": 9}
+_DT_FMT = {0: ">f4", 1: ">f8", 2: ">u2", 3: ">u1", 5: ">i4", 6: ">i2", 7: ">i8", 9: ">i1"}
 
 
 def _write_weights(path, raw):
@@ -427,6 +432,8 @@ def _read_weights(path):
     for _ in range(n):
         sid, code, size = struct.unpack_from(">iii", data, pos)
         pos += 12
+        if code not in _DT_FMT:
+            raise ValueError(f"weight file storage {sid}: unsupported BigDLDataType code {code}")
         fmt = np.dtype(_DT_FMT[code])
         out[sid] = np.frombuffer(data, dtype=fmt, count=size, offset=pos).astype(fmt.newbyteorder("="))
         pos += size * fmt.itemsize

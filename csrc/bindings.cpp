@@ -224,6 +224,9 @@ void sgd_step(const Tensor& w, const Tensor& g, const OptT& mom, const OptT& w16
               double momentum, double dampening, bool nesterov, bool first, const OptT& lr_dev,
               const OptT& seg_off, const OptT& seg_wd, int64_t base) {
   TORCH_CHECK(w.numel() == g.numel(), "sgd: size");
+  TORCH_CHECK(!(mom && mom->defined()) || mom->numel() == w.numel(), "sgd: mom has ", mom ? mom->numel() : 0,
+              " elements, w has ", w.numel());
+  TORCH_CHECK(!(w16 && w16->defined()) || w16->numel() == w.numel(), "sgd: w16 size");
   const long* so = nullptr;
   int nseg = 0;
   if (seg_off && seg_off->defined()) {
@@ -238,6 +241,7 @@ void sgd_step(const Tensor& w, const Tensor& g, const OptT& mom, const OptT& w16
 }
 void adam_step(const Tensor& w, const Tensor& g, const Tensor& m, const Tensor& v, const OptT& w16, double lr,
                double b1, double b2, double eps, double wd, double bc1, double bc2) {
+  TORCH_CHECK(w.numel() == g.numel() && m.numel() == w.numel() && v.numel() == w.numel(), "adam: state size");
   bigdl_adam_step(mf(w, "w"), cf(g, "g"), mf(m, "m"), mf(v, "v"), ombf(w16, "w16"), w.numel(), (float)lr, (float)b1,
                   (float)b2, (float)eps, (float)wd, (float)bc1, (float)bc2, stream());
 }

@@ -223,3 +223,221 @@ def test_distributed_predictor_shards_batches_and_gathers_in_order():
         assert torch.equal(r[1], ref[1])
         assert torch.allclose(r[2], ref[0], atol=1e-6)
     assert two[0][3] == [0, 2, 4, 6] and two[1][3] == [1, 3, 5, 7]
+
+
+# ------------------------------------------------------------------------------------------------------------------
+# world 4 / 8 (gloo CPU). One spawn per world runs every configuration, so the 8-rank case stays cheap. The model has
+# 843 parameters: not a multiple of 64 x world, so the flat buffers are padded; bucket_elems=256 is below a shard at
+# world 4 and rounds up to one 64 x world unit at world 8.
+_CONFIGS = [
+    ("sgd", False, None, None, False),
+    ("sgd", True, None, None, False),
+    ("sgd", True, None, None, True),        # sync-BN across the ranks
+    ("split", True, None, None, False),     # per-sub-module methods
+    ("lars", True, None, None, False),      # cross-shard LARS layer norms
+    ("sgd", True, None, 0.5, False),        # L2 clipping
+]
+
+
+def _train_many(rank, world, configs, iters):
+    return [_train(rank, world, k, ov if world > 1 else False, cp if world > 1 else None, cl, iters, bn)
+            for (k, ov, cp, cl, bn) in configs]
+
+
+@pytest.mark.parametrize("world", [4, 8])
+def test_n_ranks_equal_one_rank_n_times_batch(world):
+    iters = 3
+    many = run_distributed(_train_many, world, (_CONFIGS, iters), timeout=600)
+    one = run_distributed(_train_many, 1, (_CONFIGS, iters), timeout=600)[0]
+    for ci, cfg in enumerate(_CONFIGS):
+        w0, m0, b0 = many[0][ci]
+        assert b0 == cfg[1], cfg
+        for r in range(1, world):
+            assert torch.equal(many[r][ci][0], w0), (cfg, r)     # every rank holds the same fp32 master
+        assert torch.allclose(w0, one[ci][0], atol=2e-5, rtol=1e-4), (cfg, (w0 - one[ci][0]).abs().max())
+        for name, st in one[ci][1].items():
+            for k, v in st.items():
+                assert torch.allclose(m0[name][k], v, atol=2e-5, rtol=1e-4), (cfg, name, k)
+
+
+def _bf16_many(rank, world):
+    return _train(rank, world, "sgd", True, "bf16", None, 3, False)[0]
+
+
+@pytest.mark.parametrize("world", [4, 8])
+def test_bf16_compression_rank_identical_at_n_ranks(world):
+    res = run_distributed(_bf16_many, world, timeout=600)
+    one = run_distributed(_train, 1, ("sgd", False, None, None, 3, False))[0][0]
+    for r in res[1:]:
+        assert torch.equal(r, res[0])
+    assert ((res[0] - one).norm() / one.norm()) < 1e-2
+
+
+def _graph_model():
+    from bigdl_amd import nn
+    from bigdl_amd.utils.random_generator import RNG
+
+    RNG.setSeed(11)
+    inp = nn.Input()
+    a = nn.Linear(6, 32).setName("g1")(inp)
+    a = nn.Tanh()(a)
+    b = nn.Linear(32, 32).setName("g2")(a)
+    c = nn.Linear(32, 32).setName("g3")(a)
+    s = nn.CAddTable()(b, c)
+    s = nn.ReLU()(s)
+    o = nn.Linear(32, 3).setName("g4")(s)
+    return nn.Graph([inp], [o]).setName("gnet")
+
+
+def _graph_overlap(rank, world, iters):
+    from bigdl_amd import nn
+    from bigdl_amd import optim as O
+    from bigdl_amd.optim.train_step import TrainStep
+
+    model = _graph_model()
+    step = TrainStep(model, nn.MSECriterion(), O.SGD(0.05, momentum=0.9, dampening=0.0), device="cpu",
+                     overlap=None, bucket_elems=512)
+    bk = step.bucketed
+    events = []
+    if bk is not None:
+        orig_launch, orig_after = bk._launch, bk.after_backward
+
+        def launch(b):
+            if b not in bk.works:
+                events.append(("rs", b))
+            orig_launch(b)
+
+        def after(m):
+            if m._params:
+                events.append(("bwd", m.getName()))
+            orig_after(m)
+
+        bk._launch, bk.after_backward = launch, after
+    X, Y = _data()
+    n = X.shape[0] // world
+    for it in range(iters):
+        events.clear()
+        step.step(X[rank * n:(rank + 1) * n], Y[rank * n:(rank + 1) * n])
+    step.gather_model()
+    return step.w[:step.total].clone(), list(events), len(bk.bounds) if bk is not None else 0
+
+
+def test_graph_model_overlaps_reduce_scatter_with_backward():
+    """An nn.Graph (not a Sequential) under the bucketed path: the per-module hooks launch a bucket's
+    reduce-scatter as soon as its layers' backward finished, i.e. before the backward of the first layer ends
+    (reference AbstractModule.scala:282-297), and the result equals one rank at double batch."""
+    two = run_distributed(_graph_overlap, 2, (3,))
+    one = run_distributed(_graph_overlap, 1, (3,))[0]
+    w, ev, nb = two[0]
+    assert nb > 1
+    first_rs = next(i for i, e in enumerate(ev) if e[0] == "rs")
+    last_bwd = max(i for i, e in enumerate(ev) if e[0] == "bwd")
+    assert first_rs < last_bwd, ev
+    assert ev[last_bwd][1] == "g1"          # the first layer finishes its backward last
+    assert torch.equal(two[1][0], w)
+    assert torch.allclose(w, one[0], atol=2e-5, rtol=1e-4)
+
+
+def _parallel_drop_job(rank, world, path):
+    import time
+
+    from bigdl_amd import nn
+    from bigdl_amd import optim as O
+    from bigdl_amd.dataset.core import DataSet, Sample
+    from bigdl_amd.utils.engine import Engine
+
+    Engine.setProperty("bigdl.parallelOptimizer.bucketElems", "256")
+    model = _model()
+    X, Y = _data(64)
+    ds = DataSet.rdd([Sample(X[i], Y[i]) for i in range(64)], shuffle=False)
+    opt = O.ParallelOptimizer(model, ds, nn.MSECriterion(), batchSize=16,
+                              optimMethod=O.SGD(0.05, momentum=0.9, dampening=0.0),
+                              endTrigger=O.Trigger.maxIteration(8))
+    opt.setDropModuleProperty(0.25, 0.5, batchsize=2, warmupIteration=2)
+    if rank == 1:
+        base = opt.dataset
+
+        class Slow:
+            def __getattr__(self, k):
+                return getattr(base, k)
+
+            def data(self, train=True):
+                for i, b in enumerate(base.data(train)):
+                    if i >= 3:
+                        time.sleep(0.3)
+                    yield b
+        opt.dataset = Slow()
+    m = opt.optimize()
+    nb = len(opt._step.bucketed.bounds)
+    return m.getParameters()[0][:opt._step.total].clone(), nb
+
+
+def test_parallel_optimizer_straggler_drop_with_many_buckets(tmp_path):
+    """ParallelOptimizer (bucketed plan: one owned chunk per bucket) with straggler drop: every bucket is reduced
+    and every owned chunk updated, so all ranks end on the same finite weights."""
+    res = run_distributed(_parallel_drop_job, 2, (str(tmp_path),))
+    (w0, nb), (w1, _) = res
+    assert nb > 1
+    assert torch.equal(w0, w1)
+    assert torch.isfinite(w0).all()
+
+
+def _resume_job(rank, world, path, phase, iters):
+    from bigdl_amd import nn
+    from bigdl_amd import optim as O
+    from bigdl_amd.dataset.core import DataSet, Sample
+    from bigdl_amd.utils.engine import Engine
+
+    model = _model()
+    X, Y = _data(64)
+    ds = DataSet.rdd([Sample(X[i], Y[i]) for i in range(64)], shuffle=False)
+    opt = O.Optimizer(model, ds, nn.MSECriterion(), batchSize=16,
+                      optimMethod=O.SGD(0.05, momentum=0.9, dampening=0.0),
+                      endTrigger=O.Trigger.maxIteration(iters))
+    opt.setCheckpoint(path, O.Trigger.severalIteration(4))
+    if phase == "resume":
+        Engine.setProperty("bigdl.failure.resume", "true")
+    m = opt.optimize()
+    if phase == "resume":
+        Engine.setProperty("bigdl.failure.resume", "")
+    st = opt._step.gather_optim_state()
+    return m.getParameters()[0][:opt._step.total].clone(), st["net"].state["dfdx"].clone()
+
+
+def test_resume_from_checkpoint_restores_sharded_momentum(tmp_path):
+    """Train 8 iterations straight vs 4 iterations + checkpoint, then a fresh job resuming from it to 8 (both on 2
+    ranks): the resumed job slices the checkpoint's full momentum into each rank's shard on its device, so both
+    runs end on the same weights and momentum."""
+    straight = run_distributed(_resume_job, 2, (str(tmp_path / "a"), "fresh", 8))
+    os.makedirs(tmp_path / "b")
+    run_distributed(_resume_job, 2, (str(tmp_path / "b"), "fresh", 4))
+    resumed = run_distributed(_resume_job, 2, (str(tmp_path / "b"), "resume", 8))
+    assert torch.allclose(resumed[0][0], straight[0][0], atol=1e-6), (resumed[0][0] - straight[0][0]).abs().max()
+    assert torch.allclose(resumed[0][1], straight[0][1], atol=1e-6)
+    assert torch.equal(resumed[0][0], resumed[1][0])
+
+
+def _lars_layerwise(rank, world, expand):
+    from bigdl_amd import nn
+    from bigdl_amd import optim as O
+    from bigdl_amd.optim.train_step import TrainStep
+
+    model = _model()
+    if expand:   # ONE LarsSGD registered on the root, inherited by every leaf (expandOptimMethods)
+        methods = {"net": O.LarsSGD(None, 1.0, 0.1, 0.0, 1e-3, 0.5)}
+    else:        # the reference's per-layer clones, registered explicitly
+        methods = O.LarsSGD.createOptimForModule(model, trust=1.0, learningRate=0.1, weightDecay=1e-3, momentum=0.5)
+    step = TrainStep(model, nn.MSECriterion(), methods, device="cpu", overlap=False, expand_methods=expand)
+    X, Y = _data()
+    for _ in range(3):
+        step.step(X, Y)
+    return step.w[:step.total].clone(), [s[0] for s in step.splits]
+
+
+def test_lars_inherited_by_leaves_stays_layer_wise():
+    """ParallelOptimizer.expandOptimMethods (ParallelOptimizer.scala:642-670) clones the method per leaf layer: a
+    LarsSGD inherited from the root must keep one trust ratio per layer, not one over merged leaves."""
+    exp = run_distributed(_lars_layerwise, 1, (True,))[0]
+    ref = run_distributed(_lars_layerwise, 1, (False,))[0]
+    assert len(exp[1]) == 3                  # fc1, fc2, fc3: no merging
+    assert torch.allclose(exp[0], ref[0], atol=1e-6)

@@ -209,3 +209,36 @@ def test_bigdl_proto_field_layout_is_the_reference_schema(tmp_path):
     attrs = {e.str(1): e.msg(2) for e in sub.msgs(8)}                          # attr map<string, AttrValue> = 8
     assert attrs["inputSize"].int(3) == 2 and attrs["outputSize"].int(3) == 3  # int32Value = 3
     assert "global_storage" in {e.str(1) for e in root.msgs(8)}
+
+
+def test_bigdl_weight_file_uses_bigdl_datatype_codes(tmp_path):
+    """A weight file hand-built in the reference layout (ModuleLoader.saveWeightsToFile: big-endian magic, count,
+    then {storageId, BigDLDataType id, size, data}, then the MD5 of all of it) with the Scala enumeration codes
+    (serializer/Types.scala:51: FLOAT=0, DOUBLE=1, ..., INT=5, SHORT=6, LONG=7) reads back as those values, and our
+    writer emits the same codes."""
+    import hashlib
+    import struct
+
+    import numpy as np
+
+    from bigdl_amd.utils import bigdl_proto as bp
+
+    f32 = np.array([1.5, -2.25, 3.0], dtype=">f4")
+    f64 = np.array([0.125, 7.0], dtype=">f8")
+    i32 = np.array([5, -9], dtype=">i4")
+    i64 = np.array([1 << 40], dtype=">i8")
+    body = struct.pack(">ii", bp.MAGIC_NO, 4)
+    for sid, code, arr in ((11, 0, f32), (12, 1, f64), (13, 5, i32), (14, 7, i64)):
+        body += struct.pack(">iii", sid, code, arr.size) + arr.tobytes()
+    dig = hashlib.md5(body).digest()
+    (tmp_path / "ref.bin").write_bytes(body + struct.pack(">i", len(dig)) + dig)
+    got = bp._read_weights(str(tmp_path / "ref.bin"))
+    assert got[11].dtype == np.float32 and got[11].tolist() == [1.5, -2.25, 3.0]
+    assert got[12].dtype == np.float64 and got[12].tolist() == [0.125, 7.0]
+    assert got[13].tolist() == [5, -9] and got[14].tolist() == [1 << 40]
+
+    bp._write_weights(str(tmp_path / "ours.bin"), {3: ("FLOAT", np.arange(4, dtype=np.float32)),
+                                                   4: ("INT64", np.array([2], dtype=np.int64))})
+    raw = (tmp_path / "ours.bin").read_bytes()
+    assert struct.unpack_from(">iii", raw, 8) == (3, 0, 4)                 # FLOAT storage -> code 0
+    assert struct.unpack_from(">iii", raw, 8 + 12 + 16) == (4, 7, 1)       # LONG storage -> code 7
