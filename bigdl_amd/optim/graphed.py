@@ -24,8 +24,23 @@ from ..parallel.graph_segments import SegmentedGraph
 from .sgd import SGD
 
 
+def graphable(step):
+    """Whether ``step`` can be captured: every update is a plain SGD (its only per-step host value, the rate, is
+    published to a device scalar by ``graph_prologue``) and no parameter processor reads host values."""
+    from ..parallel.processors import LarsProcessor
+
+    return (all(type(p.method) is SGD for p in step.plan)
+            and not any(isinstance(q, LarsProcessor) for q in step.processors))
+
+
 class GraphedTrainStep:
-    def __init__(self, step, x, y, warmup=2):
+    """``prewarmed=True``: the caller has already run eager iterations of ``step`` on batches of this shape
+    (kernel plans, workspaces, momentum buffers and communicators exist), so nothing extra is executed: the
+    constructor only captures, and the first ``replay`` runs the captured iteration (the Optimizer loop uses this
+    so capturing changes no training step). Otherwise ``warmup`` eager steps on (x, y) and one more on the
+    capture stream run first (bench)."""
+
+    def __init__(self, step, x, y, warmup=2, prewarmed=False):
         self.step = step
         for p in step.plan:
             if type(p.method) is not SGD:
@@ -33,8 +48,9 @@ class GraphedTrainStep:
                                 "values; use the eager TrainStep")
         self.x = x.clone()
         self.y = y.clone()
-        for _ in range(max(warmup, 1)):
-            step.step(self.x, self.y)
+        if not prewarmed:
+            for _ in range(max(warmup, 1)):
+                step.step(self.x, self.y)
         torch.cuda.synchronize()
         methods = []
         for p in step.plan:
@@ -43,13 +59,14 @@ class GraphedTrainStep:
             methods.append(p.method)
         self.methods = methods
         self._prologue()
-        s = torch.cuda.Stream()
-        s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):          # one more eager step on the capture stream (allocator warm-up)
-            step.step(self.x, self.y)
-        torch.cuda.current_stream().wait_stream(s)
-        torch.cuda.synchronize()
-        self._prologue()
+        if not prewarmed:
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):          # one more eager step on the capture stream (allocator warm-up)
+                step.step(self.x, self.y)
+            torch.cuda.current_stream().wait_stream(s)
+            torch.cuda.synchronize()
+            self._prologue()
         self.graph = SegmentedGraph()
         with warnings.catch_warnings():
             warnings.filterwarnings("ignore", message=".*CUDA Graph is empty.*")
@@ -70,6 +87,18 @@ class GraphedTrainStep:
         self._fresh = False
         self.graph.replay()
         return self.loss
+
+    def matches(self, x, y):
+        return (tuple(x.shape) == tuple(self.x.shape) and x.dtype == self.x.dtype
+                and tuple(y.shape) == tuple(self.y.shape) and y.dtype == self.y.dtype)
+
+    def eager(self, x, y):
+        """One eager iteration while the captured methods read their rate from the device scalar (a batch whose
+        shape differs from the captured one)."""
+        if not self._fresh:
+            self._prologue()
+        self._fresh = False
+        return self.step.step(x, y)
 
     def release(self):
         for m in self.methods:

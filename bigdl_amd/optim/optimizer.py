@@ -308,7 +308,9 @@ class Optimizer:
         world = step.comm.world
         drop = _StragglerDrop(self, world) if self.dropPercentage > 0 else None
         step.defer_sync = drop is not None
-        it = iter(self.dataset.data(train=True))
+        from .device_feed import DeviceFeed
+
+        it = DeviceFeed(iter(self.dataset.data(train=True)), step.device)
         wall0 = time.perf_counter()
         pending = []  # (iteration, loss tensor, records)
         # liveness: a rank stuck (dead peer in a collective, hung kernel) exits instead of hanging the job
@@ -318,6 +320,11 @@ class Optimizer:
         try:
             self._train_iterations(st, step, world, drop, it, wall0, pending, watchdog)
         finally:
+            it.close()
+            if self._graph is not None:
+                torch.cuda.synchronize()
+                self._graph.release()
+                self._graph = None
             if watchdog is not None:
                 watchdog.stop()
         step.gather_model()
@@ -325,25 +332,59 @@ class Optimizer:
             torch.cuda.synchronize()
         return self.model
 
+    _graph = None
+    _iteration_hook = None       # callable(neval) after every iteration (benchmarks, tests)
+
+    def _use_graph(self, step, drop):
+        """Capture the iteration in HIP graphs (reference per-iteration task launch, DistriOptimizer.scala:204-396)
+        when the device is a GPU, every update is graph-safe (plain SGD), no straggler drop is active and
+        ``bigdl.optim.graph`` is not "false"."""
+        from .graphed import graphable
+
+        flag = str(Engine.getProperty("bigdl.optim.graph", "true")).lower()
+        return step.device.type == "cuda" and drop is None and flag not in ("0", "false", "no") and graphable(step)
+
     def _train_iterations(self, st, step, world, drop, it, wall0, pending, watchdog):
+        use_graph = self._use_graph(step, drop)
+        eager_done = 0
         while not self.endWhen(st):
             t0 = time.perf_counter()
-            batch = next(it)
-            batch = batch.to(step.device, non_blocking=True)
+            batch = next(it)        # device-resident; its copy was issued during the previous iteration
             fetch = time.perf_counter() - t0
             self.metrics.add("data fetch time", fetch)
             t1 = time.perf_counter()
             finished = None
-            if drop is not None and drop.timed_out(fetch):
+            x, y = batch.getInput(), batch.getTarget()
+            g = self._graph
+            if (use_graph and g is None and eager_done >= 2 and isinstance(x, torch.Tensor)
+                    and isinstance(y, torch.Tensor)):
+                from .graphed import GraphedTrainStep
+
+                try:
+                    g = self._graph = GraphedTrainStep(step, x, y, prewarmed=True)
+                    logger.info("training iteration captured in %d HIP graph segment(s)", len(g.graph))
+                except Exception as e:  # noqa: BLE001 - fall back to eager launches
+                    logger.warning("HIP graph capture failed (%s: %s); eager iterations", type(e).__name__, e)
+                    use_graph, g, self._graph = False, None, None
+            if g is not None:
+                if isinstance(x, torch.Tensor) and g.matches(x, y):
+                    loss = g.replay(x, y).detach().clone()   # the graph's loss buffer is rewritten every replay
+                else:
+                    loss = g.eager(x, y)
+                n_ok = 1
+            elif drop is not None and drop.timed_out(fetch):
                 # straggler: the deadline passed before compute could start — contribute nothing this iteration
                 loss = torch.zeros((), device=step.device)
                 finished = 0.0
             else:
                 step.zero_grad()
-                loss = step.forward_backward(batch.getInput(), batch.getTarget())
+                loss = step.forward_backward(x, y)
+                eager_done += 1
                 if drop is not None:
                     finished = drop.finished(time.perf_counter() - t0)
-            if finished is not None:
+            if g is not None:
+                pass
+            elif finished is not None:
                 step.min_finished = world * (1.0 - self.maxDropPercentage)
                 n_ok = drop.record(step.sync_and_update(loss, finished=finished), finished)
             else:
@@ -369,6 +410,8 @@ class Optimizer:
             self._validate(step)
             self._checkpoint(step)
             del n_ok
+            if self._iteration_hook is not None:
+                self._iteration_hook(st["neval"] - 1)
             if watchdog is not None:
                 watchdog.kick()
         if pending:

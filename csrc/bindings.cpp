@@ -76,6 +76,13 @@ void conv_nt(const Tensor& src, const Tensor& wt, const Tensor& out, const OptT&
   if (a.addend) TORCH_CHECK(a.ldo == a.Ncol, "conv_nt: an addend needs a dense output (ldo == Ncol)");
   TORCH_CHECK((a.OH - 1) * a.omul_h + a.ooff_h < a.OHo && (a.OW - 1) * a.omul_w + a.ooff_w < a.OWo,
               "conv_nt: output placement out of range");
+  a.ws = nullptr;
+  Tensor ws;
+  const long wsn = bigdl_conv_nt_plan(&a);
+  if (wsn > 0) {     // split-K partials in a caching-allocator workspace (graph-capture safe)
+    ws = at::empty({wsn}, out.options().dtype(at::kFloat));
+    a.ws = ws.data_ptr<float>();
+  }
   const int rc = bigdl_conv_nt(&a, stream());
   TORCH_CHECK(rc == 0, "conv_nt: unsupported shape (channels must be a multiple of 8; fp32 output needs Ncol % 8 "
               "== 0 and no fused stats / BN / ReLU / addend)");
@@ -302,6 +309,7 @@ void conv_i8(const Tensor& src, const Tensor& wt, const Tensor& out, const OptT&
   a.wt = reinterpret_cast<const uint16_t*>(wt.data_ptr<int8_t>());
   a.out = reinterpret_cast<uint16_t*>(out.data_ptr());
   a.bias = ocf(bias, "bias"); a.stats = nullptr; a.addend = nullptr; a.out32 = nullptr; a.accum32 = 0;
+  a.ws = nullptr; a.ksplit = 0;
   a.bnx = nullptr; a.bnz = nullptr; a.bnmean = nullptr; a.bnaff = nullptr; a.bnred = nullptr;
   a.Nb = geo[0]; a.Hs = geo[1]; a.Ws = geo[2]; a.Cs = geo[3]; a.OH = geo[4]; a.OW = geo[5];
   a.mul_h = geo[6]; a.mul_w = geo[7]; a.ldw = geo[8]; a.Ncol = geo[9]; a.ldo = geo[10];

@@ -1289,6 +1289,305 @@ __global__ __launch_bounds__(256) void transpose_krsc_batched_kernel(const long*
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// 256 x 256 implicit-GEMM NT tile for the compute-heavy layers (N >= 256): 8 waves as 2 (pixels) x 4 (channels),
+// wave tile 128 x 64 (32 accumulators), BK = 32 per K-step and FOUR LDS-DMA stages of 32 KB: three K-steps stay in
+// flight across every barrier (counted `s_waitcnt vmcnt`, raw s_barrier: never the vmcnt(0) of __syncthreads,
+// cdna_hip_programming.md §5 "Pipelining across barriers"). Twice the FLOP per staged byte of the 128 x 128 tile
+// (128 vs 64), which is what the per-CU LDS-DMA rate bounds on these layers (≈36 GB/s per CU measured on the
+// 256 x 128 kernel). 64-byte LDS rows; the 16-byte granule g of row r sits in slot g ^ ((r >> 1) & 3): the
+// ds_read_b128 fragment reads (16 rows x 4 granules per 16-lane group) then hit 16 distinct bank quads. All LDS is
+// one __shared__ array (a second object can make hipcc drain vmcnt before the first ds_read).
+// SPLIT: blockIdx.y is a K split of ksteps_per_split K-steps; the accumulators go to fp32 partials
+// ws[split][M][Ncol] and conv_splitk_epilogue_kernel applies the fused epilogue after summing them.
+// ------------------------------------------------------------------------------------------------
+template <int MI, int NI, int TM, int TN, int NH>
+__device__ __forceinline__ void store_partials_lds(float* __restrict__ ws, int M, int Ncol, v4f (&acc)[MI][NI],
+                                                   int mbase, int nbase, int lane, float* wl) {
+  constexpr int GR = TN / 4, LPR = TN / 8, PPI = 64 / LPR, NR = TM / PPI, MIH = MI / NH, NRH = NR / NH;
+  auto gpos = [](int p, int g) { return (p * GR + (g ^ (p & (GR - 1)))) * 4; };
+  const int q = lane % LPR;
+  const int n = nbase + q * 8;
+#pragma unroll
+  for (int h = 0; h < NH; ++h) {
+#pragma unroll
+    for (int i = 0; i < MIH; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j)
+        *reinterpret_cast<v4f*>(wl + gpos(i * 16 + (lane & 15), j * 4 + (lane >> 4))) = acc[h * MIH + i][j];
+    __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): wave-private slice
+#pragma unroll
+    for (int rr = 0; rr < NRH; ++rr) {
+      const int p = rr * PPI + lane / LPR;
+      const int m = mbase + h * (TM / NH) + p;
+      const v4f lo = *reinterpret_cast<const v4f*>(wl + gpos(p, 2 * q));
+      const v4f hi = *reinterpret_cast<const v4f*>(wl + gpos(p, 2 * q + 1));
+      if (m < M && n < Ncol) {
+        float* o = ws + (size_t)m * Ncol + n;
+        *reinterpret_cast<v4f*>(o) = lo;
+        *reinterpret_cast<v4f*>(o + 4) = hi;
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);   // the slice is rewritten by the next chunk
+  }
+}
+
+template <bool SPLIT>
+__global__ __launch_bounds__(512, 1) void conv_nt_w8_kernel(ConvArgs a) {
+  constexpr int BM = 256, BN = 256, BKS = 32, NS = 4;
+  constexpr int WGM = 2, WGN = 4;
+  constexpr int TM = BM / WGM, TN = BN / WGN;      // 128 x 64 per wave
+  constexpr int MI = TM / 16, NI = TN / 16;        // 8 x 4 MFMA tiles
+  constexpr int STAGE = (BM + BN) * BKS;           // 16384 bf16 = 32 KB
+  constexpr int L = 4;                             // DMA instructions per thread per stage (2 A + 2 B)
+  constexpr int NH = SPLIT ? 2 : 4;                 // epilogue row chunks (4: fewer live prefetch registers)
+  constexpr int SL = (TM / NH) * TN;
+  static_assert(8 * SL * 4 <= NS * STAGE * 2, "epilogue chunk must fit the stages");
+  // the tap table lives behind the stages: indexing the kernarg copy with a run-time tap makes hipcc emit VECTOR
+  // loads of it and a vmcnt(0) before their use, which would drain the DMA pipeline every K-step
+  __shared__ __attribute__((aligned(1024))) bf16_t lds[NS * STAGE + 3 * CONV_MAX_TAPS];
+  short* taps = reinterpret_cast<short*>(lds + NS * STAGE);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WGN, wn = wave % WGN;
+  const int tiles_n = (a.Ncol + BN - 1) / BN;
+  const int tiles_m = (a.M + BM - 1) / BM;
+  const int nwg = tiles_m * tiles_n;
+  const int bid = xcd_remap(blockIdx.x, nwg);
+  const int tm = bid / tiles_n, tn = bid % tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int nk_all = a.Kdim / BKS;
+  int kt0 = 0, nk = nk_all;
+  if constexpr (SPLIT) {
+    const int per = (nk_all + a.ksplit - 1) / a.ksplit;
+    kt0 = blockIdx.y * per;
+    nk = min(nk_all, kt0 + per) - kt0;
+  }
+
+  // DMA geometry: instruction j of wave w fills rows (j * 8 + w) * 16 .. +16 (64 B each, 4 granules); lane -> row
+  // + (lane >> 2), slot lane & 3, which must hold granule (lane & 3) ^ ((row >> 1) & 3)
+  const int rsub = lane >> 2;
+  const int gsrc = (lane & 3) ^ ((rsub >> 1) & 3);
+  int a_pix[2], a_h[2], a_w[2];
+  const int ohw = a.OH * a.OW;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int m = m0 + (j * 8 + wave) * 16 + rsub;
+    if (m < a.M) {
+      const int nb = m / ohw, rem = m - nb * ohw;
+      const int oh = rem / a.OW, ow = rem - oh * a.OW;
+      a_pix[j] = nb * a.Hs * a.Ws;
+      a_h[j] = oh * a.mul_h;
+      a_w[j] = ow * a.mul_w;
+    } else {
+      a_pix[j] = 0; a_h[j] = -(1 << 28); a_w[j] = -(1 << 28);
+    }
+  }
+  const bf16_t* wrow[2];
+  bool bvalid[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int n = n0 + (j * 8 + wave) * 16 + rsub;
+    bvalid[j] = n < a.Ncol;
+    wrow[j] = a.wt + (size_t)(bvalid[j] ? n : 0) * a.ldw + gsrc * 8;
+  }
+  if (tid < a.ntaps) {
+    taps[tid] = a.tap_h[tid];
+    taps[CONV_MAX_TAPS + tid] = a.tap_w[tid];
+    taps[2 * CONV_MAX_TAPS + tid] = a.tap_k[tid];
+  }
+  __syncthreads();   // tap table visible (no DMA outstanding yet)
+
+  auto issue = [&](int kt, int buf) {
+    const int k0 = kt * BKS;
+    const int t = k0 / a.Cs;
+    const int cin = k0 - t * a.Cs;
+    const int th = taps[t], tw = taps[CONV_MAX_TAPS + t];
+    const int wk = taps[2 * CONV_MAX_TAPS + t] * a.Cs + cin;
+    const int c = cin + gsrc * 8;
+    bf16_t* A = lds + buf * STAGE;
+    bf16_t* B = A + BM * BKS;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int ch = a_h[j] + th, cw = a_w[j] + tw;
+      const bool ok = (unsigned)ch < (unsigned)a.Hs && (unsigned)cw < (unsigned)a.Ws;
+      const bf16_t* src = ok ? a.src + (unsigned)((a_pix[j] + ch * a.Ws + cw) * a.Cs + c) : g_zero_granule;
+      glds16(src, (LDS_PTR(void))(A + (j * 8 + wave) * 16 * BKS));
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const bf16_t* src = bvalid[j] ? wrow[j] + wk : g_zero_granule;
+      glds16(src, (LDS_PTR(void))(B + (j * 8 + wave) * 16 * BKS));
+    }
+  };
+  // fragment of rows row0 .. row0 + 15: lane reads row row0 + (lane & 15), K granule lane >> 4
+  const int foff = (lane & 15) * BKS + ((((lane >> 4) ^ ((lane >> 1) & 3))) << 3);
+
+  v4f acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+
+  // prologue: K-steps 0, 1, 2 in flight; retire step 0
+  if (nk > 0) issue(kt0, 0);
+  if (nk > 1) issue(kt0 + 1, 1);
+  if (nk > 2) issue(kt0 + 2, 2);
+  if (nk > 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * L) : "memory");
+  else if (nk > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(L) : "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 3;
+    // stage (kt + 3) & 3 == (kt - 1) & 3 was last read in step kt - 1, before the barrier that ended it
+    if (kt + 3 < nk) issue(kt0 + kt + 3, (kt + 3) & 3);
+    const bf16_t* A = lds + cur * STAGE;
+    const bf16_t* B = A + BM * BKS;
+    v8s fa[MI], fb[NI];
+#pragma unroll
+    for (int j = 0; j < NI; ++j) fb[j] = *reinterpret_cast<const v8s*>(B + (wn * TN + j * 16) * BKS + foff);
+#pragma unroll
+    for (int i = 0; i < MI; ++i) fa[i] = *reinterpret_cast<const v8s*>(A + (wm * TM + i * 16) * BKS + foff);
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+    // retire step kt + 1 (steps kt + 2, kt + 3 stay in flight), make every wave's reads of this stage and every
+    // wave's step-(kt + 1) DMA ordered before anything after the barrier
+    const int ahead = min(nk - 1, kt + 3) - (kt + 1);
+    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(2 * L) : "memory");
+    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(L) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+  float* wl = reinterpret_cast<float*>(lds) + wave * SL;
+  if constexpr (SPLIT) {
+    store_partials_lds<MI, NI, TM, TN, NH>(a.ws + (size_t)blockIdx.y * a.M * a.Ncol, a.M, a.Ncol, acc,
+                                           m0 + wm * TM, n0 + wn * TN, lane, wl);
+  } else {
+    nt_epilogue_lds<MI, NI, TM, TN, NH, WGN * SL, WGM>(a, acc, m0 + wm * TM, n0 + wn * TN, lane, bid, wl, wm);
+  }
+}
+
+// Grid of the split-K epilogue: (row blocks, 256-group channel chunks), ~8 rows per thread, <= 8192 blocks.
+dim3 splitk_grid(long P, int C, long* rpb_out) {
+  const int G = C >> 3;
+  const int rpi = 256 / (G < 256 ? G : 256);
+  const int gy = (G + 255) / 256;
+  long rpb = (long)rpi * 8;
+  long bx = (P + rpb - 1) / rpb;
+  const long cap = 8192 / gy;
+  if (bx > cap) {
+    bx = cap;
+    rpb = (P + bx - 1) / bx;
+  }
+  if (bx < 1) bx = 1;
+  *rpb_out = rpb;
+  return dim3((unsigned)bx, (unsigned)gy);
+}
+
+// Split-K epilogue: out = fused_epilogue(sum over splits of ws[s][m][n]) with exactly nt_epilogue_lds's semantics
+// (+ bias, + addend, ReLU, bf16 store at the output placement, BN statistics of the rounded output or the consumer
+// BN's backward reduction). Channel-stationary: a thread owns 8 channels of rows rsub, rsub + rpi, ...; per-channel
+// sums are combined across the block's rows in LDS and added into the statistics slots with one atomic each.
+__global__ __launch_bounds__(256) void conv_splitk_epilogue_kernel(ConvArgs a, long rpb) {
+  __shared__ float sm[256 * 16];
+  const int G = a.Ncol >> 3;
+  const int gbase = blockIdx.y * 256;
+  const int gcount = min(256, G - gbase);
+  const int rpi = 256 / gcount;
+  const int g = gbase + threadIdx.x % gcount, rsub = threadIdx.x / gcount;
+  const bool act = rsub < rpi;
+  const long rbeg = blockIdx.x * rpb, rend = min((long)a.M, rbeg + rpb);
+  const int n = g * 8;
+  const size_t plane = (size_t)a.M * a.Ncol;
+  const int ohw = a.OH * a.OW;
+  float bs[8], bmu[8], bsc[8], bsh[8], s1[8], s2[8];
+  const bool bnw = a.bnred && !a.stats;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    bs[e] = (act && a.bias) ? a.bias[n + e] : 0.f;
+    bmu[e] = (act && bnw) ? a.bnmean[n + e] : 0.f;
+    bsc[e] = (act && bnw && a.bnaff) ? a.bnaff[n + e] : 0.f;
+    bsh[e] = (act && bnw && a.bnaff) ? a.bnaff[a.Ncol + n + e] : 0.f;
+    s1[e] = s2[e] = 0.f;
+  }
+  if (act) {
+    for (long m = rbeg + rsub; m < rend; m += rpi) {
+      float v[8];
+      const float* p = a.ws + (size_t)m * a.Ncol + n;
+      {
+        const v4f lo = *reinterpret_cast<const v4f*>(p), hi = *reinterpret_cast<const v4f*>(p + 4);
+        v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3]; v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
+      }
+      for (int s = 1; s < a.ksplit; ++s) {
+        const v4f lo = *reinterpret_cast<const v4f*>(p + s * plane), hi = *reinterpret_cast<const v4f*>(p + s * plane + 4);
+        v[0] += lo[0]; v[1] += lo[1]; v[2] += lo[2]; v[3] += lo[3]; v[4] += hi[0]; v[5] += hi[1]; v[6] += hi[2]; v[7] += hi[3];
+      }
+      long orow = m;
+      if (!a.ident_out) {
+        const int nb = (int)(m / ohw), rem = (int)(m - (long)nb * ohw);
+        const int oh = rem / a.OW, ow = rem - oh * a.OW;
+        orow = ((long)nb * a.OHo + oh * a.omul_h + a.ooff_h) * a.OWo + ow * a.omul_w + a.ooff_w;
+      }
+      const size_t off = (size_t)orow * a.ldo + n;
+      if (a.addend) {
+        const v4u q = *reinterpret_cast<const v4u*>(a.addend + off);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { v[2 * e] += lo_bf(q[e]); v[2 * e + 1] += hi_bf(q[e]); }
+      }
+      v4u o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float x0 = v[2 * e] + bs[2 * e], x1 = v[2 * e + 1] + bs[2 * e + 1];
+        if (a.relu) { x0 = fmaxf(x0, 0.f); x1 = fmaxf(x1, 0.f); }
+        o[e] = pack2bf(x0, x1);
+      }
+      if (a.stats) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float y0 = lo_bf(o[e]), y1 = hi_bf(o[e]);
+          s1[2 * e] += y0; s2[2 * e] += y0 * y0;
+          s1[2 * e + 1] += y1; s2[2 * e + 1] += y1 * y1;
+        }
+      } else if (bnw) {
+        const v4u px = *reinterpret_cast<const v4u*>(a.bnx + off);
+        v4u pz = v4u{0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
+        if (a.bnz) pz = *reinterpret_cast<const v4u*>(a.bnz + off);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float d0 = lo_bf(o[e]), d1 = hi_bf(o[e]);
+          const float x0 = lo_bf(px[e]), x1 = hi_bf(px[e]);
+          if (a.bnz) {
+            if (!(lo_bf(pz[e]) > 0.f)) d0 = 0.f;
+            if (!(hi_bf(pz[e]) > 0.f)) d1 = 0.f;
+          } else if (a.bnaff) {
+            if (!(x0 * bsc[2 * e] + bsh[2 * e] > 0.f)) d0 = 0.f;
+            if (!(x1 * bsc[2 * e + 1] + bsh[2 * e + 1] > 0.f)) d1 = 0.f;
+          }
+          s1[2 * e] += d0; s2[2 * e] += d0 * (x0 - bmu[2 * e]);
+          s1[2 * e + 1] += d1; s2[2 * e + 1] += d1 * (x1 - bmu[2 * e + 1]);
+        }
+      }
+      *reinterpret_cast<v4u*>(a.out + off) = o;
+    }
+  }
+  float* const red = a.stats ? a.stats : a.bnred;
+  if (red == nullptr) return;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { sm[threadIdx.x * 16 + e] = s1[e]; sm[threadIdx.x * 16 + 8 + e] = s2[e]; }
+  __syncthreads();
+  for (int w = threadIdx.x; w < gcount * 16; w += 256) {
+    const int gg = w >> 4, slot = w & 15;
+    float t = 0.f;
+    for (int rs = 0; rs < rpi; ++rs) t += sm[(rs * gcount + gg) * 16 + slot];
+    const int ch = (gbase + gg) * 8 + (slot & 7);
+    atomicAdd(red + (size_t)(blockIdx.x & (BIGDL_STAT_SLOTS - 1)) * 2 * a.Ncol + (slot < 8 ? 0 : a.Ncol) + ch, t);
+  }
+}
+
 template <int BM, int BN, int WM>
 void launch_nt(const ConvArgs& a, bool fastk, hipStream_t st) {
   const int nwg = ((a.M + BM - 1) / BM) * ((a.Ncol + BN - 1) / BN);
@@ -1331,6 +1630,21 @@ void launch_nt_p3(const ConvArgs& a, hipStream_t st) {
 // BIGDL_CONV_IMPL: 3 = persistent LDS-DMA kernel (next tile's loads overlap the epilogue) on grids of more
 // than two tiles per CU, 2 = deep-pipelined 256-pixel kernel on grids that fill the chip,
 // 1 (default) = LDS-DMA kernel where Cs % 64 == 0, 0 = register-staged kernel everywhere.
+// 256 x 256 8-wave kernel (BIGDL_CONV_W8=0 disables it): fast-K over 32-channel steps, aligned bf16 output, at
+// least 256 output channels, at least 4 K-steps of 32. Returns 0 (not picked) or the K split (1 = none): grids below
+// one workgroup per CU are split along K (>= 8 K-steps per split) so every CU gets work.
+static int w8_pick(const ConvArgs* a) {
+  static const int on = [] { const char* e = getenv("BIGDL_CONV_W8"); return e ? atoi(e) : 0; }();
+  if (!on || a->out32 || (a->Cs % 32) || (a->Ncol & 7) || (a->ldo & 7) || a->Ncol < 256 || a->Kdim < 128) return 0;
+  const long tiles = (long)((a->M + 255) / 256) * ((a->Ncol + 255) / 256);
+  const int nk = a->Kdim / 32;
+  if (tiles >= 200 || on == 2) return 1;
+  int split = (int)((320 + tiles - 1) / tiles);
+  split = std::min(split, std::max(1, nk / 8));
+  split = std::min(split, 8);
+  return std::max(split, 1);
+}
+
 int g_conv_impl = -1;
 int conv_impl() {
   if (g_conv_impl < 0) {
@@ -1348,6 +1662,17 @@ void bigdl_set_conv_impl(int impl) { g_conv_impl = impl; }
 int bigdl_get_conv_impl() { return conv_impl(); }
 
 // Forward or data-gradient implicit GEMM. Returns 0 on success, negative on unsupported shapes.
+long bigdl_conv_nt_plan(ConvArgs* a) {
+  a->ksplit = 0;
+  if (a->Cs % 8 != 0 || a->M <= 0 || conv_impl() < 1) return 0;
+  const int k = w8_pick(a);
+  if (k > 1) {
+    a->ksplit = k;
+    return (long)k * a->M * a->Ncol;
+  }
+  return 0;
+}
+
 int bigdl_conv_nt(const ConvArgs* a, hipStream_t st) {
   if (a->Cs % 8 != 0 || a->Kdim != a->ntaps * a->Cs || a->ntaps < 1 || a->ntaps > CONV_MAX_TAPS) return -1;
   // the BN-backward reduction lives in the LDS-transposed epilogue only
@@ -1364,7 +1689,17 @@ int bigdl_conv_nt(const ConvArgs* a, hipStream_t st) {
   // 8-wave deep-pipelined kernel (tools/bench_conv.py, impl 1 vs 2); BIGDL_CONV_P3AUTO=0 keeps them on impl 1
   static const bool p3auto = [] { const char* e = getenv("BIGDL_CONV_P3AUTO"); return e ? atoi(e) != 0 : true; }();
   const bool p3_pick = impl == 2 || (impl == 1 && p3auto && a->M <= 50176 && a->Kdim >= 1024);
-  if (fastk && p3_pick && p3_tiles >= 256) {
+  const int w8 = impl == 1 ? w8_pick(a) : 0;
+  if (w8 > 1 && a->ksplit == w8 && a->ws != nullptr) {
+    const int nwg = ((a->M + 255) / 256) * ((a->Ncol + 255) / 256);
+    conv_nt_w8_kernel<true><<<dim3(nwg, w8), dim3(512), 0, st>>>(*a);
+    long rpb = 0;
+    const dim3 grid = splitk_grid(a->M, a->Ncol, &rpb);
+    conv_splitk_epilogue_kernel<<<grid, dim3(256), 0, st>>>(*a, rpb);
+  } else if (w8 == 1) {
+    const int nwg = ((a->M + 255) / 256) * ((a->Ncol + 255) / 256);
+    conv_nt_w8_kernel<false><<<dim3(nwg), dim3(512), 0, st>>>(*a);
+  } else if (fastk && p3_pick && p3_tiles >= 256) {
     if (a->Ncol <= 64) launch_nt_p3<64, 8, 1>(*a, st);
     else launch_nt_p3<128, 4, 2>(*a, st);
   } else if (fastk && impl == 3 && aligned_out && tiles128 > 2 * 256) {

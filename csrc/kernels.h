@@ -37,6 +37,10 @@ struct ConvArgs {
   // layers computed as an NT GEMM over transposed operands (LDS-transposed epilogue only; no stats / bn / relu)
   float* out32;
   int accum32;
+  // split-K (256 x 256 kernel on grids that do not fill the chip): fp32 partials [ksplit][M][Ncol] in ws, summed
+  // by the split-K epilogue kernel, which applies everything the fused epilogue would (bigdl_conv_nt_plan sets them)
+  float* ws;
+  int ksplit;
 };
 
 struct WgradArgs {
@@ -54,6 +58,8 @@ struct WgradArgs {
 
 extern "C" {
 int bigdl_conv_nt(const ConvArgs* a, hipStream_t st);
+// Kernel choice for bigdl_conv_nt: sets a->ksplit and returns the fp32 workspace elements it needs (0: none).
+long bigdl_conv_nt_plan(ConvArgs* a);
 int bigdl_conv_wgrad(const WgradArgs* a, hipStream_t st);
 // Split-K plan for the weight gradient: fills m_per_split / splits; returns the workspace size in floats
 // (0 when the single-split path accumulates straight into dw).

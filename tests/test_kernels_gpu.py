@@ -528,3 +528,58 @@ def test_train_step_with_batched_transposes_matches_per_layer(monkeypatch):
         if mode == "batched":
             assert cv.DESC_BUILDS[0] - builds == 1      # one descriptor table for all steps (graph-capture safe)
     assert _rel(grads["batched"], grads["per_layer"]) < 1e-6
+
+
+W8_CASES = [
+    # N, C, H, K, R, stride, pad -> routed to the 256 x 256 8-wave kernel (Cs % 32 == 0, Ncol >= 256)
+    (16, 256, 56, 256, 1, 1, 0),     # 196 tiles x 8 K-steps: one pass, no split
+    (16, 256, 28, 512, 3, 1, 1),     # 98 tiles x 72 K-steps: split-K 4 + split-K epilogue
+    (4, 512, 7, 2048, 1, 1, 0),      # 8 tiles: split-K 2
+    (8, 128, 28, 320, 3, 1, 1),      # Ncol tail (320 % 256 != 0)
+    (16, 256, 28, 256, 3, 2, 1),     # stride 2: dgrad phases write a strided output placement
+    (66, 256, 28, 256, 1, 1, 0),     # >= 200 tiles, M tail
+]
+
+
+@pytest.mark.parametrize("case", W8_CASES)
+def test_conv_w8_kernel_fwd_dgrad_bnred(case):
+    """256 x 256 8-wave LDS-DMA kernel (4 stages, counted vmcnt) and its split-K path vs fp32 torch: forward with
+    bias + BN statistics and with bias + ReLU, data gradient with a residual addend and the fused backward
+    reduction of the consumer BatchNorm (sum dy, sum dy * (x - mean) under the ReLU mask)."""
+    from bigdl_amd.ops import bn as bnops
+    from bigdl_amd.ops import conv as cv
+
+    N, C, H, K, R, st, pd = case
+    torch.manual_seed(5)
+    dev = _dev()
+    x = torch.randn(N, C, H, H, device=dev).to(BF, memory_format=CL)
+    w = (torch.randn(K, C, R, R, device=dev) * (1.0 / (C * R * R) ** 0.5)).to(BF, memory_format=CL)
+    b32 = torch.randn(K, device=dev)
+    stats = bnops.new_stats(K, dev)
+    y = cv.conv2d_fwd(x, w, b32, (st, st), (pd, pd), stats=stats)
+    yr = F.conv2d(x.float(), w.float(), b32, stride=st, padding=pd)
+    assert _rel(y, yr) < 1e-2
+    st2 = stats.view(bnops.stat_slots(), 2, K).sum(0)
+    assert _rel(st2[0], y.float().sum(dim=(0, 2, 3))) < 1e-3
+    assert _rel(st2[1], (y.float() ** 2).sum(dim=(0, 2, 3))) < 1e-3
+    y2 = cv.conv2d_fwd(x, w, b32, (st, st), (pd, pd), relu=True)
+    assert _rel(y2, torch.relu(yr)) < 1e-2
+    # data gradient (+ residual addend, + consumer-BN backward reduction with the ReLU mask from x*scale+shift)
+    gy = torch.randn_like(yr).to(BF, memory_format=CL)
+    add = torch.randn(N, C, H, H, device=dev).to(BF, memory_format=CL)
+    bx = torch.randn(N, C, H, H, device=dev).to(BF, memory_format=CL)
+    mean = torch.randn(C, device=dev) * 0.1
+    aff = torch.cat([torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev) * 0.2])
+    red = bnops.new_stats(C, dev)
+    bn = {"x": bx, "z": None, "mean": mean, "aff": aff, "red": red}
+    dx = cv.conv2d_dgrad(gy, cv.transpose_w(w), x.shape, (st, st), (pd, pd), addend=add, bn=bn)
+    dxr = torch.nn.grad.conv2d_input(x.shape, w.float(), gy.float(), stride=st, padding=pd) + add.float()
+    assert _rel(dx, dxr) < 1e-2
+    if bn.get("done"):
+        d = dx.float()
+        xf = bx.float()
+        mask = (xf * aff[:C].view(1, C, 1, 1) + aff[C:].view(1, C, 1, 1)) > 0
+        dm = d * mask
+        r2 = red.view(bnops.stat_slots(), 2, C).sum(0)
+        assert _rel(r2[0], dm.sum(dim=(0, 2, 3))) < 1e-3
+        assert _rel(r2[1], (dm * (xf - mean.view(1, C, 1, 1))).sum(dim=(0, 2, 3))) < 1e-3
