@@ -156,7 +156,47 @@ class SpatialConvolution(TensorModule):
             w16 = cv.weight_krsc_bf16(w16.float())
         return w16
 
+    def _pair_path(self, x):
+        return (cv.pair_ok(x.shape[1], (self.strideH, self.strideW), (self.dilationH, self.dilationW), self.nGroup)
+                and self.nInputPlane == x.shape[1] and getattr(self, "_fuse_out", None) is None
+                and getattr(self, "_fuse_addend", None) is None)
+
+    def _fwd_gpu_pairs(self, x, ph, pw):
+        """<= 4 input channels, width stride 2 (image stems): pixel-pair packed implicit GEMM (ops/conv.py,
+        csrc/stem.hip) — 2 width taps per 16-byte granule instead of 1 pixel padded to 8 channels."""
+        R, S, sh = self.kernelH, self.kernelW, self.strideH
+        OH, OW, S2, _, _ = cv.pair_geometry(x.shape[2], x.shape[3], R, S, sh, ph, pw)
+        xp = cv.to_pairs_bf16(x, R, S, sh, ph, pw)
+        self._xpair = (xp, tuple(x.shape), ph, pw)
+        self._x16 = None
+        wp = cv.pair_weight(self.w16("weight"))
+        stats = None
+        if self.emit_stats and self.train and self.nOutputPlane % 8 == 0:
+            stats = bnops.new_stats(self.nOutputPlane, x.device)
+        y = cv.conv2d_pairs_fwd(xp, wp, self.bias, self.nOutputPlane, OH, OW, R, S2, sh, relu=self.fuse_relu,
+                                stats=stats)
+        if stats is not None:
+            y._bn_stats = stats
+        self._geom = (x.shape, ph, pw)
+        return y
+
+    def _wgrad_gpu_pairs(self, x, gy16):
+        xp, shape, ph, pw = self._xpair
+        R, S, K = self.kernelH, self.kernelW, self.nOutputPlane
+        S2 = (S + 1) // 2
+        dwp = torch.zeros(K, R * S2 * 8, device=x.device)
+        db = None
+        if self.bias is not None:
+            db = self.gradBias if self.scaleB == 1.0 else torch.zeros(K, device=x.device)
+        cv.conv2d_pairs_wgrad(gy16, xp, R, S2, self.strideH, dwp, db)
+        ops.native.get().pair_wgrad_add(dwp, self.gradWeight, float(self.scaleW))
+        if db is not None and db is not self.gradBias:
+            self.gradBias.add_(db, alpha=self.scaleB)
+
     def _fwd_gpu(self, x, ph, pw):
+        self._xpair = None
+        if self._pair_path(x) and self.nOutputPlane % 8 == 0:
+            return self._fwd_gpu_pairs(x, ph, pw)
         x16 = cv.to_nhwc_bf16(x)
         self._x16 = x16
         w16 = self._w16_padded()
@@ -312,6 +352,11 @@ class SpatialConvolution(TensorModule):
 
     def _wgrad_gpu(self, x, gy, ph, pw):
         gy16 = gy if (gy.dtype == BF16 and gy.is_contiguous(memory_format=CL)) else gy.to(BF16, memory_format=CL)
+        xpair = getattr(self, "_xpair", None)
+        if (xpair is not None and xpair[1] == tuple(x.shape) and xpair[2:] == (ph, pw) and self.nGroup == 1
+                and self.gradWeight.dtype == torch.float32):
+            self._wgrad_gpu_pairs(x, gy16)
+            return
         x16 = getattr(self, "_x16", None)
         if x16 is None or x16.shape[0] != x.shape[0] or x16.shape[2:] != x.shape[2:]:
             x16 = cv.to_nhwc_bf16(x)
@@ -359,6 +404,7 @@ class SpatialConvolution(TensorModule):
     def clearState(self):
         super().clearState()
         self._x16 = None
+        self._xpair = None
         return self
 
     def __repr__(self):

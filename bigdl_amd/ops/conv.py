@@ -294,6 +294,71 @@ def gemm_wgrad_nt(dy2d, x2d, dw32, dbias32=None):
         native.get().colsum_bf16(dy2d, dbias32)
 
 
+# ------------------------------------------------------------------------------------------------
+# Pixel-pair packing for <= 4-channel convolutions with width stride 2 (image stems; csrc/stem.hip): the zero-padded
+# image is stored NHWC4 and viewed as [N][Hp][Wp/2][8] pixel pairs, so one 16-byte granule carries two width taps.
+# ------------------------------------------------------------------------------------------------
+def pair_ok(C, stride, dil, groups):
+    import os
+
+    return (groups == 1 and C <= 4 and stride[1] == 2 and tuple(dil) == (1, 1)
+            and os.environ.get("BIGDL_CONV_PAIR", "1") != "0")
+
+
+def pair_geometry(H, W, R, S, sh, ph, pw):
+    """(OH, OW, S2, Hp, Wp) of the pair view: padded image rows / columns (Wp even) covering every tap."""
+    OH, OW = out_size(H, R, sh, ph), out_size(W, S, 2, pw)
+    S2 = (S + 1) // 2
+    Hp = max(H + 2 * ph, (OH - 1) * sh + R)
+    Wp = max(2 * (OW - 1 + S2), W + 2 * pw)
+    return OH, OW, S2, Hp, Wp + (Wp & 1)
+
+
+def to_pairs_bf16(x, R, S, sh, ph, pw):
+    N, C, H, W = x.shape
+    _, _, _, Hp, Wp = pair_geometry(H, W, R, S, sh, ph, pw)
+    y = torch.empty((N, Hp, Wp // 2, 8), dtype=BF16, device=x.device)
+    xf = x if (x.dtype == torch.float32 and x.is_contiguous()) else x.float().contiguous()
+    native.get().nchw_to_pairs(xf, y, ph, pw)
+    return y
+
+
+def pair_weight(w16):
+    """(K, C, R, S) bf16 weight -> (K, R * S2 * 8) pair-packed weight (csrc/stem.hip)."""
+    K, C, R, S = w16.shape
+    wp = torch.empty((K, R * ((S + 1) // 2) * 8), dtype=BF16, device=w16.device)
+    native.get().pair_weight(w16, wp)
+    return wp
+
+
+def _pair_taps(R, S2):
+    key = ("p", R, S2)
+    t = _TAP_CACHE.get(key)
+    if t is None:
+        t = []
+        for r in range(R):
+            for j in range(S2):
+                t += [r, j, r * S2 + j]
+        _TAP_CACHE[key] = t
+    return t
+
+
+def conv2d_pairs_fwd(xp, wp, bias, K, OH, OW, R, S2, sh, relu=False, stats=None):
+    N, Hp, Wq, _ = xp.shape
+    out = torch.empty((N, K, OH, OW), dtype=BF16, device=xp.device, memory_format=CL)
+    geo = [N, Hp, Wq, 8, OH, OW, sh, 1, R * S2 * 8, K, K, OH, OW, 1, 1, 0, 0]
+    native.get().conv_nt(xp, wp, out, bias, stats, geo, _pair_taps(R, S2), relu, None)
+    return out
+
+
+def conv2d_pairs_wgrad(dy, xp, R, S2, sh, dwp32, dbias32):
+    """dW' (fp32 (K, R * S2 * 8)) += weight gradient of the pair view; dbias += sum(dy)."""
+    N, Hp, Wq, _ = xp.shape
+    _, K, OH, OW = dy.shape
+    geo = [N, Hp, Wq, 8, OH, OW, R, S2, sh, 1, 0, 0, 1, 1, N * OH * OW, K, R * S2 * 8, K]
+    native.get().conv_wgrad(dy, xp, dwp32, dbias32, geo)
+
+
 def conv2d_wgrad(dy, x, dw32, dbias32, stride, pad, dil=(1, 1)):
     """dW (fp32, (K, C, R, S) channels_last buffer) += conv weight gradient; dbias += sum(dy)."""
     N, C, H, W = x.shape

@@ -49,9 +49,15 @@ class AllReduceParameter:
         self.shard = self.padded // self.world
         self.start = self.rank * self.shard
         self.end = self.start + self.shard
-        if compress not in (None, "bf16", "fp16"):
-            raise ValueError(f"unsupported gradient compression {compress!r} (None or 'bf16')")
-        self.compress = "bf16" if compress == "fp16" else compress  # reference "fp16" = bf16 truncation
+        if compress in ("none", "fp32"):
+            compress = None
+        if compress not in (None, "bf16", "fp16", "fp16-truncate", "bf16-rtz"):
+            raise ValueError(f"unsupported gradient compression {compress!r} (None, 'bf16' or 'fp16')")
+        # "fp16" (the reference's bigdl.compress value) is its FP16CompressedTensor: the upper 16 bits of each fp32,
+        # i.e. bf16 by truncation (S/parameters/FP16CompressedTensor.scala:271-279) — kept bit-exact here as a
+        # parity mode; "bf16" rounds to nearest even (half the error, the default for new jobs)
+        self.rtz = compress in ("fp16", "fp16-truncate", "bf16-rtz")
+        self.compress = "bf16" if compress is not None else None
         self._g16 = None
         # run the collectives even on one rank (BIGDL_FORCE_COLLECTIVES=1): exercises the RCCL path and its HIP
         # graph capture on a single GPU
@@ -109,7 +115,7 @@ class AllReduceParameter:
         op = dist.ReduceOp.AVG if average and self._avg_ok() else dist.ReduceOp.SUM
         if self.compress == "bf16":
             g16 = self._bf16_buf(g)
-            _cast_f32_bf16(g[lo:hi], g16[lo:hi])
+            (_cast_f32_bf16_rtz if self.rtz else _cast_f32_bf16)(g[lo:hi], g16[lo:hi])
             c16 = g16[lo + self.rank * n: lo + (self.rank + 1) * n]
             work = self._rs(c16, g16[lo:hi], op, async_op=async_op)
             return _Post(work, lambda: (_cast_bf16_f32(c16, chunk), self._fix_avg(chunk, op, average))), chunk
@@ -215,6 +221,13 @@ def _cast_f32_bf16(src, dst):
         _native().cast_f32_bf16(src, dst)
     else:
         dst.copy_(src)
+
+
+def _cast_f32_bf16_rtz(src, dst):
+    """bf16 by truncation (drop the low 16 mantissa bits), the reference FP16CompressedTensor encoding."""
+    from ..ops.nnk import f32_to_bf16_rtz
+
+    f32_to_bf16_rtz(src, out=dst)
 
 
 def _cast_bf16_f32(src, dst):

@@ -178,6 +178,28 @@ void nchw_to_nhwc(const Tensor& x, const Tensor& y, int64_t Cp) {
   TORCH_CHECK(y.numel() == (int64_t)N * H * W * Cp && Cp >= C && Cp % 8 == 0, "nchw_to_nhwc: y size / Cp % 8");
   bigdl_nchw_f32_to_nhwc_bf16(cf(x, "x"), mbf(y, "y"), N, C, H, W, (int)Cp, stream());
 }
+void nchw_to_pairs(const Tensor& x, const Tensor& y, int64_t ph, int64_t pw) {
+  TORCH_CHECK(x.dim() == 4 && x.is_contiguous() && x.size(1) <= 4, "nchw_to_pairs: x must be contiguous NCHW, C <= 4");
+  TORCH_CHECK(y.dim() == 4 && y.is_contiguous() && y.size(3) == 8 && y.size(0) == x.size(0), "nchw_to_pairs: y shape");
+  const int Hp = y.size(1), Wp = 2 * y.size(2);
+  TORCH_CHECK(Hp >= x.size(2) + ph && Wp >= x.size(3) + pw, "nchw_to_pairs: padded image too small");
+  bigdl_nchw_to_pairs(cf(x, "x"), mbf(y, "y"), x.size(0), x.size(1), x.size(2), x.size(3), Hp, Wp, (int)ph, (int)pw,
+                      stream());
+}
+void pair_weight(const Tensor& w, const Tensor& wp) {
+  TORCH_CHECK(w.dim() == 4 && w.size(1) <= 4, "pair_weight: w must be (K, C<=4, R, S)");
+  const int K = w.size(0), C = w.size(1), R = w.size(2), S = w.size(3), S2 = (S + 1) / 2;
+  TORCH_CHECK(wp.numel() == (int64_t)K * R * S2 * 8 && wp.is_contiguous(), "pair_weight: wp size");
+  const long st[4] = {(long)w.stride(0), (long)w.stride(1), (long)w.stride(2), (long)w.stride(3)};
+  bigdl_pair_weight(cbf(w, "w"), mbf(wp, "wp"), K, C, R, S, st, stream());
+}
+void pair_wgrad_add(const Tensor& dwp, const Tensor& gw, double scale) {
+  TORCH_CHECK(gw.dim() == 4 && gw.size(1) <= 4, "pair_wgrad_add: gw must be (K, C<=4, R, S)");
+  const int K = gw.size(0), C = gw.size(1), R = gw.size(2), S = gw.size(3), S2 = (S + 1) / 2;
+  TORCH_CHECK(dwp.numel() == (int64_t)K * R * S2 * 8 && dwp.is_contiguous(), "pair_wgrad_add: dwp size");
+  const long st[4] = {(long)gw.stride(0), (long)gw.stride(1), (long)gw.stride(2), (long)gw.stride(3)};
+  bigdl_pair_wgrad_add(cf(dwp, "dwp"), mf(gw, "gw"), K, C, R, S, st, (float)scale, stream());
+}
 void cast_f32_bf16(const Tensor& x, const Tensor& y) {
   TORCH_CHECK(x.numel() == y.numel() && x.is_contiguous() && y.is_contiguous(), "cast: size");
   bigdl_cast_f32_bf16(cf(x, "x"), mbf(y, "y"), x.numel(), stream());
@@ -861,6 +883,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("relu_bwd", &relu_bwd);
   m.def("add_bf16", &add_bf16);
   m.def("nchw_to_nhwc", &nchw_to_nhwc);
+  m.def("nchw_to_pairs", &nchw_to_pairs);
+  m.def("pair_weight", &pair_weight);
+  m.def("pair_wgrad_add", &pair_wgrad_add);
   m.def("cast_f32_bf16", &cast_f32_bf16);
   m.def("cast_bf16_f32", &cast_bf16_f32);
   m.def("maxpool_fwd", &maxpool_fwd);

@@ -60,6 +60,13 @@ extern "C" {
 int bigdl_conv_nt(const ConvArgs* a, hipStream_t st);
 // Kernel choice for bigdl_conv_nt: sets a->ksplit and returns the fp32 workspace elements it needs (0: none).
 long bigdl_conv_nt_plan(ConvArgs* a);
+// Pixel-pair packing for 3/4-channel width-stride-2 stems (stem.hip).
+void bigdl_nchw_to_pairs(const float* x, uint16_t* y, int N, int C, int H, int W, int Hp, int Wp, int ph, int pw,
+                         hipStream_t st);
+void bigdl_pair_weight(const uint16_t* w, uint16_t* wp, int K, int C, int R, int S, const long* strides,
+                       hipStream_t st);
+void bigdl_pair_wgrad_add(const float* dwp, float* gw, int K, int C, int R, int S, const long* strides, float scale,
+                          hipStream_t st);
 int bigdl_conv_wgrad(const WgradArgs* a, hipStream_t st);
 // Split-K plan for the weight gradient: fills m_per_split / splits; returns the workspace size in floats
 // (0 when the single-split path accumulates straight into dw).

@@ -33,14 +33,19 @@ def _run(graph, iters=6):
     m = opt.optimize()
     Engine.setProperty("bigdl.optim.graph", "true")
     w = m.getParameters()[0][:opt._step.total].detach().float().cpu().clone()
-    return w, graphed, float(opt.state["Loss"])
+    meth = next(iter(opt.optimMethods.values()))
+    return w, graphed, float(opt.state["Loss"]), (meth.state.get("evalCounter"), meth.learningRateSchedule.currentRate)
 
 
 def test_graphed_optimizer_matches_eager():
-    w_e, g_e, l_e = _run(False)
-    w_g, g_g, l_g = _run(True)
+    w_e, g_e, l_e, s_e = _run(False)
+    w_e2, _, _, _ = _run(False)
+    w_g, g_g, l_g, s_g = _run(True)
     assert not any(g_e)
     assert g_g[:2] == [False, False] and all(g_g[2:]), g_g     # eager warm-up, then captured replays
+    assert s_g == s_e, (s_g, s_e)                                 # same schedule position and rate
+    noise = ((w_e2 - w_e).norm() / w_e.norm()).item()             # run-to-run (fp32 atomics in BN statistics)
     rel = ((w_g - w_e).norm() / w_e.norm()).item()
-    assert rel < 2e-3, rel
+    print("graph vs eager", rel, "eager vs eager", noise)
+    assert rel < max(3 * noise, 1e-4), (rel, noise)
     assert abs(l_g - l_e) < 2e-2 * max(1.0, abs(l_e))

@@ -165,3 +165,36 @@ def test_model_broadcast_gloo():
         p.join(60)
     assert torch.equal(res[0][0], res[1][0])
     assert torch.equal(res[1][1], torch.zeros(3))
+
+
+def _compress_modes(rank, world):
+    import torch
+
+    from bigdl_amd.parallel.allreduce_parameter import AllReduceParameter
+
+    out = {}
+    for mode in ("fp16", "bf16"):
+        comm = AllReduceParameter(256, compress=mode)
+        g = torch.full((comm.padded,), 1.0 + 2 ** -8 + 2 ** -10)
+        work, chunk = comm.reduce_scatter_range(g, 0, comm.padded, average=False)
+        if work is not None:
+            work.wait()
+        out[mode] = chunk.clone()
+    return out
+
+
+def test_fp16_compression_is_reference_truncation():
+    """bigdl.compress=fp16 reproduces the reference FP16CompressedTensor (S/parameters/FP16CompressedTensor.scala:
+    271-279: the upper 16 bits of each fp32): 1 + 2^-8 + 2^-10 truncates to 1.0 on both ranks (sum 2.0), while the
+    bf16 mode rounds to nearest even (1 + 2^-7 each)."""
+    from bigdl_amd.utils.testing import run_distributed
+
+    res = run_distributed(_compress_modes, 2)
+    for r in res:
+        assert torch.all(r["fp16"] == 2.0), r["fp16"][:4]
+        assert torch.all(r["bf16"] == 2.0 * (1.0 + 2 ** -7)), r["bf16"][:4]
+    x = torch.randn(1000) * 100
+    from bigdl_amd.ops.nnk import f32_to_bf16_rtz
+
+    t = f32_to_bf16_rtz(x)
+    assert torch.equal(t.float().view(torch.int32), x.view(torch.int32) & -65536)   # bits & 0xffff0000
