@@ -24,8 +24,8 @@ class Sample:
             self.labels = []
         else:
             self.labels = list(labels) if isinstance(labels, (list, tuple)) else [labels]
-        self.features = [torch.as_tensor(f) for f in self.features]
-        self.labels = [torch.as_tensor(l) for l in self.labels]
+        self.features = [_as_tensor(f) for f in self.features]
+        self.labels = [_as_tensor(l) for l in self.labels]
 
     def feature(self, i=0):
         return self.features[i]
@@ -47,6 +47,14 @@ class Sample:
 
     def __repr__(self):
         return f"Sample(features={self.getFeatureSize()}, labels={self.getLabelSize()})"
+
+
+def _as_tensor(t):
+    """torch tensor of a feature / label: bigdl_amd Tensor / SparseTensor wrappers unwrap to their torch tensor
+    (sparse COO stays sparse)."""
+    if getattr(t, "_is_bigdl_tensor", False):
+        return t._t
+    return t if isinstance(t, torch.Tensor) else torch.as_tensor(t)
 
 
 ArraySample = Sample
@@ -122,7 +130,74 @@ def _stack(ts, pad=None):
     return out
 
 
+def _batch_sparse(ts):
+    """Concatenate per-sample sparse COO tensors along a new leading batch dimension: sample i's indices get
+    batch index i (1-D [D] features, or [1, D] rows, batch to [B, D]; reference SparseTensorUtils.concat used by
+    SparseMiniBatch.set, S/dataset/MiniBatch.scala:588-660)."""
+    idx, val = [], []
+    shape = None
+    for i, t in enumerate(ts):
+        t = t.coalesce()
+        ind = t.indices()
+        if t.dim() == 2 and t.shape[0] == 1:            # [1, D] row -> [D]
+            ind = ind[1:]
+            tshape = tuple(t.shape[1:])
+        else:
+            tshape = tuple(t.shape)
+        if shape is None:
+            shape = tshape
+        elif len(tshape) != len(shape):
+            raise ValueError(f"SparseMiniBatch: sample {i} has rank {len(tshape)}, expected {len(shape)}")
+        shape = tuple(max(a, b) for a, b in zip(shape, tshape))
+        idx.append(torch.cat([torch.full((1, ind.shape[1]), i, dtype=torch.int64), ind], 0))
+        val.append(t.values())
+    return torch.sparse_coo_tensor(torch.cat(idx, 1), torch.cat(val), (len(ts),) + shape).coalesce()
+
+
+def _batch_feature(ts, pad=None):
+    return _batch_sparse(ts) if ts[0].is_sparse else _stack(ts, pad)
+
+
+class SparseMiniBatch(MiniBatch):
+    """MiniBatch whose inputs may be sparse COO tensors (reference SparseMiniBatch, S/dataset/MiniBatch.scala:588):
+    each sparse feature of the samples is concatenated into one [batch, ...] sparse tensor, dense features and
+    labels are stacked as usual; ``SampleToMiniBatch`` produces it whenever a sample feature is sparse (wide &
+    deep: SparseLinear / SparseJoinTable inputs)."""
+
+    def size(self):
+        x = self.input
+        if isinstance(x, Table):
+            x = x[1]
+        return x.shape[0]
+
+    def slice(self, offset, length):
+        def sl(t):
+            if t is None:
+                return None
+            if isinstance(t, Table):
+                o = Table()
+                for k, v in t.items():
+                    o[k] = sl(v)
+                return o
+            if t.is_sparse:
+                return t.index_select(0, torch.arange(offset - 1, offset - 1 + length)).coalesce()
+            return t.narrow(0, offset - 1, length)
+
+        return SparseMiniBatch(sl(self.input), sl(self.target))
+
+    def to(self, device, non_blocking=False):
+        mb = super().to(device, non_blocking)
+        return SparseMiniBatch(mb.input, mb.target)
+
+
 def samples_to_minibatch(samples, featurePadding=None, labelPadding=None):
+    if any(f.is_sparse for f in samples[0].features):
+        nf, nl = samples[0].numFeature(), samples[0].numLabel()
+        feats = [_batch_feature([s.features[i] for s in samples], featurePadding) for i in range(nf)]
+        inp = feats[0] if nf == 1 else Table(*feats)
+        labs = [_batch_feature([s.labels[i] for s in samples], labelPadding) for i in range(nl)]
+        tgt = None if nl == 0 else (labs[0] if nl == 1 else Table(*labs))
+        return SparseMiniBatch(inp, tgt)
     nf = samples[0].numFeature()
     nl = samples[0].numLabel()
     if nf == 1:

@@ -635,6 +635,21 @@ class LocallyConnected2D(AutogradModule):
     def fn(self, x):
         if self.format == "NHWC":
             x = x.permute(0, 3, 1, 2)
+        if x.is_cuda:
+            # one GEMM per output location, batched: cols [L][N][C*kh*kw] x W [L][O][C*kh*kw] on the native MFMA
+            # kernel (ops/bmm.py); patches gathered with Tensor.unfold views (no im2col kernel)
+            from ..ops.bmm import matmul
+
+            N = x.shape[0]
+            ph, pw = self.p
+            xp = torch.constant_pad_nd(x.float(), (pw, pw, ph, ph)) if (ph or pw) else x.float()
+            pat = xp.unfold(2, self.k[0], self.s[0]).unfold(3, self.k[1], self.s[1])   # N, C, OH, OW, kh, kw
+            cols = pat.permute(2, 3, 0, 1, 4, 5).reshape(self.oh * self.ow, N, -1)      # L, N, C*kh*kw
+            y = matmul(cols, self.weight.transpose(1, 2))                               # L, N, O
+            if self.bias is not None:
+                y = y + self.bias.unsqueeze(1)
+            y = y.permute(1, 2, 0).reshape(N, self.cout, self.oh, self.ow)
+            return y.permute(0, 2, 3, 1) if self.format == "NHWC" else y
         cols = F.unfold(x.to(self.weight.dtype), self.k, padding=self.p, stride=self.s)   # N, CKK, L
         y = torch.einsum("nkl,lok->nol", cols, self.weight)
         if self.bias is not None:
@@ -661,6 +676,11 @@ class LocallyConnected1D(AutogradModule):
             x = x.unsqueeze(0)
         win = x.to(self.weight.dtype).unfold(1, self.kW, self.sW)          # N, L, in, kW
         win = win.permute(0, 1, 3, 2).reshape(x.shape[0], self.nOut, -1)
+        if x.is_cuda:     # batched over output frames on the native MFMA GEMM (ops/bmm.py)
+            from ..ops.bmm import matmul
+
+            y = matmul(win.transpose(0, 1), self.weight.transpose(1, 2)).transpose(0, 1) + self.bias
+            return y.squeeze(0) if squeeze else y
         y = torch.einsum("nlk,lok->nlo", win, self.weight) + self.bias
         return y.squeeze(0) if squeeze else y
 

@@ -316,6 +316,10 @@ class MM(AutogradModule):
             a = a.transpose(-1, -2)
         if self.transB:
             b = b.transpose(-1, -2)
+        if a.is_cuda:       # native batched bf16 MFMA GEMM (ops/bmm.py, csrc/bmm.hip), gradients on the same kernel
+            from ..ops.bmm import matmul
+
+            return matmul(a, b)
         return a @ b
 
 
@@ -354,6 +358,10 @@ class MV(AutogradModule):
         m, v = x[1], x[2]
         if self.trans:
             m = m.transpose(-1, -2)
+        if m.is_cuda:
+            from ..ops.bmm import matmul
+
+            return matmul(m, v.unsqueeze(-1)).squeeze(-1)
         return (m @ v.unsqueeze(-1)).squeeze(-1)
 
 

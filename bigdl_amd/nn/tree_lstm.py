@@ -24,6 +24,15 @@ from .abstractnn import AutogradModule
 from .init_methods import RandomUniform
 
 
+
+def _lin(x, w, b=None):
+    """x w^T (+ b): the native MFMA GEMM on the GPU engine (ops/conv_fn.linear), torch.addmm on the CPU."""
+    if x.is_cuda:
+        from ..ops import conv_fn
+
+        return conv_fn.linear(x.float(), w.float(), None if b is None else b.float())
+    return torch.addmm(b, x, w.t()) if b is not None else x @ w.t()
+
 class TensorTree:
     """1-based view of one tree encoding (reference BinaryTreeLSTM.scala TensorTree)."""
 
@@ -147,7 +156,7 @@ class BinaryTreeLSTM(TreeLSTM):
             ln = torch.tensor([b * N + n for b, n, _ in leaves], device=dev)
             li = torch.tensor([i for _, _, i in leaves], device=dev)
             xin = inputs[lb, li]
-            g = torch.addmm(self.leafBias, xin, self.leafWeight.t())
+            g = _lin(xin, self.leafWeight, self.leafBias)
             c = g[:, :H]
             h = torch.sigmoid(g[:, H:]) * torch.tanh(c) if self.gateOutput else torch.tanh(c)
             C = C.index_copy(0, ln, c)
@@ -158,7 +167,7 @@ class BinaryTreeLSTM(TreeLSTM):
             left = torch.tensor([b * N + l for b, _, l, _ in lvl], device=dev)
             right = torch.tensor([b * N + r for b, _, _, r in lvl], device=dev)
             lh, rh, lc, rc = Hs[left], Hs[right], C[left], C[right]
-            g = torch.addmm(bias, lh, self.leftWeight.t()) + rh @ self.rightWeight.t()
+            g = _lin(lh, self.leftWeight, bias) + _lin(rh, self.rightWeight)
             i = torch.sigmoid(g[:, :H])
             lf = torch.sigmoid(g[:, H:2 * H])
             rf = torch.sigmoid(g[:, 2 * H:3 * H])

@@ -49,9 +49,6 @@ class DeviceFeed:
     """Iterator of device-resident MiniBatches with the next batch's copy in flight (depth = host queue size)."""
 
     def __init__(self, it, device, depth=2, pin=True):
-        from ..dataset.core import MiniBatch
-
-        self._MB = MiniBatch
         self.device = torch.device(device)
         self.cuda = self.device.type == "cuda"
         self.pin = pin and self.cuda
@@ -72,7 +69,7 @@ class DeviceFeed:
                 if self._stop:
                     return
                 if self.pin:
-                    mb = self._MB(_map(mb.getInput(), _pin), _map(mb.getTarget(), _pin))
+                    mb = type(mb)(_map(mb.getInput(), _pin), _map(mb.getTarget(), _pin))
                 self._q.put(mb)
         except BaseException as e:  # noqa: BLE001 - re-raised in the consumer
             self._err = e
@@ -94,7 +91,7 @@ class DeviceFeed:
         if not self.cuda:
             return mb, None
         with torch.cuda.stream(self.stream):
-            dev = self._MB(_map(mb.getInput(), lambda t: t.to(self.device, non_blocking=True)),
+            dev = type(mb)(_map(mb.getInput(), lambda t: t.to(self.device, non_blocking=True)),
                            _map(mb.getTarget(), lambda t: t.to(self.device, non_blocking=True)))
             ev = torch.cuda.Event()
             ev.record(self.stream)
@@ -115,7 +112,11 @@ class DeviceFeed:
         cur = torch.cuda.current_stream(self.device)
         cur.wait_event(ev)
         for t in list(_tensors(dev.getInput())) + list(_tensors(dev.getTarget())):
-            t.record_stream(cur)
+            if t.is_sparse:
+                t._indices().record_stream(cur)
+                t._values().record_stream(cur)
+            else:
+                t.record_stream(cur)
         try:
             self._pending = self._issue()     # the next batch's copy overlaps this step
         except StopIteration:
@@ -132,6 +133,6 @@ class DeviceFeed:
 
 
 def _pin(t):
-    if isinstance(t, torch.Tensor) and t.device.type == "cpu" and not t.is_pinned():
+    if isinstance(t, torch.Tensor) and t.device.type == "cpu" and not t.is_sparse and not t.is_pinned():
         return t.pin_memory()
     return t

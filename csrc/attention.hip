@@ -4,8 +4,8 @@
 // Reference: S/nn/Attention.scala:90-103 (MM(transB) -> CAddTable(bias) -> SoftMax -> Dropout -> MM), the core of
 // S/nn/Transformer.scala's self / encoder-decoder attention (SURVEY K-row "attention").
 //
-// Layout: Q [BH][Lq][D], K / V [BH][Lk][D] bf16 (q pre-scaled by D^-1/2 as in SplitHeads(mul=true)), D = 64 or
-// 128; bias fp32 broadcast through element strides (sb, sh, sq, sk) over (batch, head, query, key), or causal.
+// Layout: Q [BH][Lq][D], K / V [BH][Lk][D] bf16 (q pre-scaled by D^-1/2 as in SplitHeads(mul=true)), D = 32, 64,
+// 96 or 128; bias fp32 broadcast through element strides (sb, sh, sq, sk) over (batch, head, query, key), or causal.
 // Outputs O fp32 [BH][Lq][D] and the row log-sum-exp (fp32 [BH][Lq]) kept for the backward.
 //
 // Forward: workgroup = 64 query rows (4 waves x 16) of one (batch, head); K / V stream through LDS in 64-key
@@ -36,7 +36,24 @@ struct AttnArgs {
   const float* delta;                 // backward: rowsum(dO o O) [BH][Lq]
   float* dq; float* dk; float* dv;    // backward outputs fp32
   int H, Lq, Lk, causal;
+  // attention dropout (reference Attention.scala:59 attentionDropout on the softmax output): keep iff
+  // hash(seed, row, key) >= drop_thr, kept probabilities scaled by drop_scale = 1 / (1 - p); drop_thr == 0: none
+  unsigned drop_thr; float drop_scale; unsigned seed_lo, seed_hi;
 };
+
+// Counter-based dropout mask, identical in the forward and the backward whatever the tiling: a lowbias32-style
+// integer hash (2 multiply-xorshift rounds) of the row hash and the key index. The row part is hashed once per
+// query row; a mask element costs one hash (a handful of VALU ops) instead of a Philox block per element.
+__device__ __forceinline__ unsigned mix32(unsigned x) {
+  x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
+  return x;
+}
+__device__ __forceinline__ unsigned drop_row(const AttnArgs& a, int bh, int qi) {
+  return mix32((unsigned)(bh * a.Lq + qi) ^ a.seed_lo);
+}
+__device__ __forceinline__ float drop_mul(const AttnArgs& a, unsigned row, int kj) {
+  return mix32(row + (unsigned)kj * 0x9E3779B9u + a.seed_hi) >= a.drop_thr ? a.drop_scale : 0.f;
+}
 
 __device__ __forceinline__ float bias_at(const AttnArgs& a, int bh, int qi, int kj) {
   if (!a.bias) return 0.f;
@@ -153,8 +170,17 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
     for (int c = 0; c < NC; ++c)
 #pragma unroll
       for (int i = 0; i < 4; ++i) oacc[c][i] *= scale[i];
-    // P (bf16) -> this wave's LDS slice [16 q][64 keys], read back as A fragments
+    // P (bf16) -> this wave's LDS slice [16 q][64 keys], read back as A fragments; attention dropout acts on the
+    // normalised probabilities, so it scales what enters P V while the normaliser l keeps the un-dropped sums
     bf16_t* P = sP[wave];
+    if (a.drop_thr) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const unsigned row = drop_row(a, bh, q0 + 4 * grp + i);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) s4[j][i] *= drop_mul(a, row, k0 + 16 * j + col);
+      }
+    }
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -258,10 +284,13 @@ __global__ void __launch_bounds__(256) attn_bwd_kernel(AttnArgs a) {
       dpt[j] = p_acc;               // dP[q][key] likewise
     }
     bf16_t* T = sT[wave];
-    // P^T (recomputed) -> scratch as [key][q], the A operand of dV += P^T dO
+    // P^T (recomputed) -> scratch as [key][q], the A operand of dV += P_dropped^T dO; dm keeps the dropout factor
+    // (0 or 1 / (1 - p)) of every element for dP = dm * (dO V^T)
+    float dm[4][4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int qi = q0 + 16 * j + col;
+      const unsigned row = a.drop_thr ? drop_row(a, bh, qi) : 0u;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int kj = kw + 4 * grp + i;
@@ -269,7 +298,8 @@ __global__ void __launch_bounds__(256) attn_bwd_kernel(AttnArgs a) {
         if (qi < a.Lq && kj < a.Lk && !(a.causal && kj > qi))
           p = __expf(st[j][i] + bias_at(a, bh, qi, kj) - sL[16 * j + col]);
         st[j][i] = p;
-        T[(4 * grp + i) * AT_BK + 16 * j + col] = f2bf(p);
+        dm[j][i] = a.drop_thr ? drop_mul(a, row, kj) : 1.f;
+        T[(4 * grp + i) * AT_BK + 16 * j + col] = f2bf(p * dm[j][i]);
       }
     }
     __syncthreads();
@@ -285,7 +315,7 @@ __global__ void __launch_bounds__(256) attn_bwd_kernel(AttnArgs a) {
     for (int j = 0; j < 4; ++j) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const float ds = st[j][i] * (dpt[j][i] - sDel[16 * j + col]);
+        const float ds = st[j][i] * (dpt[j][i] * dm[j][i] - sDel[16 * j + col]);
         const bf16_t d16 = f2bf(ds);
         T[(4 * grp + i) * AT_BK + 16 * j + col] = d16;
         sdS[(16 * j + col) * AT_BK + wave * 16 + 4 * grp + i] = d16;
@@ -344,28 +374,43 @@ static AttnArgs to_args(const AttnCall* c) {
   a.q = c->q; a.k = c->k; a.v = c->v; a.bias = c->bias; a.sb = c->sb; a.sh = c->sh; a.sq = c->sq; a.sk = c->sk;
   a.o = c->o; a.lse = c->lse; a.dout = c->dout; a.delta = c->delta; a.dq = c->dq; a.dk = c->dk; a.dv = c->dv;
   a.H = c->H; a.Lq = c->Lq; a.Lk = c->Lk; a.causal = c->causal;
+  const double p = c->drop_p;
+  a.drop_thr = p > 0.0 ? (unsigned)fmin(4294967295.0, p * 4294967296.0) : 0u;
+  if (p > 0.0 && a.drop_thr == 0u) a.drop_thr = 1u;
+  a.drop_scale = p > 0.0 && p < 1.0 ? (float)(1.0 / (1.0 - p)) : (p >= 1.0 ? 0.f : 1.f);
+  a.seed_lo = (unsigned)c->seed; a.seed_hi = (unsigned)(c->seed >> 32);
   return a;
 }
 
+static bool attn_dim_ok(int D) { return D == 32 || D == 64 || D == 96 || D == 128; }
+
 int bigdl_attn_fwd(const AttnCall* c, hipStream_t st) {
-  if ((c->D != 64 && c->D != 128) || c->BH <= 0 || c->Lq <= 0 || c->Lk <= 0) return -1;
+  if (!attn_dim_ok(c->D) || c->BH <= 0 || c->Lq <= 0 || c->Lk <= 0) return -1;
   const AttnArgs a = to_args(c);
   dim3 grid((c->Lq + AT_BQ - 1) / AT_BQ, c->BH);
-  if (c->D == 64) attn_fwd_kernel<64><<<grid, 256, 0, st>>>(a);
-  else attn_fwd_kernel<128><<<grid, 256, 0, st>>>(a);
+  switch (c->D) {
+    case 32: attn_fwd_kernel<32><<<grid, 256, 0, st>>>(a); break;
+    case 64: attn_fwd_kernel<64><<<grid, 256, 0, st>>>(a); break;
+    case 96: attn_fwd_kernel<96><<<grid, 256, 0, st>>>(a); break;
+    default: attn_fwd_kernel<128><<<grid, 256, 0, st>>>(a); break;
+  }
   HIP_LAUNCH_CHECK();
   return 0;
 }
 
 int bigdl_attn_bwd(const AttnCall* c, float* delta_ws, hipStream_t st) {
-  if ((c->D != 64 && c->D != 128) || c->BH <= 0 || c->Lq <= 0 || c->Lk <= 0) return -1;
+  if (!attn_dim_ok(c->D) || c->BH <= 0 || c->Lq <= 0 || c->Lk <= 0) return -1;
   const long rows = (long)c->BH * c->Lq;
   attn_delta_kernel<<<(unsigned)((rows + 3) / 4), 256, 0, st>>>(c->dout, c->o, delta_ws, rows, c->D);
   AttnArgs a = to_args(c);
   a.delta = delta_ws;
   dim3 grid((c->Lk + AT_BK - 1) / AT_BK, c->BH);
-  if (c->D == 64) attn_bwd_kernel<64><<<grid, 256, 0, st>>>(a);
-  else attn_bwd_kernel<128><<<grid, 256, 0, st>>>(a);
+  switch (c->D) {
+    case 32: attn_bwd_kernel<32><<<grid, 256, 0, st>>>(a); break;
+    case 64: attn_bwd_kernel<64><<<grid, 256, 0, st>>>(a); break;
+    case 96: attn_bwd_kernel<96><<<grid, 256, 0, st>>>(a); break;
+    default: attn_bwd_kernel<128><<<grid, 256, 0, st>>>(a); break;
+  }
   HIP_LAUNCH_CHECK();
   return 0;
 }

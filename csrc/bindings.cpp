@@ -200,6 +200,17 @@ void pair_wgrad_add(const Tensor& dwp, const Tensor& gw, double scale) {
   const long st[4] = {(long)gw.stride(0), (long)gw.stride(1), (long)gw.stride(2), (long)gw.stride(3)};
   bigdl_pair_wgrad_add(cf(dwp, "dwp"), mf(gw, "gw"), K, C, R, S, st, (float)scale, stream());
 }
+void bmm_nt(const Tensor& a, const Tensor& b, const Tensor& c, double alpha, bool accum) {
+  TORCH_CHECK(a.dim() == 3 && b.dim() == 3 && c.dim() == 3, "bmm_nt: [batch, rows, K] operands, [batch, M, N] out");
+  TORCH_CHECK(a.is_contiguous() && b.is_contiguous() && c.is_contiguous(), "bmm_nt: contiguous operands");
+  TORCH_CHECK(a.size(0) == b.size(0) && a.size(0) == c.size(0) && a.size(2) == b.size(2) && c.size(1) == a.size(1) &&
+              c.size(2) == b.size(1), "bmm_nt: shapes");
+  TORCH_CHECK(a.size(2) % 32 == 0, "bmm_nt: K must be padded to a multiple of 32");
+  const int rc = bigdl_bmm_nt(cbf(a, "a"), cbf(b, "b"), mf(c, "c"), a.size(0), a.size(1), b.size(1), a.size(2),
+                              a.stride(0), b.stride(0), c.stride(0), a.size(2), b.size(2), c.size(2), (float)alpha,
+                              accum ? 1 : 0, stream());
+  TORCH_CHECK(rc == 0, "bmm_nt: unsupported shape");
+}
 void cast_f32_bf16(const Tensor& x, const Tensor& y) {
   TORCH_CHECK(x.numel() == y.numel() && x.is_contiguous() && y.is_contiguous(), "cast: size");
   bigdl_cast_f32_bf16(cf(x, "x"), mbf(y, "y"), x.numel(), stream());
@@ -752,7 +763,7 @@ AttnCall attn_call(const Tensor& q, const Tensor& k, const Tensor& v, const OptT
   AttnCall c{};
   c.q = cbf(q, "q"); c.k = cbf(k, "k"); c.v = cbf(v, "v");
   c.BH = (int)q.size(0); c.H = (int)H; c.Lq = (int)q.size(1); c.Lk = (int)k.size(1); c.D = (int)q.size(2);
-  TORCH_CHECK(c.D == 64 || c.D == 128, "attention: head dim must be 64 or 128");
+  TORCH_CHECK(c.D == 32 || c.D == 64 || c.D == 96 || c.D == 128, "attention: head dim must be 32, 64, 96 or 128");
   TORCH_CHECK(H > 0 && c.BH % H == 0, "attention: heads");
   c.causal = causal ? 1 : 0;
   if (bias && bias->defined()) {
@@ -768,16 +779,20 @@ AttnCall attn_call(const Tensor& q, const Tensor& k, const Tensor& v, const OptT
   return c;
 }
 void attn_fwd(const Tensor& q, const Tensor& k, const Tensor& v, const OptT& bias, int64_t H, bool causal,
-              const Tensor& o, const Tensor& lse) {
+              const Tensor& o, const Tensor& lse, double drop_p, int64_t seed) {
   AttnCall c = attn_call(q, k, v, bias, H, causal);
+  TORCH_CHECK(drop_p >= 0.0 && drop_p < 1.0, "attention: dropout probability in [0, 1)");
+  c.drop_p = (float)drop_p; c.seed = (unsigned long long)seed;
   TORCH_CHECK(o.is_contiguous() && o.numel() == q.numel() && lse.numel() == (int64_t)c.BH * c.Lq, "attn_fwd: o/lse");
   c.o = mf(o, "o"); c.lse = mf(lse, "lse");
   TORCH_CHECK(bigdl_attn_fwd(&c, stream()) == 0, "attn_fwd: unsupported shape");
 }
 void attn_bwd(const Tensor& q, const Tensor& k, const Tensor& v, const OptT& bias, int64_t H, bool causal,
               const Tensor& o, const Tensor& lse, const Tensor& dout, const Tensor& dq, const Tensor& dk,
-              const Tensor& dv, const Tensor& delta_ws) {
+              const Tensor& dv, const Tensor& delta_ws, double drop_p, int64_t seed) {
   AttnCall c = attn_call(q, k, v, bias, H, causal);
+  TORCH_CHECK(drop_p >= 0.0 && drop_p < 1.0, "attention: dropout probability in [0, 1)");
+  c.drop_p = (float)drop_p; c.seed = (unsigned long long)seed;
   TORCH_CHECK(o.is_contiguous() && dout.is_contiguous() && o.numel() == q.numel() && dout.numel() == q.numel(),
               "attn_bwd: o/dout");
   TORCH_CHECK(dq.is_contiguous() && dq.numel() == q.numel() && dk.numel() == k.numel() && dv.numel() == v.numel() &&
@@ -884,6 +899,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("add_bf16", &add_bf16);
   m.def("nchw_to_nhwc", &nchw_to_nhwc);
   m.def("nchw_to_pairs", &nchw_to_pairs);
+  m.def("bmm_nt", &bmm_nt, py::arg("a"), py::arg("b"), py::arg("c"), py::arg("alpha") = 1.0, py::arg("accum") = false);
   m.def("pair_weight", &pair_weight);
   m.def("pair_wgrad_add", &pair_wgrad_add);
   m.def("cast_f32_bf16", &cast_f32_bf16);
@@ -935,9 +951,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("lstm_bwd_step", &lstm_bwd_step);
   m.def("colsum_bf16", &colsum_bf16);
   m.def("layernorm_fwd", &layernorm_fwd);
-  m.def("attn_fwd", &attn_fwd);
+  m.def("attn_fwd", &attn_fwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("bias"), py::arg("H"),
+        py::arg("causal"), py::arg("o"), py::arg("lse"), py::arg("drop_p") = 0.0, py::arg("seed") = 0);
   m.def("gconv", &gconv);
-  m.def("attn_bwd", &attn_bwd);
+  m.def("attn_bwd", &attn_bwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("bias"), py::arg("H"),
+        py::arg("causal"), py::arg("o"), py::arg("lse"), py::arg("dout"), py::arg("dq"), py::arg("dk"), py::arg("dv"),
+        py::arg("delta_ws"), py::arg("drop_p") = 0.0, py::arg("seed") = 0);
   m.def("layernorm_bwd", &layernorm_bwd);
   m.def("gru_step", &gru_step, py::arg("mode"), py::arg("A"), py::arg("W"), py::arg("B"), py::arg("H"),
         py::arg("xg") = py::none(), py::arg("hprev") = py::none(), py::arg("r") = py::none(), py::arg("z") = py::none(),

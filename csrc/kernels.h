@@ -60,6 +60,10 @@ extern "C" {
 int bigdl_conv_nt(const ConvArgs* a, hipStream_t st);
 // Kernel choice for bigdl_conv_nt: sets a->ksplit and returns the fp32 workspace elements it needs (0: none).
 long bigdl_conv_nt_plan(ConvArgs* a);
+// Batched NT GEMM (bmm.hip): C[b][m][n] (=|+=) alpha * sum_k A[b][m][k] B[b][n][k]; A, B bf16 K-contiguous (K % 32
+// == 0, row strides % 8 == 0), C fp32. Returns < 0 on unsupported shapes.
+int bigdl_bmm_nt(const uint16_t* A, const uint16_t* B, float* C, int batch, int M, int N, int K, long sa, long sb,
+                 long sc, int lda, int ldb, int ldc, float alpha, int accum, hipStream_t st);
 // Pixel-pair packing for 3/4-channel width-stride-2 stems (stem.hip).
 void bigdl_nchw_to_pairs(const float* x, uint16_t* y, int N, int C, int H, int W, int Hp, int Wp, int ph, int pw,
                          hipStream_t st);
@@ -219,12 +223,14 @@ int bigdl_layernorm_fwd(const float* x, const float* g, const float* b, float* y
 int bigdl_layernorm_bwd(const float* dy, const float* x, const float* g, const float* mean, const float* rstd,
                         float* dx, float* dg, float* db, long rows, int D, hipStream_t st);
 
-// Fused attention (csrc/attention.hip). q/k/v bf16 [BH][L][D] (D = 64 or 128), bias fp32 through element strides
-// (sb, sh, sq, sk) or nullptr, o / dq / dk / dv / dout fp32, lse / delta fp32 [BH][Lq].
+// Fused attention (csrc/attention.hip). q/k/v bf16 [BH][L][D] (D = 32, 64, 96 or 128), bias fp32 through element
+// strides (sb, sh, sq, sk) or nullptr, o / dq / dk / dv / dout fp32, lse / delta fp32 [BH][Lq]; attention dropout
+// with probability drop_p (0: none) from a counter-based hash of (seed, row, key), regenerated by the backward.
 typedef struct {
   const uint16_t* q; const uint16_t* k; const uint16_t* v; const float* bias; long sb, sh, sq, sk;
   float* o; float* lse; const float* dout; const float* delta; float* dq; float* dk; float* dv;
   int BH, H, Lq, Lk, D, causal;
+  float drop_p; unsigned long long seed;
 } AttnCall;
 int bigdl_attn_fwd(const AttnCall* c, hipStream_t st);
 int bigdl_attn_bwd(const AttnCall* c, float* delta_ws, hipStream_t st);

@@ -155,3 +155,80 @@ def test_stem_pixel_pair_conv_matches_cpu(case):
     assert _rel(gg, gc) < 2e-2, _rel(gg, gc)
     for a, b in zip(gpu.parameters()[1], cpu.parameters()[1]):
         assert _rel(a, b) < 1e-2, (a.shape, _rel(a, b))
+
+
+def _bmm_case(name):
+    from bigdl_amd import nn
+    from bigdl_amd.utils.table import Table
+
+    g = torch.Generator().manual_seed(4)
+    if name == "mm":
+        return nn.MM(), Table(torch.randn(3, 20, 37, generator=g), torch.randn(3, 37, 50, generator=g))
+    if name == "mm_trans":
+        return nn.MM(True, True), Table(torch.randn(2, 33, 17, generator=g), torch.randn(2, 70, 33, generator=g))
+    if name == "mm_2d":
+        return nn.MM(), Table(torch.randn(65, 40, generator=g), torch.randn(40, 3, generator=g))
+    if name == "mv":
+        return nn.MV(), Table(torch.randn(4, 19, 45, generator=g), torch.randn(4, 45, generator=g))
+    if name == "lc2d":
+        return nn.LocallyConnected2D(5, 9, 8, 12, 3, 3, 2, 1, 1, 1), torch.randn(3, 5, 8, 9, generator=g)
+    if name == "lc1d":
+        return nn.LocallyConnected1D(11, 6, 10, 3, 2), torch.randn(4, 11, 6, generator=g)
+    if name == "treelstm":
+        t1 = torch.tensor([[2, 5, -1], [0, 0, 1], [0, 0, 2], [0, 0, 3], [3, 4, 0], [-1, -1, -1]], dtype=torch.float32)
+        t2 = torch.tensor([[2, 3, -1], [4, 5, 0], [0, 0, 3], [0, 0, 1], [0, 0, 2], [-1, -1, -1]], dtype=torch.float32)
+        return nn.BinaryTreeLSTM(16, 24), Table(torch.randn(2, 3, 16, generator=g), torch.stack([t1, t2]))
+    raise KeyError(name)
+
+
+@pytest.mark.parametrize("name", ["mm", "mm_trans", "mm_2d", "mv", "lc2d", "lc1d", "treelstm"])
+def test_matrix_product_layers_native_match_cpu(name, monkeypatch):
+    """MM / MV (S/nn/MM.scala:34, S/nn/MV.scala:33), LocallyConnected1D/2D (S/nn/LocallyConnected2D.scala:233) and
+    BinaryTreeLSTM on the GPU engine run the native batched MFMA GEMM (csrc/bmm.hip) / linear kernels: forward and
+    all gradients vs the fp32 CPU engine, with torch's matmul / bmm / einsum / addmm patched to raise."""
+    from bigdl_amd.utils.random_generator import RNG
+    from bigdl_amd.utils.table import Table
+
+    RNG.setSeed(6)
+    cpu, x = _bmm_case(name)
+    gpu = copy.deepcopy(cpu).to("cuda")
+
+    def to_dev(a):
+        if isinstance(a, Table):
+            out = Table()
+            for k, v in a.items():
+                out[k] = to_dev(v)
+            return out
+        return a.to(torch.bfloat16).float().cuda() if a.is_floating_point() and a.dim() > 1 and name != "treelstm" \
+            else a.cuda()
+
+    def to_cpu_ref(a):
+        if isinstance(a, Table):
+            out = Table()
+            for k, v in a.items():
+                out[k] = to_cpu_ref(v)
+            return out
+        return a.to(torch.bfloat16).float() if a.is_floating_point() and a.dim() > 1 and name != "treelstm" else a
+
+    xc, xg = to_cpu_ref(x), to_dev(x)
+    yc = cpu.forward(xc)
+
+    def boom(*a, **k):
+        raise AssertionError("aten matrix product on the GPU path")
+
+    with monkeypatch.context() as mp:
+        for fn in ("matmul", "bmm", "einsum", "addmm", "mm"):
+            mp.setattr(torch, fn, boom)
+        yg = gpu.forward(xg)
+        gy = torch.randn_like(yc)
+        gg = gpu.backward(xg, gy.cuda())
+    gc = cpu.backward(xc, gy)
+    assert _rel(yg, yc) < 1e-2, _rel(yg, yc)
+    if isinstance(gc, Table):
+        for k in (1, 2):
+            if gc[k] is not None and torch.is_tensor(gc[k]) and gc[k].is_floating_point() and gc[k].abs().sum() > 0:
+                assert _rel(gg[k], gc[k]) < 2e-2, (k, _rel(gg[k], gc[k]))
+    else:
+        assert _rel(gg, gc) < 2e-2, _rel(gg, gc)
+    for a, b in zip((gpu.parameters() or ([], []))[1], (cpu.parameters() or ([], []))[1]):
+        assert _rel(a, b) < 2e-2, (a.shape, _rel(a, b))

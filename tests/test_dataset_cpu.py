@@ -182,3 +182,48 @@ def test_reference_named_vision_transforms(tmp_path):
     frame = V.SeqFileFolder.files_to_image_frame(str(tmp_path / "seq"), 2)
     assert len(frame.array) == 8 and all(float(x[ImageFeature.label][0]) <= 2 for x in frame.array)
     assert all(hasattr(V, n) for n in ("RoiHFlip", "RoiNormalize", "RoiProject", "RoiResize", "RandomSampler"))
+
+
+def test_sparse_minibatch_wide_and_deep_training():
+    """SampleToMiniBatch turns samples with sparse COO features into a SparseMiniBatch (reference
+    S/dataset/MiniBatch.scala:588): the sparse wide features become one [batch, D] sparse tensor with the sample
+    index as leading coordinate, dense deep features are stacked; a wide & deep model (SparseLinear + Linear)
+    trains on it through Optimizer.optimize()."""
+    from bigdl_amd import nn
+    from bigdl_amd import optim as O
+    from bigdl_amd.dataset.core import DataSet, Sample, SampleToMiniBatch, SparseMiniBatch
+    from bigdl_amd.utils.random_generator import RNG
+
+    RNG.setSeed(3)
+    g = torch.Generator().manual_seed(0)
+    D = 200
+    samples = []
+    for i in range(64):
+        cols = torch.randperm(D, generator=g)[:5]
+        wide = torch.sparse_coo_tensor(cols.unsqueeze(0), torch.ones(5), (D,))
+        deep = torch.randn(8, generator=g)
+        label = torch.tensor(float(1 + (int(cols.min()) % 2)))
+        samples.append(Sample([wide, deep], label))
+    batches = list(SampleToMiniBatch(16, partitionNum=1).apply(iter(samples[:32])))
+    mb = batches[0]
+    assert isinstance(mb, SparseMiniBatch) and mb.size() == 16
+    x = mb.getInput()
+    assert x[1].is_sparse and tuple(x[1].shape) == (16, D) and x[1]._nnz() == 80
+    assert tuple(x[2].shape) == (16, 8)
+    dense0 = samples[0].features[0].to_dense()
+    assert torch.equal(x[1].to_dense()[0], dense0)
+    sub = mb.slice(3, 4)
+    assert sub.size() == 4 and torch.equal(sub.getInput()[1].to_dense()[0], samples[2].features[0].to_dense())
+
+    model = nn.Sequential()
+    model.add(nn.ParallelTable().add(nn.SparseLinear(D, 2)).add(nn.Linear(8, 2)))
+    model.add(nn.CAddTable()).add(nn.LogSoftMax())
+    opt = O.Optimizer(model, DataSet.array(samples), nn.ClassNLLCriterion(), batchSize=16,
+                      optimMethod=O.SGD(0.5), endTrigger=O.Trigger.maxIteration(24))
+    opt.device = torch.device("cpu")
+    first = []
+    opt._iteration_hook = lambda n: first.append(float(opt.state.get("Loss", float("nan"))))
+    opt.setLogInterval(1)
+    opt.optimize()
+    losses = [v for v in first if v == v]
+    assert losses[-1] < losses[0], losses

@@ -65,3 +65,51 @@ def test_fused_attention_matches_fp32(B, H, Lq, Lk, D, mode):
     assert _rel(o, ref) < 1e-2, _rel(o, ref)
     for d, r in zip(dev, leaves):
         assert _rel(d.grad, r.grad) < 2e-2, (d.shape, _rel(d.grad, r.grad))
+
+
+@pytest.mark.parametrize("D", [32, 64, 96, 128])
+@pytest.mark.parametrize("p", [0.0, 0.25])
+def test_fused_attention_dropout_and_head_dims(D, p, monkeypatch):
+    """Fused attention with in-kernel attention dropout (reference S/nn/Attention.scala:59) and head dims 32 / 96
+    beside 64 / 128, forward and backward vs an fp32 autograd reference that applies the same keep mask
+    (ops.flash_attention.dropout_mask reproduces the kernel's counter hash). torch.matmul / softmax are patched to
+    raise while the fused path runs."""
+    from bigdl_amd.ops.flash_attention import dropout_mask, flash_attention
+
+    torch.manual_seed(3)
+    B, H, Lq, Lk = 2, 3, 80, 72
+    dev = torch.device("cuda:0")
+    q = torch.randn(B, H, Lq, D, device=dev) * D ** -0.5
+    k = torch.randn(B, H, Lk, D, device=dev)
+    v = torch.randn(B, H, Lk, D, device=dev)
+    bias = torch.randn(1, 1, Lq, Lk, device=dev) * 0.5
+    go = torch.randn(B, H, Lq, D, device=dev)
+    seed = 0x1234_5678_9ABC
+    qg, kg, vg = (t.clone().requires_grad_(True) for t in (q, k, v))
+
+    def boom(*a, **kw):
+        raise AssertionError("aten attention math on the fused path")
+
+    with monkeypatch.context() as mp:
+        mp.setattr(torch, "matmul", boom)
+        mp.setattr(torch, "softmax", boom)
+        o = flash_attention(qg, kg, vg, bias, False, p, seed)
+        o.backward(go)
+    # reference on the bf16-rounded operands, in fp32
+    qr, kr, vr = (t.to(torch.bfloat16).float().requires_grad_(True) for t in (q, k, v))
+    s = qr @ kr.transpose(-1, -2) + bias
+    P = torch.softmax(s, dim=-1)
+    mask = dropout_mask(seed, B * H, Lq, Lk, p).view(B, H, Lq, Lk).to(dev)
+    oref = (P * mask) @ vr
+    oref.backward(go)
+
+    def rel(a, b):
+        return ((a - b).norm() / b.norm()).item()
+
+    assert rel(o, oref) < 2e-2, rel(o, oref)
+    assert rel(qg.grad, qr.grad) < 3e-2, rel(qg.grad, qr.grad)
+    assert rel(kg.grad, kr.grad) < 3e-2, rel(kg.grad, kr.grad)
+    assert rel(vg.grad, vr.grad) < 3e-2, rel(vg.grad, vr.grad)
+    if p > 0:
+        kept = (mask > 0).float().mean().item()
+        assert abs(kept - (1 - p)) < 0.02, kept
