@@ -95,6 +95,16 @@ class _RecordInit(type):
             _REGISTRY[module_key(cls)] = cls
 
 
+class StragglerTimeout(RuntimeError):
+    """Raised at a module boundary once the straggler deadline of the current iteration has passed (reference
+    DistriOptimizer.scala:241-278 cancels the late model replicas with invokeAndWait2(..., timeout))."""
+
+
+# [deadline in time.perf_counter() seconds, 0 = none]: checked by every module forward / backward (one float
+# compare), set by the Optimizer loop while a straggler threshold is active
+STRAGGLER_DEADLINE = [0.0]
+
+
 def _sync_wrap(kind, f):
     """Per-module synchroniser hooks (reference AbstractModule.scala:282-297 / 1184-1199): every module class's
     own ``forward`` / ``backward`` — including overrides in containers, Graph, BN, recurrent layers — calls
@@ -107,6 +117,9 @@ def _sync_wrap(kind, f):
 
     if kind == "forward":
         def wrapped(self, *args, **kw):
+            dl = STRAGGLER_DEADLINE[0]
+            if dl and time.perf_counter() > dl:
+                raise StragglerTimeout(self.getPrintName())
             s = self.__dict__.get("_sync")
             if s is None:
                 return f(self, *args, **kw)
@@ -120,6 +133,9 @@ def _sync_wrap(kind, f):
                 self.__dict__[key] = d
     else:
         def wrapped(self, *args, **kw):
+            dl = STRAGGLER_DEADLINE[0]
+            if dl and time.perf_counter() > dl:
+                raise StragglerTimeout(self.getPrintName())
             s = self.__dict__.get("_sync")
             if s is None:
                 return f(self, *args, **kw)

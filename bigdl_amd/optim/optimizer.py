@@ -378,10 +378,13 @@ class Optimizer:
                 finished = 0.0
             else:
                 step.zero_grad()
-                loss = step.forward_backward(x, y)
-                eager_done += 1
                 if drop is not None:
-                    finished = drop.finished(time.perf_counter() - t0)
+                    # straggler cancellation: past the deadline every module boundary raises StragglerTimeout, so
+                    # a late rank abandons the rest of its forward / backward and joins the collective on time
+                    loss, finished = drop.run(step, x, y, t0)
+                else:
+                    loss = step.forward_backward_step(x, y)
+                eager_done += 1
             if g is not None:
                 pass
             elif finished is not None:
@@ -520,15 +523,30 @@ class _StragglerDrop:
         self.threshold = float("inf")
         self.dropped = 0
         self.iteration = 0
+        self.cancelled = 0
 
     def timed_out(self, elapsed):
         return elapsed > self.threshold
 
     def finished(self, elapsed):
-        if self.opt.device.type == "cuda" and self.threshold != float("inf"):
-            torch.cuda.synchronize()
         self.times.append(elapsed)
         return 0.0 if elapsed > self.threshold else 1.0
+
+    def run(self, step, x, y, t0):
+        """forward + backward under the iteration deadline t0 + threshold. Returns (loss, finished weight)."""
+        from ..nn.abstractnn import STRAGGLER_DEADLINE, StragglerTimeout
+
+        if self.threshold != float("inf"):
+            STRAGGLER_DEADLINE[0] = t0 + self.threshold
+        try:
+            loss = step.forward_backward_step(x, y)
+        except StragglerTimeout:
+            self.times.append(time.perf_counter() - t0)
+            self.cancelled += 1
+            return torch.zeros((), device=step.device), 0.0
+        finally:
+            STRAGGLER_DEADLINE[0] = 0.0
+        return loss, self.finished(time.perf_counter() - t0)
 
     def record(self, updated, finished):
         self.iteration += 1

@@ -299,6 +299,19 @@ class TrainStep:
                 cv.end_dgrad_weights()
         return loss
 
+    def forward_backward_step(self, x, y):
+        """forward_backward inside this step's BN-statistics arena (what ``step`` runs before the update)."""
+        arena = None
+        if self.device.type == "cuda":
+            from ..ops.bn import ARENA as arena
+
+            arena.begin(self.device)
+        try:
+            return self.forward_backward(x, y)
+        finally:
+            if arena is not None:
+                arena.end()
+
     def _dgrad_convs(self):
         """Convolutions whose backward runs the native data-gradient GEMM (GPU engine, one group)."""
         if getattr(self, "_dgrad_conv_list", None) is None:

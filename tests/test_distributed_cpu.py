@@ -441,3 +441,65 @@ def test_lars_inherited_by_leaves_stays_layer_wise():
     ref = run_distributed(_lars_layerwise, 1, (False,))[0]
     assert len(exp[1]) == 3                  # fc1, fc2, fc3: no merging
     assert torch.allclose(exp[0], ref[0], atol=1e-6)
+
+
+_ITER = [0]
+
+
+def _nap_module(rank):
+    """Injected straggler: on rank 1, after iteration 8, every forward of this layer sleeps 0.2 s."""
+    import time as _t
+
+    from bigdl_amd import nn
+
+    class Nap(nn.Identity):
+        def updateOutput(self, input):
+            if rank == 1 and _ITER[0] >= 8:
+                _t.sleep(0.2)
+            return super().updateOutput(input)
+
+    return Nap()
+
+
+def _straggle_job(rank, world):
+    import time as _t
+
+    from bigdl_amd import nn
+    from bigdl_amd import optim as O
+    from bigdl_amd.dataset.core import DataSet, Sample
+
+    model = nn.Sequential().setName("snet")
+    model.add(nn.Linear(6, 8))
+    for _ in range(10):
+        model.add(_nap_module(rank)).add(nn.Linear(8, 8)).add(nn.Tanh())
+    model.add(nn.Linear(8, 3))
+    X, Y = _data(64)
+    ds = DataSet.rdd([Sample(X[i], Y[i]) for i in range(64)], shuffle=False)
+    opt = O.Optimizer(model, ds, nn.MSECriterion(), batchSize=16, optimMethod=O.SGD(0.01),
+                      endTrigger=O.Trigger.maxIteration(14))
+    opt.setDropModuleProperty(0.25, 0.5, batchsize=4, warmupIteration=4)
+    walls = {}
+    last = [_t.perf_counter()]
+
+    def hook(n):
+        now = _t.perf_counter()
+        walls[n] = now - last[0]
+        last[0] = now
+        _ITER[0] = n
+
+    opt._iteration_hook = hook
+    m = opt.optimize()
+    return walls, m.getParameters()[0][:opt._step.total].clone()
+
+
+def test_straggler_cancellation_bounds_iteration_time():
+    """Straggler drop that saves time (reference DistriOptimizer.scala:241-278 invokeAndWait2 with a timeout): once
+    the drop threshold is set, a rank past its deadline raises at the next module boundary, contributes a zero
+    gradient with weight 0 and enters the collective on time. Rank 1 sleeps 10 x 0.2 s per iteration after
+    iteration 8: rank 0's iterations stay far below the 2 s it would wait for a full straggler iteration."""
+    res = run_distributed(_straggle_job, 2, timeout=600)
+    (w0, p0), (w1, p1) = res
+    assert torch.equal(p0, p1)
+    late = [w0[n] for n in range(10, 15) if n in w0]
+    assert late and max(late) < 1.0, w0          # a full straggler iteration would be >= 2 s
+    assert min(late) > 0.15, w0                  # the straggler did nap (the scenario ran)
