@@ -35,6 +35,9 @@ def parse():
     ap.add_argument("--graph", type=int, default=1, help="capture the training step in a HIP graph")
     ap.add_argument("--bucket", type=int, default=8, help="gradient bucket size, M elements (N > 1)")
     ap.add_argument("--profile-steps", type=int, default=0)
+    ap.add_argument("--graph-model", action="store_true",
+                    help="build the Graph-form ResNet (ResNet.graph: nn.Graph over nodes) instead of the Sequential "
+                         "one; training fusion is planned on the graph's edges")
     ap.add_argument("--via-optimizer", action="store_true",
                     help="drive the step through the user-facing Optimizer(...).optimize() loop (host batches fed "
                          "through its pinned double-buffered H2D feed, iteration captured in HIP graphs)")
@@ -105,13 +108,13 @@ def main():
     Engine.init(master=f"local[{world}]", dist=world > 1 or force)
 
     from bigdl_amd import nn
-    from bigdl_amd.models.resnet import DatasetType, ResNet
+    from bigdl_amd.models.resnet import DatasetType, ResNet, ResNetGraph
     from bigdl_amd.optim.sgd import SGD
     from bigdl_amd.optim.train_step import TrainStep
     from bigdl_amd.utils.random_generator import RNG
 
     RNG.setSeed(1234 + rank)
-    model = ResNet(1000, args.depth, dataSet=DatasetType.ImageNet)
+    model = (ResNetGraph if args.graph_model else ResNet)(1000, args.depth, dataSet=DatasetType.ImageNet)
     crit = nn.CrossEntropyCriterion()
     optim = SGD(learningRate=0.1, momentum=0.9, dampening=0.0)
     step = None
@@ -134,7 +137,7 @@ def main():
                 "n_gpus": world, "steps": args.steps, "warmup": max(args.warmup, 3), "ms_per_step": round(ms, 3),
                 "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
                 "data": "synthetic host batches (random 3x224x224 fp32, pinned) through Optimizer.optimize()",
-                "config": {"model": f"ResNet-{args.depth} v1.5 (BigDL ImageNet builder)", "global_batch": B * world,
+                "config": {"model": f"ResNet-{args.depth} v1.5 (BigDL ImageNet builder{', Graph form' if args.graph_model else ''})", "global_batch": B * world,
                            "per_gpu_batch": B, "seq_len": None, "image": args.image, "parallelism": f"dp{world}",
                            "driver": "Optimizer.optimize()", "hip_graph": opt._graph is not None or "released",
                            "loss": float(opt.state.get("Loss", float("nan")))},
@@ -210,7 +213,7 @@ def main():
             "vs_baseline": (round(ips / BASELINE, 4) if BASELINE else None),
             "dtype": "bf16",
             "data": "synthetic (random 3x224x224 images, random labels; random-init weights)",
-            "config": {"model": f"ResNet-{args.depth} v1.5 (BigDL ImageNet builder)", "global_batch": B * world,
+            "config": {"model": f"ResNet-{args.depth} v1.5 (BigDL ImageNet builder{', Graph form' if args.graph_model else ''})", "global_batch": B * world,
                        "per_gpu_batch": B, "seq_len": None, "image": args.image, "parallelism": f"dp{world}",
                        "optimizer": "SGD momentum 0.9 + L2 1e-4 (ZeRO-1 sharded over RCCL)",
                        "hip_graph": graph is not None, "bucketed_overlap": step.bucketed is not None,

@@ -27,7 +27,22 @@ from .normalization import BatchNormalization
 from .table_ops import CAddTable
 
 
+_TRAIN_NODE_ATTRS = ("res_src", "pass_index", "fold_fanout", "fold_bn")
+
+
 def _reset(m):
+    from .graph import Graph
+
+    for x in [m] + list(m.flattened_layers()):
+        if isinstance(x, Graph) and getattr(x, "_order0", None) is not None:
+            x.order = x._order0
+            x._order0 = None
+        if isinstance(x, Graph):
+            for n in x.order:
+                for a in _TRAIN_NODE_ATTRS:
+                    n.__dict__.pop(a, None)
+        if isinstance(x, BatchNormalization):
+            x._graph_dres = False
     for x in m.flattened_layers():
         for attr, val in (("emit_stats", False), ("fuse_relu", False), ("passthrough", False),
                           ("_dgrad_bn_ok", False)):
@@ -45,11 +60,124 @@ def _dgrad_bn_enabled():
 
 
 def fuse_for_training(model):
+    from .graph import DynamicGraph, Graph
+
     _reset(model)
     for m in model.flattened_layers():
         if isinstance(m, Sequential):
             _fuse_sequential(m)
+        elif isinstance(m, Graph) and not isinstance(m, DynamicGraph) and not getattr(m, "_inference_fused", False):
+            _fuse_graph_training(m)
     return model
+
+
+def _fuse_graph_training(g):
+    """Training fusion of an nn.Graph (ResNet.graph, Inception, Caffe / TF / ONNX imports): the pairwise plans of
+    _fuse_sequential decided on the graph's edges instead of list neighbours — a producer is fused with its
+    consumer only when that consumer is the producer's ONLY user and the producer is not a graph output
+    (reference: the DnnGraph compile fuses any container, S/nn/mkldnn/DnnGraph.scala:310-409, Fusion.scala:60-217):
+      conv -> BN            the conv epilogue emits the BN statistics
+      BN -> ReLU            ReLU in the BN apply pass (and its mask in the BN backward); the ReLU passes through
+      conv/Linear -> ReLU   ReLU in the GEMM epilogue
+      BN -> ReLU -> conv    the conv's data-gradient epilogue reduces the BN's backward statistics (the conv is the
+                            only user of the ReLU output, so its dgrad is that BN's complete output gradient)
+    The ResNet block's residual plan (shortcut add inside the last BN pass) stays Sequential-only."""
+    users = _graph_users(g)
+    outs = {n.id for n in g.output_nodes}
+    _plan_graph_residuals(g, users, outs)
+
+    def only_user(n):
+        us = users.get(n.id, [])
+        ok = (len(us) == 1 and n.id not in outs and len(us[0].prevs) == 1 and us[0].prev_index[0] is None
+              and not (n.element.hasName() and n.element.getName() in g._stop_grad))
+        return us[0] if ok else None
+
+    for n in g.order:
+        m, u = n.element, only_user(n)
+        if u is None:
+            continue
+        c = u.element
+        if isinstance(m, SpatialConvolution) and isinstance(c, BatchNormalization) and m.nGroup == 1:
+            m.emit_stats = True
+        elif isinstance(m, BatchNormalization) and isinstance(c, ReLU):
+            m.fuse_relu = True
+            c.passthrough = True
+        elif isinstance(m, (SpatialConvolution, Linear)) and isinstance(c, ReLU):
+            m.fuse_relu = True
+            c.passthrough = True
+    _plan_fanout_folds(g, users)
+    if not _dgrad_bn_enabled():
+        return
+    for n in g.order:
+        m, u = n.element, only_user(n)
+        if not (isinstance(m, BatchNormalization) and m.fuse_relu and u is not None and isinstance(u.element, ReLU)
+                and u.element.passthrough):
+            continue
+        v = only_user(u)
+        if v is not None and isinstance(v.element, SpatialConvolution) and v.element.nGroup == 1:
+            v.element._dgrad_bn_ok = True
+
+
+def _stopped(g, n):
+    return n.element.hasName() and n.element.getName() in g._stop_grad
+
+
+def _plan_graph_residuals(g, users, outs):
+    """BN -> CAddTable(BN, shortcut) -> ReLU: the BN adds the shortcut and applies the ReLU in its apply pass and
+    returns the shortcut's (masked) gradient from its backward pass; the add passes its BN input on and the ReLU
+    passes through — the Graph form of the Sequential residual plan (reference ResNet.graph, models/resnet)."""
+    for a in list(g.order):
+        if not isinstance(a.element, CAddTable) or len(a.prevs) != 2 or any(k is not None for k in a.prev_index):
+            continue
+        ua = users.get(a.id, [])
+        if (len(ua) != 1 or a.id in outs or _stopped(g, a) or not isinstance(ua[0].element, ReLU)
+                or len(ua[0].prevs) != 1 or ua[0].prev_index[0] is not None):
+            continue
+        for ib in (0, 1):
+            b, sc = a.prevs[ib], a.prevs[1 - ib]
+            bn = b.element
+            if (b is sc or not isinstance(bn, BatchNormalization) or users.get(b.id) != [a] or b.id in outs
+                    or _stopped(g, b) or bn.fuse_relu or bn.nOutput % 8 != 0 or getattr(b, "res_src", None)):
+                continue
+            order = g.order
+            if order.index(sc) > order.index(b):
+                # the shortcut must exist when the BN runs: move the BN right after it (its only consumer is
+                # the add, which follows both)
+                if getattr(g, "_order0", None) is None:
+                    g._order0 = list(order)
+                order.remove(b)
+                order.insert(order.index(sc) + 1, b)
+            bn.fuse_relu = True
+            bn._graph_dres = True
+            b.res_src = sc
+            a.pass_index = ib + 1
+            ua[0].element.passthrough = True
+            break
+
+
+def _plan_fanout_folds(g, users):
+    """A tensor read by several nodes: the consumer processed LAST in backward (first in forward order) is a conv
+    whose data-gradient epilogue adds the other consumers' summed gradient (the residual_backward fold of the
+    Sequential plan, for any fan-out)."""
+    pos = {n.id: i for i, n in enumerate(g.order)}
+    contrib = {}
+    for n in g.order:
+        rs = getattr(n, "res_src", None)
+        if rs is not None:
+            contrib.setdefault(rs.id, []).append(n)
+    for p in g.order:
+        us = [u for u in users.get(p.id, []) if getattr(u, "pass_index", None) is None]
+        srcs = us + contrib.get(p.id, [])
+        if len(srcs) < 2:
+            continue
+        c = min(srcs, key=lambda u: pos[u.id])
+        cv = c.element
+        if (c not in us or len(c.prevs) != 1 or c.prev_index[0] is not None or _stopped(g, c)
+                or not isinstance(cv, SpatialConvolution) or cv.nGroup != 1 or not cv.propagateBack
+                or cv.format != "NCHW" or cv.nInputPlane % 8 != 0):
+            continue
+        c.fold_fanout = True
+        c.fold_bn = _dgrad_bn_enabled()
 
 
 def unfuse(model):

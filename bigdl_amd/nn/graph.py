@@ -154,6 +154,15 @@ class Graph(Container):
             pre = getattr(n, "fuse_pre", None)   # inference fusion hook (nn.fusion.fuse_graph_for_inference)
             if pre is not None:
                 pre(outs, x)
+            # training residual fusion (nn.fusion._fuse_graph_training): this BN adds the shortcut node's output
+            # (and applies the ReLU) in its own pass; the CAddTable after it only passes that result on
+            rs = getattr(n, "res_src", None)
+            if rs is not None:
+                n.element._graph_residual = outs[rs.id]
+            pi = getattr(n, "pass_index", None)
+            if pi is not None:
+                outs[n.id] = x[pi]
+                continue
             run = getattr(n, "fuse_run", None)   # planned runner (quantized.int8_graph) replacing forward
             outs[n.id] = run(x) if run is not None else n.element.forward(x)
         self._outs = outs
@@ -178,6 +187,12 @@ class Graph(Container):
                 continue
             x = self._node_inputs[n.id]
             m = n.element
+            pi = getattr(n, "pass_index", None)
+            if pi is not None:           # fused residual add: the BN producing input ``pi`` owns the ReLU mask
+                p = n.prevs[pi - 1]
+                grads[p.id] = add_edge_grad(grads.get(p.id), g, None)
+                continue
+            folded = self._fold_fanout(n, m, x, grads) if upd_input else False
             if acc_params and upd_input:
                 gi = m.backward(x, g)
             elif upd_input:
@@ -185,7 +200,16 @@ class Graph(Container):
             else:
                 m.accGradParameters(x, g)
                 gi = m.gradInput
+            rs = getattr(n, "res_src", None)
+            if rs is not None:           # the shortcut's gradient: the ReLU-masked output gradient of the fused BN
+                d = m.__dict__.pop("_dres", None)
+                if d is None:
+                    d = g * (m.output > 0).to(g.dtype)
+                grads[rs.id] = add_edge_grad(grads.get(rs.id), d, None)
             if m.hasName() and m.getName() in self._stop_grad:
+                continue
+            if folded:                   # gi already holds the sum over every consumer of the input
+                grads[n.prevs[0].id] = gi
                 continue
             if n in self.inputs_nodes:
                 if len(self.inputs_nodes) == 1:
@@ -203,6 +227,23 @@ class Graph(Container):
                     grads[p.id] = add_edge_grad(grads.get(p.id), gi[i + 1] if gi is not None else None,
                                                 n.prev_index[i])
         return gin
+
+    @staticmethod
+    def _fold_fanout(n, m, x, grads):
+        """A conv that is the last consumer (in backward order) of a fanned-out tensor sums the gradient the other
+        consumers already produced inside its data-gradient epilogue instead of a separate add pass (planned by
+        nn.fusion._fuse_graph_training as ``node.fold_fanout``)."""
+        if not getattr(n, "fold_fanout", False):
+            return False
+        acc = grads.get(n.prevs[0].id)
+        if not (isinstance(acc, torch.Tensor) and isinstance(x, torch.Tensor) and acc.is_cuda
+                and acc.dtype == x.dtype and acc.shape == x.shape
+                and acc.is_contiguous(memory_format=torch.channels_last)):
+            return False
+        m._dgrad_addend = acc
+        # the result is the input's complete gradient: a BN that produced it may reduce in this epilogue
+        m._dgrad_bn_once = n.fold_bn
+        return True
 
     def backward(self, input, gradOutput):
         t0 = time.perf_counter_ns()

@@ -101,6 +101,8 @@ class BatchNormalization(TensorModule):
         return x
 
     def updateOutput(self, input, residual=None):
+        if residual is None:     # a Graph's fused residual add (nn.fusion._fuse_graph_training)
+            residual = self.__dict__.pop("_graph_residual", None)
         x = self._to_nchw(input)
         if self._gpu_ok(x):
             stats = getattr(input, "_bn_stats", None) if self.train else None
@@ -147,9 +149,12 @@ class BatchNormalization(TensorModule):
         db = self.gradBias if direct else (torch.zeros_like(self.runningMean) if self.affine else None)
         pre = getattr(gradOutput, "_bn_red", None)
         red = pre[1] if (pre is not None and pre[0] is self and self.train) else None
+        graph_res = getattr(self, "_graph_dres", False)
         dx, dres = bnops.bn_backward_gpu(gz, z, x, self.saveMean, self.saveStd, self.weight, dg, db,
-                                         training=self.train, need_dres=need_dres,
+                                         training=self.train, need_dres=need_dres or graph_res,
                                          sync_fn=self.sync_fn if self.train else None, aff=aff, red=red)
+        if graph_res:
+            self._dres = dres
         if not direct and self.affine and not self._frozen:
             self.gradWeight.add_(dg, alpha=self.scaleW)
             self.gradBias.add_(db, alpha=self.scaleB)

@@ -2,13 +2,22 @@
 collective launch / wait, with the RCCL calls themselves re-issued eagerly between the graph launches.
 
 Why not one graph with the collectives inside: a capture that forks onto RCCL's stream (async reduce-scatter in
-flight while the next layers' backward kernels are captured on the compute stream) replays with corrupted
-results on this ROCm 7 / PyTorch 2.10 stack — measured by ``tools/diag_overlap*.py``: an in-flight side-stream
-branch, even a trivial ``mul_(1.0)`` on a disjoint range, made the kernels captured after the fork produce wrong
-gradients (and NaNs), while eager execution with the same overlap and a capture whose collectives are joined
-immediately were bit-exact. Cutting the step at the collectives keeps every captured graph a single stream;
-overlap still happens because a collective issued between two graph launches runs on RCCL's stream while the
-next graph runs on the compute stream.
+flight while the next layers' backward kernels are captured on the compute stream) replays with wrong results on
+this ROCm 7.0 / PyTorch 2.10 stack. Localised by ``tools/diag_fork_graph.py`` (1 rank, the training step as ONE
+graph, the reduce-scatter replaced by a side-stream branch; weights after 3 replays vs 6 eager steps):
+  * pure PyTorch chains with a forked branch, joined at the end or in the middle of the chain: exact;
+  * the training step with a branch that launches NO kernel (fork + join only): exact (fp32-atomic noise, 7e-9);
+  * the same branch forked only after the last backward kernel (no backward kernel beside it): exact;
+  * a branch with ANY kernel (even ``mul_`` on a tensor the step never touches) beside the backward kernels:
+    max |dw| 1.5e-3 on 99.9 % of the weights, the same value on every run (deterministic, not a timing race);
+    the same with every memset node replaced by a kernel, and with record_stream on the branch's tensors;
+  * eager execution with the same overlapping side-stream kernel: exact (tools/diag_overlap.py eager_ov_fake).
+So the fault needs a graph with parallel branches whose kernel nodes are this step's kernels (large-kernarg
+implicit-GEMM / BN kernels from our code object) — it is not a data race in those kernels (eager overlap is
+exact) nor allocator reuse (the branch touches a pre-capture tensor); we could not reduce it to pure PyTorch.
+Cutting the step at the collectives keeps every captured graph a single stream; overlap still happens because a
+collective issued between two graph launches runs on RCCL's stream while the next graph runs on the compute
+stream.
 
 Replay cost is one ``hipGraphLaunch`` per segment plus the eager collective calls (a few µs each, all async): for
 ResNet-50 with 8M-element buckets that is ~15 launches per step instead of ~1,400 kernel launches.

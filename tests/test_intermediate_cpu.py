@@ -82,3 +82,73 @@ def test_graph_inference_fusion_plan_cpu():
     convs = [n for n in cg.order if n.fuse_pre is not None and type(n.element).__name__ == "SpatialConvolution"]
     assert convs and all(pos[pool.id] < pos[c.id] for c in convs if c.id != cg.order[1].id), order
     assert torch.allclose(cg.forward(x), ref, atol=1e-5)
+
+
+def test_graph_training_fusion_plans_on_single_consumer_edges():
+    """nn.fusion._fuse_graph_training: producers fuse only into their ONLY consumer; a fanned-out conv output,
+    a graph output and a DynamicGraph are left alone."""
+    from bigdl_amd import nn
+    from bigdl_amd.nn.fusion import fuse_for_training
+
+    inp = nn.Input()
+    c1 = nn.SpatialConvolution(3, 8, 3, 3, 1, 1, 1, 1)
+    b1 = nn.SpatialBatchNormalization(8)
+    r1 = nn.ReLU()
+    c2 = nn.SpatialConvolution(8, 8, 3, 3, 1, 1, 1, 1)
+    b2 = nn.SpatialBatchNormalization(8)
+    c3 = nn.SpatialConvolution(8, 8, 1, 1)          # c2's output fans out to b2 and c3: no stats epilogue
+    n1 = r1(b1(c1(inp)))
+    n2 = c2(n1)
+    out = nn.CAddTable()(b2(n2), c3(n2))
+    g = nn.Graph(inp, out)
+    fuse_for_training(g)
+    assert c1.emit_stats and b1.fuse_relu and r1.passthrough
+    assert c2._dgrad_bn_ok and not c2.emit_stats and not getattr(c3, "_dgrad_bn_ok", False)
+    lin = nn.Linear(4, 4)
+    rl = nn.ReLU()
+    i2 = nn.Input()
+    g2 = nn.Graph(i2, rl(lin(i2)))
+    fuse_for_training(g2)
+    assert lin.fuse_relu and rl.passthrough
+    i3 = nn.Input()
+    l3 = nn.Linear(4, 4)
+    g3 = nn.Graph(i3, [l3(i3)])
+    fuse_for_training(g3)
+    assert not l3.fuse_relu
+
+
+def test_graph_training_fusion_residual_plan_is_exact_on_cpu():
+    """The Graph residual plan (BN adds the shortcut + ReLU, the CAddTable passes through, the shortcut gradient
+    comes from the BN's masked output gradient, downsample BNs reordered after their shortcut) computes the same
+    fp32 forward and gradients as the unfused graph; unfuse restores the order."""
+    import copy
+
+    import torch
+
+    from bigdl_amd import nn
+    from bigdl_amd.models.resnet import DatasetType, ResNetGraph
+    from bigdl_amd.nn.fusion import fuse_for_training, unfuse
+    from bigdl_amd.utils.random_generator import RNG
+
+    RNG.setSeed(3)
+    base = ResNetGraph(10, 20, dataSet=DatasetType.CIFAR10)
+    torch.manual_seed(0)
+    x, y = torch.randn(4, 3, 32, 32), torch.randint(1, 11, (4,)).float()
+    res = []
+    for fused in (False, True):
+        m = copy.deepcopy(base)
+        if fused:
+            order = list(m.order)
+            fuse_for_training(m)
+            assert sum(getattr(n, "pass_index", None) is not None for n in m.order) == 9
+            assert m.order != order
+        c = nn.CrossEntropyCriterion()
+        o = m.forward(x)
+        c.forward(o, y)
+        gi = m.backward(x, c.backward(o, y))
+        res.append((o.clone(), torch.cat([t.reshape(-1) for t in m.parameters()[1]]).clone()))
+        if fused:
+            unfuse(m)
+            assert m.order == order and all(getattr(n, "pass_index", None) is None for n in m.order)
+    assert torch.allclose(res[0][0], res[1][0], atol=1e-5)
+    assert torch.allclose(res[0][1], res[1][1], atol=1e-5)
