@@ -32,7 +32,9 @@ def parse():
     ap.add_argument("--image", type=int, default=224)
     ap.add_argument("--depth", type=int, default=50)
     ap.add_argument("--compress", default=None, choices=[None, "bf16"])
-    ap.add_argument("--graph", type=int, default=1, help="capture the training step in a HIP graph")
+    ap.add_argument("--graph", type=int, default=-1,
+                    help="1: capture the training step in HIP graphs, 0: eager launches, -1 (default): time both "
+                         "during warm-up and keep the faster")
     ap.add_argument("--bucket", type=int, default=8, help="gradient bucket size, M elements (N > 1)")
     ap.add_argument("--profile-steps", type=int, default=0)
     ap.add_argument("--graph-model", action="store_true",
@@ -68,7 +70,7 @@ def _via_optimizer(args, model, crit, optim, dev, world, rank):
         def size(self):
             return B * world * 10000
 
-    W, K = max(args.warmup, 3), args.steps
+    W, K = max(args.warmup, 6), args.steps     # 2 eager + capture + 3 replays: graph-or-eager decided before timing
     marks = {}
 
     def hook(neval):
@@ -109,6 +111,7 @@ def main():
 
     from bigdl_amd import nn
     from bigdl_amd.models.resnet import DatasetType, ResNet, ResNetGraph
+    from bigdl_amd.ops import side_stream
     from bigdl_amd.optim.sgd import SGD
     from bigdl_amd.optim.train_step import TrainStep
     from bigdl_amd.utils.random_generator import RNG
@@ -134,12 +137,13 @@ def main():
         if rank == 0:
             print(json.dumps({
                 "metric": METRIC, "value": round(B * world * args.steps / dt, 2), "unit": "images/sec",
-                "n_gpus": world, "steps": args.steps, "warmup": max(args.warmup, 3), "ms_per_step": round(ms, 3),
+                "n_gpus": world, "steps": args.steps, "warmup": max(args.warmup, 6), "ms_per_step": round(ms, 3),
                 "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
                 "data": "synthetic host batches (random 3x224x224 fp32, pinned) through Optimizer.optimize()",
                 "config": {"model": f"ResNet-{args.depth} v1.5 (BigDL ImageNet builder{', Graph form' if args.graph_model else ''})", "global_batch": B * world,
                            "per_gpu_batch": B, "seq_len": None, "image": args.image, "parallelism": f"dp{world}",
-                           "driver": "Optimizer.optimize()", "hip_graph": opt._graph is not None or "released",
+                           "driver": "Optimizer.optimize()", "hip_graph": opt._graph is not None,
+                           "graph_vs_eager": getattr(opt, "graph_decision", None),
                            "loss": float(opt.state.get("Loss", float("nan")))},
             }), flush=True)
         Engine.shutdown()
@@ -157,28 +161,52 @@ def main():
 
     run = lambda: step.step(x, y)  # noqa: E731
     graph = None
-    if args.graph and (world > 1 or force):
+    decision = None
+    mode = args.graph            # 1 graph, 0 eager, -1 auto: time both during warm-up, keep the faster
+    if mode and (world > 1 or force):
         import torch.distributed as dist
 
         if dist.get_backend() != "nccl":
             # gloo collectives (single-GPU multi-rank rehearsal) run on the host: nothing to capture
             print("[bench] non-RCCL backend: eager launches", file=sys.stderr)
-            args.graph = 0
-    if args.graph:
+            mode = 0
+    for _ in range(max(args.warmup, 2)):
+        run()
+
+    def timed(fn, n=2):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(n):
+            fn()
+        e1.record()
+        e1.synchronize()
+        return e0.elapsed_time(e1) / n
+
+    if mode:
         from bigdl_amd.optim.graphed import GraphedTrainStep
 
+        eager_ms = timed(run) if mode < 0 else None
         try:
-            graph = GraphedTrainStep(step, x, y, warmup=max(args.warmup, 2))
+            graph = GraphedTrainStep(step, x, y, prewarmed=True)
+            graph.replay()
+            graph_ms = timed(graph.replay)
             run = graph.replay  # noqa: F811
-            for _ in range(2):
-                run()
         except Exception as e:  # fall back to eager launches
             print(f"[bench] HIP graph capture failed ({type(e).__name__}: {e}); running eager", file=sys.stderr)
             graph = None
-            run = lambda: step.step(x, y)  # noqa: E731
-    else:
-        for _ in range(max(args.warmup, 2)):
-            run()
+        if mode < 0 and graph is not None:
+            t = torch.tensor([eager_ms, graph_ms], device=dev)
+            if world > 1:
+                import torch.distributed as dist
+
+                dist.all_reduce(t)
+            eager_ms, graph_ms = (float(v) / world for v in t.cpu())
+            decision = {"eager_ms": round(eager_ms, 3), "graph_ms": round(graph_ms, 3)}
+            if graph_ms >= 0.99 * eager_ms:
+                graph.release()
+                graph = None
+                run = lambda: step.step(x, y)  # noqa: E731
+                run()
     torch.cuda.synchronize()
 
     barrier()
@@ -216,7 +244,8 @@ def main():
             "config": {"model": f"ResNet-{args.depth} v1.5 (BigDL ImageNet builder{', Graph form' if args.graph_model else ''})", "global_batch": B * world,
                        "per_gpu_batch": B, "seq_len": None, "image": args.image, "parallelism": f"dp{world}",
                        "optimizer": "SGD momentum 0.9 + L2 1e-4 (ZeRO-1 sharded over RCCL)",
-                       "hip_graph": graph is not None, "bucketed_overlap": step.bucketed is not None,
+                       "hip_graph": graph is not None, "graph_vs_eager": decision,
+                       "wgrad_side_stream": side_stream.enabled(), "bucketed_overlap": step.bucketed is not None,
                        "grad_compress": args.compress, "final_loss": round(loss, 4)},
         }), flush=True)
     Engine.shutdown()

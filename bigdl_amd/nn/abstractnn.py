@@ -18,6 +18,7 @@ import time
 
 import torch
 
+from ..ops import side_stream as _side
 from ..utils.table import Table
 
 _REGISTRY = {}
@@ -103,6 +104,7 @@ class StragglerTimeout(RuntimeError):
 # [deadline in time.perf_counter() seconds, 0 = none]: checked by every module forward / backward (one float
 # compare), set by the Optimizer loop while a straggler threshold is active
 STRAGGLER_DEADLINE = [0.0]
+_BWD_DEPTH = [0]
 
 
 def _sync_wrap(kind, f):
@@ -136,18 +138,24 @@ def _sync_wrap(kind, f):
             dl = STRAGGLER_DEADLINE[0]
             if dl and time.perf_counter() > dl:
                 raise StragglerTimeout(self.getPrintName())
-            s = self.__dict__.get("_sync")
-            if s is None:
-                return f(self, *args, **kw)
-            d = self.__dict__.get(key, 0)
-            self.__dict__[key] = d + 1
+            _BWD_DEPTH[0] += 1
             try:
-                out = f(self, *args, **kw)
+                s = self.__dict__.get("_sync")
+                if s is None:
+                    return f(self, *args, **kw)
+                d = self.__dict__.get(key, 0)
+                self.__dict__[key] = d + 1
+                try:
+                    out = f(self, *args, **kw)
+                finally:
+                    self.__dict__[key] = d
+                if d == 0:
+                    s.after_backward(self)
+                return out
             finally:
-                self.__dict__[key] = d
-            if d == 0:
-                s.after_backward(self)
-            return out
+                _BWD_DEPTH[0] -= 1
+                if _BWD_DEPTH[0] == 0 and _side.pending():
+                    _side.join()     # gradients final when the outermost backward returns (ops/side_stream.py)
     wrapped.__name__, wrapped.__qualname__, wrapped.__doc__ = f.__name__, f.__qualname__, f.__doc__
     wrapped.__wrapped__ = f
     wrapped._sync_wrapped = True

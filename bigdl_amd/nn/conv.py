@@ -21,6 +21,7 @@ from .. import ops
 from ..ops import bn as bnops
 from ..ops import conv as cv
 from ..ops import conv_fn
+from ..ops import side_stream
 from .abstractnn import AutogradModule, TensorModule
 from .init_methods import RandomUniform, Zeros
 
@@ -332,6 +333,24 @@ class SpatialConvolution(TensorModule):
                                  (self.dilationH, self.dilationW))
             parts.append(gi[:, :cin])
         return torch.cat(parts, dim=1).contiguous(memory_format=CL)
+
+    def backward(self, input, gradOutput):
+        side = None if self._frozen else side_stream.stream_for(gradOutput)
+        if side is None:
+            return super().backward(input, gradOutput)
+        import time
+
+        t0 = time.perf_counter_ns()
+        self.gradInput = self.updateGradInput(input, gradOutput)
+        # weight gradient on the side stream, concurrent with the data-gradient chain (ops/side_stream.py)
+        side_stream.begin(side)
+        with torch.cuda.stream(side):
+            self.accGradParameters(input, gradOutput)
+            self._apply_regularizers()
+        side_stream.keep(side, input, gradOutput, self.output, getattr(self, "_x16", None),
+                         *(getattr(self, "_xpair", None) or (None,))[:1])
+        self.backward_time += time.perf_counter_ns() - t0
+        return self.gradInput
 
     def accGradParameters(self, input, gradOutput):
         x = self._nchw(input)

@@ -1,0 +1,79 @@
+"""Weight-gradient GEMMs on a second HIP stream, concurrent with the data-gradient chain.
+
+Reference: the MKL-DNN backward computes a layer's weight gradient (accGradParameters) strictly after its input
+gradient on one thread (S/nn/mkldnn/SpatialConvolution.scala:520-589, S/nn/abstractnn/AbstractModule.scala:282
+backward = updateGradInput then accGradParameters). On MI355X every backward kernel of a batch-256 ResNet runs well
+below both the MFMA and the HBM roofline (latency-bound tiles, profiles/r2_resnet50_pmc_v2.txt: 13-27 % MFMA busy,
+1.5-4 TB/s), and a conv's weight gradient depends on nothing the next layers' backward produces. So the weight
+gradient of every GPU convolution is issued on a side stream that first waits for the compute stream (its inputs
+— the layer input and the output gradient — are ready there), and the data-gradient chain (dgrad GEMM, BN
+backward, next layer) keeps going on the compute stream: the two fill the CUs together.
+
+Ordering rules:
+  * the side stream waits on the compute stream before each weight-gradient launch (inputs ready);
+  * every tensor the side stream reads that the compute stream allocated is ``record_stream``-ed, so the caching
+    allocator does not hand its block to a later compute-stream allocation while the GEMM still reads it;
+  * the compute stream waits for the side stream (``join``) when the OUTERMOST backward returns (the gradients are
+    final for whatever reads them next: the optimizer, a clipping pass, user code), and before a gradient bucket's
+    collective is launched (parallel/bucketed.py);
+  * inside a HIP-graph capture this is an ordinary fork / join of the capture stream.
+On by default (``BIGDL_WGRAD_STREAM=0`` disables): ResNet-50 b256 eager 29.40 -> 27.84 ms/step on one MI355X
+(profiles/r3_wgrad_side_stream_ab.txt); extra side streams or stream priorities measured no better.
+"""
+import os
+
+import torch
+
+_ON = [os.environ.get("BIGDL_WGRAD_STREAM", "1") == "1"]
+_N = max(1, int(os.environ.get("BIGDL_WGRAD_STREAMS", "1")))      # round-robin side streams per device
+_PRIO = int(os.environ.get("BIGDL_WGRAD_PRIO", "0"))
+_STREAMS = {}
+_PENDING = []
+_RR = [0]
+
+
+def enabled():
+    return _ON[0]
+
+
+def set_enabled(on):
+    join()
+    _ON[0] = bool(on)
+
+
+def stream_for(t):
+    """The side stream for CUDA tensor ``t``'s device, or None when disabled / not on the GPU."""
+    if not _ON[0] or not isinstance(t, torch.Tensor) or not t.is_cuda:
+        return None
+    dev = t.device.index if t.device.index is not None else torch.cuda.current_device()
+    ss = _STREAMS.get(dev)
+    if ss is None:
+        ss = _STREAMS[dev] = [torch.cuda.Stream(device=dev, priority=_PRIO) for _ in range(_N)]
+    _RR[0] += 1
+    return ss[_RR[0] % len(ss)]
+
+
+def begin(s):
+    """Make ``s`` wait for the compute stream; returns the compute stream."""
+    cur = torch.cuda.current_stream(s.device)
+    s.wait_stream(cur)
+    if s not in _PENDING:
+        _PENDING.append(s)
+    return cur
+
+
+def keep(s, *ts):
+    for t in ts:
+        if isinstance(t, torch.Tensor) and t.is_cuda:
+            t.record_stream(s)
+
+
+def pending():
+    return bool(_PENDING)
+
+
+def join():
+    """Compute stream waits for every side stream used since the last join."""
+    while _PENDING:
+        s = _PENDING.pop()
+        torch.cuda.current_stream(s.device).wait_stream(s)

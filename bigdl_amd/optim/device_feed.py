@@ -11,6 +11,8 @@ update is in flight). MI355X design:
     event (a device-side dependency: the host never blocks on the copy);
   * ``record_stream`` tells the caching allocator that the device tensors are used on the compute stream, so their
     blocks are not recycled by the copy stream while the step still reads them.
+  * a raw batch (``on_device``, dataset/seqfile_stream.py) is finished on the device right after its copy, on the
+    copy stream: the host ships uint8 records and the preprocessing kernel overlaps the running step.
 On the CPU engine the feed is the host-thread prefetch alone.
 """
 import queue
@@ -69,7 +71,7 @@ class DeviceFeed:
                 if self._stop:
                     return
                 if self.pin:
-                    mb = type(mb)(_map(mb.getInput(), _pin), _map(mb.getTarget(), _pin))
+                    mb = _rebuild(mb, _map(mb.getInput(), _pin), _map(mb.getTarget(), _pin))
                 self._q.put(mb)
         except BaseException as e:  # noqa: BLE001 - re-raised in the consumer
             self._err = e
@@ -89,10 +91,14 @@ class DeviceFeed:
     def _issue(self):
         mb = self._take_host()
         if not self.cuda:
-            return mb, None
+            fin = getattr(mb, "on_device", None)
+            return (fin() if fin is not None else mb), None
         with torch.cuda.stream(self.stream):
-            dev = type(mb)(_map(mb.getInput(), lambda t: t.to(self.device, non_blocking=True)),
+            dev = _rebuild(mb, _map(mb.getInput(), lambda t: t.to(self.device, non_blocking=True)),
                            _map(mb.getTarget(), lambda t: t.to(self.device, non_blocking=True)))
+            fin = getattr(dev, "on_device", None)
+            if fin is not None:      # raw batch (dataset/seqfile_stream.py): finished by a kernel on this stream
+                dev = fin()
             ev = torch.cuda.Event()
             ev.record(self.stream)
         self.h2d_issued += 1
@@ -130,6 +136,12 @@ class DeviceFeed:
                 self._q.get_nowait()
         except queue.Empty:
             pass
+
+
+def _rebuild(mb, inp, tgt):
+    """Same batch type over new tensors (``rebuild`` keeps a raw batch's configuration)."""
+    fn = getattr(mb, "rebuild", None)
+    return fn(inp, tgt) if fn is not None else type(mb)(inp, tgt)
 
 
 def _pin(t):

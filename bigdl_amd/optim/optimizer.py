@@ -341,12 +341,32 @@ class Optimizer:
         ``bigdl.optim.graph`` is not "false"."""
         from .graphed import graphable
 
-        flag = str(Engine.getProperty("bigdl.optim.graph", "true")).lower()
+        flag = str(Engine.getProperty("bigdl.optim.graph", "auto")).lower()
         return step.device.type == "cuda" and drop is None and flag not in ("0", "false", "no") and graphable(step)
+
+    def _graph_keep(self, step, eager_ms, graph_ms):
+        """``bigdl.optim.graph`` = auto (default): keep the captured iteration only if its replays are faster on the
+        device than the timed eager iteration (a launch-bound model gains from the graph; a large-batch model whose
+        eager iteration overlaps its weight-gradient side stream better than the graph's replay does not). The
+        timings are averaged over ranks so every rank takes the same path."""
+        flag = str(Engine.getProperty("bigdl.optim.graph", "auto")).lower()
+        if flag != "auto":
+            return True
+        t = torch.tensor([eager_ms, graph_ms], device=step.device)
+        if step.comm.world > 1:
+            step.comm.all_reduce_scalar(t)
+        eager_ms, graph_ms = (float(v) for v in t.cpu())
+        keep = graph_ms < 0.99 * eager_ms
+        logger.info("iteration on the device: eager %.3f ms, HIP graph %.3f ms -> %s", eager_ms / max(1, step.comm.world),
+                    graph_ms / max(1, step.comm.world), "graph" if keep else "eager")
+        self.graph_decision = {"eager_ms": eager_ms / max(1, step.comm.world),
+                               "graph_ms": graph_ms / max(1, step.comm.world), "graph": keep}
+        return keep
 
     def _train_iterations(self, st, step, world, drop, it, wall0, pending, watchdog):
         use_graph = self._use_graph(step, drop)
         eager_done = 0
+        timing = {}            # device events: the 2nd eager iteration and graph replays 2-3 (auto mode)
         while not self.endWhen(st):
             t0 = time.perf_counter()
             batch = next(it)        # device-resident; its copy was issued during the previous iteration
@@ -368,7 +388,21 @@ class Optimizer:
                     use_graph, g, self._graph = False, None, None
             if g is not None:
                 if isinstance(x, torch.Tensor) and g.matches(x, y):
+                    nrep = timing.get("replays", 0)
+                    timing["replays"] = nrep + 1
+                    if nrep == 1 and "e1" in timing:
+                        timing["g1"] = torch.cuda.Event(enable_timing=True)
+                        timing["g1"].record()
                     loss = g.replay(x, y).detach().clone()   # the graph's loss buffer is rewritten every replay
+                    if nrep == 2 and "g1" in timing:
+                        timing["g3"] = torch.cuda.Event(enable_timing=True)
+                        timing["g3"].record()
+                        timing["g3"].synchronize()
+                        graph_ms = timing["g1"].elapsed_time(timing["g3"]) / 2
+                        eager_ms = timing["e0"].elapsed_time(timing["e1"])
+                        if not self._graph_keep(step, eager_ms, graph_ms):
+                            g.release()
+                            g, self._graph, use_graph = None, None, False
                 else:
                     loss = g.eager(x, y)
                 n_ok = 1
@@ -377,6 +411,9 @@ class Optimizer:
                 loss = torch.zeros((), device=step.device)
                 finished = 0.0
             else:
+                if eager_done == 1 and use_graph:
+                    timing["e0"] = torch.cuda.Event(enable_timing=True)
+                    timing["e0"].record()
                 step.zero_grad()
                 if drop is not None:
                     # straggler cancellation: past the deadline every module boundary raises StragglerTimeout, so
@@ -393,6 +430,9 @@ class Optimizer:
             else:
                 step.sync_and_update(loss)
                 n_ok = 1
+                if "e0" in timing and "e1" not in timing:
+                    timing["e1"] = torch.cuda.Event(enable_timing=True)
+                    timing["e1"].record()
             self.metrics.add("computing time", time.perf_counter() - t1)
             records = batch.size() * world
             pending.append((st["neval"], loss.detach() if torch.is_tensor(loss) else torch.tensor(float(loss)),

@@ -30,6 +30,8 @@ the same module sequence, so every rank launches the buckets in the same order (
 """
 import torch
 
+from ..ops import side_stream as _side
+
 
 def _own_ranges(m, base, es):
     """[lo, hi) element ranges of ``m``'s OWN parameters inside the flat buffer starting at ``base``."""
@@ -206,6 +208,7 @@ class BucketedGradSync:
             return
         b0, b1 = self.bounds[b]
         self.launch_log.append(b)
+        _side.join()     # weight gradients issued on the side stream (ops/side_stream.py) land first
         self.works[b] = self.comm.reduce_scatter_range(self.g, b0, b1, async_op=True)[0]
 
     def after_backward(self, m):

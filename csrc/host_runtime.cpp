@@ -19,6 +19,8 @@
 #include <mutex>
 #include <thread>
 #include <vector>
+#include <string>
+#include <cstdlib>
 
 namespace bigdl_host {
 
@@ -175,6 +177,129 @@ void gather_records(const torch::Tensor& records, const torch::Tensor& indices, 
   pool((int)threads).parallel_for(indices.size(0), [&](int64_t i) { std::memcpy(d + i * rec, s + idx[i] * rec, rec); });
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// Hadoop SequenceFile of BGR image records (reference S/dataset/DataSet.scala SeqFileFolder + BGRImage.readImage;
+// writer dataset/seqfile.py): the whole file is one uint8 tensor, indexed once in C++ so batches are gathered by
+// byte offset with the GIL released — no per-record Python on the training data path.
+// ---------------------------------------------------------------------------------------------------------------
+namespace {
+int64_t read_vlong(const uint8_t* b, int64_t n, int64_t& pos) {
+  TORCH_CHECK(pos < n, "seqfile: truncated vlong");
+  const int8_t first = (int8_t)b[pos++];
+  if (first >= -112) return first;
+  const bool neg = first < -120;
+  const int len = neg ? -(first + 120) : -(first + 112);
+  TORCH_CHECK(pos + len <= n, "seqfile: truncated vlong");
+  int64_t v = 0;
+  for (int i = 0; i < len; ++i) v = (v << 8) | b[pos++];
+  return neg ? (v ^ -1) : v;
+}
+int32_t read_be32(const uint8_t* b, int64_t n, int64_t pos) {
+  TORCH_CHECK(pos + 4 <= n, "seqfile: truncated record");
+  return (int32_t)(((uint32_t)b[pos] << 24) | ((uint32_t)b[pos + 1] << 16) | ((uint32_t)b[pos + 2] << 8) | b[pos + 3]);
+}
+}  // namespace
+
+// -> (records int64 [R, 3] = (pixel byte offset, H, W), labels float32 [R]); Text or BytesWritable values holding
+// (int32 width, int32 height, BGR bytes), keys "label" or "name\nlabel".
+std::vector<torch::Tensor> seqfile_index(const torch::Tensor& buf) {
+  TORCH_CHECK(buf.scalar_type() == at::kByte && buf.dim() == 1 && buf.is_contiguous() && !buf.is_cuda(),
+              "seqfile_index: buf must be a contiguous CPU uint8 vector");
+  const uint8_t* b = buf.data_ptr<uint8_t>();
+  const int64_t n = buf.numel();
+  TORCH_CHECK(n >= 4 && b[0] == 'S' && b[1] == 'E' && b[2] == 'Q' && b[3] >= 6, "seqfile_index: not a SequenceFile v6");
+  int64_t pos = 4;
+  std::string cls[2];
+  for (int i = 0; i < 2; ++i) {
+    const int64_t l = read_vlong(b, n, pos);
+    TORCH_CHECK(l >= 0 && pos + l <= n, "seqfile_index: bad class name");
+    cls[i].assign((const char*)b + pos, (size_t)l);
+    pos += l;
+  }
+  TORCH_CHECK(pos + 2 <= n && b[pos] == 0 && b[pos + 1] == 0, "seqfile_index: compressed SequenceFiles are not supported");
+  pos += 2;
+  const int32_t nmeta = read_be32(b, n, pos);
+  pos += 4;
+  for (int i = 0; i < 2 * nmeta; ++i) {
+    const int64_t l = read_vlong(b, n, pos);
+    pos += l;
+  }
+  TORCH_CHECK(pos + 16 <= n, "seqfile_index: truncated header");
+  const uint8_t* sync = b + pos;
+  pos += 16;
+  const bool val_bytes = cls[1] == "org.apache.hadoop.io.BytesWritable";
+  const bool key_bytes = cls[0] == "org.apache.hadoop.io.BytesWritable";
+  std::vector<int64_t> recs;
+  std::vector<float> labels;
+  while (pos < n) {
+    const int32_t rec_len = read_be32(b, n, pos);
+    pos += 4;
+    if (rec_len == -1) {
+      TORCH_CHECK(pos + 16 <= n && std::memcmp(b + pos, sync, 16) == 0, "seqfile_index: corrupt sync marker at ", pos);
+      pos += 16;
+      continue;
+    }
+    const int32_t key_len = read_be32(b, n, pos);
+    pos += 4;
+    TORCH_CHECK(rec_len >= key_len && key_len >= 0 && pos + rec_len <= n, "seqfile_index: bad record at ", pos);
+    // key text -> label (last line)
+    int64_t kp = pos, kl;
+    if (key_bytes) { kl = read_be32(b, n, kp); kp += 4; } else { kl = read_vlong(b, n, kp); }
+    int64_t ls = kp;
+    for (int64_t i = kp; i < kp + kl; ++i)
+      if (b[i] == '\n') ls = i + 1;
+    std::string lab((const char*)b + ls, (size_t)(kp + kl - ls));
+    labels.push_back((float)std::strtod(lab.c_str(), nullptr));
+    // value -> (w, h, BGR)
+    int64_t vp = pos + key_len, vl;
+    if (val_bytes) { vl = read_be32(b, n, vp); vp += 4; } else { vl = read_vlong(b, n, vp); }
+    TORCH_CHECK(vl >= 8 && vp + vl <= pos + rec_len, "seqfile_index: bad value at ", vp);
+    const int32_t w = read_be32(b, n, vp), h = read_be32(b, n, vp + 4);
+    TORCH_CHECK(w > 0 && h > 0 && (int64_t)w * h * 3 + 8 <= vl, "seqfile_index: image record larger than its value");
+    recs.push_back(vp + 8);
+    recs.push_back(h);
+    recs.push_back(w);
+    pos += rec_len;
+  }
+  const int64_t R = (int64_t)labels.size();
+  auto r = torch::empty({R, 3}, torch::kLong);
+  auto l = torch::empty({R}, torch::kFloat);
+  if (R) {
+    std::memcpy(r.data_ptr<int64_t>(), recs.data(), recs.size() * sizeof(int64_t));
+    std::memcpy(l.data_ptr<float>(), labels.data(), labels.size() * sizeof(float));
+  }
+  return {r, l};
+}
+
+// Gather variable-size records: out[dst_off[i] : dst_off[i] + nbytes[i]] = buf[src_off[i] : ...] (parallel memcpy,
+// GIL released); out is typically a pinned staging buffer that the device feed copies to the GPU.
+void gather_bytes(const torch::Tensor& buf, const torch::Tensor& src_off, const torch::Tensor& nbytes,
+                  const torch::Tensor& dst_off, const torch::Tensor& out, int64_t threads) {
+  TORCH_CHECK(buf.scalar_type() == at::kByte && buf.is_contiguous() && !buf.is_cuda(), "gather_bytes: uint8 CPU buf");
+  TORCH_CHECK(out.scalar_type() == at::kByte && out.is_contiguous() && !out.is_cuda(), "gather_bytes: uint8 CPU out");
+  TORCH_CHECK(src_off.scalar_type() == at::kLong && nbytes.scalar_type() == at::kLong && dst_off.scalar_type() == at::kLong &&
+                  src_off.is_contiguous() && nbytes.is_contiguous() && dst_off.is_contiguous() &&
+                  src_off.numel() == nbytes.numel() && dst_off.numel() == nbytes.numel(),
+              "gather_bytes: int64 offset / size vectors of one length");
+  const int64_t N = nbytes.numel(), nb = buf.numel(), no = out.numel();
+  const int64_t *so = src_off.data_ptr<int64_t>(), *sz = nbytes.data_ptr<int64_t>(), *dof = dst_off.data_ptr<int64_t>();
+  for (int64_t i = 0; i < N; ++i)
+    TORCH_CHECK(so[i] >= 0 && sz[i] >= 0 && so[i] + sz[i] <= nb && dof[i] >= 0 && dof[i] + sz[i] <= no,
+                "gather_bytes: record ", i, " out of range");
+  const uint8_t* s = buf.data_ptr<uint8_t>();
+  uint8_t* d = out.data_ptr<uint8_t>();
+  // 256 KB chunks: a few large images spread over every thread
+  constexpr int64_t CH = 256 << 10;
+  std::vector<int64_t> first(N + 1, 0);
+  for (int64_t i = 0; i < N; ++i) first[i + 1] = first[i] + std::max<int64_t>(1, (sz[i] + CH - 1) / CH);
+  pybind11::gil_scoped_release nogil;
+  pool((int)threads).parallel_for(first[N], [&](int64_t t) {
+    const int64_t i = std::upper_bound(first.begin(), first.end(), t) - first.begin() - 1;
+    const int64_t c0 = (t - first[i]) * CH, c1 = std::min(sz[i], c0 + CH);
+    if (c1 > c0) std::memcpy(d + dof[i] + c0, s + so[i] + c0, (size_t)(c1 - c0));
+  });
+}
+
 int64_t pool_size(int64_t threads) { return pool((int)threads).size() + 1; }
 
 }  // namespace bigdl_host
@@ -186,4 +311,8 @@ void register_host_runtime(pybind11::module& m) {
   m.def("gather_records", &bigdl_host::gather_records, pybind11::arg("records"), pybind11::arg("indices"),
         pybind11::arg("out"), pybind11::arg("threads") = 0);
   m.def("host_pool_size", &bigdl_host::pool_size, pybind11::arg("threads") = 0);
+  m.def("seqfile_index", &bigdl_host::seqfile_index, pybind11::arg("buf"),
+        "index a SequenceFile of BGR image records: ((pixel offset, H, W) int64 [R, 3], labels float32 [R])");
+  m.def("gather_bytes", &bigdl_host::gather_bytes, pybind11::arg("buf"), pybind11::arg("src_off"),
+        pybind11::arg("nbytes"), pybind11::arg("dst_off"), pybind11::arg("out"), pybind11::arg("threads") = 0);
 }

@@ -60,3 +60,33 @@ def test_op_codes_cover_each_transform():
         out = pipe([img], [p]).cpu()[0]
         ref = pipe.host_reference(img, p)
         assert float((out - ref).abs().mean()) < 1e-3, op
+
+
+def test_seqfile_stream_raw_batch_finished_on_device_matches_host(tmp_path):
+    """SeqFile stream (native index + pinned gather) -> DeviceFeed copy stream -> preprocessing kernel, vs the
+    host transformer math on the same raw batch."""
+    import os
+
+    from bigdl_amd.dataset.image import encode_bgr_record
+    from bigdl_amd.dataset.seqfile import SequenceFileWriter
+    from bigdl_amd.dataset.seqfile_stream import SeqFileImageStream, _host_pipeline
+    from bigdl_amd.optim.device_feed import DeviceFeed
+
+    g = torch.Generator().manual_seed(2)
+    p = os.path.join(str(tmp_path), "a.seq")
+    with SequenceFileWriter(p) as w:
+        for i in range(12):
+            h, wd = int(torch.randint(40, 90, (1,), generator=g)), int(torch.randint(40, 90, (1,), generator=g))
+            w.append(str(1 + i % 3), encode_bgr_record(torch.randint(0, 256, (h, wd, 3), generator=g,
+                                                                     dtype=torch.uint8)))
+    ds = SeqFileImageStream([p], 6, crop=(32, 32), mean=MEAN, std=STD, rank=0, world=1, threads=4)
+    raw = next(ds.data(train=True))
+    ref = _host_pipeline(*raw.getInput(), 32, 32, MEAN, STD, True)
+    feed = DeviceFeed(iter([raw]), torch.device("cuda"))
+    mb = next(feed)
+    feed.close()
+    out = mb.getInput()
+    assert out.is_cuda and tuple(out.shape) == (6, 3, 32, 32)
+    err = (out.cpu() - ref).abs()
+    assert float(err.max()) < 2e-3, float(err.max())
+    assert torch.equal(mb.getTarget().cpu(), raw.getTarget())
