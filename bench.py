@@ -193,6 +193,7 @@ def main():
             run = graph.replay  # noqa: F811
         except Exception as e:  # fall back to eager launches
             print(f"[bench] HIP graph capture failed ({type(e).__name__}: {e}); running eager", file=sys.stderr)
+            side_stream.reset()
             graph = None
         if mode < 0 and graph is not None:
             t = torch.tensor([eager_ms, graph_ms], device=dev)

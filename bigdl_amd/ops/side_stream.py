@@ -72,6 +72,12 @@ def pending():
     return bool(_PENDING)
 
 
+def reset():
+    """Forget the side streams (after an aborted HIP-graph capture a stream forked into it is not reusable)."""
+    _PENDING.clear()
+    _STREAMS.clear()
+
+
 def join():
     """Compute stream waits for every side stream used since the last join."""
     while _PENDING:

@@ -342,6 +342,11 @@ class Optimizer:
         from .graphed import graphable
 
         flag = str(Engine.getProperty("bigdl.optim.graph", "auto")).lower()
+        if step.comm.active:
+            import torch.distributed as dist
+
+            if dist.get_backend(step.comm.group) != "nccl":
+                return False        # host-side (gloo) collectives cannot be replayed between graph segments
         return step.device.type == "cuda" and drop is None and flag not in ("0", "false", "no") and graphable(step)
 
     def _graph_keep(self, step, eager_ms, graph_ms):
@@ -384,7 +389,10 @@ class Optimizer:
                     g = self._graph = GraphedTrainStep(step, x, y, prewarmed=True)
                     logger.info("training iteration captured in %d HIP graph segment(s)", len(g.graph))
                 except Exception as e:  # noqa: BLE001 - fall back to eager launches
+                    from ..ops import side_stream
+
                     logger.warning("HIP graph capture failed (%s: %s); eager iterations", type(e).__name__, e)
+                    side_stream.reset()
                     use_graph, g, self._graph = False, None, None
             if g is not None:
                 if isinstance(x, torch.Tensor) and g.matches(x, y):

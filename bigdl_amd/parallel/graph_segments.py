@@ -27,6 +27,8 @@ path announces collective boundaries with ``boundary(fn)`` / ``issue(fn)`` (no-o
 """
 import torch
 
+from ..ops import side_stream as _side
+
 _ACTIVE = None
 
 
@@ -100,6 +102,7 @@ class SegmentedGraph:
         self.n_graphs += 1
 
     def boundary(self, fn):
+        _side.join()        # a segment ends with every side-stream fork joined (ops/side_stream.py)
         self._end()
         try:
             out = fn()
