@@ -966,5 +966,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("dh0") = py::none());
   m.def("set_conv_impl", &bigdl_set_conv_impl);
   m.def("get_conv_impl", &bigdl_get_conv_impl);
+  m.def("set_conv_g4", &bigdl_set_conv_g4);
+  m.def("get_conv_g4", &bigdl_get_conv_g4);
   m.attr("arch") = "gfx950";
 }

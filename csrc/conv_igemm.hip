@@ -1471,6 +1471,145 @@ __global__ __launch_bounds__(512, 1) void conv_nt_w8_kernel(ConvArgs a) {
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// 128 x BN (BN = 128 / 64) implicit-GEMM NT tile, 4 waves as 2 x 2, BK = 32 per K-step and NS (3 or 4) LDS-DMA stages
+// of (128 + BN) x 64 B: NS - 1 K-steps stay in flight across every barrier (counted `s_waitcnt vmcnt`, raw s_barrier,
+// never the vmcnt(0) of __syncthreads — cdna_hip_programming.md §5 "Pipelining across barriers"). The pipeline of
+// conv_nt_w8_kernel at the 128 x 128 tile of conv_nt_glds_kernel: 16 KB stages, so NS = 4 leaves room for two
+// workgroups per CU (NS = 3: three) and one workgroup's epilogue overlaps the others' main loops, while the
+// 2-stage glds kernel drains its DMA queue at every K-step barrier. Same 64-byte-row LDS image, source-side swizzle
+// g ^ ((r >> 1) & 3), tap table behind the stages.
+// ------------------------------------------------------------------------------------------------
+template <int BN, int NS>
+__global__ __launch_bounds__(256, NS == 3 ? 3 : 2) void conv_nt_g4_kernel(ConvArgs a) {
+  constexpr int BM = 128, BKS = 32;
+  constexpr int WGM = 2, WGN = 2;
+  constexpr int TM = BM / WGM, TN = BN / WGN;      // 64 x 64 (or 64 x 32) per wave
+  constexpr int MI = TM / 16, NI = TN / 16;
+  constexpr int STAGE = (BM + BN) * BKS;
+  constexpr int AI = BM / 64, BI = BN / 64;        // DMA instructions per thread per stage (4 waves x 16 rows)
+  constexpr int L = AI + BI;
+  constexpr int NH = (4 * TM * TN * 4 <= NS * STAGE * 2) ? 1 : 2;   // epilogue row chunks that fit the stages
+  constexpr int SL = (TM / NH) * TN;
+  static_assert(4 * SL * 4 <= NS * STAGE * 2, "epilogue chunk must fit the stages");
+  __shared__ __attribute__((aligned(1024))) bf16_t lds[NS * STAGE + 3 * CONV_MAX_TAPS];
+  short* taps = reinterpret_cast<short*>(lds + NS * STAGE);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WGN, wn = wave % WGN;
+  const int tiles_n = (a.Ncol + BN - 1) / BN;
+  const int tiles_m = (a.M + BM - 1) / BM;
+  const int nwg = tiles_m * tiles_n;
+  const int bid = xcd_remap(blockIdx.x, nwg);
+  const int tm = bid / tiles_n, tn = bid % tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int nk = a.Kdim / BKS;
+
+  // DMA geometry: instruction j of wave w fills rows (j * 4 + w) * 16 .. +16 (64 B each); lane -> row + (lane >> 2),
+  // slot lane & 3, which holds granule (lane & 3) ^ ((row >> 1) & 3)
+  const int rsub = lane >> 2;
+  const int gsrc = (lane & 3) ^ ((rsub >> 1) & 3);
+  int a_pix[AI], a_h[AI], a_w[AI];
+  const int ohw = a.OH * a.OW;
+#pragma unroll
+  for (int j = 0; j < AI; ++j) {
+    const int m = m0 + (j * 4 + wave) * 16 + rsub;
+    if (m < a.M) {
+      const int nb = m / ohw, rem = m - nb * ohw;
+      const int oh = rem / a.OW, ow = rem - oh * a.OW;
+      a_pix[j] = nb * a.Hs * a.Ws;
+      a_h[j] = oh * a.mul_h;
+      a_w[j] = ow * a.mul_w;
+    } else {
+      a_pix[j] = 0; a_h[j] = -(1 << 28); a_w[j] = -(1 << 28);
+    }
+  }
+  const bf16_t* wrow[BI];
+  bool bvalid[BI];
+#pragma unroll
+  for (int j = 0; j < BI; ++j) {
+    const int n = n0 + (j * 4 + wave) * 16 + rsub;
+    bvalid[j] = n < a.Ncol;
+    wrow[j] = a.wt + (size_t)(bvalid[j] ? n : 0) * a.ldw + gsrc * 8;
+  }
+  if (tid < a.ntaps) {
+    taps[tid] = a.tap_h[tid];
+    taps[CONV_MAX_TAPS + tid] = a.tap_w[tid];
+    taps[2 * CONV_MAX_TAPS + tid] = a.tap_k[tid];
+  }
+  __syncthreads();   // tap table visible (no DMA outstanding yet)
+
+  auto issue = [&](int kt, int buf) {
+    const int k0 = kt * BKS;
+    const int t = k0 / a.Cs;
+    const int cin = k0 - t * a.Cs;
+    const int th = taps[t], tw = taps[CONV_MAX_TAPS + t];
+    const int wk = taps[2 * CONV_MAX_TAPS + t] * a.Cs + cin;
+    const int c = cin + gsrc * 8;
+    bf16_t* A = lds + buf * STAGE;
+    bf16_t* B = A + BM * BKS;
+#pragma unroll
+    for (int j = 0; j < AI; ++j) {
+      const int ch = a_h[j] + th, cw = a_w[j] + tw;
+      const bool ok = (unsigned)ch < (unsigned)a.Hs && (unsigned)cw < (unsigned)a.Ws;
+      const bf16_t* src = ok ? a.src + (unsigned)((a_pix[j] + ch * a.Ws + cw) * a.Cs + c) : g_zero_granule;
+      glds16(src, (LDS_PTR(void))(A + (j * 4 + wave) * 16 * BKS));
+    }
+#pragma unroll
+    for (int j = 0; j < BI; ++j) {
+      const bf16_t* src = bvalid[j] ? wrow[j] + wk : g_zero_granule;
+      glds16(src, (LDS_PTR(void))(B + (j * 4 + wave) * 16 * BKS));
+    }
+  };
+  const int foff = (lane & 15) * BKS + ((((lane >> 4) ^ ((lane >> 1) & 3))) << 3);
+
+  v4f acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+
+  // prologue: K-steps 0 .. NS - 2 in flight; retire step 0
+#pragma unroll
+  for (int k = 0; k < NS - 1; ++k)
+    if (k < nk) issue(k, k);
+  {
+    const int ahead = min(nk - 1, NS - 2);     // steps in flight behind step 0
+    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * L) : "memory");
+    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(L) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  int cur = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    // stage (kt + NS - 1) % NS == (kt - 1) % NS was last read in step kt - 1, before the barrier that ended it
+    if (kt + NS - 1 < nk) issue(kt + NS - 1, cur == 0 ? NS - 1 : cur - 1);
+    const bf16_t* A = lds + cur * STAGE;
+    const bf16_t* B = A + BM * BKS;
+    v8s fa[MI], fb[NI];
+#pragma unroll
+    for (int j = 0; j < NI; ++j) fb[j] = *reinterpret_cast<const v8s*>(B + (wn * TN + j * 16) * BKS + foff);
+#pragma unroll
+    for (int i = 0; i < MI; ++i) fa[i] = *reinterpret_cast<const v8s*>(A + (wm * TM + i * 16) * BKS + foff);
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+    // retire step kt + 1 (later steps stay in flight); order every wave's reads of this stage and its DMA before
+    // anything after the barrier
+    const int ahead = min(nk - 1, kt + NS - 1) - (kt + 1);
+    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(2 * L) : "memory");
+    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(L) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    cur = cur == NS - 1 ? 0 : cur + 1;
+  }
+  float* wl = reinterpret_cast<float*>(lds) + wave * SL;
+  nt_epilogue_lds<MI, NI, TM, TN, NH, WGN * SL, WGM>(a, acc, m0 + wm * TM, n0 + wn * TN, lane, bid, wl, wm);
+}
+
 // Grid of the split-K epilogue: (row blocks, 256-group channel chunks), ~8 rows per thread, <= 8192 blocks.
 dim3 splitk_grid(long P, int C, long* rpb_out) {
   const int G = C >> 3;
@@ -1645,6 +1784,24 @@ static int w8_pick(const ConvArgs* a) {
   return std::max(split, 1);
 }
 
+template <int BN, int NS>
+void launch_nt_g4(const ConvArgs& a, hipStream_t st) {
+  const int nwg = ((a.M + 127) / 128) * ((a.Ncol + BN - 1) / BN);
+  conv_nt_g4_kernel<BN, NS><<<dim3(nwg), dim3(256), 0, st>>>(a);
+}
+
+// BIGDL_CONV_G4 (default 3): 0 = off, 4 = 4-stage (2 workgroups per CU), 3 = 3-stage (3 per CU) deep-pipelined 128-row kernel
+// in place of the 2-stage LDS-DMA kernel on fast-K (Cs % 32 == 0), aligned-output layers; 5 = the 3-stage kernel
+// also on the deep-K small-grid layers that otherwise take the 256-row 8-wave kernel
+int g_conv_g4 = -1;
+static int g4_pick() {
+  if (g_conv_g4 < 0) {
+    const char* e = getenv("BIGDL_CONV_G4");
+    g_conv_g4 = e ? atoi(e) : 3;   // 3-stage default: ResNet-50 b256 27.35 -> 26.48 ms/step (profiles/r3_conv_g4_ab.txt)
+  }
+  return g_conv_g4;
+}
+
 int g_conv_impl = -1;
 int conv_impl() {
   if (g_conv_impl < 0) {
@@ -1659,6 +1816,8 @@ int conv_impl() {
 extern "C" {
 
 void bigdl_set_conv_impl(int impl) { g_conv_impl = impl; }
+void bigdl_set_conv_g4(int v) { g_conv_g4 = v; }
+int bigdl_get_conv_g4() { return g4_pick(); }
 int bigdl_get_conv_impl() { return conv_impl(); }
 
 // Forward or data-gradient implicit GEMM. Returns 0 on success, negative on unsupported shapes.
@@ -1699,6 +1858,15 @@ int bigdl_conv_nt(const ConvArgs* a, hipStream_t st) {
   } else if (w8 == 1) {
     const int nwg = ((a->M + 255) / 256) * ((a->Ncol + 255) / 256);
     conv_nt_w8_kernel<false><<<dim3(nwg), dim3(512), 0, st>>>(*a);
+  } else if (impl == 1 && g4_pick() && (a->Cs % 32) == 0 && aligned_out &&
+             (g4_pick() == 5 || !(p3_pick && fastk && p3_tiles >= 256))) {
+    if (g4_pick() != 4) {
+      if (a->Ncol <= 64) launch_nt_g4<64, 3>(*a, st);
+      else launch_nt_g4<128, 3>(*a, st);
+    } else {
+      if (a->Ncol <= 64) launch_nt_g4<64, 4>(*a, st);
+      else launch_nt_g4<128, 4>(*a, st);
+    }
   } else if (fastk && p3_pick && p3_tiles >= 256) {
     if (a->Ncol <= 64) launch_nt_p3<64, 8, 1>(*a, st);
     else launch_nt_p3<128, 4, 2>(*a, st);

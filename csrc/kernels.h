@@ -156,6 +156,8 @@ void bigdl_dequantize_rows(const int8_t* q, uint16_t* y, long P, int C, long ld,
 
 void bigdl_set_conv_impl(int impl);
 int bigdl_get_conv_impl();
+void bigdl_set_conv_g4(int v);
+int bigdl_get_conv_g4();
 
 // Input pipeline: crop + flip + channel reorder + normalise of a uint8 [N, H, W, 3] BGR batch.
 // params: int32 [N][3] = (y0, x0, flip). Output fp32 NCHW [N, 3, OH, OW] or bf16 NHWC [N, OH, OW, 3].

@@ -583,3 +583,51 @@ def test_conv_w8_kernel_fwd_dgrad_bnred(case):
         r2 = red.view(bnops.stat_slots(), 2, C).sum(0)
         assert _rel(r2[0], dm.sum(dim=(0, 2, 3))) < 1e-3
         assert _rel(r2[1], (dm * (xf - mean.view(1, C, 1, 1))).sum(dim=(0, 2, 3))) < 1e-3
+
+
+G4_CASES = [
+    # N, C, H, K, R, stride, pad -> 128 x BN 4-wave multi-stage kernel (Cs % 32 == 0, aligned output)
+    (16, 64, 56, 256, 1, 1, 0),      # 1x1, 2 K-steps (fewer steps than stages)
+    (8, 64, 56, 64, 3, 1, 1),        # 3x3, BN = 64 tile, padding taps
+    (8, 256, 28, 256, 3, 2, 1),      # stride 2: dgrad phases
+    (6, 128, 28, 320, 1, 1, 0),      # Ncol tail, M tail
+    (4, 96, 14, 128, 3, 1, 1),       # Cs = 96: 32-channel steps across tap edges
+]
+
+
+@pytest.mark.parametrize("stages", [4, 3])
+@pytest.mark.parametrize("case", G4_CASES)
+def test_conv_g4_kernel_fwd_dgrad(case, stages):
+    """128 x BN 4-wave kernel with 3 / 4 counted-vmcnt LDS-DMA stages (BIGDL_CONV_G4) vs fp32 torch: forward with
+    bias + BN statistics, forward + ReLU, data gradient with a residual addend."""
+    from bigdl_amd.ops import bn as bnops
+    from bigdl_amd.ops import conv as cv
+    from bigdl_amd.ops import native
+
+    C_ = native.get()
+    old = C_.get_conv_g4()
+    C_.set_conv_g4(stages)
+    try:
+        N, C, H, K, R, st, pd = case
+        torch.manual_seed(7)
+        dev = _dev()
+        x = torch.randn(N, C, H, H, device=dev).to(BF, memory_format=CL)
+        w = (torch.randn(K, C, R, R, device=dev) * (1.0 / (C * R * R) ** 0.5)).to(BF, memory_format=CL)
+        b32 = torch.randn(K, device=dev)
+        stats = bnops.new_stats(K, dev)
+        y = cv.conv2d_fwd(x, w, b32, (st, st), (pd, pd), stats=stats)
+        yr = F.conv2d(x.float(), w.float(), b32, stride=st, padding=pd)
+        assert _rel(y, yr) < 1e-2
+        st2 = stats.view(bnops.stat_slots(), 2, K).sum(0)
+        assert _rel(st2[0], y.float().sum(dim=(0, 2, 3))) < 1e-3
+        assert _rel(st2[1], (y.float() ** 2).sum(dim=(0, 2, 3))) < 1e-3
+        y2 = cv.conv2d_fwd(x, w, b32, (st, st), (pd, pd), relu=True)
+        assert _rel(y2, torch.relu(yr)) < 1e-2
+        gy = torch.randn_like(yr).to(BF, memory_format=CL)
+        add = torch.randn(N, C, H, H, device=dev).to(BF, memory_format=CL)
+        dx = cv.conv2d_dgrad(gy, cv.transpose_w(w), x.shape, (st, st), (pd, pd), addend=add)
+        dxr = torch.nn.grad.conv2d_input(x.shape, w.float(), gy.float(), stride=st, padding=pd) + add.float()
+        assert _rel(dx, dxr) < 1e-2
+        torch.cuda.synchronize()
+    finally:
+        C_.set_conv_g4(old)
