@@ -1902,9 +1902,10 @@ static bool wgrad_prefers_atomic(const WgradArgs* a) {
 long bigdl_conv_wgrad_plan(WgradArgs* a) {
   const int tiles = ((a->Ncol + WT - 1) / WT) * ((a->Kdim + WT - 1) / WT);
   if (conv_impl() < 1 || wgrad_prefers_atomic(a)) { a->splits = 0; return 0; }
-  // workspace split-K: ~4 workgroups per CU (two resident waves of 2/CU), >= 4 LDS stages per split
+  // workspace split-K: ~2 workgroups per CU (512; the kernel runs beside the dgrad chain on the side stream, so
+  // fewer splits = less partial traffic wins: 26.37 vs 26.62 ms/step, profiles/r3_wgrad_wgs_ab.txt), >= 4 LDS stages per split
   // (BIGDL_WGRAD_WGS overrides the workgroup target for A/B runs: fewer splits = fewer partials to reduce)
-  static const int target = [] { const char* e = getenv("BIGDL_WGRAD_WGS"); return e ? atoi(e) : 1024; }();
+  static const int target = [] { const char* e = getenv("BIGDL_WGRAD_WGS"); return e ? atoi(e) : 512; }();
   int splits = (target + tiles - 1) / tiles;
   const int maxsplit = (a->M + 8 * WBM - 1) / (8 * WBM);
   if (splits > maxsplit) splits = maxsplit;
