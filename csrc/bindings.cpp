@@ -968,5 +968,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("get_conv_impl", &bigdl_get_conv_impl);
   m.def("set_conv_g4", &bigdl_set_conv_g4);
   m.def("get_conv_g4", &bigdl_get_conv_g4);
+  m.def("set_wgrad_g3", &bigdl_set_wgrad_g3);
+  m.def("get_wgrad_g3", &bigdl_get_wgrad_g3);
+  m.def("set_i8_g3", &bigdl_set_i8_g3);
+  m.def("get_i8_g3", &bigdl_get_i8_g3);
   m.attr("arch") = "gfx950";
 }

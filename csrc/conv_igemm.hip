@@ -1197,6 +1197,185 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_glds_kernel(WgradArgs a) {
   }
 }
 
+// Deep-pipelined variant of conv_wgrad_glds_kernel: 32-pixel LDS stages (16 KB: dy and x tiles of 32 x 128), THREE
+// stages with two in flight across every barrier (counted `s_waitcnt vmcnt`, raw s_barrier — the 2-stage kernel's
+// __syncthreads drains the DMA queue every 64 pixels), 3 workgroups per CU. Every lane issues every DMA (zero granule
+// for columns past Ncol / Kdim) so each wave's vmcnt counts L = 4 instructions per stage exactly. The pixel tables
+// and the bias reduction live behind the stages in the one __shared__ array.
+__global__ __launch_bounds__(256, 3) void conv_wgrad_g3_kernel(WgradArgs a) {
+  constexpr int PB = 32;                     // pixels per stage
+  constexpr int STAGE = 2 * PB * WT;
+  constexpr int NS = 3;
+  constexpr int L = 2 * (PB / 16);           // DMA instructions per thread per stage (dy + x)
+  __shared__ __attribute__((aligned(1024))) bf16_t lds[NS * STAGE + (3 * PB * 8 + 4 * 128 * 4) / 2];
+  int2* tblv = reinterpret_cast<int2*>(lds + NS * STAGE);              // [3][PB]
+  float* red = reinterpret_cast<float*>(lds + NS * STAGE + 3 * PB * 4); // [4][128]
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wk = wave >> 1, wn = wave & 1;
+  const int tiles_n = (a.Ncol + WT - 1) / WT, tiles_k = (a.Kdim + WT - 1) / WT;
+  const int ntile = tiles_n * tiles_k;
+  const int Lb = blockIdx.x, kq = Lb >> 3;
+  const int split = 8 * (kq / ntile) + (Lb & 7);
+  const int t = kq % ntile;
+  const int tk = t / tiles_n, tn = t % tiles_n;
+  const int n0 = tn * WT, k0 = tk * WT;
+  const int mbeg = split * a.m_per_split;
+  const int mend = min(a.M, mbeg + a.m_per_split);
+  if (split >= a.splits || mbeg >= mend) return;
+
+  const int Lg = lane >> 4;
+  const int f = (Lg << 1) | (((wave >> 1) & 1) << 3) | (wave & 1);
+  const int gsrc = (lane & 15) ^ f;
+  const int nn = n0 + gsrc * 8;
+  const bool nvalid = nn < a.Ncol;
+  const int kk = k0 + gsrc * 8;
+  const bool kvalid = kk < a.Kdim;
+  const int SC = a.S * a.Cs;
+  int r = 0, s = 0, c = 0;
+  if (kvalid) { r = kk / SC; const int rem = kk - r * SC; s = rem / a.Cs; c = rem - s * a.Cs; }
+  const int rdh = r * a.dh, sdw = s * a.dwl;
+  const int tapoff = rdh * a.Ws + sdw;
+
+  const int ohw = a.OH * a.OW;
+  auto build_table = [&](int mb, int slot) {
+    if (tid < PB) {
+      const int m = mb + tid;
+      int2 e;
+      if (m < mend) {
+        const int nb = m / ohw, rem = m - nb * ohw;
+        const int oh = rem / a.OW, ow = rem - oh * a.OW;
+        const int hb = oh * a.sh - a.ph, wb = ow * a.sw - a.pw;
+        e.x = (nb * a.Hs + hb) * a.Ws + wb;
+        e.y = (hb << 16) | (wb & 0xffff);
+      } else {
+        e.x = 0;
+        e.y = (int)0x80008000;
+      }
+      tblv[slot * PB + tid] = e;
+    }
+  };
+  auto issue = [&](int mb, int slot, int buf) {
+    bf16_t* D = lds + buf * STAGE;
+    bf16_t* X = D + PB * WT;
+#pragma unroll
+    for (int i = 0; i < PB / 16; ++i) {
+      const int rowblk = (i * 4 + wave) * 4;
+      const int row = rowblk + Lg;
+      const int m = mb + row;
+      const int2 e = tblv[slot * PB + row];
+      const int ih = (e.y >> 16) + rdh, iw = ((int)(short)(e.y & 0xffff)) + sdw;
+      const bf16_t* pd = (nvalid && m < mend) ? a.dy + (unsigned)(m * a.ldy + nn) : g_zero_granule;
+      const bool okx = kvalid && (unsigned)ih < (unsigned)a.Hs && (unsigned)iw < (unsigned)a.Ws;
+      const bf16_t* px = okx ? a.src + (unsigned)((e.x + tapoff) * a.Cs + c) : g_zero_granule;
+      glds16(pd, (LDS_PTR(void))(D + rowblk * WT));
+      glds16(px, (LDS_PTR(void))(X + rowblk * WT));
+    }
+  };
+
+  v4f acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+  const bool do_bias = a.dbias != nullptr && tk == 0 && wk == 0;
+  float bsum[4] = {0.f, 0.f, 0.f, 0.f};
+  const int G = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  const int nst = (mend - mbeg + PB - 1) / PB;
+
+  build_table(mbeg, 0);
+  build_table(mbeg + PB, 1);
+  build_table(mbeg + 2 * PB, 2);
+  __syncthreads();                        // tables visible, no DMA outstanding yet
+  issue(mbeg, 0, 0);
+  if (nst > 1) {
+    issue(mbeg + PB, 1, 1);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(L) : "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  int cur = 0;
+  for (int st = 0; st < nst; ++st) {
+    const int mb = mbeg + st * PB;
+    const bool more2 = st + 2 < nst;
+    // stage st + 2 goes into the buffer and table slot that stage st - 1 used (retired before the last barrier)
+    if (more2) issue(mb + 2 * PB, cur == 0 ? 2 : cur - 1, cur == 0 ? 2 : cur - 1);
+    const bf16_t* D = lds + cur * STAGE;
+    const bf16_t* X = D + PB * WT;
+    {
+      v8s fx[4], fd[4];
+      const int rbase = 8 * G + q;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int col = wk * 64 + i * 16 + 4 * p;
+        v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(v4s))(X + wswz(rbase, col)));
+        v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(v4s))(X + wswz(rbase + 4, col)));
+        fx[i] = v8s{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int col = wn * 64 + j * 16 + 4 * p;
+        v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(v4s))(D + wswz(rbase, col)));
+        v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(v4s))(D + wswz(rbase + 4, col)));
+        fd[j] = v8s{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fx[i], fd[j], acc[i][j], 0, 0, 0);
+      if (do_bias) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (n0 + wn * 64 + j * 16 + (lane & 15) < a.Ncol) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) bsum[j] += bf2f((bf16_t)fd[j][e]);
+          }
+      }
+    }
+    // the table of stage st + 3 replaces stage st's (issued two steps ago); retire stage st + 1's DMA
+    build_table(mb + 3 * PB, cur);
+    if (more2) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(L) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    cur = cur == 2 ? 0 : cur + 1;
+  }
+
+  float* part = a.ws ? a.ws + (size_t)split * a.Ncol * a.Kdim : nullptr;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int kb = k0 + wk * 64 + i * 16 + 4 * (lane >> 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = n0 + wn * 64 + j * 16 + (lane & 15);
+      if (n < a.Ncol) {
+        if (part) {
+          if (kb < a.Kdim) *reinterpret_cast<v4f*>(part + (size_t)n * a.Kdim + kb) = acc[i][j];
+        } else {
+          float* o = a.dw + (size_t)n * a.Kdim + kb;
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (kb + e < a.Kdim) atomicAdd(o + e, acc[i][j][e]);
+        }
+      }
+    }
+  }
+  if (a.dbias != nullptr && tk == 0) {
+    if (do_bias) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) red[G * 128 + wn * 64 + j * 16 + (lane & 15)] = bsum[j];
+    }
+    __syncthreads();
+    if (tid < 128) {
+      const float tot = red[tid] + red[128 + tid] + red[256 + tid] + red[384 + tid];
+      const int n = n0 + tid;
+      if (n < a.Ncol) atomicAdd(a.dbias + n, tot);
+    }
+  }
+}
+
 // dw += sum over splits of the workspace partials. Split group g (blockIdx.y) sums splits g, g+G, ... with two
 // independent accumulators; with G > 1 the groups meet in dw through fp32 atomics (G-way contention at most), so
 // tiny weights (64x64 with ~1000 splits) still spread the reduction over the whole chip.
@@ -1899,6 +2078,18 @@ static bool wgrad_prefers_atomic(const WgradArgs* a) {
   return on == 2 || (on == 1 && a->Ncol <= 64 && a->Kdim > 256);
 }
 
+int g_wgrad_g3 = -1;
+// BIGDL_WGRAD_G3=1: the 3-stage counted-vmcnt weight-gradient kernel in place of the 2-stage one
+static bool wgrad_g3() {
+  if (g_wgrad_g3 < 0) {
+    const char* e = getenv("BIGDL_WGRAD_G3");
+    g_wgrad_g3 = e ? atoi(e) : 0;
+  }
+  return g_wgrad_g3 != 0;
+}
+void bigdl_set_wgrad_g3(int v) { g_wgrad_g3 = v; }
+int bigdl_get_wgrad_g3() { return wgrad_g3() ? 1 : 0; }
+
 long bigdl_conv_wgrad_plan(WgradArgs* a) {
   const int tiles = ((a->Ncol + WT - 1) / WT) * ((a->Kdim + WT - 1) / WT);
   if (conv_impl() < 1 || wgrad_prefers_atomic(a)) { a->splits = 0; return 0; }
@@ -1924,7 +2115,8 @@ int bigdl_conv_wgrad(const WgradArgs* a_in, hipStream_t st) {
   if (a.ws != nullptr && a.splits > 1 && conv_impl() >= 1) {
     const int tiles = ((a.Ncol + WT - 1) / WT) * ((a.Kdim + WT - 1) / WT);
     const int spad = (a.splits + 7) / 8 * 8;
-    conv_wgrad_glds_kernel<<<dim3(tiles * spad), dim3(256), 0, st>>>(a);
+    if (wgrad_g3()) conv_wgrad_g3_kernel<<<dim3(tiles * spad), dim3(256), 0, st>>>(a);
+    else conv_wgrad_glds_kernel<<<dim3(tiles * spad), dim3(256), 0, st>>>(a);
     const long n4 = (long)a.Ncol * a.Kdim / 4;
     const int blocks = (int)std::min<long>((n4 + 255) / 256, 8192);
     // ~2048 reduce workgroups in total, >= 4 splits per group, <= 64-way atomic contention
@@ -1952,7 +2144,9 @@ int bigdl_conv_wgrad(const WgradArgs* a_in, hipStream_t st) {
   splits = (a.M + mps - 1) / mps;
   a.m_per_split = mps;
   a.splits = splits;
-  if (conv_impl() >= 1 && !wgrad_prefers_atomic(&a))
+  if (conv_impl() >= 1 && !wgrad_prefers_atomic(&a) && wgrad_g3())
+    conv_wgrad_g3_kernel<<<dim3(tiles * ((splits + 7) / 8 * 8)), dim3(256), 0, st>>>(a);
+  else if (conv_impl() >= 1 && !wgrad_prefers_atomic(&a))
     conv_wgrad_glds_kernel<<<dim3(tiles * ((splits + 7) / 8 * 8)), dim3(256), 0, st>>>(a);
   else conv_wgrad_kernel<<<dim3(tiles, splits), dim3(256), 0, st>>>(a);
   HIP_LAUNCH_CHECK();

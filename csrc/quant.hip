@@ -12,6 +12,7 @@
 // epilogue y = acc * s_x[image] * s_w[channel] + bias (+ReLU) written as bf16 NHWC.
 #include "common.h"
 #include "kernels.h"
+#include <stdlib.h>
 
 namespace {
 
@@ -336,6 +337,221 @@ __global__ __launch_bounds__(256, 2) void conv_i8_glds_kernel(ConvArgs a, I8Epi 
   }
 }
 
+// 128 x 128 int8 tile with the counted-vmcnt pipeline of conv_nt_g4_kernel (conv_igemm.hip): 64-byte LDS rows (one
+// i8 MFMA K-step of 64 = four 16-byte granules, slot g ^ ((r >> 1) & 3)), THREE stages of 16 KB with two K-steps in
+// flight across every raw s_barrier (the 2-stage kernel above drains its DMA queue with __syncthreads every
+// 128-byte step), 3 workgroups per CU. Tap table behind the stages. Fast-K only (Cs % 64 == 0: a K-step lies in one
+// tap). The epilogue is conv_i8_glds_kernel's, run in two row halves so a wave's fp32 slice fits the stages.
+__global__ __launch_bounds__(256, 3) void conv_i8_g3_kernel(ConvArgs a, I8Epi ep) {
+  constexpr int BM = 128, BN = 128, BKB = 64, NS = 3;
+  constexpr int WGM = 2, WGN = 2;
+  constexpr int TM = BM / WGM, TN = BN / WGN;
+  constexpr int MI = TM / 16, NI = TN / 16;
+  constexpr int STAGE = (BM + BN) * BKB;          // bytes
+  constexpr int AI = BM / 64, BI = BN / 64;
+  constexpr int L = AI + BI;
+  constexpr int NH = 2;
+  static_assert(4 * (TM / NH) * TN * 4 <= NS * STAGE, "epilogue half must fit the stages");
+  __shared__ __attribute__((aligned(1024))) uint8_t lds[NS * STAGE + 6 * CONV_MAX_TAPS];
+  short* taps = reinterpret_cast<short*>(lds + NS * STAGE);
+  const uint8_t* src = reinterpret_cast<const uint8_t*>(a.src);
+  const uint8_t* wt = reinterpret_cast<const uint8_t*>(a.wt);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WGN, wn = wave % WGN;
+  const int tiles_n = (a.Ncol + BN - 1) / BN;
+  const int tiles_m = (a.M + BM - 1) / BM;
+  const int nwg = tiles_m * tiles_n;
+  const int bid = xcd_remap(blockIdx.x, nwg);
+  const int tm = bid / tiles_n, tn = bid % tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int nk = a.Kdim / BKB;
+
+  const int rsub = lane >> 2;
+  const int gsrc = (lane & 3) ^ ((rsub >> 1) & 3);
+  int a_pix[AI], a_h[AI], a_w[AI];
+  const int ohw = a.OH * a.OW;
+#pragma unroll
+  for (int j = 0; j < AI; ++j) {
+    const int m = m0 + (j * 4 + wave) * 16 + rsub;
+    if (m < a.M) {
+      const int nb = m / ohw, rem = m - nb * ohw;
+      const int oh = rem / a.OW, ow = rem - oh * a.OW;
+      a_pix[j] = nb * a.Hs * a.Ws;
+      a_h[j] = oh * a.mul_h;
+      a_w[j] = ow * a.mul_w;
+    } else {
+      a_pix[j] = 0; a_h[j] = -(1 << 28); a_w[j] = -(1 << 28);
+    }
+  }
+  const uint8_t* wrow[BI];
+  bool bvalid[BI];
+#pragma unroll
+  for (int j = 0; j < BI; ++j) {
+    const int n = n0 + (j * 4 + wave) * 16 + rsub;
+    bvalid[j] = n < a.Ncol;
+    wrow[j] = wt + (size_t)(bvalid[j] ? n : 0) * a.ldw + gsrc * 16;
+  }
+  if (tid < a.ntaps) {
+    taps[tid] = a.tap_h[tid];
+    taps[CONV_MAX_TAPS + tid] = a.tap_w[tid];
+    taps[2 * CONV_MAX_TAPS + tid] = a.tap_k[tid];
+  }
+  __syncthreads();   // tap table visible (no DMA outstanding yet)
+
+  auto issue = [&](int kt, int buf) {
+    const int k0 = kt * BKB;
+    const int t = k0 / a.Cs;
+    const int cin = k0 - t * a.Cs;
+    const int th = taps[t], tw = taps[CONV_MAX_TAPS + t];
+    const int wk = taps[2 * CONV_MAX_TAPS + t] * a.Cs + cin;
+    const int c = cin + gsrc * 16;
+    uint8_t* A = lds + buf * STAGE;
+    uint8_t* B = A + BM * BKB;
+#pragma unroll
+    for (int j = 0; j < AI; ++j) {
+      const int ch = a_h[j] + th, cw = a_w[j] + tw;
+      const bool ok = (unsigned)ch < (unsigned)a.Hs && (unsigned)cw < (unsigned)a.Ws;
+      const uint8_t* g = ok ? src + (size_t)(a_pix[j] + ch * a.Ws + cw) * a.Cs + c : g_zero16;
+      glds16(g, (LDS_PTR(void))(A + (j * 4 + wave) * 16 * BKB));
+    }
+#pragma unroll
+    for (int j = 0; j < BI; ++j) {
+      const uint8_t* g = bvalid[j] ? wrow[j] + wk : g_zero16;
+      glds16(g, (LDS_PTR(void))(B + (j * 4 + wave) * 16 * BKB));
+    }
+  };
+  const int foff = (lane & 15) * BKB + ((((lane >> 4) ^ ((lane >> 1) & 3))) << 4);
+
+  v4i acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = v4i{0, 0, 0, 0};
+
+  issue(0, 0);
+  if (nk > 1) {
+    issue(1, 1);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(L) : "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  int cur = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    const bool more2 = kt + 2 < nk;
+    if (more2) issue(kt + 2, cur == 0 ? 2 : cur - 1);
+    const uint8_t* A = lds + cur * STAGE;
+    const uint8_t* B = A + BM * BKB;
+    v4i fa[MI], fb[NI];
+#pragma unroll
+    for (int j = 0; j < NI; ++j) fb[j] = *reinterpret_cast<const v4i*>(B + (wn * TN + j * 16) * BKB + foff);
+#pragma unroll
+    for (int i = 0; i < MI; ++i) fa[i] = *reinterpret_cast<const v4i*>(A + (wm * TM + i * 16) * BKB + foff);
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fb[j], fa[i], acc[i][j], 0, 0, 0);
+    if (more2) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(L) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    cur = cur == 2 ? 0 : cur + 1;
+  }
+
+  // ---- epilogue (conv_i8_glds_kernel's), in NH row halves through a wave-private LDS slice
+  constexpr int GR = TN / 4, LPR = TN / 8, PPI = 64 / LPR, NR = TM / PPI, MIH = MI / NH, NRH = NR / NH;
+  float* wl = reinterpret_cast<float*>(lds) + wave * (TM / NH) * TN;
+  auto gpos = [](int p, int g) { return (p * GR + (g ^ (p & (GR - 1)))) * 4; };
+  const int q = lane % LPR;
+  const int n = n0 + wn * TN + q * 8;
+  const bool nok = n < a.Ncol;
+  const bool full8 = n + 8 <= a.Ncol;
+  float wsc[8], bs[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const bool ok = n + e < a.Ncol;
+    wsc[e] = ok ? ep.wscale[n + e] : 0.f;
+    bs[e] = (ok && a.bias) ? a.bias[n + e] : 0.f;
+  }
+#pragma unroll
+  for (int h = 0; h < NH; ++h) {
+#pragma unroll
+    for (int i = 0; i < MIH; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        const v4i v = acc[h * MIH + i][j];
+        *reinterpret_cast<v4f*>(wl + gpos(i * 16 + (lane & 15), j * 4 + (lane >> 4))) =
+            v4f{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
+      }
+    __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's LDS writes landed (wave-private slice)
+#pragma unroll
+    for (int r = 0; r < NRH; ++r) {
+      const int p = r * PPI + lane / LPR;
+      const int m = m0 + wm * TM + h * (TM / NH) + p;
+      const v4f lo = *reinterpret_cast<const v4f*>(wl + gpos(p, 2 * q));
+      const v4f hi = *reinterpret_cast<const v4f*>(wl + gpos(p, 2 * q + 1));
+      if (m >= a.M || !nok) continue;
+      const float xs = ep.xscale ? ep.xscale[m / ohw] : ep.xs_const;
+      float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      float ad[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if (ep.add8) {
+        const int8_t* ap = ep.add8 + (size_t)m * ep.add_ld + n;
+        if (full8 && ((reinterpret_cast<uintptr_t>(ap) & 7) == 0)) {
+          const v2u u = *reinterpret_cast<const v2u*>(ap);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) ad[e] = (float)(int8_t)((u[e >> 2] >> (8 * (e & 3))) & 0xff) * ep.add_scale;
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) ad[e] = n + e < a.Ncol ? (float)ap[e] * ep.add_scale : 0.f;
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        v[e] = v[e] * xs * wsc[e] + bs[e] + ad[e];
+        if (a.relu) v[e] = fmaxf(v[e], 0.f);
+      }
+      const size_t off = (size_t)m * a.ldo + n;
+      if (ep.out_mode == 2) {
+        int8_t* o = reinterpret_cast<int8_t*>(a.out) + off;
+        unsigned pk[2] = {0u, 0u};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int qv = max(-127, min(127, __float2int_rn(v[e] * ep.out_inv)));
+          pk[e >> 2] |= (unsigned)(qv & 0xff) << (8 * (e & 3));
+        }
+        if (full8 && (off & 7) == 0) {
+          *reinterpret_cast<v2u*>(o) = v2u{pk[0], pk[1]};
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            if (n + e < a.Ncol) o[e] = (int8_t)((pk[e >> 2] >> (8 * (e & 3))) & 0xff);
+        }
+      } else if (ep.out_mode == 1) {
+        float* o = reinterpret_cast<float*>(a.out) + off;
+        if (full8 && (off & 3) == 0) {
+          *reinterpret_cast<v4f*>(o) = v4f{v[0], v[1], v[2], v[3]};
+          *reinterpret_cast<v4f*>(o + 4) = v4f{v[4], v[5], v[6], v[7]};
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            if (n + e < a.Ncol) o[e] = v[e];
+        }
+      } else {
+        bf16_t* o = a.out + off;
+        if (full8 && (off & 7) == 0) {
+          *reinterpret_cast<v4u*>(o) = v4u{pack2bf(v[0], v[1]), pack2bf(v[2], v[3]), pack2bf(v[4], v[5]), pack2bf(v[6], v[7])};
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            if (n + e < a.Ncol) o[e] = f2bf(v[e]);
+        }
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);   // the slice is rewritten by the next half
+  }
+}
+
 // ---------------------------------------------------------------------------------- int8 pooling / quantize
 // NHWC int8 max / average pooling over [N][H][W][Cp] -> [N][OH][OW][ldo] (rows `ldo` apart, so a pooling branch
 // of an int8 concat writes its slice in place). One lane = 16 channels of one output pixel (16-byte loads); the
@@ -508,6 +724,18 @@ int bigdl_quantize_act(const void* x, int is_bf16, int8_t* q, float* amax, float
   return 0;
 }
 
+int g_i8_g3 = -1;
+// BIGDL_I8_G3 (default 1): the 3-stage counted-vmcnt 128 x 128 int8 kernel for Ncol > 64, Cs % 64 == 0
+static bool i8_g3() {
+  if (g_i8_g3 < 0) {
+    const char* e = getenv("BIGDL_I8_G3");
+    g_i8_g3 = e ? atoi(e) : 1;
+  }
+  return g_i8_g3 != 0;
+}
+void bigdl_set_i8_g3(int v) { g_i8_g3 = v; }
+int bigdl_get_i8_g3() { return i8_g3() ? 1 : 0; }
+
 int bigdl_conv_i8(const ConvArgs* a, const float* xscale, float xs_const, const float* wscale, int out_mode,
                   float out_inv, const int8_t* add8, float add_scale, long add_ld, hipStream_t st) {
   if (a->Cs % 16 != 0 || a->Kdim != a->ntaps * a->Cs || a->ntaps < 1 || a->ntaps > CONV_MAX_TAPS) return -1;
@@ -523,6 +751,8 @@ int bigdl_conv_i8(const ConvArgs* a, const float* xscale, float xs_const, const 
     const int g = ((a->M + 255) / 256) * ((a->Ncol + 63) / 64);
     if (fk) conv_i8_glds_kernel<256, 64, 4, true><<<g, 256, 0, st>>>(*a, ep);
     else conv_i8_glds_kernel<256, 64, 4, false><<<g, 256, 0, st>>>(*a, ep);
+  } else if (i8_g3() && a->Cs % 64 == 0) {
+    conv_i8_g3_kernel<<<nwg, 256, 0, st>>>(*a, ep);
   } else if (fk) {
     conv_i8_glds_kernel<128, 128, 2, true><<<nwg, 256, 0, st>>>(*a, ep);
   } else {

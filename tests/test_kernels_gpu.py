@@ -631,3 +631,38 @@ def test_conv_g4_kernel_fwd_dgrad(case, stages):
         torch.cuda.synchronize()
     finally:
         C_.set_conv_g4(old)
+
+
+WGRAD_G3_CASES = WGRAD_CASES + [
+    (8, 256, 28, 512, 1, 1, 0),      # many tiles, few splits
+    (4, 512, 7, 512, 3, 1, 1),       # 3x3 over a small grid: short splits (stage count below the pipeline depth)
+    (6, 128, 28, 136, 3, 2, 1),      # stride 2, Ncol tail
+]
+
+
+@pytest.mark.parametrize("case", WGRAD_G3_CASES)
+def test_conv_wgrad_g3_kernel(case):
+    """3-stage counted-vmcnt weight-gradient kernel (BIGDL_WGRAD_G3) vs fp32 torch, weight and bias gradients."""
+    from bigdl_amd.ops import conv as cv
+    from bigdl_amd.ops import native
+
+    C_ = native.get()
+    old = C_.get_wgrad_g3()
+    C_.set_wgrad_g3(1)
+    try:
+        N, C, H, K, R, st, pd = case
+        torch.manual_seed(4)
+        dev = _dev()
+        x = torch.randn(N, C, H, H, device=dev).to(BF, memory_format=CL)
+        w = (torch.randn(K, C, R, R, device=dev) * (1.0 / (C * R * R) ** 0.5)).to(BF, memory_format=CL)
+        yr = F.conv2d(x.float(), w.float(), None, stride=st, padding=pd)
+        gy = torch.randn_like(yr).to(BF, memory_format=CL)
+        dw = torch.zeros(K, C, R, R, device=dev).contiguous(memory_format=CL)
+        db = torch.zeros(K, device=dev)
+        cv.conv2d_wgrad(gy, x, dw, db, (st, st), (pd, pd))
+        dwr = torch.nn.grad.conv2d_weight(x.float(), w.shape, gy.float(), stride=st, padding=pd)
+        assert _rel(dw, dwr) < 1e-2
+        assert _rel(db, gy.float().sum(dim=(0, 2, 3))) < 1e-2
+        torch.cuda.synchronize()
+    finally:
+        C_.set_wgrad_g3(old)

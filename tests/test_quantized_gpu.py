@@ -36,12 +36,28 @@ I8_CASES = [
     (1, 32, 12, 12, 16, 3, 3, 1, 2, 2),
     (4, 128, 7, 7, 130, 3, 3, 1, 1, 1),
     (2, 16, 20, 20, 8, 7, 7, 2, 3, 1),
+    (2, 256, 9, 9, 256, 3, 3, 1, 1, 1),     # 36 K-steps through the 3-stage pipeline
+    (5, 192, 6, 6, 320, 1, 1, 1, 0, 1),     # Cs % 128 != 0 but % 64 == 0, Ncol tail, M tail
 ]
 
 
+@pytest.mark.parametrize("g3", [1, 0])
 @pytest.mark.parametrize("case", I8_CASES)
-def test_conv_i8_exact_integer(case):
-    """Scales are forced to exactly 1 (row maxima 127), so the fp32 output must equal the integer conv."""
+def test_conv_i8_exact_integer(case, g3):
+    """Scales are forced to exactly 1 (row maxima 127), so the fp32 output must equal the integer conv — for the
+    3-stage counted-vmcnt kernel (BIGDL_I8_G3, 128 x 128 tiles, Cs % 64 == 0) and the 2-stage one."""
+    from bigdl_amd.ops.conv import _fwd_taps, out_size
+
+    C_ = native.get()
+    old = C_.get_i8_g3()
+    C_.set_i8_g3(g3)
+    try:
+        _conv_i8_exact(case)
+    finally:
+        C_.set_i8_g3(old)
+
+
+def _conv_i8_exact(case):
     from bigdl_amd.ops.conv import _fwd_taps, out_size
 
     N, C, H, W, K, R, S, st, pd, dl = case
