@@ -20,6 +20,8 @@ import numbers
 import numpy as np
 import torch
 
+from ..ops import tensor_math as _tm
+
 _DTYPES = {"float": torch.float32, "double": torch.float64, "int": torch.int32, "long": torch.int64,
            "short": torch.int16, "byte": torch.uint8, "char": torch.int8, "boolean": torch.bool,
            "bfloat16": torch.bfloat16, "half": torch.float16}
@@ -28,6 +30,21 @@ _DTYPES = {"float": torch.float32, "double": torch.float64, "int": torch.int32, 
 def _d(dim):
     """1-based dimension -> 0-based."""
     return dim - 1
+
+
+def _g32(*ts):
+    """Every operand an fp32 GPU tensor: the native TensorMath backend (ops/tensor_math.py, csrc/tensor_math.hip)
+    runs the op; other dtypes and the CPU engine use torch."""
+    return all(isinstance(t, torch.Tensor) and t.is_cuda and t.dtype == torch.float32 for t in ts)
+
+
+# torch element functions the native backend implements (csrc/tensor_math.hip op names)
+_NATIVE_UNARY = {"abs": "ABS", "exp": "EXP", "log": "LOG", "log1p": "LOG1P", "sqrt": "SQRT", "square": "SQUARE",
+                 "tanh": "TANH", "floor": "FLOOR", "ceil": "CEIL", "sign": "SIGN"}
+
+
+def _same(*ts):
+    return all(tuple(t.shape) == tuple(ts[0].shape) for t in ts)
 
 
 def _raw(x):
@@ -372,16 +389,23 @@ class Tensor:
         src = _raw(other)
         if src.numel() != self._t.numel():
             raise ValueError(f"copy: element count mismatch {src.numel()} vs {self._t.numel()}")
-        self._t.copy_(src.reshape(self._t.shape) if src.shape != self._t.shape else src)
+        src = src.reshape(self._t.shape) if src.shape != self._t.shape else src
+        if _g32(self._t, src) and _tm.apply(_tm.COPY, self._t, src):
+            return self
+        self._t.copy_(src)
         return self
 
     def fill(self, v):
+        if _g32(self._t) and _tm.apply(_tm.FILL, self._t, s0=v):
+            return self
         self._t.fill_(v)
         return self
 
     forceFill = fill
 
     def zero(self):
+        if _g32(self._t) and _tm.apply(_tm.FILL, self._t, s0=0.0):
+            return self
         self._t.zero_()
         return self
 
@@ -430,6 +454,8 @@ class Tensor:
 
     def add(self, *args):
         """add(value) | add(y) | add(value, y) | add(x, y) | add(x, value, y) (TensorMath.scala:65-108)."""
+        if self._native_axpy(_tm.ADD, _tm.ADDS, args):
+            return self
         if len(args) == 1:
             a = args[0]
             self._t.add_(_raw(a))
@@ -445,6 +471,8 @@ class Tensor:
         return self
 
     def sub(self, *args):
+        if self._native_axpy(_tm.SUB, None, args):
+            return self
         if len(args) == 1:
             self._t.sub_(_raw(args[0]))
         elif len(args) == 2:
@@ -458,33 +486,88 @@ class Tensor:
             return self._assign(_raw(x) - v * _raw(y))
         return self
 
+    def _native_axpy(self, op, op_scalar, args):
+        """add / sub on the native backend: (value) | (y) | (value, y) | (x, y) | (x, value, y), same shapes."""
+        t = self._t
+        if not _g32(t):
+            return False
+        if len(args) == 1:
+            a = args[0]
+            if isinstance(a, numbers.Number):
+                return op_scalar is not None and _tm.apply(op_scalar, t, t, s0=a)
+            y = _raw(a)
+            return _g32(y) and _same(t, y) and _tm.apply(op, t, t, y, s0=1.0)
+        if len(args) == 2:
+            a, b = args
+            if isinstance(a, numbers.Number):
+                y = _raw(b)
+                return _g32(y) and _same(t, y) and _tm.apply(op, t, t, y, s0=a)
+            x, y = _raw(a), _raw(b)
+            return _g32(x, y) and _same(t, x, y) and _tm.apply(op, t, x, y, s0=1.0)
+        x, v, y = _raw(args[0]), args[1], _raw(args[2])
+        return _g32(x, y) and _same(t, x, y) and _tm.apply(op, t, x, y, s0=v)
+
+    def _native_ew(self, op, a, b=None, c=None, s0=0.0, s1=0.0):
+        """self = op(a, b, c) on the native backend when every tensor is fp32 on the GPU with self's shape."""
+        ts = [x for x in (a, b, c) if x is not None]
+        return (_g32(self._t, *ts) and _same(self._t, *ts)
+                and _tm.apply(op, self._t, a, b, c, s0=s0, s1=s1))
+
     def mul(self, *args):
         if len(args) == 1:
+            if isinstance(args[0], numbers.Number) and self._native_ew(_tm.MULS, self._t, s0=args[0]):
+                return self
             self._t.mul_(args[0])
             return self
         x, v = args
+        if isinstance(v, numbers.Number) and self._native_ew(_tm.MULS, _raw(x), s0=v):
+            return self
         return self._assign(_raw(x) * v)
 
     def div(self, *args):
         if len(args) == 1:
-            self._t.div_(_raw(args[0]))
+            a = args[0]
+            if isinstance(a, numbers.Number):
+                if self._native_ew(_tm.DIVS, self._t, s0=a):
+                    return self
+            elif self._native_ew(_tm.DIV, self._t, _raw(a)):
+                return self
+            self._t.div_(_raw(a))
             return self
         x, v = args
+        if not isinstance(v, numbers.Number) and self._native_ew(_tm.DIV, _raw(x), _raw(v)):
+            return self
         return self._assign(_raw(x) / _raw(v))
 
     def cmul(self, *args):
         if len(args) == 1:
+            if self._native_ew(_tm.MUL, self._t, _raw(args[0])):
+                return self
             self._t.mul_(_raw(args[0]))
+            return self
+        if self._native_ew(_tm.MUL, _raw(args[0]), _raw(args[1])):
             return self
         return self._assign(_raw(args[0]) * _raw(args[1]))
 
     def cdiv(self, *args):
         if len(args) == 1:
+            if self._native_ew(_tm.DIV, self._t, _raw(args[0])):
+                return self
             self._t.div_(_raw(args[0]))
+            return self
+        if self._native_ew(_tm.DIV, _raw(args[0]), _raw(args[1])):
             return self
         return self._assign(_raw(args[0]) / _raw(args[1]))
 
     def cmax(self, *args):
+        if len(args) == 1 and isinstance(args[0], numbers.Number):
+            if self._native_ew(_tm.CLAMP, self._t, s0=args[0], s1=math.inf):
+                return self
+        elif len(args) == 1:
+            if self._native_ew(_tm.MAX, self._t, _raw(args[0])):
+                return self
+        elif self._native_ew(_tm.MAX, _raw(args[0]), _raw(args[1])):
+            return self
         if len(args) == 1:
             o = args[0]
             res = torch.clamp(self._t, min=o) if isinstance(o, numbers.Number) else torch.maximum(self._t, _raw(o))
@@ -492,6 +575,14 @@ class Tensor:
         return self._assign(torch.maximum(_raw(args[0]), _raw(args[1])))
 
     def cmin(self, *args):
+        if len(args) == 1 and isinstance(args[0], numbers.Number):
+            if self._native_ew(_tm.CLAMP, self._t, s0=-math.inf, s1=args[0]):
+                return self
+        elif len(args) == 1:
+            if self._native_ew(_tm.MIN, self._t, _raw(args[0])):
+                return self
+        elif self._native_ew(_tm.MIN, _raw(args[0]), _raw(args[1])):
+            return self
         if len(args) == 1:
             o = args[0]
             res = torch.clamp(self._t, max=o) if isinstance(o, numbers.Number) else torch.minimum(self._t, _raw(o))
@@ -501,58 +592,72 @@ class Tensor:
     def addcmul(self, *args):
         """addcmul(value, t1, t2) | addcmul(t1, t2): self += value * t1 * t2."""
         v, t1, t2 = args if len(args) == 3 else (1.0, *args)
+        if self._native_ew(_tm.ADDCMUL, self._t, _raw(t1), _raw(t2), s0=v):
+            return self
         self._t.addcmul_(_raw(t1), _raw(t2), value=v)
         return self
 
     def addcdiv(self, *args):
         v, t1, t2 = args if len(args) == 3 else (1.0, *args)
+        if self._native_ew(_tm.ADDCDIV, self._t, _raw(t1), _raw(t2), s0=v):
+            return self
         self._t.addcdiv_(_raw(t1), _raw(t2), value=v)
         return self
 
     def negative(self, x=None):
+        if self._native_ew(_tm.NEG, self._t if x is None else _raw(x)):
+            return self
         return self._assign(-(self._t if x is None else _raw(x)))
 
     def inv(self):
+        if self._native_ew(_tm.RECIP, self._t):
+            return self
         self._t.reciprocal_()
         return self
 
     def clamp(self, minValue, maxValue):
+        if self._native_ew(_tm.CLAMP, self._t, s0=minValue, s1=maxValue):
+            return self
         self._t.clamp_(minValue, maxValue)
         return self
 
     def _unary(self, fn, x=None):
+        """``fn``: a torch function, or the name of one the native backend implements (looked up at call time)."""
         src = self._t if x is None else _raw(x)
-        return self._assign(fn(src))
+        name = _NATIVE_UNARY.get(fn) if isinstance(fn, str) else None
+        if name is not None and self._native_ew(getattr(_tm, name), src):
+            return self
+        return self._assign((getattr(torch, fn) if isinstance(fn, str) else fn)(src))
 
     def abs(self, x=None):
-        return self._unary(torch.abs, x)
+        return self._unary("abs", x)
 
     def exp(self, x=None):
-        return self._unary(torch.exp, x)
+        return self._unary("exp", x)
 
     def log(self, x=None):
-        return self._unary(torch.log, x)
+        return self._unary("log", x)
 
     def log1p(self, x=None):
-        return self._unary(torch.log1p, x)
+        return self._unary("log1p", x)
 
     def sqrt(self, x=None):
-        return self._unary(torch.sqrt, x)
+        return self._unary("sqrt", x)
 
     def square(self, x=None):
-        return self._unary(torch.square, x)
+        return self._unary("square", x)
 
     def tanh(self, x=None):
-        return self._unary(torch.tanh, x)
+        return self._unary("tanh", x)
 
     def floor(self, x=None):
-        return self._unary(torch.floor, x)
+        return self._unary("floor", x)
 
     def ceil(self, x=None):
-        return self._unary(torch.ceil, x)
+        return self._unary("ceil", x)
 
     def sign(self, x=None):
-        return self._unary(torch.sign, x)
+        return self._unary("sign", x)
 
     def erf(self, x=None):
         return self._unary(torch.erf, x)
@@ -568,7 +673,11 @@ class Tensor:
 
     def pow(self, *args):
         if len(args) == 1:
+            if isinstance(args[0], numbers.Number) and self._native_ew(_tm.POWS, self._t, s0=args[0]):
+                return self
             self._t.pow_(args[0])
+            return self
+        if isinstance(args[1], numbers.Number) and self._native_ew(_tm.POWS, _raw(args[0]), s0=args[1]):
             return self
         return self._assign(torch.pow(_raw(args[0]), args[1]))
 
@@ -586,9 +695,36 @@ class Tensor:
             v1, M, v2, a, b = 1.0, args[0], 1.0, args[1], args[2]
         else:
             v1, M, v2, (a, b) = 1.0, self._t, 1.0, args
+        if self._native_gemm(_raw(M), _raw(a), _raw(b), v1, v2):
+            return self
         return self._assign(torch.addmm(_raw(M), _raw(a), _raw(b), beta=v1, alpha=v2))
 
+    def _native_gemm(self, M, a, b, beta, alpha):
+        """self = beta * M + alpha * a @ b (2-D, or 3-D batched) on the fp32 MFMA GEMM (ops/tensor_math.py)."""
+        if not (_g32(a, b) and (M is None or _g32(M)) and a.dim() == b.dim() and a.dim() in (2, 3)):
+            return False
+        shape = tuple(a.shape[:-1]) + (b.shape[-1],)
+        if a.shape[-1] != b.shape[-2] or (a.dim() == 3 and a.shape[0] != b.shape[0]):
+            return False
+        if M is not None and tuple(M.shape) != shape:
+            try:
+                M = M.expand(shape)
+            except RuntimeError:
+                return False
+        t = self._t
+        alias = lambda x: x.untyped_storage().data_ptr() == t.untyped_storage().data_ptr()  # noqa: E731
+        if tuple(t.shape) != shape or not t.is_cuda or t.dtype != torch.float32 or alias(a) or alias(b) or (
+                M is not None and alias(M) and (M.data_ptr() != t.data_ptr() or M.stride() != t.stride())):
+            out = torch.empty(shape, device=a.device, dtype=torch.float32)
+            _tm.gemm(out, a, b, M, alpha, beta)
+            self.resize(list(shape))
+            return self._native_ew(_tm.COPY, out) or bool(self._t.copy_(out) is not None)
+        _tm.gemm(t, a, b, M, alpha, beta)
+        return True
+
     def mm(self, a, b):
+        if self._native_gemm(None, _raw(a), _raw(b), 0.0, 1.0):
+            return self
         return self._assign(_raw(a) @ _raw(b))
 
     def addmv(self, *args):
@@ -602,9 +738,30 @@ class Tensor:
             v1, M = 1.0, self._t
         else:
             v1, M, v2, (a, b) = 1.0, self._t, 1.0, args
+        if self._native_gemv(_raw(M), _raw(a), _raw(b), v1, v2):
+            return self
         return self._assign(torch.addmv(_raw(M), _raw(a), _raw(b), beta=v1, alpha=v2))
 
+    def _native_gemv(self, M, a, x, beta, alpha):
+        if not (_g32(a, x) and (M is None or _g32(M)) and a.dim() == 2 and x.dim() == 1 and a.shape[1] == x.shape[0]):
+            return False
+        m = a.shape[0]
+        t = self._t
+        if M is not None and tuple(M.shape) != (m,):
+            return False
+        alias = lambda y: y.untyped_storage().data_ptr() == t.untyped_storage().data_ptr()  # noqa: E731
+        if tuple(t.shape) != (m,) or not _g32(t) or alias(a) or alias(x) or (
+                M is not None and alias(M) and (M.data_ptr() != t.data_ptr() or M.stride() != t.stride())):
+            out = torch.empty(m, device=a.device, dtype=torch.float32)
+            _tm.gemv(out, a, x, M, alpha, beta)
+            self.resize([m])
+            return self._native_ew(_tm.COPY, out) or bool(self._t.copy_(out) is not None)
+        _tm.gemv(t, a, x, M, alpha, beta)
+        return True
+
     def mv(self, a, b):
+        if self._native_gemv(None, _raw(a), _raw(b), 0.0, 1.0):
+            return self
         return self._assign(_raw(a) @ _raw(b))
 
     def addr(self, *args):
@@ -615,7 +772,13 @@ class Tensor:
             v1, M = 1.0, self._t
         else:
             v1, M, v2, (x, y) = 1.0, self._t, 1.0, args
-        return self._assign(torch.addr(_raw(M), _raw(x), _raw(y), beta=v1, alpha=v2))
+        M, x, y = _raw(M), _raw(x), _raw(y)
+        if (_g32(M, x, y) and x.dim() == 1 and y.dim() == 1 and tuple(M.shape) == (x.shape[0], y.shape[0])
+                and tuple(self._t.shape) == tuple(M.shape)):
+            m, n = M.shape
+            if _tm.apply(_tm.AXPBYZ, self._t, M, x.view(m, 1).expand(m, n), y.view(1, n).expand(m, n), s0=v2, s1=v1):
+                return self
+        return self._assign(torch.addr(M, x, y, beta=v1, alpha=v2))
 
     def baddbmm(self, *args):
         if len(args) == 5:
@@ -625,13 +788,22 @@ class Tensor:
             M = self._t
         else:
             v1, M, v2, (a, b) = 1.0, self._t, 1.0, args
+        if self._native_gemm(_raw(M), _raw(a), _raw(b), v1, v2):
+            return self
         return self._assign(torch.baddbmm(_raw(M), _raw(a), _raw(b), beta=v1, alpha=v2))
 
     def bmm(self, a, b):
+        if self._native_gemm(None, _raw(a), _raw(b), 0.0, 1.0):
+            return self
         return self._assign(torch.bmm(_raw(a), _raw(b)))
 
     def dot(self, y):
-        return float((self._t.reshape(-1).double() * _raw(y).reshape(-1).double()).sum())
+        yr = _raw(y)
+        if _g32(self._t, yr) and self._t.numel() == yr.numel():
+            prod = torch.empty(self._t.shape, device=self._t.device)
+            if _tm.apply(_tm.MUL, prod, self._t, yr.reshape(self._t.shape)):
+                return float(_tm.reduce(prod, _tm.R_SUM)[0])
+        return float((self._t.reshape(-1).double() * yr.reshape(-1).double()).sum())
 
     # ------------------------------------------------------------------ reductions
     def _reduce_dim(self, fn, args):
@@ -642,16 +814,31 @@ class Tensor:
             return self._assign(fn(_raw(x), _d(dim)))
         return self._wrap(fn(self._t, _d(args[0])))
 
+    @staticmethod
+    def _nred(op, mean=False, fallback=None):
+        """Reduction fn(t, d) on the native backend for fp32 GPU tensors (ops/tensor_math.reduce), else ``fallback``."""
+        def fn(t, d):
+            if _g32(t) and t.numel() > 0:
+                v, _ = _tm.reduce(t, op, d, mean=mean)
+                return float(v) if d is None else v
+            return fallback(t, d)
+        return fn
+
     def sum(self, *args):
-        return self._reduce_dim(lambda t, d: t.sum().item() if d is None else t.sum(d, keepdim=True), args)
+        return self._reduce_dim(self._nred(_tm.R_SUM, fallback=lambda t, d: t.sum().item() if d is None
+                                           else t.sum(d, keepdim=True)), args)
 
     def mean(self, *args):
-        return self._reduce_dim(lambda t, d: t.float().mean().item() if d is None else t.mean(d, keepdim=True), args)
+        return self._reduce_dim(self._nred(_tm.R_SUM, True, lambda t, d: t.float().mean().item() if d is None
+                                           else t.mean(d, keepdim=True)), args)
 
     def prod(self, *args):
-        return self._reduce_dim(lambda t, d: t.prod().item() if d is None else t.prod(d, keepdim=True), args)
+        return self._reduce_dim(self._nred(_tm.R_PROD, fallback=lambda t, d: t.prod().item() if d is None
+                                           else t.prod(d, keepdim=True)), args)
 
     def sumSquare(self):
+        if _g32(self._t) and self._t.numel() > 0:
+            return float(_tm.reduce(self._t, _tm.R_SUMSQ)[0])
         return float((self._t.double() ** 2).sum())
 
     def norm(self, *args):
@@ -672,7 +859,26 @@ class Tensor:
         vals, idx = (fn(self._t, _d(dim), keepdim=True) if not isinstance(dim, Tensor) else (None, None))
         return self._wrap(vals), self._wrap(idx + 1)
 
+    def _native_minmax(self, op, args):
+        if not (_g32(self._t) and self._t.numel() > 0):
+            return None
+        if not args:
+            return float(_tm.reduce(self._t, op)[0])
+        if len(args) == 3:
+            values, indices, dim = args
+            v, i = _tm.reduce(self._t, op, _d(dim), want_index=True)
+            values._assign(v)
+            indices._assign(i.to(indices._t.dtype))
+            return values, indices
+        if isinstance(args[0], Tensor):
+            return None
+        v, i = _tm.reduce(self._t, op, _d(args[0]), want_index=True)
+        return self._wrap(v), self._wrap(i)
+
     def max(self, *args):
+        r = self._native_minmax(_tm.R_MAX, args)
+        if r is not None:
+            return r
         if len(args) == 3:     # max(values, indices, dim) on self
             values, indices, dim = args
             v, i = self._t.max(_d(dim), keepdim=True)
@@ -682,6 +888,9 @@ class Tensor:
         return self._minmax(torch.max, args)
 
     def min(self, *args):
+        r = self._native_minmax(_tm.R_MIN, args)
+        if r is not None:
+            return r
         if len(args) == 3:
             values, indices, dim = args
             v, i = self._t.min(_d(dim), keepdim=True)

@@ -211,6 +211,50 @@ void bmm_nt(const Tensor& a, const Tensor& b, const Tensor& c, double alpha, boo
                               accum ? 1 : 0, stream());
   TORCH_CHECK(rc == 0, "bmm_nt: unsupported shape");
 }
+// ---- TensorMath backend (tensor_math.hip): operands are fp32 GPU tensors already broadcast to the output's
+// sizes; the Python side collapses dimensions and passes per-operand strides (elements)
+void tensor_apply(const Tensor& out, const OptT& a, const OptT& b, const OptT& c, std::vector<int64_t> size,
+                  std::vector<int64_t> so, std::vector<int64_t> sa, std::vector<int64_t> sb, std::vector<int64_t> sc,
+                  int64_t op, double s0, double s1, bool contiguous) {
+  const int nd = (int)size.size();
+  TORCH_CHECK(nd <= 6 && so.size() == size.size() && (sa.empty() || sa.size() == size.size()) &&
+                  (sb.empty() || sb.size() == size.size()) && (sc.empty() || sc.size() == size.size()),
+              "tensor_apply: at most 6 collapsed dims, one stride per dim and operand");
+  int64_t n = 1;
+  for (auto v : size) n *= v;
+  TORCH_CHECK(n <= out.numel() || nd == 0, "tensor_apply: sizes exceed the output");
+  const int rc = bigdl_tensor_apply(mf(out, "out"), ocf(a, "a"), ocf(b, "b"), ocf(c, "c"), nd, size.data(), so.data(),
+                                    sa.empty() ? nullptr : sa.data(), sb.empty() ? nullptr : sb.data(),
+                                    sc.empty() ? nullptr : sc.data(), (int)op, (float)s0, (float)s1, contiguous ? 1 : 0,
+                                    stream());
+  TORCH_CHECK(rc == 0, "tensor_apply failed");
+}
+void tensor_reduce(const Tensor& x, int64_t outer, int64_t R, int64_t inner, int64_t op, double p, const Tensor& out,
+                   const OptT& outi, bool mean, const OptT& ws, int64_t chunks) {
+  TORCH_CHECK(x.is_contiguous() && x.numel() == outer * R * inner, "tensor_reduce: contiguous [outer, R, inner] input");
+  TORCH_CHECK(out.numel() == outer * inner && out.is_contiguous(), "tensor_reduce: out [outer * inner]");
+  if (outi && outi->defined()) TORCH_CHECK(outi->numel() == outer * inner, "tensor_reduce: indices [outer * inner]");
+  if (chunks > 1) TORCH_CHECK(ws && ws->defined() && ws->numel() >= chunks * outer * inner * 3 + 1, "tensor_reduce: workspace");
+  const int rc = bigdl_tensor_reduce(cf(x, "x"), outer, R, inner, (int)op, (float)p, mf(out, "out"), omf(outi, "outi"),
+                                     mean ? 1 : 0, omf(ws, "ws"), chunks, stream());
+  TORCH_CHECK(rc == 0, "tensor_reduce: unsupported size");
+}
+// strides s = [sam, sak, sbk, sbn, scm, scn, smm, smn, bsa, bsb, bsc, bsm]
+void gemm_f32(const Tensor& A, const Tensor& B, const OptT& Min, const Tensor& C, int64_t batch, int64_t M, int64_t N,
+              int64_t K, std::vector<int64_t> s, double alpha, double beta) {
+  TORCH_CHECK(s.size() == 12, "gemm_f32: 12 strides");
+  TORCH_CHECK(M < (1L << 31) && N < (1L << 31) && K < (1L << 31), "gemm_f32: sizes");
+  const int rc = bigdl_gemm_f32(cf(A, "A"), cf(B, "B"), ocf(Min, "M"), mf(C, "C"), (int)batch, (int)M, (int)N, (int)K,
+                                s.data(), (float)alpha, (float)beta, stream());
+  TORCH_CHECK(rc == 0, "gemm_f32: unsupported shape");
+}
+void gemv_f32(const Tensor& A, const Tensor& x, const OptT& Min, const Tensor& y, int64_t M, int64_t K,
+              std::vector<int64_t> s, double alpha, double beta) {
+  TORCH_CHECK(s.size() == 5, "gemv_f32: strides [sam, sak, sx, smin, sy]");
+  const int rc = bigdl_gemv_f32(cf(A, "A"), cf(x, "x"), ocf(Min, "M"), mf(y, "y"), (int)M, (int)K, s[0], s[1], s[2],
+                                s[3], s[4], (float)alpha, (float)beta, stream());
+  TORCH_CHECK(rc == 0, "gemv_f32 failed");
+}
 void cast_f32_bf16(const Tensor& x, const Tensor& y) {
   TORCH_CHECK(x.numel() == y.numel() && x.is_contiguous() && y.is_contiguous(), "cast: size");
   bigdl_cast_f32_bf16(cf(x, "x"), mbf(y, "y"), x.numel(), stream());
@@ -902,6 +946,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bmm_nt", &bmm_nt, py::arg("a"), py::arg("b"), py::arg("c"), py::arg("alpha") = 1.0, py::arg("accum") = false);
   m.def("pair_weight", &pair_weight);
   m.def("pair_wgrad_add", &pair_wgrad_add);
+  m.def("tensor_apply", &tensor_apply, py::arg("out"), py::arg("a"), py::arg("b"), py::arg("c"), py::arg("size"),
+        py::arg("so"), py::arg("sa"), py::arg("sb"), py::arg("sc"), py::arg("op"), py::arg("s0") = 0.0,
+        py::arg("s1") = 0.0, py::arg("contiguous") = false);
+  m.def("tensor_reduce", &tensor_reduce, py::arg("x"), py::arg("outer"), py::arg("R"), py::arg("inner"), py::arg("op"),
+        py::arg("p"), py::arg("out"), py::arg("outi"), py::arg("mean"), py::arg("ws"), py::arg("chunks"));
+  m.def("gemm_f32", &gemm_f32);
+  m.def("gemv_f32", &gemv_f32);
   m.def("cast_f32_bf16", &cast_f32_bf16);
   m.def("cast_bf16_f32", &cast_bf16_f32);
   m.def("maxpool_fwd", &maxpool_fwd);

@@ -154,6 +154,16 @@ void bigdl_quantize_nchw_f32(const float* x, int8_t* q, int N, int C, int HW, in
 void bigdl_quantize_rows_bf16(const uint16_t* x, int8_t* q, long P, int C, long ldq, float inv, hipStream_t st);
 void bigdl_dequantize_rows(const int8_t* q, uint16_t* y, long P, int C, long ld, float scale, hipStream_t st);
 
+// tensor_math.hip: native TensorMath backend (strided apply, reductions, fp32 MFMA GEMM / GEMV)
+int bigdl_tensor_apply(float* out, const float* a, const float* b, const float* c, int nd, const long* size,
+                       const long* so, const long* sa, const long* sb, const long* sc, int op, float s0, float s1,
+                       int contiguous, hipStream_t st);
+int bigdl_tensor_reduce(const float* x, long outer, long R, long inner, int op, float p, float* out, float* outi,
+                        int mean, float* ws, long chunks, hipStream_t st);
+int bigdl_gemm_f32(const float* A, const float* B, const float* Min, float* C, int batch, int M, int N, int K,
+                   const long* s, float alpha, float beta, hipStream_t st);
+int bigdl_gemv_f32(const float* A, const float* x, const float* Min, float* y, int M, int K, long sam, long sak,
+                   long sx, long smi, long sy, float alpha, float beta, hipStream_t st);
 void bigdl_set_conv_impl(int impl);
 int bigdl_get_conv_impl();
 void bigdl_set_conv_g4(int v);
