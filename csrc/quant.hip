@@ -342,13 +342,16 @@ __global__ __launch_bounds__(256, 2) void conv_i8_glds_kernel(ConvArgs a, I8Epi 
 // flight across every raw s_barrier (the 2-stage kernel above drains its DMA queue with __syncthreads every
 // 128-byte step), 3 workgroups per CU. Tap table behind the stages. Fast-K only (Cs % 64 == 0: a K-step lies in one
 // tap). The epilogue is conv_i8_glds_kernel's, run in two row halves so a wave's fp32 slice fits the stages.
-__global__ __launch_bounds__(256, 3) void conv_i8_g3_kernel(ConvArgs a, I8Epi ep) {
-  constexpr int BM = 128, BN = 128, BKB = 64, NS = 3;
-  constexpr int WGM = 2, WGN = 2;
+// Tiles: 128 x 128 (2 x 2 waves) or, for the narrow layers (Ncol <= 64 / <= 32), 256 x 64 / 256 x 32 with the four
+// waves stacked along M (as conv_i8_glds_kernel).
+template <int BM, int BN, int WGM, int WGN>
+__global__ __launch_bounds__(256, (BM + (BN + 63) / 64 * 64) * 64 * 3 <= 52 * 1024 ? 3 : 2) void conv_i8_g3_kernel(
+    ConvArgs a, I8Epi ep) {
+  constexpr int BKB = 64, NS = 3;
   constexpr int TM = BM / WGM, TN = BN / WGN;
   constexpr int MI = TM / 16, NI = TN / 16;
-  constexpr int STAGE = (BM + BN) * BKB;          // bytes
-  constexpr int AI = BM / 64, BI = BN / 64;
+  constexpr int AI = BM / 64, BI = (BN + 63) / 64;   // DMA instructions per thread per stage (4 waves x 16 rows)
+  constexpr int STAGE = (BM + BI * 64) * BKB;         // bytes (B region rounded up to the 64 rows one DMA pass fills)
   constexpr int L = AI + BI;
   constexpr int NH = 2;
   static_assert(4 * (TM / NH) * TN * 4 <= NS * STAGE, "epilogue half must fit the stages");
@@ -389,8 +392,9 @@ __global__ __launch_bounds__(256, 3) void conv_i8_g3_kernel(ConvArgs a, I8Epi ep
   bool bvalid[BI];
 #pragma unroll
   for (int j = 0; j < BI; ++j) {
-    const int n = n0 + (j * 4 + wave) * 16 + rsub;
-    bvalid[j] = n < a.Ncol;
+    const int nl = (j * 4 + wave) * 16 + rsub;     // tile row; rows past BN (BN = 32) load into a spare slot
+    const int n = n0 + nl;
+    bvalid[j] = nl < BN && n < a.Ncol;
     wrow[j] = wt + (size_t)(bvalid[j] ? n : 0) * a.ldw + gsrc * 16;
   }
   if (tid < a.ntaps) {
@@ -743,7 +747,12 @@ int bigdl_conv_i8(const ConvArgs* a, const float* xscale, float xs_const, const 
   const int nwg = ((a->M + 127) / 128) * ((a->Ncol + 127) / 128);
   const I8Epi ep{xscale, xs_const, wscale, out_mode, out_inv, add8, add_scale, add_ld};
   const bool fk = a->Cs % QBK == 0;
-  if (a->Ncol <= 32) {
+  if (a->Ncol <= 64 && i8_g3() && a->Cs % 64 == 0) {
+    const int bn = a->Ncol <= 32 ? 32 : 64;
+    const int g = ((a->M + 255) / 256) * ((a->Ncol + bn - 1) / bn);
+    if (bn == 32) conv_i8_g3_kernel<256, 32, 4, 1><<<g, 256, 0, st>>>(*a, ep);
+    else conv_i8_g3_kernel<256, 64, 4, 1><<<g, 256, 0, st>>>(*a, ep);
+  } else if (a->Ncol <= 32) {
     const int g = ((a->M + 255) / 256) * ((a->Ncol + 31) / 32);
     if (fk) conv_i8_glds_kernel<256, 32, 4, true><<<g, 256, 0, st>>>(*a, ep);
     else conv_i8_glds_kernel<256, 32, 4, false><<<g, 256, 0, st>>>(*a, ep);
@@ -752,7 +761,7 @@ int bigdl_conv_i8(const ConvArgs* a, const float* xscale, float xs_const, const 
     if (fk) conv_i8_glds_kernel<256, 64, 4, true><<<g, 256, 0, st>>>(*a, ep);
     else conv_i8_glds_kernel<256, 64, 4, false><<<g, 256, 0, st>>>(*a, ep);
   } else if (i8_g3() && a->Cs % 64 == 0) {
-    conv_i8_g3_kernel<<<nwg, 256, 0, st>>>(*a, ep);
+    conv_i8_g3_kernel<128, 128, 2, 2><<<nwg, 256, 0, st>>>(*a, ep);
   } else if (fk) {
     conv_i8_glds_kernel<128, 128, 2, true><<<nwg, 256, 0, st>>>(*a, ep);
   } else {

@@ -38,6 +38,9 @@ I8_CASES = [
     (2, 16, 20, 20, 8, 7, 7, 2, 3, 1),
     (2, 256, 9, 9, 256, 3, 3, 1, 1, 1),     # 36 K-steps through the 3-stage pipeline
     (5, 192, 6, 6, 320, 1, 1, 1, 0, 1),     # Cs % 128 != 0 but % 64 == 0, Ncol tail, M tail
+    (2, 64, 12, 12, 64, 3, 3, 1, 1, 1),     # narrow 256 x 64 tile
+    (3, 128, 9, 9, 24, 1, 1, 1, 0, 1),      # narrow 256 x 32 tile (Ncol tail)
+    (2, 64, 15, 15, 40, 3, 3, 2, 1, 1),     # 256 x 64, stride 2, Ncol tail
 ]
 
 
