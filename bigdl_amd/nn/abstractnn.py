@@ -462,18 +462,29 @@ class AbstractModule(MklInt8Convertible, metaclass=_RecordInit):
                 self._w16_managed = True
 
     def w16(self, name):
-        """bf16 compute copy of parameter ``name`` (GPU engine)."""
+        """bf16 compute copy of parameter ``name`` (GPU engine). Training steps publish it from the optimizer kernel
+        (``_w16_managed``); in evaluation mode the cast is cached until the parameter changes (its version counter,
+        which torch in-place ops and the native TensorMath backend bump), so inference casts each weight once."""
         if self._w16_managed and name in self._w16:
             return self._w16[name]
         w = getattr(self, name)
+        key = None
+        if not self.train and w.is_cuda:
+            key = (w.data_ptr(), w._version, tuple(w.shape), w.stride(), w.dtype)
+            hit = self.__dict__.get("_w16_cache", {}).get(name)
+            if hit is not None and hit[0] == key:
+                return hit[1]
         from .. import ops
 
         if w.dim() == 4 and w.is_contiguous(memory_format=torch.channels_last):
             out = torch.empty_like(w, dtype=torch.bfloat16)
             ops.native.get().cast_f32_bf16(w.permute(0, 2, 3, 1).contiguous().view(-1),
                                            out.permute(0, 2, 3, 1).view(-1))
-            return out
-        return ops.to_bf16(w)
+        else:
+            out = ops.to_bf16(w)
+        if key is not None:
+            self.__dict__.setdefault("_w16_cache", {})[name] = (key, out)
+        return out
 
     def mark_w16_dirty(self):
         pass
@@ -481,6 +492,7 @@ class AbstractModule(MklInt8Convertible, metaclass=_RecordInit):
     # ------------------------------------------------------------------ modes
     def training(self):
         self.train = True
+        self.__dict__.pop("_w16_cache", None)
         return self
 
     def evaluate(self, *args, **kw):

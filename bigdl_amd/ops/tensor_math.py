@@ -6,6 +6,7 @@ dot). ``native_ok(*tensors)`` says whether a call can take this path (every tens
 falls back to torch for other dtypes and for the CPU engine.
 """
 import torch
+from torch.autograd.graph import increment_version
 
 from . import native
 
@@ -56,6 +57,7 @@ def apply(op, out, a=None, b=None, c=None, s0=0.0, s1=0.0):
     contiguous = out.is_contiguous() and all(t.is_contiguous() for t in present)
     native.get().tensor_apply(out, ops[0], ops[1], ops[2], size, sts[0], sa, sb, sc, int(op), float(s0), float(s1),
                               contiguous)
+    increment_version(out)      # written through a raw pointer: keep version-keyed caches (Module.w16) honest
     return True
 
 
@@ -114,6 +116,7 @@ def gemm(C, A, B, M=None, alpha=1.0, beta=0.0):
          A3.stride(0) if bt > 1 else 0, B3.stride(0) if bt > 1 else 0, C3.stride(0) if bt > 1 else 0,
          M3.stride(0) if (M3 is not None and bt > 1) else 0]
     native.get().gemm_f32(A3, B3, M3, C3, bt, m, n, k, s, float(alpha), float(beta if M3 is not None else 0.0))
+    increment_version(C)
     return C
 
 
@@ -122,6 +125,7 @@ def gemv(y, A, x, M=None, alpha=1.0, beta=0.0):
     Mv = M.expand(m) if M is not None else None
     s = [A.stride(0), A.stride(1), x.stride(0), Mv.stride(0) if Mv is not None else 0, y.stride(0)]
     native.get().gemv_f32(A, x, Mv, y, m, k, s, float(alpha), float(beta if Mv is not None else 0.0))
+    increment_version(y)
     return y
 
 
