@@ -206,6 +206,8 @@ def main():
             if graph_ms >= 0.99 * eager_ms:
                 graph.release()
                 graph = None
+                torch.cuda.synchronize()
+                torch.cuda.empty_cache()      # hand the graph's private pool back to the device
                 run = lambda: step.step(x, y)  # noqa: E731
                 run()
     torch.cuda.synchronize()
@@ -218,6 +220,18 @@ def main():
     barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    if os.environ.get("BIGDL_BENCH_TRACE") == "1":     # diagnostics after the timed region: per-step times, memory
+        free, total = torch.cuda.mem_get_info(dev)
+        print(f"[bench trace] reserved {torch.cuda.memory_reserved(dev) / 2**30:.1f} GiB, max allocated "
+              f"{torch.cuda.max_memory_allocated(dev) / 2**30:.1f} GiB, device free {free / 2**30:.1f} / "
+              f"{total / 2**30:.1f} GiB", file=sys.stderr, flush=True)
+        for i in range(8):
+            torch.cuda.synchronize()
+            a = time.perf_counter()
+            run()
+            torch.cuda.synchronize()
+            print(f"[bench trace] step {i}: {(time.perf_counter() - a) * 1e3:.2f} ms, reserved "
+                  f"{torch.cuda.memory_reserved(dev) / 2**30:.1f} GiB", file=sys.stderr, flush=True)
     t = torch.tensor([dt], device=dev)
     if world > 1:
         import torch.distributed as dist

@@ -104,3 +104,4 @@ class GraphedTrainStep:
         for m in self.methods:
             m._lr_dev = None
         self.graph = None
+        self.x = self.y = self.loss = None     # static buffers live in the graph pool

@@ -411,6 +411,8 @@ class Optimizer:
                         if not self._graph_keep(step, eager_ms, graph_ms):
                             g.release()
                             g, self._graph, use_graph = None, None, False
+                            torch.cuda.synchronize()
+                            torch.cuda.empty_cache()     # the graph's private pool back to the device
                 else:
                     loss = g.eager(x, y)
                 n_ok = 1
@@ -441,6 +443,7 @@ class Optimizer:
                 if "e0" in timing and "e1" not in timing:
                     timing["e1"] = torch.cuda.Event(enable_timing=True)
                     timing["e1"].record()
+            step.throttle()          # the host stays at most TrainStep.MAX_INFLIGHT iterations ahead of the device
             self.metrics.add("computing time", time.perf_counter() - t1)
             records = batch.size() * world
             pending.append((st["neval"], loss.detach() if torch.is_tensor(loss) else torch.tensor(float(loss)),
