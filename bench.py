@@ -186,6 +186,13 @@ def main():
         from bigdl_amd.optim.graphed import GraphedTrainStep
 
         eager_ms = timed(run) if mode < 0 else None
+        host_ms = None
+        if mode < 0:       # host cost of enqueueing one iteration (right after a sync: no throttle wait)
+            torch.cuda.synchronize()
+            h0 = time.perf_counter()
+            run()
+            host_ms = (time.perf_counter() - h0) * 1e3
+            torch.cuda.synchronize()
         try:
             graph = GraphedTrainStep(step, x, y, prewarmed=True)
             graph.replay()
@@ -196,14 +203,16 @@ def main():
             side_stream.reset()
             graph = None
         if mode < 0 and graph is not None:
-            t = torch.tensor([eager_ms, graph_ms], device=dev)
+            t = torch.tensor([eager_ms, graph_ms, host_ms], device=dev)
             if world > 1:
                 import torch.distributed as dist
 
                 dist.all_reduce(t)
-            eager_ms, graph_ms = (float(v) / world for v in t.cpu())
-            decision = {"eager_ms": round(eager_ms, 3), "graph_ms": round(graph_ms, 3)}
-            if graph_ms >= 0.99 * eager_ms:
+            eager_ms, graph_ms, host_ms = (float(v) / world for v in t.cpu())
+            decision = {"eager_ms": round(eager_ms, 3), "graph_ms": round(graph_ms, 3), "host_ms": round(host_ms, 3)}
+            # eager only when clearly faster AND the host has headroom: an eager step whose enqueue takes more than
+            # half the device time turns host-bound on a busier CPU, while a replay costs ~1 ms of host time
+            if eager_ms < 0.97 * graph_ms and host_ms < 0.5 * eager_ms:
                 graph.release()
                 graph = None
                 torch.cuda.synchronize()
@@ -232,6 +241,17 @@ def main():
             torch.cuda.synchronize()
             print(f"[bench trace] step {i}: {(time.perf_counter() - a) * 1e3:.2f} ms, reserved "
                   f"{torch.cuda.memory_reserved(dev) / 2**30:.1f} GiB", file=sys.stderr, flush=True)
+        if step is not None:      # host cost of enqueueing one iteration (no throttle wait): the eager-mode CPU floor
+            old_if = step.MAX_INFLIGHT
+            step.MAX_INFLIGHT = 1 << 20
+            torch.cuda.synchronize()
+            a = time.perf_counter()
+            for _ in range(4):
+                run()
+            host = (time.perf_counter() - a) / 4 * 1e3
+            torch.cuda.synchronize()
+            step.MAX_INFLIGHT = old_if
+            print(f"[bench trace] host enqueue time {host:.2f} ms/iteration", file=sys.stderr, flush=True)
     t = torch.tensor([dt], device=dev)
     if world > 1:
         import torch.distributed as dist

@@ -349,7 +349,7 @@ class Optimizer:
                 return False        # host-side (gloo) collectives cannot be replayed between graph segments
         return step.device.type == "cuda" and drop is None and flag not in ("0", "false", "no") and graphable(step)
 
-    def _graph_keep(self, step, eager_ms, graph_ms):
+    def _graph_keep(self, step, eager_ms, graph_ms, host_ms=0.0):
         """``bigdl.optim.graph`` = auto (default): keep the captured iteration only if its replays are faster on the
         device than the timed eager iteration (a launch-bound model gains from the graph; a large-batch model whose
         eager iteration overlaps its weight-gradient side stream better than the graph's replay does not). The
@@ -357,15 +357,18 @@ class Optimizer:
         flag = str(Engine.getProperty("bigdl.optim.graph", "auto")).lower()
         if flag != "auto":
             return True
-        t = torch.tensor([eager_ms, graph_ms], device=step.device)
+        t = torch.tensor([eager_ms, graph_ms, host_ms], device=step.device)
         if step.comm.world > 1:
             step.comm.all_reduce_scalar(t)
-        eager_ms, graph_ms = (float(v) for v in t.cpu())
-        keep = graph_ms < 0.99 * eager_ms
-        logger.info("iteration on the device: eager %.3f ms, HIP graph %.3f ms -> %s", eager_ms / max(1, step.comm.world),
-                    graph_ms / max(1, step.comm.world), "graph" if keep else "eager")
-        self.graph_decision = {"eager_ms": eager_ms / max(1, step.comm.world),
-                               "graph_ms": graph_ms / max(1, step.comm.world), "graph": keep}
+        eager_ms, graph_ms, host_ms = (float(v) for v in t.cpu())
+        # eager only when clearly faster and the host has headroom (an eager iteration whose enqueue takes more than
+        # half its device time turns host-bound on a busier CPU; a replay needs ~1 ms of host time)
+        keep = not (eager_ms < 0.97 * graph_ms and host_ms < 0.5 * eager_ms)
+        w = max(1, step.comm.world)
+        logger.info("iteration: eager %.3f ms on the device (%.3f ms host), HIP graph %.3f ms -> %s", eager_ms / w,
+                    host_ms / w, graph_ms / w, "graph" if keep else "eager")
+        self.graph_decision = {"eager_ms": eager_ms / w, "graph_ms": graph_ms / w, "host_ms": host_ms / w,
+                               "graph": keep}
         return keep
 
     def _train_iterations(self, st, step, world, drop, it, wall0, pending, watchdog):
@@ -408,7 +411,7 @@ class Optimizer:
                         timing["g3"].synchronize()
                         graph_ms = timing["g1"].elapsed_time(timing["g3"]) / 2
                         eager_ms = timing["e0"].elapsed_time(timing["e1"])
-                        if not self._graph_keep(step, eager_ms, graph_ms):
+                        if not self._graph_keep(step, eager_ms, graph_ms, timing.get("host_ms", 0.0)):
                             g.release()
                             g, self._graph, use_graph = None, None, False
                             torch.cuda.synchronize()
@@ -424,6 +427,7 @@ class Optimizer:
                 if eager_done == 1 and use_graph:
                     timing["e0"] = torch.cuda.Event(enable_timing=True)
                     timing["e0"].record()
+                    timing["h0"] = time.perf_counter()
                 step.zero_grad()
                 if drop is not None:
                     # straggler cancellation: past the deadline every module boundary raises StragglerTimeout, so
@@ -443,6 +447,7 @@ class Optimizer:
                 if "e0" in timing and "e1" not in timing:
                     timing["e1"] = torch.cuda.Event(enable_timing=True)
                     timing["e1"].record()
+                    timing["host_ms"] = (time.perf_counter() - timing["h0"]) * 1e3
             step.throttle()          # the host stays at most TrainStep.MAX_INFLIGHT iterations ahead of the device
             self.metrics.add("computing time", time.perf_counter() - t1)
             records = batch.size() * world

@@ -26,6 +26,8 @@ collectives — can be captured into a HIP graph once buffers are warm (``optim/
 """
 import copy
 
+import os
+
 import torch
 
 from ..optim.regularizer import L1L2Regularizer
@@ -433,7 +435,7 @@ class TrainStep:
         self.throttle()
         return loss
 
-    MAX_INFLIGHT = 2
+    MAX_INFLIGHT = int(os.environ.get("BIGDL_MAX_INFLIGHT", "2"))
 
     def throttle(self):
         """Bound how many enqueued iterations the host runs ahead of the device (``MAX_INFLIGHT``). Blocks that a
