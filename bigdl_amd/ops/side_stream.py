@@ -72,6 +72,11 @@ def pending():
     return bool(_PENDING)
 
 
+def pending_stream():
+    """The one side stream with work not yet joined, or None (none pending, or several)."""
+    return _PENDING[0] if len(_PENDING) == 1 else None
+
+
 def reset():
     """Forget the side streams (after an aborted HIP-graph capture a stream forked into it is not reusable)."""
     _PENDING.clear()

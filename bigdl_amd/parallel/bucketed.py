@@ -208,8 +208,19 @@ class BucketedGradSync:
             return
         b0, b1 = self.bounds[b]
         self.launch_log.append(b)
-        _side.join()     # weight gradients issued on the side stream (ops/side_stream.py) land first
-        self.works[b] = self.comm.reduce_scatter_range(self.g, b0, b1, async_op=True)[0]
+        from . import graph_segments
+
+        side = _side.pending_stream()
+        if side is None or graph_segments.active() is not None or not getattr(self.comm, "_inplace", False):
+            _side.join()     # weight gradients issued on the side stream (ops/side_stream.py) land first
+            self.works[b] = self.comm.reduce_scatter_range(self.g, b0, b1, async_op=True)[0]
+            return
+        # launch from the side stream after it waited for the compute stream (BN parameter gradients are written
+        # there): the collective follows every weight gradient of the bucket, and the compute stream never stalls
+        # for the side stream mid-backward; update() waits for the collective on the compute stream
+        side.wait_stream(torch.cuda.current_stream(side.device))
+        with torch.cuda.stream(side):
+            self.works[b] = self.comm.reduce_scatter_range(self.g, b0, b1, async_op=True)[0]
 
     def after_backward(self, m):
         if self.step.defer_sync:   # straggler drop: every rank reduces after the finished vote (TrainStep)
