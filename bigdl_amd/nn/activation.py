@@ -315,12 +315,16 @@ class SoftMax(AutogradModule):
         self.pos = pos
 
     def fn(self, x):
-        return torch.softmax(x.float(), _softmax_dim(x, self.pos)).to(x.dtype)
+        from ..ops import nnk
+
+        return nnk.softmax(x, _softmax_dim(x, self.pos)).to(x.dtype)    # GPU, last dim: native (ops/nnk.py)
 
 
 class SoftMin(AutogradModule):
     def fn(self, x):
-        return torch.softmax(-x.float(), _softmax_dim(x, None)).to(x.dtype)
+        from ..ops import nnk
+
+        return nnk.softmax(-x, _softmax_dim(x, None)).to(x.dtype)
 
 
 class LogSoftMax(AutogradModule):

@@ -167,6 +167,44 @@ def log_softmax(x):
     return _LogSoftmax.apply(xf) if _gpu(x) else torch.log_softmax(xf, -1)
 
 
+class _Softmax(torch.autograd.Function):
+    """softmax = exp(log-softmax) on the native row kernel and the TensorMath backend (ops/tensor_math.py);
+    backward gx = y * (gy - sum(gy * y)) as a native reduction and one broadcast element pass."""
+
+    @staticmethod
+    def forward(ctx, x):
+        from . import tensor_math as tm
+
+        x = x.contiguous()
+        y = torch.empty_like(x)
+        native.get().log_softmax_fwd(x, y)
+        tm.apply(tm.EXP, y, y)
+        ctx.save_for_backward(y)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        from . import tensor_math as tm
+
+        (y,) = ctx.saved_tensors
+        gy = gy.contiguous().float()
+        prod = torch.empty_like(y)
+        tm.apply(tm.MUL, prod, gy, y)
+        s, _ = tm.reduce(prod, tm.R_SUM, y.dim() - 1)           # [..., 1]
+        gx = torch.empty_like(y)
+        tm.apply(tm.SUB, gx, gy, s.expand(y.shape), s0=1.0)      # gy - sum(gy * y)
+        tm.apply(tm.MUL, gx, gx, y)
+        return gx
+
+
+def softmax(x, dim=-1):
+    """Softmax over ``dim``; native on the GPU when ``dim`` is the last dimension of an fp32 / bf16 tensor."""
+    d = dim if dim >= 0 else x.dim() + dim
+    if _gpu(x) and d == x.dim() - 1 and x.numel() > 0:
+        return _Softmax.apply(x.float())
+    return torch.softmax(x.float(), d)
+
+
 # ---------------------------------------------------------------------------------------------- bf16 truncation
 def f32_to_bf16_rtz(x, out=None):
     x = x.contiguous().float()

@@ -303,8 +303,7 @@ class Int8GraphPlan:
             if view is not None:
                 return view, True
         Cp = _ceil16(C)
-        buf = (torch.empty if Cp == C else torch.zeros)((N, H, W, Cp), dtype=torch.int8, device=dev)
-        return buf, False
+        return _i8_buffer((N, H, W, Cp), C, dev), False
 
     def _input_runner(self, n):
         scale = self.scale[n.id]
@@ -314,8 +313,7 @@ class Int8GraphPlan:
                 return x
             x = x.contiguous()
             N, C, H, W = x.shape
-            q = (torch.empty if _ceil16(C) == C else torch.zeros)((N, H, W, _ceil16(C)), dtype=torch.int8,
-                                                                   device=x.device)
+            q = _i8_buffer((N, H, W, _ceil16(C)), C, x.device)
             native.get().quantize_nchw_f32(x, q, _ceil16(C), float(scale))
             return I8Act(q, C, scale)
         return run
@@ -332,8 +330,7 @@ class Int8GraphPlan:
                 return None
             o = self.res[add_id][1]
             sc = (self.amax.get(o.id, 0.0) or float(a.abs().max()) or 1.0) / 127.0
-            q = (torch.empty if _ceil16(K) == K else torch.zeros)((N, OH, OW, _ceil16(K)), dtype=torch.int8,
-                                                                   device=a.device)
+            q = _i8_buffer((N, OH, OW, _ceil16(K)), K, a.device)
             _quantize_into(a, q[..., :K], q.shape[3], sc)
             a = I8Act(q, K, sc)
         self.fused[add_id] = True
@@ -488,7 +485,7 @@ class _I8Concat:
                     return None
                 total += w
             Cp = _ceil16(total)
-            self.buf = (torch.empty if Cp == total else torch.zeros)((N, H, W, Cp), dtype=torch.int8, device=dev)
+            self.buf = _i8_buffer((N, H, W, Cp), total, dev)
             self.total = total
         b = self.buf
         if b.shape[0] != N or b.shape[1] != H or b.shape[2] != W:
@@ -506,8 +503,7 @@ class _I8Concat:
         total = sum(t.shape[1] for t in ts)
         if buf is None or buf.shape[3] != _ceil16(total):
             Cp = _ceil16(total)
-            buf = (torch.empty if Cp == total else torch.zeros)((N, H, W, Cp), dtype=torch.int8,
-                                                                 device=_device_of(ts))
+            buf = _i8_buffer((N, H, W, Cp), total, _device_of(ts))
         off = 0
         for t in ts:
             C = t.shape[1]
@@ -515,13 +511,27 @@ class _I8Concat:
             if isinstance(t, I8Act):
                 if t.data.data_ptr() != sl.data_ptr():
                     if abs(t.scale - scale) <= 1e-12 * max(scale, 1e-30):
-                        sl.copy_(t.data[..., :C])
+                        if sl.is_cuda:
+                            native.get().copy_rows_i8(t.data, sl, N * H * W, C, t.data.stride(2), sl.stride(2))
+                        else:
+                            sl.copy_(t.data[..., :C])
                     else:        # a differently scaled int8 input: go through bf16 once
                         _quantize_into(t.dequantize(), sl, buf.shape[3], scale)
             else:
                 _quantize_into(t, sl, buf.shape[3], scale)
             off += C
         return I8Act(buf, total, scale)
+
+
+def _i8_buffer(shape, C, dev):
+    """int8 NHWC buffer whose last dim is padded past C: the padding channels must read as zero (native byte fill,
+    no aten kernel); unpadded buffers are left uninitialised."""
+    buf = torch.empty(shape, dtype=torch.int8, device=dev)
+    if shape[-1] != C and buf.is_cuda:
+        native.get().fill_bytes(buf, 0)
+    elif shape[-1] != C:
+        buf.zero_()
+    return buf
 
 
 def _quantize_into(t, sl, ld, scale):

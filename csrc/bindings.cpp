@@ -255,6 +255,23 @@ void gemv_f32(const Tensor& A, const Tensor& x, const OptT& Min, const Tensor& y
                                 s[3], s[4], (float)alpha, (float)beta, stream());
   TORCH_CHECK(rc == 0, "gemv_f32 failed");
 }
+// byte fill of a whole GPU tensor (hipMemsetAsync: a runtime fill, no aten kernel) — int8 buffers' padding channels
+void fill_bytes(const Tensor& t, int64_t value) {
+  TORCH_CHECK(t.is_cuda() && t.is_contiguous(), "fill_bytes: contiguous GPU tensor");
+  if (t.numel() == 0) return;
+  TORCH_CHECK(hipMemsetAsync(t.data_ptr(), (int)value, t.numel() * t.element_size(), stream()) == hipSuccess,
+              "fill_bytes: hipMemsetAsync failed");
+}
+void copy_rows_i8(const Tensor& src, const Tensor& dst, int64_t rows, int64_t C, int64_t lds, int64_t ldd) {
+  TORCH_CHECK(src.is_cuda() && dst.is_cuda() && src.scalar_type() == at::kChar && dst.scalar_type() == at::kChar,
+              "copy_rows_i8: int8 GPU tensors");
+  TORCH_CHECK(rows >= 0 && C >= 0 && lds >= C && ldd >= C, "copy_rows_i8: geometry");
+  const int64_t span_s = rows ? (rows - 1) * lds + C : 0, span_d = rows ? (rows - 1) * ldd + C : 0;
+  TORCH_CHECK(span_s <= (int64_t)src.storage().nbytes() - src.storage_offset() &&
+                  span_d <= (int64_t)dst.storage().nbytes() - dst.storage_offset(),
+              "copy_rows_i8: rows exceed the tensors' storage");
+  bigdl_copy_rows_i8((const int8_t*)src.data_ptr(), (int8_t*)dst.data_ptr(), rows, (int)C, lds, ldd, stream());
+}
 void cast_f32_bf16(const Tensor& x, const Tensor& y) {
   TORCH_CHECK(x.numel() == y.numel() && x.is_contiguous() && y.is_contiguous(), "cast: size");
   bigdl_cast_f32_bf16(cf(x, "x"), mbf(y, "y"), x.numel(), stream());
@@ -953,6 +970,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("p"), py::arg("out"), py::arg("outi"), py::arg("mean"), py::arg("ws"), py::arg("chunks"));
   m.def("gemm_f32", &gemm_f32);
   m.def("gemv_f32", &gemv_f32);
+  m.def("fill_bytes", &fill_bytes);
+  m.def("copy_rows_i8", &copy_rows_i8);
   m.def("cast_f32_bf16", &cast_f32_bf16);
   m.def("cast_bf16_f32", &cast_bf16_f32);
   m.def("maxpool_fwd", &maxpool_fwd);

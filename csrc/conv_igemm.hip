@@ -1659,7 +1659,10 @@ __global__ __launch_bounds__(512, 1) void conv_nt_w8_kernel(ConvArgs a) {
 // 2-stage glds kernel drains its DMA queue at every K-step barrier. Same 64-byte-row LDS image, source-side swizzle
 // g ^ ((r >> 1) & 3), tap table behind the stages.
 // ------------------------------------------------------------------------------------------------
-template <int BN, int NS>
+// FASTK = false (Cs % 32 != 0, e.g. Inception's 48 / 80 / 160-channel inputs, padded to 8): a K-step spans taps, so
+// every lane resolves the tap of its own 8-channel granule (kk = k0 + 8 * gsrc) from the LDS tap table and the K
+// tail past Kdim loads zeros.
+template <int BN, int NS, bool FASTK = true>
 __global__ __launch_bounds__(256, NS == 3 ? 3 : 2) void conv_nt_g4_kernel(ConvArgs a) {
   constexpr int BM = 128, BKS = 32;
   constexpr int WGM = 2, WGN = 2;
@@ -1683,7 +1686,7 @@ __global__ __launch_bounds__(256, NS == 3 ? 3 : 2) void conv_nt_g4_kernel(ConvAr
   const int bid = xcd_remap(blockIdx.x, nwg);
   const int tm = bid / tiles_n, tn = bid % tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
-  const int nk = a.Kdim / BKS;
+  const int nk = (a.Kdim + BKS - 1) / BKS;
 
   // DMA geometry: instruction j of wave w fills rows (j * 4 + w) * 16 .. +16 (64 B each); lane -> row + (lane >> 2),
   // slot lane & 3, which holds granule (lane & 3) ^ ((row >> 1) & 3)
@@ -1710,7 +1713,7 @@ __global__ __launch_bounds__(256, NS == 3 ? 3 : 2) void conv_nt_g4_kernel(ConvAr
   for (int j = 0; j < BI; ++j) {
     const int n = n0 + (j * 4 + wave) * 16 + rsub;
     bvalid[j] = n < a.Ncol;
-    wrow[j] = a.wt + (size_t)(bvalid[j] ? n : 0) * a.ldw + gsrc * 8;
+    wrow[j] = a.wt + (size_t)(bvalid[j] ? n : 0) * a.ldw + (FASTK ? gsrc * 8 : 0);
   }
   if (tid < a.ntaps) {
     taps[tid] = a.tap_h[tid];
@@ -1721,23 +1724,35 @@ __global__ __launch_bounds__(256, NS == 3 ? 3 : 2) void conv_nt_g4_kernel(ConvAr
 
   auto issue = [&](int kt, int buf) {
     const int k0 = kt * BKS;
-    const int t = k0 / a.Cs;
-    const int cin = k0 - t * a.Cs;
-    const int th = taps[t], tw = taps[CONV_MAX_TAPS + t];
-    const int wk = taps[2 * CONV_MAX_TAPS + t] * a.Cs + cin;
-    const int c = cin + gsrc * 8;
+    int th, tw, wk, c;
+    bool kv = true;
+    if constexpr (FASTK) {                  // the whole K-step lies in one tap
+      const int t = k0 / a.Cs;
+      const int cin = k0 - t * a.Cs;
+      th = taps[t]; tw = taps[CONV_MAX_TAPS + t];
+      wk = taps[2 * CONV_MAX_TAPS + t] * a.Cs + cin;
+      c = cin + gsrc * 8;
+    } else {                                // per-lane tap of granule kk
+      const int kk = k0 + gsrc * 8;
+      kv = kk < a.Kdim;
+      const int kc = kv ? kk : 0;
+      const int t = kc / a.Cs;
+      c = kc - t * a.Cs;
+      th = taps[t]; tw = taps[CONV_MAX_TAPS + t];
+      wk = taps[2 * CONV_MAX_TAPS + t] * a.Cs + c;
+    }
     bf16_t* A = lds + buf * STAGE;
     bf16_t* B = A + BM * BKS;
 #pragma unroll
     for (int j = 0; j < AI; ++j) {
       const int ch = a_h[j] + th, cw = a_w[j] + tw;
-      const bool ok = (unsigned)ch < (unsigned)a.Hs && (unsigned)cw < (unsigned)a.Ws;
+      const bool ok = kv && (unsigned)ch < (unsigned)a.Hs && (unsigned)cw < (unsigned)a.Ws;
       const bf16_t* src = ok ? a.src + (unsigned)((a_pix[j] + ch * a.Ws + cw) * a.Cs + c) : g_zero_granule;
       glds16(src, (LDS_PTR(void))(A + (j * 4 + wave) * 16 * BKS));
     }
 #pragma unroll
     for (int j = 0; j < BI; ++j) {
-      const bf16_t* src = bvalid[j] ? wrow[j] + wk : g_zero_granule;
+      const bf16_t* src = (bvalid[j] && kv) ? wrow[j] + wk : g_zero_granule;
       glds16(src, (LDS_PTR(void))(B + (j * 4 + wave) * 16 * BKS));
     }
   };
@@ -1966,7 +1981,8 @@ static int w8_pick(const ConvArgs* a) {
 template <int BN, int NS>
 void launch_nt_g4(const ConvArgs& a, hipStream_t st) {
   const int nwg = ((a.M + 127) / 128) * ((a.Ncol + BN - 1) / BN);
-  conv_nt_g4_kernel<BN, NS><<<dim3(nwg), dim3(256), 0, st>>>(a);
+  if (a.Cs % 32 == 0) conv_nt_g4_kernel<BN, NS, true><<<dim3(nwg), dim3(256), 0, st>>>(a);
+  else conv_nt_g4_kernel<BN, NS, false><<<dim3(nwg), dim3(256), 0, st>>>(a);
 }
 
 // BIGDL_CONV_G4 (default 3): 0 = off, 4 = 4-stage (2 workgroups per CU), 3 = 3-stage (3 per CU) deep-pipelined 128-row kernel
@@ -1979,6 +1995,12 @@ static int g4_pick() {
     g_conv_g4 = e ? atoi(e) : 3;   // 3-stage default: ResNet-50 b256 27.35 -> 26.48 ms/step (profiles/r3_conv_g4_ab.txt)
   }
   return g_conv_g4;
+}
+
+// BIGDL_CONV_G4_SLOWK (default 1): the multi-stage kernel also for Cs % 32 != 0 (per-lane taps)
+static bool g4_slowk() {
+  static const int v = [] { const char* e = getenv("BIGDL_CONV_G4_SLOWK"); return e ? atoi(e) : 1; }();
+  return v != 0;
 }
 
 int g_conv_impl = -1;
@@ -2037,7 +2059,7 @@ int bigdl_conv_nt(const ConvArgs* a, hipStream_t st) {
   } else if (w8 == 1) {
     const int nwg = ((a->M + 255) / 256) * ((a->Ncol + 255) / 256);
     conv_nt_w8_kernel<false><<<dim3(nwg), dim3(512), 0, st>>>(*a);
-  } else if (impl == 1 && g4_pick() && (a->Cs % 32) == 0 && aligned_out &&
+  } else if (impl == 1 && g4_pick() && aligned_out && (a->Cs % 32 == 0 || (g4_slowk() && a->Kdim % 8 == 0)) &&
              (g4_pick() == 5 || !(p3_pick && fastk && p3_tiles >= 256))) {
     if (g4_pick() != 4) {
       if (a->Ncol <= 64) launch_nt_g4<64, 3>(*a, st);

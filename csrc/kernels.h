@@ -164,6 +164,7 @@ int bigdl_gemm_f32(const float* A, const float* B, const float* Min, float* C, i
                    const long* s, float alpha, float beta, hipStream_t st);
 int bigdl_gemv_f32(const float* A, const float* x, const float* Min, float* y, int M, int K, long sam, long sak,
                    long sx, long smi, long sy, float alpha, float beta, hipStream_t st);
+void bigdl_copy_rows_i8(const int8_t* src, int8_t* dst, long rows, int C, long lds, long ldd, hipStream_t st);
 void bigdl_set_conv_impl(int impl);
 int bigdl_get_conv_impl();
 void bigdl_set_conv_g4(int v);

@@ -344,7 +344,9 @@ __global__ __launch_bounds__(256, 2) void conv_i8_glds_kernel(ConvArgs a, I8Epi 
 // tap). The epilogue is conv_i8_glds_kernel's, run in two row halves so a wave's fp32 slice fits the stages.
 // Tiles: 128 x 128 (2 x 2 waves) or, for the narrow layers (Ncol <= 64 / <= 32), 256 x 64 / 256 x 32 with the four
 // waves stacked along M (as conv_i8_glds_kernel).
-template <int BM, int BN, int WGM, int WGN>
+// FASTK = false (Cs % 64 != 0: Inception's 48 / 80 / 96 / 160 / ...-channel inputs, padded to 16): every lane resolves
+// the tap of its own 16-channel granule from the LDS tap table; the K tail past Kdim loads zeros.
+template <int BM, int BN, int WGM, int WGN, bool FASTK = true>
 __global__ __launch_bounds__(256, (BM + (BN + 63) / 64 * 64) * 64 * 3 <= 52 * 1024 ? 3 : 2) void conv_i8_g3_kernel(
     ConvArgs a, I8Epi ep) {
   constexpr int BKB = 64, NS = 3;
@@ -369,7 +371,7 @@ __global__ __launch_bounds__(256, (BM + (BN + 63) / 64 * 64) * 64 * 3 <= 52 * 10
   const int bid = xcd_remap(blockIdx.x, nwg);
   const int tm = bid / tiles_n, tn = bid % tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
-  const int nk = a.Kdim / BKB;
+  const int nk = (a.Kdim + BKB - 1) / BKB;
 
   const int rsub = lane >> 2;
   const int gsrc = (lane & 3) ^ ((rsub >> 1) & 3);
@@ -395,7 +397,7 @@ __global__ __launch_bounds__(256, (BM + (BN + 63) / 64 * 64) * 64 * 3 <= 52 * 10
     const int nl = (j * 4 + wave) * 16 + rsub;     // tile row; rows past BN (BN = 32) load into a spare slot
     const int n = n0 + nl;
     bvalid[j] = nl < BN && n < a.Ncol;
-    wrow[j] = wt + (size_t)(bvalid[j] ? n : 0) * a.ldw + gsrc * 16;
+    wrow[j] = wt + (size_t)(bvalid[j] ? n : 0) * a.ldw + (FASTK ? gsrc * 16 : 0);
   }
   if (tid < a.ntaps) {
     taps[tid] = a.tap_h[tid];
@@ -406,23 +408,35 @@ __global__ __launch_bounds__(256, (BM + (BN + 63) / 64 * 64) * 64 * 3 <= 52 * 10
 
   auto issue = [&](int kt, int buf) {
     const int k0 = kt * BKB;
-    const int t = k0 / a.Cs;
-    const int cin = k0 - t * a.Cs;
-    const int th = taps[t], tw = taps[CONV_MAX_TAPS + t];
-    const int wk = taps[2 * CONV_MAX_TAPS + t] * a.Cs + cin;
-    const int c = cin + gsrc * 16;
+    int th, tw, wk, c;
+    bool kv = true;
+    if constexpr (FASTK) {
+      const int t = k0 / a.Cs;
+      const int cin = k0 - t * a.Cs;
+      th = taps[t]; tw = taps[CONV_MAX_TAPS + t];
+      wk = taps[2 * CONV_MAX_TAPS + t] * a.Cs + cin;
+      c = cin + gsrc * 16;
+    } else {
+      const int kk = k0 + gsrc * 16;
+      kv = kk < a.Kdim;
+      const int kc = kv ? kk : 0;
+      const int t = kc / a.Cs;
+      c = kc - t * a.Cs;
+      th = taps[t]; tw = taps[CONV_MAX_TAPS + t];
+      wk = taps[2 * CONV_MAX_TAPS + t] * a.Cs + c;
+    }
     uint8_t* A = lds + buf * STAGE;
     uint8_t* B = A + BM * BKB;
 #pragma unroll
     for (int j = 0; j < AI; ++j) {
       const int ch = a_h[j] + th, cw = a_w[j] + tw;
-      const bool ok = (unsigned)ch < (unsigned)a.Hs && (unsigned)cw < (unsigned)a.Ws;
+      const bool ok = kv && (unsigned)ch < (unsigned)a.Hs && (unsigned)cw < (unsigned)a.Ws;
       const uint8_t* g = ok ? src + (size_t)(a_pix[j] + ch * a.Ws + cw) * a.Cs + c : g_zero16;
       glds16(g, (LDS_PTR(void))(A + (j * 4 + wave) * 16 * BKB));
     }
 #pragma unroll
     for (int j = 0; j < BI; ++j) {
-      const uint8_t* g = bvalid[j] ? wrow[j] + wk : g_zero16;
+      const uint8_t* g = (bvalid[j] && kv) ? wrow[j] + wk : g_zero16;
       glds16(g, (LDS_PTR(void))(B + (j * 4 + wave) * 16 * BKB));
     }
   };
@@ -553,6 +567,17 @@ __global__ __launch_bounds__(256, (BM + (BN + 63) / 64 * 64) * 64 * 3 <= 52 * 10
       }
     }
     __builtin_amdgcn_s_waitcnt(0xc07f);   // the slice is rewritten by the next half
+  }
+}
+
+// int8 rows [rows][C] from src (row stride lds) into dst (row stride ldd): a concat input that was not produced in place
+__global__ __launch_bounds__(256) void copy_rows_i8_kernel(const int8_t* __restrict__ src, int8_t* __restrict__ dst,
+                                                           long rows, int C, long lds, long ldd) {
+  const long total = rows * C;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / C;
+    const int c = (int)(i - r * C);
+    dst[r * ldd + c] = src[r * lds + c];
   }
 }
 
@@ -747,11 +772,17 @@ int bigdl_conv_i8(const ConvArgs* a, const float* xscale, float xs_const, const 
   const int nwg = ((a->M + 127) / 128) * ((a->Ncol + 127) / 128);
   const I8Epi ep{xscale, xs_const, wscale, out_mode, out_inv, add8, add_scale, add_ld};
   const bool fk = a->Cs % QBK == 0;
-  if (a->Ncol <= 64 && i8_g3() && a->Cs % 64 == 0) {
+  const bool g3fk = a->Cs % 64 == 0;
+  if (a->Ncol <= 64 && i8_g3()) {
     const int bn = a->Ncol <= 32 ? 32 : 64;
     const int g = ((a->M + 255) / 256) * ((a->Ncol + bn - 1) / bn);
-    if (bn == 32) conv_i8_g3_kernel<256, 32, 4, 1><<<g, 256, 0, st>>>(*a, ep);
-    else conv_i8_g3_kernel<256, 64, 4, 1><<<g, 256, 0, st>>>(*a, ep);
+    if (bn == 32) {
+      if (g3fk) conv_i8_g3_kernel<256, 32, 4, 1, true><<<g, 256, 0, st>>>(*a, ep);
+      else conv_i8_g3_kernel<256, 32, 4, 1, false><<<g, 256, 0, st>>>(*a, ep);
+    } else {
+      if (g3fk) conv_i8_g3_kernel<256, 64, 4, 1, true><<<g, 256, 0, st>>>(*a, ep);
+      else conv_i8_g3_kernel<256, 64, 4, 1, false><<<g, 256, 0, st>>>(*a, ep);
+    }
   } else if (a->Ncol <= 32) {
     const int g = ((a->M + 255) / 256) * ((a->Ncol + 31) / 32);
     if (fk) conv_i8_glds_kernel<256, 32, 4, true><<<g, 256, 0, st>>>(*a, ep);
@@ -760,8 +791,9 @@ int bigdl_conv_i8(const ConvArgs* a, const float* xscale, float xs_const, const 
     const int g = ((a->M + 255) / 256) * ((a->Ncol + 63) / 64);
     if (fk) conv_i8_glds_kernel<256, 64, 4, true><<<g, 256, 0, st>>>(*a, ep);
     else conv_i8_glds_kernel<256, 64, 4, false><<<g, 256, 0, st>>>(*a, ep);
-  } else if (i8_g3() && a->Cs % 64 == 0) {
-    conv_i8_g3_kernel<128, 128, 2, 2><<<nwg, 256, 0, st>>>(*a, ep);
+  } else if (i8_g3()) {
+    if (g3fk) conv_i8_g3_kernel<128, 128, 2, 2, true><<<nwg, 256, 0, st>>>(*a, ep);
+    else conv_i8_g3_kernel<128, 128, 2, 2, false><<<nwg, 256, 0, st>>>(*a, ep);
   } else if (fk) {
     conv_i8_glds_kernel<128, 128, 2, true><<<nwg, 256, 0, st>>>(*a, ep);
   } else {
@@ -769,6 +801,13 @@ int bigdl_conv_i8(const ConvArgs* a, const float* xscale, float xs_const, const 
   }
   HIP_LAUNCH_CHECK();
   return 0;
+}
+
+void bigdl_copy_rows_i8(const int8_t* src, int8_t* dst, long rows, int C, long lds, long ldd, hipStream_t st) {
+  const long total = rows * C;
+  const int blocks = (int)std::min<long>((total + 255) / 256, 16384);
+  copy_rows_i8_kernel<<<blocks > 0 ? blocks : 1, 256, 0, st>>>(src, dst, rows, C, lds, ldd);
+  HIP_LAUNCH_CHECK();
 }
 
 void bigdl_pool_i8(const int8_t* x, int8_t* y, int N, int H, int W, int Cp, int OH, int OW, int kh, int kw, int sh,

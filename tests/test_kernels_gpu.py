@@ -592,6 +592,9 @@ G4_CASES = [
     (8, 256, 28, 256, 3, 2, 1),      # stride 2: dgrad phases
     (6, 128, 28, 320, 1, 1, 0),      # Ncol tail, M tail
     (4, 96, 14, 128, 3, 1, 1),       # Cs = 96: 32-channel steps across tap edges
+    (4, 48, 14, 128, 3, 1, 1),       # Cs % 32 != 0: per-lane taps (slow-K), K tail
+    (2, 80, 9, 200, 1, 1, 0),        # slow-K 1x1, Ncol tail
+    (3, 40, 11, 64, 3, 2, 1),        # slow-K, BN = 64 tile, stride 2
 ]
 
 

@@ -161,3 +161,23 @@ def test_reductions_native(monkeypatch, shape, dim):
     _close(gi, ci, 0)
     _close(nv, cnv, 0)
     _close(ni, cni, 0)
+
+
+def test_softmax_layer_native_matches_torch(monkeypatch):
+    """nn.SoftMax / SoftMin on the GPU engine: exp(native log-softmax) forward, TensorMath backward."""
+    from bigdl_amd import nn
+
+    torch.manual_seed(0)
+    x = torch.randn(6, 37)
+    gy = torch.randn(6, 37)
+    for layer, ref in ((nn.SoftMax(), torch.softmax(x, 1)), (nn.SoftMin(), torch.softmax(-x, 1))):
+        m = layer.to("cuda") if hasattr(layer, "to") else layer
+        with monkeypatch.context() as mp:
+            mp.setattr(torch, "softmax", lambda *a, **k: (_ for _ in ()).throw(AssertionError("aten softmax")))
+            y = m.forward(x.cuda())
+            gx = m.backward(x.cuda(), gy.cuda())
+        torch.cuda.synchronize()
+        assert torch.allclose(y.cpu(), ref, atol=1e-6)
+        xr = x.clone().requires_grad_(True)
+        (torch.softmax(xr if isinstance(layer, nn.SoftMax) else -xr, 1) * gy).sum().backward()
+        assert torch.allclose(gx.cpu(), xr.grad, atol=1e-5)
