@@ -75,6 +75,11 @@ def _via_optimizer(args, model, crit, optim, dev, world, rank):
 
     def hook(neval):
         if neval in (W, W + K):
+            from bigdl_amd.optim.train_step import wait_event
+
+            end = torch.cuda.Event()
+            end.record()
+            wait_event(end)
             torch.cuda.synchronize()
             if world > 1:
                 dist.barrier()
@@ -113,7 +118,7 @@ def main():
     from bigdl_amd.models.resnet import DatasetType, ResNet, ResNetGraph
     from bigdl_amd.ops import side_stream
     from bigdl_amd.optim.sgd import SGD
-    from bigdl_amd.optim.train_step import TrainStep
+    from bigdl_amd.optim.train_step import TrainStep, wait_event
     from bigdl_amd.utils.random_generator import RNG
 
     RNG.setSeed(1234 + rank)
@@ -224,12 +229,19 @@ def main():
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    stamps = []
     for _ in range(args.steps):
         run()
+        stamps.append(time.perf_counter())     # host clock after each enqueue (host-only: no device sync)
+    end = torch.cuda.Event()
+    end.record()
+    wait_event(end)             # poll until the device drained (see TrainStep.wait_event), then the contract's sync
     barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     if os.environ.get("BIGDL_BENCH_TRACE") == "1":     # diagnostics after the timed region: per-step times, memory
+        gaps = [round((b - a) * 1e3, 1) for a, b in zip([t0] + stamps[:-1], stamps)]
+        print(f"[bench trace] host enqueue-to-enqueue gaps in the timed loop (ms): {gaps}", file=sys.stderr, flush=True)
         free, total = torch.cuda.mem_get_info(dev)
         print(f"[bench trace] reserved {torch.cuda.memory_reserved(dev) / 2**30:.1f} GiB, max allocated "
               f"{torch.cuda.max_memory_allocated(dev) / 2**30:.1f} GiB, device free {free / 2**30:.1f} / "

@@ -11,8 +11,8 @@ backward, next layer) keeps going on the compute stream: the two fill the CUs to
 
 Ordering rules:
   * the side stream waits on the compute stream before each weight-gradient launch (inputs ready);
-  * every tensor the side stream reads that the compute stream allocated is ``record_stream``-ed, so the caching
-    allocator does not hand its block to a later compute-stream allocation while the GEMM still reads it;
+  * every tensor the side stream reads that the compute stream allocated is held (``keep``) until the next join, so
+    the caching allocator cannot hand its block to a later compute-stream allocation while the GEMM still reads it;
   * the compute stream waits for the side stream (``join``) when the OUTERMOST backward returns (the gradients are
     final for whatever reads them next: the optimizer, a clipping pass, user code), and before a gradient bucket's
     collective is launched (parallel/bucketed.py);
@@ -62,10 +62,17 @@ def begin(s):
     return cur
 
 
+_HELD = []
+
+
 def keep(s, *ts):
+    """Keep compute-stream tensors a side-stream kernel reads alive until the next join. (Not ``record_stream``: that
+    makes the caching allocator record and poll one event per tensor and stream at every free — hundreds per step —
+    and on ROCm a step with that many outstanding events intermittently ran 4x slower. A join makes the compute stream
+    wait for the side stream, so blocks released after it are safe to reuse on the compute stream.)"""
     for t in ts:
         if isinstance(t, torch.Tensor) and t.is_cuda:
-            t.record_stream(s)
+            _HELD.append(t)
 
 
 def pending():
@@ -81,6 +88,7 @@ def reset():
     """Forget the side streams (after an aborted HIP-graph capture a stream forked into it is not reusable)."""
     _PENDING.clear()
     _STREAMS.clear()
+    _HELD.clear()
 
 
 def join():
@@ -88,3 +96,4 @@ def join():
     while _PENDING:
         s = _PENDING.pop()
         torch.cuda.current_stream(s.device).wait_stream(s)
+    _HELD.clear()

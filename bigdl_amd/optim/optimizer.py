@@ -483,6 +483,12 @@ class Optimizer:
         if step.comm.world > 1:
             step.comm.all_reduce_scalar(losses)
             losses = losses / step.comm.world
+        if losses.is_cuda:          # poll, not a blocking wait (train_step.wait_event)
+            from .train_step import wait_event
+
+            ev = torch.cuda.Event()
+            ev.record()
+            wait_event(ev)
         vals = losses.cpu().tolist()
         st = self.state
         wall = time.perf_counter() - wall0
