@@ -50,7 +50,8 @@ def test_lstm_cell_kernel_is_used():
     assert _rel(out, ref) < 1e-2 and _rel(c, cr) < 1e-2
 
 
-@pytest.mark.parametrize("B,T,H", [(37, 6, 64), (64, 4, 1024), (5, 3, 192)])
+@pytest.mark.parametrize("B,T,H", [(37, 6, 64), (64, 4, 1024), (5, 3, 192),
+                                   (72, 4, 1024), (150, 3, 512)])     # > 256 tiles: 2 batch tiles per workgroup
 def test_fused_lstm_steps_match_fp32_reference(B, T, H):
     """csrc/lstm.hip forward/backward step kernels vs the fp32 torch LSTM recurrence (gate order i, g, f, o)."""
     from bigdl_amd.nn.recurrent import _LSTMSeq
