@@ -125,7 +125,7 @@ class Linear(TensorModule):
         if g.is_cuda:
             B = g.shape[0]
             Op, Ip = _pad8(self.outputSize), _pad8(self.inputSize)
-            g16 = g.to(BF16).contiguous()
+            g16 = ops.to_bf16(g) if g.dtype == torch.float32 else g.to(BF16).contiguous()
             if Op != self.outputSize:
                 g16 = F.pad(g16, (0, Op - self.outputSize))
             g4 = g16.view(B, Op, 1, 1)
@@ -144,7 +144,7 @@ class Linear(TensorModule):
             g4 = getattr(self, "_g16", None)
             if g4 is None or g4.shape[0] != g.shape[0]:
                 Op = _pad8(self.outputSize)
-                g16 = g.to(BF16).contiguous()
+                g16 = ops.to_bf16(g) if g.dtype == torch.float32 else g.to(BF16).contiguous()
                 if Op != self.outputSize:
                     g16 = F.pad(g16, (0, Op - self.outputSize))
                 g4 = g16.view(g.shape[0], Op, 1, 1)

@@ -187,7 +187,7 @@ class Cell(Container):
     # standalone cell (T(input, hidden) -> T(output, hidden))
     def updateOutput(self, input):
         x, h = input[1], input[2]
-        xl = x.detach().float().requires_grad_(True)
+        xl = _f32(x.detach()).requires_grad_(True)
         hl = [t.detach().float().requires_grad_(True) for t in _activity_to_hidden(h)]
         with _Leaves(self.modules) as L, torch.enable_grad():
             o, nh = self.step(self.pre_fn(xl), hl)
@@ -196,12 +196,12 @@ class Cell(Container):
 
     def updateGradInput(self, input, gradOutput):
         xl, hl, L, o, nh = self._ag
-        outs, gouts = [o], [gradOutput[1].float()]
+        outs, gouts = [o], [_f32(gradOutput[1])]
         gh = gradOutput[2] if len(gradOutput) >= 2 else None
         if gh is not None:
             for t, g in zip(nh, _activity_to_hidden(gh)):
                 outs.append(t)
-                gouts.append(g.float())
+                gouts.append(_f32(g))
         grads = torch.autograd.grad(outs, [xl] + hl + L.leaves, gouts, allow_unused=True, retain_graph=True)
         gx = grads[0] if grads[0] is not None else torch.zeros_like(xl)
         ghs = [g if g is not None else torch.zeros_like(t) for g, t in zip(grads[1:1 + len(hl)], hl)]
@@ -237,6 +237,13 @@ class RnnCell(Cell):
         return h, [h]
 
 
+def _f32(t):
+    """fp32 view of an activation / gradient: bf16 GPU tensors go through the native cast kernel."""
+    if t.is_cuda and t.dtype == torch.bfloat16:
+        return ops.to_f32(t)
+    return t.float()
+
+
 def _rnn_param_grads(dg16, h16, U, WT16):
     """Native MFMA GEMMs closing a fused recurrent backward sweep (no library GEMM):
     dU = sum_t dg_t^T h_{t-1} over all T*B rows (the conv weight-gradient kernel on a 1x1 'image' of T*B pixels:
@@ -248,7 +255,7 @@ def _rnn_param_grads(dg16, h16, U, WT16):
     dU = torch.zeros(G, H, 1, 1, device=dg16.device)
     cv.conv2d_wgrad(dg16.view(T * B, G, 1, 1), h16[:T].view(T * B, H, 1, 1), dU, None, (1, 1), (0, 0))
     dh0 = cv.conv2d_fwd(dg16[0].view(B, G, 1, 1), WT16.view(H, G, 1, 1), None, (1, 1), (0, 0))
-    return dh0.view(B, H).float(), dU.view(G, H)
+    return _f32(dh0.view(B, H)), dU.view(G, H)
 
 
 class _LSTMSeq(torch.autograd.Function):
@@ -290,19 +297,19 @@ class _LSTMSeq(torch.autograd.Function):
         if _LSTMSeq._fused_gpu(xg, U):
             # one fused launch per step (csrc/lstm.hip): bf16 MFMA recurrent GEMM + cell in its epilogue
             C = ops.native.get()
-            W16 = U.detach().to(torch.bfloat16).contiguous()
+            W16 = ops.to_bf16(U.detach())
             out = xg.new_empty(B, T, H)
             cs = xg.new_empty(T, B, H)
             acts = xg.new_empty(T, B, G)
             # time-major bf16 states h_{-1..T-1}: step t's GEMM operand, and (rows t*B + b) the B operand of the
             # weight-gradient GEMM after the backward sweep
             h16 = xg.new_empty(T + 1, B, H, dtype=torch.bfloat16)
-            h16[0].copy_(h0)
+            C.cast_f32_bf16(h0.contiguous(), h16[0])
             c_prev = c0.contiguous()
             for t in range(T):
                 C.lstm_fwd_step(W16, h16[t], xg[:, t], c_prev, cs[t], out[:, t], h16[t + 1], acts[t])
                 c_prev = cs[t]
-            ctx.save_for_backward(h0, c0, U, out, cs, acts, h16)
+            ctx.save_for_backward(h0, c0, U, out, cs, acts, h16, W16)
             ctx.fused = True
             return out, out[:, -1].clone(), cs[-1].clone()
         hs = xg.new_empty(T, B, H)
@@ -320,11 +327,13 @@ class _LSTMSeq(torch.autograd.Function):
 
     @staticmethod
     def _backward_fused(ctx, dout, dhT, dcT):
-        h0, c0, U, out, cs, acts, h16 = ctx.saved_tensors
+        from ..ops import conv as cv
+
+        h0, c0, U, out, cs, acts, h16, W16 = ctx.saved_tensors
         B, T, H = out.shape
         C = ops.native.get()
         dout = dout.contiguous() if dout is not None else None
-        WT16 = U.detach().t().contiguous().to(torch.bfloat16)
+        WT16 = cv.transpose_w(W16.view(4 * H, H, 1, 1)).view(H, 4 * H)
         dxg = out.new_empty(B, T, 4 * H)
         dg16 = out.new_empty(T, B, 4 * H, dtype=torch.bfloat16)      # time-major: rows t*B + b
         dc = dcT.contiguous().clone() if dcT is not None else out.new_zeros(B, H)
@@ -719,7 +728,7 @@ class Recurrent(Container):
         B = input.shape[0]
         x2, self._flat = self._project(input)
         need_grad = self.train
-        x2l = x2.detach().float().requires_grad_(need_grad)
+        x2l = _f32(x2.detach()).requires_grad_(need_grad)
         h0 = self._init_hidden if self._init_hidden is not None else self.cell.init_hidden(B, x2l[:, 0])
         h0l = [h.detach().float().to(x2l.device).requires_grad_(need_grad) for h in h0]
         mask = None
@@ -736,7 +745,7 @@ class Recurrent(Container):
             raise RuntimeError("Recurrent: backward called without a training forward")
         x2l, h0l, L, out, hid = self._ag
         targets = [x2l] + L.leaves + h0l
-        grads = torch.autograd.grad([out], targets, [gradOutput.float()], allow_unused=True, retain_graph=True)
+        grads = torch.autograd.grad([out], targets, [_f32(gradOutput)], allow_unused=True, retain_graph=True)
         gx2 = grads[0] if grads[0] is not None else torch.zeros_like(x2l)
         n = len(L.leaves)
         self._pending = grads[1:1 + n]
@@ -789,7 +798,7 @@ class RecurrentDecoder(Recurrent):
         B = input.shape[0]
         cell = self.cell
         need_grad = self.train
-        xl = input.detach().float().requires_grad_(need_grad)
+        xl = _f32(input.detach()).requires_grad_(need_grad)
         with _Leaves(cell.modules, need_grad) as L, torch.set_grad_enabled(need_grad):
             x = xl
             hid = self._init_hidden if self._init_hidden is not None else cell.init_hidden(B, cell.pre_fn(x))
@@ -807,7 +816,7 @@ class RecurrentDecoder(Recurrent):
 
     def updateGradInput(self, input, gradOutput):
         xl, h0l, L, out, hid = self._ag
-        grads = torch.autograd.grad([out], [xl] + L.leaves + h0l, [gradOutput.float()], allow_unused=True,
+        grads = torch.autograd.grad([out], [xl] + L.leaves + h0l, [_f32(gradOutput)], allow_unused=True,
                                     retain_graph=True)
         n = len(L.leaves)
         self._pending = grads[1:1 + n]

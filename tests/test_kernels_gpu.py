@@ -669,3 +669,16 @@ def test_conv_wgrad_g3_kernel(case):
         torch.cuda.synchronize()
     finally:
         C_.set_wgrad_g3(old)
+
+
+@pytest.mark.parametrize("K,RS,C", [(1000, 1, 1032), (2048, 9, 264), (32768, 1, 1024), (1032, 1, 10000)])
+def test_transpose_krsc_v8_matches_permute(K, RS, C):
+    """16-byte 64x64-tile transpose (K % 8 == 0, C % 8 == 0, >= 1M elements): [K][RS][C] -> [C][RS][K], tails on
+    both tile edges."""
+    from bigdl_amd.ops import native
+
+    w = torch.randn(K, RS, C, device=_dev()).to(BF)
+    out = torch.empty(C, RS, K, device=_dev(), dtype=BF)
+    native.get().transpose_krsc(w, out, K, RS, C)
+    torch.cuda.synchronize()
+    assert torch.equal(out, w.permute(2, 1, 0).contiguous())
