@@ -15,6 +15,13 @@ graph, the reduce-scatter replaced by a side-stream branch; weights after 3 repl
 So the fault needs a graph with parallel branches whose kernel nodes are this step's kernels (large-kernarg
 implicit-GEMM / BN kernels from our code object) — it is not a data race in those kernels (eager overlap is
 exact) nor allocator reuse (the branch touches a pre-capture tensor); we could not reduce it to pure PyTorch.
+Round 3 (profiles/r3_fork_graph_diag.txt): with the weight gradients on their own side stream (ops/side_stream.py,
+the default) every variant above is exact in ONE graph (tests/test_distributed_gpu.py::
+test_one_graph_step_with_forked_branches_matches_eager); with BIGDL_WGRAD_STREAM=0 it still diverges, and the
+divergence changes from run to run (1.5e-3, nan), so it is a race rather than a deterministic miscompute. A self-join
+of the compute stream just before the fork, forking through a kernel-less hop stream, or the weight-gradient kernel
+without its split-K workspace do not remove it. The segmented form stays the multi-rank capture path (it needs no
+assumption about which configuration is safe).
 Cutting the step at the collectives keeps every captured graph a single stream; overlap still happens because a
 collective issued between two graph launches runs on RCCL's stream while the next graph runs on the compute
 stream.

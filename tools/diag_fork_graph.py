@@ -6,7 +6,8 @@ Part 2 (the training step, 1 rank, one graph, no segmentation): the bucket reduc
 branch that (A) runs no kernel, (B) scales an unrelated tensor, (C) scales the bucket's gradient range in place
 (the r2 "graph_ov_fake" case), (D) like C but every branch tensor is also record_stream()'d on the side stream,
 (E) B with every zero_() as a kernel instead of a memset node, (H) B but only the bucket completed last (end of
-backward) forks, so no backward kernel runs beside the branch.
+backward) forks, so no backward kernel runs beside the branch, (J) B with the compute stream waiting on an event of
+its own just before the fork, (K) B forked through a second stream that runs no kernel.
 Each variant vs eager after the same number of steps. Prints one line per variant."""
 import os
 import sys
@@ -120,6 +121,7 @@ def part2(variant, steps=3):
     X, Y = _batch(16)
     X, Y = X.to(dev), Y.to(dev)
     side = torch.cuda.Stream()
+    hop = torch.cuda.Stream()
     other = torch.zeros(1 << 16, device=dev)
 
     class _W:
@@ -132,9 +134,17 @@ def part2(variant, steps=3):
     def rs_side(self, g, lo, hi, async_op=False, average=True):
         if variant == "H" and lo != 0:     # H: only the bucket finished LAST (at the end of backward) forks
             return None, g[lo:hi]
-        side.wait_stream(torch.cuda.current_stream())
+        if variant == "J":      # B, with the compute stream first waiting on an event it recorded itself
+            ev0 = torch.cuda.Event()
+            ev0.record()
+            torch.cuda.current_stream().wait_event(ev0)
+        if variant == "K":      # B, forked through a second side stream that runs no kernel
+            hop.wait_stream(torch.cuda.current_stream())
+            side.wait_stream(hop)
+        else:
+            side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
-            if variant in ("B", "E", "H"):
+            if variant in ("B", "E", "H", "J", "K"):
                 other.mul_(1.0)
             elif variant in ("C", "D"):
                 g[lo:hi].mul_(1.0)
@@ -184,14 +194,21 @@ def part2(variant, steps=3):
     d = (res["eager"] - res["graph"]).abs()
     print(f"part2 variant {variant}: max|w_graph - w_eager| {float(d.max()):.3e} "
           f"(frac != 0: {float((d > 0).float().mean()):.4f})", flush=True)
+    return float(d.max())
 
 
-def main(rank, world):
-    part1()
-    part1b()
+def main(rank, world, variants=()):
+    if not variants:
+        part1()
+        part1b()
+    for v in variants:
+        part2(v)
 
 
 if __name__ == "__main__":
     from bigdl_amd.utils.testing import run_distributed
 
-    run_distributed(main, 1, (), engine="gpu", backend="nccl", env={"BIGDL_FORCE_COLLECTIVES": "1"})
+    # python tools/diag_fork_graph.py            -> parts 1 / 1b (pure PyTorch)
+    # python tools/diag_fork_graph.py A B C H    -> part 2 variants (the training step as one graph)
+    run_distributed(main, 1, (tuple(sys.argv[1:]),), engine="gpu", backend="nccl",
+                    env={"BIGDL_FORCE_COLLECTIVES": "1"})
