@@ -143,3 +143,19 @@ def test_rccl_step_captured_in_hip_graph_matches_eager(overlap, compress):
     (we, he, le), (wg, hg, lg) = res
     assert torch.allclose(we, wg, atol=1e-5, rtol=1e-4), (we - wg).abs().max()
     assert abs(le - lg) < 1e-3 * max(1.0, abs(le))
+
+
+def _fork_one_graph(rank, world, variants):
+    from tools.diag_fork_graph import part2
+
+    return [part2(v) for v in variants]
+
+
+def test_one_graph_step_with_forked_branches_matches_eager():
+    """The training step captured as ONE HIP graph (no segmentation) with a side-stream branch forked at every bucket
+    that runs a kernel beside the backward kernels (tools/diag_fork_graph.py variants B: unrelated tensor, C: the
+    bucket's gradient range in place) equals eager when the weight gradients run on the side stream (the default).
+    With BIGDL_WGRAD_STREAM=0 the same capture diverges run to run (profiles/r3_fork_graph_diag.txt)."""
+    errs = run_distributed(_fork_one_graph, 1, (("B", "C"),), engine="gpu", backend="nccl",
+                           env={"BIGDL_FORCE_COLLECTIVES": "1"})[0]
+    assert all(e < 1e-6 for e in errs), errs
