@@ -754,7 +754,9 @@ int bigdl_quantize_act(const void* x, int is_bf16, int8_t* q, float* amax, float
 }
 
 int g_i8_g3 = -1;
-// BIGDL_I8_G3 (default 1): the 3-stage counted-vmcnt 128 x 128 int8 kernel for Ncol > 64, Cs % 64 == 0
+// BIGDL_I8_G3 (default 1): the 3-stage counted-vmcnt 128 x 128 int8 kernel for Ncol > 64, Cs % 64 == 0.
+// 2: also the 256 x 128 tile (2 x 2 waves of 128 x 64: 32 i8 MFMAs per wave between barriers instead of 16, 2
+// workgroups per CU) when its grid still fills two workgroups per CU; 3: the 256 x 128 tile always (tests).
 static bool i8_g3() {
   if (g_i8_g3 < 0) {
     const char* e = getenv("BIGDL_I8_G3");
@@ -763,7 +765,7 @@ static bool i8_g3() {
   return g_i8_g3 != 0;
 }
 void bigdl_set_i8_g3(int v) { g_i8_g3 = v; }
-int bigdl_get_i8_g3() { return i8_g3() ? 1 : 0; }
+int bigdl_get_i8_g3() { return i8_g3() ? g_i8_g3 : 0; }
 
 int bigdl_conv_i8(const ConvArgs* a, const float* xscale, float xs_const, const float* wscale, int out_mode,
                   float out_inv, const int8_t* add8, float add_scale, long add_ld, hipStream_t st) {
@@ -791,6 +793,10 @@ int bigdl_conv_i8(const ConvArgs* a, const float* xscale, float xs_const, const 
     const int g = ((a->M + 255) / 256) * ((a->Ncol + 63) / 64);
     if (fk) conv_i8_glds_kernel<256, 64, 4, true><<<g, 256, 0, st>>>(*a, ep);
     else conv_i8_glds_kernel<256, 64, 4, false><<<g, 256, 0, st>>>(*a, ep);
+  } else if (i8_g3() && (g_i8_g3 == 3 || (g_i8_g3 == 2 && ((a->M + 255) / 256) * ((a->Ncol + 127) / 128) >= 512))) {
+    const int g = ((a->M + 255) / 256) * ((a->Ncol + 127) / 128);
+    if (g3fk) conv_i8_g3_kernel<256, 128, 2, 2, true><<<g, 256, 0, st>>>(*a, ep);
+    else conv_i8_g3_kernel<256, 128, 2, 2, false><<<g, 256, 0, st>>>(*a, ep);
   } else if (i8_g3()) {
     if (g3fk) conv_i8_g3_kernel<128, 128, 2, 2, true><<<nwg, 256, 0, st>>>(*a, ep);
     else conv_i8_g3_kernel<128, 128, 2, 2, false><<<nwg, 256, 0, st>>>(*a, ep);

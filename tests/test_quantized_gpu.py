@@ -44,11 +44,11 @@ I8_CASES = [
 ]
 
 
-@pytest.mark.parametrize("g3", [1, 0])
+@pytest.mark.parametrize("g3", [1, 0, 3])
 @pytest.mark.parametrize("case", I8_CASES)
 def test_conv_i8_exact_integer(case, g3):
     """Scales are forced to exactly 1 (row maxima 127), so the fp32 output must equal the integer conv — for the
-    3-stage counted-vmcnt kernel (BIGDL_I8_G3, 128 x 128 tiles, Cs % 64 == 0) and the 2-stage one."""
+    3-stage counted-vmcnt kernel (BIGDL_I8_G3, 128 x 128 tiles, Cs % 64 == 0; 3 = its 256 x 128 tile) and the 2-stage one."""
     from bigdl_amd.ops.conv import _fwd_taps, out_size
 
     C_ = native.get()
