@@ -1695,16 +1695,19 @@ __global__ __launch_bounds__(512, 1) void conv_nt_w8_kernel(ConvArgs a) {
 // FASTK = false (Cs % 32 != 0, e.g. Inception's 48 / 80 / 160-channel inputs, padded to 8): a K-step spans taps, so
 // every lane resolves the tap of its own 8-channel granule (kk = k0 + 8 * gsrc) from the LDS tap table and the K
 // tail past Kdim loads zeros.
-template <int BN, int NS, bool FASTK = true>
-__global__ __launch_bounds__(256, NS == 3 ? 3 : 2) void conv_nt_g4_kernel(ConvArgs a) {
-  constexpr int BM = 128, BKS = 32;
+// BM = 256 (BIGDL_CONV_G4=6/7): 2 x 2 waves of 128 x 64, 32 MFMAs per wave between barriers instead of 16, 24 KB
+// stages, 2 workgroups per CU.
+template <int BN, int NS, bool FASTK = true, int BM = 128>
+__global__ __launch_bounds__(256, (NS == 3 && BM == 128) ? 3 : 2) void conv_nt_g4_kernel(ConvArgs a) {
+  constexpr int BKS = 32;
   constexpr int WGM = 2, WGN = 2;
   constexpr int TM = BM / WGM, TN = BN / WGN;      // 64 x 64 (or 64 x 32) per wave
   constexpr int MI = TM / 16, NI = TN / 16;
   constexpr int STAGE = (BM + BN) * BKS;
   constexpr int AI = BM / 64, BI = BN / 64;        // DMA instructions per thread per stage (4 waves x 16 rows)
   constexpr int L = AI + BI;
-  constexpr int NH = (4 * TM * TN * 4 <= NS * STAGE * 2) ? 1 : 2;   // epilogue row chunks that fit the stages
+  // epilogue row chunks that fit the stages (4 at BM = 256: fewer prefetched epilogue rows in flight, no spills)
+  constexpr int NH = BM == 256 ? 4 : (4 * TM * TN * 4 <= NS * STAGE * 2) ? 1 : 2;
   constexpr int SL = (TM / NH) * TN;
   static_assert(4 * SL * 4 <= NS * STAGE * 2, "epilogue chunk must fit the stages");
   __shared__ __attribute__((aligned(1024))) bf16_t lds[NS * STAGE + 3 * CONV_MAX_TAPS];
@@ -2011,16 +2014,18 @@ static int w8_pick(const ConvArgs* a) {
   return std::max(split, 1);
 }
 
-template <int BN, int NS>
+template <int BN, int NS, int BM = 128>
 void launch_nt_g4(const ConvArgs& a, hipStream_t st) {
-  const int nwg = ((a.M + 127) / 128) * ((a.Ncol + BN - 1) / BN);
-  if (a.Cs % 32 == 0) conv_nt_g4_kernel<BN, NS, true><<<dim3(nwg), dim3(256), 0, st>>>(a);
-  else conv_nt_g4_kernel<BN, NS, false><<<dim3(nwg), dim3(256), 0, st>>>(a);
+  const int nwg = ((a.M + BM - 1) / BM) * ((a.Ncol + BN - 1) / BN);
+  if (a.Cs % 32 == 0) conv_nt_g4_kernel<BN, NS, true, BM><<<dim3(nwg), dim3(256), 0, st>>>(a);
+  else conv_nt_g4_kernel<BN, NS, false, BM><<<dim3(nwg), dim3(256), 0, st>>>(a);
 }
 
 // BIGDL_CONV_G4 (default 3): 0 = off, 4 = 4-stage (2 workgroups per CU), 3 = 3-stage (3 per CU) deep-pipelined 128-row kernel
 // in place of the 2-stage LDS-DMA kernel on fast-K (Cs % 32 == 0), aligned-output layers; 5 = the 3-stage kernel
-// also on the deep-K small-grid layers that otherwise take the 256-row 8-wave kernel
+// also on the deep-K small-grid layers that otherwise take the 256-row 8-wave kernel; 6 = as 3, with the 256 x 128 tile
+// for Ncol > 64 wherever its grid still gives every CU two workgroups; 7 = as 3, with the 256 x 128 tile always
+// for Ncol > 64 (tests)
 int g_conv_g4 = -1;
 static int g4_pick() {
   if (g_conv_g4 < 0) {
@@ -2094,7 +2099,10 @@ int bigdl_conv_nt(const ConvArgs* a, hipStream_t st) {
     conv_nt_w8_kernel<false><<<dim3(nwg), dim3(512), 0, st>>>(*a);
   } else if (impl == 1 && g4_pick() && aligned_out && (a->Cs % 32 == 0 || (g4_slowk() && a->Kdim % 8 == 0)) &&
              (g4_pick() == 5 || !(p3_pick && fastk && p3_tiles >= 256))) {
-    if (g4_pick() != 4) {
+    const long tiles256 = (long)((a->M + 255) / 256) * ((a->Ncol + 127) / 128);
+    if (a->Ncol > 64 && (g4_pick() == 7 || (g4_pick() == 6 && tiles256 >= 512))) {
+      launch_nt_g4<128, 3, 256>(*a, st);
+    } else if (g4_pick() != 4) {
       if (a->Ncol <= 64) launch_nt_g4<64, 3>(*a, st);
       else launch_nt_g4<128, 3>(*a, st);
     } else {

@@ -598,10 +598,11 @@ G4_CASES = [
 ]
 
 
-@pytest.mark.parametrize("stages", [4, 3])
+@pytest.mark.parametrize("stages", [4, 3, 7])
 @pytest.mark.parametrize("case", G4_CASES)
 def test_conv_g4_kernel_fwd_dgrad(case, stages):
-    """128 x BN 4-wave kernel with 3 / 4 counted-vmcnt LDS-DMA stages (BIGDL_CONV_G4) vs fp32 torch: forward with
+    """128 x BN 4-wave kernel with 3 / 4 counted-vmcnt LDS-DMA stages (BIGDL_CONV_G4; 7 = the 256 x 128 tile for
+    Ncol > 64) vs fp32 torch: forward with
     bias + BN statistics, forward + ReLU, data gradient with a residual addend."""
     from bigdl_amd.ops import bn as bnops
     from bigdl_amd.ops import conv as cv
