@@ -58,11 +58,48 @@ class I8Act:
         return y
 
 
+class I8Stem:
+    """The graph input quantized straight into the width im2col of its only consumer, a small-channel stem conv
+    (``quantize_wim2col_f32``): ``data`` int8 [N, H, OW, 32], ``x`` the fp32 input (for a float fallback)."""
+
+    __slots__ = ("data", "x", "scale", "OW")
+
+    def __init__(self, data, x, scale, OW):
+        self.data, self.x, self.scale, self.OW = data, x, scale, OW
+
+    @property
+    def shape(self):
+        return tuple(self.x.shape)
+
+
+def _stem_ok(m):
+    """A stem conv the width-im2col path takes: <= 4 input channels, <= 8 width taps, no width dilation."""
+    import os
+
+    return (os.environ.get("BIGDL_I8_STEM", "1") != "0" and _conv_ok(m) and m.nInputPlane <= 4
+            and m.kernelW <= 8 and m.dilationW == 1 and m.dilationH == 1)
+
+
+def _stem_weight(m):
+    """w'[k][r][e*4 + c] = w[k][r][e][c] (e < S, c < 4), cached on the module (its int8 weight does not change)."""
+    w = m.weight
+    key = (w.data_ptr(), w._version)
+    c = getattr(m, "_i8_stem_w", None)
+    if c is None or c[0] != key:
+        K, R, S, _ = w.shape
+        wp = torch.zeros(K, R, 8, 4, dtype=torch.int8, device=w.device)
+        wp[:, :, :S, :] = w[..., :4]
+        m._i8_stem_w = c = (key, wp.reshape(K, R * 32).contiguous())
+    return c[1]
+
+
 def _as_float(v):
     from ..utils.table import Table
 
     if isinstance(v, I8Act):
         return v.dequantize()
+    if isinstance(v, I8Stem):
+        return v.x
     if isinstance(v, Table):
         t = Table()
         for k, x in v.items():
@@ -307,12 +344,20 @@ class Int8GraphPlan:
 
     def _input_runner(self, n):
         scale = self.scale[n.id]
+        us = self.users.get(n.id, [])
+        stem = us[0].element if len(us) == 1 and us[0].id not in self.res_conv and _stem_ok(us[0].element) else None
 
         def run(x):
             if not (isinstance(x, torch.Tensor) and x.is_cuda and x.dim() == 4 and x.dtype == torch.float32):
                 return x
             x = x.contiguous()
             N, C, H, W = x.shape
+            if stem is not None and C == stem.nInputPlane:
+                ph, pw = stem._pads(H, W)
+                OW = out_size(W, stem.kernelW, stem.strideW, pw, 1)
+                q = torch.empty((N, H, OW, 32), dtype=torch.int8, device=x.device)
+                native.get().quantize_wim2col_f32(x, q, OW, stem.kernelW, stem.strideW, pw, float(scale))
+                return I8Stem(q, x, scale, OW)
             q = _i8_buffer((N, H, W, _ceil16(C)), C, x.device)
             native.get().quantize_nchw_f32(x, q, _ceil16(C), float(scale))
             return I8Act(q, C, scale)
@@ -364,6 +409,8 @@ class Int8GraphPlan:
         res_relu = residual and self.res[self.res_conv[n.id]][2] is not None
 
         def run(x):
+            if isinstance(x, I8Stem):
+                return stem_run(x)
             if not (isinstance(x, I8Act) or (isinstance(x, torch.Tensor) and x.is_cuda and x.dim() == 4)):
                 return m.forward(_as_float(x))
             N, C, H, W = x.shape
@@ -392,6 +439,27 @@ class Int8GraphPlan:
                 return I8Act(dst, K, oscale)
             y = torch.empty((N, K, OH, OW), dtype=BF16, device=q.device, memory_format=CL)
             native.get().conv_i8(q, m.weight, y, m.bias, xs, m.weightScale, geo, taps, relu, xsc, 0.0, ad, asc)
+            return y
+
+        def stem_run(x):
+            # R x 1 convolution over the 32-byte width-im2col rows: height taps only, width stride 1
+            N, C, H, W = x.shape
+            ph, _ = m._pads(H, W)
+            R, K = m.kernelH, m.nOutputPlane
+            OH, OW = out_size(H, R, m.strideH, ph, 1), x.OW
+            taps = _fwd_taps(R, 1, ph, 0, 1, 1)
+            geo = [N, H, OW, 32, OH, OW, m.strideH, 1, R * 32, K, K, OH, OW, 1, 1, 0, 0]
+            relu = m.fuse_relu
+            wp = _stem_weight(m)
+            if out8 and not residual:
+                dst, _ = self._dest(n, N, OH, OW, K, x.data.device)
+                geo[10] = dst.stride(2)
+                native.get().conv_i8(x.data, wp, dst, m.bias, None, m.weightScale, geo, taps, relu, float(x.scale),
+                                     float(oscale), None, 0.0)
+                return I8Act(dst, K, oscale)
+            y = torch.empty((N, K, OH, OW), dtype=BF16, device=x.data.device, memory_format=CL)
+            native.get().conv_i8(x.data, wp, y, m.bias, None, m.weightScale, geo, taps, relu, float(x.scale), 0.0,
+                                 None, 0.0)
             return y
         return run
 

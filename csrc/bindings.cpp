@@ -455,6 +455,19 @@ void pool_i8(const Tensor& x, const Tensor& y, std::vector<int64_t> g, bool avg,
                 g[10], g[11], avg ? 1 : 0, count_pad ? 1 : 0, g[12], stream());
 }
 
+// int8 stem input: fp32 NCHW (C <= 4) -> int8 width im2col [N][H][OW][32] (quant.hip)
+void quantize_wim2col_f32(const Tensor& x, const Tensor& y, int64_t OW, int64_t S, int64_t sw, int64_t pw,
+                          double scale) {
+  TORCH_CHECK(x.dim() == 4 && x.is_contiguous() && x.scalar_type() == at::kFloat && x.is_cuda() && x.size(1) <= 4,
+              "quantize_wim2col_f32: x fp32 contiguous NCHW with <= 4 channels");
+  TORCH_CHECK(S >= 1 && S <= 8 && sw >= 1 && OW >= 1, "quantize_wim2col_f32: 1 <= S <= 8 width taps");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  TORCH_CHECK(y.scalar_type() == at::kChar && y.is_cuda() && y.is_contiguous() && y.numel() >= N * H * OW * 32,
+              "quantize_wim2col_f32: y is int8 [N][H][OW][32]");
+  bigdl_quantize_wim2col_f32(x.data_ptr<float>(), y.data_ptr<int8_t>(), (int)N, (int)C, (int)H, (int)W, (int)OW,
+                             (int)S, (int)sw, (int)pw, (float)(1.0 / scale), stream());
+}
+
 void quantize_nchw_f32(const Tensor& x, const Tensor& q, int64_t Cp, double scale) {
   TORCH_CHECK(x.dim() == 4 && x.is_contiguous() && x.scalar_type() == at::kFloat && x.is_cuda(),
               "quantize_nchw_f32: x fp32 contiguous NCHW");
@@ -1001,6 +1014,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("poolnd_bwd", &poolnd_bwd);
   m.def("upsample_nearest", &upsample_nearest);
   m.def("quantize_nchw_f32", &quantize_nchw_f32);
+  m.def("quantize_wim2col_f32", &quantize_wim2col_f32);
   m.def("quantize_rows_bf16", &quantize_rows_bf16);
   m.def("dequantize_rows", &dequantize_rows);
   m.def("nms", &nms);

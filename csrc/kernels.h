@@ -151,6 +151,8 @@ int bigdl_conv_i8(const ConvArgs* a, const float* xscale, float xs_const, const 
 void bigdl_pool_i8(const int8_t* x, int8_t* y, int N, int H, int W, int Cp, int OH, int OW, int kh, int kw, int sh,
                    int sw, int ph, int pw, int avg, int count_pad, long ldo, hipStream_t st);
 void bigdl_quantize_nchw_f32(const float* x, int8_t* q, int N, int C, int HW, int Cp, float inv, hipStream_t st);
+void bigdl_quantize_wim2col_f32(const float* x, int8_t* y, int N, int C, int H, int W, int OW, int S, int sw, int pw,
+                                float inv, hipStream_t st);
 void bigdl_quantize_rows_bf16(const uint16_t* x, int8_t* q, long P, int C, long ldq, float inv, hipStream_t st);
 void bigdl_dequantize_rows(const int8_t* q, uint16_t* y, long P, int C, long ld, float scale, hipStream_t st);
 

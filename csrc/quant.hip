@@ -693,6 +693,41 @@ __global__ void quantize_nchw_f32_kernel(const float* __restrict__ x, int8_t* __
   }
 }
 
+// int8 stem (C <= 4 channels, width stride sw, S <= 8 width taps): the image is quantized straight into its width
+// im2col, y[n][h][ow][e*4 + c] = q(x[n][c][h][ow*sw + e - pw]) (0 for e >= S, c >= C or outside the image), so one
+// 32-byte row holds every width tap of output column ow and the stem becomes an R x 1 convolution over 32 int8
+// "channels": a reduction of R * 32 instead of R * S * 16 (7x7: 224 vs 784; the bf16 stem's pixel pairs,
+// stem.hip, do the same for 16-bit data).
+__global__ __launch_bounds__(256) void quantize_wim2col_f32_kernel(const float* __restrict__ x, int8_t* __restrict__ y,
+                                                                   int N, int C, int H, int W, int OW, int S, int sw,
+                                                                   int pw, float inv) {
+  const long total = (long)N * H * OW;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int ow = (int)(i % OW);
+    const long t = i / OW;
+    const int h = (int)(t % H);
+    const int n = (int)(t / H);
+    const float* xb = x + ((size_t)n * C * H + h) * W;
+    unsigned u[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      u[e] = 0u;
+      const int w = ow * sw + e - pw;
+      if (e < S && (unsigned)w < (unsigned)W) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          if (c < C) {
+            const int v = max(-127, min(127, __float2int_rn(xb[(size_t)c * H * W + w] * inv)));
+            u[e] |= (unsigned)(v & 0xff) << (8 * c);
+          }
+      }
+    }
+    v4u* o = reinterpret_cast<v4u*>(y + (size_t)i * 32);
+    o[0] = v4u{u[0], u[1], u[2], u[3]};
+    o[1] = v4u{u[4], u[5], u[6], u[7]};
+  }
+}
+
 // bf16 NHWC [P][C] -> int8 [P][ldq] (written at a channel offset of a wider int8 buffer), static scale
 __global__ void quantize_rows_bf16_kernel(const bf16_t* __restrict__ x, int8_t* __restrict__ q, long P, int C,
                                           long ldq, float inv) {
@@ -833,6 +868,14 @@ void bigdl_quantize_nchw_f32(const float* x, int8_t* q, int N, int C, int HW, in
   const long total = (long)N * HW;
   const int blocks = (int)std::min<long>((total + 255) / 256, 16384);
   quantize_nchw_f32_kernel<<<blocks > 0 ? blocks : 1, 256, 0, st>>>(x, q, N, C, HW, Cp, inv);
+  HIP_LAUNCH_CHECK();
+}
+
+void bigdl_quantize_wim2col_f32(const float* x, int8_t* y, int N, int C, int H, int W, int OW, int S, int sw, int pw,
+                                float inv, hipStream_t st) {
+  const long total = (long)N * H * OW;
+  const int blocks = (int)std::min<long>((total + 255) / 256, 16384);
+  quantize_wim2col_f32_kernel<<<blocks > 0 ? blocks : 1, 256, 0, st>>>(x, y, N, C, H, W, OW, S, sw, pw, inv);
   HIP_LAUNCH_CHECK();
 }
 

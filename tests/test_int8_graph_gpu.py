@@ -135,3 +135,49 @@ def test_int8_plan_residual_conv_sum_fused():
     assert _rel(y, ref) < 0.08
     plan = q._int8_plan
     assert plan.res and all(plan.fused.get(a) for a in plan.res), "residual add was not fused into the int8 conv"
+
+
+def test_quantize_wim2col_input():
+    """Width im2col of the int8 stem input: y[n][h][ow][e*4 + c] = q(x[n][c][h][ow*sw + e - pw])."""
+    N, C, H, W, S, sw, pw = 2, 3, 6, 13, 7, 2, 3
+    OW = (W + 2 * pw - S) // sw + 1
+    x = torch.randn(N, C, H, W, device="cuda")
+    s = float(x.abs().max()) / 127
+    y = torch.full((N, H, OW, 32), 99, dtype=torch.int8, device="cuda")
+    native.get().quantize_wim2col_f32(x, y, OW, S, sw, pw, s)
+    q = torch.clamp(torch.round(x.cpu() / s), -127, 127)
+    ref = torch.zeros(N, H, OW, 8, 4)
+    for ow in range(OW):
+        for e in range(S):
+            w = ow * sw + e - pw
+            if 0 <= w < W:
+                ref[:, :, ow, e, :C] = q[:, :, :, w].permute(0, 2, 1)
+    assert (y.cpu().view(N, H, OW, 8, 4).double() - ref.double()).abs().max() <= 1
+
+
+def test_int8_stem_width_im2col_equals_direct(monkeypatch):
+    """7x7 / 2 stem (3 channels, pad 3) on the width-im2col path (R x 1 conv over 32-byte rows, reduction 224)
+    gives exactly the int8 values of the direct 7x7 conv over 16-channel pixels (reduction 784)."""
+    from bigdl_amd.quantized.int8_graph import I8Act, I8Stem
+    from bigdl_amd.quantized.quantizer import quantize
+
+    torch.manual_seed(3)
+    inp = nn.Input()
+    y = nn.ReLU()(nn.SpatialConvolution(3, 64, 7, 7, 2, 2, 3, 3)(inp))
+    y = nn.SpatialMaxPooling(3, 3, 2, 2, 1, 1)(y)
+    y = nn.ReLU()(nn.SpatialConvolution(64, 32, 1, 1)(y))
+    g = nn.Graph([inp], [y])
+    g.evaluate()
+    x = torch.randn(4, 3, 37, 41)
+    ref = g.forward(x).clone()
+    dev = torch.device("cuda:0")
+    outs = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("BIGDL_I8_STEM", mode)
+        q = quantize(g.cloneModule().to(dev), calibration=x.to(dev))
+        outs[mode] = q.forward(x.to(dev)).float().clone()
+        if mode == "1":
+            assert any(isinstance(v, I8Stem) for v in q._outs.values()), "input was not quantized into the im2col"
+            assert any(isinstance(v, I8Act) for v in q._outs.values()), "stem conv did not produce int8"
+    assert torch.equal(outs["1"], outs["0"])
+    assert _rel(outs["1"], ref) < 0.08
