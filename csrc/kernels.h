@@ -175,6 +175,8 @@ void bigdl_set_wgrad_g3(int v);
 int bigdl_get_wgrad_g3();
 void bigdl_set_i8_g3(int v);
 int bigdl_get_i8_g3();
+void bigdl_set_i8_cpl(int v);
+int bigdl_get_i8_cpl();
 
 // Input pipeline: crop + flip + channel reorder + normalise of a uint8 [N, H, W, 3] BGR batch.
 // params: int32 [N][3] = (y0, x0, flip). Output fp32 NCHW [N, 3, OH, OW] or bf16 NHWC [N, OH, OW, 3].

@@ -346,7 +346,7 @@ __global__ __launch_bounds__(256, 2) void conv_i8_glds_kernel(ConvArgs a, I8Epi 
 // waves stacked along M (as conv_i8_glds_kernel).
 // FASTK = false (Cs % 64 != 0: Inception's 48 / 80 / 96 / 160 / ...-channel inputs, padded to 16): every lane resolves
 // the tap of its own 16-channel granule from the LDS tap table; the K tail past Kdim loads zeros.
-template <int BM, int BN, int WGM, int WGN, bool FASTK = true>
+template <int BM, int BN, int WGM, int WGN, bool FASTK = true, int CPL = 8>
 __global__ __launch_bounds__(256, (BM + (BN + 63) / 64 * 64) * 64 * 3 <= 52 * 1024 ? 3 : 2) void conv_i8_g3_kernel(
     ConvArgs a, I8Epi ep) {
   constexpr int BKB = 64, NS = 3;
@@ -477,17 +477,19 @@ __global__ __launch_bounds__(256, (BM + (BN + 63) / 64 * 64) * 64 * 3 <= 52 * 10
     cur = cur == 2 ? 0 : cur + 1;
   }
 
-  // ---- epilogue (conv_i8_glds_kernel's), in NH row halves through a wave-private LDS slice
-  constexpr int GR = TN / 4, LPR = TN / 8, PPI = 64 / LPR, NR = TM / PPI, MIH = MI / NH, NRH = NR / NH;
+  // ---- epilogue (conv_i8_glds_kernel's), in NH row halves through a wave-private LDS slice; each lane finishes CPL
+  // channels of one pixel (CPL = 16: one 16-byte int8 store / addend load per lane instead of two 8-byte ones)
+  constexpr int GR = TN / 4, LPR = TN / CPL, PPI = 64 / LPR, NR = TM / PPI, MIH = MI / NH, NRH = NR / NH;
+  constexpr int GPL = CPL / 4;   // fp32 granules per lane
   float* wl = reinterpret_cast<float*>(lds) + wave * (TM / NH) * TN;
   auto gpos = [](int p, int g) { return (p * GR + (g ^ (p & (GR - 1)))) * 4; };
   const int q = lane % LPR;
-  const int n = n0 + wn * TN + q * 8;
+  const int n = n0 + wn * TN + q * CPL;
   const bool nok = n < a.Ncol;
-  const bool full8 = n + 8 <= a.Ncol;
-  float wsc[8], bs[8];
+  const bool full = n + CPL <= a.Ncol;
+  float wsc[CPL], bs[CPL];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) {
+  for (int e = 0; e < CPL; ++e) {
     const bool ok = n + e < a.Ncol;
     wsc[e] = ok ? ep.wscale[n + e] : 0.f;
     bs[e] = (ok && a.bias) ? a.bias[n + e] : 0.f;
@@ -507,61 +509,80 @@ __global__ __launch_bounds__(256, (BM + (BN + 63) / 64 * 64) * 64 * 3 <= 52 * 10
     for (int r = 0; r < NRH; ++r) {
       const int p = r * PPI + lane / LPR;
       const int m = m0 + wm * TM + h * (TM / NH) + p;
-      const v4f lo = *reinterpret_cast<const v4f*>(wl + gpos(p, 2 * q));
-      const v4f hi = *reinterpret_cast<const v4f*>(wl + gpos(p, 2 * q + 1));
+      float v[CPL];
+#pragma unroll
+      for (int g = 0; g < GPL; ++g) {
+        const v4f t = *reinterpret_cast<const v4f*>(wl + gpos(p, GPL * q + g));
+        v[4 * g] = t[0]; v[4 * g + 1] = t[1]; v[4 * g + 2] = t[2]; v[4 * g + 3] = t[3];
+      }
       if (m >= a.M || !nok) continue;
       const float xs = ep.xscale ? ep.xscale[m / ohw] : ep.xs_const;
-      float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      float ad[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      float ad[CPL];
+#pragma unroll
+      for (int e = 0; e < CPL; ++e) ad[e] = 0.f;
       if (ep.add8) {
         const int8_t* ap = ep.add8 + (size_t)m * ep.add_ld + n;
-        if (full8 && ((reinterpret_cast<uintptr_t>(ap) & 7) == 0)) {
-          const v2u u = *reinterpret_cast<const v2u*>(ap);
+        if (full && ((reinterpret_cast<uintptr_t>(ap) & (CPL - 1)) == 0)) {
+          unsigned u[CPL / 4];
+          if constexpr (CPL == 16) {
+            const v4u w = *reinterpret_cast<const v4u*>(ap);
+            u[0] = w[0]; u[1] = w[1]; u[2] = w[2]; u[3] = w[3];
+          } else {
+            const v2u w = *reinterpret_cast<const v2u*>(ap);
+            u[0] = w[0]; u[1] = w[1];
+          }
 #pragma unroll
-          for (int e = 0; e < 8; ++e) ad[e] = (float)(int8_t)((u[e >> 2] >> (8 * (e & 3))) & 0xff) * ep.add_scale;
+          for (int e = 0; e < CPL; ++e) ad[e] = (float)(int8_t)((u[e >> 2] >> (8 * (e & 3))) & 0xff) * ep.add_scale;
         } else {
 #pragma unroll
-          for (int e = 0; e < 8; ++e) ad[e] = n + e < a.Ncol ? (float)ap[e] * ep.add_scale : 0.f;
+          for (int e = 0; e < CPL; ++e) ad[e] = n + e < a.Ncol ? (float)ap[e] * ep.add_scale : 0.f;
         }
       }
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
+      for (int e = 0; e < CPL; ++e) {
         v[e] = v[e] * xs * wsc[e] + bs[e] + ad[e];
         if (a.relu) v[e] = fmaxf(v[e], 0.f);
       }
       const size_t off = (size_t)m * a.ldo + n;
       if (ep.out_mode == 2) {
         int8_t* o = reinterpret_cast<int8_t*>(a.out) + off;
-        unsigned pk[2] = {0u, 0u};
+        unsigned pk[CPL / 4];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
+        for (int g = 0; g < CPL / 4; ++g) pk[g] = 0u;
+#pragma unroll
+        for (int e = 0; e < CPL; ++e) {
           const int qv = max(-127, min(127, __float2int_rn(v[e] * ep.out_inv)));
           pk[e >> 2] |= (unsigned)(qv & 0xff) << (8 * (e & 3));
         }
-        if (full8 && (off & 7) == 0) {
-          *reinterpret_cast<v2u*>(o) = v2u{pk[0], pk[1]};
+        if (full && (reinterpret_cast<uintptr_t>(o) & (CPL - 1)) == 0) {
+          if constexpr (CPL == 16) *reinterpret_cast<v4u*>(o) = v4u{pk[0], pk[1], pk[2], pk[3]};
+          else *reinterpret_cast<v2u*>(o) = v2u{pk[0], pk[1]};
         } else {
 #pragma unroll
-          for (int e = 0; e < 8; ++e)
+          for (int e = 0; e < CPL; ++e)
             if (n + e < a.Ncol) o[e] = (int8_t)((pk[e >> 2] >> (8 * (e & 3))) & 0xff);
         }
       } else if (ep.out_mode == 1) {
         float* o = reinterpret_cast<float*>(a.out) + off;
-        if (full8 && (off & 3) == 0) {
-          *reinterpret_cast<v4f*>(o) = v4f{v[0], v[1], v[2], v[3]};
-          *reinterpret_cast<v4f*>(o + 4) = v4f{v[4], v[5], v[6], v[7]};
+        if (full && (reinterpret_cast<uintptr_t>(o) & 15) == 0) {
+#pragma unroll
+          for (int g = 0; g < CPL / 4; ++g)
+            *reinterpret_cast<v4f*>(o + 4 * g) = v4f{v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]};
         } else {
 #pragma unroll
-          for (int e = 0; e < 8; ++e)
+          for (int e = 0; e < CPL; ++e)
             if (n + e < a.Ncol) o[e] = v[e];
         }
       } else {
         bf16_t* o = a.out + off;
-        if (full8 && (off & 7) == 0) {
-          *reinterpret_cast<v4u*>(o) = v4u{pack2bf(v[0], v[1]), pack2bf(v[2], v[3]), pack2bf(v[4], v[5]), pack2bf(v[6], v[7])};
+        if (full && (reinterpret_cast<uintptr_t>(o) & 15) == 0) {
+#pragma unroll
+          for (int g = 0; g < CPL / 8; ++g)
+            *reinterpret_cast<v4u*>(o + 8 * g) = v4u{pack2bf(v[8 * g], v[8 * g + 1]), pack2bf(v[8 * g + 2], v[8 * g + 3]),
+                                                     pack2bf(v[8 * g + 4], v[8 * g + 5]), pack2bf(v[8 * g + 6], v[8 * g + 7])};
         } else {
 #pragma unroll
-          for (int e = 0; e < 8; ++e)
+          for (int e = 0; e < CPL; ++e)
             if (n + e < a.Ncol) o[e] = f2bf(v[e]);
         }
       }
@@ -761,6 +782,30 @@ __global__ void dequantize_rows_kernel(const int8_t* __restrict__ q, bf16_t* __r
 
 }  // namespace
 
+namespace {
+// BIGDL_I8_CPL (default 8): channels per lane in the int8 3-stage kernel's epilogue (16 = 16-byte int8 stores)
+int g_i8_cpl = -1;
+int i8_cpl() {
+  if (g_i8_cpl < 0) {
+    const char* e = getenv("BIGDL_I8_CPL");
+    g_i8_cpl = e ? atoi(e) : 8;
+  }
+  return g_i8_cpl;
+}
+
+template <int BM, int BN, int WGM, int WGN>
+void launch_i8_g3(int g, bool fk, const ConvArgs& a, const I8Epi& ep, hipStream_t st) {
+  if (i8_cpl() == 16 && BN / WGN >= 16) {
+    if (fk) conv_i8_g3_kernel<BM, BN, WGM, WGN, true, 16><<<g, 256, 0, st>>>(a, ep);
+    else conv_i8_g3_kernel<BM, BN, WGM, WGN, false, 16><<<g, 256, 0, st>>>(a, ep);
+  } else {
+    if (fk) conv_i8_g3_kernel<BM, BN, WGM, WGN, true, 8><<<g, 256, 0, st>>>(a, ep);
+    else conv_i8_g3_kernel<BM, BN, WGM, WGN, false, 8><<<g, 256, 0, st>>>(a, ep);
+  }
+}
+
+}  // namespace
+
 extern "C" {
 
 int bigdl_quantize_act(const void* x, int is_bf16, int8_t* q, float* amax, float* scale, int N, long P, int C,
@@ -800,6 +845,8 @@ static bool i8_g3() {
   return g_i8_g3 != 0;
 }
 void bigdl_set_i8_g3(int v) { g_i8_g3 = v; }
+void bigdl_set_i8_cpl(int v) { g_i8_cpl = v; }
+int bigdl_get_i8_cpl() { return i8_cpl(); }
 int bigdl_get_i8_g3() { return i8_g3() ? g_i8_g3 : 0; }
 
 int bigdl_conv_i8(const ConvArgs* a, const float* xscale, float xs_const, const float* wscale, int out_mode,
@@ -813,13 +860,8 @@ int bigdl_conv_i8(const ConvArgs* a, const float* xscale, float xs_const, const 
   if (a->Ncol <= 64 && i8_g3()) {
     const int bn = a->Ncol <= 32 ? 32 : 64;
     const int g = ((a->M + 255) / 256) * ((a->Ncol + bn - 1) / bn);
-    if (bn == 32) {
-      if (g3fk) conv_i8_g3_kernel<256, 32, 4, 1, true><<<g, 256, 0, st>>>(*a, ep);
-      else conv_i8_g3_kernel<256, 32, 4, 1, false><<<g, 256, 0, st>>>(*a, ep);
-    } else {
-      if (g3fk) conv_i8_g3_kernel<256, 64, 4, 1, true><<<g, 256, 0, st>>>(*a, ep);
-      else conv_i8_g3_kernel<256, 64, 4, 1, false><<<g, 256, 0, st>>>(*a, ep);
-    }
+    if (bn == 32) launch_i8_g3<256, 32, 4, 1>(g, g3fk, *a, ep, st);
+    else launch_i8_g3<256, 64, 4, 1>(g, g3fk, *a, ep, st);
   } else if (a->Ncol <= 32) {
     const int g = ((a->M + 255) / 256) * ((a->Ncol + 31) / 32);
     if (fk) conv_i8_glds_kernel<256, 32, 4, true><<<g, 256, 0, st>>>(*a, ep);
@@ -830,11 +872,9 @@ int bigdl_conv_i8(const ConvArgs* a, const float* xscale, float xs_const, const 
     else conv_i8_glds_kernel<256, 64, 4, false><<<g, 256, 0, st>>>(*a, ep);
   } else if (i8_g3() && (g_i8_g3 == 3 || (g_i8_g3 == 2 && ((a->M + 255) / 256) * ((a->Ncol + 127) / 128) >= 512))) {
     const int g = ((a->M + 255) / 256) * ((a->Ncol + 127) / 128);
-    if (g3fk) conv_i8_g3_kernel<256, 128, 2, 2, true><<<g, 256, 0, st>>>(*a, ep);
-    else conv_i8_g3_kernel<256, 128, 2, 2, false><<<g, 256, 0, st>>>(*a, ep);
+    launch_i8_g3<256, 128, 2, 2>(g, g3fk, *a, ep, st);
   } else if (i8_g3()) {
-    if (g3fk) conv_i8_g3_kernel<128, 128, 2, 2, true><<<nwg, 256, 0, st>>>(*a, ep);
-    else conv_i8_g3_kernel<128, 128, 2, 2, false><<<nwg, 256, 0, st>>>(*a, ep);
+    launch_i8_g3<128, 128, 2, 2>(nwg, g3fk, *a, ep, st);
   } else if (fk) {
     conv_i8_glds_kernel<128, 128, 2, true><<<nwg, 256, 0, st>>>(*a, ep);
   } else {

@@ -44,20 +44,23 @@ I8_CASES = [
 ]
 
 
+@pytest.mark.parametrize("cpl", [8, 16])
 @pytest.mark.parametrize("g3", [1, 0, 3])
 @pytest.mark.parametrize("case", I8_CASES)
-def test_conv_i8_exact_integer(case, g3):
+def test_conv_i8_exact_integer(case, g3, cpl):
     """Scales are forced to exactly 1 (row maxima 127), so the fp32 output must equal the integer conv — for the
     3-stage counted-vmcnt kernel (BIGDL_I8_G3, 128 x 128 tiles, Cs % 64 == 0; 3 = its 256 x 128 tile) and the 2-stage one."""
     from bigdl_amd.ops.conv import _fwd_taps, out_size
 
     C_ = native.get()
-    old = C_.get_i8_g3()
+    old, old_cpl = C_.get_i8_g3(), C_.get_i8_cpl()
     C_.set_i8_g3(g3)
+    C_.set_i8_cpl(cpl)     # channels per lane in the 3-stage kernel's epilogue (16: 16-byte stores)
     try:
         _conv_i8_exact(case)
     finally:
         C_.set_i8_g3(old)
+        C_.set_i8_cpl(old_cpl)
 
 
 def _conv_i8_exact(case):
