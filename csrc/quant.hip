@@ -783,12 +783,12 @@ __global__ void dequantize_rows_kernel(const int8_t* __restrict__ q, bf16_t* __r
 }  // namespace
 
 namespace {
-// BIGDL_I8_CPL (default 8): channels per lane in the int8 3-stage kernel's epilogue (16 = 16-byte int8 stores)
+// BIGDL_I8_CPL (default 16): channels per lane in the int8 3-stage kernel's epilogue (16 = 16-byte int8 stores)
 int g_i8_cpl = -1;
 int i8_cpl() {
   if (g_i8_cpl < 0) {
     const char* e = getenv("BIGDL_I8_CPL");
-    g_i8_cpl = e ? atoi(e) : 8;
+    g_i8_cpl = e ? atoi(e) : 16;   // 16: ResNet-50 int8 4.19 -> 3.90 ms (profiles/r3_int8_epilogue_ab.txt)
   }
   return g_i8_cpl;
 }
