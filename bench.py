@@ -19,8 +19,19 @@ import time
 
 import torch
 
+import bigdl_amd  # noqa: F401,E402  (HIP runtime graph settings must precede the first GPU call)
+
 METRIC = "images/sec (whole node) ResNet-50 224x224 bf16 at 1/2/4/8 MI355X"
 BASELINE = None  # BASELINE.json "published" is empty: no reference number on this metric
+
+
+def dist_backend():
+    import torch.distributed as dist
+
+    if not dist.is_initialized():
+        return "none"
+    b = dist.get_backend()
+    return "RCCL" if b == "nccl" else b
 
 
 def parse():
@@ -31,7 +42,9 @@ def parse():
     ap.add_argument("--batch", type=int, default=256, help="per-GPU batch")
     ap.add_argument("--image", type=int, default=224)
     ap.add_argument("--depth", type=int, default=50)
-    ap.add_argument("--compress", default=None, choices=[None, "bf16"])
+    ap.add_argument("--compress", default="auto", choices=["auto", "bf16", "fp16", "fp32"],
+                    help="gradient / weight wire format: auto (default) = bf16 whenever N > 1, the reference's 16-bit "
+                         "exchange; fp16 = the reference's truncating FP16CompressedTensor; fp32 = uncompressed")
     ap.add_argument("--graph", type=int, default=-1,
                     help="1: capture the training step in HIP graphs, 0: eager launches, -1 (default): time both "
                          "during warm-up and keep the faster")
@@ -295,10 +308,12 @@ def main():
             "data": "synthetic (random 3x224x224 images, random labels; random-init weights)",
             "config": {"model": f"ResNet-{args.depth} v1.5 (BigDL ImageNet builder{', Graph form' if args.graph_model else ''})", "global_batch": B * world,
                        "per_gpu_batch": B, "seq_len": None, "image": args.image, "parallelism": f"dp{world}",
-                       "optimizer": "SGD momentum 0.9 + L2 1e-4 (ZeRO-1 sharded over RCCL)",
+                       "optimizer": "SGD momentum 0.9 + L2 1e-4" + (
+                           f" (ZeRO-1: {dist_backend()} reduce-scatter / all-gather, optimizer state sharded)"
+                           if step.comm.active else " (one rank: no gradient exchange)"),
                        "hip_graph": graph is not None, "graph_vs_eager": decision,
                        "wgrad_side_stream": side_stream.enabled(), "bucketed_overlap": step.bucketed is not None,
-                       "grad_compress": args.compress, "final_loss": round(loss, 4)},
+                       "grad_compress": step.comm.wire_format, "final_loss": round(loss, 4)},
         }), flush=True)
     Engine.shutdown()
 

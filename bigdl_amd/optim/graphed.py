@@ -20,6 +20,7 @@ import warnings
 
 import torch
 
+from ..ops import side_stream as _side
 from ..parallel.graph_segments import SegmentedGraph
 from .sgd import SGD
 
@@ -52,25 +53,50 @@ class GraphedTrainStep:
             for _ in range(max(warmup, 1)):
                 step.step(self.x, self.y)
         torch.cuda.synchronize()
-        methods = []
+        methods, seen = [], set()
         for p in step.plan:
-            if getattr(p.method, "_lr_dev", None) is None:
-                p.method._lr_dev = torch.zeros(1, device=step.device)
-            methods.append(p.method)
+            if id(p.method) not in seen:
+                seen.add(id(p.method))
+                methods.append(p.method)
         self.methods = methods
-        self._prologue()
-        if not prewarmed:
-            s = torch.cuda.Stream()
-            s.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(s):          # one more eager step on the capture stream (allocator warm-up)
-                step.step(self.x, self.y)
-            torch.cuda.current_stream().wait_stream(s)
-            torch.cuda.synchronize()
+        # what a failed capture must undo: the schedule position the prologue advanced, and the device rate scalar
+        # (an SGD holding ``_lr_dev`` skips its own schedule update, so a stale one would freeze the rate)
+        snap = [(m, {k: v for k, v in m.state.items() if not torch.is_tensor(v)},
+                 dict(vars(m.learningRateSchedule)) if hasattr(m, "learningRateSchedule") else None,
+                 getattr(m, "_lr_dev", None)) for m in methods]
+        try:
+            for m in methods:
+                if getattr(m, "_lr_dev", None) is None:
+                    m._lr_dev = torch.zeros(1, device=step.device)
             self._prologue()
-        self.graph = SegmentedGraph()
-        with warnings.catch_warnings():
-            warnings.filterwarnings("ignore", message=".*CUDA Graph is empty.*")
-            self.loss = self.graph.record(lambda: step.step(self.x, self.y))
+            if not prewarmed:
+                s = torch.cuda.Stream()
+                s.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(s):          # one more eager step on the capture stream (allocator warm-up)
+                    step.step(self.x, self.y)
+                torch.cuda.current_stream().wait_stream(s)
+                torch.cuda.synchronize()
+                self._prologue()
+            self.graph = SegmentedGraph()
+            # single-stream capture: the weight-gradient side stream (ops/side_stream.py) is off while recording, so
+            # no captured graph has parallel branches. HIP's multi-queue graph executor was measured to break the
+            # captured edges of such graphs (module docstring of parallel/graph_segments.py).
+            was = _side.enabled()
+            _side.set_enabled(False)
+            try:
+                with warnings.catch_warnings():
+                    warnings.filterwarnings("ignore", message=".*CUDA Graph is empty.*")
+                    self.loss = self.graph.record(lambda: step.step(self.x, self.y))
+            finally:
+                _side.set_enabled(was)
+        except BaseException:
+            for m, st, sched, lr in snap:
+                m.state.update(st)
+                if sched is not None:
+                    vars(m.learningRateSchedule).update(sched)
+                m._lr_dev = lr
+            _side.reset()
+            raise
         self._fresh = True                  # capture did not execute: the first replay uses this prologue
 
     def _prologue(self):

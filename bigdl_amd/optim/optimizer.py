@@ -73,7 +73,7 @@ class Optimizer:
         self.l2NormClip = None
         self.logInterval = int(os.environ.get("BIGDL_LOG_INTERVAL", "10"))
         self.retryTimes = int(Engine.getProperty("bigdl.failure.retryTimes", 5))
-        self.compress = Engine.getProperty("bigdl.compress", None)
+        self.compress = Engine.getProperty("bigdl.compress", "auto")
         self.metrics = Metrics()
         self._step = None
         self.device = Engine.device()

@@ -223,7 +223,7 @@ def wait_event(ev, poll_s=100e-6):
 
 
 class TrainStep:
-    def __init__(self, model, criterion, optim_method, device=None, comm=None, compress=None, fuse=True,
+    def __init__(self, model, criterion, optim_method, device=None, comm=None, compress="auto", fuse=True,
                  overlap=None, bucket_elems=8 << 20, processors=None, expand_methods=False, priorities=None):
         from ..utils.engine import Engine
 

@@ -39,7 +39,7 @@ def _native():
 
 
 class AllReduceParameter:
-    def __init__(self, total, world_size=None, rank=None, compress=None, group=None, align=64):
+    def __init__(self, total, world_size=None, rank=None, compress="auto", group=None, align=64):
         self.world = world_size if world_size is not None else (dist.get_world_size(group) if dist_ready() else 1)
         self.rank = rank if rank is not None else (dist.get_rank(group) if dist_ready() else 0)
         self.group = group
@@ -49,6 +49,10 @@ class AllReduceParameter:
         self.shard = self.padded // self.world
         self.start = self.rank * self.shard
         self.end = self.start + self.shard
+        if compress == "auto":
+            # the reference's wire format: 16-bit gradients and weights whenever anything goes over the wire
+            # (S/parameters/AllReduceParameter.scala:171-172,297-302,321); fp32 is the opt-in ("none" / "fp32")
+            compress = "bf16" if self.world > 1 else None
         if compress in ("none", "fp32"):
             compress = None
         if compress not in (None, "bf16", "fp16", "fp16-truncate", "bf16-rtz"):
@@ -66,6 +70,15 @@ class AllReduceParameter:
         self.active = self.world > 1 or os.environ.get("BIGDL_FORCE_COLLECTIVES", "0") == "1" and dist_ready()
         # RCCL collectives exchange tensors in place; gloo wants distinct buffers
         self._inplace = dist_ready() and dist.get_backend(group) == "nccl"
+
+    @property
+    def wire_format(self):
+        """What the gradient / weight exchange puts on the wire (for logs and the bench JSON)."""
+        if not self.active:
+            return "none (no exchange)"
+        if self.compress is None:
+            return "fp32"
+        return "bf16-rtz (reference FP16CompressedTensor)" if self.rtz else "bf16"
 
     @property
     def localPartitionRange(self):

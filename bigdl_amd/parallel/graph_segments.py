@@ -1,27 +1,15 @@
 """Segmented HIP-graph capture: a training step recorded as a chain of single-stream HIP graphs cut at every
 collective launch / wait, with the RCCL calls themselves re-issued eagerly between the graph launches.
 
-Why not one graph with the collectives inside: a capture that forks onto RCCL's stream (async reduce-scatter in
-flight while the next layers' backward kernels are captured on the compute stream) replays with wrong results on
-this ROCm 7.0 / PyTorch 2.10 stack. Localised by ``tools/diag_fork_graph.py`` (1 rank, the training step as ONE
-graph, the reduce-scatter replaced by a side-stream branch; weights after 3 replays vs 6 eager steps):
-  * pure PyTorch chains with a forked branch, joined at the end or in the middle of the chain: exact;
-  * the training step with a branch that launches NO kernel (fork + join only): exact (fp32-atomic noise, 7e-9);
-  * the same branch forked only after the last backward kernel (no backward kernel beside it): exact;
-  * a branch with ANY kernel (even ``mul_`` on a tensor the step never touches) beside the backward kernels:
-    max |dw| 1.5e-3 on 99.9 % of the weights, the same value on every run (deterministic, not a timing race);
-    the same with every memset node replaced by a kernel, and with record_stream on the branch's tensors;
-  * eager execution with the same overlapping side-stream kernel: exact (tools/diag_overlap.py eager_ov_fake).
-So the fault needs a graph with parallel branches whose kernel nodes are this step's kernels (large-kernarg
-implicit-GEMM / BN kernels from our code object) — it is not a data race in those kernels (eager overlap is
-exact) nor allocator reuse (the branch touches a pre-capture tensor); we could not reduce it to pure PyTorch.
-Round 3 (profiles/r3_fork_graph_diag.txt): with the weight gradients on their own side stream (ops/side_stream.py,
-the default) every variant above is exact in ONE graph (tests/test_distributed_gpu.py::
-test_one_graph_step_with_forked_branches_matches_eager); with BIGDL_WGRAD_STREAM=0 it still diverges, and the
-divergence changes from run to run (1.5e-3, nan), so it is a race rather than a deterministic miscompute. A self-join
-of the compute stream just before the fork, forking through a kernel-less hop stream, or the weight-gradient kernel
-without its split-K workspace do not remove it. The segmented form stays the multi-rank capture path (it needs no
-assumption about which configuration is safe).
+Why not one graph with the collectives inside: RCCL's stream would become a parallel branch of the captured graph,
+and graphs with parallel branches replay wrong on this ROCm 7 stack when HIP spreads them over several hardware
+queues. Localised in round 4 (profiles/r4_graph_queue_probe.txt, tests/graph_fork_cases.py): the training step as
+ONE graph with a side-stream branch that runs any kernel beside the backward kernels diverges (1.5e-3 at the default
+queue count, 5.2 with 4 queues, NaN with 2) although the captured topology is right — the hipGraphDebugDotPrint dump
+orders every update kernel after the last backward kernel and marks every cross-queue source as signalling — and is
+exact with DEBUG_HIP_FORCE_GRAPH_QUEUES=1 or serialised kernels. Hence (a) bigdl_amd sets that variable before the
+HIP runtime starts (bigdl_amd/__init__.py), and (b) captures are single-stream: GraphedTrainStep records with the
+weight-gradient side stream off, and collectives cut the graph here.
 Cutting the step at the collectives keeps every captured graph a single stream; overlap still happens because a
 collective issued between two graph launches runs on RCCL's stream while the next graph runs on the compute
 stream.
@@ -37,6 +25,7 @@ import torch
 from ..ops import side_stream as _side
 
 _ACTIVE = None
+_DOT_DIR = __import__("os").environ.get("BIGDL_GRAPH_DOT", "")
 
 
 def active():
@@ -99,12 +88,19 @@ class SegmentedGraph:
     # ------------------------------------------------------------------ recording
     def _begin(self):
         self._g = torch.cuda.CUDAGraph()
+        if _DOT_DIR:
+            self._g.enable_debug_mode()
         self._g.capture_begin(pool=self.pool)
 
     def _end(self):
         g = self._g
         self._g = None
         g.capture_end()
+        if _DOT_DIR:       # BIGDL_GRAPH_DOT=dir: the captured topology (hipGraphDebugDotPrint), one file per segment
+            import os
+
+            os.makedirs(_DOT_DIR, exist_ok=True)
+            g.debug_dump(os.path.join(_DOT_DIR, f"segment_{id(self) & 0xffff:04x}_{self.n_graphs}.dot"))
         self.items.append(("g", g))
         self.n_graphs += 1
 

@@ -7,6 +7,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
+import bigdl_amd  # noqa: E402,F401  (sets the HIP runtime's graph settings before any test touches the GPU)
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP) device and the native extension")

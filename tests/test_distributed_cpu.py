@@ -110,7 +110,7 @@ def _weighted(rank, world):
     from bigdl_amd.optim.train_step import TrainStep
 
     model = _model()
-    step = TrainStep(model, nn.MSECriterion(), O.SGD(0.05), device="cpu", overlap=False)
+    step = TrainStep(model, nn.MSECriterion(), O.SGD(0.05), device="cpu", overlap=False, compress="fp32")
     X, Y = _data()
     xs, ys = X[rank * 8:(rank + 1) * 8], Y[rank * 8:(rank + 1) * 8]
     step.zero_grad()
@@ -273,6 +273,44 @@ def test_bf16_compression_rank_identical_at_n_ranks(world):
     assert ((res[0] - one).norm() / one.norm()) < 1e-2
 
 
+def _default_wire(rank, world):
+    """TrainStep and Optimizer with no compression setting: what goes over the wire, and the trained weights."""
+    from bigdl_amd import nn
+    from bigdl_amd import optim as O
+    from bigdl_amd.dataset.core import DataSet, Sample
+    from bigdl_amd.optim.train_step import TrainStep
+
+    step = TrainStep(_model(), nn.MSECriterion(), O.SGD(0.05, momentum=0.9, dampening=0.0), device="cpu")
+    X, Y = _data()
+    n = X.shape[0] // world
+    for _ in range(3):
+        step.step(X[rank * n:(rank + 1) * n], Y[rank * n:(rank + 1) * n])
+    step.gather_model()
+    X64, Y64 = _data(64)
+    ds = DataSet.rdd([Sample(X64[i], Y64[i]) for i in range(64)], shuffle=False)
+    opt = O.Optimizer(_model(), ds, nn.MSECriterion(), batchSize=16, optimMethod=O.SGD(0.05),
+                      endTrigger=O.Trigger.maxIteration(2))
+    opt.optimize()
+    return step.comm.compress, step.comm.rtz, step.comm.wire_format, opt._step.comm.compress, \
+        step.w[:step.total].clone()
+
+
+@pytest.mark.parametrize("world", [4, 8])
+def test_default_exchange_is_16_bit_at_n_ranks(world):
+    """The reference always puts 16-bit gradients and weights on the wire (S/parameters/AllReduceParameter.scala:
+    171-172,297-302,321): with no ``compress`` / ``bigdl.compress`` setting a multi-rank TrainStep and Optimizer exchange
+    bf16 (round-to-nearest), every rank ends on the same fp32 master, close to one rank at world x batch; one rank
+    exchanges nothing."""
+    res = run_distributed(_default_wire, world, timeout=600)
+    one = run_distributed(_train, 1, ("sgd", False, None, None, 3, False))[0][0]
+    for comp, rtz, wire, opt_comp, w in res:
+        assert (comp, rtz, wire, opt_comp) == ("bf16", False, "bf16", "bf16")
+        assert torch.equal(w, res[0][4])
+    assert ((res[0][4] - one).norm() / one.norm()) < 1e-2
+    solo = run_distributed(_default_wire, 1)[0]
+    assert solo[0] is None and solo[2] == "none (no exchange)"
+
+
 def _graph_model():
     from bigdl_amd import nn
     from bigdl_amd.utils.random_generator import RNG
@@ -296,7 +334,7 @@ def _graph_overlap(rank, world, iters):
 
     model = _graph_model()
     step = TrainStep(model, nn.MSECriterion(), O.SGD(0.05, momentum=0.9, dampening=0.0), device="cpu",
-                     overlap=None, bucket_elems=512)
+                     overlap=None, bucket_elems=512, compress="fp32")
     bk = step.bucketed
     events = []
     if bk is not None:

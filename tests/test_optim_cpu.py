@@ -168,7 +168,9 @@ def _distri_job(rank, world, data, seed, iters):
     from bigdl_amd import nn as _nn
     from bigdl_amd import optim as _O
     from bigdl_amd.dataset.core import DataSet as _DS
+    from bigdl_amd.utils.engine import Engine
 
+    Engine.setProperty("bigdl.compress", "fp32")     # exact equivalence needs the uncompressed exchange
     model = _mlp(seed)
     opt = _O.Optimizer(model, _DS.rdd(data, shuffle=False), _nn.MSECriterion(), batchSize=16,
                        optimMethod=_O.SGD(0.05, momentum=0.9, dampening=0.0),

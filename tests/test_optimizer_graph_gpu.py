@@ -47,5 +47,23 @@ def test_graphed_optimizer_matches_eager():
     noise = ((w_e2 - w_e).norm() / w_e.norm()).item()             # run-to-run (fp32 atomics in BN statistics)
     rel = ((w_g - w_e).norm() / w_e.norm()).item()
     print("graph vs eager", rel, "eager vs eager", noise)
-    assert rel < max(3 * noise, 1e-4), (rel, noise)
+    assert rel < 1e-5, (rel, noise)
     assert abs(l_g - l_e) < 2e-2 * max(1.0, abs(l_e))
+
+
+def test_failed_capture_rolls_back_schedule(monkeypatch):
+    """A capture that raises leaves the Optimizer on eager iterations with the schedule exactly where an eager run
+    has it: GraphedTrainStep undoes its prologue's schedule step and drops the device rate scalar (an SGD holding one
+    skips its own schedule update)."""
+    from bigdl_amd.parallel import graph_segments
+
+    def boom(self, fn):
+        raise RuntimeError("injected capture failure")
+
+    w_e, _, _, s_e = _run(False)
+    monkeypatch.setattr(graph_segments.SegmentedGraph, "record", boom)
+    w_f, g_f, _, s_f = _run(True)
+    assert not any(g_f)
+    assert s_f == s_e, (s_f, s_e)
+    rel = ((w_f - w_e).norm() / w_e.norm()).item()
+    assert rel < 1e-5, rel

@@ -52,7 +52,7 @@ def test_sync_bn_matches_global_batch():
 def _arp_job(rank, world):
     from bigdl_amd.parallel.allreduce_parameter import AllReduceParameter
 
-    arp = AllReduceParameter(1000)
+    arp = AllReduceParameter(1000, compress="fp32")
     w = torch.full((arp.padded,), float(rank))
     arp.init(w)
     g = torch.arange(arp.padded, dtype=torch.float32) * (rank + 1)
