@@ -104,7 +104,56 @@ class StragglerTimeout(RuntimeError):
 # [deadline in time.perf_counter() seconds, 0 = none]: checked by every module forward / backward (one float
 # compare), set by the Optimizer loop while a straggler threshold is active
 STRAGGLER_DEADLINE = [0.0]
+# the DevicePacer of the current iteration on a GPU rank (None: the deadline is checked against the host clock only)
+STRAGGLER_PACER = [None]
 _BWD_DEPTH = [0]
+
+
+class DevicePacer:
+    """Device-time straggler detection (reference: the replica's measured compute time, S/optim/DistriOptimizer.scala:
+    241-278). Kernel launches are asynchronous, so on a GPU the host clock at a module boundary says nothing about
+    how far the device got. The pacer records an event at every module boundary and keeps the host at most ``lag``
+    boundaries ahead of the device: while it waits for the device it checks the deadline, so a rank whose GPU is
+    slow raises ``StragglerTimeout`` within one boundary's worth of device work of the deadline, with at most
+    ``lag`` boundaries of kernels still queued behind it. ``drain`` waits for everything enqueued (end of backward)
+    under the same deadline."""
+
+    def __init__(self, lag=8, poll_s=50e-6):
+        import collections
+
+        self.lag, self.poll_s = lag, poll_s
+        self.q = collections.deque()
+
+    def _wait(self, ev, deadline, where):
+        while not ev.query():
+            if time.perf_counter() > deadline:
+                raise StragglerTimeout(where)
+            time.sleep(self.poll_s)
+
+    def boundary(self, deadline, where):
+        ev = torch.cuda.Event()
+        ev.record()
+        self.q.append(ev)
+        while len(self.q) > self.lag:
+            self._wait(self.q[0], deadline, where)
+            self.q.popleft()
+        if time.perf_counter() > deadline:
+            raise StragglerTimeout(where)
+
+    def drain(self, deadline, where="end of backward"):
+        ev = torch.cuda.Event()
+        ev.record()
+        self._wait(ev, deadline, where)
+        self.q.clear()
+
+
+def _deadline_check(m):
+    dl = STRAGGLER_DEADLINE[0]
+    p = STRAGGLER_PACER[0]
+    if p is not None:
+        p.boundary(dl, m.getPrintName())
+    elif time.perf_counter() > dl:
+        raise StragglerTimeout(m.getPrintName())
 
 
 def _sync_wrap(kind, f):
@@ -119,9 +168,8 @@ def _sync_wrap(kind, f):
 
     if kind == "forward":
         def wrapped(self, *args, **kw):
-            dl = STRAGGLER_DEADLINE[0]
-            if dl and time.perf_counter() > dl:
-                raise StragglerTimeout(self.getPrintName())
+            if STRAGGLER_DEADLINE[0]:
+                _deadline_check(self)
             s = self.__dict__.get("_sync")
             if s is None:
                 return f(self, *args, **kw)
@@ -135,9 +183,8 @@ def _sync_wrap(kind, f):
                 self.__dict__[key] = d
     else:
         def wrapped(self, *args, **kw):
-            dl = STRAGGLER_DEADLINE[0]
-            if dl and time.perf_counter() > dl:
-                raise StragglerTimeout(self.getPrintName())
+            if STRAGGLER_DEADLINE[0]:
+                _deadline_check(self)
             _BWD_DEPTH[0] += 1
             try:
                 s = self.__dict__.get("_sync")

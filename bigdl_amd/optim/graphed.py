@@ -61,7 +61,7 @@ class GraphedTrainStep:
         self.methods = methods
         # what a failed capture must undo: the schedule position the prologue advanced, and the device rate scalar
         # (an SGD holding ``_lr_dev`` skips its own schedule update, so a stale one would freeze the rate)
-        snap = [(m, {k: v for k, v in m.state.items() if not torch.is_tensor(v)},
+        snap = [(m, {k: v for k, v in list(m.state.items()) if not torch.is_tensor(v)},
                  dict(vars(m.learningRateSchedule)) if hasattr(m, "learningRateSchedule") else None,
                  getattr(m, "_lr_dev", None)) for m in methods]
         try:
@@ -91,7 +91,10 @@ class GraphedTrainStep:
                 _side.set_enabled(was)
         except BaseException:
             for m, st, sched, lr in snap:
-                m.state.update(st)
+                for k in [k for k, v in list(m.state.items()) if k not in st and not torch.is_tensor(v)]:
+                    del m.state[k]             # counters the prologue created
+                for k, v in st.items():
+                    m.state[k] = v
                 if sched is not None:
                     vars(m.learningRateSchedule).update(sched)
                 m._lr_dev = lr

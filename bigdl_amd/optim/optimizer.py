@@ -307,6 +307,9 @@ class Optimizer:
         step = self._step
         world = step.comm.world
         drop = _StragglerDrop(self, world) if self.dropPercentage > 0 else None
+        self._drop = drop
+        if drop is not None:
+            drop.forced = getattr(self, "_forced_votes", None)
         step.defer_sync = drop is not None
         from .device_feed import DeviceFeed
 
@@ -421,7 +424,7 @@ class Optimizer:
                 n_ok = 1
             elif drop is not None and drop.timed_out(fetch):
                 # straggler: the deadline passed before compute could start — contribute nothing this iteration
-                loss = torch.zeros((), device=step.device)
+                loss = torch.zeros(())          # host placeholder: nothing queued behind a slow device
                 finished = 0.0
             else:
                 if eager_done == 1 and use_graph:
@@ -448,7 +451,9 @@ class Optimizer:
                     timing["e1"] = torch.cuda.Event(enable_timing=True)
                     timing["e1"].record()
                     timing["host_ms"] = (time.perf_counter() - timing["h0"]) * 1e3
-            step.throttle()          # the host stays at most TrainStep.MAX_INFLIGHT iterations ahead of the device
+            if finished is None or finished:
+                step.throttle()      # the host stays at most TrainStep.MAX_INFLIGHT iterations ahead of the device
+            # (a dropped rank skips it: its backlog must not hold the host, the pacer bounds it next iteration)
             self.metrics.add("computing time", time.perf_counter() - t1)
             records = batch.size() * world
             pending.append((st["neval"], loss.detach() if torch.is_tensor(loss) else torch.tensor(float(loss)),
@@ -457,10 +462,15 @@ class Optimizer:
             st["recordsProcessedThisEpoch"] += records
             self._sync_states(st)
             if drop is not None:
-                drop.maybe_update_threshold(step, st["neval"] - 1)
+                with drop.control():
+                    drop.maybe_update_threshold(step, st["neval"] - 1)
             need_loss = (self.logInterval > 0 and (st["neval"] - 1) % self.logInterval == 0)
             if need_loss or self.endWhen(st) or isinstance(self.endWhen, Trigger.minLoss(0).__class__):
-                self._flush_losses(step, pending, wall0)
+                if drop is not None:
+                    with drop.control():
+                        self._flush_losses(step, pending, wall0)
+                else:
+                    self._flush_losses(step, pending, wall0)
                 pending = []
             if st["recordsProcessedThisEpoch"] >= self._epoch_size():
                 st["epoch"] += 1
@@ -479,7 +489,7 @@ class Optimizer:
     def _flush_losses(self, step, pending, wall0):
         if not pending:
             return
-        losses = torch.stack([p[1].float().reshape(()) for p in pending]).to(step.device)
+        losses = torch.stack([p[1].float().reshape(()).to(step.device) for p in pending])
         if step.comm.world > 1:
             step.comm.all_reduce_scalar(losses)
             losses = losses / step.comm.world
@@ -586,31 +596,62 @@ class _StragglerDrop:
         self.dropped = 0
         self.iteration = 0
         self.cancelled = 0
+        self.history = []        # this rank's vote per iteration (1 finished, 0 dropped)
+        self.forced = None       # {iteration: vote}: replay a recorded drop pattern (tests)
+        self._ctrl = None
 
+    def control(self):
+        """Stream context for the straggler bookkeeping (votes, threshold gathers, loss flushes): a stream that does
+        not wait for the compute stream, so a rank with a device backlog answers these collectives on time. Every
+        tensor it reads is complete: finished iterations were drained (``run``), dropped ones left host placeholders."""
+        import contextlib
+
+        if not torch.cuda.is_available() or self.opt._step is None or self.opt._step.device.type != "cuda":
+            return contextlib.nullcontext()
+        if self._ctrl is None:
+            self._ctrl = torch.cuda.Stream(device=self.opt._step.device)
+        return torch.cuda.stream(self._ctrl)
     def timed_out(self, elapsed):
-        return elapsed > self.threshold
+        return self.forced is None and elapsed > self.threshold
 
     def finished(self, elapsed):
         self.times.append(elapsed)
         return 0.0 if elapsed > self.threshold else 1.0
 
     def run(self, step, x, y, t0):
-        """forward + backward under the iteration deadline t0 + threshold. Returns (loss, finished weight)."""
-        from ..nn.abstractnn import STRAGGLER_DEADLINE, StragglerTimeout
+        """forward + backward under the iteration deadline t0 + threshold. Returns (loss, finished weight).
 
-        if self.threshold != float("inf"):
-            STRAGGLER_DEADLINE[0] = t0 + self.threshold
+        GPU ranks are paced on device progress (nn/abstractnn.py DevicePacer): the iteration counts as finished only
+        once the device has executed all of its backward, and the time recorded for the threshold is that
+        device-inclusive time, so a slow GPU (not only a slow host) is timed out and dropped."""
+        from ..nn.abstractnn import STRAGGLER_DEADLINE, STRAGGLER_PACER, DevicePacer, StragglerTimeout
+
+        if self.forced is not None:         # replay of a recorded drop pattern: same math, no clocks
+            loss = step.forward_backward_step(x, y)
+            v = float(self.forced.get(self.iteration, 1.0))
+            self.times.append(0.0)
+            return (loss, 1.0) if v else (torch.zeros(()), 0.0)
+        armed = self.threshold != float("inf")
+        deadline = t0 + self.threshold if armed else float("inf")
+        pacer = DevicePacer() if step.device.type == "cuda" else None
+        if armed:
+            STRAGGLER_DEADLINE[0] = deadline
+            STRAGGLER_PACER[0] = pacer
         try:
             loss = step.forward_backward_step(x, y)
+            if pacer is not None:
+                pacer.drain(deadline)
         except StragglerTimeout:
             self.times.append(time.perf_counter() - t0)
             self.cancelled += 1
-            return torch.zeros((), device=step.device), 0.0
+            return torch.zeros(()), 0.0
         finally:
             STRAGGLER_DEADLINE[0] = 0.0
+            STRAGGLER_PACER[0] = None
         return loss, self.finished(time.perf_counter() - t0)
 
     def record(self, updated, finished):
+        self.history.append(float(finished))
         self.iteration += 1
         if not finished:
             self.dropped += 1

@@ -351,10 +351,11 @@ class TrainStep:
         for proc in self.processors:
             proc(self)
 
-    def optimize_pieces(self, loss, pieces=None):
+    def optimize_pieces(self, loss, pieces=None, g=None):
         self._lockstep()
+        g = self.g if g is None else g
         for p in (self.plan if pieces is None else pieces):
-            gs = self.g[p.lo:p.hi]
+            gs = g[p.lo:p.hi]
             p.method.optimize(lambda _x, _g=gs: (loss, _g), self.w[p.lo:p.hi])
 
     def sync_and_update(self, loss, finished=None):
@@ -381,18 +382,40 @@ class TrainStep:
     defer_sync = False
 
     def _sync_and_update_weighted(self, loss, finished):
+        """A dropped rank (``finished`` 0) on a GPU may still have kernels of its abandoned iteration queued on the
+        compute stream (a slow device, see nn/abstractnn.py DevicePacer). Its part of the exchange — the vote, a
+        zero gradient contribution, the update of the shard it owns and the weight all-gather — runs on a stream that
+        does not wait for the compute stream, so the finished ranks are not held in the collectives by its backlog;
+        the compute stream waits for that stream before the next iteration. The zero contribution comes from a
+        separate buffer: the abandoned kernels may still be writing the gradient buffer."""
         self.flush()
+        late = not finished and self.device.type == "cuda"
+        if not late:
+            return self._weighted_exchange(loss, finished, self.g)
+        if getattr(self, "_late_stream", None) is None:
+            self._late_stream = torch.cuda.Stream(device=self.device)
+            self._late_g = torch.zeros_like(self.g)
+        cur = torch.cuda.current_stream(self.device)
+        s = self._late_stream
+        with torch.cuda.stream(s):
+            try:
+                return self._weighted_exchange(loss, 0.0, self._late_g)
+            finally:
+                self._late_g.zero_()            # the reduced chunks landed in it
+                cur.wait_stream(s)
+
+    def _weighted_exchange(self, loss, finished, g):
         cnt = torch.tensor([float(finished)], device=self.device)
         self.comm.all_reduce_scalar(cnt)
         n = float(cnt.item())
-        if not finished:
+        if not finished and g is self.g:
             self.g.zero_()
         if self.bucketed is not None:
             # the update plan is per bucket (this rank owns one chunk of every bucket, not [start, end)):
             # reduce each bucket into its owned chunk and average those chunks over the finished ranks
             chunks = []
             for (b0, b1) in self.bucketed.bounds:
-                work, chunk = self.comm.reduce_scatter_range(self.g, b0, b1, average=False)
+                work, chunk = self.comm.reduce_scatter_range(g, b0, b1, average=False)
                 if work is not None:
                     work.wait()
                 chunks.append(chunk)
@@ -401,17 +424,32 @@ class TrainStep:
             for c in chunks:
                 c.mul_(1.0 / n)
         else:
-            self.comm.reduce_scatter_gradients(self.g, out=self.g_shard, average=False)
+            shard = self.comm.shard_of(g)
+            self.comm.reduce_scatter_gradients(g, out=shard, average=False)
             if n <= 0 or n < self.min_finished:
                 return False
-            self.g_shard.mul_(1.0 / n)
-        self.apply_processors()
-        self.optimize_pieces(loss)
+            shard.mul_(1.0 / n)
+        if g is not self.g:
+            self._processors_on(g)
+        else:
+            self.apply_processors()
+        self.optimize_pieces(loss, g=g)
         if self.bucketed is not None:
             self.bucketed.gather_all()
         else:
             self.comm.all_gather_weights(self.w, self.w16)
         return True
+
+    def _processors_on(self, g):
+        """Run the parameter processors (clipping, LARS) on another gradient buffer than ``self.g``."""
+        if not self.processors:
+            return
+        keep = self.g
+        self.g = g
+        try:
+            self.apply_processors()
+        finally:
+            self.g = keep
 
     def flush(self):
         """Complete a deferred (bucketed) weight all-gather: afterwards every rank holds the current weights."""

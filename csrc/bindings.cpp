@@ -160,6 +160,10 @@ void bn_bwd_apply(const Tensor& dz, const OptT& z, const Tensor& x, const Tensor
                      ocf(aff, "aff"), stream());
 }
 
+void spin_us(double us, const Tensor& done) {
+  TORCH_CHECK(done.is_cuda() && done.scalar_type() == at::kInt && done.numel() >= 1, "spin_us: done must be int32 cuda");
+  bigdl_spin_us(us, done.data_ptr<int>(), stream());
+}
 void relu_fwd(const Tensor& x, const Tensor& y) {
   TORCH_CHECK(x.numel() == y.numel(), "relu: size");
   bigdl_relu_fwd(cbf(x, "x"), mbf(y, "y"), x.numel(), stream());
@@ -969,6 +973,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("gamma"), py::arg("red"), py::arg("nslots"), py::arg("coef"), py::arg("dx"), py::arg("dres"),
         py::arg("dgamma"), py::arg("dbeta"), py::arg("P"), py::arg("C"), py::arg("aff") = py::none());
   m.def("relu_fwd", &relu_fwd);
+  m.def("spin_us", &spin_us, "device-side delay of `us` microseconds on the current stream (straggler injection)");
   m.def("relu_bwd", &relu_bwd);
   m.def("add_bf16", &add_bf16);
   m.def("nchw_to_nhwc", &nchw_to_nhwc);

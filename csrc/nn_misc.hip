@@ -313,3 +313,21 @@ void bigdl_f32_to_bf16_rtz(const float* x, uint16_t* y, long n, hipStream_t st) 
   if (n4 * 4 < n) f32_to_bf16_rtz_tail<<<1, 64, 0, st>>>((const unsigned*)x, y, n4 * 4, n);
   HIP_LAUNCH_CHECK();
 }
+
+// ------------------------------------------------------------------------------------------------
+// Device-side delay: one wave spins on the constant-rate real-time counter (s_memrealtime, 100 MHz on gfx950) for
+// `us` microseconds, capped at 5 s so a bad argument cannot hang the queue. Injects a compute straggler for the
+// straggler-drop tests (optim/optimizer.py _StragglerDrop) without touching the host.
+namespace {
+__global__ __launch_bounds__(64) void spin_us_kernel(long ticks, int* done) {
+  const unsigned long t0 = wall_clock64();
+  while ((long)(wall_clock64() - t0) < ticks) __builtin_amdgcn_s_sleep(8);
+  if (threadIdx.x == 0) done[0] = 1;
+}
+}  // namespace
+
+void bigdl_spin_us(double us, int* done, hipStream_t st) {
+  double t = us < 0 ? 0 : (us > 5e6 ? 5e6 : us);
+  spin_us_kernel<<<1, 64, 0, st>>>((long)(t * 100.0), done);   // wall_clock64 ticks at 100 MHz
+  HIP_LAUNCH_CHECK();
+}
