@@ -129,4 +129,153 @@ def gemv(y, A, x, M=None, alpha=1.0, beta=0.0):
     return y
 
 
-__all__ = ["native_ok", "apply", "reduce", "gemm", "gemv"]
+# ------------------------------------------------------------------------------------- index / sort / mask ops
+# csrc/index_ops.hip. Every function returns None when the operands do not qualify (non-contiguous in-place
+# target, index not a 1-based fp32 / int64 cuda tensor, row too long for the in-LDS sort): the caller uses torch.
+_ERR = {}
+
+
+def _orc(shape, dim):
+    outer = 1
+    for s in shape[:dim]:
+        outer *= s
+    inner = 1
+    for s in shape[dim + 1:]:
+        inner *= s
+    return outer, shape[dim], inner
+
+
+def _idx_ok(idx):
+    return isinstance(idx, torch.Tensor) and idx.is_cuda and idx.dtype in (torch.float32, torch.int64)
+
+
+def _err(dev):
+    e = _ERR.get(dev)
+    if e is None:
+        e = _ERR[dev] = torch.zeros(1, dtype=torch.int32, device=dev)
+    return e
+
+
+def _c(t):
+    if t.is_contiguous():
+        return t
+    out = torch.empty(t.shape, dtype=t.dtype, device=t.device)
+    if t.dtype == torch.float32 and apply(COPY, out, t):
+        return out
+    return t.contiguous()
+
+
+def index_select(src, dim, idx):
+    """out = src.index_select(dim, idx - 1) with a 1-based index vector."""
+    if not (native_ok(src) and _idx_ok(idx)):
+        return None
+    idx = _c(idx.reshape(-1))
+    src = _c(src)
+    outer, R, inner = _orc(tuple(src.shape), dim)
+    shape = list(src.shape)
+    shape[dim] = idx.numel()
+    out = torch.empty(shape, device=src.device, dtype=torch.float32)
+    native.get().index_op(0, None, idx, src, out, outer, R, idx.numel(), inner, 0, _err(src.device))
+    return out
+
+
+def index_add(dst, dim, idx, src):
+    """dst.index_add_(dim, idx - 1, src) in place (duplicate indices accumulate)."""
+    if not (native_ok(dst, src) and _idx_ok(idx) and dst.is_contiguous()):
+        return None
+    idx = _c(idx.reshape(-1))
+    src = _c(src)
+    outer, R, inner = _orc(tuple(dst.shape), dim)
+    if src.numel() != outer * idx.numel() * inner:
+        return None
+    native.get().index_op(1, dst, idx, src, None, outer, R, idx.numel(), inner, 0, _err(dst.device))
+    increment_version(dst)
+    return dst
+
+
+def gather(src, dim, idx):
+    """out[..., j, ...] = src[..., idx[..., j, ...] - 1, ...] (idx shaped like the output; other dims = src's)."""
+    if not (native_ok(src) and _idx_ok(idx)) or idx.dim() != src.dim():
+        return None
+    if any(idx.shape[d] != src.shape[d] for d in range(src.dim()) if d != dim):
+        return None
+    idx, src = _c(idx), _c(src)
+    outer, R, inner = _orc(tuple(src.shape), dim)
+    out = torch.empty(idx.shape, device=src.device, dtype=torch.float32)
+    native.get().index_op(2, None, idx, src, out, outer, R, idx.shape[dim], inner, 0, _err(src.device))
+    return out
+
+
+def scatter(dst, dim, idx, src):
+    """dst[..., idx[..., j, ...] - 1, ...] = src[..., j, ...] in place."""
+    if not (native_ok(dst, src) and _idx_ok(idx) and dst.is_contiguous()) or idx.dim() != dst.dim():
+        return None
+    if any(idx.shape[d] != dst.shape[d] for d in range(dst.dim()) if d != dim) or src.dim() != dst.dim():
+        return None
+    if any(src.shape[d] != idx.shape[d] for d in range(dst.dim()) if d != dim) or src.shape[dim] < idx.shape[dim]:
+        return None
+    idx, src = _c(idx), _c(src)
+    outer, R, inner = _orc(tuple(dst.shape), dim)
+    native.get().index_op(3, dst, idx, src, None, outer, R, idx.shape[dim], inner, src.shape[dim], _err(dst.device))
+    increment_version(dst)
+    return dst
+
+
+def masked_fill(x, mask, v):
+    if not (native_ok(x, mask) and x.is_contiguous() and mask.numel() == x.numel()):
+        return None
+    native.get().masked_fill(x, _c(mask).reshape(-1), float(v))
+    increment_version(x)
+    return x
+
+
+def _mask_counts(mask):
+    C = native.get()
+    counts = torch.empty(C.mask_blocks(mask.numel()) + 1, dtype=torch.int32, device=mask.device)
+    C.mask_scan(mask, counts)
+    return counts
+
+
+def masked_select(x, mask):
+    """1-D tensor of x's elements where mask != 0, in element order (one host read of the count)."""
+    if not (native_ok(x, mask) and mask.numel() == x.numel()):
+        return None
+    x, mask = _c(x), _c(mask)
+    counts = _mask_counts(mask)
+    n = int(counts.narrow(0, counts.numel() - 1, 1).item())
+    out = torch.empty(n, device=x.device, dtype=torch.float32)
+    if n:
+        native.get().mask_write(False, x, mask, None, out, counts)
+    return out
+
+
+def masked_copy(x, mask, src):
+    """x[mask != 0] = the first elements of src, in element order, in place."""
+    if not (native_ok(x, mask, src) and x.is_contiguous() and mask.numel() == x.numel()):
+        return None
+    mask, src = _c(mask), _c(src)
+    counts = _mask_counts(mask)
+    native.get().mask_write(True, x, mask, src.reshape(-1), None, counts)
+    increment_version(x)
+    return x
+
+
+def topk(x, k, dim, largest):
+    """(values, 1-based fp32 indices) of the k smallest / largest along ``dim``, sorted; None for rows > 8192."""
+    if not native_ok(x) or x.dim() == 0:
+        return None
+    outer, R, inner = _orc(tuple(x.shape), dim)
+    if R > 8192 or k > R or k <= 0:
+        return None
+    x = _c(x)
+    shape = list(x.shape)
+    shape[dim] = k
+    vals = torch.empty(shape, device=x.device, dtype=torch.float32)
+    inds = torch.empty(shape, device=x.device, dtype=torch.float32)
+    if not native.get().topk_f32(x, outer, R, inner, k, bool(largest), vals, inds):
+        return None
+    return vals, inds
+
+
+__all__ = ["native_ok", "apply", "reduce", "gemm", "gemv", "index_select", "index_add", "gather", "scatter",
+           "masked_fill", "masked_select", "masked_copy", "topk"]

@@ -857,7 +857,8 @@ class Tensor:
             return fn(self._t).item()
         dim = args[0]
         vals, idx = (fn(self._t, _d(dim), keepdim=True) if not isinstance(dim, Tensor) else (None, None))
-        return self._wrap(vals), self._wrap(idx + 1)
+        # T-typed 1-based indices (the reference's representation), the same as the native fp32 GPU path
+        return self._wrap(vals), self._wrap((idx + 1).to(self._t.dtype) if self._t.is_floating_point() else idx + 1)
 
     def _native_minmax(self, op, args):
         if not (_g32(self._t) and self._t.numel() > 0):
@@ -902,11 +903,16 @@ class Tensor:
     def topk(self, k, dim=-1, increase=True, result=None, indices=None, sortedResult=True):
         """k smallest (``increase=True``, the Torch7 default) or largest values along ``dim``; 1-based indices."""
         d = self._t.dim() - 1 if dim == -1 else _d(dim)
-        v, i = torch.topk(self._t, k, dim=d, largest=not increase, sorted=sortedResult)
+        r = _tm.topk(self._t, k, d, not increase)      # native in-LDS sort (always sorted) for fp32 GPU rows <= 8192
+        if r is not None:
+            v, i1 = r
+        else:
+            v, i = torch.topk(self._t, k, dim=d, largest=not increase, sorted=sortedResult)
+            v, i1 = v.clone(), (i + 1).to(self._t.dtype)
         result = Tensor() if result is None else result
         indices = Tensor() if indices is None else indices
-        result._set_t(v.clone())
-        indices._set_t((i + 1).to(self._t.dtype))
+        result._set_t(v)
+        indices._set_t(i1)
         return result, indices
 
     def numNonZeroByRow(self):
@@ -935,31 +941,42 @@ class Tensor:
         return bool((self._t != v).any())
 
     def maskedFill(self, mask, e):
-        self._t.masked_fill_(_raw(mask).bool(), e)
+        if _tm.masked_fill(self._t, _raw(mask), e) is None:
+            self._t.masked_fill_(_raw(mask).bool(), e)
         return self
 
     def maskedCopy(self, mask, y):
-        m = _raw(mask).bool()
-        self._t[m] = _raw(y).reshape(-1)[: int(m.sum())].to(self._t.dtype)
+        if _tm.masked_copy(self._t, _raw(mask), _raw(y)) is None:
+            m = _raw(mask).bool()
+            self._t[m] = _raw(y).reshape(-1)[: int(m.sum())].to(self._t.dtype)
         return self
 
     def maskedSelect(self, mask, y):
-        return y._set_t(self._t[_raw(mask).bool()].clone())
+        r = _tm.masked_select(self._t, _raw(mask))
+        return y._set_t(r if r is not None else self._t[_raw(mask).bool()].clone())
 
     # ------------------------------------------------------------------ indexing (1-based index tensors)
     def index(self, dim, index, y):
         """self = y.index_select(dim, index) (TensorMath.scala index)."""
-        return self._assign(_raw(y).index_select(_d(dim), _raw(index).long().reshape(-1) - 1))
+        r = _tm.index_select(_raw(y), _d(dim), _raw(index))
+        if r is None:
+            r = _raw(y).index_select(_d(dim), _raw(index).long().reshape(-1) - 1)
+        return self._assign(r)
 
     def indexAdd(self, dim, index, y):
-        self._t.index_add_(_d(dim), _raw(index).long().reshape(-1) - 1, _raw(y))
+        if _tm.index_add(self._t, _d(dim), _raw(index), _raw(y)) is None:
+            self._t.index_add_(_d(dim), _raw(index).long().reshape(-1) - 1, _raw(y))
         return self
 
     def gather(self, dim, index, src):
-        return self._assign(torch.gather(_raw(src), _d(dim), _raw(index).long() - 1))
+        r = _tm.gather(_raw(src), _d(dim), _raw(index))
+        if r is None:
+            r = torch.gather(_raw(src), _d(dim), _raw(index).long() - 1)
+        return self._assign(r)
 
     def scatter(self, dim, index, src):
-        self._t.scatter_(_d(dim), _raw(index).long() - 1, _raw(src))
+        if _tm.scatter(self._t, _d(dim), _raw(index), _raw(src)) is None:
+            self._t.scatter_(_d(dim), _raw(index).long() - 1, _raw(src))
         return self
 
     # ------------------------------------------------------------------ conv

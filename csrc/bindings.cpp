@@ -243,6 +243,42 @@ void tensor_reduce(const Tensor& x, int64_t outer, int64_t R, int64_t inner, int
                                      mean ? 1 : 0, omf(ws, "ws"), chunks, stream());
   TORCH_CHECK(rc == 0, "tensor_reduce: unsupported size");
 }
+// index ops over [outer, R, inner] (csrc/index_ops.hip): op 0 index_select(b -> out), 1 index_add(b into a),
+// 2 gather(b -> out, idx shaped like out), 3 scatter(b into a, idx shaped like b's [outer, n, inner])
+void index_op(int64_t op, const OptT& a, const Tensor& idx, const OptT& b, const OptT& out, int64_t outer, int64_t R,
+              int64_t n, int64_t inner, int64_t Rsrc, const Tensor& err) {
+  TORCH_CHECK(idx.is_cuda() && idx.is_contiguous() && (idx.scalar_type() == at::kFloat || idx.scalar_type() == at::kLong),
+              "index_op: idx must be a contiguous fp32 or int64 cuda tensor");
+  TORCH_CHECK(err.scalar_type() == at::kInt && err.is_cuda(), "index_op: err int32");
+  for (const OptT* t : {&a, &b, &out})
+    if (*t && (*t)->defined()) TORCH_CHECK((*t)->is_contiguous(), "index_op: operands must be contiguous");
+  const int rc = bigdl_index_op((int)op, omf(a, "a"), idx.data_ptr(), idx.scalar_type() == at::kLong ? 1 : 0,
+                                ocf(b, "b"), omf(out, "out"), outer, R, n, inner, Rsrc, err.data_ptr<int>(), stream());
+  TORCH_CHECK(rc == 0, "index_op: unsupported op");
+}
+void masked_fill(const Tensor& x, const Tensor& mask, double v) {
+  TORCH_CHECK(x.is_contiguous() && mask.is_contiguous() && x.numel() == mask.numel(), "masked_fill: contiguous, same size");
+  bigdl_masked_fill(mf(x, "x"), cf(mask, "mask"), (float)v, x.numel(), stream());
+}
+int64_t mask_blocks(int64_t n) { return bigdl_mask_blocks(n); }
+void mask_scan(const Tensor& mask, const Tensor& counts) {
+  TORCH_CHECK(mask.is_contiguous() && counts.scalar_type() == at::kInt &&
+                  counts.numel() >= bigdl_mask_blocks(mask.numel()) + 1, "mask_scan: counts int32[blocks + 1]");
+  bigdl_mask_scan(cf(mask, "mask"), mask.numel(), counts.data_ptr<int>(), stream());
+}
+void mask_write(bool copy, const Tensor& x, const Tensor& mask, const OptT& src, const OptT& out, const Tensor& counts) {
+  TORCH_CHECK(x.is_contiguous() && mask.is_contiguous() && x.numel() == mask.numel(), "mask_write: contiguous, same size");
+  const long nsrc = (src && src->defined()) ? src->numel() : 0;
+  bigdl_mask_write(copy ? 1 : 0, mf(x, "x"), cf(mask, "mask"), ocf(src, "src"), omf(out, "out"), x.numel(),
+                   counts.data_ptr<int>(), nsrc, stream());
+}
+bool topk_f32(const Tensor& x, int64_t outer, int64_t R, int64_t inner, int64_t k, bool largest, const Tensor& vals,
+              const Tensor& inds) {
+  TORCH_CHECK(x.is_contiguous() && x.numel() == outer * R * inner, "topk: contiguous [outer, R, inner]");
+  TORCH_CHECK(vals.numel() == outer * k * inner && inds.numel() == vals.numel(), "topk: outputs [outer, k, inner]");
+  return bigdl_topk(cf(x, "x"), outer, R, inner, (int)k, largest ? 1 : 0, mf(vals, "vals"), mf(inds, "inds"),
+                    stream()) == 0;
+}
 // strides s = [sam, sak, sbk, sbn, scm, scn, smm, smn, bsa, bsb, bsc, bsm]
 void gemm_f32(const Tensor& A, const Tensor& B, const OptT& Min, const Tensor& C, int64_t batch, int64_t M, int64_t N,
               int64_t K, std::vector<int64_t> s, double alpha, double beta) {
@@ -987,6 +1023,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("tensor_reduce", &tensor_reduce, py::arg("x"), py::arg("outer"), py::arg("R"), py::arg("inner"), py::arg("op"),
         py::arg("p"), py::arg("out"), py::arg("outi"), py::arg("mean"), py::arg("ws"), py::arg("chunks"));
   m.def("gemm_f32", &gemm_f32);
+  m.def("index_op", &index_op);
+  m.def("masked_fill", &masked_fill);
+  m.def("mask_blocks", &mask_blocks);
+  m.def("mask_scan", &mask_scan);
+  m.def("mask_write", &mask_write);
+  m.def("topk_f32", &topk_f32);
   m.def("gemv_f32", &gemv_f32);
   m.def("fill_bytes", &fill_bytes);
   m.def("copy_rows_i8", &copy_rows_i8);

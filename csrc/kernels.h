@@ -161,6 +161,15 @@ void bigdl_dequantize_rows(const int8_t* q, uint16_t* y, long P, int C, long ld,
 int bigdl_tensor_apply(float* out, const float* a, const float* b, const float* c, int nd, const long* size,
                        const long* so, const long* sa, const long* sb, const long* sc, int op, float s0, float s1,
                        int contiguous, hipStream_t st);
+int bigdl_index_op(int op, float* a, const void* idx, int idx_i64, const float* b, float* out, long outer, long R,
+                   long n, long inner, long Rsrc, int* err, hipStream_t st);
+void bigdl_masked_fill(float* x, const float* mask, float v, long n, hipStream_t st);
+long bigdl_mask_blocks(long n);
+void bigdl_mask_scan(const float* mask, long n, int* counts, hipStream_t st);
+void bigdl_mask_write(int copy, float* x, const float* mask, const float* src, float* out, long n, const int* counts,
+                      long nsrc, hipStream_t st);
+int bigdl_topk(const float* x, long outer, long R, long inner, int k, int largest, float* vals, float* inds,
+               hipStream_t st);
 int bigdl_tensor_reduce(const float* x, long outer, long R, long inner, int op, float p, float* out, float* outi,
                         int mean, float* ws, long chunks, hipStream_t st);
 int bigdl_gemm_f32(const float* A, const float* B, const float* Min, float* C, int batch, int M, int N, int K,

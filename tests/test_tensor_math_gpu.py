@@ -181,3 +181,62 @@ def test_softmax_layer_native_matches_torch(monkeypatch):
         xr = x.clone().requires_grad_(True)
         (torch.softmax(xr if isinstance(layer, nn.SoftMax) else -xr, 1) * gy).sum().backward()
         assert torch.allclose(gx.cpu(), xr.grad, atol=1e-5)
+
+
+@contextlib.contextmanager
+def no_aten_index(monkeypatch):
+    """torch's index / sort / mask entry points raise: a pass proves csrc/index_ops.hip ran."""
+    def boom(name):
+        def f(*a, **k):
+            raise AssertionError(f"aten {name} called on the native index path")
+        return f
+    with monkeypatch.context() as mp:
+        for name in ("topk", "gather", "sort"):
+            mp.setattr(torch, name, boom(name))
+        for name in ("index_select", "index_add_", "scatter_", "masked_fill_", "masked_select", "topk", "gather",
+                     "__setitem__"):
+            mp.setattr(torch.Tensor, name, boom(name))
+        yield
+
+
+def test_index_sort_mask_ops_native(monkeypatch):
+    """TensorMath gather (:199), scatter (:209), topk (:622), masked* (:700-719), index (:739), indexAdd (:751):
+    fp32 GPU results vs the torch CPU path of the same Tensor calls (1-based T-typed indices)."""
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(6, 300, 5, generator=g)
+    idx = torch.randint(1, 301, (40,), generator=g).float()
+    gidx = torch.randint(1, 301, (6, 17, 5), generator=g).float()
+    sidx = torch.stack([torch.randperm(300, generator=g)[:17] + 1 for _ in range(30)]).float().reshape(6, 5, 17) \
+        .transpose(1, 2).contiguous()
+    src = torch.randn(6, 17, 5, generator=g)
+    mask = (torch.rand(6, 300, 5, generator=g) > 0.6).float()
+    addsrc = torch.randn(6, 40, 5, generator=g)
+    cpu = {"x": Tensor(x.clone())}
+    gpu = {"x": Tensor(x.clone().cuda())}
+    res = {}
+    for name, T, dev in (("cpu", cpu, "cpu"), ("gpu", gpu, "cuda")):
+        d = lambda t: Tensor(t.clone().to(dev))  # noqa: E731
+        ctx = no_aten_index(monkeypatch) if dev == "cuda" else contextlib.nullcontext()
+        with ctx:
+            out = {}
+            out["index"] = Tensor().index(2, d(idx), T["x"])
+            out["gather"] = Tensor().gather(2, d(gidx), T["x"])
+            sc = d(x)
+            out["scatter"] = sc.scatter(2, d(sidx), d(src))
+            ia = d(x)
+            out["indexAdd"] = ia.indexAdd(2, d(idx), d(addsrc))
+            for k, inc in ((1, True), (7, False), (300, True)):
+                v, i = T["x"].topk(k, 2, inc)
+                out[f"topk{k}{inc}_v"], out[f"topk{k}{inc}_i"] = v, i
+            mf = d(x)
+            out["maskedFill"] = mf.maskedFill(d(mask), -3.5)
+            out["maskedSelect"] = T["x"].maskedSelect(d(mask), Tensor())
+            mc = d(x)
+            out["maskedCopy"] = mc.maskedCopy(d(mask), d(torch.arange(float(mask.numel()))))
+            vmax, imax = T["x"].max(2)
+            out["max_i"] = imax
+        res[name] = out
+    for k in res["cpu"]:
+        _close(res["gpu"][k], res["cpu"][k], tol=1e-5)
+        if k.endswith("_i"):
+            assert res["gpu"][k]._t.dtype == res["cpu"][k]._t.dtype == torch.float32, k   # T-typed indices
