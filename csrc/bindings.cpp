@@ -1098,6 +1098,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_conv_impl", &bigdl_set_conv_impl);
   m.def("get_conv_impl", &bigdl_get_conv_impl);
   m.def("set_conv_g4", &bigdl_set_conv_g4);
+  m.def("set_conv_p8", &bigdl_set_conv_p8);
   m.def("get_conv_g4", &bigdl_get_conv_g4);
   m.def("set_wgrad_g3", &bigdl_set_wgrad_g3);
   m.def("get_wgrad_g3", &bigdl_get_wgrad_g3);

@@ -1840,6 +1840,224 @@ __global__ __launch_bounds__(256, (NS == 3 && BM == 128) ? 3 : 2) void conv_nt_g
   nt_epilogue_lds<MI, NI, TM, TN, NH, WGN * SL, WGM>(a, acc, m0 + wm * TM, n0 + wn * TN, lane, bid, wl, wm);
 }
 
+// ------------------------------------------------------------------------------------------------
+// 256 x 256 implicit-GEMM NT tile, BK = 64, 8 waves (2 M-halves x 4 N-quarters, 128 x 64 outputs per wave), one
+// workgroup per CU, two 64 KB LDS buffers. Phase-interleaved K-loop after the 8-phase template of
+// cdna_hip_programming.md §5: every K-tile is four phases; a phase is a LOAD segment (one LDS-DMA piece, fragment
+// ds_reads, a counted vmcnt) + barrier + a COMPUTE segment of 16 MFMAs (one 64 x 32 quadrant of the wave's tile,
+// K = 64) + barrier. The wave group of the second M-half runs one barrier behind the first, so on every SIMD one wave
+// computes while its partner loads.
+// A buffer holds a K-tile as four 16 KB pieces of 128 rows x 128 B (slot s of row r holds granule s ^ (r & 7), the
+// swizzle applied on the DMA source side), cut by the phase that first reads them:
+//   P0 = A rows of quadrant 0 of both M-halves, P1 = B rows of N-quadrant 0 of the four N-quarters,
+//   P2 = A quadrant 1, P3 = B quadrant 1.
+// Per K-tile t (reads from buffer t & 1; B fragments of both N-quadrants stay in registers through the tile):
+//   ph0: DMA P3(t+1); read A q0 + B q0 (P0, P1); vmcnt -> P3(t) landed        -> MFMA (0, 0)
+//   ph1: DMA P2(t+1); read B q1 (P3);            vmcnt -> P2(t) landed        -> MFMA (0, 1)
+//   ph2: DMA P0(t+2); read A q1 (P2)                                          -> MFMA (1, 1)
+//   ph3: DMA P1(t+2);                            vmcnt -> P0, P1(t+1) landed  -> MFMA (1, 0)
+// so one DMA piece is issued per phase, each piece has 4-5 phases to land, and at most four pieces (eight DMA
+// instructions per thread) are in flight. Hazards: a piece is waited for (counted vmcnt by every issuing wave) in the
+// LOAD segment before the one that reads it, i.e. before a barrier both groups pass first; a piece of buffer b is
+// overwritten at least two phases after its last read, by which time both groups retired that read (lgkmcnt(0) at
+// the start of their COMPUTE segment). The wave tile and the epilogue are those of conv_nt_w8_kernel.
+// FASTK only (Cs % 64 == 0: a K-tile lies in one tap). SPLIT: fp32 partials of a K range per blockIdx.y.
+// ABL (diagnostic ablation builds, BIGDL_P8_ABL; wrong outputs): bit 0 no LDS-DMA inside the K-loop, bit 1 no fragment
+// ds_reads after the first K-tile, bit 2 no wave-group stagger, bit 3 no MFMAs, bit 4 no A-operand DMA, bit 5 no
+// B-operand DMA
+template <bool SPLIT, int ABL = 0>
+__global__ __launch_bounds__(512, 2) void conv_nt_p8_kernel(ConvArgs a) {
+  constexpr int BM = 256, BN = 256, BKT = 64;
+  constexpr int WGM = 2, WGN = 4;
+  constexpr int TM = BM / WGM, TN = BN / WGN;      // 128 x 64 per wave
+  constexpr int MI = TM / 16, NI = TN / 16;        // 8 x 4 MFMA tiles
+  constexpr int PIECE = 128 * BKT;                 // bf16 elements per piece (16 KB)
+  constexpr int BUF = 4 * PIECE;                   // P0 P1 P2 P3 (64 KB)
+  constexpr int NH = 4;                            // epilogue row chunks
+  constexpr int SL = (TM / NH) * TN;
+  static_assert(8 * SL * 4 <= 2 * BUF * 2, "epilogue chunk must fit the buffers");
+  __shared__ __attribute__((aligned(1024))) bf16_t lds[2 * BUF + 3 * CONV_MAX_TAPS];
+  short* taps = reinterpret_cast<short*>(lds + 2 * BUF);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WGN, wn = wave % WGN;
+  const int tiles_n = (a.Ncol + BN - 1) / BN;
+  const int tiles_m = (a.M + BM - 1) / BM;
+  const int nwg = tiles_m * tiles_n;
+  const int bid = xcd_remap(blockIdx.x, nwg);
+  const int tm = bid / tiles_n, tn = bid % tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int nk_all = a.Kdim / BKT;
+  int kt0 = 0, nk = nk_all;
+  if constexpr (SPLIT) {
+    const int per = (nk_all + a.ksplit - 1) / a.ksplit;
+    kt0 = blockIdx.y * per;
+    nk = max(0, min(nk_all, kt0 + per) - kt0);
+  }
+
+  // DMA geometry: instruction j of wave w fills piece rows (j * 8 + w) * 8 .. +8 (8 rows x 128 B); lane -> row
+  // + (lane >> 3), slot lane & 7, which must hold granule (lane & 7) ^ (row & 7) = (lane & 7) ^ (lane >> 3).
+  // Piece row lr of an A piece of quadrant q is tile row (lr >> 6) * 128 + q * 64 + (lr & 63); of a B piece of
+  // quadrant q, tile column (lr >> 5) * 64 + q * 32 + (lr & 31). Slot q2 = q * 2 + j of the per-thread tables.
+  const int gsrc = (lane & 7) ^ (lane >> 3);
+  const int ohw = a.OH * a.OW;
+  int a_pix[4], a_h[4], a_w[4];
+  const bf16_t* wrow[4];
+  bool bvalid[4];
+#pragma unroll
+  for (int q2 = 0; q2 < 4; ++q2) {
+    const int q = q2 >> 1, lr = ((q2 & 1) * 8 + wave) * 8 + (lane >> 3);
+    const int m = m0 + (lr >> 6) * 128 + q * 64 + (lr & 63);
+    if (m < a.M) {
+      const int nb = m / ohw, rem = m - nb * ohw;
+      const int oh = rem / a.OW, ow = rem - oh * a.OW;
+      a_pix[q2] = nb * a.Hs * a.Ws;
+      a_h[q2] = oh * a.mul_h;
+      a_w[q2] = ow * a.mul_w;
+    } else {
+      a_pix[q2] = 0; a_h[q2] = -(1 << 28); a_w[q2] = -(1 << 28);
+    }
+    const int n = n0 + (lr >> 5) * 64 + q * 32 + (lr & 31);
+    bvalid[q2] = n < a.Ncol;
+    wrow[q2] = a.wt + (size_t)(bvalid[q2] ? n : 0) * a.ldw + gsrc * 8;
+  }
+  if (tid < a.ntaps) {
+    taps[tid] = a.tap_h[tid];
+    taps[CONV_MAX_TAPS + tid] = a.tap_w[tid];
+    taps[2 * CONV_MAX_TAPS + tid] = a.tap_k[tid];
+  }
+  __syncthreads();   // tap table visible (no DMA outstanding yet)
+
+  // piece P (0 A q0, 1 B q0, 2 A q1, 3 B q1) of K-tile kt into buffer buf: 2 DMA instructions per thread
+  auto issue = [&](int kt, int buf, int P) {
+    const int k0 = kt * BKT;
+    const int t = k0 / a.Cs;
+    const int cin = k0 - t * a.Cs;
+    bf16_t* base = lds + buf * BUF + P * PIECE;
+    const int q = P >> 1;
+    if ((ABL & 16) && (P & 1) == 0) return;
+    if ((ABL & 32) && (P & 1) == 1) return;
+    if ((P & 1) == 0) {
+      const int th = taps[t], tw = taps[CONV_MAX_TAPS + t];
+      const int c = cin + gsrc * 8;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int q2 = q * 2 + j;
+        const int ch = a_h[q2] + th, cw = a_w[q2] + tw;
+        const bool ok = (unsigned)ch < (unsigned)a.Hs && (unsigned)cw < (unsigned)a.Ws;
+        const bf16_t* src = ok ? a.src + (unsigned)((a_pix[q2] + ch * a.Ws + cw) * a.Cs + c) : g_zero_granule;
+        glds16(src, (LDS_PTR(void))(base + (j * 8 + wave) * 8 * BKT));
+      }
+    } else {
+      const int wk = taps[2 * CONV_MAX_TAPS + t] * a.Cs + cin;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int q2 = q * 2 + j;
+        const bf16_t* src = bvalid[q2] ? wrow[q2] + wk : g_zero_granule;
+        glds16(src, (LDS_PTR(void))(base + (j * 8 + wave) * 8 * BKT));
+      }
+    }
+  };
+  // fragment slot of K-half kh: granule kh * 4 + (lane >> 4) of piece row (lane & 15) + 16 i lives at slot ^ (lane & 7)
+  const int fo0 = (lane & 15) * BKT + (((lane >> 4)) ^ (lane & 7)) * 8;
+  const int fo1 = (lane & 15) * BKT + ((4 + (lane >> 4)) ^ (lane & 7)) * 8;
+  const int a_row = wm * 64 * BKT;                 // this wave's rows inside an A piece
+  const int b_row = wn * 32 * BKT;                 // this wave's rows inside a B piece
+
+  v4f acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+
+  v8s fa[4][2], fb[NI][2];
+  // 16 MFMAs of one 64 x 32 quadrant (rows ib .. ib + 3, columns jb, jb + 1), K-halves outermost so no two
+  // consecutive MFMAs accumulate into the same tile
+  auto quad = [&](int ib, int jb) {
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[ib + i][jb + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[jb + j][kh], fa[i][kh], acc[ib + i][jb + j], 0, 0, 0);
+  };
+  auto read_a = [&](const bf16_t* P) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      fa[i][0] = *reinterpret_cast<const v8s*>(P + a_row + i * 16 * BKT + fo0);
+      fa[i][1] = *reinterpret_cast<const v8s*>(P + a_row + i * 16 * BKT + fo1);
+    }
+  };
+  auto read_b = [&](const bf16_t* P, int jb) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      fb[jb + j][0] = *reinterpret_cast<const v8s*>(P + b_row + j * 16 * BKT + fo0);
+      fb[jb + j][1] = *reinterpret_cast<const v8s*>(P + b_row + j * 16 * BKT + fo1);
+    }
+  };
+  auto compute = [&](int ib, int jb) {
+    __builtin_amdgcn_s_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+    if constexpr (!(ABL & 8)) quad(ib, jb);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+  };
+
+  // prologue: K-tile 0 whole, then P0, P1 of K-tile 1; retire P0, P1 of K-tile 0
+  if (nk > 0) {
+    issue(kt0, 0, 0); issue(kt0, 0, 1); issue(kt0, 0, 3); issue(kt0, 0, 2);
+  }
+  if (nk > 1) {
+    issue(kt0 + 1, 1, 0); issue(kt0 + 1, 1, 1);
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  if (!(ABL & 4) && wm == 1) __builtin_amdgcn_s_barrier();   // stagger: the second M-half runs one barrier behind
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    const bf16_t* L = lds + cur * BUF;
+    const bool n1 = kt + 1 < nk, n2 = kt + 2 < nk;
+    // ---- phase 0
+    if (!(ABL & 1) && n1) issue(kt0 + kt + 1, cur ^ 1, 3);
+    if (!(ABL & 2) || kt == 0) { read_a(L); read_b(L + PIECE, 0); }
+    if (n1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");          // P3(t) landed
+    else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    compute(0, 0);
+    // ---- phase 1
+    if (!(ABL & 1) && n1) issue(kt0 + kt + 1, cur ^ 1, 2);
+    if (!(ABL & 2) || kt == 0) read_b(L + 3 * PIECE, 2);
+    if (n1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");          // P2(t) landed
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    compute(0, 2);
+    // ---- phase 2
+    if (!(ABL & 1) && n2) issue(kt0 + kt + 2, cur, 0);
+    if (!(ABL & 2) || kt == 0) read_a(L + 2 * PIECE);
+    compute(4, 2);
+    // ---- phase 3
+    if (!(ABL & 1) && n2) issue(kt0 + kt + 2, cur, 1);
+    if (n2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");          // P0, P1(t+1) landed
+    else if (n1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    compute(4, 0);
+  }
+  if (!(ABL & 4) && wm == 0) __builtin_amdgcn_s_barrier();   // balance the stagger: every wave has left the K-loop
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  float* wl = reinterpret_cast<float*>(lds) + wave * SL;
+  if constexpr (SPLIT) {
+    store_partials_lds<MI, NI, TM, TN, NH>(a.ws + (size_t)blockIdx.y * a.M * a.Ncol, a.M, a.Ncol, acc,
+                                           m0 + wm * TM, n0 + wn * TN, lane, wl);
+  } else {
+    nt_epilogue_lds<MI, NI, TM, TN, NH, WGN * SL, WGM>(a, acc, m0 + wm * TM, n0 + wn * TN, lane, bid, wl, wm);
+  }
+}
+
 // Grid of the split-K epilogue: (row blocks, 256-group channel chunks), ~8 rows per thread, <= 8192 blocks.
 dim3 splitk_grid(long P, int C, long* rpb_out) {
   const int G = C >> 3;
@@ -2014,6 +2232,33 @@ static int w8_pick(const ConvArgs* a) {
   return std::max(split, 1);
 }
 
+// BIGDL_CONV_P8: 0 = off, 1 (default) = the 256 x 256 phase-interleaved kernel on fast-K (Cs % 64 == 0) layers with
+// Ncol >= 256 and Kdim >= 256, split over K when its grid would leave CUs idle; 2 = wherever it applies (tests).
+// Returns 0 (not used), 1 (one pass) or the K split.
+int g_conv_p8 = -1;
+static int p8_pick(const ConvArgs* a) {
+  if (g_conv_p8 < 0) {
+    const char* e = getenv("BIGDL_CONV_P8");
+    g_conv_p8 = e ? atoi(e) : 1;
+  }
+  const int on = g_conv_p8;
+  if (!on || a->out32 || (a->Cs % 64) || (a->Ncol & 7) || (a->ldo & 7) || a->Kdim < 128) return 0;
+  // auto: deep reductions only. Per layer (tools/conv_roofline.py, ResNet-50 b256) the one-workgroup-per-CU tile wins
+  // from K = 1024 up (3x3 over 256 channels 101 -> 86 us) and loses below, where its prologue / epilogue are not
+  // hidden by a co-resident workgroup (1x1 512 -> 1024 stride 2: 103 -> 147 us)
+  if (on == 1 && (a->Ncol < 256 || a->Kdim < 1024)) return 0;
+  const long tiles = (long)((a->M + 255) / 256) * ((a->Ncol + 255) / 256);
+  const int nk = a->Kdim / 64;
+  if (tiles >= 160) return 1;
+  // split-K measured slower than the 256 x 128 deep-K kernel on the small ResNet grids (12544 x 512, K 4608:
+  // 452 vs 544 TF/s, tools/gemm_ceiling.py): auto mode leaves grids under 160 tiles to the other kernels
+  if (on == 1) return 0;
+  int split = (int)((256 + tiles - 1) / tiles);
+  split = std::min(split, std::max(1, nk / 4));
+  split = std::min(split, 8);
+  return std::max(split, 1);
+}
+
 template <int BN, int NS, int BM = 128>
 void launch_nt_g4(const ConvArgs& a, hipStream_t st) {
   const int nwg = ((a.M + BM - 1) / BM) * ((a.Ncol + BN - 1) / BN);
@@ -2056,6 +2301,7 @@ extern "C" {
 
 void bigdl_set_conv_impl(int impl) { g_conv_impl = impl; }
 void bigdl_set_conv_g4(int v) { g_conv_g4 = v; }
+void bigdl_set_conv_p8(int v) { g_conv_p8 = v; }
 int bigdl_get_conv_g4() { return g4_pick(); }
 int bigdl_get_conv_impl() { return conv_impl(); }
 
@@ -2063,6 +2309,12 @@ int bigdl_get_conv_impl() { return conv_impl(); }
 long bigdl_conv_nt_plan(ConvArgs* a) {
   a->ksplit = 0;
   if (a->Cs % 8 != 0 || a->M <= 0 || conv_impl() < 1) return 0;
+  const int p8 = conv_impl() == 1 ? p8_pick(a) : 0;
+  if (p8 > 1) {
+    a->ksplit = p8;
+    return (long)p8 * a->M * a->Ncol;
+  }
+  if (p8 == 1) return 0;
   const int k = w8_pick(a);
   if (k > 1) {
     a->ksplit = k;
@@ -2087,8 +2339,28 @@ int bigdl_conv_nt(const ConvArgs* a, hipStream_t st) {
   // 8-wave deep-pipelined kernel (tools/bench_conv.py, impl 1 vs 2); BIGDL_CONV_P3AUTO=0 keeps them on impl 1
   static const bool p3auto = [] { const char* e = getenv("BIGDL_CONV_P3AUTO"); return e ? atoi(e) != 0 : true; }();
   const bool p3_pick = impl == 2 || (impl == 1 && p3auto && a->M <= 50176 && a->Kdim >= 1024);
-  const int w8 = impl == 1 ? w8_pick(a) : 0;
-  if (w8 > 1 && a->ksplit == w8 && a->ws != nullptr) {
+  const int p8 = impl == 1 ? p8_pick(a) : 0;
+  const int w8 = (impl == 1 && p8 == 0) ? w8_pick(a) : 0;
+  if (p8 > 1 && a->ksplit == p8 && a->ws != nullptr) {
+    const int nwg = ((a->M + 255) / 256) * ((a->Ncol + 255) / 256);
+    conv_nt_p8_kernel<true><<<dim3(nwg, p8), dim3(512), 0, st>>>(*a);
+    long rpb = 0;
+    const dim3 grid = splitk_grid(a->M, a->Ncol, &rpb);
+    conv_splitk_epilogue_kernel<<<grid, dim3(256), 0, st>>>(*a, rpb);
+  } else if (p8 == 1) {
+    const int nwg = ((a->M + 255) / 256) * ((a->Ncol + 255) / 256);
+    static const int abl = [] { const char* e = getenv("BIGDL_P8_ABL"); return e ? atoi(e) : 0; }();
+    switch (abl) {
+      case 1: conv_nt_p8_kernel<false, 1><<<dim3(nwg), dim3(512), 0, st>>>(*a); break;
+      case 2: conv_nt_p8_kernel<false, 2><<<dim3(nwg), dim3(512), 0, st>>>(*a); break;
+      case 4: conv_nt_p8_kernel<false, 4><<<dim3(nwg), dim3(512), 0, st>>>(*a); break;
+      case 8: conv_nt_p8_kernel<false, 8><<<dim3(nwg), dim3(512), 0, st>>>(*a); break;
+      case 16: conv_nt_p8_kernel<false, 16><<<dim3(nwg), dim3(512), 0, st>>>(*a); break;
+      case 32: conv_nt_p8_kernel<false, 32><<<dim3(nwg), dim3(512), 0, st>>>(*a); break;
+      case 10: conv_nt_p8_kernel<false, 10><<<dim3(nwg), dim3(512), 0, st>>>(*a); break;
+      default: conv_nt_p8_kernel<false><<<dim3(nwg), dim3(512), 0, st>>>(*a);
+    }
+  } else if (w8 > 1 && a->ksplit == w8 && a->ws != nullptr) {
     const int nwg = ((a->M + 255) / 256) * ((a->Ncol + 255) / 256);
     conv_nt_w8_kernel<true><<<dim3(nwg, w8), dim3(512), 0, st>>>(*a);
     long rpb = 0;

@@ -180,6 +180,7 @@ void bigdl_copy_rows_i8(const int8_t* src, int8_t* dst, long rows, int C, long l
 void bigdl_set_conv_impl(int impl);
 int bigdl_get_conv_impl();
 void bigdl_set_conv_g4(int v);
+void bigdl_set_conv_p8(int v);
 int bigdl_get_conv_g4();
 void bigdl_set_wgrad_g3(int v);
 int bigdl_get_wgrad_g3();

@@ -683,3 +683,32 @@ def test_transpose_krsc_v8_matches_permute(K, RS, C):
     native.get().transpose_krsc(w, out, K, RS, C)
     torch.cuda.synchronize()
     assert torch.equal(out, w.permute(2, 1, 0).contiguous())
+
+
+P8_CASES = [
+    # N, C, H, K, R, stride, pad -> 256 x 256 phase-interleaved 8-wave kernel (Cs % 64 == 0)
+    (16, 256, 56, 256, 1, 1, 0),     # 196 tiles x 4 K-tiles: one pass
+    (16, 256, 14, 256, 3, 1, 1),     # 13 tiles x 36 K-tiles: split-K + split-K epilogue, padding taps
+    (4, 512, 7, 2048, 1, 1, 0),      # 8 tiles: split-K 2
+    (8, 128, 28, 320, 3, 1, 1),      # Ncol tail (320 % 256 != 0)
+    (16, 256, 28, 256, 3, 2, 1),     # stride 2: dgrad phases write a strided output placement
+    (66, 256, 28, 256, 1, 1, 0),     # >= 192 tiles, M tail
+    (3, 64, 10, 512, 3, 1, 1),       # tiny M (one tile), Cs = 64
+]
+
+
+@pytest.mark.parametrize("case", P8_CASES)
+def test_conv_p8_kernel_fwd_dgrad(case):
+    """256 x 256 phase-interleaved LDS-DMA kernel (BIGDL_CONV_P8=2 forces it wherever Cs % 64 == 0) and its split-K
+    path vs fp32 torch: forward + bias + BN statistics, forward + ReLU, data gradient + residual addend + the consumer
+    BN's fused backward reduction."""
+    from bigdl_amd.ops import native
+
+    C_ = native.get()
+    C_.set_conv_p8(2)
+    try:
+        test_conv_w8_kernel_fwd_dgrad_bnred.__wrapped__(case) if hasattr(test_conv_w8_kernel_fwd_dgrad_bnred, "__wrapped__") \
+            else test_conv_w8_kernel_fwd_dgrad_bnred(case)
+        torch.cuda.synchronize()
+    finally:
+        C_.set_conv_p8(1)
