@@ -88,11 +88,23 @@ class _Engine:
 
         timeout = datetime.timedelta(seconds=float(self.getProperty("bigdl.network.timeout", 1800)))
         os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+        kw = {"timeout": timeout}
+        attempt = os.environ.get("TORCHELASTIC_RESTART_COUNT")
+        if attempt is not None and "RANK" in os.environ and "WORLD_SIZE" in os.environ:
+            # under torch.distributed.run: rendezvous through the launcher's store under a key prefix of this restart
+            # attempt. With the default env:// rendezvous a job restarted by --max-restarts (the failure policy of
+            # optim/optimizer.py) finds the previous attempt's gloo peer addresses and fails to connect (measured on
+            # torch 2.10; tests/test_failure_recovery_cpu.py)
+            rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+            agent = os.environ.get("TORCHELASTIC_USE_AGENT_STORE", "False").lower() == "true"
+            base = td.TCPStore(os.environ["MASTER_ADDR"], int(os.environ["MASTER_PORT"]), world,
+                               is_master=(not agent and rank == 0), timeout=timeout)
+            kw.update(store=td.PrefixStore(f"bigdl/attempt_{attempt}", base), rank=rank, world_size=world)
         if backend == "nccl":
             torch.cuda.set_device(self.local_rank())
-            td.init_process_group(backend, device_id=torch.device("cuda", self.local_rank()), timeout=timeout)
+            td.init_process_group(backend, device_id=torch.device("cuda", self.local_rank()), **kw)
         else:
-            td.init_process_group(backend, timeout=timeout)
+            td.init_process_group(backend, **kw)
         self._pg_owned = True
 
     def shutdown(self):
