@@ -29,7 +29,10 @@ class _StatsArena:
         if self.need and (self.buf is None or self.buf.numel() < self.need or self.buf.device != device):
             self.buf = torch.empty(self.need, dtype=torch.float32, device=device)
         if self.buf is not None:
-            self.buf.zero_()
+            if self.buf.is_cuda:
+                native.get().fill_bytes(self.buf, 0)
+            else:
+                self.buf.zero_()
         self.off, self.need, self.active = 0, 0, True
 
     def end(self):

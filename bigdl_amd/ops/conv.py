@@ -169,14 +169,15 @@ def conv2d_dgrad(dy, w16t, x_shape, stride, pad, dil=(1, 1), out=None, addend=No
     if addend is not None and not addend.is_contiguous(memory_format=CL):
         addend = addend.contiguous(memory_format=CL)
     if out is None:
-        if covered != H * W and addend is not None:
-            out = addend.clone(memory_format=CL)
-        else:
-            out = torch.empty((N, C, H, W), dtype=BF16, device=dy.device, memory_format=CL)
-            if covered != H * W:
-                out.zero_()
-    elif covered != H * W:
-        if addend is not None:
+        out = torch.empty((N, C, H, W), dtype=BF16, device=dy.device, memory_format=CL)
+    if covered != H * W:
+        # pixels no phase reaches: zeros, or the folded residual addend (the phase GEMMs add it to theirs)
+        mask = 0
+        for (a, b, _, _, _) in phases:
+            mask |= 1 << (a * stride[1] + b)
+        if out.is_contiguous(memory_format=CL) and C % 8 == 0 and stride[0] * stride[1] <= 32:
+            native.get().dgrad_fill(out, addend, stride[0], stride[1], mask)
+        elif addend is not None:
             out.copy_(addend)
         else:
             out.zero_()

@@ -30,6 +30,8 @@ import os
 
 import torch
 
+from ..ops import native
+
 from ..optim.regularizer import L1L2Regularizer
 from ..parallel.allreduce_parameter import AllReduceParameter
 
@@ -285,7 +287,10 @@ class TrainStep:
 
     # ------------------------------------------------------------------ pieces
     def zero_grad(self):
-        self.g.zero_()
+        if self.g.is_cuda:
+            native.get().fill_bytes(self.g, 0)       # one runtime memset, no aten fill kernel
+        else:
+            self.g.zero_()
 
     def forward_backward(self, x, y):
         m, c = self.model, self.criterion

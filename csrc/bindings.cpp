@@ -160,6 +160,16 @@ void bn_bwd_apply(const Tensor& dz, const OptT& z, const Tensor& x, const Tensor
                      ocf(aff, "aff"), stream());
 }
 
+void dgrad_fill(const Tensor& out, const OptT& addend, int64_t sh, int64_t sw, int64_t mask) {
+  TORCH_CHECK(out.dim() == 4 && out.is_contiguous(at::MemoryFormat::ChannelsLast) && out.size(1) % 8 == 0,
+              "dgrad_fill: out must be NHWC bf16 with C % 8 == 0");
+  TORCH_CHECK(sh * sw <= 32, "dgrad_fill: at most 32 stride phases");
+  if (addend && addend->defined())
+    TORCH_CHECK(addend->sizes() == out.sizes() && addend->is_contiguous(at::MemoryFormat::ChannelsLast),
+                "dgrad_fill: addend must match out (NHWC)");
+  bigdl_dgrad_fill(mbf(out, "out"), ocbf(addend, "addend"), out.size(0) * out.size(2) * out.size(3), out.size(2),
+                   out.size(3), out.size(1), (int)sh, (int)sw, (unsigned)mask, stream());
+}
 void spin_us(double us, const Tensor& done) {
   TORCH_CHECK(done.is_cuda() && done.scalar_type() == at::kInt && done.numel() >= 1, "spin_us: done must be int32 cuda");
   bigdl_spin_us(us, done.data_ptr<int>(), stream());
@@ -1009,6 +1019,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("gamma"), py::arg("red"), py::arg("nslots"), py::arg("coef"), py::arg("dx"), py::arg("dres"),
         py::arg("dgamma"), py::arg("dbeta"), py::arg("P"), py::arg("C"), py::arg("aff") = py::none());
   m.def("relu_fwd", &relu_fwd);
+  m.def("dgrad_fill", &dgrad_fill);
   m.def("spin_us", &spin_us, "device-side delay of `us` microseconds on the current stream (straggler injection)");
   m.def("relu_bwd", &relu_bwd);
   m.def("add_bf16", &add_bf16);

@@ -746,3 +746,35 @@ void bigdl_lstm_cell_bwd(const float* act, const float* c_prev, const float* c, 
 }
 
 }  // extern "C"
+
+// ------------------------------------------------------------------------------------------------
+// Strided-conv data gradient: pixels of stride phases that no tap reaches (a 1x1 stride-2 conv covers one phase in
+// four) get zeros, or the residual addend when one is folded in; the phase GEMMs write every other pixel. Replaces
+// a full-tensor zero fill / addend copy ahead of the GEMMs (ops/conv.py conv2d_dgrad). NHWC bf16, C % 8 == 0, one
+// lane per 8-channel granule, 16-byte loads / stores; `mask` bit ph set = phase ph = (h % sh) * sw + (w % sw) covered.
+namespace {
+__global__ __launch_bounds__(256) void dgrad_fill_kernel(uint16_t* __restrict__ out, const uint16_t* __restrict__ add,
+                                                         long npix, int H, int W, int C8, int sh, int sw,
+                                                         unsigned mask) {
+  const long total = npix * C8;
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
+    const long pix = e / C8;
+    const int w = (int)(pix % W), h = (int)((pix / W) % H);
+    const int ph = (h % sh) * sw + (w % sw);
+    if ((mask >> ph) & 1u) continue;
+    v4u v = v4u{0u, 0u, 0u, 0u};
+    if (add) v = reinterpret_cast<const v4u*>(add)[e];
+    reinterpret_cast<v4u*>(out)[e] = v;
+  }
+}
+}  // namespace
+
+void bigdl_dgrad_fill(uint16_t* out, const uint16_t* add, long npix, int H, int W, int C, int sh, int sw, unsigned mask,
+                      hipStream_t st) {
+  const long total = npix * (C / 8);
+  if (total <= 0) return;
+  long g = (total + 255) / 256;
+  if (g > 16384) g = 16384;
+  dgrad_fill_kernel<<<(unsigned)g, 256, 0, st>>>(out, add, npix, H, W, C / 8, sh, sw, mask);
+  HIP_LAUNCH_CHECK();
+}

@@ -100,6 +100,8 @@ void bigdl_bn_bwd_apply(const uint16_t* dz, const uint16_t* z, const uint16_t* x
 // elementwise
 void bigdl_relu_fwd(const uint16_t* x, uint16_t* y, long n, hipStream_t st);
 void bigdl_spin_us(double us, int* done, hipStream_t st);
+void bigdl_dgrad_fill(uint16_t* out, const uint16_t* add, long npix, int H, int W, int C, int sh, int sw, unsigned mask,
+                      hipStream_t st);
 void bigdl_relu_bwd(const uint16_t* dy, const uint16_t* y, uint16_t* dx, long n, hipStream_t st);
 void bigdl_add_bf16(const uint16_t* a, const uint16_t* b, uint16_t* y, long n, hipStream_t st);
 void bigdl_nchw_f32_to_nhwc_bf16(const float* x, uint16_t* y, int N, int C, int H, int W, int Cp,
