@@ -305,10 +305,17 @@ class _LSTMSeq(torch.autograd.Function):
             # weight-gradient GEMM after the backward sweep
             h16 = xg.new_empty(T + 1, B, H, dtype=torch.bfloat16)
             C.cast_f32_bf16(h0.contiguous(), h16[0])
-            c_prev = c0.contiguous()
-            for t in range(T):
-                C.lstm_fwd_step(W16, h16[t], xg[:, t], c_prev, cs[t], out[:, t], h16[t + 1], acts[t])
-                c_prev = cs[t]
+            ctx.seq = bool(C.lstm_seq_supported(B, H))
+            if ctx.seq:
+                # whole sequence in ONE persistent launch (csrc/lstm_seq.hip): W resident in VGPRs, per-step
+                # state exchange inside each XCD's batch group
+                sync = torch.empty(C.lstm_seq_sync_words(), dtype=torch.int32, device=xg.device)
+                C.lstm_seq_fwd(W16, xg, c0.contiguous(), h16, out, cs, acts, sync)
+            else:
+                c_prev = c0.contiguous()
+                for t in range(T):
+                    C.lstm_fwd_step(W16, h16[t], xg[:, t], c_prev, cs[t], out[:, t], h16[t + 1], acts[t])
+                    c_prev = cs[t]
             ctx.save_for_backward(h0, c0, U, out, cs, acts, h16, W16)
             ctx.fused = True
             return out, out[:, -1].clone(), cs[-1].clone()
@@ -333,6 +340,19 @@ class _LSTMSeq(torch.autograd.Function):
         B, T, H = out.shape
         C = ops.native.get()
         dout = dout.contiguous() if dout is not None else None
+        if ctx.seq:
+            # one persistent launch for the whole backward sweep, dh0 = dg_0 U included (no transposed copy of U)
+            dxg = out.new_empty(B, T, 4 * H)
+            dg16 = out.new_empty(T, B, 4 * H, dtype=torch.bfloat16)
+            dc0, dh0 = out.new_empty(B, H), out.new_empty(B, H)
+            sync = torch.empty(C.lstm_seq_sync_words(), dtype=torch.int32, device=out.device)
+            C.lstm_seq_bwd(W16, dout, dhT.contiguous() if dhT is not None else None,
+                           dcT.contiguous() if dcT is not None else None, acts, cs, c0.contiguous(), dg16, dxg, dc0,
+                           dh0, sync)
+            dU = out.new_empty(4 * H, H, 1, 1)
+            C.fill_bytes(dU, 0)
+            cv.conv2d_wgrad(dg16.view(T * B, 4 * H, 1, 1), h16[:T].view(T * B, H, 1, 1), dU, None, (1, 1), (0, 0))
+            return dxg, dh0, dc0, dU.view(4 * H, H)
         WT16 = cv.transpose_w(W16.view(4 * H, H, 1, 1)).view(H, 4 * H)
         dxg = out.new_empty(B, T, 4 * H)
         dg16 = out.new_empty(T, B, 4 * H, dtype=torch.bfloat16)      # time-major: rows t*B + b

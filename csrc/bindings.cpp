@@ -857,6 +857,45 @@ void lstm_bwd_step(const Tensor& WT16, const OptT& dg16_next, const OptT& dout, 
                       ldg, mbf(dg16_out, "dg16_out"), B, H, stream());
 }
 
+// Whole-sequence persistent LSTM: xg [B, T, 4H] f32, h16 [T + 1, B, H] bf16 (h16[0] = h0), out [B, T, H],
+// cs [T, B, H], acts [T, B, 4H]; sync = int32 workspace of lstm_seq_sync_words() words (zeroed by the launch).
+bool lstm_seq_supported(int64_t B, int64_t H) { return bigdl_lstm_seq_supported((int)B, (int)H) != 0; }
+int64_t lstm_seq_sync_words() { return bigdl_lstm_seq_sync_words(); }
+void lstm_seq_fwd(const Tensor& W16, const Tensor& xg, const OptT& c0, const Tensor& h16, const Tensor& out,
+                  const Tensor& cs, const Tensor& acts, const Tensor& sync) {
+  TORCH_CHECK(xg.dim() == 3 && xg.is_contiguous(), "lstm_seq_fwd: xg must be [B, T, 4H] contiguous");
+  const int64_t B = xg.size(0), T = xg.size(1), H = W16.size(1);
+  TORCH_CHECK(W16.size(0) == 4 * H && W16.is_contiguous() && xg.size(2) == 4 * H, "lstm_seq_fwd: W16 [4H, H]");
+  TORCH_CHECK(h16.is_contiguous() && h16.numel() == (T + 1) * B * H, "lstm_seq_fwd: h16 [T + 1, B, H]");
+  TORCH_CHECK(out.is_contiguous() && out.numel() == B * T * H && cs.is_contiguous() && cs.numel() == T * B * H &&
+              acts.is_contiguous() && acts.numel() == T * B * 4 * H, "lstm_seq_fwd: out / cs / acts");
+  TORCH_CHECK(sync.scalar_type() == at::kInt && sync.numel() >= bigdl_lstm_seq_sync_words(), "lstm_seq_fwd: sync");
+  if (c0 && c0->defined()) TORCH_CHECK(c0->is_contiguous() && c0->numel() == B * H, "lstm_seq_fwd: c0");
+  TORCH_CHECK(bigdl_lstm_seq_fwd(cbf(W16, "W16"), cf(xg, "xg"), ocf(c0, "c0"), mbf(h16, "h16"), mf(out, "out"),
+                                 mf(cs, "cs"), mf(acts, "acts"), reinterpret_cast<unsigned*>(sync.data_ptr<int>()),
+                                 (int)B, (int)H, (int)T, stream()) == 0, "lstm_seq_fwd: unsupported shape");
+}
+void lstm_seq_bwd(const Tensor& W16, const OptT& dout, const OptT& dhT, const OptT& dcT, const Tensor& acts,
+                  const Tensor& cs, const OptT& c0, const Tensor& dg16, const Tensor& dxg, const Tensor& dc0,
+                  const Tensor& dh0, const Tensor& sync) {
+  TORCH_CHECK(dxg.dim() == 3 && dxg.is_contiguous(), "lstm_seq_bwd: dxg must be [B, T, 4H] contiguous");
+  const int64_t B = dxg.size(0), T = dxg.size(1), H = W16.size(1);
+  TORCH_CHECK(W16.size(0) == 4 * H && W16.is_contiguous() && dxg.size(2) == 4 * H, "lstm_seq_bwd: W16 [4H, H]");
+  TORCH_CHECK(acts.is_contiguous() && acts.numel() == T * B * 4 * H && cs.is_contiguous() && cs.numel() == T * B * H,
+              "lstm_seq_bwd: acts / cs");
+  TORCH_CHECK(dg16.is_contiguous() && dg16.numel() == T * B * 4 * H && dc0.is_contiguous() && dc0.numel() == B * H &&
+              dh0.is_contiguous() && dh0.numel() == B * H, "lstm_seq_bwd: dg16 / dc0 / dh0");
+  TORCH_CHECK(sync.scalar_type() == at::kInt && sync.numel() >= bigdl_lstm_seq_sync_words(), "lstm_seq_bwd: sync");
+  if (dout && dout->defined()) TORCH_CHECK(dout->is_contiguous() && dout->numel() == B * T * H, "lstm_seq_bwd: dout");
+  if (dhT && dhT->defined()) TORCH_CHECK(dhT->is_contiguous() && dhT->numel() == B * H, "lstm_seq_bwd: dhT");
+  if (dcT && dcT->defined()) TORCH_CHECK(dcT->is_contiguous() && dcT->numel() == B * H, "lstm_seq_bwd: dcT");
+  if (c0 && c0->defined()) TORCH_CHECK(c0->is_contiguous() && c0->numel() == B * H, "lstm_seq_bwd: c0");
+  TORCH_CHECK(bigdl_lstm_seq_bwd(cbf(W16, "W16"), ocf(dout, "dout"), ocf(dhT, "dhT"), ocf(dcT, "dcT"), cf(acts, "acts"),
+                                 cf(cs, "cs"), ocf(c0, "c0"), mbf(dg16, "dg16"), mf(dxg, "dxg"), mf(dc0, "dc0"),
+                                 mf(dh0, "dh0"), reinterpret_cast<unsigned*>(sync.data_ptr<int>()), (int)B, (int)H,
+                                 (int)T, stream()) == 0, "lstm_seq_bwd: unsupported shape");
+}
+
 void layernorm_fwd(const Tensor& x, const OptT& g, const OptT& b, const Tensor& y, const Tensor& mean,
                    const Tensor& rstd, double eps) {
   TORCH_CHECK(x.is_contiguous() && y.is_contiguous() && x.numel() == y.numel() && x.dim() >= 1, "layernorm_fwd: x/y");
@@ -1091,6 +1130,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("f32_to_bf16_rtz", &f32_to_bf16_rtz);
   m.def("lstm_fwd_step", &lstm_fwd_step);
   m.def("lstm_bwd_step", &lstm_bwd_step);
+  m.def("lstm_seq_supported", &lstm_seq_supported);
+  m.def("set_lstm_seq", &bigdl_set_lstm_seq);
+  m.def("lstm_seq_sync_words", &lstm_seq_sync_words);
+  m.def("lstm_seq_fwd", &lstm_seq_fwd);
+  m.def("lstm_seq_bwd", &lstm_seq_bwd);
   m.def("colsum_bf16", &colsum_bf16);
   m.def("layernorm_fwd", &layernorm_fwd);
   m.def("attn_fwd", &attn_fwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("bias"), py::arg("H"),
@@ -1110,6 +1154,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("get_conv_impl", &bigdl_get_conv_impl);
   m.def("set_conv_g4", &bigdl_set_conv_g4);
   m.def("set_conv_p8", &bigdl_set_conv_p8);
+  m.def("set_wgrad_p8", &bigdl_set_wgrad_p8);
   m.def("get_conv_g4", &bigdl_get_conv_g4);
   m.def("set_wgrad_g3", &bigdl_set_wgrad_g3);
   m.def("get_wgrad_g3", &bigdl_get_wgrad_g3);

@@ -1405,6 +1405,235 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Weight gradient on the phase-interleaved 256 x 256 tile of conv_nt_p8_kernel: dW[n][kk] = sum_p dy[p][n] x[p][kk]
+// (kk = (r, s, c) of KRSC, x gathered im2col-style), reduction over output pixels p in K-steps of 64, split over
+// pixel ranges per blockIdx.y (fp32 partials [split][Ncol][Kdim] summed by wgrad_reduce_kernel; one split adds into
+// dw directly; the bias gradient goes out as fp32 atomics, one per column and split). 8 waves = 2 kk-halves x 4
+// n-quarters, 128 kk x 64 n per wave, MFMA A = x fragment (rows kk), B = dy fragment (columns n), so a lane ends up
+// with 4 consecutive kk of one n: 16-byte stores along dw's rows.
+// LDS: per K-step four 16 KB pieces of 64 pixel rows x 128 columns (256 B rows): P0 / P2 = x columns of
+// kk-quadrant 0 / 1 of both kk-halves, P1 / P3 = dy columns of n-quadrant 0 / 1 of the four n-quarters. The
+// fragments are read down the pixel rows with the transposing ds_read_b64_tr_b16 (T10); 16-byte chunk k of row r
+// sits at slot k ^ f(r), f(r) = 2 * ((r & 3) | ((r >> 3) & 1) << 2), which keeps every 32-lane transposed read
+// conflict-free; the DMA applies f on the source side (constant per lane and wave, so each lane's tap / channel /
+// output channel is fixed for the whole kernel). Phases, pieces, waits and the wave-group stagger are exactly those
+// of conv_nt_p8_kernel (see there for the hazard argument).
+__device__ __forceinline__ int p8w_f(int r) { return 2 * ((r & 3) | (((r >> 3) & 1) << 2)); }
+typedef __bf16 v2bf __attribute__((ext_vector_type(2)));
+typedef int v4i_t __attribute__((ext_vector_type(4)));
+
+__global__ __launch_bounds__(512, 2) void conv_wgrad_p8_kernel(WgradArgs a) {
+  constexpr int PIX = 64;                          // pixels per K-step
+  constexpr int PC = 128;                          // columns per piece
+  constexpr int PIECE = PIX * PC;                  // 16 KB
+  constexpr int BUF = 4 * PIECE;
+  __shared__ __attribute__((aligned(1024))) bf16_t lds[2 * BUF];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;         // wave tile: kk rows wm * 128 .., n columns wn * 64 ..
+  const int tiles_n = (a.Ncol + 255) / 256, tiles_k = (a.Kdim + 255) / 256;
+  const int ntile = tiles_n * tiles_k;
+  const int t = xcd_remap(blockIdx.x, ntile);
+  const int tk = t / tiles_n, tn = t % tiles_n;
+  const int n0 = tn * 256, k0 = tk * 256;
+  const int mbeg = blockIdx.y * a.m_per_split;
+  const int mend = min(a.M, mbeg + a.m_per_split);
+  const int nk = mend > mbeg ? (mend - mbeg + PIX - 1) / PIX : 0;
+
+  // DMA geometry: instruction j of wave w fills piece rows (j * 8 + w) * 4 .. +4 (4 rows x 256 B); lane -> row
+  // + (lane >> 4), slot lane & 15, which holds chunk (lane & 15) ^ f(row), f constant per lane and wave
+  const int fr = p8w_f((lane >> 4) | (((wave >> 1) & 1) << 3));
+  const int chunk = (lane & 15) ^ fr;              // this lane's source chunk (8 columns) of every piece
+  // A pieces (x): tile column kk of piece column pc = chunk * 8 is (pc >> 6) * 128 + q * 64 + (pc & 63)
+  int xr[2], xs[2], xc[2];
+  bool xv[2];
+  const int SC = a.S * a.Cs;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int pc = chunk * 8;
+    const int kk = k0 + (pc >> 6) * 128 + q * 64 + (pc & 63);
+    xv[q] = kk < a.Kdim;
+    const int k = xv[q] ? kk : 0;
+    xr[q] = k / SC;
+    const int rem = k - xr[q] * SC;
+    xs[q] = rem / a.Cs;
+    xc[q] = rem - xs[q] * a.Cs;
+  }
+  // B pieces (dy): tile column n of piece column pc is (pc >> 5) * 64 + q * 32 + (pc & 31)
+  int dn[2];
+  bool dv[2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int pc = chunk * 8;
+    dn[q] = n0 + (pc >> 5) * 64 + q * 32 + (pc & 31);
+    dv[q] = dn[q] < a.Ncol;
+  }
+  const int ohw = a.OH * a.OW;
+
+  // piece P (0 x q0, 1 dy q0, 2 x q1, 3 dy q1) of K-step kt into buffer buf: 2 DMA instructions per thread
+  auto issue = [&](int kt, int buf, int P) {
+    bf16_t* base = lds + buf * BUF + P * PIECE;
+    const int q = P >> 1;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int row = (j * 8 + wave) * 4 + (lane >> 4);
+      const int m = mbeg + kt * PIX + row;
+      const bf16_t* src = g_zero_granule;
+      if (m < mend) {
+        if ((P & 1) == 0) {
+          if (xv[q]) {
+            const int nb = m / ohw, rem = m - nb * ohw;
+            const int oh = rem / a.OW, ow = rem - oh * a.OW;
+            const int ih = oh * a.sh - a.ph + xr[q] * a.dh, iw = ow * a.sw - a.pw + xs[q] * a.dwl;
+            if ((unsigned)ih < (unsigned)a.Hs && (unsigned)iw < (unsigned)a.Ws)
+              src = a.src + (unsigned)(((nb * a.Hs + ih) * a.Ws + iw) * a.Cs + xc[q]);
+          }
+        } else if (dv[q]) {
+          src = a.dy + (unsigned)(m * a.ldy + dn[q]);
+        }
+      }
+      glds16(src, (LDS_PTR(void))(base + (j * 8 + wave) * 4 * PC));
+    }
+  };
+  // transposed fragment reads: lane 4q'+p of 16-lane group g supplies row 32 kh + 8 g + q' (+4), columns c0 + 4p
+  const int G = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;
+  auto tr = [&](const bf16_t* P, int row, int col) -> v4s {
+    const int off = row * PC + (((col >> 3) ^ p8w_f(row)) << 3) + (col & 7);
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_PTR(v4s))(P + off));
+  };
+  auto frag = [&](const bf16_t* P, int kh, int c0) -> v8s {
+    const int r = 32 * kh + 8 * G + qq;
+    const v4s lo = tr(P, r, c0 + 4 * pp), hi = tr(P, r + 4, c0 + 4 * pp);
+    return v8s{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  };
+
+  v4f acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+  v8s fa[4][2], fb[4][2];
+  auto quad = [&](int ib, int jb) {
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[ib + i][jb + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][kh], fb[jb + j][kh], acc[ib + i][jb + j], 0, 0, 0);
+  };
+  auto read_a = [&](const bf16_t* P) {            // x: this wave's kk quadrant = piece columns wm * 64 + 16 i
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      fa[i][0] = frag(P, 0, wm * 64 + i * 16);
+      fa[i][1] = frag(P, 1, wm * 64 + i * 16);
+    }
+  };
+  auto read_b = [&](const bf16_t* P, int jb) {    // dy: this wave's n quadrant = piece columns wn * 32 + 16 j
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      fb[jb + j][0] = frag(P, 0, wn * 32 + j * 16);
+      fb[jb + j][1] = frag(P, 1, wn * 32 + j * 16);
+    }
+  };
+  // bias gradient: the kk-tile-0 workgroups also sum their dy fragments over the pixels, wave half wm taking the
+  // n columns of fb[2 wm], fb[2 wm + 1] (v_dot2 against ones: 4 VALU per fragment beside 16 MFMA)
+  const bool do_bias = a.dbias != nullptr && tk == 0;
+  float bsum[2] = {0.f, 0.f};
+  auto bias = [&](int jb) {
+    const v2bf one = {(__bf16)1.0f, (__bf16)1.0f};
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh) {
+        const v4i_t u = __builtin_bit_cast(v4i_t, fb[jb + j][kh]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) bsum[j] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(v2bf, u[e]), one, bsum[j], false);
+      }
+  };
+  auto compute = [&](int ib, int jb, bool sum_bias) {
+    __builtin_amdgcn_s_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+    quad(ib, jb);
+    if (sum_bias) bias(jb);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+  };
+
+  if (nk > 0) {
+    issue(0, 0, 0); issue(0, 0, 1); issue(0, 0, 3); issue(0, 0, 2);
+  }
+  if (nk > 1) {
+    issue(1, 1, 0); issue(1, 1, 1);
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  if (wm == 1) __builtin_amdgcn_s_barrier();     // stagger
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    const bf16_t* L = lds + cur * BUF;
+    const bool n1 = kt + 1 < nk, n2 = kt + 2 < nk;
+    if (n1) issue(kt + 1, cur ^ 1, 3);
+    read_a(L); read_b(L + PIECE, 0);
+    if (n1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    compute(0, 0, do_bias && wm == 0);
+    if (n1) issue(kt + 1, cur ^ 1, 2);
+    read_b(L + 3 * PIECE, 2);
+    if (n1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    compute(0, 2, do_bias && wm == 1);
+    if (n2) issue(kt + 2, cur, 0);
+    read_a(L + 2 * PIECE);
+    compute(4, 2, false);
+    if (n2) issue(kt + 2, cur, 1);
+    if (n2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (n1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    compute(4, 0, false);
+  }
+  if (wm == 0) __builtin_amdgcn_s_barrier();     // balance the stagger
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  // acc[i][j] = D[kk][n]: kk = k0 + wm * 128 + 16 i + 4 (lane >> 4) + e (quadrant rows: i < 4 -> q0, else q1),
+  // n = n0 + wn * 64 + 16 j + (lane & 15)
+  if (do_bias) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      float v = bsum[j];
+      v += __shfl_xor(v, 16);
+      v += __shfl_xor(v, 32);
+      const int n = n0 + wn * 64 + (2 * wm + j) * 16 + lane;
+      if (lane < 16 && n < a.Ncol) unsafeAtomicAdd(a.dbias + n, v);
+    }
+  }
+  float* part = a.splits > 1 ? a.ws + (size_t)blockIdx.y * a.Ncol * a.Kdim : nullptr;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int kb = k0 + wm * 128 + i * 16 + 4 * (lane >> 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = n0 + wn * 64 + j * 16 + (lane & 15);
+      if (n < a.Ncol && kb < a.Kdim) {
+        if (part) {
+          *reinterpret_cast<v4f*>(part + (size_t)n * a.Kdim + kb) = acc[i][j];
+        } else {
+          float* o = a.dw + (size_t)n * a.Kdim + kb;   // a view into the flat gradient: maybe only 4-byte aligned
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] += acc[i][j][e];
+        }
+      }
+    }
+  }
+}
+
 // wt[c][rs][k] = w[k][rs][c]: per tap, a [K][C] -> [C][K] transpose through a 32 x 32 LDS tile (coalesced
 // reads along c and writes along k, +1 column pad against bank conflicts). Small tiles keep >= 4 workgroups on
 // the 64 x 64 layers: most of the 53 per-step launches are latency-, not bandwidth-bound.
@@ -2301,7 +2530,9 @@ extern "C" {
 
 void bigdl_set_conv_impl(int impl) { g_conv_impl = impl; }
 void bigdl_set_conv_g4(int v) { g_conv_g4 = v; }
+int g_wgrad_p8 = -1;
 void bigdl_set_conv_p8(int v) { g_conv_p8 = v; }
+void bigdl_set_wgrad_p8(int v) { g_wgrad_p8 = v; }
 int bigdl_get_conv_g4() { return g4_pick(); }
 int bigdl_get_conv_impl() { return conv_impl(); }
 
@@ -2425,7 +2656,35 @@ static bool wgrad_g3() {
 void bigdl_set_wgrad_g3(int v) { g_wgrad_g3 = v; }
 int bigdl_get_wgrad_g3() { return wgrad_g3() ? 1 : 0; }
 
+// BIGDL_WGRAD_P8: 1 (default) = conv_wgrad_p8_kernel for layers with Ncol >= 256 and Kdim >= 256; 0 = off.
+// Returns its pixel split (>= 1) or 0 when it does not apply; sets m_per_split.
+static int p8w_pick(WgradArgs* a) {
+  if (g_wgrad_p8 < 0) {
+    const char* e = getenv("BIGDL_WGRAD_P8");
+    g_wgrad_p8 = e ? atoi(e) : 1;
+  }
+  if (!g_wgrad_p8 || conv_impl() < 1 || a->Ncol < 256 || a->Kdim < 256 || (a->Cs % 8) ||
+      (a->Ncol % 8) || (a->Kdim % 8) || a->M <= 0)
+    return 0;
+  const long tiles = (long)((a->Ncol + 255) / 256) * ((a->Kdim + 255) / 256);
+  const long steps = (a->M + 63) / 64;
+  long splits = (256 + tiles - 1) / tiles;                         // one workgroup per CU
+  splits = std::min(splits, std::max(1L, steps / 8));              // >= 8 pixel steps per split
+  const long cap = (96L << 20) / ((long)a->Ncol * a->Kdim * 4);    // <= 96 MB of fp32 partials
+  splits = std::max(1L, std::min(splits, std::max(1L, cap)));
+  long mps = (a->M + splits - 1) / splits;
+  mps = (mps + 63) / 64 * 64;
+  splits = (a->M + mps - 1) / mps;
+  a->m_per_split = (int)mps;
+  return (int)splits;
+}
+
 long bigdl_conv_wgrad_plan(WgradArgs* a) {
+  const int p8w = p8w_pick(a);
+  if (p8w > 0) {
+    a->splits = p8w;
+    return p8w > 1 ? (long)p8w * a->Ncol * a->Kdim : 0;
+  }
   const int tiles = ((a->Ncol + WT - 1) / WT) * ((a->Kdim + WT - 1) / WT);
   if (conv_impl() < 1 || wgrad_prefers_atomic(a)) { a->splits = 0; return 0; }
   // workspace split-K: ~2 workgroups per CU (512; the kernel runs beside the dgrad chain on the side stream, so
@@ -2447,6 +2706,24 @@ long bigdl_conv_wgrad_plan(WgradArgs* a) {
 int bigdl_conv_wgrad(const WgradArgs* a_in, hipStream_t st) {
   WgradArgs a = *a_in;
   if (a.Cs % 8 != 0 || a.Ncol % 8 != 0 || a.Kdim % 8 != 0) return -1;
+  {
+    WgradArgs b = a;
+    const int p8w = p8w_pick(&b);
+    if (p8w > 0 && p8w == a.splits && (p8w == 1 || a.ws != nullptr)) {
+      b.splits = p8w;
+      b.ws = a.ws;
+      const int tiles = ((a.Ncol + 255) / 256) * ((a.Kdim + 255) / 256);
+      conv_wgrad_p8_kernel<<<dim3(tiles, p8w), dim3(512), 0, st>>>(b);
+      if (p8w > 1) {
+        const long n4 = (long)a.Ncol * a.Kdim / 4;
+        const int blocks = (int)std::min<long>((n4 + 255) / 256, 8192);
+        if ((reinterpret_cast<uintptr_t>(a.dw) & 15) == 0) wgrad_reduce_kernel<true><<<dim3(blocks, 1), 256, 0, st>>>(a.ws, a.dw, n4, p8w);
+        else wgrad_reduce_kernel<false><<<dim3(blocks, 1), 256, 0, st>>>(a.ws, a.dw, n4, p8w);
+      }
+      HIP_LAUNCH_CHECK();
+      return 0;
+    }
+  }
   if (a.ws != nullptr && a.splits > 1 && conv_impl() >= 1) {
     const int tiles = ((a.Ncol + WT - 1) / WT) * ((a.Kdim + WT - 1) / WT);
     const int spad = (a.splits + 7) / 8 * 8;

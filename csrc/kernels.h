@@ -183,6 +183,7 @@ void bigdl_set_conv_impl(int impl);
 int bigdl_get_conv_impl();
 void bigdl_set_conv_g4(int v);
 void bigdl_set_conv_p8(int v);
+void bigdl_set_wgrad_p8(int v);
 int bigdl_get_conv_g4();
 void bigdl_set_wgrad_g3(int v);
 int bigdl_get_wgrad_g3();
@@ -239,6 +240,15 @@ int bigdl_lstm_fwd_step(const uint16_t* W16, const uint16_t* h16_prev, const flo
 int bigdl_lstm_bwd_step(const uint16_t* WT16, const uint16_t* dg16_next, const float* dout, long ldd,
                         const float* dh_ext, const float* acts, long lda, const float* c_prev, const float* c_t,
                         float* dc, float* dg_out, long ldg, uint16_t* dg16_out, int B, int H, hipStream_t st);
+// Whole-sequence persistent LSTM (csrc/lstm_seq.hip): one launch per direction, W resident in VGPRs.
+int bigdl_lstm_seq_supported(int B, int H);
+void bigdl_set_lstm_seq(int v);
+int bigdl_lstm_seq_sync_words();
+int bigdl_lstm_seq_fwd(const uint16_t* W16, const float* xg, const float* c0, uint16_t* h16, float* out, float* cs,
+                       float* acts, unsigned* sync, int B, int H, int T, hipStream_t st);
+int bigdl_lstm_seq_bwd(const uint16_t* W16, const float* dout, const float* dhT, const float* dcT, const float* acts,
+                       const float* cs, const float* c0, uint16_t* dg16, float* dxg, float* dc0, float* dh0,
+                       unsigned* sync, int B, int H, int T, hipStream_t st);
 
 // Fused GRU steps (csrc/gru.hip). mode: 0 fwd r/z, 1 fwd n + h, 2 bwd dh_t + dn/dz, 3 bwd dr + r-path, 4 bwd dh_0.
 // GEMM D[b][n] = sum_k A[b][k] W[n][k] (A rows lda apart; W [N][K] contiguous); row strides of the fp32 per-step

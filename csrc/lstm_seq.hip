@@ -1,0 +1,380 @@
+// Whole-sequence LSTM recurrence as ONE persistent launch per direction (gfx950).
+//
+// Reference: the fused whole-sequence MKL-DNN RNN primitive S/nn/mkldnn/RNN.scala:167-320 (forward + backward over
+// all time steps in one call), cell math S/nn/LSTM.scala:77-185 (gates i, g, f, o; c' = f*c + i*g; h' = o*tanh(c')).
+//
+// MI355X design. The per-step kernels of lstm.hip pay, every time step, a kernel boundary plus a re-read of their
+// weight slice from L2 and of the previous state from other XCDs. Here the launch holds the recurrent weight for the
+// whole sequence and only the state crosses workgroups:
+//  * grid = 8 batch groups x M = H / 32 workgroups (256 for H = 1024: one 512-thread workgroup per CU). Group g =
+//    blockIdx % 8 owns batch rows [g * Bg, (g + 1) * Bg) (Bg <= 16): under the round-robin dispatch its workgroups sit
+//    on one XCD, so the per-step exchange is L2-local (placement only changes speed, never correctness: every
+//    hand-off is an agent-scope protocol).
+//  * member m owns hidden units [32 m, 32 m + 32); each of its 8 waves keeps its slice of W (16 gate rows x H for the
+//    forward, 16 units x one gate block of W^T for the backward) in VGPRs as MFMA A fragments: KS = H / 32 fragments,
+//    128 VGPRs at H = 1024, loaded once.
+//  * per step a workgroup waits for its group's counter, pulls the group's previous state (bf16, 16 rows) into LDS
+//    with write-through (sc1) 16-byte loads, runs KS MFMAs per wave on two accumulator chains, applies the cell in
+//    registers, publishes its 16 x 32 slice of the new state with sc1 16-byte stores, drains them (vmcnt(0)) and adds
+//    1 to the group counter (agent-scope atomic). This is the write-through hand-off of the CDNA4 programming guide's
+//    inter-workgroup rule: every handed-off byte is stored sc1 and drained before the counter add, every load of it is
+//    an sc1 load to registers behind the poll, and no other load reads bytes written in the launch.
+//  * counters are zeroed by a memset ahead of every launch (graph-replay safe); every spin is bounded (0.5 s of the
+//    100 MHz wall clock): on timeout the workgroup sets the error word, poisons its outputs with NaN and leaves.
+// Forward per step: gates = W h_{t-1} (+ xg, the input projection computed beforehand as one GEMM), c and h in
+// fp32, h16 bf16 hand-off (also the B operand of the weight-gradient GEMM). Backward per step: dh = dout + dg_{t+1} W
+// (K = 4H split over the 4 gate blocks = 4 waves per unit tile, partials summed in LDS), the cell backward per
+// (unit, batch) thread, dg_t as fp32 (input-projection gradients) and bf16 (hand-off + weight gradient); one extra
+// round after t = 0 produces dh0 = dg_0 W, so no transposed weight copy is ever made.
+#include "common.h"
+#include "kernels.h"
+
+namespace {
+
+typedef __attribute__((address_space(1))) unsigned gu32;
+
+constexpr int NGRP = 8;                          // batch groups (= XCDs)
+constexpr int CNT_STRIDE = 32;                   // one 128-byte line per group counter
+constexpr unsigned long long SPIN_TICKS = 50000000ull;   // 0.5 s at 100 MHz
+
+struct LstmSeqArgs {
+  const bf16_t* W16;       // [4H][H] gate blocks i, g, f, o
+  const float* xg;         // fwd: [B][T][4H] gate pre-activations from the input projection
+  const float* c0;         // [B][H] or null
+  const float* dout;       // bwd: [B][T][H] or null
+  const float* dhT;        // bwd: [B][H] or null
+  const float* dcT;        // bwd: [B][H] or null
+  bf16_t* h16;             // [T + 1][B][H]: h_{-1} .. h_{T-1}
+  float* out;              // fwd: [B][T][H]
+  float* cs;               // [T][B][H]
+  float* acts;             // [T][B][4H]
+  bf16_t* dg16;            // bwd: [T][B][4H]
+  float* dxg;              // bwd: [B][T][4H]
+  float* dc0;              // bwd: [B][H] (dc flowing into c0)
+  float* dh0;              // bwd: [B][H]
+  unsigned* sync;          // NGRP counters (CNT_STRIDE apart) + error word
+  int B, H, T, Bg;
+};
+
+__device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + __expf(-x)); }
+__device__ __forceinline__ float tanh_f(float x) {
+  const float e = __expf(-2.f * fabsf(x));
+  const float t = (1.f - e) / (1.f + e);
+  return x < 0.f ? -t : t;
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, int bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, bytes, 0x00020000);
+}
+// 16-byte write-through load / store (aux 16 = sc1)
+__device__ __forceinline__ v4u ld_sc1(__amdgpu_buffer_rsrc_t r, int off) {
+  return __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16));
+}
+__device__ __forceinline__ void st_sc1(v4u v, __amdgpu_buffer_rsrc_t r, int off) {
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 16);
+}
+
+// One lane polls the group counter (relaxed agent-scope load = global_load sc1) until it reaches target.
+__device__ __noinline__ bool wait_count(unsigned* cnt, unsigned target, unsigned* err) {
+  const unsigned long long t0 = wall_clock64();
+  while (__hip_atomic_load((gu32*)cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+    __builtin_amdgcn_s_sleep(1);
+    if (wall_clock64() - t0 > SPIN_TICKS) {
+      __hip_atomic_store((gu32*)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+  }
+  return true;
+}
+
+// Wave 0 polls, the verdict goes to every wave through LDS. Returns false when the group timed out.
+__device__ __forceinline__ bool group_wait(unsigned* cnt, unsigned target, unsigned* err, int* flag, int wave,
+                                           int lane) {
+  if (wave == 0 && lane == 0) *flag = wait_count(cnt, target, err) ? 0 : 1;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keeps the sc1 state loads below the poll
+  __syncthreads();
+  return *flag == 0;
+}
+
+__device__ __forceinline__ void signal(unsigned* cnt) {
+  __hip_atomic_fetch_add((gu32*)cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ------------------------------------------------------------------------------------------------ forward
+template <int KS>
+__global__ __launch_bounds__(512, 1) void lstm_seq_fwd_kernel(LstmSeqArgs a) {
+  constexpr int H = KS * 32;
+  constexpr int HP = H + 8;                      // LDS row pitch: consecutive batch rows 4 banks apart
+  constexpr int CH = 16 * H / 8 / 512;           // 16-byte chunks of h_{t-1} per thread
+  __shared__ __attribute__((aligned(16))) bf16_t hs[16 * HP];
+  __shared__ __attribute__((aligned(16))) bf16_t hst[16 * 32];   // this workgroup's h_t slice [batch][unit]
+  __shared__ int flag;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = blockIdx.x % NGRP, m = blockIdx.x / NGRP, M = gridDim.x / NGRP;
+  const int b_lo = g * a.Bg, nb = min(a.Bg, a.B - b_lo);
+  if (nb <= 0) return;                            // no rows: nobody waits on this group
+  const int G = lane >> 4, col = lane & 15;
+  const int ub = m * 32 + wave * 4;               // the wave's 4 units; A row r = unit (r >> 2), gate (r & 3)
+  const int j = ub + G;                           // this lane's unit in D (rows 4G .. 4G + 3 = its 4 gates)
+  const bool live = col < nb;
+  const int b = b_lo + (live ? col : 0);
+  v8s wa[KS];
+  {
+    const bf16_t* wp = a.W16 + (size_t)((col & 3) * H + ub + (col >> 2)) * H + 8 * G;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) wa[s] = *reinterpret_cast<const v8s*>(wp + s * 32);
+  }
+  float c = a.c0 ? a.c0[(size_t)b * H + j] : 0.f;
+  unsigned* cnt = a.sync + g * CNT_STRIDE;
+  unsigned* err = a.sync + NGRP * CNT_STRIDE;
+  const size_t slab = (size_t)a.B * H;            // one time step of h16
+
+  for (int t = 0; t < a.T; ++t) {
+    const float* xp = a.xg + ((size_t)b * a.T + t) * 4 * H + j;
+    const float x0 = xp[0], x1 = xp[H], x2 = xp[2 * H], x3 = xp[3 * H];
+    if (t > 0 && !group_wait(cnt, (unsigned)(M * t), err, &flag, wave, lane)) {
+      if (live) for (int u = t; u < a.T; ++u) a.out[((size_t)b * a.T + u) * H + j] = __builtin_nanf("");
+      return;
+    }
+    {   // h_{t-1} of the group's rows -> LDS (rows past the group read as zero)
+      const __amdgpu_buffer_rsrc_t r = rsrc(a.h16 + t * slab + (size_t)b_lo * H, nb * H * 2);
+      v4u v[CH];
+#pragma unroll
+      for (int i = 0; i < CH; ++i) {
+        const int q = tid + 512 * i, row = q / (H / 8), c8 = q % (H / 8);
+        v[i] = ld_sc1(r, (row * H + c8 * 8) * 2);
+      }
+#pragma unroll
+      for (int i = 0; i < CH; ++i) {
+        const int q = tid + 512 * i, row = q / (H / 8), c8 = q % (H / 8);
+        *reinterpret_cast<v4u*>(hs + row * HP + c8 * 8) = v[i];
+      }
+    }
+    __syncthreads();
+    v4f acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+    const bf16_t* hb = hs + col * HP + 8 * G;
+#pragma unroll
+    for (int s = 0; s < KS; s += 2) {
+      if ((s & 7) == 0) asm volatile("" ::: "memory");     // <= 8 fragment reads in flight (VGPR budget)
+      const v8s h0 = *reinterpret_cast<const v8s*>(hb + s * 32), h1 = *reinterpret_cast<const v8s*>(hb + (s + 1) * 32);
+      acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[s], h0, acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[s + 1], h1, acc1, 0, 0, 0);
+    }
+    const v4f gs = acc0 + acc1;
+    const float ig = sigm(gs[0] + x0), gg = tanh_f(gs[1] + x1), fg = sigm(gs[2] + x2), og = sigm(gs[3] + x3);
+    c = fg * c + ig * gg;
+    const float h = og * tanh_f(c);
+    if (live) {
+      a.out[((size_t)b * a.T + t) * H + j] = h;
+      a.cs[((size_t)t * a.B + b) * H + j] = c;
+      float* ap = a.acts + ((size_t)t * a.B + b) * 4 * H + j;
+      ap[0] = ig; ap[H] = gg; ap[2 * H] = fg; ap[3 * H] = og;
+    }
+    hst[col * 32 + wave * 4 + G] = f2bf(h);
+    __syncthreads();
+    if (wave == 0) {   // publish: 16 rows x 64 B, lane -> (row, 16-byte quarter); drained before the counter add
+      const int row = lane >> 2, qq = lane & 3;
+      if (row < nb) {
+        const __amdgpu_buffer_rsrc_t r = rsrc(a.h16 + (t + 1) * slab, (int)(slab * 2));
+        st_sc1(*reinterpret_cast<const v4u*>(hst + row * 32 + qq * 8), r, (int)(((b_lo + row) * H + m * 32 + qq * 8) * 2));
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0) signal(cnt);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------ backward
+// Wave w: unit tile ut = w & 1 (16 units), gate block q = w >> 1 (K chunk of H). A[unit][k] = W[q H + k][unit]
+// gathered once; B = dg_{t+1}[batch][q H + k] from LDS; D[unit][batch] partials summed over q in LDS.
+template <int KS>
+__global__ __launch_bounds__(512, 1) void lstm_seq_bwd_kernel(LstmSeqArgs a) {
+  constexpr int H = KS * 32, G4 = 4 * H;
+  constexpr int DP = G4 + 8;
+  constexpr int CH = 16 * G4 / 8 / 512;          // 16-byte chunks of dg_{t+1} per thread
+  __shared__ __attribute__((aligned(16))) bf16_t dgs[16 * DP];
+  __shared__ float red[4][32][17];               // [gate block][unit][batch]
+  __shared__ __attribute__((aligned(16))) bf16_t dst[16 * 4 * 32];   // dg_t slice [batch][gate][unit]
+  __shared__ int flag;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = blockIdx.x % NGRP, m = blockIdx.x / NGRP, M = gridDim.x / NGRP;
+  const int b_lo = g * a.Bg, nb = min(a.Bg, a.B - b_lo);
+  if (nb <= 0) return;
+  const int G = lane >> 4, col = lane & 15;
+  const int ut = wave & 1, q = wave >> 1;
+  v8s wa[KS];
+  {
+    const bf16_t* wp = a.W16 + (size_t)(q * H + 8 * G) * H + m * 32 + ut * 16 + col;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      v4u f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        f[i] = (unsigned)wp[(size_t)(s * 32 + 2 * i) * H] | ((unsigned)wp[(size_t)(s * 32 + 2 * i + 1) * H] << 16);
+      asm volatile("" : "+v"(f) :: "memory");   // packed per fragment: 8 loads in flight, 4 VGPRs kept
+      wa[s] = __builtin_bit_cast(v8s, f);
+    }
+  }
+  // cell thread: unit jj, batch bb
+  const int jj = tid >> 4, bb = tid & 15;
+  const int j = m * 32 + jj;
+  const bool live = bb < nb;
+  const int b = b_lo + (live ? bb : 0);
+  float dc = a.dcT ? a.dcT[(size_t)b * H + j] : 0.f;
+  unsigned* cnt = a.sync + g * CNT_STRIDE;
+  unsigned* err = a.sync + NGRP * CNT_STRIDE;
+  const size_t slab = (size_t)a.B * G4;          // one time step of dg16
+
+  // round i handles t = T-1-i; round T computes dh0 from dg_0
+  for (int i = 0; i <= a.T; ++i) {
+    const int t = a.T - 1 - i;
+    float dh = 0.f, ig = 0.f, gg = 0.f, fg = 0.f, og = 0.f, cv = 0.f, cp = 0.f;
+    if (t >= 0) {
+      if (a.dout) dh = a.dout[((size_t)b * a.T + t) * H + j];
+      if (i == 0 && a.dhT) dh += a.dhT[(size_t)b * H + j];
+      const float* ap = a.acts + ((size_t)t * a.B + b) * G4 + j;
+      ig = ap[0]; gg = ap[H]; fg = ap[2 * H]; og = ap[3 * H];
+      cv = a.cs[((size_t)t * a.B + b) * H + j];
+      cp = t > 0 ? a.cs[((size_t)(t - 1) * a.B + b) * H + j] : (a.c0 ? a.c0[(size_t)b * H + j] : 0.f);
+    }
+    if (i > 0) {
+      if (!group_wait(cnt, (unsigned)(M * i), err, &flag, wave, lane)) {
+        if (live) a.dh0[(size_t)b * H + j] = __builtin_nanf("");
+        return;
+      }
+      {   // dg_{t+1} of the group's rows -> LDS
+        const __amdgpu_buffer_rsrc_t r = rsrc(a.dg16 + (t + 1) * slab + (size_t)b_lo * G4, nb * G4 * 2);
+        constexpr int U = CH < 4 ? CH : 4;       // loads in flight per thread (VGPR budget: W takes 128)
+#pragma unroll
+        for (int h = 0; h < CH; h += U) {
+          v4u v[U];
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            const int qc = tid + 512 * (h + u), row = qc / (G4 / 8), c8 = qc % (G4 / 8);
+            v[u] = ld_sc1(r, (row * G4 + c8 * 8) * 2);
+          }
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            const int qc = tid + 512 * (h + u), row = qc / (G4 / 8), c8 = qc % (G4 / 8);
+            *reinterpret_cast<v4u*>(dgs + row * DP + c8 * 8) = v[u];
+          }
+        }
+      }
+      __syncthreads();
+      v4f acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+      const bf16_t* db = dgs + col * DP + q * H + 8 * G;
+#pragma unroll
+      for (int s = 0; s < KS; s += 2) {
+        const v8s d0 = *reinterpret_cast<const v8s*>(db + s * 32), d1 = *reinterpret_cast<const v8s*>(db + (s + 1) * 32);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[s], d0, acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[s + 1], d1, acc1, 0, 0, 0);
+        if ((s & 7) == 6) asm volatile("" ::: "memory");   // <= 8 fragment reads in flight (VGPR budget)
+      }
+      const v4f p = acc0 + acc1;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) red[q][ut * 16 + 4 * G + e][col] = p[e];
+      __syncthreads();
+      dh += red[0][jj][bb] + red[1][jj][bb] + red[2][jj][bb] + red[3][jj][bb];
+    }
+    if (t < 0) {   // final round: dh0 = dg_0 W
+      if (live) a.dh0[(size_t)b * H + j] = dh;
+      break;
+    }
+    const float tc = tanh_f(cv);
+    const float dcv = dh * og * (1.f - tc * tc) + dc;
+    const float di = dcv * gg * ig * (1.f - ig);
+    const float dgg = dcv * ig * (1.f - gg * gg);
+    const float df = dcv * cp * fg * (1.f - fg);
+    const float dog = dh * tc * og * (1.f - og);
+    dc = dcv * fg;
+    if (live) {
+      float* gp = a.dxg + ((size_t)b * a.T + t) * G4 + j;
+      gp[0] = di; gp[H] = dgg; gp[2 * H] = df; gp[3 * H] = dog;
+    }
+    dst[(bb * 4 + 0) * 32 + jj] = f2bf(di);
+    dst[(bb * 4 + 1) * 32 + jj] = f2bf(dgg);
+    dst[(bb * 4 + 2) * 32 + jj] = f2bf(df);
+    dst[(bb * 4 + 3) * 32 + jj] = f2bf(dog);
+    __syncthreads();
+    if (wave == 0) {   // publish 16 rows x 4 gates x 64 B; drained before the counter add
+      const __amdgpu_buffer_rsrc_t r = rsrc(a.dg16 + t * slab, (int)(slab * 2));
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int cidx = lane + 64 * k, row = cidx >> 4, gt = (cidx >> 2) & 3, qq = cidx & 3;
+        if (row < nb)
+          st_sc1(*reinterpret_cast<const v4u*>(dst + (row * 4 + gt) * 32 + qq * 8), r,
+                 (int)(((b_lo + row) * G4 + gt * H + m * 32 + qq * 8) * 2));
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0) signal(cnt);
+    }
+  }
+  if (live) a.dc0[(size_t)b * H + j] = dc;
+}
+
+int g_lstm_seq = -1;   // BIGDL_LSTM_SEQ: 1 (default) persistent whole-sequence kernels, 0 = per-step kernels
+int seq_enabled() {
+  if (g_lstm_seq < 0) {
+    const char* e = getenv("BIGDL_LSTM_SEQ");
+    g_lstm_seq = e ? atoi(e) : 1;
+  }
+  return g_lstm_seq;
+}
+
+int cu_count() {
+  static const int n = [] {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+    return cus;
+  }();
+  return n;
+}
+
+bool seq_shape_ok(int B, int H) {
+  if (!seq_enabled() || B <= 0 || (H != 256 && H != 512 && H != 1024)) return false;
+  if ((B + NGRP - 1) / NGRP > 16) return false;
+  return NGRP * (H / 32) <= cu_count();   // one workgroup per CU, all resident
+}
+
+}  // namespace
+
+extern "C" {
+
+int bigdl_lstm_seq_supported(int B, int H) { return seq_shape_ok(B, H) ? 1 : 0; }
+void bigdl_set_lstm_seq(int v) { g_lstm_seq = v; }
+int bigdl_lstm_seq_sync_words() { return NGRP * CNT_STRIDE + CNT_STRIDE; }
+
+int bigdl_lstm_seq_fwd(const uint16_t* W16, const float* xg, const float* c0, uint16_t* h16, float* out, float* cs,
+                       float* acts, unsigned* sync, int B, int H, int T, hipStream_t st) {
+  if (!seq_shape_ok(B, H) || T <= 0) return -1;
+  LstmSeqArgs a{};
+  a.W16 = W16; a.xg = xg; a.c0 = c0; a.h16 = h16; a.out = out; a.cs = cs; a.acts = acts; a.sync = sync;
+  a.B = B; a.H = H; a.T = T; a.Bg = (B + NGRP - 1) / NGRP;
+  if (hipMemsetAsync(sync, 0, sizeof(unsigned) * bigdl_lstm_seq_sync_words(), st) != hipSuccess) return -2;
+  const dim3 grid(NGRP * (H / 32));
+  if (H == 1024) lstm_seq_fwd_kernel<32><<<grid, 512, 0, st>>>(a);
+  else if (H == 512) lstm_seq_fwd_kernel<16><<<grid, 512, 0, st>>>(a);
+  else lstm_seq_fwd_kernel<8><<<grid, 512, 0, st>>>(a);
+  HIP_LAUNCH_CHECK();
+  return 0;
+}
+
+int bigdl_lstm_seq_bwd(const uint16_t* W16, const float* dout, const float* dhT, const float* dcT, const float* acts,
+                       const float* cs, const float* c0, uint16_t* dg16, float* dxg, float* dc0, float* dh0,
+                       unsigned* sync, int B, int H, int T, hipStream_t st) {
+  if (!seq_shape_ok(B, H) || T <= 0) return -1;
+  LstmSeqArgs a{};
+  a.W16 = W16; a.dout = dout; a.dhT = dhT; a.dcT = dcT; a.acts = const_cast<float*>(acts); a.cs = const_cast<float*>(cs); a.c0 = c0; a.dg16 = dg16;
+  a.dxg = dxg; a.dc0 = dc0; a.dh0 = dh0; a.sync = sync;
+  a.B = B; a.H = H; a.T = T; a.Bg = (B + NGRP - 1) / NGRP;
+  if (hipMemsetAsync(sync, 0, sizeof(unsigned) * bigdl_lstm_seq_sync_words(), st) != hipSuccess) return -2;
+  const dim3 grid(NGRP * (H / 32));
+  if (H == 1024) lstm_seq_bwd_kernel<32><<<grid, 512, 0, st>>>(a);
+  else if (H == 512) lstm_seq_bwd_kernel<16><<<grid, 512, 0, st>>>(a);
+  else lstm_seq_bwd_kernel<8><<<grid, 512, 0, st>>>(a);
+  HIP_LAUNCH_CHECK();
+  return 0;
+}
+
+}  // extern "C"

@@ -712,3 +712,46 @@ def test_conv_p8_kernel_fwd_dgrad(case):
         torch.cuda.synchronize()
     finally:
         C_.set_conv_p8(1)
+
+
+WGRAD_P8_CASES = [
+    # N, C, H, K, R, stride, pad -> 256 x 256 phase-interleaved weight-gradient kernel (no bias, Ncol, Kdim >= 256)
+    (16, 64, 56, 256, 1, 1, 0),      # Kdim 64 < 256: stays on the older kernels (dispatch check)
+    (16, 256, 56, 256, 1, 1, 0),     # 1 tile, deep pixel split
+    (8, 128, 28, 256, 3, 1, 1),      # Kdim 1152 (4.5 tiles: kk tail), padding taps
+    (8, 256, 28, 512, 3, 2, 1),      # stride 2, M tail
+    (4, 512, 7, 512, 3, 1, 1),       # few pixels: one split, dw += directly
+    (6, 264, 14, 320, 1, 1, 0),      # Ncol and Kdim tails (320, 264)
+]
+
+
+@pytest.mark.parametrize("case", WGRAD_P8_CASES)
+@pytest.mark.parametrize("offset", [0, 1])
+def test_conv_wgrad_p8_kernel(case, offset):
+    """Phase-interleaved 256 x 256 weight-gradient kernel vs fp32 torch, accumulating into an existing gradient;
+    offset 0 also checks the fused bias gradient, offset 1 places dW at a 4-byte (not 16-byte) aligned view of a
+    flat buffer with no bias."""
+    from bigdl_amd.ops import native
+
+    N, C, H, K, R, st, pd = case
+    torch.manual_seed(5)
+    dev = _dev()
+    x = torch.randn(N, C, H, H, device=dev).to(BF, memory_format=CL)
+    OH = (H + 2 * pd - R) // st + 1
+    gy = torch.randn(N, K, OH, OH, device=dev).to(BF, memory_format=CL)
+    n = K * C * R * R
+    flat = torch.randn(n + offset, device=dev)
+    base = flat[offset:].clone()
+    pre = flat[:offset].clone()
+    dw = flat[offset:]                       # (K, R, S, C) = channels_last (K, C, R, S) storage
+    geo = [N, H, H, C, OH, OH, R, R, st, st, pd, pd, 1, 1, N * OH * OH, K, R * R * C, K]
+    db = torch.randn(K, device=dev) if offset == 0 else None
+    db0 = db.clone() if db is not None else None
+    native.get().conv_wgrad(gy, x, dw, db, geo)
+    torch.cuda.synchronize()
+    if db is not None:
+        assert _rel(db - db0, gy.float().sum(dim=(0, 2, 3))) < 1e-2
+    dwr = torch.nn.grad.conv2d_weight(x.float(), (K, C, R, R), gy.float(), stride=st, padding=pd)
+    got = (dw - base).view(K, R, R, C).permute(0, 3, 1, 2)
+    assert _rel(got, dwr) < 1e-2
+    assert torch.equal(flat[:offset], pre)

@@ -141,3 +141,46 @@ def test_bidirectional_two_layer_rnn_gpu_matches_cpu(cellname):
     wc = torch.cat([g.reshape(-1) for g in cpu.parameters()[1]])
     wg = torch.cat([g.float().cpu().reshape(-1) for g in gpu.parameters()[1]])
     assert _rel(wg, wc) < 3e-2
+
+
+@pytest.mark.parametrize("B,T,H", [(128, 16, 1024), (100, 7, 512), (9, 5, 256), (64, 3, 1024)])
+def test_persistent_lstm_sequence_matches_step_kernels(B, T, H):
+    """csrc/lstm_seq.hip (one persistent launch per direction, W resident in VGPRs, per-step group hand-off) vs the
+    per-step kernels of csrc/lstm.hip and the fp64 torch recurrence: outputs, final state and all four gradients;
+    the launch's error word (set by a timed-out spin) stays 0."""
+    from bigdl_amd.nn.recurrent import _LSTMSeq
+    from bigdl_amd.ops import native
+
+    C = native.get()
+    torch.manual_seed(1)
+    xg = torch.randn(B, T, 4 * H) * 0.5
+    h0, c0 = torch.randn(B, H) * 0.5, torch.randn(B, H) * 0.5
+    U = (torch.randn(4 * H, H) / H ** 0.5).to(torch.bfloat16).float()
+    go = torch.randn(B, T, H)
+    gh, gc = torch.randn(B, H), torch.randn(B, H)
+    res = {}
+    try:
+        for seq in (1, 0):
+            C.set_lstm_seq(seq)
+            assert bool(C.lstm_seq_supported(B, H)) == bool(seq)
+            dev = [t.cuda().requires_grad_(True) for t in (xg, h0, c0, U)]
+            out, hT, cT = _LSTMSeq.apply(*dev)
+            torch.autograd.backward([out, hT, cT], [go.cuda(), gh.cuda(), gc.cuda()])
+            torch.cuda.synchronize()
+            res[seq] = [out.detach(), hT.detach(), cT.detach()] + [d.grad for d in dev]
+    finally:
+        C.set_lstm_seq(1)
+    for a, b in zip(res[1], res[0]):
+        assert torch.isfinite(a).all()
+        assert _rel(a, b) < 1e-2, _rel(a, b)
+    # direct launch: error word untouched
+    W16 = U.cuda().to(torch.bfloat16)
+    h16 = torch.zeros(T + 1, B, H, device="cuda", dtype=torch.bfloat16)
+    h16[0] = h0.cuda().to(torch.bfloat16)
+    out = torch.empty(B, T, H, device="cuda")
+    cs, acts = torch.empty(T, B, H, device="cuda"), torch.empty(T, B, 4 * H, device="cuda")
+    sync = torch.full((C.lstm_seq_sync_words(),), 7, dtype=torch.int32, device="cuda")
+    C.lstm_seq_fwd(W16, xg.cuda(), c0.cuda(), h16, out, cs, acts, sync)
+    torch.cuda.synchronize()
+    assert int(sync[8 * 32].item()) == 0
+    assert _rel(out, res[0][0]) < 1e-2
