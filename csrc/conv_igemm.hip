@@ -1421,7 +1421,7 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
 // of conv_nt_p8_kernel (see there for the hazard argument).
 __device__ __forceinline__ int p8w_f(int r) { return 2 * ((r & 3) | (((r >> 3) & 1) << 2)); }
 typedef __bf16 v2bf __attribute__((ext_vector_type(2)));
-typedef int v4i_t __attribute__((ext_vector_type(4)));
+typedef __bf16 v8bf __attribute__((ext_vector_type(8)));
 
 __global__ __launch_bounds__(512, 2) void conv_wgrad_p8_kernel(WgradArgs a) {
   constexpr int PIX = 64;                          // pixels per K-step
@@ -1548,9 +1548,9 @@ __global__ __launch_bounds__(512, 2) void conv_wgrad_p8_kernel(WgradArgs a) {
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int kh = 0; kh < 2; ++kh) {
-        const v4i_t u = __builtin_bit_cast(v4i_t, fb[jb + j][kh]);
+        const v8bf f = __builtin_bit_cast(v8bf, fb[jb + j][kh]);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) bsum[j] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(v2bf, u[e]), one, bsum[j], false);
+        for (int e = 0; e < 4; ++e) bsum[j] = __builtin_amdgcn_fdot2_f32_bf16(v2bf{f[2 * e], f[2 * e + 1]}, one, bsum[j], false);
       }
   };
   auto compute = [&](int ib, int jb, bool sum_bias) {
