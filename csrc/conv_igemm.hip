@@ -2656,7 +2656,8 @@ static bool wgrad_g3() {
 void bigdl_set_wgrad_g3(int v) { g_wgrad_g3 = v; }
 int bigdl_get_wgrad_g3() { return wgrad_g3() ? 1 : 0; }
 
-// BIGDL_WGRAD_P8: 1 (default) = conv_wgrad_p8_kernel for layers with Ncol >= 256 and Kdim >= 256; 0 = off.
+// BIGDL_WGRAD_P8: 1 (default) = conv_wgrad_p8_kernel where it measured faster (below), 2 = on every layer with
+// Ncol >= 256 and Kdim >= 256 (tests / A/B), 0 = off.
 // Returns its pixel split (>= 1) or 0 when it does not apply; sets m_per_split.
 static int p8w_pick(WgradArgs* a) {
   if (g_wgrad_p8 < 0) {
@@ -2667,6 +2668,10 @@ static int p8w_pick(WgradArgs* a) {
       (a->Ncol % 8) || (a->Kdim % 8) || a->M <= 0)
     return 0;
   const long tiles = (long)((a->Ncol + 255) / 256) * ((a->Kdim + 255) / 256);
+  // per-layer A/B on ResNet-50 b256 (profiles/r4_wgrad_p8_layers.txt): wins on the im2col (R x S > 1) layers with
+  // Kdim >= 2304 (-15..-25 %) and on grids of >= 32 tiles; loses on 1x1 layers with few tiles, where its deep pixel
+  // split turns into fp32 partial traffic
+  if (g_wgrad_p8 == 1 && !((a->R * a->S > 1 && a->Kdim >= 2048) || tiles >= 32)) return 0;
   const long steps = (a->M + 63) / 64;
   long splits = (256 + tiles - 1) / tiles;                         // one workgroup per CU
   splits = std::min(splits, std::max(1L, steps / 8));              // >= 8 pixel steps per split
