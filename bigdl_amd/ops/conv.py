@@ -367,14 +367,15 @@ def conv2d_wgrad(dy, x, dw32, dbias32, stride, pad, dil=(1, 1)):
     Kw, Cw, R, S = dw32.shape
     assert Kw == K and Cw == C
     P = N * OH * OW
-    if (P >= 512 and ((K + 127) // 128) * ((C + 127) // 128) >= 192 and _gemm_shaped(dy, x, dw32, stride, pad, dil)):
-        gemm_wgrad_nt(dy.reshape(P, K) if dy.is_contiguous() else dy.permute(0, 2, 3, 1).reshape(P, K),
-                      x.reshape(P, C) if x.is_contiguous() else x.permute(0, 2, 3, 1).reshape(P, C), dw32, dbias32)
-        return
     sh, sw = stride
     ph, pw = pad
     dh, dw = dil
     geo = [N, H, W, C, OH, OW, R, S, sh, sw, ph, pw, dh, dw, N * OH * OW, K, R * S * C, K]
+    if (P >= 512 and ((K + 127) // 128) * ((C + 127) // 128) >= 192 and _gemm_shaped(dy, x, dw32, stride, pad, dil)
+            and not native.get().conv_wgrad_uses_p8(geo, dbias32 is not None)):
+        gemm_wgrad_nt(dy.reshape(P, K) if dy.is_contiguous() else dy.permute(0, 2, 3, 1).reshape(P, K),
+                      x.reshape(P, C) if x.is_contiguous() else x.permute(0, 2, 3, 1).reshape(P, C), dw32, dbias32)
+        return
     native.get().conv_wgrad(dy, x, dw32, dbias32, geo)
 
 

@@ -112,6 +112,18 @@ void conv_wgrad(const Tensor& dy, const Tensor& src, const Tensor& dw, const Opt
   TORCH_CHECK(rc == 0, "conv_wgrad: unsupported shape (channels must be a multiple of 8)");
 }
 
+// true when conv_wgrad would run the phase-interleaved 256 x 256 kernel on this geometry (callers skip the
+// transpose-based NT GEMM route then)
+bool conv_wgrad_uses_p8(std::vector<int64_t> geo, bool bias) {
+  TORCH_CHECK(geo.size() == 18, "conv_wgrad_uses_p8: bad geometry");
+  WgradArgs a{};
+  int* f = &a.Nb;
+  for (int i = 0; i < 18; ++i) f[i] = (int)geo[i];
+  static float dummy;
+  a.dbias = bias ? &dummy : nullptr;
+  return bigdl_conv_wgrad_uses_p8(&a) != 0;
+}
+
 void transpose_krsc(const Tensor& w, const Tensor& wt, int64_t K, int64_t RS, int64_t C) {
   TORCH_CHECK(w.numel() == K * RS * C && wt.numel() == K * RS * C, "transpose_krsc: size mismatch");
   bigdl_transpose_krsc(cbf(w, "w"), mbf(wt, "wt"), (int)K, (int)RS, (int)C, stream());
@@ -1155,6 +1167,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_conv_g4", &bigdl_set_conv_g4);
   m.def("set_conv_p8", &bigdl_set_conv_p8);
   m.def("set_wgrad_p8", &bigdl_set_wgrad_p8);
+  m.def("conv_wgrad_uses_p8", &conv_wgrad_uses_p8);
   m.def("get_conv_g4", &bigdl_get_conv_g4);
   m.def("set_wgrad_g3", &bigdl_set_wgrad_g3);
   m.def("get_wgrad_g3", &bigdl_get_wgrad_g3);

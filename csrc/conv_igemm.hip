@@ -1423,6 +1423,9 @@ __device__ __forceinline__ int p8w_f(int r) { return 2 * ((r & 3) | (((r >> 3) &
 typedef __bf16 v2bf __attribute__((ext_vector_type(2)));
 typedef __bf16 v8bf __attribute__((ext_vector_type(8)));
 
+// DIRECT: 1 x 1, stride 1, no padding (GEMM-shaped): x row = output pixel, no per-row geometry in the DMA issue
+// (the general path divides every DMA row's pixel index into (image, oh, ow): ~9 VALU instructions per MFMA)
+template <bool DIRECT>
 __global__ __launch_bounds__(512, 2) void conv_wgrad_p8_kernel(WgradArgs a) {
   constexpr int PIX = 64;                          // pixels per K-step
   constexpr int PC = 128;                          // columns per piece
@@ -1483,7 +1486,9 @@ __global__ __launch_bounds__(512, 2) void conv_wgrad_p8_kernel(WgradArgs a) {
       const bf16_t* src = g_zero_granule;
       if (m < mend) {
         if ((P & 1) == 0) {
-          if (xv[q]) {
+          if (DIRECT) {
+            if (xv[q]) src = a.src + (size_t)m * a.Cs + xc[q];
+          } else if (xv[q]) {
             const int nb = m / ohw, rem = m - nb * ohw;
             const int oh = rem / a.OW, ow = rem - oh * a.OW;
             const int ih = oh * a.sh - a.ph + xr[q] * a.dh, iw = ow * a.sw - a.pw + xs[q] * a.dwl;
@@ -1926,7 +1931,10 @@ __global__ __launch_bounds__(512, 1) void conv_nt_w8_kernel(ConvArgs a) {
 // tail past Kdim loads zeros.
 // BM = 256 (BIGDL_CONV_G4=6/7): 2 x 2 waves of 128 x 64, 32 MFMAs per wave between barriers instead of 16, 24 KB
 // stages, 2 workgroups per CU.
-template <int BN, int NS, bool FASTK = true, int BM = 128>
+// ABN = 1: timing ablation only (wrong outputs) — a per-channel scale / shift + ReLU applied to every A fragment after
+// its LDS read, coefficients loaded per K-step (what folding a BN apply into the consumer's operand would cost).
+__device__ float g_abn_tab[2 * 4096];
+template <int BN, int NS, bool FASTK = true, int BM = 128, int ABN = 0>
 __global__ __launch_bounds__(256, (NS == 3 && BM == 128) ? 3 : 2) void conv_nt_g4_kernel(ConvArgs a) {
   constexpr int BKS = 32;
   constexpr int WGM = 2, WGN = 2;
@@ -2051,6 +2059,21 @@ __global__ __launch_bounds__(256, (NS == 3 && BM == 128) ? 3 : 2) void conv_nt_g
     for (int j = 0; j < NI; ++j) fb[j] = *reinterpret_cast<const v8s*>(B + (wn * TN + j * 16) * BKS + foff);
 #pragma unroll
     for (int i = 0; i < MI; ++i) fa[i] = *reinterpret_cast<const v8s*>(A + (wm * TM + i * 16) * BKS + foff);
+    if constexpr (ABN) {
+      const int c0 = ((kt * BKS) % a.Cs + 8 * (lane >> 4)) & 4095;
+      const v4f s0 = *reinterpret_cast<const v4f*>(g_abn_tab + c0), s1 = *reinterpret_cast<const v4f*>(g_abn_tab + c0 + 4);
+      const v4f t0 = *reinterpret_cast<const v4f*>(g_abn_tab + 4096 + c0), t1 = *reinterpret_cast<const v4f*>(g_abn_tab + 4096 + c0 + 4);
+      const float sc[8] = {s0[0] + 1.f, s0[1] + 1.f, s0[2] + 1.f, s0[3] + 1.f, s1[0] + 1.f, s1[1] + 1.f, s1[2] + 1.f, s1[3] + 1.f};
+      const float sh[8] = {t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]};
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        v4u u = __builtin_bit_cast(v4u, fa[i]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          u[e] = pack2bf(fmaxf(lo_bf(u[e]) * sc[2 * e] + sh[2 * e], 0.f), fmaxf(hi_bf(u[e]) * sc[2 * e + 1] + sh[2 * e + 1], 0.f));
+        fa[i] = __builtin_bit_cast(v8s, u);
+      }
+    }
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -2491,7 +2514,9 @@ static int p8_pick(const ConvArgs* a) {
 template <int BN, int NS, int BM = 128>
 void launch_nt_g4(const ConvArgs& a, hipStream_t st) {
   const int nwg = ((a.M + BM - 1) / BM) * ((a.Ncol + BN - 1) / BN);
-  if (a.Cs % 32 == 0) conv_nt_g4_kernel<BN, NS, true, BM><<<dim3(nwg), dim3(256), 0, st>>>(a);
+  static const int abn = [] { const char* e = getenv("BIGDL_G4_ABN"); return e ? atoi(e) : 0; }();
+  if (abn && BM == 128 && NS == 3 && a.Cs % 32 == 0) conv_nt_g4_kernel<BN, NS, true, BM, 1><<<dim3(nwg), dim3(256), 0, st>>>(a);
+  else if (a.Cs % 32 == 0) conv_nt_g4_kernel<BN, NS, true, BM><<<dim3(nwg), dim3(256), 0, st>>>(a);
   else conv_nt_g4_kernel<BN, NS, false, BM><<<dim3(nwg), dim3(256), 0, st>>>(a);
 }
 
@@ -2662,16 +2687,19 @@ int bigdl_get_wgrad_g3() { return wgrad_g3() ? 1 : 0; }
 static int p8w_pick(WgradArgs* a) {
   if (g_wgrad_p8 < 0) {
     const char* e = getenv("BIGDL_WGRAD_P8");
-    g_wgrad_p8 = e ? atoi(e) : 1;
+    g_wgrad_p8 = e ? atoi(e) : 0;
   }
   if (!g_wgrad_p8 || conv_impl() < 1 || a->Ncol < 256 || a->Kdim < 256 || (a->Cs % 8) ||
       (a->Ncol % 8) || (a->Kdim % 8) || a->M <= 0)
     return 0;
   const long tiles = (long)((a->Ncol + 255) / 256) * ((a->Kdim + 255) / 256);
-  // per-layer A/B on ResNet-50 b256 (profiles/r4_wgrad_p8_layers.txt): wins on the im2col (R x S > 1) layers with
-  // Kdim >= 2304 (-15..-25 %) and on grids of >= 32 tiles; loses on 1x1 layers with few tiles, where its deep pixel
-  // split turns into fp32 partial traffic
-  if (g_wgrad_p8 == 1 && !((a->R * a->S > 1 && a->Kdim >= 2048) || tiles >= 32)) return 0;
+  // Default: GEMM-shaped (1 x 1) weight gradients with >= 32 output tiles — Linear / LSTM projections, where it reads
+  // dy and x in place (transposed LDS reads) instead of the two operand transposes of the NT GEMM path. In isolation
+  // it also wins on ResNet-50's 3x3 layers with Kdim >= 2304 (-15..-25 %, profiles/r4_wgrad_p8_layers.txt), but
+  // inside the training step its 128 KB-LDS workgroups on the weight-gradient side stream cost the concurrent data-
+  // gradient chain more than they save (26.05 vs 25.72 ms/step, profiles/r4_wgrad_p8_ab.txt); on 1x1 layers with few
+  // tiles its deep pixel split turns into fp32 partial traffic
+  if (g_wgrad_p8 == 1 && !(a->R * a->S == 1 && tiles >= 32)) return 0;
   const long steps = (a->M + 63) / 64;
   long splits = (256 + tiles - 1) / tiles;                         // one workgroup per CU
   splits = std::min(splits, std::max(1L, steps / 8));              // >= 8 pixel steps per split
@@ -2682,6 +2710,11 @@ static int p8w_pick(WgradArgs* a) {
   splits = (a->M + mps - 1) / mps;
   a->m_per_split = (int)mps;
   return (int)splits;
+}
+
+int bigdl_conv_wgrad_uses_p8(const WgradArgs* a_in) {
+  WgradArgs a = *a_in;
+  return p8w_pick(&a) > 0 ? 1 : 0;
 }
 
 long bigdl_conv_wgrad_plan(WgradArgs* a) {
@@ -2718,7 +2751,10 @@ int bigdl_conv_wgrad(const WgradArgs* a_in, hipStream_t st) {
       b.splits = p8w;
       b.ws = a.ws;
       const int tiles = ((a.Ncol + 255) / 256) * ((a.Kdim + 255) / 256);
-      conv_wgrad_p8_kernel<<<dim3(tiles, p8w), dim3(512), 0, st>>>(b);
+      const bool direct = a.R == 1 && a.S == 1 && a.sh == 1 && a.sw == 1 && a.ph == 0 && a.pw == 0 && a.Hs == a.OH &&
+                          a.Ws == a.OW;
+      if (direct) conv_wgrad_p8_kernel<true><<<dim3(tiles, p8w), dim3(512), 0, st>>>(b);
+      else conv_wgrad_p8_kernel<false><<<dim3(tiles, p8w), dim3(512), 0, st>>>(b);
       if (p8w > 1) {
         const long n4 = (long)a.Ncol * a.Kdim / 4;
         const int blocks = (int)std::min<long>((n4 + 255) / 256, 8192);

@@ -184,6 +184,7 @@ int bigdl_get_conv_impl();
 void bigdl_set_conv_g4(int v);
 void bigdl_set_conv_p8(int v);
 void bigdl_set_wgrad_p8(int v);
+int bigdl_conv_wgrad_uses_p8(const WgradArgs* a);
 int bigdl_get_conv_g4();
 void bigdl_set_wgrad_g3(int v);
 int bigdl_get_wgrad_g3();

@@ -7,7 +7,7 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _run(graph, iters=6):
+def _run(graph, iters=6, hook=None):
     from bigdl_amd import nn
     from bigdl_amd import optim as O
     from bigdl_amd.dataset.core import DataSet, Sample
@@ -27,7 +27,12 @@ def _run(graph, iters=6):
                       endTrigger=O.Trigger.maxIteration(iters))
     opt.device = torch.device("cuda:0")
     graphed = []
-    opt._iteration_hook = lambda n: graphed.append(opt._graph is not None)
+    def _hook(n):
+        graphed.append(opt._graph is not None)
+        if hook is not None:
+            hook(opt)
+
+    opt._iteration_hook = _hook
     # the dataset reshuffles from a random offset: pin it
     RNG.setSeed(7)
     m = opt.optimize()
@@ -37,17 +42,45 @@ def _run(graph, iters=6):
     return w, graphed, float(opt.state["Loss"]), (meth.state.get("evalCounter"), meth.learningRateSchedule.currentRate)
 
 
+def _train_state(opt):
+    """Every tensor an iteration reads and writes: fp32 master weights, their bf16 shadow, optimizer state buffers."""
+    st = opt._step
+    out = [st.w] + ([st.w16] if st.w16 is not None else [])
+    for m in opt.optimMethods.values():
+        for k in sorted(m.state.keys(), key=str):
+            v = m.state[k]
+            if torch.is_tensor(v) and v.is_floating_point() and v.numel() > 1:
+                out.append(v)
+    return out
+
+
 def test_graphed_optimizer_matches_eager():
-    w_e, g_e, l_e, s_e = _run(False)
-    w_e2, _, _, _ = _run(False)
-    w_g, g_g, l_g, s_g = _run(True)
+    """Lock-step: the eager run records the training state after every iteration; the graph run (2 eager warm-up
+    iterations, then captured replays) is compared with it after every iteration and then reset to it, so each
+    comparison covers exactly one iteration from identical state. (End-to-end trajectories of ANY two runs, eager or
+    graph, separate by 5e-4..7e-3 after 6 iterations: fp32-atomic ordering in the parameter gradients flips the
+    rare ReLU mask element within ~1e-8 of zero, profiles/r4_determinism.txt; one iteration from identical state
+    differs by ~1e-9.)"""
+    snaps = []
+    w_e, g_e, l_e, s_e = _run(False, hook=lambda opt: snaps.append([t.detach().clone() for t in _train_state(opt)]))
+    rels = []
+
+    def lockstep(opt):
+        cur = _train_state(opt)
+        ref = snaps[len(rels)]
+        assert len(cur) == len(ref)
+        rels.append(max(((c.float() - r.float()).norm() / r.float().norm().clamp_min(1e-30)).item()
+                        for c, r in zip(cur, ref)))
+        for c, r in zip(cur, ref):
+            c.copy_(r)
+
+    w_g, g_g, l_g, s_g = _run(True, hook=lockstep)
     assert not any(g_e)
     assert g_g[:2] == [False, False] and all(g_g[2:]), g_g     # eager warm-up, then captured replays
     assert s_g == s_e, (s_g, s_e)                                 # same schedule position and rate
-    noise = ((w_e2 - w_e).norm() / w_e.norm()).item()             # run-to-run (fp32 atomics in BN statistics)
-    rel = ((w_g - w_e).norm() / w_e.norm()).item()
-    print("graph vs eager", rel, "eager vs eager", noise)
-    assert rel < 1e-5, (rel, noise)
+    print("per-iteration graph vs eager", rels)
+    assert len(rels) == len(snaps) == 6
+    assert max(rels) < 1e-5, rels
     assert abs(l_g - l_e) < 2e-2 * max(1.0, abs(l_e))
 
 
