@@ -171,6 +171,10 @@ class Cell(Container):
     def step(self, x, hid):
         raise NotImplementedError
 
+    def bf16_sequence_ok(self, x2, mask=None):
+        """True when ``sequence`` takes the bf16 gate inputs as they come from the projection GEMM (GPU)."""
+        return False
+
     def sequence(self, x2, hid, mask=None):
         """Run ``step`` over the time dimension of x2 [B, T, ...]; returns (out [B, T, ...], last hidden)."""
         outs = []
@@ -288,7 +292,11 @@ class _LSTMSeq(torch.autograd.Function):
 
     @staticmethod
     def _fused_gpu(xg, U):
-        return xg.is_cuda and U.shape[1] % 32 == 0 and xg.dtype == torch.float32
+        if not (xg.is_cuda and U.shape[1] % 32 == 0):
+            return False
+        if xg.dtype == torch.bfloat16:     # bf16 gate inputs: whole-sequence kernels only (Recurrent checks first)
+            return bool(ops.native.get().lstm_seq_supported(xg.shape[0], U.shape[1]))
+        return xg.dtype == torch.float32
 
     @staticmethod
     def forward(ctx, xg, h0, c0, U):
@@ -308,9 +316,14 @@ class _LSTMSeq(torch.autograd.Function):
             ctx.seq = bool(C.lstm_seq_supported(B, H))
             if ctx.seq:
                 # whole sequence in ONE persistent launch (csrc/lstm_seq.hip): W resident in VGPRs, per-step
-                # state exchange inside each XCD's batch group
+                # state exchange inside each XCD's batch group; bf16 xg -> bf16 out (the projections' dtype)
                 sync = torch.empty(C.lstm_seq_sync_words(), dtype=torch.int32, device=xg.device)
-                C.lstm_seq_fwd(W16, xg, c0.contiguous(), h16, out, cs, acts, sync)
+                out = xg.new_empty(B, T, H)
+                hT = xg.new_empty(B, H, dtype=torch.float32)
+                C.lstm_seq_fwd(W16, xg, c0.contiguous(), h16, out, hT, cs, acts, sync)
+                ctx.save_for_backward(h0, c0, U, out, cs, acts, h16, W16)
+                ctx.fused = True
+                return out, hT, cs[-1].clone()
             else:
                 c_prev = c0.contiguous()
                 for t in range(T):
@@ -342,14 +355,17 @@ class _LSTMSeq(torch.autograd.Function):
         dout = dout.contiguous() if dout is not None else None
         if ctx.seq:
             # one persistent launch for the whole backward sweep, dh0 = dg_0 U included (no transposed copy of U)
-            dxg = out.new_empty(B, T, 4 * H)
+            dxg = out.new_empty(B, T, 4 * H)        # out's dtype: bf16 in, bf16 gradient out
+            if dout is not None and dout.dtype != out.dtype:
+                dout = dout.to(out.dtype)
             dg16 = out.new_empty(T, B, 4 * H, dtype=torch.bfloat16)
-            dc0, dh0 = out.new_empty(B, H), out.new_empty(B, H)
+            dc0 = out.new_empty(B, H, dtype=torch.float32)
+            dh0 = out.new_empty(B, H, dtype=torch.float32)
             sync = torch.empty(C.lstm_seq_sync_words(), dtype=torch.int32, device=out.device)
             C.lstm_seq_bwd(W16, dout, dhT.contiguous() if dhT is not None else None,
                            dcT.contiguous() if dcT is not None else None, acts, cs, c0.contiguous(), dg16, dxg, dc0,
                            dh0, sync)
-            dU = out.new_empty(4 * H, H, 1, 1)
+            dU = out.new_empty(4 * H, H, 1, 1, dtype=torch.float32)
             C.fill_bytes(dU, 0)
             cv.conv2d_wgrad(dg16.view(T * B, 4 * H, 1, 1), h16[:T].view(T * B, H, 1, 1), dU, None, (1, 1), (0, 0))
             return dxg, dh0, dc0, dU.view(4 * H, H)
@@ -491,6 +507,10 @@ class LSTM(Cell):
         c2 = f * c + i * gg
         h2 = o * tanh(c2)
         return h2, [h2, c2]
+
+    def bf16_sequence_ok(self, x2, mask=None):
+        return (mask is None and self._fused_ok() and x2.is_cuda and x2.dim() == 3
+                and bool(ops.native.get().lstm_seq_supported(x2.shape[0], self.hiddenSize)))
 
     def sequence(self, x2, hid, mask=None):
         if mask is None and self._fused_ok():
@@ -748,7 +768,12 @@ class Recurrent(Container):
         B = input.shape[0]
         x2, self._flat = self._project(input)
         need_grad = self.train
-        x2l = _f32(x2.detach()).requires_grad_(need_grad)
+        mask0 = None if not self.maskZero else True
+        if (self.bn is None and mask0 is None and x2.is_cuda and x2.dtype == torch.bfloat16
+                and self.cell.bf16_sequence_ok(x2)):
+            x2l = x2.detach().requires_grad_(need_grad)     # bf16 straight from the projection GEMM
+        else:
+            x2l = _f32(x2.detach()).requires_grad_(need_grad)
         h0 = self._init_hidden if self._init_hidden is not None else self.cell.init_hidden(B, x2l[:, 0])
         h0l = [h.detach().float().to(x2l.device).requires_grad_(need_grad) for h in h0]
         mask = None
@@ -765,7 +790,8 @@ class Recurrent(Container):
             raise RuntimeError("Recurrent: backward called without a training forward")
         x2l, h0l, L, out, hid = self._ag
         targets = [x2l] + L.leaves + h0l
-        grads = torch.autograd.grad([out], targets, [_f32(gradOutput)], allow_unused=True, retain_graph=True)
+        go = gradOutput.to(out.dtype) if out.dtype == torch.bfloat16 else _f32(gradOutput)
+        grads = torch.autograd.grad([out], targets, [go], allow_unused=True, retain_graph=True)
         gx2 = grads[0] if grads[0] is not None else torch.zeros_like(x2l)
         n = len(L.leaves)
         self._pending = grads[1:1 + n]

@@ -874,8 +874,11 @@ void lstm_bwd_step(const Tensor& WT16, const OptT& dg16_next, const OptT& dout, 
 bool lstm_seq_supported(int64_t B, int64_t H) { return bigdl_lstm_seq_supported((int)B, (int)H) != 0; }
 int64_t lstm_seq_sync_words() { return bigdl_lstm_seq_sync_words(); }
 void lstm_seq_fwd(const Tensor& W16, const Tensor& xg, const OptT& c0, const Tensor& h16, const Tensor& out,
-                  const Tensor& cs, const Tensor& acts, const Tensor& sync) {
+                  const OptT& hT, const Tensor& cs, const Tensor& acts, const Tensor& sync) {
   TORCH_CHECK(xg.dim() == 3 && xg.is_contiguous(), "lstm_seq_fwd: xg must be [B, T, 4H] contiguous");
+  const bool bio = xg.scalar_type() == at::kBFloat16;
+  TORCH_CHECK(bio || xg.scalar_type() == at::kFloat, "lstm_seq_fwd: xg must be float32 or bfloat16");
+  TORCH_CHECK(out.scalar_type() == xg.scalar_type(), "lstm_seq_fwd: out must have xg's dtype");
   const int64_t B = xg.size(0), T = xg.size(1), H = W16.size(1);
   TORCH_CHECK(W16.size(0) == 4 * H && W16.is_contiguous() && xg.size(2) == 4 * H, "lstm_seq_fwd: W16 [4H, H]");
   TORCH_CHECK(h16.is_contiguous() && h16.numel() == (T + 1) * B * H, "lstm_seq_fwd: h16 [T + 1, B, H]");
@@ -883,14 +886,18 @@ void lstm_seq_fwd(const Tensor& W16, const Tensor& xg, const OptT& c0, const Ten
               acts.is_contiguous() && acts.numel() == T * B * 4 * H, "lstm_seq_fwd: out / cs / acts");
   TORCH_CHECK(sync.scalar_type() == at::kInt && sync.numel() >= bigdl_lstm_seq_sync_words(), "lstm_seq_fwd: sync");
   if (c0 && c0->defined()) TORCH_CHECK(c0->is_contiguous() && c0->numel() == B * H, "lstm_seq_fwd: c0");
-  TORCH_CHECK(bigdl_lstm_seq_fwd(cbf(W16, "W16"), cf(xg, "xg"), ocf(c0, "c0"), mbf(h16, "h16"), mf(out, "out"),
-                                 mf(cs, "cs"), mf(acts, "acts"), reinterpret_cast<unsigned*>(sync.data_ptr<int>()),
-                                 (int)B, (int)H, (int)T, stream()) == 0, "lstm_seq_fwd: unsupported shape");
+  if (hT && hT->defined()) TORCH_CHECK(hT->is_contiguous() && hT->numel() == B * H, "lstm_seq_fwd: hT");
+  TORCH_CHECK(bigdl_lstm_seq_fwd(cbf(W16, "W16"), xg.data_ptr(), ocf(c0, "c0"), mbf(h16, "h16"), out.data_ptr(),
+                                 (hT && hT->defined()) ? mf(*hT, "hT") : nullptr, mf(cs, "cs"), mf(acts, "acts"),
+                                 reinterpret_cast<unsigned*>(sync.data_ptr<int>()), (int)B, (int)H, (int)T, bio ? 1 : 0,
+                                 stream()) == 0, "lstm_seq_fwd: unsupported shape");
 }
 void lstm_seq_bwd(const Tensor& W16, const OptT& dout, const OptT& dhT, const OptT& dcT, const Tensor& acts,
                   const Tensor& cs, const OptT& c0, const Tensor& dg16, const Tensor& dxg, const Tensor& dc0,
                   const Tensor& dh0, const Tensor& sync) {
   TORCH_CHECK(dxg.dim() == 3 && dxg.is_contiguous(), "lstm_seq_bwd: dxg must be [B, T, 4H] contiguous");
+  const bool bio = dxg.scalar_type() == at::kBFloat16;
+  TORCH_CHECK(bio || dxg.scalar_type() == at::kFloat, "lstm_seq_bwd: dxg must be float32 or bfloat16");
   const int64_t B = dxg.size(0), T = dxg.size(1), H = W16.size(1);
   TORCH_CHECK(W16.size(0) == 4 * H && W16.is_contiguous() && dxg.size(2) == 4 * H, "lstm_seq_bwd: W16 [4H, H]");
   TORCH_CHECK(acts.is_contiguous() && acts.numel() == T * B * 4 * H && cs.is_contiguous() && cs.numel() == T * B * H,
@@ -898,14 +905,19 @@ void lstm_seq_bwd(const Tensor& W16, const OptT& dout, const OptT& dhT, const Op
   TORCH_CHECK(dg16.is_contiguous() && dg16.numel() == T * B * 4 * H && dc0.is_contiguous() && dc0.numel() == B * H &&
               dh0.is_contiguous() && dh0.numel() == B * H, "lstm_seq_bwd: dg16 / dc0 / dh0");
   TORCH_CHECK(sync.scalar_type() == at::kInt && sync.numel() >= bigdl_lstm_seq_sync_words(), "lstm_seq_bwd: sync");
-  if (dout && dout->defined()) TORCH_CHECK(dout->is_contiguous() && dout->numel() == B * T * H, "lstm_seq_bwd: dout");
+  const void* dp = nullptr;
+  if (dout && dout->defined()) {
+    TORCH_CHECK(dout->is_contiguous() && dout->numel() == B * T * H && dout->scalar_type() == dxg.scalar_type(),
+                "lstm_seq_bwd: dout must be [B, T, H] contiguous with dxg's dtype");
+    dp = dout->data_ptr();
+  }
   if (dhT && dhT->defined()) TORCH_CHECK(dhT->is_contiguous() && dhT->numel() == B * H, "lstm_seq_bwd: dhT");
   if (dcT && dcT->defined()) TORCH_CHECK(dcT->is_contiguous() && dcT->numel() == B * H, "lstm_seq_bwd: dcT");
   if (c0 && c0->defined()) TORCH_CHECK(c0->is_contiguous() && c0->numel() == B * H, "lstm_seq_bwd: c0");
-  TORCH_CHECK(bigdl_lstm_seq_bwd(cbf(W16, "W16"), ocf(dout, "dout"), ocf(dhT, "dhT"), ocf(dcT, "dcT"), cf(acts, "acts"),
-                                 cf(cs, "cs"), ocf(c0, "c0"), mbf(dg16, "dg16"), mf(dxg, "dxg"), mf(dc0, "dc0"),
-                                 mf(dh0, "dh0"), reinterpret_cast<unsigned*>(sync.data_ptr<int>()), (int)B, (int)H,
-                                 (int)T, stream()) == 0, "lstm_seq_bwd: unsupported shape");
+  TORCH_CHECK(bigdl_lstm_seq_bwd(cbf(W16, "W16"), dp, ocf(dhT, "dhT"), ocf(dcT, "dcT"), cf(acts, "acts"), cf(cs, "cs"),
+                                 ocf(c0, "c0"), mbf(dg16, "dg16"), dxg.data_ptr(), mf(dc0, "dc0"), mf(dh0, "dh0"),
+                                 reinterpret_cast<unsigned*>(sync.data_ptr<int>()), (int)B, (int)H, (int)T, bio ? 1 : 0,
+                                 stream()) == 0, "lstm_seq_bwd: unsupported shape");
 }
 
 void layernorm_fwd(const Tensor& x, const OptT& g, const OptT& b, const Tensor& y, const Tensor& mean,

@@ -245,11 +245,11 @@ int bigdl_lstm_bwd_step(const uint16_t* WT16, const uint16_t* dg16_next, const f
 int bigdl_lstm_seq_supported(int B, int H);
 void bigdl_set_lstm_seq(int v);
 int bigdl_lstm_seq_sync_words();
-int bigdl_lstm_seq_fwd(const uint16_t* W16, const float* xg, const float* c0, uint16_t* h16, float* out, float* cs,
-                       float* acts, unsigned* sync, int B, int H, int T, hipStream_t st);
-int bigdl_lstm_seq_bwd(const uint16_t* W16, const float* dout, const float* dhT, const float* dcT, const float* acts,
-                       const float* cs, const float* c0, uint16_t* dg16, float* dxg, float* dc0, float* dh0,
-                       unsigned* sync, int B, int H, int T, hipStream_t st);
+int bigdl_lstm_seq_fwd(const uint16_t* W16, const void* xg, const float* c0, uint16_t* h16, void* out, float* hT,
+                       float* cs, float* acts, unsigned* sync, int B, int H, int T, int bf16io, hipStream_t st);
+int bigdl_lstm_seq_bwd(const uint16_t* W16, const void* dout, const float* dhT, const float* dcT, const float* acts,
+                       const float* cs, const float* c0, uint16_t* dg16, void* dxg, float* dc0, float* dh0,
+                       unsigned* sync, int B, int H, int T, int bf16io, hipStream_t st);
 
 // Fused GRU steps (csrc/gru.hip). mode: 0 fwd r/z, 1 fwd n + h, 2 bwd dh_t + dn/dz, 3 bwd dr + r-path, 4 bwd dh_0.
 // GEMM D[b][n] = sum_k A[b][k] W[n][k] (A rows lda apart; W [N][K] contiguous); row strides of the fp32 per-step

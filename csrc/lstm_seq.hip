@@ -39,17 +39,18 @@ constexpr unsigned long long SPIN_TICKS = 50000000ull;   // 0.5 s at 100 MHz
 
 struct LstmSeqArgs {
   const bf16_t* W16;       // [4H][H] gate blocks i, g, f, o
-  const float* xg;         // fwd: [B][T][4H] gate pre-activations from the input projection
+  const void* xg;          // fwd: [B][T][4H] gate pre-activations from the input projection (f32 or bf16: BIO)
   const float* c0;         // [B][H] or null
-  const float* dout;       // bwd: [B][T][H] or null
+  const void* dout;        // bwd: [B][T][H] or null (f32 or bf16: BIO)
   const float* dhT;        // bwd: [B][H] or null
   const float* dcT;        // bwd: [B][H] or null
   bf16_t* h16;             // [T + 1][B][H]: h_{-1} .. h_{T-1}
-  float* out;              // fwd: [B][T][H]
+  void* out;               // fwd: [B][T][H] (f32 or bf16: BIO)
+  float* hT;               // fwd: [B][H] f32 last hidden state, or null
   float* cs;               // [T][B][H]
   float* acts;             // [T][B][4H]
   bf16_t* dg16;            // bwd: [T][B][4H]
-  float* dxg;              // bwd: [B][T][4H]
+  void* dxg;               // bwd: [B][T][4H] (f32 or bf16: BIO)
   float* dc0;              // bwd: [B][H] (dc flowing into c0)
   float* dh0;              // bwd: [B][H]
   unsigned* sync;          // NGRP counters (CNT_STRIDE apart) + error word
@@ -101,7 +102,10 @@ __device__ __forceinline__ void signal(unsigned* cnt) {
 }
 
 // ------------------------------------------------------------------------------------------------ forward
-template <int KS>
+__device__ __forceinline__ float bf2f(bf16_t v) { return __uint_as_float((unsigned)v << 16); }
+
+// BIO: xg / out (forward) and dout / dxg (backward) are bf16 (the projection GEMMs' own dtype; no f32 round trip)
+template <int KS, bool BIO>
 __global__ __launch_bounds__(512, 1) void lstm_seq_fwd_kernel(LstmSeqArgs a) {
   constexpr int H = KS * 32;
   constexpr int HP = H + 8;                      // LDS row pitch: consecutive batch rows 4 banks apart
@@ -130,10 +134,21 @@ __global__ __launch_bounds__(512, 1) void lstm_seq_fwd_kernel(LstmSeqArgs a) {
   const size_t slab = (size_t)a.B * H;            // one time step of h16
 
   for (int t = 0; t < a.T; ++t) {
-    const float* xp = a.xg + ((size_t)b * a.T + t) * 4 * H + j;
-    const float x0 = xp[0], x1 = xp[H], x2 = xp[2 * H], x3 = xp[3 * H];
+    const size_t xo = ((size_t)b * a.T + t) * 4 * H + j;
+    float x0, x1, x2, x3;
+    if constexpr (BIO) {
+      const bf16_t* xp = static_cast<const bf16_t*>(a.xg) + xo;
+      x0 = bf2f(xp[0]); x1 = bf2f(xp[H]); x2 = bf2f(xp[2 * H]); x3 = bf2f(xp[3 * H]);
+    } else {
+      const float* xp = static_cast<const float*>(a.xg) + xo;
+      x0 = xp[0]; x1 = xp[H]; x2 = xp[2 * H]; x3 = xp[3 * H];
+    }
     if (t > 0 && !group_wait(cnt, (unsigned)(M * t), err, &flag, wave, lane)) {
-      if (live) for (int u = t; u < a.T; ++u) a.out[((size_t)b * a.T + u) * H + j] = __builtin_nanf("");
+      if (live)
+        for (int u = t; u < a.T; ++u) {
+          if constexpr (BIO) static_cast<bf16_t*>(a.out)[((size_t)b * a.T + u) * H + j] = 0x7fc0;
+          else static_cast<float*>(a.out)[((size_t)b * a.T + u) * H + j] = __builtin_nanf("");
+        }
       return;
     }
     {   // h_{t-1} of the group's rows -> LDS (rows past the group read as zero)
@@ -165,7 +180,8 @@ __global__ __launch_bounds__(512, 1) void lstm_seq_fwd_kernel(LstmSeqArgs a) {
     c = fg * c + ig * gg;
     const float h = og * tanh_f(c);
     if (live) {
-      a.out[((size_t)b * a.T + t) * H + j] = h;
+      if constexpr (!BIO) static_cast<float*>(a.out)[((size_t)b * a.T + t) * H + j] = h;
+      if (t == a.T - 1 && a.hT) a.hT[(size_t)b * H + j] = h;
       a.cs[((size_t)t * a.B + b) * H + j] = c;
       float* ap = a.acts + ((size_t)t * a.B + b) * 4 * H + j;
       ap[0] = ig; ap[H] = gg; ap[2 * H] = fg; ap[3 * H] = og;
@@ -176,7 +192,10 @@ __global__ __launch_bounds__(512, 1) void lstm_seq_fwd_kernel(LstmSeqArgs a) {
       const int row = lane >> 2, qq = lane & 3;
       if (row < nb) {
         const __amdgpu_buffer_rsrc_t r = rsrc(a.h16 + (t + 1) * slab, (int)(slab * 2));
-        st_sc1(*reinterpret_cast<const v4u*>(hst + row * 32 + qq * 8), r, (int)(((b_lo + row) * H + m * 32 + qq * 8) * 2));
+        const v4u hv = *reinterpret_cast<const v4u*>(hst + row * 32 + qq * 8);
+        st_sc1(hv, r, (int)(((b_lo + row) * H + m * 32 + qq * 8) * 2));
+        if constexpr (BIO)   // the layer output is the same bf16 h: one plain 16-byte store per lane
+          *reinterpret_cast<v4u*>(static_cast<bf16_t*>(a.out) + ((size_t)(b_lo + row) * a.T + t) * H + m * 32 + qq * 8) = hv;
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (lane == 0) signal(cnt);
@@ -187,7 +206,7 @@ __global__ __launch_bounds__(512, 1) void lstm_seq_fwd_kernel(LstmSeqArgs a) {
 // ------------------------------------------------------------------------------------------------ backward
 // Wave w: unit tile ut = w & 1 (16 units), gate block q = w >> 1 (K chunk of H). A[unit][k] = W[q H + k][unit]
 // gathered once; B = dg_{t+1}[batch][q H + k] from LDS; D[unit][batch] partials summed over q in LDS.
-template <int KS>
+template <int KS, bool BIO>
 __global__ __launch_bounds__(512, 1) void lstm_seq_bwd_kernel(LstmSeqArgs a) {
   constexpr int H = KS * 32, G4 = 4 * H;
   constexpr int DP = G4 + 8;
@@ -230,7 +249,10 @@ __global__ __launch_bounds__(512, 1) void lstm_seq_bwd_kernel(LstmSeqArgs a) {
     const int t = a.T - 1 - i;
     float dh = 0.f, ig = 0.f, gg = 0.f, fg = 0.f, og = 0.f, cv = 0.f, cp = 0.f;
     if (t >= 0) {
-      if (a.dout) dh = a.dout[((size_t)b * a.T + t) * H + j];
+      if (a.dout) {
+        const size_t o = ((size_t)b * a.T + t) * H + j;
+        dh = BIO ? bf2f(static_cast<const bf16_t*>(a.dout)[o]) : static_cast<const float*>(a.dout)[o];
+      }
       if (i == 0 && a.dhT) dh += a.dhT[(size_t)b * H + j];
       const float* ap = a.acts + ((size_t)t * a.B + b) * G4 + j;
       ig = ap[0]; gg = ap[H]; fg = ap[2 * H]; og = ap[3 * H];
@@ -287,8 +309,8 @@ __global__ __launch_bounds__(512, 1) void lstm_seq_bwd_kernel(LstmSeqArgs a) {
     const float df = dcv * cp * fg * (1.f - fg);
     const float dog = dh * tc * og * (1.f - og);
     dc = dcv * fg;
-    if (live) {
-      float* gp = a.dxg + ((size_t)b * a.T + t) * G4 + j;
+    if (!BIO && live) {
+      float* gp = static_cast<float*>(a.dxg) + ((size_t)b * a.T + t) * G4 + j;
       gp[0] = di; gp[H] = dgg; gp[2 * H] = df; gp[3 * H] = dog;
     }
     dst[(bb * 4 + 0) * 32 + jj] = f2bf(di);
@@ -301,9 +323,13 @@ __global__ __launch_bounds__(512, 1) void lstm_seq_bwd_kernel(LstmSeqArgs a) {
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const int cidx = lane + 64 * k, row = cidx >> 4, gt = (cidx >> 2) & 3, qq = cidx & 3;
-        if (row < nb)
-          st_sc1(*reinterpret_cast<const v4u*>(dst + (row * 4 + gt) * 32 + qq * 8), r,
-                 (int)(((b_lo + row) * G4 + gt * H + m * 32 + qq * 8) * 2));
+        if (row < nb) {
+          const v4u gv = *reinterpret_cast<const v4u*>(dst + (row * 4 + gt) * 32 + qq * 8);
+          st_sc1(gv, r, (int)(((b_lo + row) * G4 + gt * H + m * 32 + qq * 8) * 2));
+          if constexpr (BIO)   // the input-projection gradient is the same bf16 dg: plain 16-byte store
+            *reinterpret_cast<v4u*>(static_cast<bf16_t*>(a.dxg) + ((size_t)(b_lo + row) * a.T + t) * G4 + gt * H + m * 32 +
+                                    qq * 8) = gv;
+        }
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (lane == 0) signal(cnt);
@@ -345,34 +371,46 @@ int bigdl_lstm_seq_supported(int B, int H) { return seq_shape_ok(B, H) ? 1 : 0; 
 void bigdl_set_lstm_seq(int v) { g_lstm_seq = v; }
 int bigdl_lstm_seq_sync_words() { return NGRP * CNT_STRIDE + CNT_STRIDE; }
 
-int bigdl_lstm_seq_fwd(const uint16_t* W16, const float* xg, const float* c0, uint16_t* h16, float* out, float* cs,
-                       float* acts, unsigned* sync, int B, int H, int T, hipStream_t st) {
+int bigdl_lstm_seq_fwd(const uint16_t* W16, const void* xg, const float* c0, uint16_t* h16, void* out, float* hT,
+                       float* cs, float* acts, unsigned* sync, int B, int H, int T, int bf16io, hipStream_t st) {
   if (!seq_shape_ok(B, H) || T <= 0) return -1;
   LstmSeqArgs a{};
-  a.W16 = W16; a.xg = xg; a.c0 = c0; a.h16 = h16; a.out = out; a.cs = cs; a.acts = acts; a.sync = sync;
+  a.W16 = W16; a.xg = xg; a.c0 = c0; a.h16 = h16; a.out = out; a.hT = hT; a.cs = cs; a.acts = acts; a.sync = sync;
   a.B = B; a.H = H; a.T = T; a.Bg = (B + NGRP - 1) / NGRP;
   if (hipMemsetAsync(sync, 0, sizeof(unsigned) * bigdl_lstm_seq_sync_words(), st) != hipSuccess) return -2;
   const dim3 grid(NGRP * (H / 32));
-  if (H == 1024) lstm_seq_fwd_kernel<32><<<grid, 512, 0, st>>>(a);
-  else if (H == 512) lstm_seq_fwd_kernel<16><<<grid, 512, 0, st>>>(a);
-  else lstm_seq_fwd_kernel<8><<<grid, 512, 0, st>>>(a);
+#define SEQ_FWD(K)                                                  \
+  do {                                                              \
+    if (bf16io) lstm_seq_fwd_kernel<K, true><<<grid, 512, 0, st>>>(a); \
+    else lstm_seq_fwd_kernel<K, false><<<grid, 512, 0, st>>>(a);       \
+  } while (0)
+  if (H == 1024) SEQ_FWD(32);
+  else if (H == 512) SEQ_FWD(16);
+  else SEQ_FWD(8);
+#undef SEQ_FWD
   HIP_LAUNCH_CHECK();
   return 0;
 }
 
-int bigdl_lstm_seq_bwd(const uint16_t* W16, const float* dout, const float* dhT, const float* dcT, const float* acts,
-                       const float* cs, const float* c0, uint16_t* dg16, float* dxg, float* dc0, float* dh0,
-                       unsigned* sync, int B, int H, int T, hipStream_t st) {
+int bigdl_lstm_seq_bwd(const uint16_t* W16, const void* dout, const float* dhT, const float* dcT, const float* acts,
+                       const float* cs, const float* c0, uint16_t* dg16, void* dxg, float* dc0, float* dh0,
+                       unsigned* sync, int B, int H, int T, int bf16io, hipStream_t st) {
   if (!seq_shape_ok(B, H) || T <= 0) return -1;
   LstmSeqArgs a{};
-  a.W16 = W16; a.dout = dout; a.dhT = dhT; a.dcT = dcT; a.acts = const_cast<float*>(acts); a.cs = const_cast<float*>(cs); a.c0 = c0; a.dg16 = dg16;
-  a.dxg = dxg; a.dc0 = dc0; a.dh0 = dh0; a.sync = sync;
+  a.W16 = W16; a.dout = dout; a.dhT = dhT; a.dcT = dcT; a.acts = const_cast<float*>(acts);
+  a.cs = const_cast<float*>(cs); a.c0 = c0; a.dg16 = dg16; a.dxg = dxg; a.dc0 = dc0; a.dh0 = dh0; a.sync = sync;
   a.B = B; a.H = H; a.T = T; a.Bg = (B + NGRP - 1) / NGRP;
   if (hipMemsetAsync(sync, 0, sizeof(unsigned) * bigdl_lstm_seq_sync_words(), st) != hipSuccess) return -2;
   const dim3 grid(NGRP * (H / 32));
-  if (H == 1024) lstm_seq_bwd_kernel<32><<<grid, 512, 0, st>>>(a);
-  else if (H == 512) lstm_seq_bwd_kernel<16><<<grid, 512, 0, st>>>(a);
-  else lstm_seq_bwd_kernel<8><<<grid, 512, 0, st>>>(a);
+#define SEQ_BWD(K)                                                  \
+  do {                                                              \
+    if (bf16io) lstm_seq_bwd_kernel<K, true><<<grid, 512, 0, st>>>(a); \
+    else lstm_seq_bwd_kernel<K, false><<<grid, 512, 0, st>>>(a);       \
+  } while (0)
+  if (H == 1024) SEQ_BWD(32);
+  else if (H == 512) SEQ_BWD(16);
+  else SEQ_BWD(8);
+#undef SEQ_BWD
   HIP_LAUNCH_CHECK();
   return 0;
 }

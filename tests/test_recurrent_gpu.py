@@ -180,7 +180,32 @@ def test_persistent_lstm_sequence_matches_step_kernels(B, T, H):
     out = torch.empty(B, T, H, device="cuda")
     cs, acts = torch.empty(T, B, H, device="cuda"), torch.empty(T, B, 4 * H, device="cuda")
     sync = torch.full((C.lstm_seq_sync_words(),), 7, dtype=torch.int32, device="cuda")
-    C.lstm_seq_fwd(W16, xg.cuda(), c0.cuda(), h16, out, cs, acts, sync)
+    C.lstm_seq_fwd(W16, xg.cuda(), c0.cuda(), h16, out, None, cs, acts, sync)
     torch.cuda.synchronize()
     assert int(sync[8 * 32].item()) == 0
     assert _rel(out, res[0][0]) < 1e-2
+
+
+@pytest.mark.parametrize("B,T,H", [(128, 12, 1024), (40, 5, 256)])
+def test_persistent_lstm_bf16_io_matches_f32_io(B, T, H):
+    """bf16 gate inputs / outputs / gradients (the projection GEMMs' dtype, no f32 round trip) vs the f32-I/O launch of
+    the same kernels: outputs, final state and all four gradients within bf16 rounding of the I/O tensors."""
+    from bigdl_amd.nn.recurrent import _LSTMSeq
+
+    torch.manual_seed(3)
+    xg = (torch.randn(B, T, 4 * H) * 0.5).to(torch.bfloat16).float()
+    h0, c0 = torch.randn(B, H) * 0.5, torch.randn(B, H) * 0.5
+    U = (torch.randn(4 * H, H) / H ** 0.5).to(torch.bfloat16).float()
+    go = torch.randn(B, T, H).to(torch.bfloat16).float()
+    gh, gc = torch.randn(B, H), torch.randn(B, H)
+    res = {}
+    for dt in (torch.float32, torch.bfloat16):
+        dev = [xg.cuda().to(dt).requires_grad_(True)] + [t.cuda().requires_grad_(True) for t in (h0, c0, U)]
+        out, hT, cT = _LSTMSeq.apply(*dev)
+        assert out.dtype == dt and hT.dtype == torch.float32
+        torch.autograd.backward([out, hT, cT], [go.cuda().to(dt), gh.cuda(), gc.cuda()])
+        torch.cuda.synchronize()
+        res[dt] = [out.detach().float(), hT.detach(), cT.detach()] + [d.grad.float() for d in dev]
+    for a, b in zip(res[torch.bfloat16], res[torch.float32]):
+        assert torch.isfinite(a).all()
+        assert _rel(a, b) < 1.5e-2, _rel(a, b)
