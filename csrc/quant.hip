@@ -337,6 +337,125 @@ __global__ __launch_bounds__(256, 2) void conv_i8_glds_kernel(ConvArgs a, I8Epi 
   }
 }
 
+// int8 conv epilogue of one wave's TM x TN accumulator tile, in NH row chunks through the wave-private LDS slice wl:
+// dequantize (x scale per sample x per-channel weight scale), bias, int8 residual addend, ReLU, then int8 (requantized
+// with the consumer's scale), fp32 or bf16 stores; each lane finishes CPL channels of one pixel (CPL = 16: one
+// 16-byte int8 store / addend load per lane instead of two 8-byte ones).
+template <int MI, int NI, int TM, int TN, int NH, int CPL>
+__device__ __forceinline__ void i8_tile_epilogue(const ConvArgs& a, const I8Epi& ep, v4i (&acc)[MI][NI], int mbase,
+                                                 int nbase, int lane, float* wl) {
+  constexpr int GR = TN / 4, LPR = TN / CPL, PPI = 64 / LPR, NR = TM / PPI, MIH = MI / NH, NRH = NR / NH;
+  const int ohw = a.OH * a.OW;
+  constexpr int GPL = CPL / 4;   // fp32 granules per lane
+  auto gpos = [](int p, int g) { return (p * GR + (g ^ (p & (GR - 1)))) * 4; };
+  const int q = lane % LPR;
+  const int n = nbase + q * CPL;
+  const bool nok = n < a.Ncol;
+  const bool full = n + CPL <= a.Ncol;
+  float wsc[CPL], bs[CPL];
+#pragma unroll
+  for (int e = 0; e < CPL; ++e) {
+    const bool ok = n + e < a.Ncol;
+    wsc[e] = ok ? ep.wscale[n + e] : 0.f;
+    bs[e] = (ok && a.bias) ? a.bias[n + e] : 0.f;
+  }
+#pragma unroll
+  for (int h = 0; h < NH; ++h) {
+#pragma unroll
+    for (int i = 0; i < MIH; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        const v4i v = acc[h * MIH + i][j];
+        *reinterpret_cast<v4f*>(wl + gpos(i * 16 + (lane & 15), j * 4 + (lane >> 4))) =
+            v4f{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
+      }
+    __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's LDS writes landed (wave-private slice)
+#pragma unroll
+    for (int r = 0; r < NRH; ++r) {
+      const int p = r * PPI + lane / LPR;
+      const int m = mbase + h * (TM / NH) + p;
+      float v[CPL];
+#pragma unroll
+      for (int g = 0; g < GPL; ++g) {
+        const v4f t = *reinterpret_cast<const v4f*>(wl + gpos(p, GPL * q + g));
+        v[4 * g] = t[0]; v[4 * g + 1] = t[1]; v[4 * g + 2] = t[2]; v[4 * g + 3] = t[3];
+      }
+      if (m >= a.M || !nok) continue;
+      const float xs = ep.xscale ? ep.xscale[m / ohw] : ep.xs_const;
+      float ad[CPL];
+#pragma unroll
+      for (int e = 0; e < CPL; ++e) ad[e] = 0.f;
+      if (ep.add8) {
+        const int8_t* ap = ep.add8 + (size_t)m * ep.add_ld + n;
+        if (full && ((reinterpret_cast<uintptr_t>(ap) & (CPL - 1)) == 0)) {
+          unsigned u[CPL / 4];
+          if constexpr (CPL == 16) {
+            const v4u w = *reinterpret_cast<const v4u*>(ap);
+            u[0] = w[0]; u[1] = w[1]; u[2] = w[2]; u[3] = w[3];
+          } else {
+            const v2u w = *reinterpret_cast<const v2u*>(ap);
+            u[0] = w[0]; u[1] = w[1];
+          }
+#pragma unroll
+          for (int e = 0; e < CPL; ++e) ad[e] = (float)(int8_t)((u[e >> 2] >> (8 * (e & 3))) & 0xff) * ep.add_scale;
+        } else {
+#pragma unroll
+          for (int e = 0; e < CPL; ++e) ad[e] = n + e < a.Ncol ? (float)ap[e] * ep.add_scale : 0.f;
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < CPL; ++e) {
+        v[e] = v[e] * xs * wsc[e] + bs[e] + ad[e];
+        if (a.relu) v[e] = fmaxf(v[e], 0.f);
+      }
+      const size_t off = (size_t)m * a.ldo + n;
+      if (ep.out_mode == 2) {
+        int8_t* o = reinterpret_cast<int8_t*>(a.out) + off;
+        unsigned pk[CPL / 4];
+#pragma unroll
+        for (int g = 0; g < CPL / 4; ++g) pk[g] = 0u;
+#pragma unroll
+        for (int e = 0; e < CPL; ++e) {
+          const int qv = max(-127, min(127, __float2int_rn(v[e] * ep.out_inv)));
+          pk[e >> 2] |= (unsigned)(qv & 0xff) << (8 * (e & 3));
+        }
+        if (full && (reinterpret_cast<uintptr_t>(o) & (CPL - 1)) == 0) {
+          if constexpr (CPL == 16) *reinterpret_cast<v4u*>(o) = v4u{pk[0], pk[1], pk[2], pk[3]};
+          else *reinterpret_cast<v2u*>(o) = v2u{pk[0], pk[1]};
+        } else {
+#pragma unroll
+          for (int e = 0; e < CPL; ++e)
+            if (n + e < a.Ncol) o[e] = (int8_t)((pk[e >> 2] >> (8 * (e & 3))) & 0xff);
+        }
+      } else if (ep.out_mode == 1) {
+        float* o = reinterpret_cast<float*>(a.out) + off;
+        if (full && (reinterpret_cast<uintptr_t>(o) & 15) == 0) {
+#pragma unroll
+          for (int g = 0; g < CPL / 4; ++g)
+            *reinterpret_cast<v4f*>(o + 4 * g) = v4f{v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]};
+        } else {
+#pragma unroll
+          for (int e = 0; e < CPL; ++e)
+            if (n + e < a.Ncol) o[e] = v[e];
+        }
+      } else {
+        bf16_t* o = a.out + off;
+        if (full && (reinterpret_cast<uintptr_t>(o) & 15) == 0) {
+#pragma unroll
+          for (int g = 0; g < CPL / 8; ++g)
+            *reinterpret_cast<v4u*>(o + 8 * g) = v4u{pack2bf(v[8 * g], v[8 * g + 1]), pack2bf(v[8 * g + 2], v[8 * g + 3]),
+                                                     pack2bf(v[8 * g + 4], v[8 * g + 5]), pack2bf(v[8 * g + 6], v[8 * g + 7])};
+        } else {
+#pragma unroll
+          for (int e = 0; e < CPL; ++e)
+            if (n + e < a.Ncol) o[e] = f2bf(v[e]);
+        }
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);   // the slice is rewritten by the next half
+  }
+}
+
 // 128 x 128 int8 tile with the counted-vmcnt pipeline of conv_nt_g4_kernel (conv_igemm.hip): 64-byte LDS rows (one
 // i8 MFMA K-step of 64 = four 16-byte granules, slot g ^ ((r >> 1) & 3)), THREE stages of 16 KB with two K-steps in
 // flight across every raw s_barrier (the 2-stage kernel above drains its DMA queue with __syncthreads every
@@ -477,118 +596,184 @@ __global__ __launch_bounds__(256, (BM + (BN + 63) / 64 * 64) * 64 * 3 <= 52 * 10
     cur = cur == 2 ? 0 : cur + 1;
   }
 
-  // ---- epilogue (conv_i8_glds_kernel's), in NH row halves through a wave-private LDS slice; each lane finishes CPL
-  // channels of one pixel (CPL = 16: one 16-byte int8 store / addend load per lane instead of two 8-byte ones)
-  constexpr int GR = TN / 4, LPR = TN / CPL, PPI = 64 / LPR, NR = TM / PPI, MIH = MI / NH, NRH = NR / NH;
-  constexpr int GPL = CPL / 4;   // fp32 granules per lane
-  float* wl = reinterpret_cast<float*>(lds) + wave * (TM / NH) * TN;
-  auto gpos = [](int p, int g) { return (p * GR + (g ^ (p & (GR - 1)))) * 4; };
-  const int q = lane % LPR;
-  const int n = n0 + wn * TN + q * CPL;
-  const bool nok = n < a.Ncol;
-  const bool full = n + CPL <= a.Ncol;
-  float wsc[CPL], bs[CPL];
+  // ---- epilogue (conv_i8_glds_kernel's), in NH row halves through a wave-private LDS slice
+  i8_tile_epilogue<MI, NI, TM, TN, NH, CPL>(a, ep, acc, m0 + wm * TM, n0 + wn * TN, lane,
+                                           reinterpret_cast<float*>(lds) + wave * (TM / NH) * TN);
+}
+
+// 256 x 256 int8 tile on the phase-interleaved schedule of conv_nt_p8_kernel (conv_igemm.hip: pieces, phases, counted
+// waits, wave-group stagger — see there): 8 waves of 128 x 64, two 64 KB LDS buffers of four 16 KB pieces of 128 rows
+// x 128 B. A 128-byte row is one K-tile of 128 int8 = two i8 MFMA K-steps of 64, so the byte-level schedule is the bf16
+// kernel's unchanged; the MFMA is v_mfma_i32_16x16x64_i8 and the epilogue i8_tile_epilogue (4 row chunks through the
+// buffers). Fast-K only (Cs % 128 == 0: a K-tile lies in one tap).
+__global__ __launch_bounds__(512, 2) void conv_i8_p8_kernel(ConvArgs a, I8Epi ep) {
+  constexpr int BM = 256, BN = 256, BKB = 128;
+  constexpr int WGM = 2, WGN = 4;
+  constexpr int TM = BM / WGM, TN = BN / WGN;      // 128 x 64 per wave
+  constexpr int MI = TM / 16, NI = TN / 16;        // 8 x 4 MFMA tiles
+  constexpr int PIECE = 128 * BKB;                 // bytes (16 KB)
+  constexpr int BUF = 4 * PIECE;                   // 64 KB
+  constexpr int NH = 4;
+  static_assert(8 * (TM / NH) * TN * 4 <= 2 * BUF, "epilogue chunk must fit the buffers");
+  __shared__ __attribute__((aligned(1024))) uint8_t lds[2 * BUF + 6 * CONV_MAX_TAPS];
+  short* taps = reinterpret_cast<short*>(lds + 2 * BUF);
+  const uint8_t* src8 = reinterpret_cast<const uint8_t*>(a.src);
+  const uint8_t* wt8 = reinterpret_cast<const uint8_t*>(a.wt);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WGN, wn = wave % WGN;
+  const int tiles_n = (a.Ncol + BN - 1) / BN;
+  const int tiles_m = (a.M + BM - 1) / BM;
+  const int nwg = tiles_m * tiles_n;
+  const int bid = xcd_remap(blockIdx.x, nwg);
+  const int tm = bid / tiles_n, tn = bid % tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int nk = a.Kdim / BKB;
+
+  // DMA geometry as conv_nt_p8_kernel: instruction j of wave w fills piece rows (j * 8 + w) * 8 .. +8; lane -> row
+  // + (lane >> 3), slot lane & 7 holding granule (lane & 7) ^ (lane >> 3)
+  const int gsrc = (lane & 7) ^ (lane >> 3);
+  const int ohw = a.OH * a.OW;
+  int a_pix[4], a_h[4], a_w[4];
+  const uint8_t* wrow[4];
+  bool bvalid[4];
 #pragma unroll
-  for (int e = 0; e < CPL; ++e) {
-    const bool ok = n + e < a.Ncol;
-    wsc[e] = ok ? ep.wscale[n + e] : 0.f;
-    bs[e] = (ok && a.bias) ? a.bias[n + e] : 0.f;
+  for (int q2 = 0; q2 < 4; ++q2) {
+    const int q = q2 >> 1, lr = ((q2 & 1) * 8 + wave) * 8 + (lane >> 3);
+    const int m = m0 + (lr >> 6) * 128 + q * 64 + (lr & 63);
+    if (m < a.M) {
+      const int nb = m / ohw, rem = m - nb * ohw;
+      const int oh = rem / a.OW, ow = rem - oh * a.OW;
+      a_pix[q2] = nb * a.Hs * a.Ws;
+      a_h[q2] = oh * a.mul_h;
+      a_w[q2] = ow * a.mul_w;
+    } else {
+      a_pix[q2] = 0; a_h[q2] = -(1 << 28); a_w[q2] = -(1 << 28);
+    }
+    const int n = n0 + (lr >> 5) * 64 + q * 32 + (lr & 31);
+    bvalid[q2] = n < a.Ncol;
+    wrow[q2] = wt8 + (size_t)(bvalid[q2] ? n : 0) * a.ldw + gsrc * 16;
   }
+  if (tid < a.ntaps) {
+    taps[tid] = a.tap_h[tid];
+    taps[CONV_MAX_TAPS + tid] = a.tap_w[tid];
+    taps[2 * CONV_MAX_TAPS + tid] = a.tap_k[tid];
+  }
+  __syncthreads();
+
+  auto issue = [&](int kt, int buf, int P) {
+    const int k0 = kt * BKB;
+    const int t = k0 / a.Cs;
+    const int cin = k0 - t * a.Cs;
+    uint8_t* base = lds + buf * BUF + P * PIECE;
+    const int q = P >> 1;
+    if ((P & 1) == 0) {
+      const int th = taps[t], tw = taps[CONV_MAX_TAPS + t];
+      const int c = cin + gsrc * 16;
 #pragma unroll
-  for (int h = 0; h < NH; ++h) {
-#pragma unroll
-    for (int i = 0; i < MIH; ++i)
-#pragma unroll
-      for (int j = 0; j < NI; ++j) {
-        const v4i v = acc[h * MIH + i][j];
-        *reinterpret_cast<v4f*>(wl + gpos(i * 16 + (lane & 15), j * 4 + (lane >> 4))) =
-            v4f{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
+      for (int j = 0; j < 2; ++j) {
+        const int q2 = q * 2 + j;
+        const int ch = a_h[q2] + th, cw = a_w[q2] + tw;
+        const bool ok = (unsigned)ch < (unsigned)a.Hs && (unsigned)cw < (unsigned)a.Ws;
+        const uint8_t* g = ok ? src8 + (size_t)(a_pix[q2] + ch * a.Ws + cw) * a.Cs + c : g_zero16;
+        glds16(g, (LDS_PTR(void))(base + (j * 8 + wave) * 8 * BKB));
       }
-    __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's LDS writes landed (wave-private slice)
+    } else {
+      const int wk = taps[2 * CONV_MAX_TAPS + t] * a.Cs + cin;
 #pragma unroll
-    for (int r = 0; r < NRH; ++r) {
-      const int p = r * PPI + lane / LPR;
-      const int m = m0 + wm * TM + h * (TM / NH) + p;
-      float v[CPL];
-#pragma unroll
-      for (int g = 0; g < GPL; ++g) {
-        const v4f t = *reinterpret_cast<const v4f*>(wl + gpos(p, GPL * q + g));
-        v[4 * g] = t[0]; v[4 * g + 1] = t[1]; v[4 * g + 2] = t[2]; v[4 * g + 3] = t[3];
-      }
-      if (m >= a.M || !nok) continue;
-      const float xs = ep.xscale ? ep.xscale[m / ohw] : ep.xs_const;
-      float ad[CPL];
-#pragma unroll
-      for (int e = 0; e < CPL; ++e) ad[e] = 0.f;
-      if (ep.add8) {
-        const int8_t* ap = ep.add8 + (size_t)m * ep.add_ld + n;
-        if (full && ((reinterpret_cast<uintptr_t>(ap) & (CPL - 1)) == 0)) {
-          unsigned u[CPL / 4];
-          if constexpr (CPL == 16) {
-            const v4u w = *reinterpret_cast<const v4u*>(ap);
-            u[0] = w[0]; u[1] = w[1]; u[2] = w[2]; u[3] = w[3];
-          } else {
-            const v2u w = *reinterpret_cast<const v2u*>(ap);
-            u[0] = w[0]; u[1] = w[1];
-          }
-#pragma unroll
-          for (int e = 0; e < CPL; ++e) ad[e] = (float)(int8_t)((u[e >> 2] >> (8 * (e & 3))) & 0xff) * ep.add_scale;
-        } else {
-#pragma unroll
-          for (int e = 0; e < CPL; ++e) ad[e] = n + e < a.Ncol ? (float)ap[e] * ep.add_scale : 0.f;
-        }
-      }
-#pragma unroll
-      for (int e = 0; e < CPL; ++e) {
-        v[e] = v[e] * xs * wsc[e] + bs[e] + ad[e];
-        if (a.relu) v[e] = fmaxf(v[e], 0.f);
-      }
-      const size_t off = (size_t)m * a.ldo + n;
-      if (ep.out_mode == 2) {
-        int8_t* o = reinterpret_cast<int8_t*>(a.out) + off;
-        unsigned pk[CPL / 4];
-#pragma unroll
-        for (int g = 0; g < CPL / 4; ++g) pk[g] = 0u;
-#pragma unroll
-        for (int e = 0; e < CPL; ++e) {
-          const int qv = max(-127, min(127, __float2int_rn(v[e] * ep.out_inv)));
-          pk[e >> 2] |= (unsigned)(qv & 0xff) << (8 * (e & 3));
-        }
-        if (full && (reinterpret_cast<uintptr_t>(o) & (CPL - 1)) == 0) {
-          if constexpr (CPL == 16) *reinterpret_cast<v4u*>(o) = v4u{pk[0], pk[1], pk[2], pk[3]};
-          else *reinterpret_cast<v2u*>(o) = v2u{pk[0], pk[1]};
-        } else {
-#pragma unroll
-          for (int e = 0; e < CPL; ++e)
-            if (n + e < a.Ncol) o[e] = (int8_t)((pk[e >> 2] >> (8 * (e & 3))) & 0xff);
-        }
-      } else if (ep.out_mode == 1) {
-        float* o = reinterpret_cast<float*>(a.out) + off;
-        if (full && (reinterpret_cast<uintptr_t>(o) & 15) == 0) {
-#pragma unroll
-          for (int g = 0; g < CPL / 4; ++g)
-            *reinterpret_cast<v4f*>(o + 4 * g) = v4f{v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]};
-        } else {
-#pragma unroll
-          for (int e = 0; e < CPL; ++e)
-            if (n + e < a.Ncol) o[e] = v[e];
-        }
-      } else {
-        bf16_t* o = a.out + off;
-        if (full && (reinterpret_cast<uintptr_t>(o) & 15) == 0) {
-#pragma unroll
-          for (int g = 0; g < CPL / 8; ++g)
-            *reinterpret_cast<v4u*>(o + 8 * g) = v4u{pack2bf(v[8 * g], v[8 * g + 1]), pack2bf(v[8 * g + 2], v[8 * g + 3]),
-                                                     pack2bf(v[8 * g + 4], v[8 * g + 5]), pack2bf(v[8 * g + 6], v[8 * g + 7])};
-        } else {
-#pragma unroll
-          for (int e = 0; e < CPL; ++e)
-            if (n + e < a.Ncol) o[e] = f2bf(v[e]);
-        }
+      for (int j = 0; j < 2; ++j) {
+        const int q2 = q * 2 + j;
+        const uint8_t* g = bvalid[q2] ? wrow[q2] + wk : g_zero16;
+        glds16(g, (LDS_PTR(void))(base + (j * 8 + wave) * 8 * BKB));
       }
     }
-    __builtin_amdgcn_s_waitcnt(0xc07f);   // the slice is rewritten by the next half
+  };
+  // fragment of K-step kh (64 int8 = 4 granules): granule kh * 4 + (lane >> 4) of row (lane & 15) at slot ^ (lane & 7)
+  const int fo0 = (lane & 15) * BKB + (((lane >> 4)) ^ (lane & 7)) * 16;
+  const int fo1 = (lane & 15) * BKB + ((4 + (lane >> 4)) ^ (lane & 7)) * 16;
+  const int a_row = wm * 64 * BKB;
+  const int b_row = wn * 32 * BKB;
+
+  v4i acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = v4i{0, 0, 0, 0};
+  v4i fa[4][2], fb[NI][2];
+  auto quad = [&](int ib, int jb) {
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[ib + i][jb + j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fb[jb + j][kh], fa[i][kh], acc[ib + i][jb + j], 0, 0, 0);
+  };
+  auto read_a = [&](const uint8_t* P) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      fa[i][0] = *reinterpret_cast<const v4i*>(P + a_row + i * 16 * BKB + fo0);
+      fa[i][1] = *reinterpret_cast<const v4i*>(P + a_row + i * 16 * BKB + fo1);
+    }
+  };
+  auto read_b = [&](const uint8_t* P, int jb) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      fb[jb + j][0] = *reinterpret_cast<const v4i*>(P + b_row + j * 16 * BKB + fo0);
+      fb[jb + j][1] = *reinterpret_cast<const v4i*>(P + b_row + j * 16 * BKB + fo1);
+    }
+  };
+  auto compute = [&](int ib, int jb) {
+    __builtin_amdgcn_s_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+    quad(ib, jb);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+  };
+
+  if (nk > 0) {
+    issue(0, 0, 0); issue(0, 0, 1); issue(0, 0, 3); issue(0, 0, 2);
   }
+  if (nk > 1) {
+    issue(1, 1, 0); issue(1, 1, 1);
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  if (wm == 1) __builtin_amdgcn_s_barrier();   // stagger
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    const uint8_t* L = lds + cur * BUF;
+    const bool n1 = kt + 1 < nk, n2 = kt + 2 < nk;
+    if (n1) issue(kt + 1, cur ^ 1, 3);
+    read_a(L); read_b(L + PIECE, 0);
+    if (n1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    compute(0, 0);
+    if (n1) issue(kt + 1, cur ^ 1, 2);
+    read_b(L + 3 * PIECE, 2);
+    if (n1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    compute(0, 2);
+    if (n2) issue(kt + 2, cur, 0);
+    read_a(L + 2 * PIECE);
+    compute(4, 2);
+    if (n2) issue(kt + 2, cur, 1);
+    if (n2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (n1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    compute(4, 0);
+  }
+  if (wm == 0) __builtin_amdgcn_s_barrier();   // balance the stagger
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();                            // every wave is done with the buffers before the epilogue reuses them
+  i8_tile_epilogue<MI, NI, TM, TN, NH, 16>(a, ep, acc, m0 + wm * TM, n0 + wn * TN, lane,
+                                           reinterpret_cast<float*>(lds) + wave * (TM / NH) * TN);
 }
 
 // int8 rows [rows][C] from src (row stride lds) into dst (row stride ldd): a concat input that was not produced in place
@@ -845,6 +1030,17 @@ static bool i8_g3() {
   return g_i8_g3 != 0;
 }
 void bigdl_set_i8_g3(int v) { g_i8_g3 = v; }
+// BIGDL_I8_P8 (default 1): the 256 x 256 phase-interleaved int8 kernel for Cs % 128 == 0, Kdim >= 1024, Ncol >= 256
+// and >= 160 tiles (the bf16 kernel's rule); 2: whenever the shape allows (tests); 0: off
+int g_i8_p8 = -1;
+static bool i8_p8() {
+  if (g_i8_p8 < 0) {
+    const char* e = getenv("BIGDL_I8_P8");
+    g_i8_p8 = e ? atoi(e) : 1;
+  }
+  return g_i8_p8 != 0;
+}
+void bigdl_set_i8_p8(int v) { g_i8_p8 = v; }
 void bigdl_set_i8_cpl(int v) { g_i8_cpl = v; }
 int bigdl_get_i8_cpl() { return i8_cpl(); }
 int bigdl_get_i8_g3() { return i8_g3() ? g_i8_g3 : 0; }
@@ -857,7 +1053,11 @@ int bigdl_conv_i8(const ConvArgs* a, const float* xscale, float xs_const, const 
   const I8Epi ep{xscale, xs_const, wscale, out_mode, out_inv, add8, add_scale, add_ld};
   const bool fk = a->Cs % QBK == 0;
   const bool g3fk = a->Cs % 64 == 0;
-  if (a->Ncol <= 64 && i8_g3()) {
+  const long p8_tiles = (long)((a->M + 255) / 256) * ((a->Ncol + 255) / 256);
+  if (i8_p8() && fk && a->Kdim >= 1024 && a->Ncol >= 256 && a->Ncol % 16 == 0 &&
+      (g_i8_p8 == 2 || p8_tiles >= 160)) {
+    conv_i8_p8_kernel<<<dim3((unsigned)p8_tiles), dim3(512), 0, st>>>(*a, ep);
+  } else if (a->Ncol <= 64 && i8_g3()) {
     const int bn = a->Ncol <= 32 ? 32 : 64;
     const int g = ((a->M + 255) / 256) * ((a->Ncol + bn - 1) / bn);
     if (bn == 32) launch_i8_g3<256, 32, 4, 1>(g, g3fk, *a, ep, st);

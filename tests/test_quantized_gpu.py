@@ -63,6 +63,26 @@ def test_conv_i8_exact_integer(case, g3, cpl):
         C_.set_i8_cpl(old_cpl)
 
 
+I8_P8_CASES = [
+    (2, 256, 9, 9, 256, 3, 3, 1, 1, 1),     # one 256 x 256 tile, 18 K-tiles, padding taps
+    (3, 1024, 7, 7, 512, 1, 1, 1, 0, 1),    # 1x1, two N tiles, M tail
+    (2, 128, 14, 14, 272, 3, 3, 2, 1, 1),   # stride 2, Ncol tail (272)
+    (5, 512, 7, 7, 2048, 1, 1, 1, 0, 1),    # 8 N tiles
+]
+
+
+@pytest.mark.parametrize("case", I8_P8_CASES)
+def test_conv_i8_p8_exact_integer(case):
+    """256 x 256 phase-interleaved int8 kernel (BIGDL_I8_P8=2 forces it wherever Cs % 128 == 0, Kdim >= 1024,
+    Ncol >= 256): fp32 output equal to the integer conv."""
+    C_ = native.get()
+    C_.set_i8_p8(2)
+    try:
+        _conv_i8_exact(case)
+    finally:
+        C_.set_i8_p8(1)
+
+
 def _conv_i8_exact(case):
     from bigdl_amd.ops.conv import _fwd_taps, out_size
 

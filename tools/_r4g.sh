@@ -10,3 +10,12 @@ done
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/lstmprof -o run -- python3 tools/bench_lstm.py --steps 2 --warmup 1 --batch 128 --graph 0 \
   > gpurun_out/lstm_prof.log 2>&1) || { tail -20 gpurun_out/lstm_prof.log; exit 1; }
 echo done
+timeout -k 10 300 python -u -m pytest tests/test_quantized_gpu.py tests/test_int8_graph_gpu.py -x -q --timeout 120 --timeout-method thread > gpurun_out/r4g_i8test.log 2>&1; rc=$?; tail -3 gpurun_out/r4g_i8test.log; [ $rc -eq 0 ] || exit $rc
+for v in 1 0; do for m in resnet50 inception_v3; do
+  BIGDL_I8_P8=$v timeout -k 10 300 python -u tools/bench_inference.py --model $m --mode int8 > gpurun_out/r4g_inf_${m}_$v.log 2>&1 || { tail -20 gpurun_out/r4g_inf_${m}_$v.log; exit 1; }
+  echo "I8_P8=$v $m $(tail -1 gpurun_out/r4g_inf_${m}_$v.log | cut -c1-220)"
+done; done
+for m in resnet50 inception_v3; do
+  timeout -k 10 300 python -u tools/bench_inference.py --model $m --mode bf16 > gpurun_out/r4g_inf_${m}_bf16.log 2>&1 || { tail -20 gpurun_out/r4g_inf_${m}_bf16.log; exit 1; }
+  echo "bf16 $m $(tail -1 gpurun_out/r4g_inf_${m}_bf16.log | cut -c1-220)"
+done
