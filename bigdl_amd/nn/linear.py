@@ -242,7 +242,19 @@ class LookupTable(TensorModule):
             idx = idx.clamp_min(-1)
         return idx
 
+    def _native_ids(self, input):
+        """GPU fast path: the kernels read the raw 1-based ids (no index tensor, no aten index arithmetic)."""
+        return (input.is_cuda and self.weight.is_cuda and self.weight.dtype == torch.float32
+                and input.dtype in (torch.float32, torch.int64) and self.maxNorm == float("inf"))
+
     def updateOutput(self, input):
+        if self._native_ids(input):
+            from ..ops import native
+
+            ids = input.contiguous()
+            out = torch.empty(tuple(ids.shape) + (self.nOutput,), device=ids.device, dtype=torch.float32)
+            native.get().embedding_fwd_ids(self.weight, ids, out, bool(self.maskZero))
+            return out
         idx = self._idx(input)
         if self.maxNorm != float("inf"):
             with torch.no_grad():
@@ -262,9 +274,23 @@ class LookupTable(TensorModule):
         return out
 
     def updateGradInput(self, input, gradOutput):
-        return torch.zeros_like(input, dtype=torch.float32)
+        gi = torch.empty_like(input, dtype=torch.float32)
+        if gi.is_cuda:
+            from ..ops import native
+
+            native.get().fill_bytes(gi, 0)
+            return gi
+        return gi.zero_()
 
     def accGradParameters(self, input, gradOutput):
+        if (self._native_ids(input) and self.gradWeight.is_cuda and not self.shouldScaleGradByFreq
+                and gradOutput.dtype in (torch.float32, torch.bfloat16)):
+            from ..ops import native
+
+            pad = int(self.paddingValue) - 1 if self.paddingValue != 0 else -1
+            native.get().embedding_bwd_ids(gradOutput.contiguous(), input.contiguous(), self.gradWeight, pad,
+                                           float(self.scaleW))
+            return
         idx = self._idx(input).reshape(-1)
         g = gradOutput.reshape(-1, self.nOutput).float()
         keep = idx >= 0

@@ -799,6 +799,24 @@ void embedding_bwd(const Tensor& gout, const Tensor& idx, const Tensor& gW, doub
   bigdl_embedding_bwd(cf(gout, "gout"), (const long*)idx.data_ptr(), mf(gW, "gW"), idx.numel(), gW.size(1), gW.size(0),
                       scale, stream());
 }
+// LookupTable on its raw 1-based ids (float32 or int64 input tensor): no index tensor, bf16 or f32 output gradient
+void embedding_fwd_ids(const Tensor& W, const Tensor& ids, const Tensor& out, bool mask_zero) {
+  contig(W, "W"); contig(ids, "ids"); contig(out, "out");
+  const bool il = ids.scalar_type() == at::kLong;
+  TORCH_CHECK(W.dim() == 2 && ids.is_cuda() && (il || ids.scalar_type() == at::kFloat), "embedding_fwd_ids: ids f32/i64");
+  TORCH_CHECK(out.numel() == ids.numel() * W.size(1), "embedding_fwd_ids: out size");
+  bigdl_embedding_fwd_ids(cf(W, "W"), ids.data_ptr(), il ? 1 : 0, mf(out, "out"), ids.numel(), W.size(1), W.size(0),
+                          mask_zero ? 1 : 0, stream());
+}
+void embedding_bwd_ids(const Tensor& gout, const Tensor& ids, const Tensor& gW, int64_t pad, double scale) {
+  contig(gout, "gout"); contig(ids, "ids"); contig(gW, "gW");
+  const bool il = ids.scalar_type() == at::kLong, gb = gout.scalar_type() == at::kBFloat16;
+  TORCH_CHECK(gW.dim() == 2 && ids.is_cuda() && (il || ids.scalar_type() == at::kFloat), "embedding_bwd_ids: ids f32/i64");
+  TORCH_CHECK(gb || gout.scalar_type() == at::kFloat, "embedding_bwd_ids: gout f32 or bf16");
+  TORCH_CHECK(gout.numel() == ids.numel() * gW.size(1), "embedding_bwd_ids: gout size");
+  bigdl_embedding_bwd_ids(gout.data_ptr(), gb ? 1 : 0, ids.data_ptr(), il ? 1 : 0, mf(gW, "gW"), ids.numel(), gW.size(1),
+                          gW.size(0), pad, (float)scale, stream());
+}
 void resize_bilinear_fwd(const Tensor& x, const Tensor& y, double sh, double sw) {
   contig(x, "x"); contig(y, "y");
   TORCH_CHECK(x.dim() == 4 && y.dim() == 4 && x.size(0) * x.size(1) == y.size(0) * y.size(1), "resize: shapes");
@@ -1147,6 +1165,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("dropout", &dropout);
   m.def("embedding_fwd", &embedding_fwd);
   m.def("embedding_bwd", &embedding_bwd);
+  m.def("embedding_fwd_ids", &embedding_fwd_ids);
+  m.def("embedding_bwd_ids", &embedding_bwd_ids);
   m.def("resize_bilinear_fwd", &resize_bilinear_fwd);
   m.def("resize_bilinear_bwd", &resize_bilinear_bwd);
   m.def("log_softmax_fwd", &log_softmax_fwd);

@@ -224,6 +224,10 @@ void bigdl_lrn_bwd(const float* x, const float* y, const float* scale, const flo
 void bigdl_dropout(const void* x, void* y, int is_bf16, long n, float p, float mul, unsigned long long seed,
                    hipStream_t st);
 void bigdl_embedding_fwd(const float* W, const long* idx, float* out, long rows, int D, long nIndex, hipStream_t st);
+void bigdl_embedding_fwd_ids(const float* W, const void* ids, int ids_long, float* out, long rows, int D, long nIndex,
+                             int mask_zero, hipStream_t st);
+void bigdl_embedding_bwd_ids(const void* gout, int gout_bf16, const void* ids, int ids_long, float* gW, long rows, int D,
+                             long nIndex, long pad, float scale, hipStream_t st);
 void bigdl_embedding_bwd(const float* gout, const long* idx, float* gW, long rows, int D, long nIndex, float scale,
                          hipStream_t st);
 void bigdl_resize_bilinear_fwd(const float* x, float* y, long NC, int H, int W, int OH, int OW, float sh, float sw,

@@ -155,6 +155,55 @@ __global__ void embedding_bwd_kernel(const float* __restrict__ gout, const long*
   }
 }
 
+// Same gather / scatter-add from the layer's raw 1-based ids (float or int64: LookupTable input), so no index tensor
+// is ever materialised: k = id - 1; forward: k < 0 -> zero row if mask_zero else row 0 (the reference's clamp);
+// backward: rows with k < 0 or k == pad are skipped; the output gradient is f32 or bf16 (GB: bf16).
+template <typename ID>
+__device__ __forceinline__ long emb_id(const ID* ids, long r) { return (long)ids[r] - 1; }
+
+template <typename ID>
+__global__ void embedding_fwd_ids_kernel(const float* __restrict__ W, const ID* __restrict__ ids, float* __restrict__ out,
+                                         long rows, int D, long nIndex, int mask_zero) {
+  const int lane = threadIdx.x & 63;
+  const long wid = (blockIdx.x * (long)blockDim.x + threadIdx.x) >> 6;
+  const long nw = ((long)gridDim.x * blockDim.x) >> 6;
+  for (long r = wid; r < rows; r += nw) {
+    long k = emb_id(ids, r);
+    if (k < 0 && !mask_zero) k = 0;
+    float* o = out + r * D;
+    if (k < 0 || k >= nIndex) {
+      for (int d = lane; d < D; d += 64) o[d] = 0.f;
+      continue;
+    }
+    const float* w = W + k * D;
+    if ((D & 3) == 0) {
+      for (int d = lane; d < (D >> 2); d += 64) reinterpret_cast<float4*>(o)[d] = reinterpret_cast<const float4*>(w)[d];
+    } else {
+      for (int d = lane; d < D; d += 64) o[d] = w[d];
+    }
+  }
+}
+
+template <typename ID, bool GB>
+__global__ void embedding_bwd_ids_kernel(const void* __restrict__ gout, const ID* __restrict__ ids,
+                                         float* __restrict__ gW, long rows, int D, long nIndex, long pad, float scale) {
+  const int lane = threadIdx.x & 63;
+  const long wid = (blockIdx.x * (long)blockDim.x + threadIdx.x) >> 6;
+  const long nw = ((long)gridDim.x * blockDim.x) >> 6;
+  for (long r = wid; r < rows; r += nw) {
+    const long k = emb_id(ids, r);
+    if (k < 0 || k >= nIndex || k == pad) continue;
+    float* w = gW + k * D;
+    if (GB) {
+      const bf16_t* g = static_cast<const bf16_t*>(gout) + r * D;
+      for (int d = lane; d < D; d += 64) atomicAdd(w + d, __uint_as_float((unsigned)g[d] << 16) * scale);
+    } else {
+      const float* g = static_cast<const float*>(gout) + r * D;
+      for (int d = lane; d < D; d += 64) atomicAdd(w + d, g[d] * scale);
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------------ bilinear resize (NCHW)
 // TF legacy mapping src = dst * scale, scale = in/out (align_corners: (in-1)/(out-1)), clamped at the edge.
 __device__ __forceinline__ void bil_src(int o, int in, float scale, int& i0, int& i1, float& f) {
@@ -282,6 +331,28 @@ void bigdl_dropout(const void* x, void* y, int is_bf16, long n, float p, float m
 }
 void bigdl_embedding_fwd(const float* W, const long* idx, float* out, long rows, int D, long nIndex, hipStream_t st) {
   embedding_fwd_kernel<<<blocks_for(rows * 64), 256, 0, st>>>(W, idx, out, rows, D, nIndex);
+  HIP_LAUNCH_CHECK();
+}
+void bigdl_embedding_fwd_ids(const float* W, const void* ids, int ids_long, float* out, long rows, int D, long nIndex,
+                             int mask_zero, hipStream_t st) {
+  if (ids_long)
+    embedding_fwd_ids_kernel<long><<<blocks_for(rows * 64), 256, 0, st>>>(W, (const long*)ids, out, rows, D, nIndex,
+                                                                          mask_zero);
+  else
+    embedding_fwd_ids_kernel<float><<<blocks_for(rows * 64), 256, 0, st>>>(W, (const float*)ids, out, rows, D, nIndex,
+                                                                           mask_zero);
+  HIP_LAUNCH_CHECK();
+}
+void bigdl_embedding_bwd_ids(const void* gout, int gout_bf16, const void* ids, int ids_long, float* gW, long rows, int D,
+                             long nIndex, long pad, float scale, hipStream_t st) {
+  const int g = blocks_for(rows * 64);
+  if (ids_long) {
+    if (gout_bf16) embedding_bwd_ids_kernel<long, true><<<g, 256, 0, st>>>(gout, (const long*)ids, gW, rows, D, nIndex, pad, scale);
+    else embedding_bwd_ids_kernel<long, false><<<g, 256, 0, st>>>(gout, (const long*)ids, gW, rows, D, nIndex, pad, scale);
+  } else {
+    if (gout_bf16) embedding_bwd_ids_kernel<float, true><<<g, 256, 0, st>>>(gout, (const float*)ids, gW, rows, D, nIndex, pad, scale);
+    else embedding_bwd_ids_kernel<float, false><<<g, 256, 0, st>>>(gout, (const float*)ids, gW, rows, D, nIndex, pad, scale);
+  }
   HIP_LAUNCH_CHECK();
 }
 void bigdl_embedding_bwd(const float* gout, const long* idx, float* gW, long rows, int D, long nIndex, float scale,

@@ -392,6 +392,35 @@ def test_embedding_kernels_match_reference():
     assert torch.allclose(lt.gradWeight.cpu(), ref_g, atol=1e-5)
 
 
+@pytest.mark.parametrize("mask_zero,pad,ids_long,gbf16", [(False, 0, False, False), (True, 0, False, True),
+                                                           (False, 3, True, False), (True, 5, True, True)])
+def test_embedding_raw_id_kernels(mask_zero, pad, ids_long, gbf16):
+    """LookupTable's GPU path reads the raw 1-based ids (f32 / int64) in the kernels: zero-id rows (maskZero -> zero
+    row, else row 0), padding ids skipped in the gradient, bf16 output gradients; vs the reference index arithmetic."""
+    from bigdl_amd import nn
+
+    torch.manual_seed(1)
+    lt = nn.LookupTable(40, 16, paddingValue=float(pad), maskZero=mask_zero)
+    ids = torch.randint(0 if mask_zero else 1, 41, (6, 11)).float()
+    ids[0, :3] = 0 if mask_zero else 1
+    if pad:
+        ids[1, :4] = pad
+    idx = ids.long() - 1
+    ref = lt.weight[idx.clamp_min(0)] * ((idx >= 0) | (not mask_zero)).unsqueeze(-1).float()
+    gy = torch.randn(6, 11, 16)
+    if gbf16:
+        gy = gy.to(torch.bfloat16).float()
+    keep = (idx >= 0) & ((idx != pad - 1) if pad else True)
+    ref_g = torch.zeros(40, 16).index_add_(0, idx[keep], gy[keep])
+    lt = lt.to(torch.device("cuda"))
+    x = ids.long().cuda() if ids_long else ids.cuda()
+    out = lt.forward(x)
+    lt.zeroGradParameters()
+    lt.backward(x, gy.cuda().to(torch.bfloat16) if gbf16 else gy.cuda())
+    assert torch.allclose(out.cpu(), ref)
+    assert torch.allclose(lt.gradWeight.cpu(), ref_g, atol=1e-5)
+
+
 def test_resize_bilinear_and_log_softmax_kernels():
     from bigdl_amd.ops import nnk
 

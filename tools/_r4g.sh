@@ -1,6 +1,6 @@
 export PYTHONPATH=$PWD
 mkdir -p gpurun_out/pmcw
-timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py tests/test_recurrent_gpu.py -x -q --timeout 120 --timeout-method thread -k "wgrad_p8 or lstm or recurrent or rnn" > gpurun_out/r4g_test.log 2>&1; rc=$?; tail -3 gpurun_out/r4g_test.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py tests/test_recurrent_gpu.py -x -q --timeout 120 --timeout-method thread -k "wgrad_p8 or lstm or recurrent or rnn or embedding" > gpurun_out/r4g_test.log 2>&1; rc=$?; tail -3 gpurun_out/r4g_test.log; [ $rc -eq 0 ] || exit $rc
 for v in 2 0; do BIGDL_WGRAD_P8=$v timeout -k 10 120 python -u tools/wgrad_p8_probe.py || exit 1; done
 for v in 1 0; do
   BIGDL_WGRAD_P8=$v timeout -k 10 300 python -u tools/bench_lstm.py --steps 10 --warmup 3 --batch 128 > gpurun_out/r4g_lstm_$v.log 2>&1 || { tail -20 gpurun_out/r4g_lstm_$v.log; exit 1; }
