@@ -366,8 +366,8 @@ class TimeDistributedCriterion(AbstractCriterion):
         if self._flat_ok(input, target):       # one launch over B*T rows instead of T small ones
             x, y = self._flat(input, target)
             loss = self.critrn.forward(x, y)
-            loss = loss * T if self.critrn.sizeAverage else loss
-            return loss / T if self.sizeAverage else loss
+            scale = (T if self.critrn.sizeAverage else 1.0) / (T if self.sizeAverage else 1.0)
+            return loss * scale if scale != 1.0 else loss      # (no scalar kernel when the T's cancel)
         loss = 0.0
         for t in range(T):
             loss = loss + self.critrn.forward(input.select(d, t), target.select(d, t) if target.dim() > d else target)

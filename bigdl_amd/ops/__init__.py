@@ -72,7 +72,8 @@ def softmax_xent_gpu(logits, labels, label_base=1.0, size_average=True, need_gra
     B = logits.shape[0]
     logits = logits.contiguous()
     labels = labels.to(dtype=torch.float32).contiguous()
-    loss = torch.zeros(1, dtype=torch.float32, device=logits.device)
+    loss = torch.empty(1, dtype=torch.float32, device=logits.device)
+    native.get().fill_bytes(loss, 0)
     dl = torch.empty_like(logits) if need_grad else None
     scale = 1.0 / B if size_average else 1.0
     native.get().softmax_xent(logits, labels, loss, dl, float(label_base), float(scale))
