@@ -302,13 +302,15 @@ class _LSTMSeq(torch.autograd.Function):
     def forward(ctx, xg, h0, c0, U):
         B, T, G = xg.shape
         H = G // 4
+        if xg.dtype != torch.float32 and not _LSTMSeq._fused_gpu(xg, U):
+            xg = _f32(xg)                   # bf16 inputs outside the whole-sequence kernels' shapes
         if _LSTMSeq._fused_gpu(xg, U):
             # one fused launch per step (csrc/lstm.hip): bf16 MFMA recurrent GEMM + cell in its epilogue
             C = ops.native.get()
             W16 = ops.to_bf16(U.detach())
             out = xg.new_empty(B, T, H)
-            cs = xg.new_empty(T, B, H)
-            acts = xg.new_empty(T, B, G)
+            cs = xg.new_empty(T, B, H, dtype=torch.float32)
+            acts = xg.new_empty(T, B, G, dtype=torch.float32)
             # time-major bf16 states h_{-1..T-1}: step t's GEMM operand, and (rows t*B + b) the B operand of the
             # weight-gradient GEMM after the backward sweep
             h16 = xg.new_empty(T + 1, B, H, dtype=torch.bfloat16)
