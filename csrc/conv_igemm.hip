@@ -2687,7 +2687,7 @@ int bigdl_get_wgrad_g3() { return wgrad_g3() ? 1 : 0; }
 static int p8w_pick(WgradArgs* a) {
   if (g_wgrad_p8 < 0) {
     const char* e = getenv("BIGDL_WGRAD_P8");
-    g_wgrad_p8 = e ? atoi(e) : 0;
+    g_wgrad_p8 = e ? atoi(e) : 1;
   }
   if (!g_wgrad_p8 || conv_impl() < 1 || a->Ncol < 256 || a->Kdim < 256 || (a->Cs % 8) ||
       (a->Ncol % 8) || (a->Kdim % 8) || a->M <= 0)
@@ -2701,10 +2701,18 @@ static int p8w_pick(WgradArgs* a) {
   // tiles its deep pixel split turns into fp32 partial traffic
   if (g_wgrad_p8 == 1 && !(a->R * a->S == 1 && tiles >= 32)) return 0;
   const long steps = (a->M + 63) / 64;
-  long splits = (256 + tiles - 1) / tiles;                         // one workgroup per CU
-  splits = std::min(splits, std::max(1L, steps / 8));              // >= 8 pixel steps per split
-  const long cap = (96L << 20) / ((long)a->Ncol * a->Kdim * 4);    // <= 96 MB of fp32 partials
-  splits = std::max(1L, std::min(splits, std::max(1L, cap)));
+  // pixel split: one workgroup per CU, so pick the split (<= 8, >= 8 pixel steps each, <= 256 MB of fp32 partials)
+  // whose grid fills its last dispatch round best (vocab 160 tiles: 2 splits = 320 workgroups = 1.25 rounds ran at
+  // 326 TF/s; 3 = 480 fills 1.9 rounds)
+  const long cap = std::max(1L, (256L << 20) / ((long)a->Ncol * a->Kdim * 4));
+  const long smax = std::max(1L, std::min({8L, steps / 8, cap}));
+  long splits = 1;
+  double best = 0.0;
+  for (long sp = 1; sp <= smax; ++sp) {
+    const long wgs = tiles * sp;
+    const double eff = (double)wgs / (double)(((wgs + 255) / 256) * 256);
+    if (eff > best + 0.02) { best = eff; splits = sp; }
+  }
   long mps = (a->M + splits - 1) / splits;
   mps = (mps + 63) / 64 * 64;
   splits = (a->M + mps - 1) / mps;
