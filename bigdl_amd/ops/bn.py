@@ -4,6 +4,7 @@ Reference semantics (S/nn/SpatialBatchNormalization.scala:418-480, S/nn/BatchNor
 biased batch variance for normalisation, unbiased variance for the running estimate,
 ``running = momentum * batch + (1 - momentum) * running``.
 """
+import os
 import torch
 
 from . import native
@@ -29,7 +30,7 @@ class _StatsArena:
         if self.need and (self.buf is None or self.buf.numel() < self.need or self.buf.device != device):
             self.buf = torch.empty(self.need, dtype=torch.float32, device=device)
         if self.buf is not None:
-            if self.buf.is_cuda:
+            if self.buf.is_cuda and int(os.environ.get("BIGDL_NATIVE_FILL", "7")) & 2:
                 native.get().fill_bytes(self.buf, 0)
             else:
                 self.buf.zero_()

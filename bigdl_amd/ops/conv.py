@@ -6,6 +6,7 @@ the reference's MklBlas engine, used for the LeNet local-CPU configuration and a
 
 Reference: S/nn/SpatialConvolution.scala:253-520 (fwd / bwd-data / bwd-weight), S/nn/Linear.scala:84-160.
 """
+import os
 import torch
 import torch.nn.functional as F
 
@@ -175,7 +176,8 @@ def conv2d_dgrad(dy, w16t, x_shape, stride, pad, dil=(1, 1), out=None, addend=No
         mask = 0
         for (a, b, _, _, _) in phases:
             mask |= 1 << (a * stride[1] + b)
-        if out.is_contiguous(memory_format=CL) and C % 8 == 0 and stride[0] * stride[1] <= 32:
+        if (out.is_contiguous(memory_format=CL) and C % 8 == 0 and stride[0] * stride[1] <= 32
+                and int(os.environ.get("BIGDL_NATIVE_FILL", "7")) & 4):
             native.get().dgrad_fill(out, addend, stride[0], stride[1], mask)
         elif addend is not None:
             out.copy_(addend)

@@ -32,6 +32,10 @@ import torch
 
 from ..ops import native
 
+# BIGDL_NATIVE_FILL bit mask (default 7): 1 gradient zeroing, 2 BN statistics arena, 4 strided-dgrad phase fill as
+# runtime memsets / native kernels instead of aten fills (A/B and bisection switch)
+_NATIVE_FILL = int(os.environ.get("BIGDL_NATIVE_FILL", "7"))
+
 from ..optim.regularizer import L1L2Regularizer
 from ..parallel.allreduce_parameter import AllReduceParameter
 
@@ -287,7 +291,7 @@ class TrainStep:
 
     # ------------------------------------------------------------------ pieces
     def zero_grad(self):
-        if self.g.is_cuda:
+        if self.g.is_cuda and _NATIVE_FILL & 1:
             native.get().fill_bytes(self.g, 0)       # one runtime memset, no aten fill kernel
         else:
             self.g.zero_()

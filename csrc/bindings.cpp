@@ -321,8 +321,7 @@ void gemv_f32(const Tensor& A, const Tensor& x, const OptT& Min, const Tensor& y
 void fill_bytes(const Tensor& t, int64_t value) {
   TORCH_CHECK(t.is_cuda() && t.is_contiguous(), "fill_bytes: contiguous GPU tensor");
   if (t.numel() == 0) return;
-  TORCH_CHECK(hipMemsetAsync(t.data_ptr(), (int)value, t.numel() * t.element_size(), stream()) == hipSuccess,
-              "fill_bytes: hipMemsetAsync failed");
+  bigdl_fill_bytes(t.data_ptr(), (int)value, (long)(t.numel() * t.element_size()), stream());   // a kernel, not a memset node
 }
 void copy_rows_i8(const Tensor& src, const Tensor& dst, int64_t rows, int64_t C, int64_t lds, int64_t ldd) {
   TORCH_CHECK(src.is_cuda() && dst.is_cuda() && src.scalar_type() == at::kChar && dst.scalar_type() == at::kChar,

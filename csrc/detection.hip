@@ -181,7 +181,7 @@ extern "C" {
 int bigdl_nms(const float* boxes_sorted, int n, float thresh, int normalized, int max_keep,
               unsigned long long* mask_ws, int* keep_out, int* count_out, hipStream_t st) {
   const int words = (n + 63) / 64;
-  if (n <= 0) return (void)hipMemsetAsync(count_out, 0, sizeof(int), st), 0;
+  if (n <= 0) return bigdl_fill_bytes(count_out, 0, (long)sizeof(int), st), 0;
   if (words > 64 * NMS_MAX_WORDS_PER_LANE) return -1;
   nms_mask_kernel<<<dim3(words, words), 64, 0, st>>>(boxes_sorted, n, thresh, normalized, mask_ws, words);
   nms_scan_kernel<<<1, 64, 0, st>>>(mask_ws, n, words, max_keep, keep_out, count_out);

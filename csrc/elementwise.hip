@@ -769,6 +769,29 @@ __global__ __launch_bounds__(256) void dgrad_fill_kernel(uint16_t* __restrict__ 
 }
 }  // namespace
 
+namespace {
+// Byte fill as a kernel: work captured into a HIP graph must not contain memset nodes — with the one-queue graph
+// executor (bigdl_amd/__init__.py) a captured hipMemsetAsync was not ordered with the kernels around it (training
+// diverged after a graph trial, tools/_bisect.sh: profiles/r4_memset_node_bisect.txt)
+__global__ __launch_bounds__(256) void fill_bytes_kernel(uint8_t* __restrict__ p, unsigned v4, long n16, long bytes) {
+  const long stride = (long)gridDim.x * 256;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n16; i += stride)
+    reinterpret_cast<v4u*>(p)[i] = v4u{v4, v4, v4, v4};
+  for (long b = n16 * 16 + blockIdx.x * 256L + threadIdx.x; b < bytes; b += stride) p[b] = (uint8_t)(v4 & 0xff);
+}
+}  // namespace
+
+void bigdl_fill_bytes(void* ptr, int value, long bytes, hipStream_t st) {
+  if (bytes <= 0) return;
+  const unsigned v = (unsigned)(value & 0xff), v4 = v | (v << 8) | (v << 16) | (v << 24);
+  const bool al = (reinterpret_cast<uintptr_t>(ptr) & 15) == 0;
+  const long n16 = al ? bytes / 16 : 0;
+  long g = ((al ? n16 : bytes) + 255) / 256;
+  g = g < 1 ? 1 : (g > 4096 ? 4096 : g);
+  fill_bytes_kernel<<<(unsigned)g, 256, 0, st>>>(static_cast<uint8_t*>(ptr), v4, n16, bytes);
+  HIP_LAUNCH_CHECK();
+}
+
 void bigdl_dgrad_fill(uint16_t* out, const uint16_t* add, long npix, int H, int W, int C, int sh, int sw, unsigned mask,
                       hipStream_t st) {
   const long total = npix * (C / 8);

@@ -57,6 +57,7 @@ struct WgradArgs {
 };
 
 extern "C" {
+void bigdl_fill_bytes(void* ptr, int value, long bytes, hipStream_t st);
 int bigdl_conv_nt(const ConvArgs* a, hipStream_t st);
 // Kernel choice for bigdl_conv_nt: sets a->ksplit and returns the fp32 workspace elements it needs (0: none).
 long bigdl_conv_nt_plan(ConvArgs* a);

@@ -19,7 +19,8 @@
 //    1 to the group counter (agent-scope atomic). This is the write-through hand-off of the CDNA4 programming guide's
 //    inter-workgroup rule: every handed-off byte is stored sc1 and drained before the counter add, every load of it is
 //    an sc1 load to registers behind the poll, and no other load reads bytes written in the launch.
-//  * counters are zeroed by a memset ahead of every launch (graph-replay safe); every spin is bounded (0.5 s of the
+//  * counters are zeroed by a fill kernel ahead of every launch (graph-replay safe: no memset node, see
+//    bigdl_fill_bytes); every spin is bounded (0.5 s of the
 //    100 MHz wall clock): on timeout the workgroup sets the error word, poisons its outputs with NaN and leaves.
 // Forward per step: gates = W h_{t-1} (+ xg, the input projection computed beforehand as one GEMM), c and h in
 // fp32, h16 bf16 hand-off (also the B operand of the weight-gradient GEMM). Backward per step: dh = dout + dg_{t+1} W
@@ -377,7 +378,7 @@ int bigdl_lstm_seq_fwd(const uint16_t* W16, const void* xg, const float* c0, uin
   LstmSeqArgs a{};
   a.W16 = W16; a.xg = xg; a.c0 = c0; a.h16 = h16; a.out = out; a.hT = hT; a.cs = cs; a.acts = acts; a.sync = sync;
   a.B = B; a.H = H; a.T = T; a.Bg = (B + NGRP - 1) / NGRP;
-  if (hipMemsetAsync(sync, 0, sizeof(unsigned) * bigdl_lstm_seq_sync_words(), st) != hipSuccess) return -2;
+  bigdl_fill_bytes(sync, 0, (long)sizeof(unsigned) * bigdl_lstm_seq_sync_words(), st);   // kernel: graph-safe
   const dim3 grid(NGRP * (H / 32));
 #define SEQ_FWD(K)                                                  \
   do {                                                              \
@@ -400,7 +401,7 @@ int bigdl_lstm_seq_bwd(const uint16_t* W16, const void* dout, const float* dhT, 
   a.W16 = W16; a.dout = dout; a.dhT = dhT; a.dcT = dcT; a.acts = const_cast<float*>(acts);
   a.cs = const_cast<float*>(cs); a.c0 = c0; a.dg16 = dg16; a.dxg = dxg; a.dc0 = dc0; a.dh0 = dh0; a.sync = sync;
   a.B = B; a.H = H; a.T = T; a.Bg = (B + NGRP - 1) / NGRP;
-  if (hipMemsetAsync(sync, 0, sizeof(unsigned) * bigdl_lstm_seq_sync_words(), st) != hipSuccess) return -2;
+  bigdl_fill_bytes(sync, 0, (long)sizeof(unsigned) * bigdl_lstm_seq_sync_words(), st);   // kernel: graph-safe
   const dim3 grid(NGRP * (H / 32));
 #define SEQ_BWD(K)                                                  \
   do {                                                              \

@@ -997,7 +997,7 @@ int bigdl_quantize_act(const void* x, int is_bf16, int8_t* q, float* amax, float
                        int Cp, int static_amax, hipStream_t st) {
   const long per = P * C;
   if (!static_amax) {            // dynamic per-sample range; with static_amax the caller filled amax (calibrated)
-    (void)hipMemsetAsync(amax, 0, sizeof(float) * N, st);
+    bigdl_fill_bytes(amax, 0, (long)sizeof(float) * N, st);
     const int bx = (int)std::min<long>((per / (is_bf16 && (per & 7) == 0 ? 8 : 1) + 255) / 256, 256);
     dim3 g1(bx > 0 ? bx : 1, N);
     if (is_bf16) amax_kernel<uint16_t><<<g1, 256, 0, st>>>((const uint16_t*)x, per, amax);
