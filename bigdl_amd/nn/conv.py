@@ -185,10 +185,10 @@ class SpatialConvolution(TensorModule):
         xp, shape, ph, pw = self._xpair
         R, S, K = self.kernelH, self.kernelW, self.nOutputPlane
         S2 = (S + 1) // 2
-        dwp = torch.zeros(K, R * S2 * 8, device=x.device)
+        dwp = ops.zeros(K, R * S2 * 8, device=x.device)
         db = None
         if self.bias is not None:
-            db = self.gradBias if self.scaleB == 1.0 else torch.zeros(K, device=x.device)
+            db = self.gradBias if self.scaleB == 1.0 else ops.zeros(K, device=x.device)
         cv.conv2d_pairs_wgrad(gy16, xp, R, S2, self.strideH, dwp, db)
         ops.native.get().pair_wgrad_add(dwp, self.gradWeight, float(self.scaleW))
         if db is not None and db is not self.gradBias:
@@ -384,8 +384,8 @@ class SpatialConvolution(TensorModule):
             xf = getattr(self, "_xf", None)
             if xf is None or xf.shape != x.shape:
                 xf = x.float().contiguous()
-            dw = torch.zeros(self.weight.shape, device=x.device)
-            db = torch.zeros(self.nOutputPlane, device=x.device) if self.bias is not None else None
+            dw = ops.zeros(self.weight.shape, device=x.device)
+            db = ops.zeros(self.nOutputPlane, device=x.device) if self.bias is not None else None
             ops.native.get().gconv(2, xf, dw, db, gy.float().contiguous(), self._geo_g(pd[0], pd[1]))
             self.gradWeight.add_(dw, alpha=self.scaleW)
             if db is not None:
@@ -397,9 +397,9 @@ class SpatialConvolution(TensorModule):
             for g in range(G):
                 xg = cv.to_nhwc_bf16(x[:, g * cin:(g + 1) * cin].contiguous(memory_format=CL))
                 gyg = cv.pad_dim(gy16[:, g * cout:(g + 1) * cout].contiguous(memory_format=CL), 1)
-                dw = torch.zeros(gyg.shape[1], xg.shape[1], self.kernelH, self.kernelW, device=x.device).contiguous(
-                    memory_format=CL)
-                db = torch.zeros(gyg.shape[1], device=x.device) if self.bias is not None else None
+                dw = ops.zeros(gyg.shape[1], xg.shape[1], self.kernelH, self.kernelW, device=x.device,
+                               memory_format=CL)
+                db = ops.zeros(gyg.shape[1], device=x.device) if self.bias is not None else None
                 cv.conv2d_wgrad(gyg, xg, dw, db, st, pd, dl)
                 self.gradWeight[g * cout:(g + 1) * cout].add_(dw[:cout, :cin], alpha=self.scaleW)
                 if db is not None:
@@ -412,9 +412,9 @@ class SpatialConvolution(TensorModule):
             cv.conv2d_wgrad(gy16, x16, self.gradWeight, self.gradBias, st, pd, dl)
         else:
             gyp = cv.pad_dim(gy16, 1)
-            dw = torch.zeros(gyp.shape[1], x16.shape[1], self.kernelH, self.kernelW,
-                             device=x.device).contiguous(memory_format=CL)
-            db = torch.zeros(gyp.shape[1], device=x.device) if self.bias is not None else None
+            dw = ops.zeros(gyp.shape[1], x16.shape[1], self.kernelH, self.kernelW, device=x.device,
+                           memory_format=CL)
+            db = ops.zeros(gyp.shape[1], device=x.device) if self.bias is not None else None
             cv.conv2d_wgrad(gyp, x16, dw, db, st, pd, dl)
             self.gradWeight.add_(dw[:K, : self.nInputPlane], alpha=self.scaleW)
             if db is not None:

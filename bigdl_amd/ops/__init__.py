@@ -13,6 +13,19 @@ BF16 = torch.bfloat16
 CL = torch.channels_last
 
 
+def zeros(*shape, device=None, dtype=torch.float32, memory_format=None):
+    """torch.zeros without the aten fill kernel on the GPU: one native fill kernel (graph-capture safe)."""
+    if len(shape) == 1 and isinstance(shape[0], (tuple, list, torch.Size)):
+        shape = tuple(shape[0])
+    kw = {"memory_format": memory_format} if memory_format is not None else {}
+    t = torch.empty(shape, dtype=dtype, device=device, **kw)
+    if t.is_cuda:
+        native.get().fill_bytes(t, 0)
+    else:
+        t.zero_()
+    return t
+
+
 def is_gpu(t):
     return isinstance(t, torch.Tensor) and t.is_cuda
 

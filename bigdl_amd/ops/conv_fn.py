@@ -18,6 +18,12 @@ import torch.nn.functional as F
 
 from . import conv as cv
 
+
+def _zeros(*shape, **kw):
+    from . import zeros
+
+    return zeros(*shape, **kw)
+
 BF16 = torch.bfloat16
 CL = torch.channels_last
 
@@ -73,8 +79,8 @@ class _Conv2d(torch.autograd.Function):
             gi = cv.conv2d_dgrad(gy16, cv.transpose_w(w16), (xshape[0], C8, xshape[2], xshape[3]), stride, pad, dil)
             gx = gi[:, :C].float().contiguous()
         if ctx.needs_input_grad[1] or (has_b and ctx.needs_input_grad[2]):
-            dw = torch.zeros(w16.shape, device=gy.device).contiguous(memory_format=CL)
-            db = torch.zeros(K8, device=gy.device) if has_b else None
+            dw = _zeros(w16.shape, device=gy.device, memory_format=CL)
+            db = _zeros(K8, device=gy.device) if has_b else None
             cv.conv2d_wgrad(gy16, x16, dw, db, stride, pad, dil)
             gw = dw[:K, :C].contiguous()
             gb = db[:K] if has_b else None
@@ -121,7 +127,7 @@ class _ConvT2d(torch.autograd.Function):
             gi = cv.conv2d_fwd(gy16, w16, None, stride, pad)
             gx = gi[:, :Cin, :x16.shape[2], :x16.shape[3]].float().contiguous()
         if ctx.needs_input_grad[1]:
-            dw = torch.zeros(w16.shape, device=gy.device).contiguous(memory_format=CL)
+            dw = _zeros(w16.shape, device=gy.device, memory_format=CL)
             cv.conv2d_wgrad(x16, gy16, dw, None, stride, pad)
             gw = dw[:Cin, :Cout].contiguous()
         if has_b and ctx.needs_input_grad[2]:

@@ -319,7 +319,7 @@ void gemv_f32(const Tensor& A, const Tensor& x, const OptT& Min, const Tensor& y
 }
 // byte fill of a whole GPU tensor (hipMemsetAsync: a runtime fill, no aten kernel) — int8 buffers' padding channels
 void fill_bytes(const Tensor& t, int64_t value) {
-  TORCH_CHECK(t.is_cuda() && t.is_contiguous(), "fill_bytes: contiguous GPU tensor");
+  TORCH_CHECK(t.is_cuda() && t.is_non_overlapping_and_dense(), "fill_bytes: dense GPU tensor (any memory format)");
   if (t.numel() == 0) return;
   bigdl_fill_bytes(t.data_ptr(), (int)value, (long)(t.numel() * t.element_size()), stream());   // a kernel, not a memset node
 }
