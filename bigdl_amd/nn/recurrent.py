@@ -157,7 +157,7 @@ class Cell(Container):
         return [m for m in self.modules if m is not self.preTopology]
 
     def init_hidden(self, B, x_t):
-        return [torch.zeros(B, h, device=x_t.device, dtype=torch.float32) for h in self.hiddensShape]
+        return [ops.zeros(B, h, device=x_t.device, dtype=torch.float32) for h in self.hiddensShape]
 
     def pre_fn(self, x):
         """Differentiable preTopology (used when the projection cannot be hoisted out of the time loop)."""

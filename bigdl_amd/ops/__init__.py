@@ -26,6 +26,15 @@ def zeros(*shape, device=None, dtype=torch.float32, memory_format=None):
     return t
 
 
+def zero_(t):
+    """In-place zero without a memset node or aten fill on the GPU (dense tensors); returns t."""
+    if t.is_cuda and t.is_non_overlapping_and_dense():
+        native.get().fill_bytes(t, 0)
+    else:
+        t.zero_()
+    return t
+
+
 def is_gpu(t):
     return isinstance(t, torch.Tensor) and t.is_cuda
 

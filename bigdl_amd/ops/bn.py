@@ -46,7 +46,11 @@ class _StatsArena:
             t = self.buf[self.off:self.off + n]
             self.off += n_al
             return t
-        return torch.zeros(n, dtype=torch.float32, device=device)
+        t = torch.empty(n, dtype=torch.float32, device=device)
+        if t.is_cuda:
+            native.get().fill_bytes(t, 0)
+            return t
+        return t.zero_()
 
 
 ARENA = _StatsArena()

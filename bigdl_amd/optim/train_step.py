@@ -30,6 +30,7 @@ import os
 
 import torch
 
+from .. import ops
 from ..ops import native
 
 # BIGDL_NATIVE_FILL bit mask (default 7): 1 gradient zeroing, 2 BN statistics arena, 4 strided-dgrad phase fill as
@@ -403,14 +404,14 @@ class TrainStep:
             return self._weighted_exchange(loss, finished, self.g)
         if getattr(self, "_late_stream", None) is None:
             self._late_stream = torch.cuda.Stream(device=self.device)
-            self._late_g = torch.zeros_like(self.g)
+            self._late_g = ops.zero_(torch.empty_like(self.g))
         cur = torch.cuda.current_stream(self.device)
         s = self._late_stream
         with torch.cuda.stream(s):
             try:
                 return self._weighted_exchange(loss, 0.0, self._late_g)
             finally:
-                self._late_g.zero_()            # the reduced chunks landed in it
+                ops.zero_(self._late_g)         # the reduced chunks landed in it
                 cur.wait_stream(s)
 
     def _weighted_exchange(self, loss, finished, g):
@@ -418,7 +419,7 @@ class TrainStep:
         self.comm.all_reduce_scalar(cnt)
         n = float(cnt.item())
         if not finished and g is self.g:
-            self.g.zero_()
+            ops.zero_(self.g)
         if self.bucketed is not None:
             # the update plan is per bucket (this rank owns one chunk of every bucket, not [start, end)):
             # reduce each bucket into its owned chunk and average those chunks over the finished ranks

@@ -13,6 +13,8 @@ no host synchronisation, the scales stay on the device.
 """
 import torch
 
+from .. import ops
+
 
 def _native():
     from ..ops import native
@@ -81,7 +83,7 @@ class L2NormClippingProcessor(ParameterProcessor):
         self.threshold = float(l2NormThreshold)
 
     def collectGlobalData(self, step, state):
-        sq = torch.zeros(1, device=step.device)
+        sq = ops.zeros(1, device=step.device)
         for g in _owned_grads(step):
             _sumsq_into(g, sq)
         if step.comm is not None:
@@ -110,7 +112,7 @@ class LarsProcessor(ParameterProcessor):
 
         names = [s[0] for s in step.splits if isinstance(s[3], LarsSGD)]
         idx = {n: i for i, n in enumerate(names)}
-        acc = torch.zeros(2 * len(names), device=step.device)
+        acc = ops.zeros(2 * len(names), device=step.device)
         for p in step.plan:
             i = idx.get(p.name)
             if i is None:
