@@ -28,7 +28,7 @@ def zeros(*shape, device=None, dtype=torch.float32, memory_format=None):
 
 def zero_(t):
     """In-place zero without a memset node or aten fill on the GPU (dense tensors); returns t."""
-    if t.is_cuda and t.is_non_overlapping_and_dense():
+    if t.is_cuda and (t.is_contiguous() or (t.dim() == 4 and t.is_contiguous(memory_format=torch.channels_last))):
         native.get().fill_bytes(t, 0)
     else:
         t.zero_()
