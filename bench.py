@@ -246,11 +246,20 @@ def main():
     gc.freeze()                 # setup objects out of the collector's generations: no long GC pass mid-loop
     barrier()
     torch.cuda.synchronize()
+    trace = os.environ.get("BIGDL_BENCH_TRACE") == "1"
+    if trace:                   # a host stall > 1 s inside the loop dumps the Python stack where it sits
+        import faulthandler
+    reserved = []
     t0 = time.perf_counter()
     stamps = []
     for _ in range(args.steps):
+        if trace:
+            faulthandler.dump_traceback_later(1.0, repeat=False, file=sys.stderr)
         run()
         stamps.append(time.perf_counter())     # host clock after each enqueue (host-only: no device sync)
+        if trace:
+            faulthandler.cancel_dump_traceback_later()
+            reserved.append((round(torch.cuda.memory_reserved(dev) / 2**30, 2), round(torch.cuda.memory_allocated(dev) / 2**30, 2)))
     end = torch.cuda.Event()
     end.record()
     wait_event(end)             # poll until the device drained (see TrainStep.wait_event), then the contract's sync
@@ -260,6 +269,7 @@ def main():
     if os.environ.get("BIGDL_BENCH_TRACE") == "1":     # diagnostics after the timed region: per-step times, memory
         gaps = [round((b - a) * 1e3, 1) for a, b in zip([t0] + stamps[:-1], stamps)]
         print(f"[bench trace] host enqueue-to-enqueue gaps in the timed loop (ms): {gaps}", file=sys.stderr, flush=True)
+        print(f"[bench trace] (reserved, allocated) GiB after each enqueue: {reserved}", file=sys.stderr, flush=True)
         free, total = torch.cuda.mem_get_info(dev)
         print(f"[bench trace] reserved {torch.cuda.memory_reserved(dev) / 2**30:.1f} GiB, max allocated "
               f"{torch.cuda.max_memory_allocated(dev) / 2**30:.1f} GiB, device free {free / 2**30:.1f} / "

@@ -268,6 +268,8 @@ class SpatialConvolution(TensorModule):
             once = getattr(self, "_dgrad_bn_once", False)
             self._dgrad_bn_once = False
             bn_src = getattr(input, "_bn_bwd", None) if (getattr(self, "_dgrad_bn_ok", False) or once) else None
+            if bn_src is not None:          # flag -> the BN's post-ReLU output, which is this conv's input
+                bn_src = bn_src[:4] + ((input if bn_src[4] else None),)
             gi = self._dgrad_gpu(x, gy, ph, pw, None if (squeeze or eh or ew or self.format != "NCHW") else bn_src)
         else:
             gy = self._relu_mask(gy)
