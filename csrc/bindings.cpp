@@ -1204,6 +1204,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("get_wgrad_g3", &bigdl_get_wgrad_g3);
   m.def("set_i8_g3", &bigdl_set_i8_g3);
   m.def("set_i8_p8", &bigdl_set_i8_p8);
+  m.def("set_i8_epi", &bigdl_set_i8_epi);
   m.def("get_i8_g3", &bigdl_get_i8_g3);
   m.def("set_i8_cpl", &bigdl_set_i8_cpl);
   m.def("get_i8_cpl", &bigdl_get_i8_cpl);

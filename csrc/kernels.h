@@ -191,6 +191,7 @@ void bigdl_set_wgrad_g3(int v);
 int bigdl_get_wgrad_g3();
 void bigdl_set_i8_g3(int v);
 void bigdl_set_i8_p8(int v);
+void bigdl_set_i8_epi(int v);
 int bigdl_get_i8_g3();
 void bigdl_set_i8_cpl(int v);
 int bigdl_get_i8_cpl();

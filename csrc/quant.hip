@@ -456,6 +456,66 @@ __device__ __forceinline__ void i8_tile_epilogue(const ConvArgs& a, const I8Epi&
   }
 }
 
+// Register-direct variant of i8_tile_epilogue: the i8 MFMA's D[n][m] layout already gives a lane 4 consecutive
+// channels of one pixel per 16 x 16 tile, so each tile is finished in registers and stored as one 4-byte int8 group
+// (8-byte bf16 / 16-byte fp32) per lane — no LDS round trip, no barrier — with the per-channel factors folded once:
+// q = rn(acc * (xs * wsc * out_inv) + bias * out_inv + add * add_scale * out_inv). Needs Ncol % 4 == 0 and
+// ldo % 4 == 0 (4-byte aligned groups); the caller checks (i8_direct_ok).
+template <int MI, int NI>
+__device__ __forceinline__ void i8_tile_epilogue_direct(const ConvArgs& a, const I8Epi& ep, v4i (&acc)[MI][NI],
+                                                        int mbase, int nbase, int lane) {
+  const int ohw = a.OH * a.OW;
+  const int nl = 4 * (lane >> 4), ml = lane & 15;
+  const bool q8 = ep.out_mode == 2;
+  const float oi = q8 ? ep.out_inv : 1.f;
+  float ws[NI][4], bs[NI][4];
+#pragma unroll
+  for (int j = 0; j < NI; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int n = nbase + j * 16 + nl + e;
+      const bool ok = n < a.Ncol;
+      ws[j][e] = ok ? ep.wscale[n] * oi : 0.f;
+      bs[j][e] = (ok && a.bias) ? a.bias[n] * oi : 0.f;
+    }
+  const float as = ep.add_scale * oi;
+#pragma unroll
+  for (int i = 0; i < MI; ++i) {
+    const int m = mbase + i * 16 + ml;
+    if (m >= a.M) continue;
+    const float xs = ep.xscale ? ep.xscale[m / ohw] : ep.xs_const;
+    unsigned addw[NI];
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {     // residual groups first, all in flight before the first store
+      const int n = nbase + j * 16 + nl;
+      addw[j] = (ep.add8 && n < a.Ncol) ? *reinterpret_cast<const unsigned*>(ep.add8 + (size_t)m * ep.add_ld + n) : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int n = nbase + j * 16 + nl;
+      if (n >= a.Ncol) continue;
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[e] = (float)acc[i][j][e] * (xs * ws[j][e]) + bs[j][e];
+        if (ep.add8) v[e] += (float)(int8_t)((addw[j] >> (8 * e)) & 0xff) * as;
+        if (a.relu) v[e] = fmaxf(v[e], 0.f);
+      }
+      const size_t off = (size_t)m * a.ldo + n;
+      if (q8) {
+        unsigned pk = 0u;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) pk |= (unsigned)(max(-127, min(127, __float2int_rn(v[e]))) & 0xff) << (8 * e);
+        *reinterpret_cast<unsigned*>(reinterpret_cast<int8_t*>(a.out) + off) = pk;
+      } else if (ep.out_mode == 1) {
+        *reinterpret_cast<v4f*>(reinterpret_cast<float*>(a.out) + off) = v4f{v[0], v[1], v[2], v[3]};
+      } else {
+        *reinterpret_cast<v2u*>(a.out + off) = v2u{pack2bf(v[0], v[1]), pack2bf(v[2], v[3])};
+      }
+    }
+  }
+}
+
 // 128 x 128 int8 tile with the counted-vmcnt pipeline of conv_nt_g4_kernel (conv_igemm.hip): 64-byte LDS rows (one
 // i8 MFMA K-step of 64 = four 16-byte granules, slot g ^ ((r >> 1) & 3)), THREE stages of 16 KB with two K-steps in
 // flight across every raw s_barrier (the 2-stage kernel above drains its DMA queue with __syncthreads every
@@ -465,7 +525,7 @@ __device__ __forceinline__ void i8_tile_epilogue(const ConvArgs& a, const I8Epi&
 // waves stacked along M (as conv_i8_glds_kernel).
 // FASTK = false (Cs % 64 != 0: Inception's 48 / 80 / 96 / 160 / ...-channel inputs, padded to 16): every lane resolves
 // the tap of its own 16-channel granule from the LDS tap table; the K tail past Kdim loads zeros.
-template <int BM, int BN, int WGM, int WGN, bool FASTK = true, int CPL = 8>
+template <int BM, int BN, int WGM, int WGN, bool FASTK = true, int CPL = 8, bool DIRECT = false>
 __global__ __launch_bounds__(256, (BM + (BN + 63) / 64 * 64) * 64 * 3 <= 52 * 1024 ? 3 : 2) void conv_i8_g3_kernel(
     ConvArgs a, I8Epi ep) {
   constexpr int BKB = 64, NS = 3;
@@ -596,9 +656,12 @@ __global__ __launch_bounds__(256, (BM + (BN + 63) / 64 * 64) * 64 * 3 <= 52 * 10
     cur = cur == 2 ? 0 : cur + 1;
   }
 
-  // ---- epilogue (conv_i8_glds_kernel's), in NH row halves through a wave-private LDS slice
-  i8_tile_epilogue<MI, NI, TM, TN, NH, CPL>(a, ep, acc, m0 + wm * TM, n0 + wn * TN, lane,
-                                           reinterpret_cast<float*>(lds) + wave * (TM / NH) * TN);
+  // ---- epilogue: in registers (DIRECT), or conv_i8_glds_kernel's in NH row halves through a wave-private LDS slice
+  if constexpr (DIRECT)
+    i8_tile_epilogue_direct<MI, NI>(a, ep, acc, m0 + wm * TM, n0 + wn * TN, lane);
+  else
+    i8_tile_epilogue<MI, NI, TM, TN, NH, CPL>(a, ep, acc, m0 + wm * TM, n0 + wn * TN, lane,
+                                             reinterpret_cast<float*>(lds) + wave * (TM / NH) * TN);
 }
 
 // 256 x 256 int8 tile on the phase-interleaved schedule of conv_nt_p8_kernel (conv_igemm.hip: pieces, phases, counted
@@ -606,6 +669,7 @@ __global__ __launch_bounds__(256, (BM + (BN + 63) / 64 * 64) * 64 * 3 <= 52 * 10
 // x 128 B. A 128-byte row is one K-tile of 128 int8 = two i8 MFMA K-steps of 64, so the byte-level schedule is the bf16
 // kernel's unchanged; the MFMA is v_mfma_i32_16x16x64_i8 and the epilogue i8_tile_epilogue (4 row chunks through the
 // buffers). Fast-K only (Cs % 128 == 0: a K-tile lies in one tap).
+template <bool DIRECT>
 __global__ __launch_bounds__(512, 2) void conv_i8_p8_kernel(ConvArgs a, I8Epi ep) {
   constexpr int BM = 256, BN = 256, BKB = 128;
   constexpr int WGM = 2, WGN = 4;
@@ -771,9 +835,13 @@ __global__ __launch_bounds__(512, 2) void conv_i8_p8_kernel(ConvArgs a, I8Epi ep
   }
   if (wm == 0) __builtin_amdgcn_s_barrier();   // balance the stagger
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();                            // every wave is done with the buffers before the epilogue reuses them
-  i8_tile_epilogue<MI, NI, TM, TN, NH, 16>(a, ep, acc, m0 + wm * TM, n0 + wn * TN, lane,
-                                           reinterpret_cast<float*>(lds) + wave * (TM / NH) * TN);
+  if constexpr (DIRECT) {
+    i8_tile_epilogue_direct<MI, NI>(a, ep, acc, m0 + wm * TM, n0 + wn * TN, lane);
+  } else {
+    __syncthreads();                          // every wave is done with the buffers before the epilogue reuses them
+    i8_tile_epilogue<MI, NI, TM, TN, NH, 16>(a, ep, acc, m0 + wm * TM, n0 + wn * TN, lane,
+                                             reinterpret_cast<float*>(lds) + wave * (TM / NH) * TN);
+  }
 }
 
 // int8 rows [rows][C] from src (row stride lds) into dst (row stride ldd): a concat input that was not produced in place
@@ -978,8 +1046,23 @@ int i8_cpl() {
   return g_i8_cpl;
 }
 
+// BIGDL_I8_EPI (default 1): register-direct int8 epilogue where the output groups are 4-byte aligned; 0 = LDS-staged
+int g_i8_epi = -1;
+bool i8_direct_ok(const ConvArgs& a, const I8Epi& ep) {
+  if (g_i8_epi < 0) {
+    const char* e = getenv("BIGDL_I8_EPI");
+    g_i8_epi = e ? atoi(e) : 1;
+  }
+  return g_i8_epi != 0 && a.Ncol % 4 == 0 && a.ldo % 4 == 0 && (ep.add8 == nullptr || ep.add_ld % 4 == 0) &&
+         (ep.out_mode != 1 || a.ldo % 4 == 0);
+}
+
 template <int BM, int BN, int WGM, int WGN>
 void launch_i8_g3(int g, bool fk, const ConvArgs& a, const I8Epi& ep, hipStream_t st) {
+  if (fk && i8_direct_ok(a, ep)) {
+    conv_i8_g3_kernel<BM, BN, WGM, WGN, true, 16, true><<<g, 256, 0, st>>>(a, ep);
+    return;
+  }
   if (i8_cpl() == 16 && BN / WGN >= 16) {
     if (fk) conv_i8_g3_kernel<BM, BN, WGM, WGN, true, 16><<<g, 256, 0, st>>>(a, ep);
     else conv_i8_g3_kernel<BM, BN, WGM, WGN, false, 16><<<g, 256, 0, st>>>(a, ep);
@@ -1041,6 +1124,7 @@ static bool i8_p8() {
   return g_i8_p8 != 0;
 }
 void bigdl_set_i8_p8(int v) { g_i8_p8 = v; }
+void bigdl_set_i8_epi(int v) { g_i8_epi = v; }
 void bigdl_set_i8_cpl(int v) { g_i8_cpl = v; }
 int bigdl_get_i8_cpl() { return i8_cpl(); }
 int bigdl_get_i8_g3() { return i8_g3() ? g_i8_g3 : 0; }
@@ -1056,7 +1140,8 @@ int bigdl_conv_i8(const ConvArgs* a, const float* xscale, float xs_const, const 
   const long p8_tiles = (long)((a->M + 255) / 256) * ((a->Ncol + 255) / 256);
   if (i8_p8() && fk && a->Kdim >= 1024 && a->Ncol >= 256 && a->Ncol % 16 == 0 &&
       (g_i8_p8 == 2 || p8_tiles >= 160)) {
-    conv_i8_p8_kernel<<<dim3((unsigned)p8_tiles), dim3(512), 0, st>>>(*a, ep);
+    if (i8_direct_ok(*a, ep)) conv_i8_p8_kernel<true><<<dim3((unsigned)p8_tiles), dim3(512), 0, st>>>(*a, ep);
+    else conv_i8_p8_kernel<false><<<dim3((unsigned)p8_tiles), dim3(512), 0, st>>>(*a, ep);
   } else if (a->Ncol <= 64 && i8_g3()) {
     const int bn = a->Ncol <= 32 ? 32 : 64;
     const int g = ((a->M + 255) / 256) * ((a->Ncol + bn - 1) / bn);
