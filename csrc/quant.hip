@@ -1046,12 +1046,14 @@ int i8_cpl() {
   return g_i8_cpl;
 }
 
-// BIGDL_I8_EPI (default 1): register-direct int8 epilogue where the output groups are 4-byte aligned; 0 = LDS-staged
+// BIGDL_I8_EPI (default 0): 1 = register-direct int8 epilogue where the output groups are 4-byte aligned. Measured
+// slower: ResNet-50 int8 3.83 -> 5.11 ms (4-byte groups scattered over 16 pixel rows per store instruction vs the
+// LDS-staged 16-byte rows; profiles/r4_int8_epilogue_direct_ab.txt)
 int g_i8_epi = -1;
 bool i8_direct_ok(const ConvArgs& a, const I8Epi& ep) {
   if (g_i8_epi < 0) {
     const char* e = getenv("BIGDL_I8_EPI");
-    g_i8_epi = e ? atoi(e) : 1;
+    g_i8_epi = e ? atoi(e) : 0;
   }
   return g_i8_epi != 0 && a.Ncol % 4 == 0 && a.ldo % 4 == 0 && (ep.add8 == nullptr || ep.add_ld % 4 == 0) &&
          (ep.out_mode != 1 || a.ldo % 4 == 0);

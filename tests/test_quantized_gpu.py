@@ -56,13 +56,13 @@ def test_conv_i8_exact_integer(case, g3, cpl):
     old, old_cpl = C_.get_i8_g3(), C_.get_i8_cpl()
     C_.set_i8_g3(g3)
     C_.set_i8_cpl(cpl)     # channels per lane in the 3-stage kernel's LDS-staged epilogue (16: 16-byte stores)
-    C_.set_i8_epi(1 if cpl == 16 else 0)   # cpl 16 runs the register-direct epilogue where the shape allows
+    C_.set_i8_epi(1 if cpl == 16 else 0)   # cpl 16: the register-direct epilogue (BIGDL_I8_EPI=1) where it applies
     try:
         _conv_i8_exact(case)
     finally:
         C_.set_i8_g3(old)
         C_.set_i8_cpl(old_cpl)
-        C_.set_i8_epi(1)
+        C_.set_i8_epi(0)
 
 
 I8_P8_CASES = [
