@@ -2116,7 +2116,7 @@ __global__ __launch_bounds__(256, (NS == 3 && BM == 128) ? 3 : 2) void conv_nt_g
 // FASTK only (Cs % 64 == 0: a K-tile lies in one tap). SPLIT: fp32 partials of a K range per blockIdx.y.
 // ABL (diagnostic ablation builds, BIGDL_P8_ABL; wrong outputs): bit 0 no LDS-DMA inside the K-loop, bit 1 no fragment
 // ds_reads after the first K-tile, bit 2 no wave-group stagger, bit 3 no MFMAs, bit 4 no A-operand DMA, bit 5 no
-// B-operand DMA
+// B-operand DMA; bit 6 (64) is not an ablation: the one-tap K-tail mode (Cs % 64 != 0, granules past Kdim zero)
 template <bool SPLIT, int ABL = 0>
 __global__ __launch_bounds__(512, 2) void conv_nt_p8_kernel(ConvArgs a) {
   constexpr int BM = 256, BN = 256, BKT = 64;
@@ -2140,7 +2140,8 @@ __global__ __launch_bounds__(512, 2) void conv_nt_p8_kernel(ConvArgs a) {
   const int bid = xcd_remap(blockIdx.x, nwg);
   const int tm = bid / tiles_n, tn = bid % tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
-  const int nk_all = a.Kdim / BKT;
+  constexpr bool KTAIL = (ABL & 64) != 0;          // one tap, Cs % 64 != 0: granules past Kdim load zeros
+  const int nk_all = KTAIL ? (a.Kdim + BKT - 1) / BKT : a.Kdim / BKT;
   int kt0 = 0, nk = nk_all;
   if constexpr (SPLIT) {
     const int per = (nk_all + a.ksplit - 1) / a.ksplit;
@@ -2193,20 +2194,22 @@ __global__ __launch_bounds__(512, 2) void conv_nt_p8_kernel(ConvArgs a) {
     if ((P & 1) == 0) {
       const int th = taps[t], tw = taps[CONV_MAX_TAPS + t];
       const int c = cin + gsrc * 8;
+      const bool kin = !KTAIL || c < a.Cs;
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int q2 = q * 2 + j;
         const int ch = a_h[q2] + th, cw = a_w[q2] + tw;
-        const bool ok = (unsigned)ch < (unsigned)a.Hs && (unsigned)cw < (unsigned)a.Ws;
+        const bool ok = kin && (unsigned)ch < (unsigned)a.Hs && (unsigned)cw < (unsigned)a.Ws;
         const bf16_t* src = ok ? a.src + (unsigned)((a_pix[q2] + ch * a.Ws + cw) * a.Cs + c) : g_zero_granule;
         glds16(src, (LDS_PTR(void))(base + (j * 8 + wave) * 8 * BKT));
       }
     } else {
       const int wk = taps[2 * CONV_MAX_TAPS + t] * a.Cs + cin;
+      const bool kin = !KTAIL || cin + gsrc * 8 < a.Cs;
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int q2 = q * 2 + j;
-        const bf16_t* src = bvalid[q2] ? wrow[q2] + wk : g_zero_granule;
+        const bf16_t* src = (kin && bvalid[q2]) ? wrow[q2] + wk : g_zero_granule;
         glds16(src, (LDS_PTR(void))(base + (j * 8 + wave) * 8 * BKT));
       }
     }
@@ -2494,7 +2497,8 @@ static int p8_pick(const ConvArgs* a) {
     g_conv_p8 = e ? atoi(e) : 1;
   }
   const int on = g_conv_p8;
-  if (!on || a->out32 || (a->Cs % 64) || (a->Ncol & 7) || (a->ldo & 7) || a->Kdim < 128) return 0;
+  const bool ktail = (a->Cs % 64) != 0 && a->ntaps == 1 && a->Cs % 8 == 0 && a->Kdim == a->Cs;   // p8_ktail()
+  if (!on || a->out32 || ((a->Cs % 64) && !ktail) || (a->Ncol & 7) || (a->ldo & 7) || a->Kdim < 128) return 0;
   // auto: deep reductions only. Per layer (tools/conv_roofline.py, ResNet-50 b256) the one-workgroup-per-CU tile wins
   // from K = 1024 up (3x3 over 256 channels 101 -> 86 us) and loses below, where its prologue / epilogue are not
   // hidden by a co-resident workgroup (1x1 512 -> 1024 stride 2: 103 -> 147 us)
@@ -2597,16 +2601,20 @@ int bigdl_conv_nt(const ConvArgs* a, hipStream_t st) {
   const bool p3_pick = impl == 2 || (impl == 1 && p3auto && a->M <= 50176 && a->Kdim >= 1024);
   const int p8 = impl == 1 ? p8_pick(a) : 0;
   const int w8 = (impl == 1 && p8 == 0) ? w8_pick(a) : 0;
+  // K tail (one tap, Cs % 64 != 0, e.g. a 10000-word vocabulary projection's data gradient): granules past Kdim zero
+  const bool p8_ktail = (a->Cs % 64) != 0;
   if (p8 > 1 && a->ksplit == p8 && a->ws != nullptr) {
     const int nwg = ((a->M + 255) / 256) * ((a->Ncol + 255) / 256);
-    conv_nt_p8_kernel<true><<<dim3(nwg, p8), dim3(512), 0, st>>>(*a);
+    if (p8_ktail) conv_nt_p8_kernel<true, 64><<<dim3(nwg, p8), dim3(512), 0, st>>>(*a);
+    else conv_nt_p8_kernel<true><<<dim3(nwg, p8), dim3(512), 0, st>>>(*a);
     long rpb = 0;
     const dim3 grid = splitk_grid(a->M, a->Ncol, &rpb);
     conv_splitk_epilogue_kernel<<<grid, dim3(256), 0, st>>>(*a, rpb);
   } else if (p8 == 1) {
     const int nwg = ((a->M + 255) / 256) * ((a->Ncol + 255) / 256);
     static const int abl = [] { const char* e = getenv("BIGDL_P8_ABL"); return e ? atoi(e) : 0; }();
-    switch (abl) {
+    switch (p8_ktail ? 64 : abl) {
+      case 64: conv_nt_p8_kernel<false, 64><<<dim3(nwg), dim3(512), 0, st>>>(*a); break;
       case 1: conv_nt_p8_kernel<false, 1><<<dim3(nwg), dim3(512), 0, st>>>(*a); break;
       case 2: conv_nt_p8_kernel<false, 2><<<dim3(nwg), dim3(512), 0, st>>>(*a); break;
       case 4: conv_nt_p8_kernel<false, 4><<<dim3(nwg), dim3(512), 0, st>>>(*a); break;

@@ -723,6 +723,8 @@ P8_CASES = [
     (16, 256, 28, 256, 3, 2, 1),     # stride 2: dgrad phases write a strided output placement
     (66, 256, 28, 256, 1, 1, 0),     # >= 192 tiles, M tail
     (3, 64, 10, 512, 3, 1, 1),       # tiny M (one tile), Cs = 64
+    (8, 200, 14, 256, 1, 1, 0),      # 1x1 with Cs % 64 != 0: one-tap K-tail mode (forward)
+    (4, 256, 9, 520, 1, 1, 0),       # K-tail on the data gradient (its Cs = 520)
 ]
 
 
