@@ -404,7 +404,8 @@ class TrainStep:
             return self._weighted_exchange(loss, finished, self.g)
         if getattr(self, "_late_stream", None) is None:
             self._late_stream = torch.cuda.Stream(device=self.device)
-            self._late_g = ops.zero_(torch.empty_like(self.g))
+            with torch.cuda.stream(self._late_stream):     # zeroed on the stream that reads it (the compute stream
+                self._late_g = ops.zero_(torch.empty_like(self.g))   # may be backlogged: a fill there races the use)
         cur = torch.cuda.current_stream(self.device)
         s = self._late_stream
         with torch.cuda.stream(s):
