@@ -1196,6 +1196,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_conv_impl", &bigdl_set_conv_impl);
   m.def("get_conv_impl", &bigdl_get_conv_impl);
   m.def("set_conv_g4", &bigdl_set_conv_g4);
+  m.def("set_conv_shortk", &bigdl_set_conv_shortk);
   m.def("set_conv_p8", &bigdl_set_conv_p8);
   m.def("set_wgrad_p8", &bigdl_set_wgrad_p8);
   m.def("conv_wgrad_uses_p8", &conv_wgrad_uses_p8);
@@ -1205,6 +1206,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_i8_g3", &bigdl_set_i8_g3);
   m.def("set_i8_p8", &bigdl_set_i8_p8);
   m.def("set_i8_epi", &bigdl_set_i8_epi);
+  m.def("set_i8_shortk", &bigdl_set_i8_shortk);
   m.def("get_i8_g3", &bigdl_get_i8_g3);
   m.def("set_i8_cpl", &bigdl_set_i8_cpl);
   m.def("get_i8_cpl", &bigdl_get_i8_cpl);

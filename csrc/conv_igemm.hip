@@ -1935,8 +1935,11 @@ __global__ __launch_bounds__(512, 1) void conv_nt_w8_kernel(ConvArgs a) {
 // its LDS read, coefficients loaded per K-step (what folding a BN apply into the consumer's operand would cost).
 __device__ float g_abn_tab[2 * 4096];
 template <int BN, int NS, bool FASTK = true, int BM = 128, int ABN = 0>
-__global__ __launch_bounds__(256, (NS == 3 && BM == 128) ? 3 : 2) void conv_nt_g4_kernel(ConvArgs a) {
+// NS = 2 (short-K variant, BIGDL_CONV_SHORTK): Kdim <= 64, both K-steps issued up front, 32 KB of stages and four
+// workgroups per CU for these one-DMA-round, epilogue-heavy tiles (the caller guarantees nk <= 2).
+__global__ __launch_bounds__(256, NS == 2 ? 4 : ((NS == 3 && BM == 128) ? 3 : 2)) void conv_nt_g4_kernel(ConvArgs a) {
   constexpr int BKS = 32;
+  constexpr bool SHORTK = NS == 2;
   constexpr int WGM = 2, WGN = 2;
   constexpr int TM = BM / WGM, TN = BN / WGN;      // 64 x 64 (or 64 x 32) per wave
   constexpr int MI = TM / 16, NI = TN / 16;
@@ -2039,10 +2042,10 @@ __global__ __launch_bounds__(256, (NS == 3 && BM == 128) ? 3 : 2) void conv_nt_g
 
   // prologue: K-steps 0 .. NS - 2 in flight; retire step 0
 #pragma unroll
-  for (int k = 0; k < NS - 1; ++k)
+  for (int k = 0; k < (SHORTK ? 2 : NS - 1); ++k)
     if (k < nk) issue(k, k);
   {
-    const int ahead = min(nk - 1, NS - 2);     // steps in flight behind step 0
+    const int ahead = min(nk - 1, SHORTK ? 1 : NS - 2);     // steps in flight behind step 0
     if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * L) : "memory");
     else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(L) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -2051,7 +2054,7 @@ __global__ __launch_bounds__(256, (NS == 3 && BM == 128) ? 3 : 2) void conv_nt_g
   int cur = 0;
   for (int kt = 0; kt < nk; ++kt) {
     // stage (kt + NS - 1) % NS == (kt - 1) % NS was last read in step kt - 1, before the barrier that ended it
-    if (kt + NS - 1 < nk) issue(kt + NS - 1, cur == 0 ? NS - 1 : cur - 1);
+    if (!SHORTK && kt + NS - 1 < nk) issue(kt + NS - 1, cur == 0 ? NS - 1 : cur - 1);
     const bf16_t* A = lds + cur * STAGE;
     const bf16_t* B = A + BM * BKS;
     v8s fa[MI], fb[NI];
@@ -2544,6 +2547,18 @@ static bool g4_slowk() {
   return v != 0;
 }
 
+// BIGDL_CONV_SHORTK (default 0): the two-stage, 4-workgroups-per-CU variant of the 128 x 64 multi-stage kernel when
+// Kdim <= 64 and Ncol <= 64. Measured neutral on ResNet-50 b256 training (25.78 / 25.89 vs 25.81 / 25.91 ms,
+// profiles/r4_shortk_ab.txt)
+int g_conv_shortk = -1;
+static bool conv_shortk() {
+  if (g_conv_shortk < 0) {
+    const char* e = getenv("BIGDL_CONV_SHORTK");
+    g_conv_shortk = e ? atoi(e) : 0;
+  }
+  return g_conv_shortk != 0;
+}
+
 int g_conv_impl = -1;
 int conv_impl() {
   if (g_conv_impl < 0) {
@@ -2559,6 +2574,7 @@ extern "C" {
 
 void bigdl_set_conv_impl(int impl) { g_conv_impl = impl; }
 void bigdl_set_conv_g4(int v) { g_conv_g4 = v; }
+void bigdl_set_conv_shortk(int v) { g_conv_shortk = v; }
 int g_wgrad_p8 = -1;
 void bigdl_set_conv_p8(int v) { g_conv_p8 = v; }
 void bigdl_set_wgrad_p8(int v) { g_wgrad_p8 = v; }
@@ -2638,6 +2654,8 @@ int bigdl_conv_nt(const ConvArgs* a, hipStream_t st) {
     const long tiles256 = (long)((a->M + 255) / 256) * ((a->Ncol + 127) / 128);
     if (a->Ncol > 64 && (g4_pick() == 7 || (g4_pick() == 6 && tiles256 >= 512))) {
       launch_nt_g4<128, 3, 256>(*a, st);
+    } else if (conv_shortk() && fastk && a->Kdim <= 64 && a->Ncol <= 64) {
+      launch_nt_g4<64, 2>(*a, st);   // (the 128-wide tile needs 168 VGPRs: no fourth workgroup)
     } else if (g4_pick() != 4) {
       if (a->Ncol <= 64) launch_nt_g4<64, 3>(*a, st);
       else launch_nt_g4<128, 3>(*a, st);

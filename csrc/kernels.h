@@ -183,6 +183,7 @@ void bigdl_copy_rows_i8(const int8_t* src, int8_t* dst, long rows, int C, long l
 void bigdl_set_conv_impl(int impl);
 int bigdl_get_conv_impl();
 void bigdl_set_conv_g4(int v);
+void bigdl_set_conv_shortk(int v);
 void bigdl_set_conv_p8(int v);
 void bigdl_set_wgrad_p8(int v);
 int bigdl_conv_wgrad_uses_p8(const WgradArgs* a);
@@ -192,6 +193,7 @@ int bigdl_get_wgrad_g3();
 void bigdl_set_i8_g3(int v);
 void bigdl_set_i8_p8(int v);
 void bigdl_set_i8_epi(int v);
+void bigdl_set_i8_shortk(int v);
 int bigdl_get_i8_g3();
 void bigdl_set_i8_cpl(int v);
 int bigdl_get_i8_cpl();

@@ -525,17 +525,20 @@ __device__ __forceinline__ void i8_tile_epilogue_direct(const ConvArgs& a, const
 // waves stacked along M (as conv_i8_glds_kernel).
 // FASTK = false (Cs % 64 != 0: Inception's 48 / 80 / 96 / 160 / ...-channel inputs, padded to 16): every lane resolves
 // the tap of its own 16-channel granule from the LDS tap table; the K tail past Kdim loads zeros.
-template <int BM, int BN, int WGM, int WGN, bool FASTK = true, int CPL = 8, bool DIRECT = false>
-__global__ __launch_bounds__(256, (BM + (BN + 63) / 64 * 64) * 64 * 3 <= 52 * 1024 ? 3 : 2) void conv_i8_g3_kernel(
-    ConvArgs a, I8Epi ep) {
-  constexpr int BKB = 64, NS = 3;
+// NS_ = 2 (short-K variant, Kdim <= 128: at most two K-steps, no ring): two 16 KB stages and the epilogue in four row
+// chunks, so 4 workgroups share a CU instead of 3 — these layers are one or two K-steps per tile and latency-bound.
+template <int BM, int BN, int WGM, int WGN, bool FASTK = true, int CPL = 8, bool DIRECT = false, int NS_ = 3>
+__global__ __launch_bounds__(256, NS_ == 2 ? 4 : ((BM + (BN + 63) / 64 * 64) * 64 * 3 <= 52 * 1024 ? 3 : 2)) void
+conv_i8_g3_kernel(ConvArgs a, I8Epi ep) {
+  constexpr int BKB = 64, NS = NS_;
   constexpr int TM = BM / WGM, TN = BN / WGN;
   constexpr int MI = TM / 16, NI = TN / 16;
   constexpr int AI = BM / 64, BI = (BN + 63) / 64;   // DMA instructions per thread per stage (4 waves x 16 rows)
   constexpr int STAGE = (BM + BI * 64) * BKB;         // bytes (B region rounded up to the 64 rows one DMA pass fills)
   constexpr int L = AI + BI;
-  constexpr int NH = 2;
-  static_assert(4 * (TM / NH) * TN * 4 <= NS * STAGE, "epilogue half must fit the stages");
+  constexpr int NH = NS == 2 ? 4 : 2;
+  static_assert(NS == 2 || NS == 3, "stage ring of three, or the short-K pair");
+  static_assert(4 * (TM / NH) * TN * 4 <= NS * STAGE, "epilogue chunk must fit the stages");
   __shared__ __attribute__((aligned(1024))) uint8_t lds[NS * STAGE + 6 * CONV_MAX_TAPS];
   short* taps = reinterpret_cast<short*>(lds + NS * STAGE);
   const uint8_t* src = reinterpret_cast<const uint8_t*>(a.src);
@@ -637,7 +640,7 @@ __global__ __launch_bounds__(256, (BM + (BN + 63) / 64 * 64) * 64 * 3 <= 52 * 10
   __builtin_amdgcn_s_barrier();
   int cur = 0;
   for (int kt = 0; kt < nk; ++kt) {
-    const bool more2 = kt + 2 < nk;
+    const bool more2 = NS == 3 && kt + 2 < nk;   // NS == 2: the caller guarantees nk <= 2
     if (more2) issue(kt + 2, cur == 0 ? 2 : cur - 1);
     const uint8_t* A = lds + cur * STAGE;
     const uint8_t* B = A + BM * BKB;
@@ -1059,8 +1062,28 @@ bool i8_direct_ok(const ConvArgs& a, const I8Epi& ep) {
          (ep.out_mode != 1 || a.ldo % 4 == 0);
 }
 
+// BIGDL_I8_SHORTK (default 0): 1 = the two-stage, 4-workgroups-per-CU 128 x 128 variant when Kdim <= 128 (fast-K);
+// 2: that variant with the 8-channel epilogue (106 VGPRs, no spill, vs 16 spilled VGPRs with 16 channels per lane).
+// Measured: 1 slower (ResNet-50 int8 3.83 -> 4.22 ms), 2 neutral (3.85 ms) — the one-K-step layers are not
+// occupancy-bound (profiles/r4_shortk_ab.txt)
+int g_i8_shortk = -1;
+bool i8_shortk() {
+  if (g_i8_shortk < 0) {
+    const char* e = getenv("BIGDL_I8_SHORTK");
+    g_i8_shortk = e ? atoi(e) : 0;
+  }
+  return g_i8_shortk != 0;
+}
+
 template <int BM, int BN, int WGM, int WGN>
 void launch_i8_g3(int g, bool fk, const ConvArgs& a, const I8Epi& ep, hipStream_t st) {
+  if constexpr (BM == 128 && BN == 128) {
+    if (fk && a.Kdim <= 128 && i8_shortk() && !i8_direct_ok(a, ep)) {
+      if (i8_cpl() == 16 && g_i8_shortk != 2) conv_i8_g3_kernel<BM, BN, WGM, WGN, true, 16, false, 2><<<g, 256, 0, st>>>(a, ep);
+      else conv_i8_g3_kernel<BM, BN, WGM, WGN, true, 8, false, 2><<<g, 256, 0, st>>>(a, ep);
+      return;
+    }
+  }
   if (fk && i8_direct_ok(a, ep)) {
     conv_i8_g3_kernel<BM, BN, WGM, WGN, true, 16, true><<<g, 256, 0, st>>>(a, ep);
     return;
@@ -1127,6 +1150,7 @@ static bool i8_p8() {
 }
 void bigdl_set_i8_p8(int v) { g_i8_p8 = v; }
 void bigdl_set_i8_epi(int v) { g_i8_epi = v; }
+void bigdl_set_i8_shortk(int v) { g_i8_shortk = v; }
 void bigdl_set_i8_cpl(int v) { g_i8_cpl = v; }
 int bigdl_get_i8_cpl() { return i8_cpl(); }
 int bigdl_get_i8_g3() { return i8_g3() ? g_i8_g3 : 0; }

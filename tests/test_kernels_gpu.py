@@ -624,14 +624,16 @@ G4_CASES = [
     (4, 48, 14, 128, 3, 1, 1),       # Cs % 32 != 0: per-lane taps (slow-K), K tail
     (2, 80, 9, 200, 1, 1, 0),        # slow-K 1x1, Ncol tail
     (3, 40, 11, 64, 3, 2, 1),        # slow-K, BN = 64 tile, stride 2
+    (8, 64, 28, 64, 1, 1, 0),        # Kdim 64, Ncol 64: the two-stage short-K variant (stages 2) in both passes
+    (5, 64, 13, 40, 1, 1, 0),        # short-K, Ncol tail, M tail
 ]
 
 
-@pytest.mark.parametrize("stages", [4, 3, 7])
+@pytest.mark.parametrize("stages", [4, 3, 7, 2])
 @pytest.mark.parametrize("case", G4_CASES)
 def test_conv_g4_kernel_fwd_dgrad(case, stages):
     """128 x BN 4-wave kernel with 3 / 4 counted-vmcnt LDS-DMA stages (BIGDL_CONV_G4; 7 = the 256 x 128 tile for
-    Ncol > 64) vs fp32 torch: forward with
+    Ncol > 64; 2 = BIGDL_CONV_G4=3 with the two-stage short-K variant, BIGDL_CONV_SHORTK=1) vs fp32 torch: forward with
     bias + BN statistics, forward + ReLU, data gradient with a residual addend."""
     from bigdl_amd.ops import bn as bnops
     from bigdl_amd.ops import conv as cv
@@ -639,7 +641,8 @@ def test_conv_g4_kernel_fwd_dgrad(case, stages):
 
     C_ = native.get()
     old = C_.get_conv_g4()
-    C_.set_conv_g4(stages)
+    C_.set_conv_g4(3 if stages == 2 else stages)
+    C_.set_conv_shortk(1 if stages == 2 else 0)
     try:
         N, C, H, K, R, st, pd = case
         torch.manual_seed(7)
@@ -664,6 +667,7 @@ def test_conv_g4_kernel_fwd_dgrad(case, stages):
         torch.cuda.synchronize()
     finally:
         C_.set_conv_g4(old)
+        C_.set_conv_shortk(0)
 
 
 WGRAD_G3_CASES = WGRAD_CASES + [

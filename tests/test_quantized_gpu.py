@@ -65,6 +65,26 @@ def test_conv_i8_exact_integer(case, g3, cpl):
         C_.set_i8_epi(0)
 
 
+I8_SHORTK_CASES = [
+    (3, 64, 14, 14, 200, 1, 1, 1, 0, 1),    # one K-step, Ncol tail
+    (3, 128, 13, 13, 256, 1, 1, 1, 0, 1),   # two K-steps, M tail
+    (2, 64, 15, 15, 136, 1, 1, 2, 0, 1),    # stride 2, Ncol tail
+]
+
+
+@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("case", I8_SHORTK_CASES)
+def test_conv_i8_shortk_exact_integer(case, mode):
+    """Two-stage 128 x 128 short-K int8 kernel (Kdim <= 128; BIGDL_I8_SHORTK 1: 16 channels per lane in the epilogue,
+    2: 8; off by default): fp32 output equal to the integer conv."""
+    C_ = native.get()
+    C_.set_i8_shortk(mode)
+    try:
+        _conv_i8_exact(case)
+    finally:
+        C_.set_i8_shortk(0)
+
+
 I8_P8_CASES = [
     (2, 256, 9, 9, 256, 3, 3, 1, 1, 1),     # one 256 x 256 tile, 18 K-tiles, padding taps
     (3, 1024, 7, 7, 512, 1, 1, 1, 0, 1),    # 1x1, two N tiles, M tail
