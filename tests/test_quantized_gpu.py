@@ -105,6 +105,41 @@ def test_conv_i8_p8_exact_integer(case):
         C_.set_i8_p8(1)
 
 
+@pytest.mark.parametrize("relu", [False, True])
+@pytest.mark.parametrize("g3", [1, 0, 3])
+@pytest.mark.parametrize("case", [I8_CASES[1], I8_CASES[4], I8_CASES[7], I8_CASES[9], I8_P8_CASES[1]])
+def test_conv_i8_int8_output_exact(case, g3, relu):
+    """int8 output (requantized, out_scale 1) with an int8 residual addend: with unit scales the result is the integer
+    conv + bias + addend, clamped to [-127, 127] (or [0, 127] with the ReLU) — exact, for every int8 kernel."""
+    from bigdl_amd.ops.conv import _fwd_taps, out_size
+
+    C_ = native.get()
+    old = C_.get_i8_g3()
+    C_.set_i8_g3(g3)
+    C_.set_i8_p8(2 if g3 == 3 else 1)   # g3 == 3: the 256 x 256 kernel wherever the shape allows
+    try:
+        N, C, H, W, K, R, S, st, pd, dl = case
+        g = torch.Generator().manual_seed(3)
+        x = torch.randint(-3, 4, (N, H, W, C), generator=g, dtype=torch.int8)   # small: most outputs inside the range
+        w = torch.randint(-3, 4, (K, R, S, C), generator=g, dtype=torch.int8)
+        OH, OW = out_size(H, R, st, pd, dl), out_size(W, S, st, pd, dl)
+        ref = F.conv2d(x.permute(0, 3, 1, 2).double(), w.permute(0, 3, 1, 2).double(), None, st, pd, dl)
+        ref = ref.permute(0, 2, 3, 1).reshape(N * OH * OW, K)
+        bias = torch.randint(-20, 21, (K,), generator=g).float()
+        add = torch.randint(-127, 128, (N * OH * OW, K), generator=g, dtype=torch.int8)
+        exp = (ref + bias.double() + add.double()).clamp(0 if relu else -127, 127).to(torch.int8)
+        out = torch.zeros(N * OH * OW, K, dtype=torch.int8, device="cuda")
+        ones_x, ones_w = torch.ones(N, device="cuda"), torch.ones(K, device="cuda")
+        geo = [N, H, W, C, OH, OW, st, st, R * S * C, K, K, OH, OW, 1, 1, 0, 0]
+        C_.conv_i8(x.cuda(), w.cuda(), out, bias.cuda(), ones_x, ones_w, geo, _fwd_taps(R, S, pd, pd, dl, dl), relu,
+                   1.0, 1.0, add.view(N, OH, OW, K).cuda(), 1.0)
+        torch.cuda.synchronize()
+        assert torch.equal(out.cpu(), exp)
+    finally:
+        C_.set_i8_g3(old)
+        C_.set_i8_p8(1)
+
+
 def _conv_i8_exact(case):
     from bigdl_amd.ops.conv import _fwd_taps, out_size
 

@@ -5,7 +5,7 @@ For every distinct conv shape (tools/bench_conv.py SHAPES, counted as in the net
 epilogue), with the bytes bound of each (operands read once, result written once, at --hbm TB/s) and the
 FLOP bound at the dense i8 / bf16 MFMA peaks, and prints the int8 / bf16 speedup per layer and count-weighted.
 
-    python tools/int8_roofline.py [--batch 256] [--iters 20]
+    python tools/int8_roofline.py [--batch 256] [--iters 20] [--only IDX]
 """
 import argparse
 import os
@@ -45,6 +45,7 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--hbm", type=float, default=8.0)
+    ap.add_argument("--only", type=int, default=-1, help="time one shape index (PMC passes)")
     a = ap.parse_args()
     N, dev, hbm = a.batch, torch.device("cuda"), a.hbm * 1e12
     C_ = native.get()
@@ -52,7 +53,7 @@ def main():
           f"{'bf bnd':>7} {'i8/bf16':>7}", flush=True)
     tot_i8 = tot_bf = 0.0
     for si, (C, H, K, R, st, pd, cnt) in enumerate(SHAPES):
-        if si == 0:
+        if si == 0 or (a.only >= 0 and si != a.only):
             continue                      # the stem runs as a width-im2col int8 conv in the plan (own kernel)
         OH = out_size(H, R, st, pd)
         g = torch.Generator(device=dev).manual_seed(si)
