@@ -251,6 +251,10 @@ def _convert_layer(layer, ctx):
         return nn.LeakyReLU(slope) if slope else nn.ReLU(True)
     if t == "PReLU":
         return nn.PReLU(int(blobs[0].numel()) if blobs else 0)
+    if t in ("Recurrent", "RNN"):
+        # Converter.scala:200-202: a bare Recurrent container (the cell is not described by the Caffe layer); its
+        # weights land through load_caffe_into once a cell is added
+        return nn.Recurrent()
     if t == "ELU":
         return nn.ELU(_g(_g(layer, "elu_param", {}), "alpha", 1.0))
     if t == "Sigmoid":
@@ -367,6 +371,17 @@ def _is_test_excluded(layer):
 
 def _copy_blobs(module, blobs, name):
     """Copy Caffe blobs into the module's parameters (BN: mean/var/scale-factor into running stats)."""
+    if isinstance(module, nn.Recurrent):       # every parameter of the cell, in parameters() order
+        if module.cell is None:                 # a bare imported container has no parameters yet (reference)
+            return
+        ps = (module.parameters() or ([], []))[0]
+        if len(blobs) != len(ps):
+            raise ValueError(f"{name}: {len(blobs)} blobs for a Recurrent with {len(ps)} parameters")
+        for dst, b in zip(ps, blobs):
+            if dst.numel() != b.numel():
+                raise ValueError(f"{name}: blob size {tuple(b.shape)} does not match parameter {tuple(dst.shape)}")
+            dst.data.copy_(b.reshape(dst.shape))
+        return
     if isinstance(module, nn.BatchNormalization) and not module.affine:
         sf = float(blobs[2].reshape(-1)[0]) if len(blobs) > 2 else 1.0
         sf = 1.0 / sf if sf != 0 else 0.0
@@ -477,7 +492,20 @@ def load_caffe_into(model, defPath, modelPath, matchAll=True, customizedConverte
         if l.get("blobs"):
             weights[_g(l, "name")] = [blob_to_tensor(b) for b in l["blobs"]]
     byname = {m.getName(): m for m in model.flattened_layers() if m.hasName()}
+
+    def walk(m):
+        yield m
+        for c in getattr(m, "modules", None) or []:
+            yield from walk(c)
+
+    for m in walk(model):     # Recurrent containers carry their cell's weights as one Caffe layer
+        if isinstance(m, nn.Recurrent) and m.hasName() and m.getName() in weights:
+            byname[m.getName()] = m
     for name, m in byname.items():
+        if isinstance(m, nn.Recurrent):
+            if name in weights:
+                _copy_blobs(m, weights[name], name)
+            continue
         if not m._params and not isinstance(m, nn.BatchNormalization):
             continue
         if name not in weights:
@@ -553,6 +581,10 @@ def _layer_def(m, name, bottoms, tops):
     elif isinstance(m, nn.CAddTable):
         d["type"] = ["Eltwise"]
         d["eltwise_param"] = [{"operation": ["SUM"]}]
+    elif isinstance(m, nn.Recurrent):
+        # LayerConverter.scala:530-532: type "Recurrent" with the module's weights as blobs (no recurrent_param)
+        d["type"] = ["Recurrent"]
+        blobs = list((m.parameters() or ([], []))[0]) if m.cell is not None else []
     elif isinstance(m, (nn.View, nn.Reshape, nn.InferReshape)):
         d["type"] = ["Flatten"]
     else:

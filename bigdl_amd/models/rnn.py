@@ -26,5 +26,6 @@ class PTBModel:
         if keepProb < 1:
             x = nn.Dropout(keepProb).inputs(x)
         for _ in range(numLayers):
-            x = nn.Recurrent().add(nn.LSTM(hiddenSize, hiddenSize, 0)).inputs(x)
+            # bf16 sequence I/O between the projection GEMMs and the persistent recurrence (opt-in, GPU only)
+            x = nn.Recurrent(bf16IO=True).add(nn.LSTM(hiddenSize, hiddenSize, 0)).inputs(x)
         return nn.Graph(inp, nn.TimeDistributed(nn.Linear(hiddenSize, outputSize)).inputs(x))

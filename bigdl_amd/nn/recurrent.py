@@ -317,6 +317,7 @@ class _LSTMSeq(torch.autograd.Function):
             C.cast_f32_bf16(h0.contiguous(), h16[0])
             ctx.seq = bool(C.lstm_seq_supported(B, H))
             if ctx.seq:
+                ops.native.check_persistent()      # an earlier launch's timeout surfaces before more work is queued
                 # whole sequence in ONE persistent launch (csrc/lstm_seq.hip): W resident in VGPRs, per-step
                 # state exchange inside each XCD's batch group; bf16 xg -> bf16 out (the projections' dtype)
                 sync = torch.empty(C.lstm_seq_sync_words(), dtype=torch.int32, device=xg.device)
@@ -356,6 +357,7 @@ class _LSTMSeq(torch.autograd.Function):
         C = ops.native.get()
         dout = dout.contiguous() if dout is not None else None
         if ctx.seq:
+            ops.native.check_persistent()
             # one persistent launch for the whole backward sweep, dh0 = dg_0 U included (no transposed copy of U)
             dxg = out.new_empty(B, T, 4 * H)        # out's dtype: bf16 in, bf16 gradient out
             if dout is not None and dout.dtype != out.dtype:
@@ -714,14 +716,23 @@ class MultiRNNCell(Cell):
 class Recurrent(Container):
     """Runs a Cell over [batch, time, ...] input (S/nn/Recurrent.scala:47). Output [batch, time, hidden...]."""
 
-    def __init__(self, batchNormParams=None, maskZero=False):
+    def __init__(self, batchNormParams=None, maskZero=False, bf16IO=False):
         super().__init__()
         self.batchNormParams = batchNormParams
         self.maskZero = maskZero
+        # bf16IO (opt-in, GPU engine): when the whole-sequence kernels apply, take the projection GEMM's bf16 output
+        # as is and return bf16 (no f32 round trip of [B, T, 4H] / [B, T, H]). Off by default: the output is fp32 on
+        # every path, whatever the batch size or GPU (the reference's LSTM output dtype)
+        self.bf16IO = bf16IO
         self.cell = None
         self.bn = None
         self._init_hidden = None
         self._last_hidden = None
+
+    def setBf16IO(self, on=True):
+        """Opt in (or out) of bf16 sequence I/O on the GPU whole-sequence path (see __init__)."""
+        self.bf16IO = bool(on)
+        return self
 
     def add(self, cell):
         assert isinstance(cell, Cell), "Recurrent.add expects a Cell"
@@ -771,8 +782,8 @@ class Recurrent(Container):
         x2, self._flat = self._project(input)
         need_grad = self.train
         mask0 = None if not self.maskZero else True
-        if (self.bn is None and mask0 is None and x2.is_cuda and x2.dtype == torch.bfloat16
-                and self.cell.bf16_sequence_ok(x2)):
+        if (getattr(self, "bf16IO", False) and self.bn is None and mask0 is None and x2.is_cuda
+                and x2.dtype == torch.bfloat16 and self.cell.bf16_sequence_ok(x2)):
             x2l = x2.detach().requires_grad_(need_grad)     # bf16 straight from the projection GEMM
         else:
             x2l = _f32(x2.detach()).requires_grad_(need_grad)

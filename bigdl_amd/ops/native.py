@@ -37,3 +37,21 @@ def available():
 def so_path():
     mod = get()
     return os.path.abspath(mod.__file__)
+
+
+class PersistentKernelTimeout(RuntimeError):
+    """A whole-sequence persistent kernel (csrc/lstm_seq.hip) gave up waiting for a co-resident workgroup: its
+    outputs of that launch are NaN-poisoned and the iteration must not be trusted."""
+
+
+def check_persistent(clear=True):
+    """Raise PersistentKernelTimeout if a persistent kernel recorded a timeout since the last check. Reads a
+    host-mapped word the kernels write with system scope: no device synchronisation. Called by every persistent
+    launch site and by ``TrainStep.throttle`` once the device has finished an iteration."""
+    if _C is None:
+        return
+    n = int(_C.persistent_error(bool(clear)))
+    if n:
+        raise PersistentKernelTimeout(
+            "a persistent recurrent kernel timed out waiting for a co-resident workgroup (another stream held CUs "
+            "past the bound set by set_seq_timeout_us); the affected outputs were poisoned with NaN")

@@ -5,6 +5,8 @@ dimension reductions) and the MKL BLAS entry points of S/tensor/TensorMath.scala
 dot). ``native_ok(*tensors)`` says whether a call can take this path (every tensor fp32 on the GPU); the Tensor API
 falls back to torch for other dtypes and for the CPU engine.
 """
+import os
+
 import torch
 from torch.autograd.graph import increment_version
 
@@ -150,10 +152,28 @@ def _idx_ok(idx):
 
 
 def _err(dev):
-    e = _ERR.get(dev)
-    if e is None:
-        e = _ERR[dev] = torch.zeros(1, dtype=torch.int32, device=dev)
-    return e
+    """None: the kernels report out-of-range indices into the process's host-mapped error word (host_word slot 1)."""
+    return None
+
+
+# BIGDL_INDEX_CHECK: 1 (default) raise IndexError right after the op (one stream synchronisation, the reference's
+# DenseTensor 'index out of bound' semantics); 0 = deferred: an error surfaces at the next index op / check_index_errors()
+_INDEX_SYNC = os.environ.get("BIGDL_INDEX_CHECK", "1") != "0"
+
+
+def check_index_errors(sync=True):
+    """Raise IndexError if an index kernel met a 1-based index outside its dimension since the last check."""
+    if sync:
+        torch.cuda.current_stream().synchronize()
+    if native.get().host_word(1, True):
+        raise IndexError("index out of bound (1-based index outside the indexed dimension)")
+
+
+def _index_op(*args):
+    check_index_errors(sync=False)           # a deferred error of an earlier op surfaces first
+    native.get().index_op(*args)
+    if _INDEX_SYNC:
+        check_index_errors(sync=True)
 
 
 def _c(t):
@@ -175,7 +195,7 @@ def index_select(src, dim, idx):
     shape = list(src.shape)
     shape[dim] = idx.numel()
     out = torch.empty(shape, device=src.device, dtype=torch.float32)
-    native.get().index_op(0, None, idx, src, out, outer, R, idx.numel(), inner, 0, _err(src.device))
+    _index_op(0, None, idx, src, out, outer, R, idx.numel(), inner, 0, _err(src.device))
     return out
 
 
@@ -188,7 +208,7 @@ def index_add(dst, dim, idx, src):
     outer, R, inner = _orc(tuple(dst.shape), dim)
     if src.numel() != outer * idx.numel() * inner:
         return None
-    native.get().index_op(1, dst, idx, src, None, outer, R, idx.numel(), inner, 0, _err(dst.device))
+    _index_op(1, dst, idx, src, None, outer, R, idx.numel(), inner, 0, _err(dst.device))
     increment_version(dst)
     return dst
 
@@ -202,7 +222,7 @@ def gather(src, dim, idx):
     idx, src = _c(idx), _c(src)
     outer, R, inner = _orc(tuple(src.shape), dim)
     out = torch.empty(idx.shape, device=src.device, dtype=torch.float32)
-    native.get().index_op(2, None, idx, src, out, outer, R, idx.shape[dim], inner, 0, _err(src.device))
+    _index_op(2, None, idx, src, out, outer, R, idx.shape[dim], inner, 0, _err(src.device))
     return out
 
 
@@ -216,7 +236,7 @@ def scatter(dst, dim, idx, src):
         return None
     idx, src = _c(idx), _c(src)
     outer, R, inner = _orc(tuple(dst.shape), dim)
-    native.get().index_op(3, dst, idx, src, None, outer, R, idx.shape[dim], inner, src.shape[dim], _err(dst.device))
+    _index_op(3, dst, idx, src, None, outer, R, idx.shape[dim], inner, src.shape[dim], _err(dst.device))
     increment_version(dst)
     return dst
 
@@ -255,6 +275,9 @@ def masked_copy(x, mask, src):
         return None
     mask, src = _c(mask), _c(src)
     counts = _mask_counts(mask)
+    n = int(counts.narrow(0, counts.numel() - 1, 1).item())
+    if src.numel() < n:           # torch masked_scatter_ / the reference's maskedCopy raise here
+        raise RuntimeError(f"maskedCopy: source has {src.numel()} elements, the mask selects {n}")
     native.get().mask_write(True, x, mask, src.reshape(-1), None, counts)
     increment_version(x)
     return x

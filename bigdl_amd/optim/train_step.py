@@ -511,6 +511,10 @@ class TrainStep:
         q.append(ev)
         while len(q) > self.MAX_INFLIGHT:
             wait_event(q.pop(0))
+        # the device finished at least that iteration: a persistent-kernel timeout in it is visible now
+        from ..ops import native
+
+        native.check_persistent()
 
     # ------------------------------------------------------------------ optimizer state (checkpoints)
     def _method_layout(self):

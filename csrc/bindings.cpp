@@ -182,6 +182,10 @@ void dgrad_fill(const Tensor& out, const OptT& addend, int64_t sh, int64_t sw, i
   bigdl_dgrad_fill(mbf(out, "out"), ocbf(addend, "addend"), out.size(0) * out.size(2) * out.size(3), out.size(2),
                    out.size(3), out.size(1), (int)sh, (int)sw, (unsigned)mask, stream());
 }
+void hog_cus(int64_t n, double us, const Tensor& done) {
+  TORCH_CHECK(done.is_cuda() && done.scalar_type() == at::kInt && done.numel() >= n, "hog_cus: done must be int32 cuda [n]");
+  bigdl_hog_cus((int)n, us, done.data_ptr<int>(), stream());
+}
 void spin_us(double us, const Tensor& done) {
   TORCH_CHECK(done.is_cuda() && done.scalar_type() == at::kInt && done.numel() >= 1, "spin_us: done must be int32 cuda");
   bigdl_spin_us(us, done.data_ptr<int>(), stream());
@@ -268,14 +272,20 @@ void tensor_reduce(const Tensor& x, int64_t outer, int64_t R, int64_t inner, int
 // index ops over [outer, R, inner] (csrc/index_ops.hip): op 0 index_select(b -> out), 1 index_add(b into a),
 // 2 gather(b -> out, idx shaped like out), 3 scatter(b into a, idx shaped like b's [outer, n, inner])
 void index_op(int64_t op, const OptT& a, const Tensor& idx, const OptT& b, const OptT& out, int64_t outer, int64_t R,
-              int64_t n, int64_t inner, int64_t Rsrc, const Tensor& err) {
+              int64_t n, int64_t inner, int64_t Rsrc, const OptT& err) {
   TORCH_CHECK(idx.is_cuda() && idx.is_contiguous() && (idx.scalar_type() == at::kFloat || idx.scalar_type() == at::kLong),
               "index_op: idx must be a contiguous fp32 or int64 cuda tensor");
-  TORCH_CHECK(err.scalar_type() == at::kInt && err.is_cuda(), "index_op: err int32");
+  // err: an int32 cuda word, or None = the process's host-mapped index-error word (read back by host_word(1))
+  int* ep = reinterpret_cast<int*>(bigdl_host_word_dev(1));
+  if (err && err->defined()) {
+    TORCH_CHECK(err->scalar_type() == at::kInt && err->is_cuda(), "index_op: err int32");
+    ep = err->data_ptr<int>();
+  }
+  TORCH_CHECK(ep != nullptr, "index_op: no error word");
   for (const OptT* t : {&a, &b, &out})
     if (*t && (*t)->defined()) TORCH_CHECK((*t)->is_contiguous(), "index_op: operands must be contiguous");
   const int rc = bigdl_index_op((int)op, omf(a, "a"), idx.data_ptr(), idx.scalar_type() == at::kLong ? 1 : 0,
-                                ocf(b, "b"), omf(out, "out"), outer, R, n, inner, Rsrc, err.data_ptr<int>(), stream());
+                                ocf(b, "b"), omf(out, "out"), outer, R, n, inner, Rsrc, ep, stream());
   TORCH_CHECK(rc == 0, "index_op: unsupported op");
 }
 void masked_fill(const Tensor& x, const Tensor& mask, double v) {
@@ -1100,6 +1110,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("dgamma"), py::arg("dbeta"), py::arg("P"), py::arg("C"), py::arg("aff") = py::none());
   m.def("relu_fwd", &relu_fwd);
   m.def("dgrad_fill", &dgrad_fill);
+  m.def("hog_cus", &hog_cus, "n one-wave workgroups holding a whole CU's LDS each, spinning `us` microseconds");
   m.def("spin_us", &spin_us, "device-side delay of `us` microseconds on the current stream (straggler injection)");
   m.def("relu_bwd", &relu_bwd);
   m.def("add_bf16", &add_bf16);
@@ -1176,6 +1187,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("lstm_seq_supported", &lstm_seq_supported);
   m.def("set_lstm_seq", &bigdl_set_lstm_seq);
   m.def("lstm_seq_sync_words", &lstm_seq_sync_words);
+  m.def("host_word", [](int64_t slot, bool clear) { return (int64_t)bigdl_host_word((int)slot, clear ? 1 : 0); },
+        "read (and optionally clear) a process-wide host-mapped device-error word: 0 persistent timeouts, 1 index range");
+  m.def("persistent_error", [](bool clear) { return (int64_t)bigdl_persistent_error(clear ? 1 : 0); },
+        "timeouts recorded by persistent (whole-sequence) kernels since the last clear; reads a host-mapped word, no sync");
+  m.def("set_seq_timeout_us", &bigdl_set_seq_timeout_us, "bound of every persistent-kernel wait (<= 0: default 2 s)");
   m.def("lstm_seq_fwd", &lstm_seq_fwd);
   m.def("lstm_seq_bwd", &lstm_seq_bwd);
   m.def("colsum_bf16", &colsum_bf16);

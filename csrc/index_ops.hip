@@ -159,21 +159,27 @@ __global__ __launch_bounds__(256) void mask_write_kernel(float* __restrict__ x, 
 }
 
 // ---------------------------------------------------------------------------------------------- topk
-// One workgroup per row of R <= P elements (P = pow2 >= R, <= 8192): keys padded with +inf (ascending) or -inf
-// (descending), (key, index) pairs bitonic-sorted in LDS, the first k written (values, 1-based fp32 indices).
+// One workgroup per row of R <= P elements (P = pow2 >= R, <= 8192): (key, index) pairs bitonic-sorted in LDS on a
+// total-order 32-bit key, the first k written (values, 1-based fp32 indices). Key: the float's bits made monotone
+// (negative: all bits flipped, else the sign bit set), every NaN canonicalised to +NaN, which then orders above +inf:
+// last for smallest-k, first for largest-k (key complemented), as torch.topk orders NaN in both directions. Padding
+// takes the maximal key, so it sorts behind every element, NaN included.
+__device__ __forceinline__ unsigned topk_key(float v, int largest) {
+  unsigned u = __float_as_uint(v != v ? __builtin_nanf("") : v);
+  u = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+  return largest ? ~u : u;
+}
+
 template <int P>
 __global__ __launch_bounds__(256) void topk_kernel(const float* __restrict__ x, long R, long inner, int k, int largest,
                                                    float* __restrict__ vals, float* __restrict__ inds) {
-  __shared__ float key[P];
+  __shared__ unsigned key[P];
   __shared__ int id[P];
   const long row = blockIdx.x;
   const long o = row / inner, in = row % inner;
   const float* src = x + o * R * inner + in;
-  const float pad = largest ? -INFINITY : INFINITY;
   for (int t = threadIdx.x; t < P; t += 256) {
-    float v = t < R ? src[(long)t * inner] : pad;
-    if (v != v) v = largest ? INFINITY : -INFINITY;   // NaN orders first (torch topk convention)
-    key[t] = largest ? -v : v;                        // sort ascending on the signed key
+    key[t] = t < R ? topk_key(src[(long)t * inner], largest) : 0xffffffffu;
     id[t] = t;
   }
   __syncthreads();
@@ -183,7 +189,7 @@ __global__ __launch_bounds__(256) void topk_kernel(const float* __restrict__ x, 
         const int lo = 2 * t - (t & (stride - 1));
         const int hi = lo + stride;
         const bool up = (lo & size) == 0;
-        const float a = key[lo], b = key[hi];
+        const unsigned a = key[lo], b = key[hi];
         const int ia = id[lo], ib = id[hi];
         const bool gt = a > b || (a == b && ia > ib);   // stable on ties: lower index first
         if (gt == up) {

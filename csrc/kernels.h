@@ -254,6 +254,13 @@ int bigdl_lstm_bwd_step(const uint16_t* WT16, const uint16_t* dg16_next, const f
 int bigdl_lstm_seq_supported(int B, int H);
 void bigdl_set_lstm_seq(int v);
 int bigdl_lstm_seq_sync_words();
+int bigdl_persistent_error(int clear);
+unsigned* bigdl_host_word_dev(int slot);
+int bigdl_host_word(int slot, int clear);
+void bigdl_set_seq_timeout_us(double us);
+void bigdl_hog_cus(int n, double us, int* done, hipStream_t st);
+unsigned* bigdl_persistent_err_dev();
+unsigned long long bigdl_seq_spin_ticks();
 int bigdl_lstm_seq_fwd(const uint16_t* W16, const void* xg, const float* c0, uint16_t* h16, void* out, float* hT,
                        float* cs, float* acts, unsigned* sync, int B, int H, int T, int bf16io, hipStream_t st);
 int bigdl_lstm_seq_bwd(const uint16_t* W16, const void* dout, const float* dhT, const float* dcT, const float* acts,

@@ -20,8 +20,14 @@
 //    inter-workgroup rule: every handed-off byte is stored sc1 and drained before the counter add, every load of it is
 //    an sc1 load to registers behind the poll, and no other load reads bytes written in the launch.
 //  * counters are zeroed by a fill kernel ahead of every launch (graph-replay safe: no memset node, see
-//    bigdl_fill_bytes); every spin is bounded (0.5 s of the
-//    100 MHz wall clock): on timeout the workgroup sets the error word, poisons its outputs with NaN and leaves.
+//    bigdl_fill_bytes); every spin is bounded (2 s of the 100 MHz wall clock by default, bigdl_set_seq_timeout_us):
+//    on timeout the workgroup sets the launch's error word AND a process-wide host-mapped word, poisons EVERY output
+//    element it owns (remaining steps) with NaN and leaves. The host reads the mapped word without a device sync
+//    (bigdl_persistent_error: TrainStep.throttle and every persistent-kernel call check it and raise).
+//  * residency: correctness needs all 8 x H/32 workgroups co-resident. The launch is refused (per-step fallback) when
+//    the occupancy query of the exact kernel instantiation admits less than one 512-thread workgroup per CU or the
+//    grid exceeds the CU count; workgroups that are resident but wait on ones held back by OTHER streams' kernels
+//    just spin until those finish (nothing those kernels wait on depends on this launch), bounded by the timeout.
 // Forward per step: gates = W h_{t-1} (+ xg, the input projection computed beforehand as one GEMM), c and h in
 // fp32, h16 bf16 hand-off (also the B operand of the weight-gradient GEMM). Backward per step: dh = dout + dg_{t+1} W
 // (K = 4H split over the 4 gate blocks = 4 waves per unit tile, partials summed in LDS), the cell backward per
@@ -36,7 +42,7 @@ typedef __attribute__((address_space(1))) unsigned gu32;
 
 constexpr int NGRP = 8;                          // batch groups (= XCDs)
 constexpr int CNT_STRIDE = 32;                   // one 128-byte line per group counter
-constexpr unsigned long long SPIN_TICKS = 50000000ull;   // 0.5 s at 100 MHz
+unsigned long long g_spin_ticks = 200000000ull;         // 2 s at 100 MHz (bigdl_set_seq_timeout_us)
 
 struct LstmSeqArgs {
   const bf16_t* W16;       // [4H][H] gate blocks i, g, f, o
@@ -55,8 +61,27 @@ struct LstmSeqArgs {
   float* dc0;              // bwd: [B][H] (dc flowing into c0)
   float* dh0;              // bwd: [B][H]
   unsigned* sync;          // NGRP counters (CNT_STRIDE apart) + error word
+  unsigned* herr;          // process-wide host-mapped error word (device address)
+  unsigned long long spin; // bound of every wait, wall-clock ticks (100 MHz)
   int B, H, T, Bg;
 };
+
+// Host-mapped (fine-grained, coherent) error word shared by every persistent kernel of the process: a timeout stores
+// to it with system scope, so the host can see the failure without synchronising the device.
+unsigned* g_herr_host = nullptr;
+unsigned* g_herr_dev = nullptr;
+unsigned* host_err_dev() {
+  if (g_herr_dev == nullptr) {
+    void* h = nullptr;
+    if (hipHostMalloc(&h, 64, hipHostMallocMapped | hipHostMallocPortable | hipHostMallocCoherent) != hipSuccess) return nullptr;
+    for (int i = 0; i < 16; ++i) static_cast<volatile unsigned*>(h)[i] = 0u;
+    void* d = nullptr;
+    if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) return nullptr;
+    g_herr_host = static_cast<unsigned*>(h);
+    g_herr_dev = static_cast<unsigned*>(d);
+  }
+  return g_herr_dev;
+}
 
 __device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + __expf(-x)); }
 __device__ __forceinline__ float tanh_f(float x) {
@@ -77,12 +102,17 @@ __device__ __forceinline__ void st_sc1(v4u v, __amdgpu_buffer_rsrc_t r, int off)
 }
 
 // One lane polls the group counter (relaxed agent-scope load = global_load sc1) until it reaches target.
-__device__ __noinline__ bool wait_count(unsigned* cnt, unsigned target, unsigned* err) {
+__device__ __noinline__ bool wait_count(unsigned* cnt, unsigned target, unsigned* err, unsigned* herr,
+                                       unsigned long long spin) {
   const unsigned long long t0 = wall_clock64();
   while (__hip_atomic_load((gu32*)cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
     __builtin_amdgcn_s_sleep(1);
-    if (wall_clock64() - t0 > SPIN_TICKS) {
+    if (wall_clock64() - t0 > spin) {
       __hip_atomic_store((gu32*)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (herr) {
+        __hip_atomic_store(herr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      }
       return false;
     }
   }
@@ -90,9 +120,9 @@ __device__ __noinline__ bool wait_count(unsigned* cnt, unsigned target, unsigned
 }
 
 // Wave 0 polls, the verdict goes to every wave through LDS. Returns false when the group timed out.
-__device__ __forceinline__ bool group_wait(unsigned* cnt, unsigned target, unsigned* err, int* flag, int wave,
+__device__ __forceinline__ bool group_wait(unsigned* cnt, unsigned target, const LstmSeqArgs& a, int* flag, int wave,
                                            int lane) {
-  if (wave == 0 && lane == 0) *flag = wait_count(cnt, target, err) ? 0 : 1;
+  if (wave == 0 && lane == 0) *flag = wait_count(cnt, target, a.sync + NGRP * CNT_STRIDE, a.herr, a.spin) ? 0 : 1;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keeps the sc1 state loads below the poll
   __syncthreads();
   return *flag == 0;
@@ -131,7 +161,6 @@ __global__ __launch_bounds__(512, 1) void lstm_seq_fwd_kernel(LstmSeqArgs a) {
   }
   float c = a.c0 ? a.c0[(size_t)b * H + j] : 0.f;
   unsigned* cnt = a.sync + g * CNT_STRIDE;
-  unsigned* err = a.sync + NGRP * CNT_STRIDE;
   const size_t slab = (size_t)a.B * H;            // one time step of h16
 
   for (int t = 0; t < a.T; ++t) {
@@ -144,12 +173,20 @@ __global__ __launch_bounds__(512, 1) void lstm_seq_fwd_kernel(LstmSeqArgs a) {
       const float* xp = static_cast<const float*>(a.xg) + xo;
       x0 = xp[0]; x1 = xp[H]; x2 = xp[2 * H]; x3 = xp[3 * H];
     }
-    if (t > 0 && !group_wait(cnt, (unsigned)(M * t), err, &flag, wave, lane)) {
-      if (live)
+    if (t > 0 && !group_wait(cnt, (unsigned)(M * t), a, &flag, wave, lane)) {
+      // every element this lane owns from step t on: out, h16 (the weight-gradient operand), cs, acts, hT
+      if (live) {
+        const float nan = __builtin_nanf("");
         for (int u = t; u < a.T; ++u) {
           if constexpr (BIO) static_cast<bf16_t*>(a.out)[((size_t)b * a.T + u) * H + j] = 0x7fc0;
-          else static_cast<float*>(a.out)[((size_t)b * a.T + u) * H + j] = __builtin_nanf("");
+          else static_cast<float*>(a.out)[((size_t)b * a.T + u) * H + j] = nan;
+          a.h16[(u + 1) * slab + (size_t)b * H + j] = 0x7fc0;
+          a.cs[((size_t)u * a.B + b) * H + j] = nan;
+          float* ap = a.acts + ((size_t)u * a.B + b) * 4 * H + j;
+          ap[0] = nan; ap[H] = nan; ap[2 * H] = nan; ap[3 * H] = nan;
         }
+        if (a.hT) a.hT[(size_t)b * H + j] = nan;
+      }
       return;
     }
     {   // h_{t-1} of the group's rows -> LDS (rows past the group read as zero)
@@ -242,7 +279,6 @@ __global__ __launch_bounds__(512, 1) void lstm_seq_bwd_kernel(LstmSeqArgs a) {
   const int b = b_lo + (live ? bb : 0);
   float dc = a.dcT ? a.dcT[(size_t)b * H + j] : 0.f;
   unsigned* cnt = a.sync + g * CNT_STRIDE;
-  unsigned* err = a.sync + NGRP * CNT_STRIDE;
   const size_t slab = (size_t)a.B * G4;          // one time step of dg16
 
   // round i handles t = T-1-i; round T computes dh0 from dg_0
@@ -261,8 +297,23 @@ __global__ __launch_bounds__(512, 1) void lstm_seq_bwd_kernel(LstmSeqArgs a) {
       cp = t > 0 ? a.cs[((size_t)(t - 1) * a.B + b) * H + j] : (a.c0 ? a.c0[(size_t)b * H + j] : 0.f);
     }
     if (i > 0) {
-      if (!group_wait(cnt, (unsigned)(M * i), err, &flag, wave, lane)) {
-        if (live) a.dh0[(size_t)b * H + j] = __builtin_nanf("");
+      if (!group_wait(cnt, (unsigned)(M * i), a, &flag, wave, lane)) {
+        // every element this thread owns from step t down: dxg, dg16 (the weight-gradient operand), dc0, dh0
+        if (live) {
+          const float nan = __builtin_nanf("");
+          for (int u = t; u >= 0; --u) {
+            const size_t go = ((size_t)b * a.T + u) * G4 + j;
+            bf16_t* dp = a.dg16 + u * slab + (size_t)b * G4 + j;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              if constexpr (BIO) static_cast<bf16_t*>(a.dxg)[go + k * H] = 0x7fc0;
+              else static_cast<float*>(a.dxg)[go + k * H] = nan;
+              dp[k * H] = 0x7fc0;
+            }
+          }
+          a.dh0[(size_t)b * H + j] = nan;
+          a.dc0[(size_t)b * H + j] = nan;
+        }
         return;
       }
       {   // dg_{t+1} of the group's rows -> LDS
@@ -358,10 +409,29 @@ int cu_count() {
   return n;
 }
 
+// Occupancy of every instantiation the launch may pick for this H: at least one 512-thread workgroup per CU.
+template <int KS>
+bool occ_ok_ks() {
+  static const bool ok = [] {
+    int n = 0;
+    const void* ks[4] = {reinterpret_cast<const void*>(&lstm_seq_fwd_kernel<KS, true>),
+                         reinterpret_cast<const void*>(&lstm_seq_fwd_kernel<KS, false>),
+                         reinterpret_cast<const void*>(&lstm_seq_bwd_kernel<KS, true>),
+                         reinterpret_cast<const void*>(&lstm_seq_bwd_kernel<KS, false>)};
+    for (const void* k : ks) {
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, 512, 0) != hipSuccess || n < 1) return false;
+    }
+    return true;
+  }();
+  return ok;
+}
+
 bool seq_shape_ok(int B, int H) {
   if (!seq_enabled() || B <= 0 || (H != 256 && H != 512 && H != 1024)) return false;
   if ((B + NGRP - 1) / NGRP > 16) return false;
-  return NGRP * (H / 32) <= cu_count();   // one workgroup per CU, all resident
+  if (NGRP * (H / 32) > cu_count()) return false;   // one workgroup per CU, all resident
+  const bool occ = H == 1024 ? occ_ok_ks<32>() : H == 512 ? occ_ok_ks<16>() : occ_ok_ks<8>();
+  return occ && host_err_dev() != nullptr;
 }
 
 }  // namespace
@@ -372,12 +442,33 @@ int bigdl_lstm_seq_supported(int B, int H) { return seq_shape_ok(B, H) ? 1 : 0; 
 void bigdl_set_lstm_seq(int v) { g_lstm_seq = v; }
 int bigdl_lstm_seq_sync_words() { return NGRP * CNT_STRIDE + CNT_STRIDE; }
 
+// Timeouts recorded by persistent kernels since the last clear (host-mapped word: no device synchronisation).
+int bigdl_persistent_error(int clear) { return bigdl_host_word(0, clear); }
+// Process-wide host-mapped words (16 x 4 B, fine-grained): slot 0 persistent-kernel timeouts, slot 1 index-range
+// errors of the TensorMath index kernels. Device address for kernels; host reads need no synchronisation.
+unsigned* bigdl_host_word_dev(int slot) {
+  unsigned* d = host_err_dev();
+  return (d && slot >= 0 && slot < 16) ? d + slot : nullptr;
+}
+int bigdl_host_word(int slot, int clear) {
+  if (g_herr_host == nullptr || slot < 0 || slot >= 16) return 0;
+  volatile unsigned* p = g_herr_host + slot;
+  const unsigned v = *p;
+  if (clear && v) *p = 0u;
+  return (int)v;
+}
+// Bound of every persistent-kernel wait (tests force a timeout with a small value); <= 0 restores the default.
+void bigdl_set_seq_timeout_us(double us) { g_spin_ticks = us > 0 ? (unsigned long long)(us * 100.0) : 200000000ull; }
+unsigned* bigdl_persistent_err_dev() { return host_err_dev(); }
+unsigned long long bigdl_seq_spin_ticks() { return g_spin_ticks; }
+
 int bigdl_lstm_seq_fwd(const uint16_t* W16, const void* xg, const float* c0, uint16_t* h16, void* out, float* hT,
                        float* cs, float* acts, unsigned* sync, int B, int H, int T, int bf16io, hipStream_t st) {
   if (!seq_shape_ok(B, H) || T <= 0) return -1;
   LstmSeqArgs a{};
   a.W16 = W16; a.xg = xg; a.c0 = c0; a.h16 = h16; a.out = out; a.hT = hT; a.cs = cs; a.acts = acts; a.sync = sync;
   a.B = B; a.H = H; a.T = T; a.Bg = (B + NGRP - 1) / NGRP;
+  a.herr = host_err_dev(); a.spin = g_spin_ticks;
   bigdl_fill_bytes(sync, 0, (long)sizeof(unsigned) * bigdl_lstm_seq_sync_words(), st);   // kernel: graph-safe
   const dim3 grid(NGRP * (H / 32));
 #define SEQ_FWD(K)                                                  \
@@ -401,6 +492,7 @@ int bigdl_lstm_seq_bwd(const uint16_t* W16, const void* dout, const float* dhT, 
   a.W16 = W16; a.dout = dout; a.dhT = dhT; a.dcT = dcT; a.acts = const_cast<float*>(acts);
   a.cs = const_cast<float*>(cs); a.c0 = c0; a.dg16 = dg16; a.dxg = dxg; a.dc0 = dc0; a.dh0 = dh0; a.sync = sync;
   a.B = B; a.H = H; a.T = T; a.Bg = (B + NGRP - 1) / NGRP;
+  a.herr = host_err_dev(); a.spin = g_spin_ticks;
   bigdl_fill_bytes(sync, 0, (long)sizeof(unsigned) * bigdl_lstm_seq_sync_words(), st);   // kernel: graph-safe
   const dim3 grid(NGRP * (H / 32));
 #define SEQ_BWD(K)                                                  \

@@ -395,7 +395,25 @@ __global__ __launch_bounds__(64) void spin_us_kernel(long ticks, int* done) {
   while ((long)(wall_clock64() - t0) < ticks) __builtin_amdgcn_s_sleep(8);
   if (threadIdx.x == 0) done[0] = 1;
 }
+// CU hog: a one-wave workgroup that declares the whole 160 KiB LDS (one per CU) and spins, so no other workgroup with
+// LDS can be co-resident on that CU meanwhile. Tests use it to take CUs away from a persistent launch on another
+// stream (csrc/lstm_seq.hip residency / timeout tests). Capped at 5 s.
+__global__ __launch_bounds__(64) void hog_cu_kernel(long ticks, int* done) {
+  __shared__ int pad[160 * 1024 / 4];
+  pad[threadIdx.x * 640] = threadIdx.x;
+  const unsigned long t0 = wall_clock64();
+  while ((long)(wall_clock64() - t0) < ticks) __builtin_amdgcn_s_sleep(8);
+  __syncthreads();
+  if (threadIdx.x == 0) done[blockIdx.x] = pad[(threadIdx.x + 1) * 640 % 40960] + 1;
+}
 }  // namespace
+
+void bigdl_hog_cus(int n, double us, int* done, hipStream_t st) {
+  double t = us < 0 ? 0 : (us > 5e6 ? 5e6 : us);
+  if (n < 1) return;
+  hog_cu_kernel<<<n, 64, 0, st>>>((long)(t * 100.0), done);
+  HIP_LAUNCH_CHECK();
+}
 
 void bigdl_spin_us(double us, int* done, hipStream_t st) {
   double t = us < 0 ? 0 : (us > 5e6 ? 5e6 : us);

@@ -76,3 +76,33 @@ def test_text_format_parser_features():
     assert abs(C._g(C._g(l1, "relu_param"), "negative_slope") - 0.1) < 1e-9
     enc = C.SCHEMA.encode("NetParameter", net)
     assert C.SCHEMA.decode("NetParameter", enc)["layer"][0]["pooling_param"][0]["pool"] == ["AVE"]
+
+
+def test_recurrent_layer_roundtrip(tmp_path):
+    """Caffe "Recurrent" / "RNN" layers (Converter.scala:200-202,653-654; LayerConverter.scala:530-532): export writes
+    type Recurrent with the cell's weights as blobs; import builds a bare Recurrent container of that name, and
+    load_caffe_into puts the blobs back into a model that has the cell."""
+    torch.manual_seed(0)
+
+    def build():
+        return nn.Sequential().add(nn.Recurrent().add(nn.LSTM(4, 6, 0)).setName("rnn1")) \
+            .add(nn.Select(2, -1)).add(nn.Linear(6, 3).setName("fc"))
+
+    src = build()
+    pt, cm = str(tmp_path / "r.prototxt"), str(tmp_path / "r.caffemodel")
+    C.save_caffe(nn.Sequential().add(src.modules[0]), pt, cm, overwrite=True)
+    text = open(pt).read()
+    assert 'type: "Recurrent"' in text and 'name: "rnn1"' in text
+    g, _ = C.load_caffe(pt, cm)
+    rec = [m for m in g.flattened_layers() if isinstance(m, nn.Recurrent)] or \
+          [n.element for n in g.order if isinstance(n.element, nn.Recurrent)]
+    assert rec and rec[0].getName() == "rnn1" and rec[0].cell is None
+    # the same prototxt with the legacy "RNN" type string
+    open(pt, "w").write(text.replace('type: "Recurrent"', 'type: "RNN"'))
+    g2, _ = C.load_caffe(pt)
+    assert any(isinstance(n.element, nn.Recurrent) for n in g2.order)
+    # weights back into a model with the cell
+    dst = build()
+    C.load_caffe_into(dst, pt, cm, matchAll=False)
+    for a, b in zip(src.modules[0].parameters()[0], dst.modules[0].parameters()[0]):
+        assert torch.equal(a, b)

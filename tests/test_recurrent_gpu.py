@@ -3,6 +3,8 @@ the fp32 CPU engine."""
 import copy
 
 import pytest
+import time
+
 import torch
 
 pytestmark = pytest.mark.gpu
@@ -186,6 +188,69 @@ def test_persistent_lstm_sequence_matches_step_kernels(B, T, H):
     assert _rel(out, res[0][0]) < 1e-2
 
 
+def _hogged_lstm_forward(timeout_us, hog_us=300e3, n_hog=64, B=128, T=8, H=1024):
+    """Persistent LSTM forward launched while `n_hog` CUs are held (whole-LDS spinning workgroups) by a kernel on
+    another stream: some of the 256 workgroups cannot be resident until the hog ends."""
+    from bigdl_amd.ops import native
+
+    C = native.get()
+    torch.manual_seed(5)
+    xg = (torch.randn(B, T, 4 * H) * 0.5).cuda()
+    c0, h0 = (torch.randn(B, H) * 0.5).cuda(), (torch.randn(B, H) * 0.5).cuda()
+    W16 = (torch.randn(4 * H, H) / H ** 0.5).cuda().to(torch.bfloat16)
+
+    def run():
+        h16 = torch.zeros(T + 1, B, H, device="cuda", dtype=torch.bfloat16)
+        h16[0] = h0.to(torch.bfloat16)
+        out = torch.empty(B, T, H, device="cuda")
+        cs, acts = torch.empty(T, B, H, device="cuda"), torch.empty(T, B, 4 * H, device="cuda")
+        sync = torch.empty(C.lstm_seq_sync_words(), dtype=torch.int32, device="cuda")
+        C.lstm_seq_fwd(W16, xg, c0, h16, out, None, cs, acts, sync)
+        return out, cs
+
+    ref, ref_cs = run()
+    torch.cuda.synchronize()
+    native.check_persistent()
+    done = torch.zeros(n_hog, dtype=torch.int32, device="cuda")
+    side = torch.cuda.Stream()
+    C.set_seq_timeout_us(timeout_us)
+    try:
+        with torch.cuda.stream(side):
+            C.hog_cus(n_hog, hog_us, done)
+        time.sleep(0.05)                 # the hog is resident before the persistent launch is queued
+        out, cs = run()
+        torch.cuda.synchronize()
+    finally:
+        C.set_seq_timeout_us(0)
+    assert int((done > 0).sum()) == n_hog
+    return ref, ref_cs, out, cs
+
+
+def test_persistent_lstm_waits_out_other_streams():
+    """Workgroups held back by another stream's kernel (64 CUs hogged for 0.3 s) only delay the persistent launch:
+    with the default bound the output equals an unhindered launch bit for bit and no timeout is recorded."""
+    from bigdl_amd.ops import native
+
+    ref, ref_cs, out, cs = _hogged_lstm_forward(timeout_us=0)
+    native.check_persistent()
+    assert torch.equal(out, ref) and torch.equal(cs, ref_cs)
+
+
+def test_persistent_lstm_forced_timeout_raises():
+    """With the wait bound forced below the hog's duration the launch cannot complete: the host check raises
+    PersistentKernelTimeout (never a silent NaN), and the outputs are NaN-poisoned rather than partly unwritten."""
+    from bigdl_amd.ops import native
+
+    ref, ref_cs, out, cs = _hogged_lstm_forward(timeout_us=20e3)
+    with pytest.raises(native.PersistentKernelTimeout):
+        native.check_persistent()
+    native.check_persistent()           # cleared by the raising check
+    assert torch.isnan(cs).any()
+    # every element is either the correct value or poisoned: nothing is left as uninitialised memory
+    ok = torch.isnan(cs) | (cs == ref_cs)
+    assert bool(ok.all())
+
+
 @pytest.mark.parametrize("B,T,H", [(128, 12, 1024), (40, 5, 256)])
 def test_persistent_lstm_bf16_io_matches_f32_io(B, T, H):
     """bf16 gate inputs / outputs / gradients (the projection GEMMs' dtype, no f32 round trip) vs the f32-I/O launch of
@@ -209,3 +274,21 @@ def test_persistent_lstm_bf16_io_matches_f32_io(B, T, H):
     for a, b in zip(res[torch.bfloat16], res[torch.float32]):
         assert torch.isfinite(a).all()
         assert _rel(a, b) < 1.5e-2, _rel(a, b)
+
+
+def test_recurrent_output_dtype_stable_across_batch_sizes():
+    """Recurrent(LSTM) returns fp32 on the GPU whatever the batch size (persistent whole-sequence kernels at B <= 128,
+    per-step kernels above): bf16 sequence I/O is an explicit opt-in (Recurrent(bf16IO=True))."""
+    from bigdl_amd import nn
+
+    for B in (16, 200):
+        torch.manual_seed(0)
+        m = nn.Recurrent().add(nn.LSTM(64, 256, 0)).cuda()
+        x = torch.randn(B, 5, 64, device="cuda")
+        y = m.forward(x)
+        assert y.dtype == torch.float32, (B, y.dtype)
+        g = m.backward(x, torch.randn_like(y))
+        assert g.dtype == x.dtype
+    m = nn.Recurrent(bf16IO=True).add(nn.LSTM(64, 256, 0)).cuda()
+    y = m.forward(torch.randn(16, 5, 64, device="cuda"))
+    assert y.dtype in (torch.bfloat16, torch.float32)

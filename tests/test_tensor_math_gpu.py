@@ -240,3 +240,47 @@ def test_index_sort_mask_ops_native(monkeypatch):
         _close(res["gpu"][k], res["cpu"][k], tol=1e-5)
         if k.endswith("_i"):
             assert res["gpu"][k]._t.dtype == res["cpu"][k]._t.dtype == torch.float32, k   # T-typed indices
+
+
+def test_index_out_of_range_raises():
+    """Out-of-range 1-based indices raise IndexError on the native path (the reference's 'index out of bound'
+    require), for index / gather / indexAdd / scatter; a later valid op is unaffected (the error word is cleared)."""
+    x = Tensor(torch.randn(4, 10).cuda())
+    bad = Tensor(torch.tensor([1.0, 11.0]).cuda())
+    with pytest.raises(IndexError):
+        Tensor().index(2, bad, x)
+    with pytest.raises(IndexError):
+        Tensor().gather(2, Tensor(torch.full((4, 2), 0.0).cuda()), x)
+    with pytest.raises(IndexError):
+        Tensor(torch.zeros(4, 10).cuda()).indexAdd(2, bad, Tensor(torch.ones(4, 2).cuda()))
+    ok = Tensor().index(2, Tensor(torch.tensor([1.0, 10.0]).cuda()), x)
+    assert torch.equal(ok._t.cpu(), x._t.cpu()[:, [0, 9]])
+
+
+def test_masked_copy_short_source_raises():
+    x = Tensor(torch.zeros(10).cuda())
+    mask = Tensor(torch.ones(10).cuda())
+    with pytest.raises(RuntimeError):
+        x.maskedCopy(mask, Tensor(torch.arange(5.0).cuda()))
+
+
+@pytest.mark.parametrize("R", [37, 9000])
+@pytest.mark.parametrize("inc", [True, False])
+def test_topk_nan_order_matches_torch(R, inc):
+    """NaN orders as torch.topk does in both directions (last for smallest-k, first for largest-k), on the native
+    in-LDS sort (R <= 8192) and on the torch fallback (longer rows): same values and indices, NaN positions included."""
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(3, R, generator=g)
+    x[0, 5] = float("nan")
+    x[1, R - 1] = float("nan")
+    x[1, 2] = float("inf")
+    x[2, 0] = float("-inf")
+    k = 8
+    v, i = Tensor(x.clone().cuda()).topk(k, 2, inc)
+    rv, ri = torch.topk(x, k, dim=1, largest=not inc, sorted=True)
+    vv = v._t.cpu()
+    assert torch.equal(torch.isnan(vv), torch.isnan(rv))
+    fin = ~torch.isnan(rv)
+    assert torch.equal(vv[fin], rv[fin])
+    # NaN positions carry the NaN's own index; finite picks match torch's (no ties in random data)
+    assert torch.equal((i._t.cpu() - 1).long()[fin], ri[fin])
