@@ -93,6 +93,12 @@ def conv2d_fwd(x, w16, bias, stride, pad, dil=(1, 1), relu=False, stats=None, ou
             "conv2d_fwd: a residual addend needs a dense NHWC output"
     geo = _fwd_geo(N, H, W, C, OH, OW, sh, sw, R * S * C, K)
     geo[10] = ldo
+    if stats is not None and native.deterministic():
+        # deterministic mode: statistics in a separate one-writer-per-slot reduction, not the GEMM epilogue
+        native.get().conv_nt(x, w16, out, bias, None, geo, _fwd_taps(R, S, ph, pw, dh, dw), relu, addend)
+        dense = out if ldo == K else out.contiguous(memory_format=CL)
+        native.get().bn_stats(dense, stats, N * OH * OW, K)
+        return out
     native.get().conv_nt(x, w16, out, bias, stats, geo, _fwd_taps(R, S, ph, pw, dh, dw), relu, addend)
     return out
 
@@ -187,7 +193,7 @@ def conv2d_dgrad(dy, w16t, x_shape, stride, pad, dil=(1, 1), out=None, addend=No
     ldw = R * S * K
     bnk = {}
     if bn is not None and (covered == H * W or addend is None) and bn["x"].shape == out.shape \
-            and bn["x"].stride() == out.stride():
+            and bn["x"].stride() == out.stride() and not native.deterministic():
         bnk = dict(bn_x=bn["x"], bn_z=bn["z"], bn_mean=bn["mean"], bn_aff=bn["aff"], bn_red=bn["red"])
         bn["done"] = True
     for (a, b, nI, nJ, taps) in phases:

@@ -23,7 +23,44 @@ def get():
             f"{e}. Build it with `python setup.py build_ext --inplace` (hipcc --offload-arch=gfx950)."
         ) from e
     _C = mod
+    _check_build()
+    if hasattr(_C, "set_deterministic"):
+        _C.set_deterministic(1 if _DET[0] else 0)
     return _C
+
+
+BUILD_INFO = None
+
+
+def _check_build():
+    """Compare the content hash recorded at build time (bigdl_amd/_build_info.json, setup.py) with the sources in
+    this tree: a stale extension warns, or raises with BIGDL_STRICT_BUILD=1. Trees without csrc/ (installed copies)
+    skip the comparison."""
+    global BUILD_INFO
+    import json
+    import warnings
+
+    pkg = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    path = os.path.join(pkg, "_build_info.json")
+    try:
+        with open(path) as f:
+            BUILD_INFO = json.load(f)
+    except OSError:
+        BUILD_INFO = None
+        return
+    root = os.path.dirname(pkg)
+    if not os.path.isdir(os.path.join(root, "csrc")):
+        return
+    from .. import _buildhash
+
+    now = _buildhash.source_digest(root, BUILD_INFO.get("hip_flags", []))
+    BUILD_INFO["source_matches"] = now == BUILD_INFO.get("source_sha256")
+    if not BUILD_INFO["source_matches"]:
+        msg = ("bigdl_amd/_C was built from different sources than csrc/ in this tree (stale build): "
+               "run `python setup.py build_ext --inplace`")
+        if os.environ.get("BIGDL_STRICT_BUILD", "0") == "1":
+            raise RuntimeError(msg)
+        warnings.warn(msg, RuntimeWarning, stacklevel=3)
 
 
 def available():
@@ -37,6 +74,24 @@ def available():
 def so_path():
     mod = get()
     return os.path.abspath(mod.__file__)
+
+
+_DET = [os.environ.get("BIGDL_DETERMINISTIC", "0") not in ("0", "", "false", "False")]
+
+
+def deterministic():
+    """Deterministic mode (``bigdl.deterministic`` / BIGDL_DETERMINISTIC=1): every GPU reduction that would land
+    through float atomics from several workgroups runs in a fixed order instead (BN statistics and backward sums in
+    one-writer slots outside the GEMM epilogues, weight gradients through workspace partials + a fixed-order reduce,
+    bias gradients, loss and norms in one row block), so two training runs from the same seed are bitwise equal.
+    Costs speed (tools/det_check.py records how much)."""
+    return _DET[0]
+
+
+def set_deterministic(on=True):
+    _DET[0] = bool(on)
+    if _C is not None:
+        _C.set_deterministic(1 if on else 0)
 
 
 class PersistentKernelTimeout(RuntimeError):

@@ -32,6 +32,12 @@ _PENDING = []
 _RR = [0]
 
 
+def _one_queue():
+    import bigdl_amd
+
+    return bigdl_amd.graph_one_queue()
+
+
 def enabled():
     return _ON[0]
 
@@ -45,6 +51,8 @@ def stream_for(t):
     """The side stream for CUDA tensor ``t``'s device, or None when disabled / not on the GPU."""
     if not _ON[0] or not isinstance(t, torch.Tensor) or not t.is_cuda:
         return None
+    if not _one_queue() and torch.cuda.is_current_stream_capturing():
+        return None          # forked captures only where graph replays are known to keep the captured order
     dev = t.device.index if t.device.index is not None else torch.cuda.current_device()
     ss = _STREAMS.get(dev)
     if ss is None:

@@ -155,6 +155,10 @@ class _Engine:
 
     def setProperty(self, k, v):
         self.properties[k] = v
+        if k == "bigdl.deterministic":
+            from ..ops import native
+
+            native.set_deterministic(str(v).lower() in ("1", "true", "yes"))
 
     def getProperty(self, k, default=None):
         return self.properties.get(k, os.environ.get(k, default))

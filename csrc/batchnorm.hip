@@ -344,6 +344,8 @@ void launch_reduce(int mode, const bf16_t* x, const bf16_t* dz, const bf16_t* z,
   const int rpi = 256 / (G < 256 ? G : 256);
   long blocks = (P + rpi * 16 - 1) / (rpi * 16);   // >= 16 rows per thread
   if (blocks > 2048) blocks = 2048;
+  // deterministic mode: one block per statistics slot, so every slot word receives a single atomic onto zero
+  if (bigdl_deterministic() && blocks > STAT_SLOTS) blocks = STAT_SLOTS;
   if (blocks < 1) blocks = 1;
   const long rpb = (P + blocks - 1) / blocks;
   blocks = (P + rpb - 1) / rpb;

@@ -1210,6 +1210,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("dx") = py::none(), py::arg("dn16") = py::none(), py::arg("drz16") = py::none(),
         py::arg("dh0") = py::none());
   m.def("set_conv_impl", &bigdl_set_conv_impl);
+  m.def("set_conv_s1", &bigdl_set_conv_s1);
+  m.def("set_deterministic", &bigdl_set_deterministic, "1: bitwise-reproducible reductions (no multi-writer float atomics)");
+  m.def("deterministic", &bigdl_deterministic);
   m.def("get_conv_impl", &bigdl_get_conv_impl);
   m.def("set_conv_g4", &bigdl_set_conv_g4);
   m.def("set_conv_shortk", &bigdl_set_conv_shortk);

@@ -2316,6 +2316,216 @@ __global__ __launch_bounds__(512, 2) void conv_nt_p8_kernel(ConvArgs a) {
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Streaming 1x1 kernel for the HBM-bound one-tap GEMMs: identity pixel mapping (1x1, stride 1, no padding: A row m =
+// source pixel m, dense rows of Kdim = Cs channels), Kdim in {64, 128}, Ncol % 64 == 0, identity output rows.
+// ResNet-50's 64 -> 256 expansions, 128 -> 512, 64 -> 64 and the data gradients of the 256 -> 64 / 512 -> 128
+// reductions are such GEMMs: 1-4 K-steps of MFMA per tile and a 2-8x wider output than input, so the per-tile kernel
+// (conv_nt_g4: load, 2 K-steps, LDS epilogue, per-tile statistics atomics) ran them at 2-3 TB/s, latency- and
+// issue-bound (layer 3 fwd: 43 % of wave time waiting, 1,300 VALU per wave). Here (measured on the standalone
+// structure first, tools/ubench/nt_stream.hip: layer 3 fwd 202 -> 108 us = the 4.8 TB/s copy ceiling of its bytes):
+//  * persistent: 2 workgroups per CU, each strides over pixel tiles of one fixed channel block, so every
+//    per-channel quantity (the weight fragments, bias, BN mean / scale / shift, the statistics sums) is loaded or
+//    reduced ONCE per workgroup instead of once per tile;
+//  * wave w owns 64 output channels (cg = w % CG) of a BMW-pixel sub-tile (pg = w / CG); its weights live in VGPRs
+//    as MFMA A fragments for the whole launch (K = 64: 32 VGPRs, K = 128: 64);
+//  * A fragments are loaded straight from HBM into VGPRs (16 B per lane, no LDS staging: the tile is read once and
+//    used by one wave), two tiles ahead of the one being computed (register triple buffer, static indices);
+//  * epilogue: the wave parks its tile in its own LDS slice ([pixel][64 channels], 16-byte granules XOR-swizzled by
+//    pixel; bf16 when nothing is added before rounding, else fp32), re-reads it row-wise (8 channels of one pixel per
+//    lane) and writes whole 128-byte lines with 16-byte stores; addend / BN x / z rows for the consumer-BN backward
+//    reduction are loaded before the tile's MFMAs (EXT);
+//  * statistics (sum, sum of squares of the rounded output) or the consumer-BN backward sums accumulate in packed
+//    2 x f32 registers across all tiles of the workgroup; one shuffle reduction and one slotted atomic per channel at
+//    the end (same-address atomics serialise at the memory side: slots = block id % BIGDL_STAT_SLOTS).
+// Semantics are nt_epilogue_lds's (bias + addend added in fp32 before rounding, ReLU, BN statistics of the rounded
+// output, consumer-BN reduction of the rounded gradient with the z / affine ReLU mask).
+template <int K, int CG, int BMW, bool F32T, bool EXT>
+__global__ __launch_bounds__(256, 2) void conv_nt_s1_kernel(ConvArgs a) {
+  constexpr int KF = K / 32, MI = BMW / 16, PGN = 4 / CG, BM = BMW * PGN;
+  constexpr int GPR = F32T ? 16 : 8;               // 16-byte granules per 64-channel row of the LDS slice
+  constexpr int NR = BMW / 8;                      // row-phase passes (8 pixels x 8 lanes each)
+  __shared__ __attribute__((aligned(16))) unsigned lds[4 * BMW * GPR * 4];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int cg = wave % CG, pg = wave / CG;
+  const int nchb = a.Ncol / (64 * CG);
+  const int chb = blockIdx.x % nchb, wgi = blockIdx.x / nchb, ngr = gridDim.x / nchb;
+  const int c0 = (chb * CG + cg) * 64;
+  const int ntiles = (a.M + BM - 1) / BM;
+  unsigned* wl = lds + wave * BMW * GPR * 4;
+  const int q = lane & 7;                          // row phase: channels c0 + 8 q .. + 7
+  const int n = c0 + 8 * q;
+
+  v8s wf[4][KF];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int kk = 0; kk < KF; ++kk)
+      wf[j][kk] = *reinterpret_cast<const v8s*>(a.wt + (size_t)(c0 + 16 * j + (lane & 15)) * a.ldw + 32 * kk +
+                                                8 * (lane >> 4));
+  float bs[8], bmu[8], bsc[8], bsh[8];
+  const bool bnw = EXT && a.bnred && !a.stats;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    bs[e] = (F32T && a.bias) ? a.bias[n + e] : 0.f;
+    bmu[e] = bnw ? a.bnmean[n + e] : 0.f;
+    bsc[e] = (bnw && a.bnaff) ? a.bnaff[n + e] : 0.f;
+    bsh[e] = (bnw && a.bnaff) ? a.bnaff[a.Ncol + n + e] : 0.f;
+  }
+  typedef float v2f __attribute__((ext_vector_type(2)));
+  v2f p1[4], p2[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) p1[e] = p2[e] = v2f{0.f, 0.f};
+
+  auto load = [&](v8s (&af)[MI][KF], int t) {
+    const int p0 = t * BM + pg * BMW;
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int m = min(p0 + 16 * i + (lane & 15), a.M - 1);   // tail rows: any valid row (never stored)
+#pragma unroll
+      for (int kk = 0; kk < KF; ++kk)
+        af[i][kk] = *reinterpret_cast<const v8s*>(a.src + (size_t)m * K + 32 * kk + 8 * (lane >> 4));
+    }
+  };
+
+  auto compute_store = [&](v8s (&af)[MI][KF], int t) {
+    const int p0 = t * BM + pg * BMW;
+    v4u pad[EXT ? NR : 1], px[EXT ? NR : 1], pz[EXT ? NR : 1];
+    if constexpr (EXT) {     // epilogue operands first: their latency overlaps the MFMAs and the LDS transpose
+#pragma unroll
+      for (int rr = 0; rr < NR; ++rr) {
+        const int m = min(p0 + rr * 8 + (lane >> 3), a.M - 1);
+        const size_t off = (size_t)m * a.ldo + n;
+        pad[rr] = a.addend ? *reinterpret_cast<const v4u*>(a.addend + off) : v4u{0u, 0u, 0u, 0u};
+        px[rr] = bnw ? *reinterpret_cast<const v4u*>(a.bnx + off) : v4u{0u, 0u, 0u, 0u};
+        pz[rr] = (bnw && a.bnz) ? *reinterpret_cast<const v4u*>(a.bnz + off)
+                                : v4u{0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
+      }
+    }
+    v4f acc[MI][4];
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < KF; ++kk)
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j][kk], af[i][kk], acc[i][j], 0, 0, 0);
+    // D[n][m]: lane holds channels 16 j + 4 (lane >> 4) + e of pixel 16 i + (lane & 15)
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int p = 16 * i + (lane & 15), qq = lane >> 4;
+        if constexpr (F32T) {
+          const int g = 4 * j + qq;
+          *reinterpret_cast<v4f*>(wl + (p * GPR + (g ^ (p & 15))) * 4) = acc[i][j];
+        } else {
+          const int g = 2 * j + (qq >> 1);
+          *reinterpret_cast<v2u*>(wl + (p * GPR + (g ^ (p & 7))) * 4 + (qq & 1) * 2) =
+              v2u{pack2bf(acc[i][j][0], acc[i][j][1]), pack2bf(acc[i][j][2], acc[i][j][3])};
+        }
+      }
+    __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): wave-private slice
+#pragma unroll
+    for (int rr = 0; rr < NR; ++rr) {
+      const int p = rr * 8 + (lane >> 3);
+      const int m = p0 + p;
+      v4u o;
+      if constexpr (F32T) {
+        const v4f lo = *reinterpret_cast<const v4f*>(wl + (p * GPR + ((2 * q) ^ (p & 15))) * 4);
+        const v4f hi = *reinterpret_cast<const v4f*>(wl + (p * GPR + ((2 * q + 1) ^ (p & 15))) * 4);
+        float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        if constexpr (EXT) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) { v[2 * e] += lo_bf(pad[rr][e]); v[2 * e + 1] += hi_bf(pad[rr][e]); }
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float x0 = v[2 * e] + bs[2 * e], x1 = v[2 * e + 1] + bs[2 * e + 1];
+          if (a.relu) { x0 = fmaxf(x0, 0.f); x1 = fmaxf(x1, 0.f); }
+          o[e] = pack2bf(x0, x1);
+        }
+      } else {
+        o = *reinterpret_cast<const v4u*>(wl + (p * GPR + (q ^ (p & 7))) * 4);
+        if (a.relu) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] = pack2bf(fmaxf(lo_bf(o[e]), 0.f), fmaxf(hi_bf(o[e]), 0.f));
+        }
+      }
+      if (m < a.M) {
+        if (a.stats) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const v2f y = {lo_bf(o[e]), hi_bf(o[e])};
+            p1[e] += y;
+            p2[e] = __builtin_elementwise_fma(y, y, p2[e]);
+          }
+        } else if constexpr (EXT) {
+          if (bnw) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              v2f d = {lo_bf(o[e]), hi_bf(o[e])};
+              const v2f x = {lo_bf(px[rr][e]), hi_bf(px[rr][e])};
+              if (a.bnz) {
+                if (!(lo_bf(pz[rr][e]) > 0.f)) d[0] = 0.f;
+                if (!(hi_bf(pz[rr][e]) > 0.f)) d[1] = 0.f;
+              } else if (a.bnaff) {
+                if (!(x[0] * bsc[2 * e] + bsh[2 * e] > 0.f)) d[0] = 0.f;
+                if (!(x[1] * bsc[2 * e + 1] + bsh[2 * e + 1] > 0.f)) d[1] = 0.f;
+              }
+              p1[e] += d;
+              p2[e] = __builtin_elementwise_fma(d, x - v2f{bmu[2 * e], bmu[2 * e + 1]}, p2[e]);
+            }
+          }
+        }
+        *reinterpret_cast<v4u*>(a.out + (size_t)m * a.ldo + n) = o;
+      }
+    }
+  };
+
+  v8s a0[MI][KF], a1[MI][KF], a2[MI][KF];
+  int t = wgi;
+  if (t < ntiles) load(a0, t);
+  if (t + ngr < ntiles) load(a1, t + ngr);
+  for (; t < ntiles; t += 3 * ngr) {
+    if (t + 2 * ngr < ntiles) load(a2, t + 2 * ngr);
+    compute_store(a0, t);
+    if (t + ngr >= ntiles) break;
+    if (t + 3 * ngr < ntiles) load(a0, t + 3 * ngr);
+    compute_store(a1, t + ngr);
+    if (t + 2 * ngr >= ntiles) break;
+    if (t + 4 * ngr < ntiles) load(a1, t + 4 * ngr);
+    compute_store(a2, t + 2 * ngr);
+  }
+  float* const red = a.stats ? a.stats : (bnw ? a.bnred : nullptr);
+  if (red) {
+    float s1[8], s2[8];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { s1[2 * e] = p1[e][0]; s1[2 * e + 1] = p1[e][1]; s2[2 * e] = p2[e][0]; s2[2 * e + 1] = p2[e][1]; }
+    // lanes l, l + 8, ... hold the same 8 channels: reduce over lane >> 3
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+#pragma unroll
+      for (int o = 8; o < 64; o <<= 1) {
+        s1[e] += __shfl_xor(s1[e], o, 64);
+        s2[e] += __shfl_xor(s2[e], o, 64);
+      }
+    if (lane < 8) {
+      float* sp = red + (size_t)(blockIdx.x & (BIGDL_STAT_SLOTS - 1)) * 2 * a.Ncol;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        atomicAdd(sp + n + e, s1[e]);
+        atomicAdd(sp + a.Ncol + n + e, s2[e]);
+      }
+    }
+  }
+}
+
 // Grid of the split-K epilogue: (row blocks, 256-group channel chunks), ~8 rows per thread, <= 8192 blocks.
 dim3 splitk_grid(long P, int C, long* rpb_out) {
   const int G = C >> 3;
@@ -2559,6 +2769,59 @@ static bool conv_shortk() {
   return g_conv_shortk != 0;
 }
 
+// BIGDL_CONV_S1 (default 1): the streaming 1x1 kernel (conv_nt_s1_kernel) wherever it applies; 0 = off (A/B)
+int g_conv_s1 = -1;
+static bool s1_applies(const ConvArgs* a) {
+  if (g_conv_s1 < 0) {
+    const char* e = getenv("BIGDL_CONV_S1");
+    g_conv_s1 = e ? atoi(e) : 1;
+  }
+  if (!g_conv_s1 || a->out32 || !a->ident_out || a->ntaps != 1 || a->tap_h[0] || a->tap_w[0] || a->tap_k[0]) return false;
+  if (a->mul_h != 1 || a->mul_w != 1 || a->Hs != a->OH || a->Ws != a->OW) return false;
+  if ((a->Kdim != 64 && a->Kdim != 128) || a->Cs != a->Kdim || (a->Ncol % 64) || (a->ldo % 8) || (a->ldw % 8)) return false;
+  auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  return al(a->src) && al(a->wt) && al(a->out) && al(a->addend) && al(a->bnx) && al(a->bnz);
+}
+
+template <int K, int CG, int BMW, bool F32T, bool EXT>
+void launch_s1(const ConvArgs& a, hipStream_t st) {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (cus <= 0) cus = 256;
+  }
+  const int nchb = a.Ncol / (64 * CG);
+  const int tiles = (a.M + BMW * (4 / CG) - 1) / (BMW * (4 / CG));
+  int per = std::max(1, (2 * cus) / nchb);
+  per = std::min(per, tiles);
+  conv_nt_s1_kernel<K, CG, BMW, F32T, EXT><<<dim3(per * nchb), dim3(256), 0, st>>>(a);
+}
+
+template <int K, int CG>
+void launch_s1_cg(const ConvArgs& a, hipStream_t st) {
+  const bool ext = a.addend != nullptr || (a.bnred != nullptr && a.stats == nullptr);
+  const bool f32t = ext || a.bias != nullptr;
+  constexpr int BW = K == 64 ? 64 : 32;            // pixels per wave tile (ubench: 64 / 32 best at K 64 / 128)
+  if (ext) launch_s1<K, CG, BW / 2, true, true>(a, st);
+  else if (f32t) launch_s1<K, CG, BW / 2, true, false>(a, st);
+  else launch_s1<K, CG, BW, false, false>(a, st);
+}
+
+static void launch_s1_any(const ConvArgs& a, hipStream_t st) {
+  const int cg = (a.Ncol % 256 == 0) ? 4 : (a.Ncol % 128 == 0) ? 2 : 1;
+  if (a.Kdim == 64) {
+    if (cg == 4) launch_s1_cg<64, 4>(a, st);
+    else if (cg == 2) launch_s1_cg<64, 2>(a, st);
+    else launch_s1_cg<64, 1>(a, st);
+  } else {
+    if (cg == 4) launch_s1_cg<128, 4>(a, st);
+    else if (cg == 2) launch_s1_cg<128, 2>(a, st);
+    else launch_s1_cg<128, 1>(a, st);
+  }
+}
+
 int g_conv_impl = -1;
 int conv_impl() {
   if (g_conv_impl < 0) {
@@ -2573,6 +2836,7 @@ int conv_impl() {
 extern "C" {
 
 void bigdl_set_conv_impl(int impl) { g_conv_impl = impl; }
+void bigdl_set_conv_s1(int v) { g_conv_s1 = v; }
 void bigdl_set_conv_g4(int v) { g_conv_g4 = v; }
 void bigdl_set_conv_shortk(int v) { g_conv_shortk = v; }
 int g_wgrad_p8 = -1;
@@ -2585,6 +2849,7 @@ int bigdl_get_conv_impl() { return conv_impl(); }
 long bigdl_conv_nt_plan(ConvArgs* a) {
   a->ksplit = 0;
   if (a->Cs % 8 != 0 || a->M <= 0 || conv_impl() < 1) return 0;
+  if (conv_impl() == 1 && s1_applies(a)) return 0;
   const int p8 = conv_impl() == 1 ? p8_pick(a) : 0;
   if (p8 > 1) {
     a->ksplit = p8;
@@ -2608,6 +2873,11 @@ int bigdl_conv_nt(const ConvArgs* a, hipStream_t st) {
   if (a->M <= 0) return 0;
   const bool fastk = (a->Cs % BK) == 0;
   const int impl = conv_impl();
+  if (impl == 1 && s1_applies(a)) {
+    launch_s1_any(*a, st);
+    HIP_LAUNCH_CHECK();
+    return 0;
+  }
   const long p3_tiles = (long)((a->M + 255) / 256) * ((a->Ncol + 127) / 128);
   const long tiles128 = (long)((a->M + 127) / 128) * ((a->Ncol + (a->Ncol <= 64 ? 63 : 127)) / (a->Ncol <= 64 ? 64 : 128));
   const bool aligned_out = (a->Ncol & 7) == 0 && (a->ldo & 7) == 0;   // the persistent kernel has no fallback epilogue
@@ -2690,8 +2960,9 @@ int bigdl_conv_nt(const ConvArgs* a, hipStream_t st) {
 // 64-wide output-channel layers with a deep reduction (stem 7x7, 3x3 over 64 channels) run half-empty 128x128
 // tiles; the register-staged atomic kernel is faster there (measured per layer, profiles/r1_ab_wgrad.txt)
 static bool wgrad_prefers_atomic(const WgradArgs* a) {
-  // BIGDL_WGRAD_ATOMIC: 1 (default) this rule, 0 never, 2 always (per-layer A/B runs)
+  // BIGDL_WGRAD_ATOMIC: 1 (default) this rule, 0 never, 2 always (per-layer A/B runs); never in deterministic mode
   static const int on = [] { const char* e = getenv("BIGDL_WGRAD_ATOMIC"); return e ? atoi(e) : 1; }();
+  if (bigdl_deterministic()) return false;
   return on == 2 || (on == 1 && a->Ncol <= 64 && a->Kdim > 256);
 }
 
@@ -2775,7 +3046,23 @@ long bigdl_conv_wgrad_plan(WgradArgs* a) {
   return splits > 1 ? (long)splits * a->Ncol * a->Kdim : 0;
 }
 
+static int conv_wgrad_impl(const WgradArgs* a_in, hipStream_t st);
+
+// Deterministic mode: the split kernels add their bias partials with one atomic per split, so the bias gradient is
+// taken out of them and summed by a one-row-block column sum (one atomic per channel); the weight gradient always
+// goes through the workspace partials + fixed-order reduce (no multi-split atomics, see bigdl_conv_wgrad_plan).
 int bigdl_conv_wgrad(const WgradArgs* a_in, hipStream_t st) {
+  if (bigdl_deterministic() && a_in->dbias != nullptr && (a_in->ldy % 8) == 0) {
+    WgradArgs b = *a_in;
+    b.dbias = nullptr;
+    const int rc = conv_wgrad_impl(&b, st);
+    if (rc == 0) bigdl_colsum_bf16_ld(a_in->dy, a_in->dbias, a_in->M, a_in->Ncol, a_in->ldy, st);
+    return rc;
+  }
+  return conv_wgrad_impl(a_in, st);
+}
+
+static int conv_wgrad_impl(const WgradArgs* a_in, hipStream_t st) {
   WgradArgs a = *a_in;
   if (a.Cs % 8 != 0 || a.Ncol % 8 != 0 || a.Kdim % 8 != 0) return -1;
   {
@@ -2807,7 +3094,8 @@ int bigdl_conv_wgrad(const WgradArgs* a_in, hipStream_t st) {
     const long n4 = (long)a.Ncol * a.Kdim / 4;
     const int blocks = (int)std::min<long>((n4 + 255) / 256, 8192);
     // ~2048 reduce workgroups in total, >= 4 splits per group, <= 64-way atomic contention
-    const int groups = blocks >= 256 ? 1 : std::max(1, std::min({2048 / blocks, a.splits / 4, 64}));
+    const int groups = (blocks >= 256 || bigdl_deterministic()) ? 1
+                                                               : std::max(1, std::min({2048 / blocks, a.splits / 4, 64}));
     const dim3 rgrid(blocks, groups);
     if ((reinterpret_cast<uintptr_t>(a.dw) & 15) == 0) wgrad_reduce_kernel<true><<<rgrid, 256, 0, st>>>(a.ws, a.dw, n4, a.splits);
     else wgrad_reduce_kernel<false><<<rgrid, 256, 0, st>>>(a.ws, a.dw, n4, a.splits);
@@ -2825,7 +3113,7 @@ int bigdl_conv_wgrad(const WgradArgs* a_in, hipStream_t st) {
   if (splits > cap_atomic) splits = cap_atomic;
   const int maxsplit = (a.M + 4 * WBM - 1) / (4 * WBM);   // >= 4 LDS stages per split
   if (splits > maxsplit) splits = maxsplit;
-  if (splits < 1) splits = 1;
+  if (splits < 1 || bigdl_deterministic()) splits = 1;   // det: no workspace given -> one split, one atomic each
   int mps = (a.M + splits - 1) / splits;
   mps = (mps + WBM - 1) / WBM * WBM;
   splits = (a.M + mps - 1) / mps;

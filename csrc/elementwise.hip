@@ -85,7 +85,7 @@ __global__ __launch_bounds__(256) void nchw_to_nhwc_kernel(const float* __restri
 // consecutive columns (one 16-byte load per row), the 4 waves of a block take interleaved rows of the block's row
 // chunk, partials meet in LDS and one atomic per column per block lands in out.
 __global__ void __launch_bounds__(256) colsum_bf16_kernel(const bf16_t* __restrict__ x, float* __restrict__ out,
-                                                         long P, int K, long rows_per_block) {
+                                                         long P, int K, long rows_per_block, long ld) {
   __shared__ float part[4][64][9];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int c0 = (blockIdx.x * 64 + lane) * 8;
@@ -94,7 +94,7 @@ __global__ void __launch_bounds__(256) colsum_bf16_kernel(const bf16_t* __restri
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if (c0 < K) {
     for (long r = r0 + wave; r < r1; r += 4) {
-      const v4u q = *reinterpret_cast<const v4u*>(x + r * K + c0);
+      const v4u q = *reinterpret_cast<const v4u*>(x + r * ld + c0);
 #pragma unroll
       for (int e = 0; e < 4; ++e) { acc[2 * e] += lo_bf(q[e]); acc[2 * e + 1] += hi_bf(q[e]); }
     }
@@ -649,13 +649,30 @@ void bigdl_nchw_f32_to_nhwc_bf16(const float* x, uint16_t* y, int N, int C, int 
   nchw_to_nhwc_kernel<<<grid, 256, 0, st>>>(x, y, N, C, H, W, Cp);
   HIP_LAUNCH_CHECK();
 }
+// Deterministic mode (bigdl_set_deterministic): every reduction that lands through float atomics from several
+// workgroups is launched so each output element receives exactly ONE atomic (one row block, unique statistics slots),
+// or is replaced by a fixed-order pass; training runs are then bitwise reproducible (tests/test_deterministic_gpu.py).
+int g_det = -1;
+int bigdl_deterministic() {
+  if (g_det < 0) {
+    const char* e = getenv("BIGDL_DETERMINISTIC");
+    g_det = (e && atoi(e) != 0) ? 1 : 0;
+  }
+  return g_det;
+}
+void bigdl_set_deterministic(int v) { g_det = v ? 1 : 0; }
+
 void bigdl_colsum_bf16(const uint16_t* x, float* out, long P, int K, hipStream_t st) {
+  bigdl_colsum_bf16_ld(x, out, P, K, K, st);
+}
+// out[k] += sum over P rows (row stride ld, ld % 8 == 0) of x[r][k]
+void bigdl_colsum_bf16_ld(const uint16_t* x, float* out, long P, int K, long ld, hipStream_t st) {
   const int bx = (K / 8 + 63) / 64;
   long by = (P + 255) / 256;                   // >= 64 rows per wave, ~2048 blocks at most
   if ((long)bx * by > 2048) by = (2048 + bx - 1) / bx;
-  if (by < 1) by = 1;
+  if (by < 1 || bigdl_deterministic()) by = 1;
   const long rpb = (P + by - 1) / by;
-  colsum_bf16_kernel<<<dim3(bx, (unsigned)by), 256, 0, st>>>(x, out, P, K, rpb);
+  colsum_bf16_kernel<<<dim3(bx, (unsigned)by), 256, 0, st>>>(x, out, P, K, rpb, ld);
   HIP_LAUNCH_CHECK();
 }
 
@@ -699,7 +716,7 @@ void bigdl_avgpool_bwd(const uint16_t* dy, uint16_t* dx, int N, int H, int W, in
 }
 void bigdl_softmax_xent(const uint16_t* lb, const float* lf, const float* labels, float* loss, uint16_t* db, float* df,
                         int B, int K, float label_base, float grad_scale, hipStream_t st) {
-  const int blocks = std::min((B + 3) / 4, 2048);
+  const int blocks = bigdl_deterministic() ? 1 : std::min((B + 3) / 4, 2048);   // det: one loss atomic
   const bool vec = lb ? (K % 8 == 0) : (K % 4 == 0);   // rows start 16-byte aligned when K is a multiple
   if (vec)
     softmax_xent_kernel<true><<<blocks, 256, 0, st>>>(lb, lf, labels, loss, db, df, B, K, label_base, grad_scale);
@@ -727,7 +744,7 @@ void bigdl_adam_step(float* w, const float* g, float* m, float* v, uint16_t* w16
   HIP_LAUNCH_CHECK();
 }
 void bigdl_sumsq(const float* x, float* out, long n, hipStream_t st) {
-  sumsq_kernel<<<grid_cap(n, 2048), 256, 0, st>>>(x, out, n);
+  sumsq_kernel<<<bigdl_deterministic() ? 1 : grid_cap(n, 2048), 256, 0, st>>>(x, out, n);
   HIP_LAUNCH_CHECK();
 }
 void bigdl_scale_f32(float* x, long n, const float* sdev, float s, hipStream_t st) {

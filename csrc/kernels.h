@@ -58,6 +58,9 @@ struct WgradArgs {
 
 extern "C" {
 void bigdl_fill_bytes(void* ptr, int value, long bytes, hipStream_t st);
+int bigdl_deterministic();
+void bigdl_set_deterministic(int v);
+void bigdl_colsum_bf16_ld(const uint16_t* x, float* out, long P, int K, long ld, hipStream_t st);
 int bigdl_conv_nt(const ConvArgs* a, hipStream_t st);
 // Kernel choice for bigdl_conv_nt: sets a->ksplit and returns the fp32 workspace elements it needs (0: none).
 long bigdl_conv_nt_plan(ConvArgs* a);
@@ -181,6 +184,7 @@ int bigdl_gemv_f32(const float* A, const float* x, const float* Min, float* y, i
                    long sx, long smi, long sy, float alpha, float beta, hipStream_t st);
 void bigdl_copy_rows_i8(const int8_t* src, int8_t* dst, long rows, int C, long lds, long ldd, hipStream_t st);
 void bigdl_set_conv_impl(int impl);
+void bigdl_set_conv_s1(int v);
 int bigdl_get_conv_impl();
 void bigdl_set_conv_g4(int v);
 void bigdl_set_conv_shortk(int v);

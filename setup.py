@@ -10,9 +10,12 @@
 ``__graft_entry__.build()`` runs this.
 """
 import glob
+import hashlib
+import json
 import os
 import subprocess
 import sys
+import time
 from concurrent.futures import ThreadPoolExecutor
 
 from setuptools import setup
@@ -27,14 +30,40 @@ HIP_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-fno-gpu-r
              "-I" + os.path.join(HERE, "csrc"), "-Wno-unused-result"]
 
 
+def _load_buildhash():
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("_bigdl_buildhash", os.path.join(HERE, "bigdl_amd", "_buildhash.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+_BH = _load_buildhash()
+_digest = _BH.digest
+
+
+def source_digest():
+    """Content hash of every native source and header plus the compile flags: what bigdl_amd/_build_info.json
+    records and bigdl_amd.ops.native compares at import (stale-build check)."""
+    return _BH.source_digest(HERE, HIP_FLAGS)
+
+
 def _compile_one(src):
+    # rebuilt unless the recorded content hash of (source, every header, flags) matches: an object is never reused
+    # on timestamps alone (a stale build/hipobj from another tree or checkout would otherwise be linked unnoticed)
     obj = os.path.join(OBJ_DIR, os.path.basename(src) + ".o")
-    deps = [src] + glob.glob(os.path.join(HERE, "csrc", "*.h"))
-    if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(d) for d in deps):
-        return obj
+    want = _digest([src] + glob.glob(os.path.join(HERE, "csrc", "*.h")), " ".join(HIP_FLAGS))
+    stamp = obj + ".sha256"
+    if os.path.exists(obj) and os.path.exists(stamp):
+        with open(stamp) as f:
+            if f.read().strip() == want:
+                return obj
     cmd = [HIPCC] + HIP_FLAGS + ["-c", src, "-o", obj]
     print(" ".join(cmd), flush=True)
     subprocess.check_call(cmd)
+    with open(stamp, "w") as f:
+        f.write(want)
     return obj
 
 
@@ -52,6 +81,11 @@ class HipBuildExt(BuildExtension):
         for ext in self.extensions:
             ext.extra_objects = list(ext.extra_objects or []) + objs
         super().build_extensions()
+        info = {"source_sha256": source_digest(), "arch": ARCH, "hip_flags": HIP_FLAGS,
+                "objects": {os.path.basename(o): open(o + ".sha256").read().strip() for o in objs},
+                "built_unix": int(time.time()), "mode": "setup.py build_ext"}
+        with open(os.path.join(HERE, "bigdl_amd", "_build_info.json"), "w") as f:
+            json.dump(info, f, indent=1)
 
 
 ext = CppExtension(

@@ -541,3 +541,39 @@ def test_straggler_cancellation_bounds_iteration_time():
     late = [w0[n] for n in range(10, 15) if n in w0]
     assert late and max(late) < 1.0, w0          # a full straggler iteration would be >= 2 s
     assert min(late) > 0.15, w0                  # the straggler did nap (the scenario ran)
+
+
+def _ref_distri(rank, world, iters, ranks):
+    """RefDistriOptimizer analogue (T/optim/RefDistriOptimizer.scala): one process computes every partition's
+    gradient from the same weights, sums them in partition order and averages, then applies the same update."""
+    from bigdl_amd import nn
+    from bigdl_amd.optim.train_step import TrainStep
+
+    model = _model(False)
+    step = TrainStep(model, nn.MSECriterion(), _methods("sgd", model), device="cpu", compress=None)
+    X, Y = _data()
+    n = X.shape[0] // ranks
+    for _ in range(iters):
+        gs = []
+        for r in range(ranks):
+            step.zero_grad()
+            loss = step.forward_backward(X[r * n:(r + 1) * n], Y[r * n:(r + 1) * n])
+            gs.append(step.g.clone())
+        tot = gs[0]
+        for gg in gs[1:]:
+            tot = tot + gg
+        step.g.copy_(tot.mul_(1.0 / ranks))
+        step.sync_and_update(loss)
+    step.gather_model()
+    return step.w[:step.total].clone()
+
+
+def test_two_rank_distri_matches_ref_distri_bitwise():
+    """DistriOptimizerSpec 'be same compare to ref optimizer' (:378-392): 2 gloo ranks (fp32 exchange) end with
+    exactly the weights of the single-process reference that computes both partitions' gradients itself."""
+    iters = 5
+    two = run_distributed(_train, 2, ("sgd", False, "none", None, iters, False))
+    ref = run_distributed(_ref_distri, 1, (iters, 2))[0]
+    w0, w1 = two[0][0], two[1][0]
+    assert torch.equal(w0, w1)
+    assert torch.equal(w0, ref), (w0 - ref).abs().max()

@@ -794,3 +794,86 @@ def test_conv_wgrad_p8_kernel(case, offset):
     got = (dw - base).view(K, R, R, C).permute(0, 3, 1, 2)
     assert _rel(got, dwr) < 1e-2
     assert torch.equal(flat[:offset], pre)
+
+
+S1_CASES = [
+    # N, C, H, K (1x1, stride 1): the streaming 1x1 kernel takes fwd when C in {64, 128} and dgrad when K in {64, 128}
+    (16, 64, 56, 256),     # fwd K 64 -> 256 (ResNet layer 3 shape at batch 16), 4 channel groups
+    (8, 256, 28, 64),      # dgrad 64 -> 256 with addend + consumer-BN reduction (fwd on the other kernels)
+    (6, 128, 28, 512),     # fwd K 128 -> 512, two channel blocks of 256
+    (5, 64, 13, 64),       # one channel group, M tail (845 rows)
+    (3, 128, 11, 192),     # Ncol 192: three one-group channel blocks, M tail
+    (4, 192, 9, 128),      # dgrad 128 -> 192
+    (7, 128, 10, 128),     # two channel groups both ways
+]
+
+
+@pytest.mark.parametrize("zmask", [False, True])
+@pytest.mark.parametrize("case", S1_CASES)
+def test_conv_s1_stream_kernel(case, zmask):
+    """Streaming 1x1 kernel (conv_nt_s1_kernel: persistent, weights in VGPRs, register-prefetched operand tiles,
+    statistics accumulated across tiles) vs fp32 torch: forward + BN statistics, forward + bias + ReLU, data gradient
+    + residual addend + consumer-BN backward reduction under the affine (or z) ReLU mask; and bit-equal outputs with
+    the kernel switched off where the per-tile kernels round the same fp32 sums (forward without bias)."""
+    from bigdl_amd.ops import bn as bnops
+    from bigdl_amd.ops import conv as cv
+    from bigdl_amd.ops import native
+
+    C_ = native.get()
+    N, C, H, K = case
+    torch.manual_seed(11)
+    dev = _dev()
+    x = torch.randn(N, C, H, H, device=dev).to(BF, memory_format=CL)
+    w = (torch.randn(K, C, 1, 1, device=dev) * (1.0 / C ** 0.5)).to(BF, memory_format=CL)
+    b32 = torch.randn(K, device=dev)
+    yr0 = F.conv2d(x.float(), w.float())
+    res = {}
+    for s1 in (1, 0):
+        C_.set_conv_s1(s1)
+        try:
+            stats = bnops.new_stats(K, dev)
+            y = cv.conv2d_fwd(x, w, None, (1, 1), (0, 0), stats=stats)
+            y2 = cv.conv2d_fwd(x, w, b32, (1, 1), (0, 0), relu=True)
+            gy = (torch.randn(N, K, H, H, device=dev, generator=torch.Generator(dev).manual_seed(3))).to(
+                BF, memory_format=CL)
+            add = torch.randn(N, C, H, H, device=dev, generator=torch.Generator(dev).manual_seed(4)).to(
+                BF, memory_format=CL)
+            bx = torch.randn(N, C, H, H, device=dev, generator=torch.Generator(dev).manual_seed(5)).to(
+                BF, memory_format=CL)
+            bz = torch.relu(torch.randn(N, C, H, H, device=dev, generator=torch.Generator(dev).manual_seed(6))).to(
+                BF, memory_format=CL)
+            mean = torch.linspace(-0.1, 0.1, C, device=dev)
+            aff = torch.cat([torch.linspace(0.5, 1.5, C, device=dev), torch.linspace(-0.2, 0.2, C, device=dev)])
+            red = bnops.new_stats(C, dev)
+            bn = {"x": bx, "z": bz if zmask else None, "mean": mean, "aff": aff, "red": red}
+            dx = cv.conv2d_dgrad(gy, cv.transpose_w(w), x.shape, (1, 1), (0, 0), addend=add, bn=bn)
+            torch.cuda.synchronize()
+            res[s1] = (y, stats, y2, dx, red, bool(bn.get("done")))
+        finally:
+            C_.set_conv_s1(1)
+    y, stats, y2, dx, red, done = res[1]
+    assert _rel(y, yr0) < 1e-2
+    st2 = stats.view(bnops.stat_slots(), 2, K).sum(0)
+    assert _rel(st2[0], y.float().sum(dim=(0, 2, 3))) < 1e-4
+    assert _rel(st2[1], (y.float() ** 2).sum(dim=(0, 2, 3))) < 1e-4
+    assert _rel(y2, torch.relu(yr0 + b32.view(1, K, 1, 1))) < 1e-2
+    assert torch.equal(y, res[0][0])                   # same fp32 sums, same rounding
+    gy = res[1][3]  # placeholder to keep names short below
+    gyr = (torch.randn(N, K, H, H, device=dev, generator=torch.Generator(dev).manual_seed(3))).to(BF).float()
+    addr = torch.randn(N, C, H, H, device=dev, generator=torch.Generator(dev).manual_seed(4)).to(BF).float()
+    dxr = torch.nn.grad.conv2d_input(x.shape, w.float(), gyr) + addr
+    assert _rel(dx, dxr) < 1e-2
+    assert _rel(dx, res[0][3]) < 1e-2
+    if done:
+        d = dx.float()
+        xf = torch.randn(N, C, H, H, device=dev, generator=torch.Generator(dev).manual_seed(5)).to(BF).float()
+        if zmask:
+            zf = torch.relu(torch.randn(N, C, H, H, device=dev, generator=torch.Generator(dev).manual_seed(6))).to(BF).float()
+            mask = zf > 0
+        else:
+            mask = (xf * torch.linspace(0.5, 1.5, C, device=dev).view(1, C, 1, 1)
+                    + torch.linspace(-0.2, 0.2, C, device=dev).view(1, C, 1, 1)) > 0
+        dm = d * mask
+        r2 = red.view(bnops.stat_slots(), 2, C).sum(0)
+        assert _rel(r2[0], dm.sum(dim=(0, 2, 3))) < 1e-3
+        assert _rel(r2[1], (dm * (xf - torch.linspace(-0.1, 0.1, C, device=dev).view(1, C, 1, 1))).sum(dim=(0, 2, 3))) < 1e-3

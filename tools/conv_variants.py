@@ -23,8 +23,8 @@ from bigdl_amd.ops import conv as cv  # noqa: E402
 from bigdl_amd.ops import native  # noqa: E402
 
 SETTERS = {"impl": "set_conv_impl", "g4": "set_conv_g4", "p8": "set_conv_p8", "nt2": "set_conv_nt2",
-           "shortk": "set_conv_shortk"}
-DEFAULTS = {"impl": 1, "g4": 3, "p8": 1, "nt2": 0, "shortk": 0}
+           "shortk": "set_conv_shortk", "s1": "set_conv_s1"}
+DEFAULTS = {"impl": 1, "g4": 3, "p8": 1, "nt2": 0, "shortk": 0, "s1": 1}
 
 
 def parse_variants(spec):
@@ -50,7 +50,7 @@ def apply(sw):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--layers", default="3,4,7,13")
-    ap.add_argument("--ops", default="fwd,fwd_nostats,dgrad")
+    ap.add_argument("--ops", default="fwd,fwd_nostats,dgrad,dgrad_bn")
     ap.add_argument("--variants", default="base:")
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--iters", type=int, default=10)
@@ -70,13 +70,20 @@ def main():
         gy = torch.randn(N, K, OH, OH, device=dev).to(BF, memory_format=CL)
         wt = cv.transpose_w(w)
         stats = bnops.new_stats(K, dev)
+        add = torch.randn(N, C, H, H, device=dev).to(BF, memory_format=CL)
+        bx = torch.randn(N, C, H, H, device=dev).to(BF, memory_format=CL)
+        bz = torch.relu(torch.randn(N, C, H, H, device=dev)).to(BF, memory_format=CL)
+        red = bnops.new_stats(C, dev)
+        bnarg = {"x": bx, "z": bz, "mean": torch.zeros(C, device=dev), "aff": None, "red": red}
         passes = {
             "fwd": lambda: cv.conv2d_fwd(x, w, None, (st, st), (pd, pd), stats=stats),
             "fwd_nostats": lambda: cv.conv2d_fwd(x, w, None, (st, st), (pd, pd)),
             "dgrad": lambda: cv.conv2d_dgrad(gy, wt, x.shape, (st, st), (pd, pd)),
+            # training form: residual-gradient addend + the consumer BN's fused backward reduction (z mask)
+            "dgrad_bn": lambda: cv.conv2d_dgrad(gy, wt, x.shape, (st, st), (pd, pd), addend=add, bn=dict(bnarg)),
         }
         for op in a.ops.split(","):
-            if op == "dgrad" and li == 0:
+            if op.startswith("dgrad") and li == 0:
                 continue
             fn = passes[op]
             times = {n: [] for n, _ in variants}
