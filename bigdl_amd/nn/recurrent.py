@@ -300,6 +300,7 @@ class _LSTMSeq(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, xg, h0, c0, U):
+        ctx.set_materialize_grads(False)   # unused outputs (final h / c) get None, not a zero-filled aten tensor
         B, T, G = xg.shape
         H = G // 4
         if xg.dtype != torch.float32 and not _LSTMSeq._fused_gpu(xg, U):
@@ -409,9 +410,11 @@ class _LSTMSeq(torch.autograd.Function):
 
 
 class _GRUSeq(torch.autograd.Function):
-    """Whole-sequence GRU (preTopology order r, z, n) on the fused HIP step kernels (csrc/gru.hip): two MFMA
-    launches per step forward (r/z, then n and h) and two per step backward, then the recurrent weight gradients
-    as two native GEMMs over all T*B rows."""
+    """Whole-sequence GRU (preTopology order r, z, n). Where the persistent kernels apply (B <= 128 per GPU,
+    H in {256, 512, 1024}: csrc/lstm_seq.hip gru_seq_*_kernel) the whole sequence is ONE launch per direction (the
+    reference's fused VanillaGru RNN primitive, S/nn/mkldnn/RNN.scala:213-219); otherwise the fused HIP step kernels
+    (csrc/gru.hip: two MFMA launches per step and direction). Then the recurrent weight gradients as two native
+    GEMMs over all T*B rows."""
 
     @staticmethod
     def usable(x, H):
@@ -419,11 +422,28 @@ class _GRUSeq(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, xg, h0, Urz, Un):
+        ctx.set_materialize_grads(False)
         B, T, G = xg.shape
         H = G // 3
         C = ops.native.get()
         bf = torch.bfloat16
         Wrz, Wn = Urz.detach().to(bf).contiguous(), Un.detach().to(bf).contiguous()
+        ctx.seq = bool(C.gru_seq_supported(B, H))
+        if ctx.seq:
+            # whole sequence in ONE persistent launch (csrc/lstm_seq.hip gru_seq_fwd_kernel): both recurrent weight
+            # blocks resident in VGPRs, two group hand-offs per step (r * h, then h)
+            ops.native.check_persistent()
+            out = xg.new_empty(B, T, H)
+            gates = xg.new_empty(3, T, B, H)
+            h16 = xg.new_empty(T + 1, B, H, dtype=bf)
+            rh16 = xg.new_empty(T, B, H, dtype=bf)
+            h0 = h0.contiguous()
+            C.cast_f32_bf16(h0, h16[0])
+            sync = torch.empty(C.lstm_seq_sync_words(), dtype=torch.int32, device=xg.device)
+            C.gru_seq_fwd(Wrz, Wn, xg, h0, h16, rh16, gates, out, sync)
+            ctx.save_for_backward(h0, Urz, Un, out, gates, h16, rh16)
+            ctx.w16 = (Wrz, Wn)
+            return out, out[:, -1].clone()
         out = xg.new_empty(B, T, H)
         gates = xg.new_empty(3, T, B, H)                 # r, z, n per step
         h16 = xg.new_empty(T + 1, B, H, dtype=bf)         # h_{t-1} operands, time-major
@@ -446,6 +466,23 @@ class _GRUSeq(torch.autograd.Function):
         B, T, H = out.shape
         C = ops.native.get()
         bf = torch.bfloat16
+        if ctx.seq:
+            ops.native.check_persistent()
+            Wrz, Wn = ctx.w16
+            dx = out.new_empty(B, T, 3 * H)
+            dn16 = out.new_empty(T, B, H, dtype=bf)
+            drz16 = out.new_empty(T, B, 2 * H, dtype=bf)
+            dh0 = out.new_empty(B, H)
+            sync = torch.empty(C.lstm_seq_sync_words(), dtype=torch.int32, device=out.device)
+            C.gru_seq_bwd(Wrz, Wn, h0, gates, out, dout.contiguous() if dout is not None else None,
+                          dhT.contiguous() if dhT is not None else None, dx, dn16, drz16, dh0, sync)
+            dUrz = out.new_empty(2 * H, H, 1, 1)
+            C.fill_bytes(dUrz, 0)
+            cv.conv2d_wgrad(drz16.view(T * B, 2 * H, 1, 1), h16[:T].view(T * B, H, 1, 1), dUrz, None, (1, 1), (0, 0))
+            dUn = out.new_empty(H, H, 1, 1)
+            C.fill_bytes(dUn, 0)
+            cv.conv2d_wgrad(dn16.view(T * B, H, 1, 1), rh16.view(T * B, H, 1, 1), dUn, None, (1, 1), (0, 0))
+            return dx, dh0, dUrz.view(2 * H, H), dUn.view(H, H)
         UrzT = Urz.detach().t().contiguous().to(bf)       # [H, 2H]: D = drz . U_rz
         UnT = Un.detach().t().contiguous().to(bf)         # [H, H]:  D = dn . U_n
         dout = dout.contiguous() if dout is not None else None

@@ -352,9 +352,28 @@ def _pair_taps(R, S2):
     return t
 
 
+def _window_taps(R):
+    key = ("w", R)
+    t = _TAP_CACHE.get(key)
+    if t is None:
+        t = [v for r in range(R) for v in (r, 0, r)]
+        _TAP_CACHE[key] = t
+    return t
+
+
 def conv2d_pairs_fwd(xp, wp, bias, K, OH, OW, R, S2, sh, relu=False, stats=None):
     N, Hp, Wq, _ = xp.shape
     out = torch.empty((N, K, OH, OW), dtype=BF16, device=xp.device, memory_format=CL)
+    if S2 == 4 and os.environ.get("BIGDL_STEM_WINDOW", "0") != "0":
+        # width im2col in place: output column ow reads pairs ow .. ow + 3 = all 7 (8) width taps as ONE 32-element
+        # "pixel" of an overlapping-window view (pixel stride 8 elements), so the stem is an R x 1 convolution with a
+        # 32-channel fast-K reduction per row tap (csrc/kernels.h ConvArgs::pstride) instead of R x 4 pair taps of 8.
+        # Opt-in (BIGDL_STEM_WINDOW=1): bitwise the same result and no faster at batch 256 (369 vs 353 us,
+        # profiles/r5_stem_window.txt) — the stem forward is bound by its 411 MB output + statistics epilogue, not
+        # by the gather
+        geo = [N, Hp, Wq, 32, OH, OW, sh, 1, R * 32, K, K, OH, OW, 1, 1, 0, 0, 8]
+        native.get().conv_nt(xp, wp, out, bias, stats, geo, _window_taps(R), relu, None)
+        return out
     geo = [N, Hp, Wq, 8, OH, OW, sh, 1, R * S2 * 8, K, K, OH, OW, 1, 1, 0, 0]
     native.get().conv_nt(xp, wp, out, bias, stats, geo, _pair_taps(R, S2), relu, None)
     return out

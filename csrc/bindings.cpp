@@ -34,7 +34,7 @@ float* omf(const OptT& t, const char* n) { return (t && t->defined()) ? mf(*t, n
 void conv_nt(const Tensor& src, const Tensor& wt, const Tensor& out, const OptT& bias, const OptT& stats,
              std::vector<int64_t> geo, std::vector<int64_t> taps, bool relu, const OptT& addend, const OptT& bn_x,
              const OptT& bn_z, const OptT& bn_mean, const OptT& bn_aff, const OptT& bn_red, bool accumulate) {
-  TORCH_CHECK(geo.size() == 17, "conv_nt: bad geometry");
+  TORCH_CHECK(geo.size() == 17 || geo.size() == 18, "conv_nt: bad geometry");
   if (stats && stats->defined())
     TORCH_CHECK(stats->numel() >= BIGDL_STAT_SLOTS * 2 * geo[9], "conv_nt: stats must hold STAT_SLOTS x 2Ncol");
   TORCH_CHECK(taps.size() % 3 == 0 && !taps.empty() && taps.size() / 3 <= CONV_MAX_TAPS, "conv_nt: bad taps");
@@ -57,6 +57,8 @@ void conv_nt(const Tensor& src, const Tensor& wt, const Tensor& out, const OptT&
   a.Nb = geo[0]; a.Hs = geo[1]; a.Ws = geo[2]; a.Cs = geo[3]; a.OH = geo[4]; a.OW = geo[5];
   a.mul_h = geo[6]; a.mul_w = geo[7]; a.ldw = geo[8]; a.Ncol = geo[9]; a.ldo = geo[10];
   a.OHo = geo[11]; a.OWo = geo[12]; a.omul_h = geo[13]; a.omul_w = geo[14]; a.ooff_h = geo[15]; a.ooff_w = geo[16];
+  a.pstride = geo.size() == 18 ? (int)geo[17] : 0;
+  TORCH_CHECK(a.pstride >= 0 && a.pstride % 8 == 0, "conv_nt: pixel stride must be a multiple of 8");
   a.ntaps = (int)(taps.size() / 3);
   a.Kdim = a.ntaps * a.Cs;
   a.M = a.Nb * a.OH * a.OW;
@@ -67,7 +69,15 @@ void conv_nt(const Tensor& src, const Tensor& wt, const Tensor& out, const OptT&
     a.tap_h[t] = (short)taps[3 * t]; a.tap_w[t] = (short)taps[3 * t + 1]; a.tap_k[t] = (short)taps[3 * t + 2];
     max_tk = std::max(max_tk, (int)a.tap_k[t]);
   }
-  TORCH_CHECK(src.numel() >= (int64_t)a.Nb * a.Hs * a.Ws * a.Cs, "conv_nt: src too small");
+  if (a.pstride > 0) {   // overlapping windows: every window must end inside its source row
+    int max_tw = 0;
+    for (int t = 0; t < a.ntaps; ++t) max_tw = std::max(max_tw, (int)a.tap_w[t]);
+    TORCH_CHECK(((int64_t)(a.OW - 1) * a.mul_w + max_tw) * a.pstride + a.Cs <= (int64_t)a.Ws * a.pstride,
+                "conv_nt: a window crosses its source row");
+    TORCH_CHECK(src.numel() >= (int64_t)a.Nb * a.Hs * a.Ws * a.pstride, "conv_nt: src too small");
+  } else {
+    TORCH_CHECK(src.numel() >= (int64_t)a.Nb * a.Hs * a.Ws * a.Cs, "conv_nt: src too small");
+  }
   TORCH_CHECK(wt.numel() >= (int64_t)(a.Ncol - 1) * a.ldw + (int64_t)(max_tk + 1) * a.Cs, "conv_nt: weight too small");
   // `out` may be a channel-slice view of a wider NHWC buffer (concat written in place): bound by its storage
   const int64_t out_avail = (int64_t)(out.storage().nbytes() / out.element_size()) - out.storage_offset();
@@ -474,7 +484,7 @@ void conv_i8(const Tensor& src, const Tensor& wt, const Tensor& out, const OptT&
   a.wt = reinterpret_cast<const uint16_t*>(wt.data_ptr<int8_t>());
   a.out = reinterpret_cast<uint16_t*>(out.data_ptr());
   a.bias = ocf(bias, "bias"); a.stats = nullptr; a.addend = nullptr; a.out32 = nullptr; a.accum32 = 0;
-  a.ws = nullptr; a.ksplit = 0;
+  a.ws = nullptr; a.ksplit = 0; a.pstride = 0;
   a.bnx = nullptr; a.bnz = nullptr; a.bnmean = nullptr; a.bnaff = nullptr; a.bnred = nullptr;
   a.Nb = geo[0]; a.Hs = geo[1]; a.Ws = geo[2]; a.Cs = geo[3]; a.OH = geo[4]; a.OW = geo[5];
   a.mul_h = geo[6]; a.mul_w = geo[7]; a.ldw = geo[8]; a.Ncol = geo[9]; a.ldo = geo[10];
@@ -896,6 +906,46 @@ void lstm_bwd_step(const Tensor& WT16, const OptT& dg16_next, const OptT& dout, 
                       ldg, mbf(dg16_out, "dg16_out"), B, H, stream());
 }
 
+// Whole-sequence persistent GRU (csrc/lstm_seq.hip): Wrz16 [2H, H], Wn16 [H, H] bf16; xg [B, T, 3H] f32 (r|z|n),
+// h16 [T + 1, B, H] bf16 (h16[0] = h0), rh16 [T, B, H] bf16, gates [3, T, B, H] f32, out [B, T, H] f32.
+bool gru_seq_supported(int64_t B, int64_t H) { return bigdl_gru_seq_supported((int)B, (int)H) != 0; }
+void gru_seq_fwd(const Tensor& Wrz16, const Tensor& Wn16, const Tensor& xg, const OptT& h0, const Tensor& h16,
+                 const Tensor& rh16, const Tensor& gates, const Tensor& out, const Tensor& sync) {
+  TORCH_CHECK(xg.dim() == 3 && xg.is_contiguous() && xg.scalar_type() == at::kFloat, "gru_seq_fwd: xg [B, T, 3H] f32");
+  const int64_t B = xg.size(0), T = xg.size(1), H = Wn16.size(0);
+  TORCH_CHECK(Wrz16.is_contiguous() && Wrz16.size(0) == 2 * H && Wrz16.size(1) == H && Wn16.is_contiguous() &&
+              Wn16.size(1) == H && xg.size(2) == 3 * H, "gru_seq_fwd: weights");
+  TORCH_CHECK(h16.is_contiguous() && h16.numel() == (T + 1) * B * H && rh16.is_contiguous() && rh16.numel() == T * B * H &&
+              gates.is_contiguous() && gates.numel() == 3 * T * B * H && out.is_contiguous() && out.numel() == B * T * H,
+              "gru_seq_fwd: buffers");
+  TORCH_CHECK(sync.scalar_type() == at::kInt && sync.numel() >= bigdl_lstm_seq_sync_words(), "gru_seq_fwd: sync");
+  if (h0 && h0->defined()) TORCH_CHECK(h0->is_contiguous() && h0->numel() == B * H, "gru_seq_fwd: h0");
+  TORCH_CHECK(bigdl_gru_seq(0, cbf(Wrz16, "Wrz16"), cbf(Wn16, "Wn16"), cf(xg, "xg"), ocf(h0, "h0"), mbf(h16, "h16"),
+                            mbf(rh16, "rh16"), mf(gates, "gates"), mf(out, "out"), nullptr, nullptr, nullptr, nullptr,
+                            nullptr, nullptr, reinterpret_cast<unsigned*>(sync.data_ptr<int>()), (int)B, (int)H, (int)T,
+                            stream()) == 0, "gru_seq_fwd: unsupported shape");
+}
+void gru_seq_bwd(const Tensor& Wrz16, const Tensor& Wn16, const OptT& h0, const Tensor& gates, const Tensor& out,
+                 const OptT& dout, const OptT& dhT, const Tensor& dx, const Tensor& dn16, const Tensor& drz16,
+                 const Tensor& dh0, const Tensor& sync) {
+  TORCH_CHECK(dx.dim() == 3 && dx.is_contiguous() && dx.scalar_type() == at::kFloat, "gru_seq_bwd: dx [B, T, 3H] f32");
+  const int64_t B = dx.size(0), T = dx.size(1), H = Wn16.size(0);
+  TORCH_CHECK(Wrz16.is_contiguous() && Wrz16.size(0) == 2 * H && Wn16.is_contiguous() && dx.size(2) == 3 * H,
+              "gru_seq_bwd: weights");
+  TORCH_CHECK(gates.numel() == 3 * T * B * H && out.numel() == B * T * H && dn16.numel() == T * B * H &&
+              drz16.numel() == T * B * 2 * H && dh0.numel() == B * H && gates.is_contiguous() && out.is_contiguous() &&
+              dn16.is_contiguous() && drz16.is_contiguous() && dh0.is_contiguous(), "gru_seq_bwd: buffers");
+  TORCH_CHECK(sync.scalar_type() == at::kInt && sync.numel() >= bigdl_lstm_seq_sync_words(), "gru_seq_bwd: sync");
+  if (dout && dout->defined()) TORCH_CHECK(dout->is_contiguous() && dout->numel() == B * T * H, "gru_seq_bwd: dout");
+  if (dhT && dhT->defined()) TORCH_CHECK(dhT->is_contiguous() && dhT->numel() == B * H, "gru_seq_bwd: dhT");
+  if (h0 && h0->defined()) TORCH_CHECK(h0->is_contiguous() && h0->numel() == B * H, "gru_seq_bwd: h0");
+  TORCH_CHECK(bigdl_gru_seq(1, cbf(Wrz16, "Wrz16"), cbf(Wn16, "Wn16"), nullptr, ocf(h0, "h0"), nullptr, nullptr,
+                            mf(gates, "gates"), mf(out, "out"), ocf(dout, "dout"), ocf(dhT, "dhT"), mf(dx, "dx"),
+                            mbf(dn16, "dn16"), mbf(drz16, "drz16"), mf(dh0, "dh0"),
+                            reinterpret_cast<unsigned*>(sync.data_ptr<int>()), (int)B, (int)H, (int)T, stream()) == 0,
+              "gru_seq_bwd: unsupported shape");
+}
+
 // Whole-sequence persistent LSTM: xg [B, T, 4H] f32, h16 [T + 1, B, H] bf16 (h16[0] = h0), out [B, T, H],
 // cs [T, B, H], acts [T, B, 4H]; sync = int32 workspace of lstm_seq_sync_words() words (zeroed by the launch).
 bool lstm_seq_supported(int64_t B, int64_t H) { return bigdl_lstm_seq_supported((int)B, (int)H) != 0; }
@@ -1193,6 +1243,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "timeouts recorded by persistent (whole-sequence) kernels since the last clear; reads a host-mapped word, no sync");
   m.def("set_seq_timeout_us", &bigdl_set_seq_timeout_us, "bound of every persistent-kernel wait (<= 0: default 2 s)");
   m.def("lstm_seq_fwd", &lstm_seq_fwd);
+  m.def("gru_seq_supported", &gru_seq_supported);
+  m.def("gru_seq_fwd", &gru_seq_fwd);
+  m.def("gru_seq_bwd", &gru_seq_bwd);
   m.def("lstm_seq_bwd", &lstm_seq_bwd);
   m.def("colsum_bf16", &colsum_bf16);
   m.def("layernorm_fwd", &layernorm_fwd);
@@ -1211,6 +1264,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("dh0") = py::none());
   m.def("set_conv_impl", &bigdl_set_conv_impl);
   m.def("set_conv_s1", &bigdl_set_conv_s1);
+  m.def("set_conv_sk", &bigdl_set_conv_sk);
+  m.def("set_wgrad_halo", &bigdl_set_wgrad_halo);
   m.def("set_deterministic", &bigdl_set_deterministic, "1: bitwise-reproducible reductions (no multi-writer float atomics)");
   m.def("deterministic", &bigdl_deterministic);
   m.def("get_conv_impl", &bigdl_get_conv_impl);
@@ -1224,6 +1279,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("get_wgrad_g3", &bigdl_get_wgrad_g3);
   m.def("set_i8_g3", &bigdl_set_i8_g3);
   m.def("set_i8_p8", &bigdl_set_i8_p8);
+  m.def("set_i8_s1", &bigdl_set_i8_s1);
   m.def("set_i8_epi", &bigdl_set_i8_epi);
   m.def("set_i8_shortk", &bigdl_set_i8_shortk);
   m.def("get_i8_g3", &bigdl_get_i8_g3);

@@ -1968,6 +1968,7 @@ __global__ __launch_bounds__(256, NS == 2 ? 4 : ((NS == 3 && BM == 128) ? 3 : 2)
   // slot lane & 3, which holds granule (lane & 3) ^ ((row >> 1) & 3)
   const int rsub = lane >> 2;
   const int gsrc = (lane & 3) ^ ((rsub >> 1) & 3);
+  const int ps = a.pstride > 0 ? a.pstride : a.Cs;   // source pixel stride (ConvArgs::pstride)
   int a_pix[AI], a_h[AI], a_w[AI];
   const int ohw = a.OH * a.OW;
 #pragma unroll
@@ -2023,7 +2024,7 @@ __global__ __launch_bounds__(256, NS == 2 ? 4 : ((NS == 3 && BM == 128) ? 3 : 2)
     for (int j = 0; j < AI; ++j) {
       const int ch = a_h[j] + th, cw = a_w[j] + tw;
       const bool ok = kv && (unsigned)ch < (unsigned)a.Hs && (unsigned)cw < (unsigned)a.Ws;
-      const bf16_t* src = ok ? a.src + (unsigned)((a_pix[j] + ch * a.Ws + cw) * a.Cs + c) : g_zero_granule;
+      const bf16_t* src = ok ? a.src + (unsigned)((a_pix[j] + ch * a.Ws + cw) * ps + c) : g_zero_granule;
       glds16(src, (LDS_PTR(void))(A + (j * 4 + wave) * 16 * BKS));
     }
 #pragma unroll
@@ -2120,7 +2121,16 @@ __global__ __launch_bounds__(256, NS == 2 ? 4 : ((NS == 3 && BM == 128) ? 3 : 2)
 // ABL (diagnostic ablation builds, BIGDL_P8_ABL; wrong outputs): bit 0 no LDS-DMA inside the K-loop, bit 1 no fragment
 // ds_reads after the first K-tile, bit 2 no wave-group stagger, bit 3 no MFMAs, bit 4 no A-operand DMA, bit 5 no
 // B-operand DMA; bit 6 (64) is not an ablation: the one-tap K-tail mode (Cs % 64 != 0, granules past Kdim zero)
-template <bool SPLIT, int ABL = 0>
+// SK (stream-K): gridDim.x persistent workgroups (one per CU) share the tiles x K-tiles iteration space evenly, so a
+// small grid (ResNet-50's 14x14 / 7x7 layers: 98-392 tiles of 256 x 256 on 256 CUs) keeps every CU busy. A workgroup
+// runs its range as segments (one tile's K sub-range each) through the same pipeline; a segment that covers a whole
+// tile finishes it directly, otherwise it parks its fp32 accumulators (register order, write-through sc1 stores, one
+// 256 KB slot per (tile, segment) in ws), drains them, and takes a ticket on the tile's counter; the workgroup that
+// draws the last ticket reads every slot of the tile (sc1 loads) in segment order (the sum is independent of
+// arrival order: deterministic), and runs the fused epilogue. Nobody waits on anybody: correct whatever the
+// residency (the splitk-seam recipe of cdna_hip_programming.md §5 item 2, last-arriver form). a.ksplit = slots per
+// tile; the tickets follow the slots in ws and are zeroed by a fill kernel before the launch.
+template <bool SPLIT, int ABL = 0, bool SK = false>
 __global__ __launch_bounds__(512, 2) void conv_nt_p8_kernel(ConvArgs a) {
   constexpr int BM = 256, BN = 256, BKT = 64;
   constexpr int WGM = 2, WGN = 4;
@@ -2131,8 +2141,9 @@ __global__ __launch_bounds__(512, 2) void conv_nt_p8_kernel(ConvArgs a) {
   constexpr int NH = 4;                            // epilogue row chunks
   constexpr int SL = (TM / NH) * TN;
   static_assert(8 * SL * 4 <= 2 * BUF * 2, "epilogue chunk must fit the buffers");
-  __shared__ __attribute__((aligned(1024))) bf16_t lds[2 * BUF + 3 * CONV_MAX_TAPS];
+  __shared__ __attribute__((aligned(1024))) bf16_t lds[2 * BUF + 3 * CONV_MAX_TAPS + 8];
   short* taps = reinterpret_cast<short*>(lds + 2 * BUF);
+  int* skflag = reinterpret_cast<int*>(lds + 2 * BUF + 3 * CONV_MAX_TAPS);   // in the one LDS array (see above)
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -2140,17 +2151,48 @@ __global__ __launch_bounds__(512, 2) void conv_nt_p8_kernel(ConvArgs a) {
   const int tiles_n = (a.Ncol + BN - 1) / BN;
   const int tiles_m = (a.M + BM - 1) / BM;
   const int nwg = tiles_m * tiles_n;
-  const int bid = xcd_remap(blockIdx.x, nwg);
-  const int tm = bid / tiles_n, tn = bid % tiles_n;
-  const int m0 = tm * BM, n0 = tn * BN;
   constexpr bool KTAIL = (ABL & 64) != 0;          // one tap, Cs % 64 != 0: granules past Kdim load zeros
   const int nk_all = KTAIL ? (a.Kdim + BKT - 1) / BKT : a.Kdim / BKT;
-  int kt0 = 0, nk = nk_all;
-  if constexpr (SPLIT) {
-    const int per = (nk_all + a.ksplit - 1) / a.ksplit;
-    kt0 = blockIdx.y * per;
-    nk = max(0, min(nk_all, kt0 + per) - kt0);
+  if (tid < a.ntaps) {
+    taps[tid] = a.tap_h[tid];
+    taps[CONV_MAX_TAPS + tid] = a.tap_w[tid];
+    taps[2 * CONV_MAX_TAPS + tid] = a.tap_k[tid];
   }
+  __syncthreads();   // tap table visible (no DMA outstanding yet)
+
+  // stream-K range of this workgroup in the (tile, K-tile) iteration space
+  const long I = (long)nwg * nk_all;
+  const long G = gridDim.x;
+  long it = SK ? ((long)blockIdx.x * I) / G : 0;
+  const long it_end = SK ? ((long)(blockIdx.x + 1) * I) / G : 1;
+  auto wg_of = [&](long x) -> int {                // the workgroup whose range holds iteration x
+    long w = (x * G) / I;
+    while (w + 1 < G && ((w + 1) * I) / G <= x) ++w;
+    while (w > 0 && (w * I) / G > x) --w;
+    return (int)w;
+  };
+
+  for (;;) {
+  int bid, tm, tn, kt0, nk;
+  if constexpr (SK) {
+    if (it >= it_end) break;
+    const int tile = (int)(it / nk_all);
+    kt0 = (int)(it - (long)tile * nk_all);
+    nk = (int)min((long)(nk_all - kt0), it_end - it);
+    it += nk;
+    bid = tile;
+    tm = tile / tiles_n; tn = tile % tiles_n;
+  } else {
+    bid = xcd_remap(blockIdx.x, nwg);
+    tm = bid / tiles_n; tn = bid % tiles_n;
+    kt0 = 0; nk = nk_all;
+    if constexpr (SPLIT) {
+      const int per = (nk_all + a.ksplit - 1) / a.ksplit;
+      kt0 = blockIdx.y * per;
+      nk = max(0, min(nk_all, kt0 + per) - kt0);
+    }
+  }
+  const int m0 = tm * BM, n0 = tn * BN;
 
   // DMA geometry: instruction j of wave w fills piece rows (j * 8 + w) * 8 .. +8 (8 rows x 128 B); lane -> row
   // + (lane >> 3), slot lane & 7, which must hold granule (lane & 7) ^ (row & 7) = (lane & 7) ^ (lane >> 3).
@@ -2178,13 +2220,6 @@ __global__ __launch_bounds__(512, 2) void conv_nt_p8_kernel(ConvArgs a) {
     bvalid[q2] = n < a.Ncol;
     wrow[q2] = a.wt + (size_t)(bvalid[q2] ? n : 0) * a.ldw + gsrc * 8;
   }
-  if (tid < a.ntaps) {
-    taps[tid] = a.tap_h[tid];
-    taps[CONV_MAX_TAPS + tid] = a.tap_w[tid];
-    taps[2 * CONV_MAX_TAPS + tid] = a.tap_k[tid];
-  }
-  __syncthreads();   // tap table visible (no DMA outstanding yet)
-
   // piece P (0 A q0, 1 B q0, 2 A q1, 3 B q1) of K-tile kt into buffer buf: 2 DMA instructions per thread
   auto issue = [&](int kt, int buf, int P) {
     const int k0 = kt * BKT;
@@ -2308,11 +2343,60 @@ __global__ __launch_bounds__(512, 2) void conv_nt_p8_kernel(ConvArgs a) {
   if (!(ABL & 4) && wm == 0) __builtin_amdgcn_s_barrier();   // balance the stagger: every wave has left the K-loop
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   float* wl = reinterpret_cast<float*>(lds) + wave * SL;
-  if constexpr (SPLIT) {
+  if constexpr (SK) {
+    bool finish = kt0 == 0 && nk == nk_all;
+    if (!finish) {
+      const int tile = bid;
+      const int w0 = wg_of((long)tile * nk_all), w1 = wg_of((long)(tile + 1) * nk_all - 1);
+      const int nseg = w1 - w0 + 1, seg = (int)blockIdx.x - w0;
+      constexpr int SLOT = MI * NI * 512 * 4;      // floats per (tile, segment) slot
+      float* slots = a.ws + (size_t)tile * a.ksplit * SLOT;
+      {
+        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(slots + (size_t)seg * SLOT, (short)0,
+                                                                           SLOT * 4, 0x00020000);
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < NI; ++j)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, acc[i][j]), r, (((i * NI + j) * 512 + tid) * 4) * 4,
+                                                   0, 16);   // sc1: write-through
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave: its slot stores have left
+      __syncthreads();
+      if (tid == 0) {
+        unsigned* cnt = reinterpret_cast<unsigned*>(a.ws + (size_t)nwg * a.ksplit * SLOT) + tile;
+        const unsigned prev = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *skflag = (prev == (unsigned)(nseg - 1)) ? 1 : 0;
+      }
+      __syncthreads();
+      finish = *skflag != 0;
+      if (finish) {   // last arriver: every slot of the tile, in segment order
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < NI; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+        for (int sgi = 0; sgi < nseg; ++sgi) {
+          const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(slots + (size_t)sgi * SLOT, (short)0,
+                                                                             SLOT * 4, 0x00020000);
+#pragma unroll
+          for (int i = 0; i < MI; ++i) {
+            if (i & 1) asm volatile("" ::: "memory");     // <= 8 slot loads in flight (VGPR budget)
+#pragma unroll
+            for (int j = 0; j < NI; ++j)
+              acc[i][j] += __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(r, (((i * NI + j) * 512 + tid) * 4) * 4, 0, 16));
+          }
+        }
+      }
+    }
+    if (finish) nt_epilogue_lds<MI, NI, TM, TN, NH, WGN * SL, WGM>(a, acc, m0 + wm * TM, n0 + wn * TN, lane, bid, wl, wm);
+    __syncthreads();   // the LDS is restaged by the next segment
+  } else if constexpr (SPLIT) {
     store_partials_lds<MI, NI, TM, TN, NH>(a.ws + (size_t)blockIdx.y * a.M * a.Ncol, a.M, a.Ncol, acc,
                                            m0 + wm * TM, n0 + wn * TN, lane, wl);
   } else {
     nt_epilogue_lds<MI, NI, TM, TN, NH, WGN * SL, WGM>(a, acc, m0 + wm * TM, n0 + wn * TN, lane, bid, wl, wm);
+  }
+  if constexpr (!SK) break;
   }
 }
 
@@ -2728,6 +2812,41 @@ static int p8_pick(const ConvArgs* a) {
   return std::max(split, 1);
 }
 
+// BIGDL_CONV_SK: stream-K for the 256 x 256 P8 kernel. 0 (default): off — it measured slower than the plain P8
+// grid on every ResNet-50 layer its rule selects (profiles/r5_stream_k_ab.txt); 1 = on grids that leave CUs idle (a
+// plain grid of tiles fills < 85 % of its last dispatch round) with deep reductions (Kdim >= BIGDL_CONV_SK_K, default
+// 1024); 2 = wherever the P8 kernel applies (tests). Returns the (tile, segment) slots per tile, 0 when not used.
+int g_conv_sk = -1;
+int conv_impl();
+static int sk_cus() {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (cus <= 0) cus = 256;
+  }
+  return cus;
+}
+static int sk_pick(const ConvArgs* a) {
+  if (g_conv_sk < 0) {
+    const char* e = getenv("BIGDL_CONV_SK");
+    g_conv_sk = e ? atoi(e) : 0;
+  }
+  static const int kmin = [] { const char* e = getenv("BIGDL_CONV_SK_K"); return e ? atoi(e) : 1024; }();
+  if (!g_conv_sk || conv_impl() != 1 || a->out32 || (a->Cs % 64) || (a->Ncol & 7) || (a->ldo & 7)) return 0;
+  if (g_conv_p8 == 0) return 0;
+  if (g_conv_sk == 1 && (a->Ncol < 256 || a->Kdim < kmin)) return 0;
+  const long tiles = (long)((a->M + 255) / 256) * ((a->Ncol + 255) / 256);
+  const int G = sk_cus();
+  const int nk = a->Kdim / 64;
+  const double eff = (double)tiles / (double)(((tiles + G - 1) / G) * G);
+  if (g_conv_sk == 1 && eff >= 0.85) return 0;
+  const long q = (tiles * nk) / G;
+  if (q < 4) return 0;                      // ranges too short for the pipeline
+  return (int)(nk / q + 2);
+}
+
 template <int BN, int NS, int BM = 128>
 void launch_nt_g4(const ConvArgs& a, hipStream_t st) {
   const int nwg = ((a.M + BM - 1) / BM) * ((a.Ncol + BN - 1) / BN);
@@ -2837,6 +2956,7 @@ extern "C" {
 
 void bigdl_set_conv_impl(int impl) { g_conv_impl = impl; }
 void bigdl_set_conv_s1(int v) { g_conv_s1 = v; }
+void bigdl_set_conv_sk(int v) { g_conv_sk = v; }
 void bigdl_set_conv_g4(int v) { g_conv_g4 = v; }
 void bigdl_set_conv_shortk(int v) { g_conv_shortk = v; }
 int g_wgrad_p8 = -1;
@@ -2849,7 +2969,15 @@ int bigdl_get_conv_impl() { return conv_impl(); }
 long bigdl_conv_nt_plan(ConvArgs* a) {
   a->ksplit = 0;
   if (a->Cs % 8 != 0 || a->M <= 0 || conv_impl() < 1) return 0;
+  if (a->pstride > 0 && a->pstride != a->Cs) return 0;   // overlapping windows: g4 only, no split-K
   if (conv_impl() == 1 && s1_applies(a)) return 0;
+  if (g_conv_p8 < 0) (void)p8_pick(a);      // reads BIGDL_CONV_P8 once
+  const int sk = sk_pick(a);
+  if (sk > 0) {
+    a->ksplit = -sk;                        // stream-K: slots per tile (negative marks the mode)
+    const long tiles = (long)((a->M + 255) / 256) * ((a->Ncol + 255) / 256);
+    return tiles * sk * 65536L + tiles;     // fp32 slots + one ticket word per tile
+  }
   const int p8 = conv_impl() == 1 ? p8_pick(a) : 0;
   if (p8 > 1) {
     a->ksplit = p8;
@@ -2873,8 +3001,25 @@ int bigdl_conv_nt(const ConvArgs* a, hipStream_t st) {
   if (a->M <= 0) return 0;
   const bool fastk = (a->Cs % BK) == 0;
   const int impl = conv_impl();
+  if (a->pstride > 0 && a->pstride != a->Cs) {   // overlapping-window source: the g4 kernel is the one that reads it
+    if ((a->Ncol & 7) || (a->ldo & 7) || a->out32 || a->ws || a->bnred || !(fastk || a->Kdim % 8 == 0)) return -4;
+    if (a->Ncol <= 64) launch_nt_g4<64, 3>(*a, st);
+    else launch_nt_g4<128, 3>(*a, st);
+    HIP_LAUNCH_CHECK();
+    return 0;
+  }
   if (impl == 1 && s1_applies(a)) {
     launch_s1_any(*a, st);
+    HIP_LAUNCH_CHECK();
+    return 0;
+  }
+  if (a->ksplit < 0 && a->ws != nullptr) {  // stream-K P8 (bigdl_conv_nt_plan)
+    ConvArgs b = *a;
+    b.ksplit = -a->ksplit;
+    const long tiles = (long)((a->M + 255) / 256) * ((a->Ncol + 255) / 256);
+    bigdl_fill_bytes(b.ws + tiles * b.ksplit * 65536L, 0, tiles * 4, st);   // tickets (a kernel: graph-safe)
+    const dim3 grid((unsigned)std::min<long>(sk_cus(), tiles * (a->Kdim / 64)));
+    conv_nt_p8_kernel<false, 0, true><<<grid, dim3(512), 0, st>>>(b);
     HIP_LAUNCH_CHECK();
     return 0;
   }
@@ -3023,6 +3168,11 @@ int bigdl_conv_wgrad_uses_p8(const WgradArgs* a_in) {
 }
 
 long bigdl_conv_wgrad_plan(WgradArgs* a) {
+  const int hs = bigdl_wgrad_halo_plan(a);
+  if (hs > 0) {
+    a->splits = hs;
+    return hs > 1 ? (long)hs * a->Ncol * a->Kdim : 0;
+  }
   const int p8w = p8w_pick(a);
   if (p8w > 0) {
     a->splits = p8w;
@@ -3065,6 +3215,18 @@ int bigdl_conv_wgrad(const WgradArgs* a_in, hipStream_t st) {
 static int conv_wgrad_impl(const WgradArgs* a_in, hipStream_t st) {
   WgradArgs a = *a_in;
   if (a.Cs % 8 != 0 || a.Ncol % 8 != 0 || a.Kdim % 8 != 0) return -1;
+  {
+    WgradArgs b = a;
+    const int hs = bigdl_wgrad_halo_plan(&b);
+    if (hs > 0 && hs == a.splits && (hs == 1 || a.ws != nullptr)) {
+      b.splits = hs;
+      b.ws = hs > 1 ? a.ws : nullptr;
+      if (bigdl_wgrad_halo(&b, st) == 0) {
+        HIP_LAUNCH_CHECK();
+        return 0;
+      }
+    }
+  }
   {
     WgradArgs b = a;
     const int p8w = p8w_pick(&b);

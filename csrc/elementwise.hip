@@ -576,6 +576,24 @@ __global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ x,
   if (threadIdx.x == 0) atomicAdd(out, sm[0] + sm[1] + sm[2] + sm[3]);
 }
 
+__device__ float g_sumsq_slots[128];
+__global__ __launch_bounds__(256) void sumsq_det_kernel(const float* __restrict__ x, long n) {
+  float acc = 0.f;
+  GRID_STRIDE(i, n) { const float v = x[i]; acc += v * v; }
+  acc = wave_sum(acc);
+  __shared__ float sm[4];
+  if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) g_sumsq_slots[blockIdx.x] = sm[0] + sm[1] + sm[2] + sm[3];
+}
+__global__ void sumsq_det_finish_kernel(float* __restrict__ out) {
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int s = 0; s < 128; ++s) t += g_sumsq_slots[s];
+    out[0] += t;
+  }
+}
+
 __global__ void scale_kernel(float* __restrict__ x, long n, const float* __restrict__ sdev, float s) {
   const float f = sdev ? sdev[0] : s;
   GRID_STRIDE(i, n) x[i] *= f;
@@ -665,10 +683,57 @@ void bigdl_set_deterministic(int v) { g_det = v ? 1 : 0; }
 void bigdl_colsum_bf16(const uint16_t* x, float* out, long P, int K, hipStream_t st) {
   bigdl_colsum_bf16_ld(x, out, P, K, K, st);
 }
+// Deterministic column sum: row block y writes its partial to its own slot (plain stores, no atomics), then one
+// fixed-order pass adds the slots into out (one writer per column).
+constexpr int DET_SLOTS = 128, DET_MAXK = 8192;
+__device__ float g_colsum_slots[DET_SLOTS * DET_MAXK];
+__global__ void __launch_bounds__(256) colsum_det_kernel(const bf16_t* __restrict__ x, long P, int K,
+                                                        long rows_per_block, long ld) {
+  __shared__ float part[4][64][9];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c0 = (blockIdx.x * 64 + lane) * 8;
+  const long r0 = (long)blockIdx.y * rows_per_block;
+  const long r1 = r0 + rows_per_block < P ? r0 + rows_per_block : P;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (c0 < K) {
+    for (long r = r0 + wave; r < r1; r += 4) {
+      const v4u q = *reinterpret_cast<const v4u*>(x + r * ld + c0);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { acc[2 * e] += lo_bf(q[e]); acc[2 * e + 1] += hi_bf(q[e]); }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) part[wave][lane][e] = acc[e];
+  __syncthreads();
+  if (wave == 0 && c0 < K) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      g_colsum_slots[(size_t)blockIdx.y * DET_MAXK + c0 + e] =
+          part[0][lane][e] + part[1][lane][e] + part[2][lane][e] + part[3][lane][e];
+  }
+}
+__global__ void __launch_bounds__(256) colsum_det_finish_kernel(float* __restrict__ out, int K, int nslots) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= K) return;
+  float t = 0.f;
+  for (int s = 0; s < nslots; ++s) t += g_colsum_slots[(size_t)s * DET_MAXK + c];
+  out[c] += t;
+}
+
 // out[k] += sum over P rows (row stride ld, ld % 8 == 0) of x[r][k]
 void bigdl_colsum_bf16_ld(const uint16_t* x, float* out, long P, int K, long ld, hipStream_t st) {
   const int bx = (K / 8 + 63) / 64;
   long by = (P + 255) / 256;                   // >= 64 rows per wave, ~2048 blocks at most
+  if (bigdl_deterministic() && K <= DET_MAXK) {
+    if (by > DET_SLOTS) by = DET_SLOTS;
+    if (by < 1) by = 1;
+    const long rpb = (P + by - 1) / by;
+    by = (P + rpb - 1) / rpb;
+    colsum_det_kernel<<<dim3(bx, (unsigned)by), 256, 0, st>>>(x, P, K, rpb, ld);
+    colsum_det_finish_kernel<<<(K + 255) / 256, 256, 0, st>>>(out, K, (int)by);
+    HIP_LAUNCH_CHECK();
+    return;
+  }
   if ((long)bx * by > 2048) by = (2048 + bx - 1) / bx;
   if (by < 1 || bigdl_deterministic()) by = 1;
   const long rpb = (P + by - 1) / by;
@@ -744,7 +809,13 @@ void bigdl_adam_step(float* w, const float* g, float* m, float* v, uint16_t* w16
   HIP_LAUNCH_CHECK();
 }
 void bigdl_sumsq(const float* x, float* out, long n, hipStream_t st) {
-  sumsq_kernel<<<bigdl_deterministic() ? 1 : grid_cap(n, 2048), 256, 0, st>>>(x, out, n);
+  if (bigdl_deterministic()) {   // fixed order: per-block partials into slots, then one ordered sum
+    sumsq_det_kernel<<<DET_SLOTS, 256, 0, st>>>(x, n);
+    sumsq_det_finish_kernel<<<1, 64, 0, st>>>(out);
+    HIP_LAUNCH_CHECK();
+    return;
+  }
+  sumsq_kernel<<<grid_cap(n, 2048), 256, 0, st>>>(x, out, n);
   HIP_LAUNCH_CHECK();
 }
 void bigdl_scale_f32(float* x, long n, const float* sdev, float s, hipStream_t st) {

@@ -41,6 +41,10 @@ struct ConvArgs {
   // by the split-K epilogue kernel, which applies everything the fused epilogue would (bigdl_conv_nt_plan sets them)
   float* ws;
   int ksplit;
+  // elements between consecutive source pixels (0 = Cs). pstride < Cs views a row of small pixels as overlapping
+  // windows of Cs elements: the bf16 stem's pixel pairs (stem.hip) read 4 consecutive pairs (all 7 width taps of
+  // one output column) as one 32-element "pixel" (conv_nt_g4_kernel only)
+  int pstride;
 };
 
 struct WgradArgs {
@@ -185,6 +189,12 @@ int bigdl_gemv_f32(const float* A, const float* x, const float* Min, float* y, i
 void bigdl_copy_rows_i8(const int8_t* src, int8_t* dst, long rows, int C, long lds, long ldd, hipStream_t st);
 void bigdl_set_conv_impl(int impl);
 void bigdl_set_conv_s1(int v);
+void bigdl_set_conv_sk(int v);
+// 3x3 / stride 1 / pad 1 weight gradient from halo tiles (wgrad_halo.hip): plan returns its splits (0 = n/a)
+void bigdl_set_wgrad_halo(int v);
+int bigdl_wgrad_halo_plan(WgradArgs* a);
+int bigdl_wgrad_halo(const WgradArgs* a, hipStream_t st);
+void bigdl_set_i8_s1(int v);
 int bigdl_get_conv_impl();
 void bigdl_set_conv_g4(int v);
 void bigdl_set_conv_shortk(int v);
@@ -258,6 +268,11 @@ int bigdl_lstm_bwd_step(const uint16_t* WT16, const uint16_t* dg16_next, const f
 int bigdl_lstm_seq_supported(int B, int H);
 void bigdl_set_lstm_seq(int v);
 int bigdl_lstm_seq_sync_words();
+int bigdl_gru_seq_supported(int B, int H);
+int bigdl_gru_seq(int bwd, const uint16_t* Wrz16, const uint16_t* Wn16, const float* xg, const float* h0,
+                  uint16_t* h16, uint16_t* rh16, float* gates, float* out, const float* dout, const float* dhT,
+                  float* dx, uint16_t* dn16, uint16_t* drz16, float* dh0, unsigned* sync, int B, int H, int T,
+                  hipStream_t st);
 int bigdl_persistent_error(int clear);
 unsigned* bigdl_host_word_dev(int slot);
 int bigdl_host_word(int slot, int clear);

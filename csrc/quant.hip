@@ -1075,6 +1075,202 @@ bool i8_shortk() {
   return g_i8_shortk != 0;
 }
 
+// Streaming 1x1 int8 kernel: the structure of conv_nt_s1_kernel (conv_igemm.hip) on v_mfma_i32_16x16x64_i8 for the
+// one-tap int8 GEMMs of the static int8 plan (identity pixel mapping, Kdim = Cs in {64, 128, 256} int8 channels,
+// Ncol % 64 == 0, identity output rows). Persistent workgroups (2 per CU) stride over pixel tiles of one channel
+// block; a wave's weights stay in VGPRs as i8 MFMA fragments for the whole launch (K 256: 64 VGPRs); operand tiles
+// come straight from HBM into VGPRs two tiles ahead; the int32 tile is parked as fp32 in a wave-private LDS slice
+// (16-byte granules XOR-swizzled by pixel) and re-read as 16 channels of one pixel per lane, so the epilogue
+// (y = acc * s_x * s_w[n] + bias (+ int8 residual * s_add), ReLU, bf16 / fp32 / requantized int8) runs once per
+// 16 outputs with the per-channel factors held in registers for the whole launch, and stores whole 16-byte groups.
+// Semantics are i8_tile_epilogue's (CPL = 16).
+template <int K, int CG, int BMW, int OUT, bool ADD>
+__global__ __launch_bounds__(256, 2) void conv_i8_s1_kernel(ConvArgs a, I8Epi ep) {
+  constexpr int KF = K / 64, MI = BMW / 16, PGN = 4 / CG, BM = BMW * PGN;
+  constexpr int NR = BMW / 16;                     // row passes: 16 pixels x 4 lanes (16 channels each)
+  __shared__ __attribute__((aligned(16))) float lds[4 * BMW * 64];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int cg = wave % CG, pg = wave / CG;
+  const int nchb = a.Ncol / (64 * CG);
+  const int chb = blockIdx.x % nchb, wgi = blockIdx.x / nchb, ngr = gridDim.x / nchb;
+  const int c0 = (chb * CG + cg) * 64;
+  const int ntiles = (a.M + BM - 1) / BM;
+  float* wl = lds + wave * BMW * 64;
+  const int q = lane & 3;                          // row phase: channels c0 + 16 q .. + 15
+  const int n = c0 + 16 * q;
+  const int8_t* W8 = reinterpret_cast<const int8_t*>(a.wt);
+  const int8_t* X8 = reinterpret_cast<const int8_t*>(a.src);
+  const int ohw = a.OH * a.OW;
+
+  v4i wf[4][KF];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int kk = 0; kk < KF; ++kk)
+      wf[j][kk] = *reinterpret_cast<const v4i*>(W8 + (size_t)(c0 + 16 * j + (lane & 15)) * a.ldw + 64 * kk +
+                                                16 * (lane >> 4));
+  const float oi = OUT == 2 ? ep.out_inv : 1.f;
+  float wsc[16], bs[16];
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    wsc[e] = ep.wscale[n + e] * oi;
+    bs[e] = a.bias ? a.bias[n + e] * oi : 0.f;
+  }
+  const float as = ep.add_scale * oi;
+
+  auto load = [&](v4i (&af)[MI][KF], int t) {
+    const int p0 = t * BM + pg * BMW;
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int m = min(p0 + 16 * i + (lane & 15), a.M - 1);
+#pragma unroll
+      for (int kk = 0; kk < KF; ++kk)
+        af[i][kk] = *reinterpret_cast<const v4i*>(X8 + (size_t)m * K + 64 * kk + 16 * (lane >> 4));
+    }
+  };
+
+  auto compute_store = [&](v4i (&af)[MI][KF], int t) {
+    const int p0 = t * BM + pg * BMW;
+    v4u pad[ADD ? NR : 1];
+    if constexpr (ADD) {
+#pragma unroll
+      for (int rr = 0; rr < NR; ++rr) {
+        const int m = min(p0 + rr * 16 + (lane >> 2), a.M - 1);
+        pad[rr] = *reinterpret_cast<const v4u*>(ep.add8 + (size_t)m * ep.add_ld + n);
+      }
+    }
+    v4i acc[MI][4];
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = v4i{0, 0, 0, 0};
+#pragma unroll
+    for (int kk = 0; kk < KF; ++kk)
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(wf[j][kk], af[i][kk], acc[i][j], 0, 0, 0);
+    // D[n][m]: lane holds channels 16 j + 4 (lane >> 4) + e of pixel 16 i + (lane & 15): fp32 granule g = 4 j + qq
+    // of a 16-granule (64-channel) row, at slot g ^ (p & 15)
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int p = 16 * i + (lane & 15), g = 4 * j + (lane >> 4);
+        const v4i v = acc[i][j];
+        *reinterpret_cast<v4f*>(wl + (p * 16 + (g ^ (p & 15))) * 4) = v4f{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
+      }
+    __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): wave-private slice
+#pragma unroll
+    for (int rr = 0; rr < NR; ++rr) {
+      const int p = rr * 16 + (lane >> 2);
+      const int m = p0 + p;
+      float v[16];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const v4f t4 = *reinterpret_cast<const v4f*>(wl + (p * 16 + ((4 * q + g) ^ (p & 15))) * 4);
+        v[4 * g] = t4[0]; v[4 * g + 1] = t4[1]; v[4 * g + 2] = t4[2]; v[4 * g + 3] = t4[3];
+      }
+      if (m >= a.M) continue;
+      const float xs = ep.xscale ? ep.xscale[m / ohw] : ep.xs_const;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        float y = v[e] * (xs * wsc[e]) + bs[e];
+        if constexpr (ADD) y += (float)(int8_t)((pad[rr][e >> 2] >> (8 * (e & 3))) & 0xff) * as;
+        if (a.relu) y = fmaxf(y, 0.f);
+        v[e] = y;
+      }
+      const size_t off = (size_t)m * a.ldo + n;
+      if constexpr (OUT == 2) {
+        unsigned pk[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int e = 0; e < 16; ++e) pk[e >> 2] |= (unsigned)(max(-127, min(127, __float2int_rn(v[e]))) & 0xff) << (8 * (e & 3));
+        *reinterpret_cast<v4u*>(reinterpret_cast<int8_t*>(a.out) + off) = v4u{pk[0], pk[1], pk[2], pk[3]};
+      } else if constexpr (OUT == 1) {
+        float* o = reinterpret_cast<float*>(a.out) + off;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) *reinterpret_cast<v4f*>(o + 4 * g) = v4f{v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]};
+      } else {
+        bf16_t* o = a.out + off;
+#pragma unroll
+        for (int g = 0; g < 2; ++g)
+          *reinterpret_cast<v4u*>(o + 8 * g) = v4u{pack2bf(v[8 * g], v[8 * g + 1]), pack2bf(v[8 * g + 2], v[8 * g + 3]),
+                                                   pack2bf(v[8 * g + 4], v[8 * g + 5]), pack2bf(v[8 * g + 6], v[8 * g + 7])};
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);   // the slice is rewritten by the next tile
+  };
+
+  v4i a0[MI][KF], a1[MI][KF], a2[MI][KF];
+  int t = wgi;
+  if (t < ntiles) load(a0, t);
+  if (t + ngr < ntiles) load(a1, t + ngr);
+  for (; t < ntiles; t += 3 * ngr) {
+    if (t + 2 * ngr < ntiles) load(a2, t + 2 * ngr);
+    compute_store(a0, t);
+    if (t + ngr >= ntiles) break;
+    if (t + 3 * ngr < ntiles) load(a0, t + 3 * ngr);
+    compute_store(a1, t + ngr);
+    if (t + 2 * ngr >= ntiles) break;
+    if (t + 4 * ngr < ntiles) load(a1, t + 4 * ngr);
+    compute_store(a2, t + 2 * ngr);
+  }
+}
+
+int g_i8_s1 = -1;   // BIGDL_I8_S1 (default 1): the streaming 1x1 int8 kernel wherever it applies
+bool i8_s1_applies(const ConvArgs& a, const I8Epi& ep) {
+  if (g_i8_s1 < 0) {
+    const char* e = getenv("BIGDL_I8_S1");
+    g_i8_s1 = e ? atoi(e) : 1;
+  }
+  if (!g_i8_s1 || !a.ident_out || a.ntaps != 1 || a.tap_h[0] || a.tap_w[0] || a.tap_k[0]) return false;
+  if (a.mul_h != 1 || a.mul_w != 1 || a.Hs != a.OH || a.Ws != a.OW) return false;
+  if ((a.Kdim != 64 && a.Kdim != 128 && a.Kdim != 256) || a.Cs != a.Kdim || (a.Ncol % 64) || (a.ldw % 16)) return false;
+  const int osz = ep.out_mode == 2 ? 1 : ep.out_mode == 1 ? 4 : 2;
+  if ((a.ldo * osz) % 16 || (ep.add8 && (ep.add_ld % 16))) return false;
+  auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  return al(a.src) && al(a.wt) && al(a.out) && al(ep.add8);
+}
+
+template <int K, int CG, int BMW, int OUT>
+void launch_i8_s1_o(const ConvArgs& a, const I8Epi& ep, hipStream_t st) {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (cus <= 0) cus = 256;
+  }
+  const int nchb = a.Ncol / (64 * CG);
+  const int tiles = (a.M + BMW * (4 / CG) - 1) / (BMW * (4 / CG));
+  int per = std::max(1, (2 * cus) / nchb);
+  per = std::min(per, tiles);
+  if (ep.add8) conv_i8_s1_kernel<K, CG, BMW, OUT, true><<<dim3(per * nchb), dim3(256), 0, st>>>(a, ep);
+  else conv_i8_s1_kernel<K, CG, BMW, OUT, false><<<dim3(per * nchb), dim3(256), 0, st>>>(a, ep);
+}
+
+template <int K, int CG>
+void launch_i8_s1_cg(const ConvArgs& a, const I8Epi& ep, hipStream_t st) {
+  constexpr int BW = K == 256 ? 16 : 32;
+  if (ep.out_mode == 2) launch_i8_s1_o<K, CG, BW, 2>(a, ep, st);
+  else if (ep.out_mode == 1) launch_i8_s1_o<K, CG, BW, 1>(a, ep, st);
+  else launch_i8_s1_o<K, CG, BW, 0>(a, ep, st);
+}
+
+void launch_i8_s1(const ConvArgs& a, const I8Epi& ep, hipStream_t st) {
+  const int cg = (a.Ncol % 256 == 0) ? 4 : (a.Ncol % 128 == 0) ? 2 : 1;
+#define I8S1_K(KK)                                 \
+  if (cg == 4) launch_i8_s1_cg<KK, 4>(a, ep, st);   \
+  else if (cg == 2) launch_i8_s1_cg<KK, 2>(a, ep, st); \
+  else launch_i8_s1_cg<KK, 1>(a, ep, st);
+  if (a.Kdim == 64) { I8S1_K(64) }
+  else if (a.Kdim == 128) { I8S1_K(128) }
+  else { I8S1_K(256) }
+#undef I8S1_K
+}
+
 template <int BM, int BN, int WGM, int WGN>
 void launch_i8_g3(int g, bool fk, const ConvArgs& a, const I8Epi& ep, hipStream_t st) {
   if constexpr (BM == 128 && BN == 128) {
@@ -1149,6 +1345,7 @@ static bool i8_p8() {
   return g_i8_p8 != 0;
 }
 void bigdl_set_i8_p8(int v) { g_i8_p8 = v; }
+void bigdl_set_i8_s1(int v) { g_i8_s1 = v; }
 void bigdl_set_i8_epi(int v) { g_i8_epi = v; }
 void bigdl_set_i8_shortk(int v) { g_i8_shortk = v; }
 void bigdl_set_i8_cpl(int v) { g_i8_cpl = v; }
@@ -1164,7 +1361,9 @@ int bigdl_conv_i8(const ConvArgs* a, const float* xscale, float xs_const, const 
   const bool fk = a->Cs % QBK == 0;
   const bool g3fk = a->Cs % 64 == 0;
   const long p8_tiles = (long)((a->M + 255) / 256) * ((a->Ncol + 255) / 256);
-  if (i8_p8() && fk && a->Kdim >= 1024 && a->Ncol >= 256 && a->Ncol % 16 == 0 &&
+  if (i8_s1_applies(*a, ep)) {
+    launch_i8_s1(*a, ep, st);
+  } else if (i8_p8() && fk && a->Kdim >= 1024 && a->Ncol >= 256 && a->Ncol % 16 == 0 &&
       (g_i8_p8 == 2 || p8_tiles >= 160)) {
     if (i8_direct_ok(*a, ep)) conv_i8_p8_kernel<true><<<dim3((unsigned)p8_tiles), dim3(512), 0, st>>>(*a, ep);
     else conv_i8_p8_kernel<false><<<dim3((unsigned)p8_tiles), dim3(512), 0, st>>>(*a, ep);

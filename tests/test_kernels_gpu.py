@@ -877,3 +877,78 @@ def test_conv_s1_stream_kernel(case, zmask):
         r2 = red.view(bnops.stat_slots(), 2, C).sum(0)
         assert _rel(r2[0], dm.sum(dim=(0, 2, 3))) < 1e-3
         assert _rel(r2[1], (dm * (xf - torch.linspace(-0.1, 0.1, C, device=dev).view(1, C, 1, 1))).sum(dim=(0, 2, 3))) < 1e-3
+
+
+SK_CASES = [
+    # N, C, H, K, R, stride, pad -> stream-K P8 (BIGDL_CONV_SK=2: wherever the 256 x 256 kernel applies)
+    (16, 256, 14, 256, 3, 1, 1),     # 13 tiles x 36 K-tiles over the CUs: multi-segment tiles, padding taps
+    (4, 512, 7, 512, 3, 1, 1),       # 2 x 2 tiles x 72 K-tiles, M tail
+    (16, 256, 28, 256, 3, 2, 1),     # stride 2: dgrad phases with 1-4 taps
+    (8, 1024, 14, 512, 1, 1, 0),     # 1x1, Ncol 512
+    (3, 64, 10, 512, 3, 1, 1),       # tiny M, Cs = 64
+]
+
+
+@pytest.mark.parametrize("case", SK_CASES)
+def test_conv_p8_stream_k(case):
+    """Stream-K 256 x 256 kernel (persistent, segments of the tiles x K-tiles space, last-arriver fixup over
+    write-through partial slots) vs fp32 torch: forward + bias + BN statistics, + ReLU, data gradient + addend + the
+    consumer BN reduction; and run-to-run bit equality (the fixup sums the slots in segment order)."""
+    from bigdl_amd.ops import conv as cv
+    from bigdl_amd.ops import native
+
+    C_ = native.get()
+    C_.set_conv_sk(2)
+    try:
+        test_conv_w8_kernel_fwd_dgrad_bnred(case)
+        N, C, H, K, R, st, pd = case
+        torch.manual_seed(9)
+        x = torch.randn(N, C, H, H, device=_dev()).to(BF, memory_format=CL)
+        w = (torch.randn(K, C, R, R, device=_dev()) * (1.0 / (C * R * R) ** 0.5)).to(BF, memory_format=CL)
+        y1 = cv.conv2d_fwd(x, w, None, (st, st), (pd, pd))
+        y2 = cv.conv2d_fwd(x, w, None, (st, st), (pd, pd))
+        torch.cuda.synchronize()
+        assert torch.equal(y1, y2)
+        C_.set_conv_sk(0)
+        y0 = cv.conv2d_fwd(x, w, None, (st, st), (pd, pd))
+        assert _rel(y1, y0) < 1e-2
+    finally:
+        C_.set_conv_sk(1)
+
+
+# 3x3 / stride 1 / pad 1 weight gradients on the halo-tile kernel (csrc/wgrad_halo.hip): every supported width, both
+# output-channel blocks (64 / 128), a single split (direct add into dW) and many splits (workspace + reduce), a
+# non-zero starting dW (the kernel accumulates), and the same shapes with the kernel switched off as a control.
+HALO_CASES = [
+    (4, 64, 56, 64), (2, 64, 56, 128), (8, 128, 28, 128), (3, 64, 28, 64), (16, 256, 14, 256), (5, 64, 14, 192),
+    (32, 512, 7, 512), (1, 64, 7, 64), (256, 64, 7, 128),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", HALO_CASES)
+def test_conv_wgrad_halo_matches_fp32(case):
+    from bigdl_amd.ops import conv as cv
+    from bigdl_amd.ops import native
+
+    N, C, H, K = case
+    torch.manual_seed(5)
+    dev = _dev()
+    x = torch.randn(N, C, H, H, device=dev).to(BF, memory_format=CL)
+    gy = torch.randn(N, K, H, H, device=dev).to(BF, memory_format=CL)
+    dw0 = torch.randn(K, C, 3, 3, device=dev).contiguous(memory_format=CL)
+    ref = dw0 + torch.nn.grad.conv2d_weight(x.float(), (K, C, 3, 3), gy.float(), stride=1, padding=1)
+    outs = []
+    try:
+        for on in (1, 0):
+            native.get().set_wgrad_halo(on)
+            dw = dw0.clone()
+            cv.conv2d_wgrad(gy, x, dw, None, (1, 1), (1, 1))
+            torch.cuda.synchronize()
+            outs.append(dw)
+    finally:
+        native.get().set_wgrad_halo(1)
+    for dw in outs:
+        assert torch.isfinite(dw).all()
+        assert _rel(dw, ref) < 5e-3, _rel(dw, ref)
+    assert _rel(outs[0], outs[1]) < 5e-3

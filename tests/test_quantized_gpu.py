@@ -201,3 +201,59 @@ def test_quantized_resnet_block_model_gpu():
     q.cuda()
     y = q.forward(x.cuda())
     assert _rel(y.float().cpu(), y_cpu) < 2e-2
+
+
+I8_S1_CASES = [
+    # 1x1 stride-1 layers the streaming int8 kernel takes (Cs in {64, 128, 256}, Ncol % 64 == 0)
+    (3, 64, 14, 14, 256, 1, 1, 1, 0, 1),    # four channel groups, M tail
+    (2, 128, 13, 13, 512, 1, 1, 1, 0, 1),   # two channel blocks
+    (4, 256, 9, 9, 64, 1, 1, 1, 0, 1),      # K 256 (4 i8 MFMA K-steps), one channel group
+    (5, 64, 11, 11, 128, 1, 1, 1, 0, 1),    # two channel groups
+    (2, 256, 7, 7, 192, 1, 1, 1, 0, 1),     # three one-group channel blocks
+]
+
+
+@pytest.mark.parametrize("case", I8_S1_CASES)
+def test_conv_i8_s1_exact(case):
+    """Streaming 1x1 int8 kernel (conv_i8_s1_kernel): fp32 output equal to the integer conv (unit scales), int8
+    output with an int8 residual and ReLU exactly clamped, and the same int8 bytes as the per-tile kernels."""
+    from bigdl_amd.ops.conv import _fwd_taps, out_size
+
+    C_ = native.get()
+    _conv_i8_exact(case)
+    N, C, H, W, K, R, S, st, pd, dl = case
+    g = torch.Generator().manual_seed(3)
+    x = torch.randint(-3, 4, (N, H, W, C), generator=g, dtype=torch.int8)
+    w = torch.randint(-3, 4, (K, R, S, C), generator=g, dtype=torch.int8)
+    OH, OW = out_size(H, R, st, pd, dl), out_size(W, S, st, pd, dl)
+    ref = F.conv2d(x.permute(0, 3, 1, 2).double(), w.permute(0, 3, 1, 2).double(), None, st, pd, dl)
+    ref = ref.permute(0, 2, 3, 1).reshape(N * OH * OW, K)
+    bias = torch.randint(-20, 21, (K,), generator=g).float()
+    add = torch.randint(-127, 128, (N * OH * OW, K), generator=g, dtype=torch.int8)
+    geo = [N, H, W, C, OH, OW, st, st, R * S * C, K, K, OH, OW, 1, 1, 0, 0]
+    outs = {}
+    for s1 in (1, 0):
+        C_.set_i8_s1(s1)
+        try:
+            for relu in (False, True):
+                out = torch.zeros(N * OH * OW, K, dtype=torch.int8, device="cuda")
+                C_.conv_i8(x.cuda(), w.cuda(), out, bias.cuda(), torch.ones(N, device="cuda"),
+                           torch.ones(K, device="cuda"), geo, _fwd_taps(R, S, pd, pd, dl, dl), relu, 1.0, 1.0,
+                           add.view(N, OH, OW, K).cuda(), 1.0)
+                bf = torch.zeros(N * OH * OW, K, dtype=torch.bfloat16, device="cuda")
+                xs = torch.rand(N, device="cuda") + 0.5
+                C_.conv_i8(x.cuda(), w.cuda(), bf, bias.cuda(), xs, torch.ones(K, device="cuda"), geo,
+                           _fwd_taps(R, S, pd, pd, dl, dl), relu)
+                torch.cuda.synchronize()
+                outs[(s1, relu)] = (out.cpu(), bf.float().cpu(), xs.cpu())
+        finally:
+            C_.set_i8_s1(1)
+    for relu in (False, True):
+        exp = (ref + bias.double() + add.double()).clamp(0 if relu else -127, 127).to(torch.int8)
+        assert torch.equal(outs[(1, relu)][0], exp)
+        assert torch.equal(outs[(1, relu)][0], outs[(0, relu)][0])
+        xs = outs[(1, relu)][2].double().repeat_interleave(OH * OW).view(-1, 1)
+        yb = ref * xs + bias.double()
+        if relu:
+            yb = yb.clamp(min=0)
+        assert _rel(outs[(1, relu)][1], yb) < 1e-2

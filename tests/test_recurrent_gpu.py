@@ -145,7 +145,8 @@ def test_bidirectional_two_layer_rnn_gpu_matches_cpu(cellname):
     assert _rel(wg, wc) < 3e-2
 
 
-@pytest.mark.parametrize("B,T,H", [(128, 16, 1024), (100, 7, 512), (9, 5, 256), (64, 3, 1024)])
+@pytest.mark.parametrize("B,T,H", [(128, 16, 1024), (100, 7, 512), (9, 5, 256), (64, 3, 1024), (256, 8, 1024),
+                                   (200, 5, 512), (137, 4, 256)])
 def test_persistent_lstm_sequence_matches_step_kernels(B, T, H):
     """csrc/lstm_seq.hip (one persistent launch per direction, W resident in VGPRs, per-step group hand-off) vs the
     per-step kernels of csrc/lstm.hip and the fp64 torch recurrence: outputs, final state and all four gradients;
@@ -251,7 +252,7 @@ def test_persistent_lstm_forced_timeout_raises():
     assert bool(ok.all())
 
 
-@pytest.mark.parametrize("B,T,H", [(128, 12, 1024), (40, 5, 256)])
+@pytest.mark.parametrize("B,T,H", [(128, 12, 1024), (40, 5, 256), (256, 6, 1024)])
 def test_persistent_lstm_bf16_io_matches_f32_io(B, T, H):
     """bf16 gate inputs / outputs / gradients (the projection GEMMs' dtype, no f32 round trip) vs the f32-I/O launch of
     the same kernels: outputs, final state and all four gradients within bf16 rounding of the I/O tensors."""
@@ -281,7 +282,7 @@ def test_recurrent_output_dtype_stable_across_batch_sizes():
     per-step kernels above): bf16 sequence I/O is an explicit opt-in (Recurrent(bf16IO=True))."""
     from bigdl_amd import nn
 
-    for B in (16, 200):
+    for B in (16, 300):
         torch.manual_seed(0)
         m = nn.Recurrent().add(nn.LSTM(64, 256, 0)).cuda()
         x = torch.randn(B, 5, 64, device="cuda")
@@ -292,3 +293,47 @@ def test_recurrent_output_dtype_stable_across_batch_sizes():
     m = nn.Recurrent(bf16IO=True).add(nn.LSTM(64, 256, 0)).cuda()
     y = m.forward(torch.randn(16, 5, 64, device="cuda"))
     assert y.dtype in (torch.bfloat16, torch.float32)
+
+
+@pytest.mark.parametrize("B,T,H", [(128, 12, 1024), (37, 6, 512), (9, 5, 256)])
+def test_persistent_gru_sequence_matches_step_kernels(B, T, H):
+    """Persistent whole-sequence GRU (csrc/lstm_seq.hip gru_seq_*_kernel: one launch per direction, two group
+    hand-offs per step) vs the per-step GRU kernels (csrc/gru.hip) and an fp64 torch recurrence: outputs, final state
+    and all four gradients (input gates, h0, U_rz, U_n)."""
+    from bigdl_amd.nn.recurrent import _GRUSeq
+    from bigdl_amd.ops import native
+
+    C = native.get()
+    torch.manual_seed(2)
+    xg = torch.randn(B, T, 3 * H) * 0.5
+    h0 = torch.randn(B, H) * 0.5
+    Urz = (torch.randn(2 * H, H) / H ** 0.5).to(torch.bfloat16).float()
+    Un = (torch.randn(H, H) / H ** 0.5).to(torch.bfloat16).float()
+    go, gh = torch.randn(B, T, H), torch.randn(B, H)
+    res = {}
+    try:
+        for seq in (1, 0):
+            C.set_lstm_seq(seq)
+            assert bool(C.gru_seq_supported(B, H)) == bool(seq)
+            dev = [t.cuda().requires_grad_(True) for t in (xg, h0, Urz, Un)]
+            out, hT = _GRUSeq.apply(*dev)
+            torch.autograd.backward([out, hT], [go.cuda(), gh.cuda()])
+            torch.cuda.synchronize()
+            res[seq] = [out.detach(), hT.detach()] + [d.grad for d in dev]
+    finally:
+        C.set_lstm_seq(1)
+    native.check_persistent()
+    for a, b in zip(res[1], res[0]):
+        assert torch.isfinite(a).all()
+        assert _rel(a, b) < 2e-2, _rel(a, b)
+    # fp64 recurrence for the outputs
+    x64, h = xg.double(), h0.double()
+    outs = []
+    for t in range(T):
+        rz = torch.sigmoid(x64[:, t, :2 * H] + h @ Urz.double().t())
+        r, z = rz[:, :H], rz[:, H:]
+        n = torch.tanh(x64[:, t, 2 * H:] + (r * h) @ Un.double().t())
+        h = (1 - z) * n + z * h
+        outs.append(h)
+    ref = torch.stack(outs, 1)
+    assert _rel(res[1][0], ref) < 1e-2

@@ -24,8 +24,11 @@ OH = cv.out_size(H, R, st, pd)
 gy = torch.randn(N, K, OH, OH, device=dev).to(BF, memory_format=CL)
 wt = cv.transpose_w(w)
 stats = bnops.new_stats(K, dev)
+dw = torch.zeros(K, C, R, R, device=dev).contiguous(memory_format=CL)
 for _ in range(a.iters):
-    if a.op == "fwd":
+    if a.op == "wgrad":
+        cv.conv2d_wgrad(gy, x, dw, None, (st, st), (pd, pd))
+    elif a.op == "fwd":
         cv.conv2d_fwd(x, w, None, (st, st), (pd, pd), stats=stats)
     else:
         cv.conv2d_dgrad(gy, wt, x.shape, (st, st), (pd, pd))

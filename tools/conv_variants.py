@@ -1,7 +1,7 @@
 """A/B of conv kernel choices on single ResNet-50 layers, interleaved in one process (GPU).
 
 For each selected layer (tools/bench_conv.py SHAPES index) and pass (fwd with the BN-statistics epilogue, fwd without
-statistics, dgrad), every variant (a set of runtime switches: set_conv_impl / set_conv_g4 / set_conv_p8 / set_conv_nt2)
+statistics, dgrad, dgrad with the BN-backward epilogue, wgrad), every variant (a set of runtime switches: set_conv_impl / set_conv_g4 / set_conv_p8 / set_conv_nt2)
 is timed over --rounds interleaved rounds of --iters launches; the table prints the median per variant and the
 output's max abs difference against the first variant (so a variant that computes something else shows).
 
@@ -23,8 +23,9 @@ from bigdl_amd.ops import conv as cv  # noqa: E402
 from bigdl_amd.ops import native  # noqa: E402
 
 SETTERS = {"impl": "set_conv_impl", "g4": "set_conv_g4", "p8": "set_conv_p8", "nt2": "set_conv_nt2",
-           "shortk": "set_conv_shortk", "s1": "set_conv_s1"}
-DEFAULTS = {"impl": 1, "g4": 3, "p8": 1, "nt2": 0, "shortk": 0, "s1": 1}
+           "shortk": "set_conv_shortk", "s1": "set_conv_s1", "sk": "set_conv_sk",
+           "halo": "set_wgrad_halo"}
+DEFAULTS = {"impl": 1, "g4": 3, "p8": 1, "nt2": 0, "shortk": 0, "s1": 1, "sk": 0, "halo": 1}
 
 
 def parse_variants(spec):
@@ -74,6 +75,7 @@ def main():
         bx = torch.randn(N, C, H, H, device=dev).to(BF, memory_format=CL)
         bz = torch.relu(torch.randn(N, C, H, H, device=dev)).to(BF, memory_format=CL)
         red = bnops.new_stats(C, dev)
+        dw = torch.zeros(K, C, R, R, device=dev).contiguous(memory_format=CL)
         bnarg = {"x": bx, "z": bz, "mean": torch.zeros(C, device=dev), "aff": None, "red": red}
         passes = {
             "fwd": lambda: cv.conv2d_fwd(x, w, None, (st, st), (pd, pd), stats=stats),
@@ -81,6 +83,8 @@ def main():
             "dgrad": lambda: cv.conv2d_dgrad(gy, wt, x.shape, (st, st), (pd, pd)),
             # training form: residual-gradient addend + the consumer BN's fused backward reduction (z mask)
             "dgrad_bn": lambda: cv.conv2d_dgrad(gy, wt, x.shape, (st, st), (pd, pd), addend=add, bn=dict(bnarg)),
+            # weight gradient into a zeroed fp32 dW (the memset is inside the timed launches)
+            "wgrad": lambda: cv.conv2d_wgrad(gy, x, dw.zero_(), None, (st, st), (pd, pd)) or dw,
         }
         for op in a.ops.split(","):
             if op.startswith("dgrad") and li == 0:
@@ -90,7 +94,7 @@ def main():
             outs = {}
             for n, sw in variants:
                 apply(sw)
-                outs[n] = fn().float()
+                outs[n] = fn().float().clone()
             torch.cuda.synchronize()
             for _ in range(a.rounds):
                 for n, sw in variants:
