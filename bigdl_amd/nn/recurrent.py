@@ -299,8 +299,12 @@ class _LSTMSeq(torch.autograd.Function):
         return xg.dtype == torch.float32
 
     @staticmethod
-    def forward(ctx, xg, h0, c0, U):
+    def forward(ctx, xg, h0, c0, U, gsink=None):
         ctx.set_materialize_grads(False)   # unused outputs (final h / c) get None, not a zero-filled aten tensor
+        # gsink: the module's fp32 gradWeight buffer (Recurrent training, scale 1): the whole-sequence backward then
+        # accumulates dU straight into it with the weight-gradient kernel (+=) and returns no U gradient — no zeroed
+        # temporary and no separate add into gradWeight afterwards
+        ctx.gsink = gsink
         B, T, G = xg.shape
         H = G // 4
         if xg.dtype != torch.float32 and not _LSTMSeq._fused_gpu(xg, U):
@@ -327,7 +331,7 @@ class _LSTMSeq(torch.autograd.Function):
                 C.lstm_seq_fwd(W16, xg, c0.contiguous(), h16, out, hT, cs, acts, sync)
                 ctx.save_for_backward(h0, c0, U, out, cs, acts, h16, W16)
                 ctx.fused = True
-                return out, hT, cs[-1].clone()
+                return out, hT, cs[T - 1]          # a view of the saved states: no device copy
             else:
                 c_prev = c0.contiguous()
                 for t in range(T):
@@ -370,10 +374,14 @@ class _LSTMSeq(torch.autograd.Function):
             C.lstm_seq_bwd(W16, dout, dhT.contiguous() if dhT is not None else None,
                            dcT.contiguous() if dcT is not None else None, acts, cs, c0.contiguous(), dg16, dxg, dc0,
                            dh0, sync)
-            dU = out.new_empty(4 * H, H, 1, 1, dtype=torch.float32)
-            C.fill_bytes(dU, 0)
+            sink = ctx.gsink
+            if sink is not None:
+                dU = sink.view(4 * H, H, 1, 1)
+            else:
+                dU = out.new_empty(4 * H, H, 1, 1, dtype=torch.float32)
+                C.fill_bytes(dU, 0)
             cv.conv2d_wgrad(dg16.view(T * B, 4 * H, 1, 1), h16[:T].view(T * B, H, 1, 1), dU, None, (1, 1), (0, 0))
-            return dxg, dh0, dc0, dU.view(4 * H, H)
+            return dxg, dh0, dc0, (None if sink is not None else dU.view(4 * H, H)), None
         WT16 = cv.transpose_w(W16.view(4 * H, H, 1, 1)).view(H, 4 * H)
         dxg = out.new_empty(B, T, 4 * H)
         dg16 = out.new_empty(T, B, 4 * H, dtype=torch.bfloat16)      # time-major: rows t*B + b
@@ -385,7 +393,10 @@ class _LSTMSeq(torch.autograd.Function):
                             dout[:, t] if dout is not None else None, dhT if t == T - 1 else None, acts[t],
                             cs[t - 1] if t > 0 else c0, cs[t], dc, dxg[:, t], dg16[t])
         dh0, dU = _rnn_param_grads(dg16, h16, U, WT16)
-        return dxg, dh0, dc, dU
+        if ctx.gsink is not None:
+            ctx.gsink.add_(dU)
+            dU = None
+        return dxg, dh0, dc, dU, None
 
     @staticmethod
     def backward(ctx, dout, dhT, dcT):
@@ -406,7 +417,10 @@ class _LSTMSeq(torch.autograd.Function):
             dc_next, dc_prev = dc_prev, dc_next
         hprev = torch.cat([h0.unsqueeze(0), hs[:-1]], 0).reshape(T * B, H)
         dU = dgs.reshape(T * B, 4 * H).t() @ hprev
-        return dgs.transpose(0, 1), dh_next, dc_next, dU
+        if ctx.gsink is not None:
+            ctx.gsink.add_(dU)
+            dU = None
+        return dgs.transpose(0, 1), dh_next, dc_next, dU, None
 
 
 class _GRUSeq(torch.autograd.Function):
@@ -505,6 +519,114 @@ class _GRUSeq(torch.autograd.Function):
         return dx, dh0, dUrz.view(2 * H, H), dUn.view(H, H)
 
 
+def _ceil(v, m):
+    return (v + m - 1) // m * m
+
+
+class _LSTMDropSeq(torch.autograd.Function):
+    """LSTM with dropout p != 0 on the GPU, the reference's per-gate Dropout + Linear branches
+    (S/nn/LSTM.scala:68-96) as native kernels (csrc/lstm_drop.hip): gate g of step t reads x_t and h_{t-1} through
+    their own Philox masks (regenerated, never stored). The input side is ONE batched gate GEMM over all T * B rows
+    (four masked copies of x, biases folded in as a ones column); per step: mask h_{t-1} (one launch), the four
+    recurrent GEMMs accumulating into that step's gate pre-activations (bmm_nt on a [4][B][H] view of [B][4H]), the
+    fused cell. Backward mirrors it; weight gradients are one NT GEMM per gate over the whole sequence."""
+
+    @staticmethod
+    def usable(x, H, I):
+        return x.is_cuda and x.dim() == 3 and H % 32 == 0 and I % 4 == 0 and x.dtype == torch.float32
+
+    @staticmethod
+    def forward(ctx, x, h0, c0, Wi, bi, U, bu, p):
+        from ..ops import nnk
+
+        C = ops.native.get()
+        B, T, I = x.shape
+        H = U.shape[1]
+        R, Ip = T * B, _ceil(I + 1, 32)
+        keep = 1.0 - p
+        mul = 1.0 / keep
+        sx, sh = nnk.next_seed(), nnk.next_seed()
+        dev = x.device
+        x = x.contiguous()
+        Wi4 = torch.empty(4, H, Ip, dtype=torch.bfloat16, device=dev)
+        C.lstm_pack_gate_w(Wi.detach().contiguous(), bi, bu, H, I, Ip, Wi4, None)
+        U4 = torch.empty(4, H, H, dtype=torch.bfloat16, device=dev)
+        C.lstm_pack_gate_w(U.detach().contiguous(), None, None, H, H, H, U4, None)
+        xm = torch.empty(4, R, Ip, dtype=torch.bfloat16, device=dev)
+        C.lstm_drop_rep(x, T * I, I, xm, R * Ip, B, T, I, Ip, True, p, mul, sx, 0)
+        G = torch.empty(T, B, 4 * H, dtype=torch.float32, device=dev)      # gate pre-activations, time-major
+        C.bmm_nt(xm, Wi4, G.view(R, 4, H).permute(1, 0, 2), 1.0, False)
+        hm = torch.empty(4, T, B, H, dtype=torch.bfloat16, device=dev)    # masked h_{t-1} per gate (dU operand)
+        cs = torch.empty(T, B, H, dtype=torch.float32, device=dev)
+        hs = torch.empty(T, B, H, dtype=torch.float32, device=dev)
+        acts = torch.empty(T, B, 4 * H, dtype=torch.float32, device=dev)
+        h_prev, c_prev = h0.detach().contiguous(), c0.detach().contiguous()
+        for t in range(T):
+            C.lstm_drop_rep(h_prev, H, 0, hm[:, t], T * B * H, B, 1, H, H, False, p, mul, sh, t * 4 * B * H)
+            C.bmm_nt(hm[:, t], U4, G[t].view(B, 4, H).permute(1, 0, 2), 1.0, True)
+            C.lstm_cell_fwd(G[t], c_prev, cs[t], hs[t], acts[t])
+            h_prev, c_prev = hs[t], cs[t]
+        ctx.save_for_backward(c0, Wi, U, xm, hm, cs, acts)
+        ctx.cfg = (p, mul, sx, sh, B, T, I, H)
+        ctx.set_materialize_grads(False)
+        return hs.transpose(0, 1).contiguous(), hs[T - 1], cs[T - 1]
+
+    @staticmethod
+    def backward(ctx, dout, dhT, dcT):
+        C = ops.native.get()
+        c0, Wi, U, xm, hm, cs, acts = ctx.saved_tensors
+        p, mul, sx, sh, B, T, I, H = ctx.cfg
+        R, Ip = T * B, xm.shape[2]
+        dev = xm.device
+        dout = dout.float().contiguous() if dout is not None else None
+        UT4 = torch.empty(4, H, H, dtype=torch.bfloat16, device=dev)
+        C.lstm_pack_gate_w(U.detach().contiguous(), None, None, H, H, H, None, UT4)
+        dG = torch.empty(T, B, 4 * H, dtype=torch.float32, device=dev)
+        dG16 = torch.empty(T, B, 4 * H, dtype=torch.bfloat16, device=dev)
+        dhm = torch.empty(4, B, H, dtype=torch.float32, device=dev)
+        dc = dcT.float().contiguous().clone() if dcT is not None else ops.zeros(B, H, device=dev)
+        if dout is not None and dhT is not None:
+            dh = dout[:, T - 1] + dhT.float()
+        elif dout is not None:
+            dh = dout[:, T - 1].contiguous()
+        elif dhT is not None:
+            dh = dhT.float().contiguous().clone()
+        else:
+            dh = ops.zeros(B, H, device=dev)
+        dh0 = torch.empty(B, H, dtype=torch.float32, device=dev)
+        dhb = torch.empty(B, H, dtype=torch.float32, device=dev)     # dh of steps T-2 .. 0 (stream-ordered reuse)
+        c0 = c0.detach().contiguous()
+        for t in range(T - 1, -1, -1):
+            C.lstm_cell_bwd(acts[t], cs[t - 1] if t > 0 else c0, cs[t], dh, dc, dG[t], dc)
+            C.cast_f32_bf16(dG[t], dG16[t])
+            C.bmm_nt(dG16[t].view(B, 4, H).permute(1, 0, 2), UT4, dhm, 1.0, False)
+            if t > 0:     # dh_{t-1} = dout_{t-1} + sum_g (dG_g U_g) * mask_h(g, t)
+                C.lstm_drop_rep_bwd(dhm, B * H, H, dhb, H, 0, dout[:, t - 1] if dout is not None else None, T * H, 0,
+                                    B, 1, H, p, mul, sh, t * 4 * B * H)
+                dh = dhb
+            else:
+                C.lstm_drop_rep_bwd(dhm, B * H, H, dh0, H, 0, None, 0, 0, B, 1, H, p, mul, sh, 0)
+        # weight / bias gradients: one NT GEMM per gate over all T * B rows (dbu = column sums of dG_g)
+        dU = ops.zeros(4 * H, H, device=dev)
+        dbu = ops.zeros(4 * H, device=dev)
+        dWi4 = ops.zeros(4, H, Ip, device=dev)
+        flat = dG16.view(-1)
+        for g in range(4):
+            C.conv_wgrad(flat[g * H:], hm[g], dU[g * H:(g + 1) * H], dbu[g * H:(g + 1) * H],
+                         [R, 1, 1, H, 1, 1, 1, 1, 1, 1, 0, 0, 1, 1, R, H, H, 4 * H])
+            C.conv_wgrad(flat[g * H:], xm[g], dWi4[g], None, [R, 1, 1, Ip, 1, 1, 1, 1, 1, 1, 0, 0, 1, 1, R, H, Ip, 4 * H])
+        dWi = dWi4[:, :, :I].reshape(4 * H, I)
+        dbi = dWi4[:, :, I].reshape(4 * H)
+        # input gradient: dxm_g = dG_g Wi_g, summed back through the input masks into [B][T][I]
+        WiT4 = torch.empty(4, I, H, dtype=torch.bfloat16, device=dev)
+        C.lstm_pack_gate_w(Wi.detach().contiguous(), None, None, H, I, I, None, WiT4)
+        dxm = torch.empty(4, R, I, dtype=torch.float32, device=dev)
+        C.bmm_nt(dG16.view(R, 4, H).permute(1, 0, 2), WiT4, dxm, 1.0, False)
+        dx = torch.empty(B, T, I, dtype=torch.float32, device=dev)
+        C.lstm_drop_rep_bwd(dxm, R * I, I, dx, T * I, I, None, 0, 0, B, T, I, p, mul, sx, 0)
+        return dx, dh0, dc, dWi, dbi, dU, dbu, None
+
+
 class LSTM(Cell):
     """Long short-term memory cell (S/nn/LSTM.scala:46). Hidden = T(h, c); gate order (i, g, f, o)."""
 
@@ -514,9 +636,17 @@ class LSTM(Cell):
         self.inputSize, self.hiddenSize, self.p = inputSize, hiddenSize, p
         self.activation = activation if activation is not None else Tanh()
         self.innerActivation = innerActivation if innerActivation is not None else Sigmoid()
-        self._set_pre(Linear(inputSize, 4 * hiddenSize, wRegularizer=wRegularizer, bRegularizer=bRegularizer))
-        self.h2g = Linear(hiddenSize, 4 * hiddenSize, withBias=p != 0, wRegularizer=uRegularizer,
-                          bRegularizer=bRegularizer if p != 0 else None)
+        if p != 0:
+            # the reference's dropout topology (LSTM.scala:76-129): no preTopology; every step, gate g reads
+            # Dropout(p)(x_t) through its own input Linear and Dropout(p)(h_{t-1}) through its own hidden Linear
+            # (with bias, wRegularizer / bRegularizer). The four per-gate Linears of each side are stored stacked
+            # as one [4H, .] Linear (gate order i, g, f, o)
+            self.i2g = Linear(inputSize, 4 * hiddenSize, wRegularizer=wRegularizer, bRegularizer=bRegularizer)
+            self.modules.append(self.i2g)
+            self.h2g = Linear(hiddenSize, 4 * hiddenSize, wRegularizer=wRegularizer, bRegularizer=bRegularizer)
+        else:
+            self._set_pre(Linear(inputSize, 4 * hiddenSize, wRegularizer=wRegularizer, bRegularizer=bRegularizer))
+            self.h2g = Linear(hiddenSize, 4 * hiddenSize, withBias=False, wRegularizer=uRegularizer)
         self.modules.append(self.h2g)
 
     def hiddenSizeOfPreTopo(self):
@@ -526,18 +656,22 @@ class LSTM(Cell):
         return self.p == 0 and _is(self.activation, Tanh) and _is(self.innerActivation, Sigmoid)
 
     def _gate_inputs(self, x, h):
-        """p != 0: the reference uses four independent Dropout+Linear branches per gate (LSTM.scala:68-96);
-        here the recurrent input gets four independent dropout masks (one per gate block of U)."""
+        """Gate pre-activations [B, 4H]. p != 0 (x is the raw input then): four independent dropout masks per side,
+        one per gate block, in training (LSTM.scala:68-96); the plain affine maps otherwise."""
         H = self.hiddenSize
-        if self.p != 0 and self.train:
-            keep = 1.0 - self.p
-            hm = torch.stack([torch.bernoulli(torch.full_like(h, keep)) / keep for _ in range(4)])
-            U = self.h2g.weight.view(4, H, H)
-            hg = torch.bmm(h.unsqueeze(0) * hm, U.transpose(1, 2)).permute(1, 0, 2).reshape(h.shape[0], 4 * H)
-            if self.h2g.bias is not None:
-                hg = hg + self.h2g.bias
-            return x + hg
-        return x + _linear(h, self.h2g.weight, self.h2g.bias)
+        if self.p == 0:
+            return x + _linear(h, self.h2g.weight, self.h2g.bias)
+        Wi, U = self.i2g.weight, self.h2g.weight
+        if not self.train:
+            return _linear(x, Wi, self.i2g.bias) + _linear(h, U, self.h2g.bias)
+        keep = 1.0 - self.p
+
+        def gated(v, W):
+            m = torch.stack([torch.bernoulli(torch.full_like(v, keep)) / keep for _ in range(4)])
+            out = torch.bmm(v.unsqueeze(0) * m, W.view(4, H, -1).transpose(1, 2))      # [4, B, H]
+            return out.permute(1, 0, 2).reshape(v.shape[0], 4 * H)
+
+        return gated(x, Wi) + self.i2g.bias + gated(h, U) + self.h2g.bias
 
     def step(self, x, hid):
         h, c = hid
@@ -553,10 +687,30 @@ class LSTM(Cell):
         return (mask is None and self._fused_ok() and x2.is_cuda and x2.dim() == 3
                 and bool(ops.native.get().lstm_seq_supported(x2.shape[0], self.hiddenSize)))
 
+    def _grad_sink(self, m):
+        """m.gradWeight when a fused backward may accumulate into it directly (see _LSTMSeq.forward)."""
+        g = getattr(m, "gradWeight", None)
+        if (not self.train or m._frozen or getattr(m, "scaleW", 1.0) != 1.0 or g is None or not g.is_cuda
+                or g.dtype != torch.float32 or not g.is_contiguous()):
+            return None
+        return g
+
     def sequence(self, x2, hid, mask=None):
         if mask is None and self._fused_ok():
-            out, h, c = _LSTMSeq.apply(x2.contiguous(), hid[0], hid[1], self.h2g.weight)
+            out, h, c = _LSTMSeq.apply(x2.contiguous(), hid[0], hid[1], self.h2g.weight, self._grad_sink(self.h2g))
             return out, [h, c]
+        default_act = _is(self.activation, Tanh) and _is(self.innerActivation, Sigmoid)
+        if self.p != 0 and mask is None and default_act:
+            if self.train and _LSTMDropSeq.usable(x2, self.hiddenSize, self.inputSize):
+                out, h, c = _LSTMDropSeq.apply(x2, hid[0], hid[1], self.i2g.weight, self.i2g.bias, self.h2g.weight,
+                                               self.h2g.bias, float(self.p))
+                return out, [h, c]
+            if not self.train and x2.is_cuda:
+                # evaluation: dropout is the identity -> one input GEMM with both biases, then the fused recurrence
+                B, T = x2.shape[:2]
+                xg = _linear(x2.reshape(B * T, -1), self.i2g.weight, self.i2g.bias + self.h2g.bias)
+                out, h, c = _LSTMSeq.apply(xg.reshape(B, T, -1).contiguous(), hid[0], hid[1], self.h2g.weight)
+                return out, [h, c]
         return super().sequence(x2, hid, mask)
 
 
@@ -855,8 +1009,10 @@ class Recurrent(Container):
             self._gbn = g
             g = self.bn.updateGradInput(pre.output, g)
         self._gpre = g
-        gi = pre.updateGradInput(self._flat, g)
-        return gi.reshape(input.shape).to(input.dtype)
+        gi = pre.updateGradInput(self._flat, g).reshape(input.shape)
+        if gi.dtype == torch.bfloat16 and input.dtype == torch.float32 and gi.is_cuda:
+            return ops.to_f32(gi)           # native cast (bf16 projection gradient -> fp32 embedding gradient)
+        return gi.to(input.dtype)
 
     def accGradParameters(self, input, gradOutput):
         if getattr(self, "_pending", None) is not None:

@@ -240,15 +240,25 @@ void pair_wgrad_add(const Tensor& dwp, const Tensor& gw, double scale) {
   const long st[4] = {(long)gw.stride(0), (long)gw.stride(1), (long)gw.stride(2), (long)gw.stride(3)};
   bigdl_pair_wgrad_add(cf(dwp, "dwp"), mf(gw, "gw"), K, C, R, S, st, (float)scale, stream());
 }
+// Strided views are accepted as long as each row is contiguous (stride(2) == 1): batch / row strides are passed
+// through (the LSTM dropout path writes gate GEMMs straight into a [T][B][4H] buffer viewed as [4][B][H]).
+static void bmm_operand(const Tensor& t, const char* n, at::ScalarType ty) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == ty, "bmm_nt: ", n, " has the wrong dtype / device");
+  TORCH_CHECK(t.stride(2) == 1 && t.stride(1) >= t.size(2) && t.stride(0) >= 0, "bmm_nt: ", n, " rows must be dense");
+  const int64_t last = (t.size(0) - 1) * t.stride(0) + (t.size(1) - 1) * t.stride(1) + t.size(2);
+  TORCH_CHECK((int64_t)(t.storage().nbytes() / t.element_size()) - t.storage_offset() >= last, "bmm_nt: ", n,
+              " view exceeds its storage");
+}
 void bmm_nt(const Tensor& a, const Tensor& b, const Tensor& c, double alpha, bool accum) {
   TORCH_CHECK(a.dim() == 3 && b.dim() == 3 && c.dim() == 3, "bmm_nt: [batch, rows, K] operands, [batch, M, N] out");
-  TORCH_CHECK(a.is_contiguous() && b.is_contiguous() && c.is_contiguous(), "bmm_nt: contiguous operands");
+  bmm_operand(a, "a", at::kBFloat16); bmm_operand(b, "b", at::kBFloat16); bmm_operand(c, "c", at::kFloat);
   TORCH_CHECK(a.size(0) == b.size(0) && a.size(0) == c.size(0) && a.size(2) == b.size(2) && c.size(1) == a.size(1) &&
               c.size(2) == b.size(1), "bmm_nt: shapes");
   TORCH_CHECK(a.size(2) % 32 == 0, "bmm_nt: K must be padded to a multiple of 32");
-  const int rc = bigdl_bmm_nt(cbf(a, "a"), cbf(b, "b"), mf(c, "c"), a.size(0), a.size(1), b.size(1), a.size(2),
-                              a.stride(0), b.stride(0), c.stride(0), a.size(2), b.size(2), c.size(2), (float)alpha,
-                              accum ? 1 : 0, stream());
+  const int rc = bigdl_bmm_nt(reinterpret_cast<const uint16_t*>(a.data_ptr()),
+                              reinterpret_cast<const uint16_t*>(b.data_ptr()), c.data_ptr<float>(), a.size(0),
+                              a.size(1), b.size(1), a.size(2), a.stride(0), b.stride(0), c.stride(0), a.stride(1),
+                              b.stride(1), c.stride(1), (float)alpha, accum ? 1 : 0, stream());
   TORCH_CHECK(rc == 0, "bmm_nt: unsupported shape");
 }
 // ---- TensorMath backend (tensor_math.hip): operands are fp32 GPU tensors already broadcast to the output's
@@ -796,6 +806,55 @@ void lrn_bwd(const Tensor& x, const Tensor& y, const Tensor& scale, const Tensor
   bigdl_lrn_bwd(cf(x, "x"), cf(y, "y"), cf(scale, "scale"), cf(gy, "gy"), mf(gx, "gx"), x.size(0), x.size(1),
                 x.size(2) * x.size(3), size, alpha, beta, stream());
 }
+static int64_t view_room(const Tensor& t) {
+  return (int64_t)(t.storage().nbytes() / t.element_size()) - t.storage_offset();
+}
+// y[g][(t*B + b)*Kp + k] = x[b*xs_b + t*xs_t + k] * mask * mul (+ a ones column at k == K): lstm_drop.hip
+void lstm_drop_rep(const Tensor& x, int64_t xs_b, int64_t xs_t, const Tensor& y, int64_t ys_g, int64_t B, int64_t T,
+                   int64_t K, int64_t Kp, bool ones, double p, double mul, int64_t seed, int64_t off) {
+  TORCH_CHECK(x.is_cuda() && y.is_cuda() && y.scalar_type() == at::kBFloat16, "lstm_drop_rep: bf16 y on the GPU");
+  const bool bf = x.scalar_type() == at::kBFloat16;
+  TORCH_CHECK(bf || x.scalar_type() == at::kFloat, "lstm_drop_rep: x fp32 or bf16");
+  TORCH_CHECK(view_room(x) >= (B - 1) * xs_b + (T - 1) * xs_t + K, "lstm_drop_rep: x view too small");
+  TORCH_CHECK(view_room(y) >= 3 * ys_g + T * B * Kp && ys_g >= T * B * Kp, "lstm_drop_rep: y view too small");
+  const int rc = bigdl_lstm_drop_rep(x.data_ptr(), bf ? 1 : 0, xs_b, xs_t, reinterpret_cast<uint16_t*>(y.data_ptr()),
+                                     ys_g, (int)B, (int)T, (int)K, (int)Kp, ones ? 1 : 0, (float)p, (float)mul,
+                                     (unsigned long long)seed, (long long)off, stream());
+  TORCH_CHECK(rc == 0, "lstm_drop_rep: K and Kp must be multiples of 4 (Kp > K with the ones column)");
+}
+// dx[b*dxs_b + t*dxs_t + k] = add[...] + sum_g dy[g*dys_g + (t*B + b)*ldy + k] * mask * mul
+void lstm_drop_rep_bwd(const Tensor& dy, int64_t dys_g, int64_t ldy, const Tensor& dx, int64_t dxs_b, int64_t dxs_t,
+                       const OptT& add, int64_t as_b, int64_t as_t, int64_t B, int64_t T, int64_t K, double p,
+                       double mul, int64_t seed, int64_t off) {
+  TORCH_CHECK(dy.is_cuda() && dy.scalar_type() == at::kFloat && dx.scalar_type() == at::kFloat, "lstm_drop_rep_bwd: fp32");
+  TORCH_CHECK(view_room(dy) >= 3 * dys_g + (T * B - 1) * ldy + K, "lstm_drop_rep_bwd: dy view too small");
+  TORCH_CHECK(view_room(dx) >= (B - 1) * dxs_b + (T - 1) * dxs_t + K, "lstm_drop_rep_bwd: dx view too small");
+  const float* ap = nullptr;
+  if (add && add->defined()) {
+    TORCH_CHECK(add->scalar_type() == at::kFloat && view_room(*add) >= (B - 1) * as_b + (T - 1) * as_t + K,
+                "lstm_drop_rep_bwd: addend");
+    ap = add->data_ptr<float>();
+  }
+  const int rc = bigdl_lstm_drop_rep_bwd(dy.data_ptr<float>(), dys_g, (int)ldy, dx.data_ptr<float>(), dxs_b, dxs_t,
+                                         ap, as_b, as_t, (int)B, (int)T, (int)K, (float)p, (float)mul,
+                                         (unsigned long long)seed, (long long)off, stream());
+  TORCH_CHECK(rc == 0, "lstm_drop_rep_bwd: K must be a multiple of 4");
+}
+// gate-blocked bf16 weights: out [4][H][Kp] (bias column b1 + b2 at k == Kin), outT [4][Kin][H]
+void lstm_pack_gate_w(const Tensor& W, const OptT& b1, const OptT& b2, int64_t H, int64_t Kin, int64_t Kp,
+                      const OptT& out, const OptT& outT) {
+  contig(W, "W");
+  TORCH_CHECK(W.scalar_type() == at::kFloat && W.numel() == 4 * H * Kin, "lstm_pack_gate_w: W [4H, Kin] fp32");
+  if (b1 && b1->defined()) TORCH_CHECK(b1->numel() == 4 * H && b1->is_contiguous(), "lstm_pack_gate_w: b1");
+  if (b2 && b2->defined()) TORCH_CHECK(b2->numel() == 4 * H && b2->is_contiguous(), "lstm_pack_gate_w: b2");
+  if (out && out->defined()) TORCH_CHECK(out->numel() == 4 * H * Kp && out->is_contiguous(), "lstm_pack_gate_w: out");
+  if (outT && outT->defined())
+    TORCH_CHECK(outT->numel() == 4 * H * Kin && outT->is_contiguous(), "lstm_pack_gate_w: outT");
+  bigdl_lstm_pack_gate_w(cf(W, "W"), ocf(b1, "b1"), ocf(b2, "b2"), (int)H, (int)Kin, (int)Kp,
+                         (out && out->defined()) ? reinterpret_cast<uint16_t*>(out->data_ptr()) : nullptr,
+                         (outT && outT->defined()) ? reinterpret_cast<uint16_t*>(outT->data_ptr()) : nullptr,
+                         stream());
+}
 void dropout(const Tensor& x, const Tensor& y, double p, double mul, int64_t seed) {
   contig(x, "x"); contig(y, "y");
   TORCH_CHECK(x.numel() == y.numel() && x.scalar_type() == y.scalar_type(), "dropout: x/y mismatch");
@@ -1223,6 +1282,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("lrn_fwd", &lrn_fwd);
   m.def("lrn_bwd", &lrn_bwd);
   m.def("dropout", &dropout);
+  m.def("lstm_drop_rep", &lstm_drop_rep);
+  m.def("lstm_drop_rep_bwd", &lstm_drop_rep_bwd);
+  m.def("lstm_pack_gate_w", &lstm_pack_gate_w);
   m.def("embedding_fwd", &embedding_fwd);
   m.def("embedding_bwd", &embedding_bwd);
   m.def("embedding_fwd_ids", &embedding_fwd_ids);

@@ -192,6 +192,14 @@ void bigdl_set_conv_s1(int v);
 void bigdl_set_conv_sk(int v);
 // 3x3 / stride 1 / pad 1 weight gradient from halo tiles (wgrad_halo.hip): plan returns its splits (0 = n/a)
 void bigdl_set_wgrad_halo(int v);
+// LSTM with per-gate dropout masks (lstm_drop.hip)
+int bigdl_lstm_drop_rep(const void* x, int x_bf16, long xs_b, long xs_t, uint16_t* y, long ys_g, int B, int T, int K,
+                        int Kp, int ones, float p, float mul, unsigned long long seed, long long off, hipStream_t st);
+int bigdl_lstm_drop_rep_bwd(const float* dy, long dys_g, int ldy, float* dx, long dxs_b, long dxs_t, const float* add,
+                            long as_b, long as_t, int B, int T, int K, float p, float mul, unsigned long long seed,
+                            long long off, hipStream_t st);
+void bigdl_lstm_pack_gate_w(const float* W, const float* b1, const float* b2, int H, int Kin, int Kp, uint16_t* out,
+                            uint16_t* outT, hipStream_t st);
 int bigdl_wgrad_halo_plan(WgradArgs* a);
 int bigdl_wgrad_halo(const WgradArgs* a, hipStream_t st);
 void bigdl_set_i8_s1(int v);

@@ -185,3 +185,34 @@ def test_recurrent_serialization_roundtrip(tmp_path):
     b.saveModule(p, overWrite=True)
     b2 = Module.loadModule(p)
     assert torch.allclose(b.forward(x), b2.forward(x), atol=1e-6)
+
+
+def test_lstm_dropout_topology_and_eval_equivalence():
+    """p != 0 follows the reference's dropout topology (S/nn/LSTM.scala:76-129): no preTopology, stacked per-gate
+    input and hidden Linears, both with bias; in evaluation mode (dropout = identity) the output equals the plain
+    LSTM with the same weights and the two biases summed; in training the masks change the output and gradients flow
+    to every parameter."""
+    RNG.setSeed(3)
+    I, H, B, Tn = 6, 8, 3, 5
+    cell = nn.LSTM(I, H, p=0.3)
+    assert cell.preTopology is None and cell.i2g.weight.shape == (4 * H, I) and cell.h2g.bias.shape == (4 * H,)
+    rec = nn.Recurrent().add(cell)
+    x = torch.randn(B, Tn, I)
+    rec.evaluate()
+    y_eval = rec.forward(x).clone()
+    plain = nn.LSTM(I, H)
+    with torch.no_grad():
+        plain.preTopology.weight.copy_(cell.i2g.weight)
+        plain.preTopology.bias.copy_(cell.i2g.bias + cell.h2g.bias)
+        plain.h2g.weight.copy_(cell.h2g.weight)
+    ref = nn.Recurrent().add(plain)
+    ref.evaluate()
+    assert torch.allclose(y_eval, ref.forward(x), atol=1e-5)
+    rec.training()
+    y_train = rec.forward(x)
+    assert not torch.allclose(y_train, y_eval)
+    rec.zeroGradParameters()
+    gi = rec.backward(x, torch.ones_like(y_train))
+    assert gi.shape == x.shape and torch.isfinite(gi).all()
+    for w, g in zip(*rec.parameters()):
+        assert g.abs().sum() > 0, w.shape

@@ -337,3 +337,129 @@ def test_persistent_gru_sequence_matches_step_kernels(B, T, H):
         outs.append(h)
     ref = torch.stack(outs, 1)
     assert _rel(res[1][0], ref) < 1e-2
+
+
+def _philox_np(seed, ctr):
+    """Philox-4x32-10 (csrc/lstm_drop.hip philox4) over a numpy array of 64-bit counters -> 4 uint32 arrays."""
+    import numpy as np
+
+    M = np.uint64(0xFFFFFFFF)
+    ctr = ctr.astype(np.uint64)
+    c0, c1 = ctr & M, ctr >> np.uint64(32)
+    c2 = np.zeros_like(c0)
+    c3 = np.zeros_like(c0)
+    k0, k1 = np.uint64(seed & 0xFFFFFFFF), np.uint64((seed >> 32) & 0xFFFFFFFF)
+    for _ in range(10):
+        p0 = np.uint64(0xD2511F53) * c0
+        p1 = np.uint64(0xCD9E8D57) * c2
+        n0 = (p1 >> np.uint64(32)) ^ c1 ^ k0
+        n2 = (p0 >> np.uint64(32)) ^ c3 ^ k1
+        c1, c3, c0, c2 = p1 & M, p0 & M, n0 & M, n2 & M
+        k0, k1 = (k0 + np.uint64(0x9E3779B9)) & M, (k1 + np.uint64(0xBB67AE85)) & M
+    return c0, c1, c2, c3
+
+
+def _keep_mask(seed, ids, p):
+    import numpy as np
+
+    r = _philox_np(seed, ids >> 2)
+    sel = np.choose((ids & 3).astype(np.int64), r)
+    return ((sel >> np.uint64(8)).astype(np.float64) / 16777216.0) >= p
+
+
+@pytest.mark.parametrize("B,T,I,H,p", [(5, 4, 12, 32, 0.3), (16, 6, 40, 64, 0.5)])
+def test_native_lstm_dropout_matches_masked_fp32_reference(B, T, I, H, p):
+    """The native p != 0 LSTM (csrc/lstm_drop.hip + bmm_nt + the fused cell) against an fp32 torch LSTM that applies
+    the SAME per-gate masks, regenerated here from the kernel's Philox counters: output, final state and the
+    gradients of input, initial state and all four parameter tensors."""
+    import numpy as np
+
+    from bigdl_amd.nn import recurrent as rc
+    from bigdl_amd.ops import nnk
+
+    torch.manual_seed(0)
+    dev = "cuda"
+    x = torch.randn(B, T, I, device=dev)
+    h0 = torch.randn(B, H, device=dev) * 0.5
+    c0 = torch.randn(B, H, device=dev) * 0.5
+    Wi = torch.randn(4 * H, I, device=dev) / I ** 0.5
+    bi = torch.randn(4 * H, device=dev) * 0.1
+    U = torch.randn(4 * H, H, device=dev) / H ** 0.5
+    bu = torch.randn(4 * H, device=dev) * 0.1
+    seeds = []
+    orig = nnk.next_seed
+
+    def rec_seed():
+        s = orig()
+        seeds.append(s)
+        return s
+
+    nnk.next_seed = rec_seed
+    try:
+        leaves = [t.clone().requires_grad_(True) for t in (x, h0, c0, Wi, bi, U, bu)]
+        out, hT, cT = rc._LSTMDropSeq.apply(*leaves, p)
+        go = torch.randn_like(out)
+        gh = torch.randn_like(hT)
+        (out * go).sum().backward(retain_graph=True)
+    finally:
+        nnk.next_seed = orig
+    sx, sh = seeds
+    keep = 1.0 - p
+    # masks: x -> id ((g*T + t)*B + b)*I + k; h at step t -> ((g*B + b)*H + k) + t*4*B*H
+    g_, t_, b_, k_ = np.meshgrid(np.arange(4), np.arange(T), np.arange(B), np.arange(I), indexing="ij")
+    mx = _keep_mask(sx, ((g_ * T + t_) * B + b_) * I + k_, p)                         # [4, T, B, I]
+    g2, b2, k2 = np.meshgrid(np.arange(4), np.arange(B), np.arange(H), indexing="ij")
+    mh = np.stack([_keep_mask(sh, (g2 * B + b2) * H + k2 + t * 4 * B * H, p) for t in range(T)])   # [T, 4, B, H]
+    mx = torch.as_tensor(mx, dtype=torch.float32, device=dev) / keep
+    mh = torch.as_tensor(mh, dtype=torch.float32, device=dev) / keep
+    refl = [t.clone().requires_grad_(True) for t in (x, h0, c0, Wi, bi, U, bu)]
+    xr, hr, cr, Wr, bir, Ur, bur = refl
+    outs = []
+    h, c = hr, cr
+    for t in range(T):
+        gx = torch.einsum("gbi,ghi->bgh", xr[:, t].unsqueeze(0) * mx[:, t], Wr.view(4, H, I)).reshape(B, 4 * H)
+        gh_ = torch.einsum("gbk,ghk->bgh", h.unsqueeze(0) * mh[t], Ur.view(4, H, H)).reshape(B, 4 * H)
+        g = gx + bir + gh_ + bur
+        i, gg, f, o = (torch.sigmoid(g[:, :H]), torch.tanh(g[:, H:2 * H]), torch.sigmoid(g[:, 2 * H:3 * H]),
+                       torch.sigmoid(g[:, 3 * H:]))
+        c = f * c + i * gg
+        h = o * torch.tanh(c)
+        outs.append(h)
+    outr = torch.stack(outs, 1)
+    (outr * go).sum().backward()
+    assert _rel(out, outr) < 2e-2, _rel(out, outr)
+    assert _rel(hT, h) < 2e-2 and _rel(cT, c) < 2e-2
+    for a, r, name in zip(leaves, refl, ["x", "h0", "c0", "Wi", "bi", "U", "bu"]):
+        assert a.grad is not None, name
+        assert _rel(a.grad, r.grad) < 3e-2, (name, _rel(a.grad, r.grad))
+
+
+def test_lstm_dropout_module_runs_native_path_on_gpu():
+    """nn.LSTM(p != 0) inside Recurrent on the GPU takes the native dropout path in training (no per-step aten
+    bernoulli / bmm), and evaluation matches the CPU engine."""
+    from bigdl_amd import nn
+    from bigdl_amd.nn import recurrent as rc
+    from bigdl_amd.utils.random_generator import RNG
+
+    RNG.setSeed(7)
+    cpu = nn.Recurrent().add(nn.LSTM(16, 64, p=0.25))
+    gpu = copy.deepcopy(cpu).to("cuda")
+    x = torch.randn(8, 5, 16)
+    calls = []
+    orig = rc._LSTMDropSeq.forward
+
+    def spy(ctx, *a):
+        calls.append(1)
+        return orig(ctx, *a)
+
+    rc._LSTMDropSeq.forward = staticmethod(spy)
+    try:
+        gpu.training()
+        y = gpu.forward(x.cuda())
+        gpu.backward(x.cuda(), torch.ones_like(y))
+    finally:
+        rc._LSTMDropSeq.forward = staticmethod(orig)
+    assert calls, "native dropout LSTM path not taken"
+    cpu.evaluate()
+    gpu.evaluate()
+    assert _rel(gpu.forward(x.cuda()), cpu.forward(x)) < 1e-2
