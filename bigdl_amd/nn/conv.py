@@ -268,7 +268,8 @@ class SpatialConvolution(TensorModule):
             once = getattr(self, "_dgrad_bn_once", False)
             self._dgrad_bn_once = False
             bn_src = getattr(input, "_bn_bwd", None) if (getattr(self, "_dgrad_bn_ok", False) or once) else None
-            if bn_src is not None:          # flag -> the BN's post-ReLU output, which is this conv's input
+            if bn_src is not None and not torch.is_tensor(bn_src[4]):
+                # flag -> the BN's post-ReLU output, which is this conv's input (a tensor there is its sign mask)
                 bn_src = bn_src[:4] + ((input if bn_src[4] else None),)
             gi = self._dgrad_gpu(x, gy, ph, pw, None if (squeeze or eh or ew or self.format != "NCHW") else bn_src)
         else:
@@ -311,7 +312,11 @@ class SpatialConvolution(TensorModule):
             if bn_src is not None and Cp == x.shape[1]:
                 # the input is a training BN's output: reduce that BN's backward statistics in our epilogue
                 bnmod, bx, bmean, baff, bz = bn_src
-                bn = {"x": bx, "z": bz, "mean": bmean, "aff": baff, "red": bnops.new_stats(Cp, gy16.device)}
+                bzm = None
+                if bz is not None and bz.dtype == torch.uint8:
+                    bz, bzm = None, bz
+                bn = {"x": bx, "z": bz, "zm": bzm, "mean": bmean, "aff": baff,
+                      "red": bnops.new_stats(Cp, gy16.device)}
             gi = cv.conv2d_dgrad(gy16, wt, xs, (self.strideH, self.strideW), (ph, pw),
                                  (self.dilationH, self.dilationW), addend=addend, bn=bn)
             if Cp != x.shape[1]:

@@ -11,6 +11,7 @@ ReLU of a ResNet block are fused into the apply pass (flags set by nn.fusion), a
 packed [sum, sumsq] / [sum dy, sum dy*xhat] buffers between the reduce and apply phases.
 """
 import math
+import os
 
 import torch
 import torch.nn.functional as F
@@ -20,6 +21,7 @@ from ..ops import bn as bnops
 from .abstractnn import AutogradModule, TensorModule
 from .init_methods import Ones, RandomUniform, Zeros
 
+_ZMASK = os.environ.get("BIGDL_BN_ZMASK", "1") != "0"
 CL = torch.channels_last
 BF16 = torch.bfloat16
 
@@ -110,19 +112,27 @@ class BatchNormalization(TensorModule):
             res = residual
             if res is not None and (res.dtype != BF16 or res.stride() != x.stride()):
                 res = res.to(BF16).contiguous(memory_format=CL if x.dim() == 4 else torch.contiguous_format)
+            # with a residual the ReLU mask is not a function of x: the apply pass stores it as one sign bit per
+            # element, which the backward reads instead of the output itself (BIGDL_BN_ZMASK=0: read the output)
+            zm = None
+            if self.train and self.fuse_relu and res is not None and x.shape[1] % 8 == 0 and _ZMASK:
+                zm = torch.empty(x.numel() // 8, dtype=torch.uint8, device=x.device)
             y, sm, si, aff = bnops.bn_forward_gpu(x, self.weight, self.bias, self.runningMean, self.runningVar,
                                                    self.eps, self.momentum, self.train, stats=stats, res=res,
-                                                   relu=self.fuse_relu, sync_fn=self.sync_fn if self.train else None)
+                                                   relu=self.fuse_relu, sync_fn=self.sync_fn if self.train else None,
+                                                   zm=zm)
             self.saveMean, self.saveStd = sm, si
             # without a residual the ReLU mask is a function of x: backward recomputes it from (scale, shift)
             self._aff = aff if (self.fuse_relu and res is None) else None
+            self._zm = zm
             self._xin = x
             if self.train and self.fuse_relu:
                 # lets a consuming conv reduce this BN's backward statistics in its dgrad epilogue (nn.fusion)
                 # (no reference to y itself: y -> _bn_bwd -> y was a reference cycle that kept every such output alive
                 # until a GC pass, growing the caching allocator by ~5 GB per ResNet-50 step; the consuming conv's
                 # input IS y, so it supplies the post-ReLU tensor itself)
-                y._bn_bwd = (self, x, sm, self._aff, res is not None)
+                # last element: the sign mask, else whether the ReLU mask must come from y (a residual add)
+                y._bn_bwd = (self, x, sm, self._aff, zm if zm is not None else res is not None)
             return self._from_nchw(y)
         xf = x.float()
         y, mean, invstd = bnops.bn_forward_cpu(xf, self.weight, self.bias, self.runningMean, self.runningVar, self.eps,
@@ -146,7 +156,8 @@ class BatchNormalization(TensorModule):
         if gz.dtype != BF16 or gz.stride() != x.stride():
             gz = gz.to(BF16).contiguous(memory_format=CL if x.dim() == 4 else torch.contiguous_format)
         aff = getattr(self, "_aff", None)
-        z = self._to_nchw(self.output) if (self.fuse_relu and aff is None) else None
+        zm = getattr(self, "_zm", None)
+        z = self._to_nchw(self.output) if (self.fuse_relu and aff is None and zm is None) else None
         direct = self._direct_grads()
         dg = self.gradWeight if direct else (torch.zeros_like(self.runningMean) if self.affine else None)
         db = self.gradBias if direct else (torch.zeros_like(self.runningMean) if self.affine else None)
@@ -155,7 +166,7 @@ class BatchNormalization(TensorModule):
         graph_res = getattr(self, "_graph_dres", False)
         dx, dres = bnops.bn_backward_gpu(gz, z, x, self.saveMean, self.saveStd, self.weight, dg, db,
                                          training=self.train, need_dres=need_dres or graph_res,
-                                         sync_fn=self.sync_fn if self.train else None, aff=aff, red=red)
+                                         sync_fn=self.sync_fn if self.train else None, aff=aff, red=red, zm=zm)
         if graph_res:
             self._dres = dres
         if not direct and self.affine and not self._frozen:

@@ -69,9 +69,11 @@ def _reduce_slots_for_sync(buf, C, P, sync_fn):
 
 
 def bn_forward_gpu(x, gamma, beta, rmean, rvar, eps, momentum, training, stats=None, res=None, relu=False,
-                   out=None, sync_fn=None):
+                   out=None, sync_fn=None, zm=None):
     """Returns (y, save_mean, save_invstd, aff) with aff = [scale | shift] of the apply pass (fp32 [2C]).
 
+    ``zm`` (optional, uint8 [P * C / 8]) receives the sign mask of y (bit e of byte (p, g): y[p][8g + e] > 0), which
+    the backward passes read in place of y itself (csrc/batchnorm.hip: 1/16 of the bytes).
     x: (N, C, H, W) bf16 channels_last (or (N, C) bf16 contiguous). ``stats`` may hold the slotted
     (sum, sumsq) already produced by the preceding conv epilogue; otherwise they are computed here.
     ``sync_fn(buf[2C], count) -> total count`` (sync-BN) all-reduces the statistics across replicas.
@@ -98,18 +100,19 @@ def bn_forward_gpu(x, gamma, beta, rmean, rvar, eps, momentum, training, stats=N
         stats, nslots = scale, 0  # unused in inference mode
     C_.bn_finalize(stats, nslots, gamma, beta, rmean, rvar, smean, sinv, scale, shift, Ptot, C, float(eps),
                    float(momentum), bool(training))
-    C_.bn_apply(x, scale, shift, res, out, P, C, bool(relu))
+    C_.bn_apply(x, scale, shift, res, out, P, C, bool(relu), zm)
     return out, smean, sinv, aff
 
 
 def bn_backward_gpu(dz, z, x, smean, sinv, gamma, dgamma, dbeta, training=True, need_dres=False, need_dx=True,
-                    sync_fn=None, aff=None, red=None):
+                    sync_fn=None, aff=None, red=None, zm=None):
     """Backward of y = relu?(bn(x) [+ res]).
 
     dz: gradient w.r.t. the (post-relu) output; z: the forward output (ReLU mask) or None. With z None and
     ``aff`` (the forward's [scale | shift]) the ReLU mask is recomputed from x, so z is never read back.
     Returns (dx, dres) — dres is the gradient flowing into the residual branch (= masked dz).
     ``red``: the slotted backward reduction already accumulated by the producer of dz (a dgrad epilogue).
+    ``zm``: the forward's sign mask of the output (bn_forward_gpu), used in place of z.
     """
     C = x.shape[1]
     P = _P(x)
@@ -119,7 +122,7 @@ def bn_backward_gpu(dz, z, x, smean, sinv, gamma, dgamma, dbeta, training=True, 
         red = None
     elif red is None:
         red = new_stats(C, x.device)
-        C_.bn_bwd_reduce(dz, z, x, smean, red, P, C, aff)
+        C_.bn_bwd_reduce(dz, z, x, smean, red, P, C, aff, zm)
     if training:
         nslots = stat_slots()
         if sync_fn is not None:
@@ -127,7 +130,7 @@ def bn_backward_gpu(dz, z, x, smean, sinv, gamma, dgamma, dbeta, training=True, 
     coef = torch.empty(3 * C, dtype=torch.float32, device=x.device)
     dx = torch.empty_like(x) if need_dx else None
     dres = torch.empty_like(x) if need_dres else None
-    C_.bn_bwd_apply(dz, z, x, smean, sinv, gamma, red, nslots, coef, dx, dres, dgamma, dbeta, Ptot, C, aff)
+    C_.bn_bwd_apply(dz, z, x, smean, sinv, gamma, red, nslots, coef, dx, dres, dgamma, dbeta, Ptot, C, aff, zm)
     return dx, dres
 
 

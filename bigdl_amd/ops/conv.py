@@ -163,8 +163,8 @@ def conv2d_dgrad(dy, w16t, x_shape, stride, pad, dil=(1, 1), out=None, addend=No
     ``addend`` (same shape/layout as dx) is summed in the GEMM epilogue — used to fold the residual
     branch gradient of a ResNet block into the block-input gradient.
 
-    ``bn`` = {"x", "z", "mean", "aff", "red"}: dx is the gradient of a training BatchNorm's (ReLU-fused)
-    output, and the epilogue also accumulates that BN's backward reduction into ``red`` (the pass
+    ``bn`` = {"x", "z", "mean", "aff", "red"[, "zm"]}: dx is the gradient of a training BatchNorm's (ReLU-fused)
+    output (ReLU mask from z, or its sign mask zm, or x * aff), and the epilogue also accumulates that BN's backward reduction into ``red`` (the pass
     bn_bwd_reduce would make over dx and x). Only when every pixel of dx is written by a GEMM phase (or the
     uncovered pixels are zero); ``bn["done"]`` reports whether it ran.
     """
@@ -194,7 +194,8 @@ def conv2d_dgrad(dy, w16t, x_shape, stride, pad, dil=(1, 1), out=None, addend=No
     bnk = {}
     if bn is not None and (covered == H * W or addend is None) and bn["x"].shape == out.shape \
             and bn["x"].stride() == out.stride() and not native.deterministic():
-        bnk = dict(bn_x=bn["x"], bn_z=bn["z"], bn_mean=bn["mean"], bn_aff=bn["aff"], bn_red=bn["red"])
+        bnk = dict(bn_x=bn["x"], bn_z=bn["z"], bn_mean=bn["mean"], bn_aff=bn["aff"], bn_red=bn["red"],
+                   bn_zm=bn.get("zm"))
         bn["done"] = True
     for (a, b, nI, nJ, taps) in phases:
         geo = [N, OH, OW, K, nI, nJ, 1, 1, ldw, C, C, H, W, stride[0], stride[1], a, b]

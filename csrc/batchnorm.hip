@@ -27,7 +27,7 @@ template <int MODE, int U>
 __global__ __launch_bounds__(256) void chan_reduce_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dz,
                                                           const bf16_t* __restrict__ z, const float* __restrict__ mean,
                                                           float* __restrict__ out, long P, int C, long rows_per_block,
-                                                          const float* __restrict__ aff) {
+                                                          const float* __restrict__ aff, const uint8_t* __restrict__ zm) {
   __shared__ float sm[256 * 16];
   const int G = C >> 3;
   const int tid = threadIdx.x;
@@ -40,7 +40,7 @@ __global__ __launch_bounds__(256) void chan_reduce_kernel(const bf16_t* __restri
     float a1[8], a2[8], mu[8], sc[8], sh[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) { a1[e] = 0.f; a2[e] = 0.f; mu[e] = 0.f; sc[e] = 0.f; sh[e] = 0.f; }
-    const bool xmask = MODE == 1 && z == nullptr && aff != nullptr;
+    const bool xmask = MODE == 1 && z == nullptr && zm == nullptr && aff != nullptr;
     if (MODE == 1 && rsub < rpi) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) mu[e] = mean[g * 8 + e];
@@ -62,7 +62,8 @@ __global__ __launch_bounds__(256) void chan_reduce_kernel(const bf16_t* __restri
           vx[u] = *reinterpret_cast<const v4u*>(x + off);
           if (MODE == 1) {
             vd[u] = *reinterpret_cast<const v4u*>(dz + off);
-            if (z) vz[u] = *reinterpret_cast<const v4u*>(z + off);
+            if (zm) vz[u] = mask8_to_bf(zm[off >> 3]);
+            else if (z) vz[u] = *reinterpret_cast<const v4u*>(z + off);
           }
         }
 #pragma unroll
@@ -80,7 +81,7 @@ __global__ __launch_bounds__(256) void chan_reduce_kernel(const bf16_t* __restri
             for (int e = 0; e < 4; ++e) {
               float dl = ok ? lo_bf(vd[u][e]) : 0.f, dh = ok ? hi_bf(vd[u][e]) : 0.f;
               const float xl = lo_bf(vx[u][e]), xh = hi_bf(vx[u][e]);
-              if (z) { if (!(lo_bf(vz[u][e]) > 0.f)) dl = 0.f; if (!(hi_bf(vz[u][e]) > 0.f)) dh = 0.f; }
+              if (z || zm) { if (!(lo_bf(vz[u][e]) > 0.f)) dl = 0.f; if (!(hi_bf(vz[u][e]) > 0.f)) dh = 0.f; }
               if (xmask) {
                 if (!(xl * sc[2 * e] + sh[2 * e] > 0.f)) dl = 0.f;
                 if (!(xh * sc[2 * e + 1] + sh[2 * e + 1] > 0.f)) dh = 0.f;
@@ -177,7 +178,8 @@ __global__ void bn_finalize_kernel(const float* __restrict__ stats, int nslots, 
 template <int U>
 __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* __restrict__ x, const float* __restrict__ scale,
                                                        const float* __restrict__ shift, const bf16_t* __restrict__ res,
-                                                       bf16_t* __restrict__ y, long P, int C, long rpb, int relu) {
+                                                       bf16_t* __restrict__ y, long P, int C, long rpb, int relu,
+                                                       uint8_t* __restrict__ zm) {
   const int G = C >> 3;
   const int gbase = blockIdx.y * 256;
   const int gcount = min(256, G - gbase);
@@ -212,7 +214,10 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* __restrict_
         if (relu) { l = fmaxf(l, 0.f); h = fmaxf(h, 0.f); }
         o[e] = pack2bf(l, h);
       }
-      if (r < rend) reinterpret_cast<v4u*>(y)[r * G + g] = o;
+      if (r < rend) {
+        reinterpret_cast<v4u*>(y)[r * G + g] = o;
+        if (zm) zm[r * G + g] = (uint8_t)bf_to_mask8(o);   // 1 byte per 8 channels: the backward's ReLU mask
+      }
     }
   }
 }
@@ -259,9 +264,10 @@ template <int U>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16_t* __restrict__ dz, const bf16_t* __restrict__ z,
                                                            const bf16_t* __restrict__ x, const float* __restrict__ coef,
                                                            bf16_t* __restrict__ dx, bf16_t* __restrict__ dres, long P,
-                                                           int C, long rpb, const float* __restrict__ aff) {
+                                                           int C, long rpb, const float* __restrict__ aff,
+                                                           const uint8_t* __restrict__ zm) {
   const int G = C >> 3;
-  const bool xmask = z == nullptr && aff != nullptr;   // ReLU mask from x*scale + shift (see chan_reduce_kernel)
+  const bool xmask = z == nullptr && zm == nullptr && aff != nullptr;   // ReLU mask from x*scale + shift (see chan_reduce_kernel)
   const int gbase = blockIdx.y * 256;
   const int gcount = min(256, G - gbase);
   const int rpi = 256 / gcount;
@@ -285,7 +291,8 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16_t* __restr
       const long i = (r < rend ? r : rbeg) * G + g;
       vd[u] = reinterpret_cast<const v4u*>(dz)[i];
       vz[u] = v4u{0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
-      if (z) vz[u] = reinterpret_cast<const v4u*>(z)[i];
+      if (zm) vz[u] = mask8_to_bf(zm[i]);
+      else if (z) vz[u] = reinterpret_cast<const v4u*>(z)[i];
       vx[u] = reinterpret_cast<const v4u*>(x)[i];
     }
 #pragma unroll
@@ -296,7 +303,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16_t* __restr
       for (int e = 0; e < 4; ++e) {
         float d0 = lo_bf(vd[u][e]), d1 = hi_bf(vd[u][e]);
         const float x0 = lo_bf(vx[u][e]), x1 = hi_bf(vx[u][e]);
-        if (z) { if (!(lo_bf(vz[u][e]) > 0.f)) d0 = 0.f; if (!(hi_bf(vz[u][e]) > 0.f)) d1 = 0.f; }
+        if (z || zm) { if (!(lo_bf(vz[u][e]) > 0.f)) d0 = 0.f; if (!(hi_bf(vz[u][e]) > 0.f)) d1 = 0.f; }
         if (xmask) {
           if (!(x0 * S[2 * e] + T[2 * e] > 0.f)) d0 = 0.f;
           if (!(x1 * S[2 * e + 1] + T[2 * e + 1] > 0.f)) d1 = 0.f;
@@ -339,7 +346,7 @@ int grid_for(long work, int per_block, int cap) {
 }
 
 void launch_reduce(int mode, const bf16_t* x, const bf16_t* dz, const bf16_t* z, const float* mean, float* out, long P,
-                   int C, hipStream_t st, const float* aff = nullptr) {
+                   int C, hipStream_t st, const float* aff = nullptr, const uint8_t* zm = nullptr) {
   const int G = C >> 3;
   const int rpi = 256 / (G < 256 ? G : 256);
   long blocks = (P + rpi * 16 - 1) / (rpi * 16);   // >= 16 rows per thread
@@ -349,8 +356,8 @@ void launch_reduce(int mode, const bf16_t* x, const bf16_t* dz, const bf16_t* z,
   if (blocks < 1) blocks = 1;
   const long rpb = (P + blocks - 1) / blocks;
   blocks = (P + rpb - 1) / rpb;
-#define BN_RED(M, U) chan_reduce_kernel<M, U><<<(int)blocks, 256, 0, st>>>(x, dz, z, mean, out, P, C, rpb, aff)
-  if (mode == 0) aff = nullptr;
+#define BN_RED(M, U) chan_reduce_kernel<M, U><<<(int)blocks, 256, 0, st>>>(x, dz, z, mean, out, P, C, rpb, aff, zm)
+  if (mode == 0) { aff = nullptr; zm = nullptr; }
   switch (bn_unroll()) {
     case 1: if (mode == 0) BN_RED(0, 1); else BN_RED(1, 1); break;
     case 2: if (mode == 0) BN_RED(0, 2); else BN_RED(1, 2); break;
@@ -383,38 +390,38 @@ void bigdl_bn_slot_reduce(const float* in, int nslots, int C, float* out, hipStr
 }
 
 void bigdl_bn_apply(const uint16_t* x, const float* scale, const float* shift, const uint16_t* res, uint16_t* y,
-                    long P, int C, int relu, hipStream_t st) {
+                    long P, int C, int relu, hipStream_t st, uint8_t* zm) {
   long rpb = 0;
   const dim3 grid = stationary_grid(P, C, &rpb);
   switch (bn_unroll()) {
-    case 1: bn_apply_kernel<1><<<grid, 256, 0, st>>>(x, scale, shift, res, y, P, C, rpb, relu); break;
-    case 2: bn_apply_kernel<2><<<grid, 256, 0, st>>>(x, scale, shift, res, y, P, C, rpb, relu); break;
-    case 8: bn_apply_kernel<8><<<grid, 256, 0, st>>>(x, scale, shift, res, y, P, C, rpb, relu); break;
-    default: bn_apply_kernel<4><<<grid, 256, 0, st>>>(x, scale, shift, res, y, P, C, rpb, relu); break;
+    case 1: bn_apply_kernel<1><<<grid, 256, 0, st>>>(x, scale, shift, res, y, P, C, rpb, relu, zm); break;
+    case 2: bn_apply_kernel<2><<<grid, 256, 0, st>>>(x, scale, shift, res, y, P, C, rpb, relu, zm); break;
+    case 8: bn_apply_kernel<8><<<grid, 256, 0, st>>>(x, scale, shift, res, y, P, C, rpb, relu, zm); break;
+    default: bn_apply_kernel<4><<<grid, 256, 0, st>>>(x, scale, shift, res, y, P, C, rpb, relu, zm); break;
   }
   HIP_LAUNCH_CHECK();
 }
 
 void bigdl_bn_bwd_reduce(const uint16_t* dz, const uint16_t* z, const uint16_t* x, const float* mean, float* red,
-                         long P, int C, const float* aff, hipStream_t st) {
-  launch_reduce(1, x, dz, z, mean, red, P, C, st, aff);
+                         long P, int C, const float* aff, hipStream_t st, const uint8_t* zm) {
+  launch_reduce(1, x, dz, z, mean, red, P, C, st, aff, zm);
   HIP_LAUNCH_CHECK();
 }
 
 void bigdl_bn_bwd_apply(const uint16_t* dz, const uint16_t* z, const uint16_t* x, const float* mean,
                         const float* invstd, const float* gamma, const float* red, int nslots, float* coef,
                         uint16_t* dx, uint16_t* dres, float* dgamma, float* dbeta, long P, int C, int training,
-                        const float* aff, hipStream_t st) {
+                        const float* aff, hipStream_t st, const uint8_t* zm) {
   bn_bwd_coeff_kernel<<<(C + 7) / 8, 256, 0, st>>>(red, nslots, mean, invstd, gamma, coef, dgamma, dbeta, P, C,
                                                     training);
   if (dx || dres) {
     long rpb = 0;
     const dim3 grid = stationary_grid(P, C, &rpb);
     switch (bn_unroll()) {
-      case 1: bn_bwd_apply_kernel<1><<<grid, 256, 0, st>>>(dz, z, x, coef, dx, dres, P, C, rpb, aff); break;
-      case 2: bn_bwd_apply_kernel<2><<<grid, 256, 0, st>>>(dz, z, x, coef, dx, dres, P, C, rpb, aff); break;
-      case 8: bn_bwd_apply_kernel<8><<<grid, 256, 0, st>>>(dz, z, x, coef, dx, dres, P, C, rpb, aff); break;
-      default: bn_bwd_apply_kernel<4><<<grid, 256, 0, st>>>(dz, z, x, coef, dx, dres, P, C, rpb, aff); break;
+      case 1: bn_bwd_apply_kernel<1><<<grid, 256, 0, st>>>(dz, z, x, coef, dx, dres, P, C, rpb, aff, zm); break;
+      case 2: bn_bwd_apply_kernel<2><<<grid, 256, 0, st>>>(dz, z, x, coef, dx, dres, P, C, rpb, aff, zm); break;
+      case 8: bn_bwd_apply_kernel<8><<<grid, 256, 0, st>>>(dz, z, x, coef, dx, dres, P, C, rpb, aff, zm); break;
+      default: bn_bwd_apply_kernel<4><<<grid, 256, 0, st>>>(dz, z, x, coef, dx, dres, P, C, rpb, aff, zm); break;
     }
   }
   HIP_LAUNCH_CHECK();

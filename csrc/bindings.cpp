@@ -28,12 +28,20 @@ const uint16_t* ocbf(const OptT& t, const char* n) { return (t && t->defined()) 
 uint16_t* ombf(const OptT& t, const char* n) { return (t && t->defined()) ? mbf(*t, n) : nullptr; }
 const float* ocf(const OptT& t, const char* n) { return (t && t->defined()) ? cf(*t, n) : nullptr; }
 float* omf(const OptT& t, const char* n) { return (t && t->defined()) ? mf(*t, n) : nullptr; }
+// optional [P][C / 8] uint8 ReLU sign mask (bigdl_bn_apply zm)
+uint8_t* omzm(const OptT& t, int64_t P, int64_t C, const char* n) {
+  if (!(t && t->defined())) return nullptr;
+  check(*t, at::kByte, n);
+  TORCH_CHECK(t->is_contiguous() && t->numel() == P * (C / 8), n, ": sign mask must be a contiguous [P][C/8] uint8 tensor");
+  return (uint8_t*)t->data_ptr();
+}
 
 // geo = [Nb, Hs, Ws, Cs, OH, OW, mul_h, mul_w, ldw, Ncol, ldo, OHo, OWo, omul_h, omul_w, ooff_h, ooff_w]
 // taps = flat [tap_h0, tap_w0, tap_k0, tap_h1, ...]
 void conv_nt(const Tensor& src, const Tensor& wt, const Tensor& out, const OptT& bias, const OptT& stats,
              std::vector<int64_t> geo, std::vector<int64_t> taps, bool relu, const OptT& addend, const OptT& bn_x,
-             const OptT& bn_z, const OptT& bn_mean, const OptT& bn_aff, const OptT& bn_red, bool accumulate) {
+             const OptT& bn_z, const OptT& bn_mean, const OptT& bn_aff, const OptT& bn_red, bool accumulate,
+             const OptT& bn_zm) {
   TORCH_CHECK(geo.size() == 17 || geo.size() == 18, "conv_nt: bad geometry");
   if (stats && stats->defined())
     TORCH_CHECK(stats->numel() >= BIGDL_STAT_SLOTS * 2 * geo[9], "conv_nt: stats must hold STAT_SLOTS x 2Ncol");
@@ -48,6 +56,11 @@ void conv_nt(const Tensor& src, const Tensor& wt, const Tensor& out, const OptT&
   if (a.addend) TORCH_CHECK(addend->numel() == out.numel(), "conv_nt: addend must match out");
   a.bnx = ocbf(bn_x, "bn_x"); a.bnz = ocbf(bn_z, "bn_z"); a.bnmean = ocf(bn_mean, "bn_mean");
   a.bnaff = ocf(bn_aff, "bn_aff"); a.bnred = omf(bn_red, "bn_red");
+  a.bnzm = nullptr;
+  if (bn_zm && bn_zm->defined()) {
+    TORCH_CHECK(geo[10] == geo[9] && geo[9] % 8 == 0, "conv_nt: a sign-mask z needs a dense output (ldo == Ncol)");
+    a.bnzm = omzm(bn_zm, out.numel() / geo[9], geo[9], "bn_zm");
+  }
   if (a.bnred) {
     TORCH_CHECK(a.bnx && a.bnmean && bn_x->numel() == out.numel(), "conv_nt: bn_x must match out, bn_mean required");
     TORCH_CHECK(!a.bnz || bn_z->numel() == out.numel(), "conv_nt: bn_z must match out");
@@ -157,29 +170,30 @@ void bn_slot_reduce(const Tensor& in, int64_t nslots, int64_t C, const Tensor& o
   bigdl_bn_slot_reduce(cf(in, "in"), (int)nslots, (int)C, mf(out, "out"), stream());
 }
 void bn_apply(const Tensor& x, const Tensor& scale, const Tensor& shift, const OptT& res, const Tensor& y, int64_t P,
-              int64_t C, bool relu) {
+              int64_t C, bool relu, const OptT& zm) {
   TORCH_CHECK(C % 8 == 0 && x.numel() == P * C && y.numel() == P * C, "bn_apply: shape");
   bigdl_bn_apply(cbf(x, "x"), cf(scale, "scale"), cf(shift, "shift"), ocbf(res, "res"), mbf(y, "y"), P, (int)C,
-                 relu ? 1 : 0, stream());
+                 relu ? 1 : 0, stream(), omzm(zm, P, C, "zm"));
 }
 void bn_bwd_reduce(const Tensor& dz, const OptT& z, const Tensor& x, const Tensor& mean, const Tensor& red, int64_t P,
-                   int64_t C, const OptT& aff) {
+                   int64_t C, const OptT& aff, const OptT& zm) {
   TORCH_CHECK(C % 8 == 0 && x.numel() == P * C && dz.numel() == P * C, "bn_bwd_reduce: shape");
   TORCH_CHECK(red.numel() >= BIGDL_STAT_SLOTS * 2 * C, "bn_bwd_reduce: red must hold STAT_SLOTS x 2C");
   if (aff && aff->defined()) TORCH_CHECK(aff->numel() >= 2 * C && aff->is_contiguous(), "bn_bwd_reduce: aff is [2C]");
   bigdl_bn_bwd_reduce(cbf(dz, "dz"), ocbf(z, "z"), cbf(x, "x"), cf(mean, "mean"), mf(red, "red"), P, (int)C,
-                      ocf(aff, "aff"), stream());
+                      ocf(aff, "aff"), stream(), omzm(zm, P, C, "zm"));
 }
 void bn_bwd_apply(const Tensor& dz, const OptT& z, const Tensor& x, const Tensor& mean, const Tensor& invstd,
                   const OptT& gamma, const OptT& red, int64_t nslots, const Tensor& coef, const OptT& dx,
-                  const OptT& dres, const OptT& dgamma, const OptT& dbeta, int64_t P, int64_t C, const OptT& aff) {
+                  const OptT& dres, const OptT& dgamma, const OptT& dbeta, int64_t P, int64_t C, const OptT& aff,
+                  const OptT& zm) {
   TORCH_CHECK(coef.numel() >= 3 * C, "bn_bwd_apply: coef size");
   if (aff && aff->defined()) TORCH_CHECK(aff->numel() >= 2 * C && aff->is_contiguous(), "bn_bwd_apply: aff is [2C]");
   const bool training = red && red->defined();
   bigdl_bn_bwd_apply(cbf(dz, "dz"), ocbf(z, "z"), cbf(x, "x"), cf(mean, "mean"), cf(invstd, "invstd"),
                      ocf(gamma, "gamma"), ocf(red, "red"), (int)nslots, mf(coef, "coef"), ombf(dx, "dx"),
                      ombf(dres, "dres"), omf(dgamma, "dgamma"), omf(dbeta, "dbeta"), P, (int)C, training ? 1 : 0,
-                     ocf(aff, "aff"), stream());
+                     ocf(aff, "aff"), stream(), omzm(zm, P, C, "zm"));
 }
 
 void dgrad_fill(const Tensor& out, const OptT& addend, int64_t sh, int64_t sw, int64_t mask) {
@@ -495,7 +509,7 @@ void conv_i8(const Tensor& src, const Tensor& wt, const Tensor& out, const OptT&
   a.out = reinterpret_cast<uint16_t*>(out.data_ptr());
   a.bias = ocf(bias, "bias"); a.stats = nullptr; a.addend = nullptr; a.out32 = nullptr; a.accum32 = 0;
   a.ws = nullptr; a.ksplit = 0; a.pstride = 0;
-  a.bnx = nullptr; a.bnz = nullptr; a.bnmean = nullptr; a.bnaff = nullptr; a.bnred = nullptr;
+  a.bnx = nullptr; a.bnz = nullptr; a.bnzm = nullptr; a.bnmean = nullptr; a.bnaff = nullptr; a.bnred = nullptr;
   a.Nb = geo[0]; a.Hs = geo[1]; a.Ws = geo[2]; a.Cs = geo[3]; a.OH = geo[4]; a.OW = geo[5];
   a.mul_h = geo[6]; a.mul_w = geo[7]; a.ldw = geo[8]; a.Ncol = geo[9]; a.ldo = geo[10];
   a.OHo = geo[11]; a.OWo = geo[12]; a.omul_h = geo[13]; a.omul_w = geo[14]; a.ooff_h = geo[15]; a.ooff_w = geo[16];
@@ -1204,19 +1218,21 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_nt", &conv_nt, py::arg("src"), py::arg("wt"), py::arg("out"), py::arg("bias"), py::arg("stats"),
         py::arg("geo"), py::arg("taps"), py::arg("relu"), py::arg("addend") = py::none(), py::arg("bn_x") = py::none(),
         py::arg("bn_z") = py::none(), py::arg("bn_mean") = py::none(), py::arg("bn_aff") = py::none(),
-        py::arg("bn_red") = py::none(), py::arg("accumulate") = false);
+        py::arg("bn_red") = py::none(), py::arg("accumulate") = false, py::arg("bn_zm") = py::none());
   m.def("conv_wgrad", &conv_wgrad);
   m.def("transpose_krsc", &transpose_krsc);
   m.def("bn_stats", &bn_stats);
   m.def("bn_finalize", &bn_finalize);
-  m.def("bn_apply", &bn_apply);
+  m.def("bn_apply", &bn_apply, py::arg("x"), py::arg("scale"), py::arg("shift"), py::arg("res"), py::arg("y"),
+        py::arg("P"), py::arg("C"), py::arg("relu"), py::arg("zm") = py::none());
   m.def("bn_slot_reduce", &bn_slot_reduce);
   m.attr("STAT_SLOTS") = BIGDL_STAT_SLOTS;
   m.def("bn_bwd_reduce", &bn_bwd_reduce, py::arg("dz"), py::arg("z"), py::arg("x"), py::arg("mean"), py::arg("red"),
-        py::arg("P"), py::arg("C"), py::arg("aff") = py::none());
+        py::arg("P"), py::arg("C"), py::arg("aff") = py::none(), py::arg("zm") = py::none());
   m.def("bn_bwd_apply", &bn_bwd_apply, py::arg("dz"), py::arg("z"), py::arg("x"), py::arg("mean"), py::arg("invstd"),
         py::arg("gamma"), py::arg("red"), py::arg("nslots"), py::arg("coef"), py::arg("dx"), py::arg("dres"),
-        py::arg("dgamma"), py::arg("dbeta"), py::arg("P"), py::arg("C"), py::arg("aff") = py::none());
+        py::arg("dgamma"), py::arg("dbeta"), py::arg("P"), py::arg("C"), py::arg("aff") = py::none(),
+        py::arg("zm") = py::none());
   m.def("relu_fwd", &relu_fwd);
   m.def("dgrad_fill", &dgrad_fill);
   m.def("hog_cus", &hog_cus, "n one-wave workgroups holding a whole CU's LDS each, spinning `us` microseconds");
@@ -1326,6 +1342,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("dh0") = py::none());
   m.def("set_conv_impl", &bigdl_set_conv_impl);
   m.def("set_conv_s1", &bigdl_set_conv_s1);
+  m.def("set_conv_halo", &bigdl_set_conv_halo);
   m.def("set_conv_sk", &bigdl_set_conv_sk);
   m.def("set_wgrad_halo", &bigdl_set_wgrad_halo);
   m.def("set_deterministic", &bigdl_set_deterministic, "1: bitwise-reproducible reductions (no multi-writer float atomics)");

@@ -52,4 +52,20 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return base + (bid >> 3);
 }
 
+// One byte of a post-ReLU sign mask (bit e = channel e of an 8-channel group is > 0) as the 16-byte bf16 granule the
+// z-mask consumers compare against zero: 1.0 where the bit is set, 0 elsewhere (batchnorm.hip bn_apply writes it).
+__device__ __forceinline__ v4u mask8_to_bf(unsigned b) {
+  v4u r;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) r[e] = (((b >> (2 * e)) & 1u) ? 0x3f80u : 0u) | (((b >> (2 * e + 1)) & 1u) ? 0x3f800000u : 0u);
+  return r;
+}
+// sign-mask byte of 8 bf16 values (bit e: value e > 0)
+__device__ __forceinline__ unsigned bf_to_mask8(const v4u& o) {
+  unsigned b = 0;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) b |= ((lo_bf(o[e]) > 0.f) ? 1u : 0u) << (2 * e) | ((hi_bf(o[e]) > 0.f) ? 1u : 0u) << (2 * e + 1);
+  return b;
+}
+
 #define HIP_LAUNCH_CHECK() (void)hipGetLastError()

@@ -1,0 +1,333 @@
+// Forward / data-gradient 3x3, stride-1, pad-1 convolutions from halo tiles (gfx950).
+//
+// out[p][k] = sum over taps (dh, dw) in [-1, 1]^2 and channels c of x[p + (dh, dw)][c] * w[k][tap][c]
+// (reference: S/nn/SpatialConvolution.scala updateOutput / updateGradInput, the MKL-DNN forward and backward-data
+// primitives of S/nn/mkldnn/SpatialConvolution.scala:331-589). The data gradient of a 3x3 / stride-1 / pad-1
+// convolution is the same computation over dy with the (C, R, S, K) transposed weight and the taps flipped, which
+// conv2d_dgrad already describes through ConvArgs' tap table, so one kernel serves both passes.
+//
+// The im2col implicit-GEMM tiles (conv_igemm.hip conv_nt_g4 / p8) DMA one input granule per (pixel, tap): every
+// activation crosses the DMA engine 9 times, and a 128 x 128 tile brings in 64 FLOP per staged byte. ResNet-50's 3x3
+// layers ran at 4-6x their MFMA bound there (profiles/r4_resnet50_layer_roofline.txt). Here a workgroup stages a
+// halo tile of the input ONCE per 32-channel chunk and reads the 9 shifted windows out of LDS:
+//   * tile = NIMG segments of RB output rows (RB < H: one segment of an image; RB == H: NIMG whole images stacked
+//     with one shared zero row between them). Its rows are stored padded by one zero column on each side (WP = W + 2
+//     "virtual pixel" columns), behind one guard row, so output virtual pixel v = (vr, j) reads tap (dh, dw) at tile
+//     row v + 1 + (1 + dh) * WP + dw: a constant shift per tap, no masks (the wgrad_halo.hip layout). Virtual pixels
+//     on the pad columns / separator rows compute garbage that the epilogue never stores.
+//   * x chunks (32 channels = one 64-byte row per tile row) are double-buffered and issued 9 K-steps ahead; the
+//     weights of one (chunk, tap) K-step (KT rows of 64 B) stream through an NSW-slot ring D = NSW - 1 steps ahead.
+//     Everything moves by LDS-DMA (buffer_load ... lds) with precomputed per-lane offsets; halo rows and columns
+//     outside the image are offsets past num_records, which the buffer unit returns as zeros.
+//   * 64-byte rows hold granule g of row r in slot g ^ (2 * ((r >> 2) & 1)): every ds_read_b128 fragment read (16
+//     consecutive rows, 4 granules) is conflict-free for ANY row offset, so one swizzle serves all 9 tap shifts, and
+//     fragment fm of a wave (16 rows further) has the same swizzle: one address per K-step + immediate offsets.
+//   * staged FLOP per byte: 256 virtual pixels x 64 channels (W = 56) or 224 x 128 (W <= 28) per K-step against one
+//     4 / 8 KB weight slice plus 1/9 of a chunk: 130-200, 2-3x the im2col tile.
+// 4 waves (WPX pixel groups x WCH channel groups), 2 workgroups per CU; the fused epilogue is nt_epilogue_lds
+// (conv_epilogue.h) with a virtual-pixel row map: BN statistics, the consumer-BN backward reduction, addend, ReLU.
+#include <algorithm>
+#include <cstdlib>
+#include <type_traits>
+#include <utility>
+
+#include "common.h"
+#include "kernels.h"
+#include "conv_epilogue.h"
+
+namespace {
+
+__device__ __forceinline__ int hswz(int r) { return ((r >> 2) & 1) << 1; }
+
+template <int W, int RB, int NIMG, int KT, int WPX>
+struct HaloF {
+  static constexpr int WP = W + 2;
+  static constexpr int VR = NIMG * (RB + 1) - 1;                 // virtual output rows
+  static constexpr int VM = 16 * WPX;                            // virtual pixels rounded to whole wave groups
+  static constexpr int V = (VR * WP + VM - 1) / VM * VM;         // virtual pixels per tile
+  static constexpr int HR = NIMG * (RB + 1) + 1;                 // halo rows (incl. top / bottom / separators)
+  static constexpr int XROWS = V + 2 * WP + 2;                   // tile rows any tap of any virtual pixel reads
+  static constexpr int XI = (XROWS + 63) / 64;                   // x DMA instructions per thread per chunk
+  static constexpr int XR = XI * 64;
+  static constexpr int XBYTES = XR * 64;
+  static constexpr int WI = KT / 64;                             // weight DMA instructions per thread per step
+  static constexpr int WBYTES = KT * 64;
+  static constexpr int NSW = 4, D = NSW - 1;
+  static constexpr int LDS = 2 * XBYTES + NSW * WBYTES;
+  static constexpr int WCH = 4 / WPX;
+  static constexpr int TM = V / WPX, TN = KT / WCH;
+  static constexpr int FM = TM / 16, FN = TN / 16;
+  static_assert(V % (16 * WPX) == 0 && KT % (16 * WCH) == 0 && KT % 64 == 0, "tile");
+  static_assert(2 * LDS <= 160 * 1024, "two workgroups per CU");
+};
+
+template <int N>
+__device__ __forceinline__ void vmw() {
+  static_assert(N >= 0 && N < 64, "vmcnt");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int OFF>
+__device__ __forceinline__ v8s ldsr(unsigned addr) {
+  static_assert(OFF >= 0 && OFF < 65536, "ds offset");
+  v8s r;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "n"(OFF));
+  return r;
+}
+
+template <class F, int... I>
+__device__ __forceinline__ void hfor_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void hfor(F&& f) {
+  hfor_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+// Virtual pixel -> output row (-1: pad column, separator row, tail, or an image past the batch)
+template <int W, int RB, int NIMG>
+struct HaloRowMap {
+  int n0, oh0, vend;
+  __device__ __forceinline__ long operator()(const ConvArgs& a, int v) const {
+    constexpr int WP = W + 2;
+    if (v >= vend) return -1;
+    const int vr = v / WP, j = v - vr * WP;
+    if (j < 1 || j > W) return -1;
+    const int b = vr / (RB + 1), i = vr - b * (RB + 1);
+    if (i == RB) return -1;                                   // separator row between stacked images
+    const int n = n0 + b;
+    if (n >= a.Nb) return -1;
+    return ((long)n * a.OH + oh0 + i) * a.OW + (j - 1);
+  }
+};
+
+template <int W, int RB, int NIMG, int KT, int WPX>
+__global__ __launch_bounds__(256, 2) void conv_halo_kernel(ConvArgs a) {
+  using H = HaloF<W, RB, NIMG, KT, WPX>;
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[H::LDS];
+  constexpr int WCH = H::WCH, FM = H::FM, FN = H::FN, WP = H::WP;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wpx = wave / WCH, wch = wave % WCH;
+  const int C = a.Cs, IH = a.Hs;
+  const int tiles_n = a.Ncol / KT;
+  const int segs = IH / RB;                                   // RB < H: segments per image; RB == H: 1
+  const int tiles_m = NIMG == 1 ? a.Nb * segs : (a.Nb + NIMG - 1) / NIMG;
+  const int nwg = tiles_m * tiles_n;
+  const int bid = xcd_remap(blockIdx.x, nwg);
+  const int tm = bid / tiles_n, tn = bid % tiles_n;
+  const int n0 = NIMG == 1 ? tm / segs : tm * NIMG;
+  const int oh0 = NIMG == 1 ? (tm - n0 * segs) * RB : 0;
+  const int k0 = tn * KT;
+  const int nch = C / 32, nk = nch * 9;
+
+  // ---- x DMA: instruction d of wave w fills tile rows (d * 4 + w) * 16 + lane / 4, slot lane & 3 (granule
+  // (lane & 3) ^ hswz(row)). Offsets (bytes) from the segment base pixel (n0, oh0 - 1, 0); variant bit 0 / 1 = the
+  // top / bottom halo row lies outside the image (RB < H only; RB == H separators are always zero).
+  constexpr unsigned OOB = 0x7ffffff0u;
+  // per instruction: its offset, and whether its row is the top / bottom halo row (for RB < H those are zeroed
+  // per tile by a uniform select when they fall outside the image; no per-variant copies)
+  unsigned xo[H::XI];
+  unsigned xtop = 0, xbot = 0;                                  // bit d: instruction d's row is the top / bottom halo
+#pragma unroll
+  for (int d = 0; d < H::XI; ++d) {
+    const int row = (d * 4 + wave) * 16 + (lane >> 2);
+    const int g = (lane & 3) ^ hswz(row);
+    const int t = row - 1;
+    const int hr = t >= 0 ? t / WP : -1, pc = t - hr * WP;
+    const int b = hr >= 0 ? hr / (RB + 1) : 0, i = hr - b * (RB + 1);   // i == 0: separator / top halo
+    const bool real = t >= 0 && hr < H::HR && pc >= 1 && pc <= W;
+    // source image row relative to the segment's first row - 1
+    const int srow = NIMG == 1 ? hr : (b * IH + i);
+    const bool sep = NIMG == 1 ? false : (i == 0);
+    xo[d] = (real && !sep) ? (unsigned)(((srow * W) + (pc - 1)) * C + g * 8) * 2u : OOB;
+    if (NIMG == 1 && hr == 0) xtop |= 1u << d;
+    if (NIMG == 1 && hr == RB + 1) xbot |= 1u << d;
+  }
+  // ---- weight DMA: instruction j of wave w fills rows (j * 4 + w) * 16 + lane / 4 of the KT x 64 B slice
+  unsigned wo[H::WI];
+#pragma unroll
+  for (int j = 0; j < H::WI; ++j) {
+    const int row = (j * 4 + wave) * 16 + (lane >> 2);
+    const int g = (lane & 3) ^ hswz(row);
+    wo[j] = (unsigned)((k0 + row) * a.ldw + g * 8) * 2u;
+  }
+  const bf16_t* xsrc = reinterpret_cast<const bf16_t*>(a.src);
+  const size_t xend = (size_t)a.Nb * IH * W * C;
+  // segment base: pixel (n0, oh0 - 1, 0) for RB < H (one image row above; wraps below 0 only when n0 = oh0 = 0, and
+  // every top-halo offset is OOB then), pixel (n0, -1, 0) for stacked whole images (row -1 is a separator: OOB)
+  const size_t xbase = ((size_t)n0 * IH + oh0) * W * C - (size_t)W * C;
+  const bool top_out = NIMG == 1 && oh0 == 0, bot_out = NIMG == 1 && oh0 + RB == IH;
+  if (top_out || bot_out) {
+#pragma unroll
+    for (int d = 0; d < H::XI; ++d)
+      if ((top_out && ((xtop >> d) & 1)) || (bot_out && ((xbot >> d) & 1))) xo[d] = OOB;
+  }
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16_t*>(reinterpret_cast<const bf16_t*>(a.wt)), (short)0,
+      (int)(((size_t)(a.Ncol - 1) * a.ldw + a.Kdim) * 2), 0x00020000);
+
+  auto issue_x = [&](int ch) {
+    const size_t xb = xbase + (size_t)ch * 32;
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<bf16_t*>(xsrc + xb), (short)0, (int)((xend - xb) * 2), 0x00020000);
+    unsigned char* X = lds + (ch & 1) * H::XBYTES;
+#pragma unroll
+    for (int d = 0; d < H::XI; ++d)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (LDS_PTR(void))(X + (d * 4 + wave) * 1024), 16, (int)xo[d], 0, 0, 0);
+  };
+  // tap tables in SGPRs (the K-loop runs the 9 taps as static iterations): LDS row shift and weight K offset
+  int tshift[9], twk[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    tshift[t] = __builtin_amdgcn_readfirstlane(1 + (1 + a.tap_h[t]) * WP + a.tap_w[t]);
+    twk[t] = __builtin_amdgcn_readfirstlane(a.tap_k[t] * C * 2);
+  }
+  auto issue_w = [&](int ch, int t, int slot) {
+    const int soff = twk[t] + ch * 64;
+    unsigned char* Wt = lds + 2 * H::XBYTES + slot * H::WBYTES;
+#pragma unroll
+    for (int j = 0; j < H::WI; ++j)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (LDS_PTR(void))(Wt + (j * 4 + wave) * 1024), 16, (int)wo[j],
+                                               soff, 0, 0);
+  };
+  auto issue_ws = [&](int s) {            // weight step s = 9 * chunk + tap (prologue: s < D, static)
+    const int ch = s / 9;
+    issue_w(ch, s - 9 * ch, s % H::NSW);
+  };
+
+  // ---- fragment read addresses: weight rows wch * TN + fn * 16 + (lane & 15), x rows v0 + shift + fm * 16
+  const unsigned lds_base = (unsigned)(uintptr_t)(LDS_PTR(unsigned char))lds;
+  const int gi = lane >> 4;
+  const int wrow = wch * H::TN + (lane & 15);
+  const unsigned wrd = (unsigned)(2 * H::XBYTES + wrow * 64 + ((gi ^ hswz(wrow)) << 4));
+  const int v0 = wpx * H::TM + (lane & 15);
+
+  v4f acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+
+  // prologue: chunk 0 and weight steps 0 .. D-1; retire step 0 (younger: steps 1 .. D-1)
+  issue_x(0);
+#pragma unroll
+  for (int s = 0; s < H::D; ++s)
+    if (s < nk) issue_ws(s);
+  if (nk > H::D - 1) vmw<(H::D - 1) * H::WI>();
+  else vmw<0>();
+  __builtin_amdgcn_s_barrier();
+
+  for (int ch = 0; ch < nch; ++ch) {
+    const unsigned xb = lds_base + (unsigned)((ch & 1) * H::XBYTES);
+    hfor<9>([&](auto tc) {
+      constexpr int t = decltype(tc)::value;
+      const int s = ch * 9 + t;
+      // slot (s + D) % NSW was read in step s - 1 (retired by the barrier that ended it); x buffer (ch + 1) & 1 was
+      // last read by chunk ch - 1
+      if (s + H::D < nk) {
+        constexpr int t2 = (t + H::D) % 9, dc = (t + H::D) / 9;
+        issue_w(ch + dc, t2, (s + H::D) % H::NSW);
+      }
+      if (t == 0 && ch + 1 < nch) issue_x(ch + 1);
+      const int r0 = v0 + tshift[t];
+      const unsigned xrd = xb + (unsigned)(r0 * 64 + ((gi ^ hswz(r0)) << 4));
+      const unsigned wrs = lds_base + wrd + (unsigned)((s % H::NSW) * H::WBYTES);
+      v8s fw[FN], fx[FM];
+      hfor<FN>([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        fw[j] = ldsr<j * 16 * 64>(wrs);
+      });
+      hfor<FM>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        fx[i] = ldsr<i * 16 * 64>(xrd);
+      });
+      // pixel fragment i's MFMAs start once it landed (the weight fragments were read first); the tie keeps every
+      // use of fx[i] behind its wait
+      hfor<FM>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(fx[i]) : "n"(FM - 1 - i));
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[j], fx[i], acc[i][j], 0, 0, 0);
+      });
+      __builtin_amdgcn_sched_barrier(0);
+      // retire step s + 1 for every wave: younger than W(s + 1) are W(s + 2 .. s + D) and the x chunk issued at this
+      // chunk's start when that start lies in [s + 1 - D, s] (it was issued after W(D) = W(s + 1) or later)
+      if (s + H::D < nk) {
+        if (t + 1 - H::D <= 0 && ch + 1 < nch) vmw<(H::D - 1) * H::WI + H::XI>();
+        else vmw<(H::D - 1) * H::WI>();
+      } else {
+        vmw<0>();
+      }
+      __builtin_amdgcn_s_barrier();
+    });
+  }
+
+  // epilogue: nt_epilogue_lds over the (now idle) LDS, one 16-row chunk of the wave tile at a time
+  constexpr int NH = FM;
+  constexpr int SL = (H::TM / NH) * H::TN;
+  static_assert(4 * SL * 4 <= H::LDS, "epilogue slices must fit the LDS");
+  float* wl = reinterpret_cast<float*>(lds) + wave * SL;
+  HaloRowMap<W, RB, NIMG> rm{n0, oh0, H::VR * WP};
+  nt_epilogue_lds<FM, FN, H::TM, H::TN, NH, 0, 2, HaloRowMap<W, RB, NIMG>>(a, acc, wpx * H::TM, k0 + wch * H::TN,
+                                                                           lane, bid, wl, 0, rm);
+}
+
+template <int W, int RB, int NIMG, int KT, int WPX>
+void launch_halo_f(const ConvArgs& a, hipStream_t st) {
+  const int segs = a.Hs / RB;
+  const int tiles_m = NIMG == 1 ? a.Nb * segs : (a.Nb + NIMG - 1) / NIMG;
+  const int nwg = tiles_m * (a.Ncol / KT);
+  conv_halo_kernel<W, RB, NIMG, KT, WPX><<<dim3(nwg), dim3(256), 0, st>>>(a);
+}
+
+int g_conv_halo = -1;
+
+}  // namespace
+
+extern "C" {
+
+void bigdl_set_conv_halo(int v) { g_conv_halo = v; }
+
+// 1 when bigdl_conv_halo takes this forward / data-gradient GEMM (BIGDL_CONV_HALO=0 turns it off)
+int bigdl_conv_halo_applies(const ConvArgs* a) {
+  if (g_conv_halo < 0) {
+    const char* e = getenv("BIGDL_CONV_HALO");
+    g_conv_halo = e ? atoi(e) : 1;
+  }
+  if (!g_conv_halo || a->ntaps != 9 || a->mul_h != 1 || a->mul_w != 1 || !a->ident_out || a->out32 || a->pstride ||
+      a->Hs != a->OH || a->Ws != a->OW || a->Hs != a->Ws || a->Kdim != 9 * a->Cs || (a->Cs % 32) ||
+      (a->ldo % 8) || (a->Ncol % 8) || a->ldw < a->Kdim || (a->ldw % 8))
+    return 0;
+  const int W = a->Ws;
+  const int kt = W == 56 ? 64 : 128;
+  if (W != 56 && W != 28 && W != 14 && W != 7) return 0;
+  if (a->Ncol % kt) return 0;
+  unsigned seen = 0;
+  for (int t = 0; t < 9; ++t) {
+    if (a->tap_h[t] < -1 || a->tap_h[t] > 1 || a->tap_w[t] < -1 || a->tap_w[t] > 1 || a->tap_k[t] < 0 ||
+        a->tap_k[t] > 8)
+      return 0;
+    seen |= 1u << ((a->tap_h[t] + 1) * 3 + a->tap_w[t] + 1);
+  }
+  if (seen != 0x1ffu) return 0;
+  if ((size_t)a->Nb * a->Hs * a->Ws * a->Cs * 2 >= (1ull << 31) - (1ull << 20)) return 0;   // 32-bit buffer offsets
+  if ((size_t)a->Ncol * a->ldw * 2 >= (1ull << 31)) return 0;
+  auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  return al(a->src) && al(a->wt) && al(a->out) && al(a->addend) && al(a->bnx) && al(a->bnz);
+}
+
+int bigdl_conv_halo(const ConvArgs* a, hipStream_t st) {
+  switch (a->Ws) {
+    case 56: launch_halo_f<56, 4, 1, 64, 4>(*a, st); break;
+    case 28: launch_halo_f<28, 7, 1, 128, 2>(*a, st); break;
+    case 14: launch_halo_f<14, 14, 1, 128, 2>(*a, st); break;
+    case 7: launch_halo_f<7, 7, 3, 128, 2>(*a, st); break;
+    default: return -1;
+  }
+  return 0;
+}
+
+}  // extern "C"

@@ -23,6 +23,8 @@
 #include "kernels.h"
 #include <stdlib.h>
 
+#include "conv_epilogue.h"
+
 
 namespace {
 
@@ -119,186 +121,7 @@ __device__ __forceinline__ void nt_epilogue(const ConvArgs& a, v4f (&acc)[MI][NI
   }
 }
 
-// Coalescing epilogue (Ncol % 8 == 0, ldo % 8 == 0): each wave parks its fp32 TM x TN tile in its own
-// slice of the (now idle) staging LDS — [pixel][channel], 16-byte granules XOR-swizzled by pixel so both
-// the 16-byte writes (lanes of 16 consecutive pixels) and the 2 x 16-byte reads (lanes along a pixel row)
-// are conflict-free — then re-reads it row-wise: a lane owns 8 channels of one pixel, so every store is
-// 16 B and one wave instruction writes 64/(TN/8) whole pixel rows of TN channels. bias / addend / ReLU /
-// BN statistics are applied in the row phase (the addend is read with the same 16-byte coalesced pattern).
-// PAIR > 0: the workgroup's two pixel-half waves (wm = 0 / 1) that share a channel range combine their BN
-// statistics through LDS (PAIR = float offset from the wm = 0 wave's slice to its partner's) and only the wm = 0
-// wave issues the atomics: half the atomic traffic into the statistics slots.
-template <int MI, int NI, int TM, int TN, int NH = 1, int PAIR = 0, int NWM = 2>
-__device__ __forceinline__ void nt_epilogue_lds(const ConvArgs& a, v4f (&acc)[MI][NI], int mbase, int nbase,
-                                                int lane, int bid, float* wl, int wm = 0) {
-  constexpr int GR = TN / 4;            // 16-byte fp32 granules per pixel row
-  constexpr int LPR = TN / 8;           // lanes per pixel row in the read phase
-  constexpr int PPI = 64 / LPR;         // pixels per read instruction
-  static_assert(TN % 8 == 0 && 64 % LPR == 0, "tile");
-  auto gpos = [](int p, int g) { return (p * GR + (g ^ (p & (GR - 1)))) * 4; };
-  const int ohw = a.OH * a.OW;
-  const int q = lane % LPR;              // this lane's 8-channel group within the wave tile
-  const int n = nbase + q * 8;
-  const bool nok = n < a.Ncol;
-  float bs[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) bs[e] = (a.bias && nok) ? a.bias[n + e] : 0.f;
-  float s1[8], s2[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) s1[e] = s2[e] = 0.f;
-  float bmu[8], bsc[8], bsh[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const bool on = a.bnred && !a.stats && nok;
-    bmu[e] = on ? a.bnmean[n + e] : 0.f;
-    bsc[e] = (on && a.bnaff) ? a.bnaff[n + e] : 0.f;
-    bsh[e] = (on && a.bnaff) ? a.bnaff[a.Ncol + n + e] : 0.f;
-  }
-  // NH > 1: the accumulator tile goes through LDS in NH row chunks, so the wave slice is TM/NH x TN floats
-  constexpr int NR = TM / PPI;
-  constexpr int MIH = MI / NH, NRH = NR / NH;
-  static_assert(MI % NH == 0 && NR % NH == 0, "row chunks");
-  const bool bnw = a.bnred && !a.stats;
-#pragma unroll
-  for (int h = 0; h < NH; ++h) {
-  // Phase 1: every global read of the chunk (addend, consumer-BN x / z) is issued before its first store:
-  // `out` may alias them as far as the compiler knows, so loads left inside the store loop would be serialised
-  // one round trip per row group.
-  long orows[NRH];
-  v4u pad[NRH], px[NRH], pz[NRH];
-#pragma unroll
-  for (int rr = 0; rr < NRH; ++rr) {
-    const int m = mbase + (h * NRH + rr) * PPI + lane / LPR;
-    long orow = -1;
-    if (m < a.M && nok) {
-      orow = m;
-      if (!a.ident_out) {
-        const int nb = m / ohw, rem = m - nb * ohw;
-        const int oh = rem / a.OW, ow = rem - oh * a.OW;
-        orow = ((long)nb * a.OHo + oh * a.omul_h + a.ooff_h) * a.OWo + ow * a.omul_w + a.ooff_w;
-      }
-    }
-    orows[rr] = orow;
-    const size_t off = (size_t)(orow < 0 ? 0 : orow) * a.ldo + n;
-    pad[rr] = v4u{0u, 0u, 0u, 0u};
-    px[rr] = v4u{0u, 0u, 0u, 0u};
-    pz[rr] = v4u{0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
-    if (orow >= 0) {
-      if (a.addend) pad[rr] = *reinterpret_cast<const v4u*>(a.addend + off);
-      if (bnw) {
-        px[rr] = *reinterpret_cast<const v4u*>(a.bnx + off);
-        if (a.bnz) pz[rr] = *reinterpret_cast<const v4u*>(a.bnz + off);
-      }
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < MIH; ++i)
-#pragma unroll
-    for (int j = 0; j < NI; ++j) {
-      const int p = i * 16 + (lane & 15);
-      const int g = j * 4 + (lane >> 4);
-      *reinterpret_cast<v4f*>(wl + gpos(p, g)) = acc[h * MIH + i][j];
-    }
-  __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's LDS writes landed (wave-private slice)
-#pragma unroll
-  for (int rr = 0; rr < NRH; ++rr) {
-    const int r = rr;
-    const int p = rr * PPI + lane / LPR;
-    const v4f lo = *reinterpret_cast<const v4f*>(wl + gpos(p, 2 * q));
-    const v4f hi = *reinterpret_cast<const v4f*>(wl + gpos(p, 2 * q + 1));
-    const long orow = orows[r];
-    if (orow >= 0 && a.out32) {        // fp32 GEMM output (+ bias), optionally accumulated: 2 x 16-byte stores
-      float* o32 = a.out32 + (size_t)orow * a.ldo + n;
-      v4f p0 = {lo[0] + bs[0], lo[1] + bs[1], lo[2] + bs[2], lo[3] + bs[3]};
-      v4f p1 = {hi[0] + bs[4], hi[1] + bs[5], hi[2] + bs[6], hi[3] + bs[7]};
-      if (a.accum32) {
-        p0 += *reinterpret_cast<const v4f*>(o32);
-        p1 += *reinterpret_cast<const v4f*>(o32 + 4);
-      }
-      *reinterpret_cast<v4f*>(o32) = p0;
-      *reinterpret_cast<v4f*>(o32 + 4) = p1;
-      continue;
-    }
-    if (orow >= 0) {
-      float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      if (a.addend) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) { v[2 * e] += lo_bf(pad[r][e]); v[2 * e + 1] += hi_bf(pad[r][e]); }
-      }
-      v4u o;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float x0 = v[2 * e] + bs[2 * e], x1 = v[2 * e + 1] + bs[2 * e + 1];
-        if (a.relu) { x0 = fmaxf(x0, 0.f); x1 = fmaxf(x1, 0.f); }
-        o[e] = pack2bf(x0, x1);
-      }
-      if (a.stats) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float y0 = lo_bf(o[e]), y1 = hi_bf(o[e]);
-          s1[2 * e] += y0; s2[2 * e] += y0 * y0;
-          s1[2 * e + 1] += y1; s2[2 * e + 1] += y1 * y1;
-        }
-      } else if (bnw) {
-        // consumer-BN backward reduction on the rounded gradient (what bn_bwd_reduce would read back)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float d0 = lo_bf(o[e]), d1 = hi_bf(o[e]);
-          const float x0 = lo_bf(px[r][e]), x1 = hi_bf(px[r][e]);
-          if (a.bnz) {
-            if (!(lo_bf(pz[r][e]) > 0.f)) d0 = 0.f;
-            if (!(hi_bf(pz[r][e]) > 0.f)) d1 = 0.f;
-          } else if (a.bnaff) {
-            if (!(x0 * bsc[2 * e] + bsh[2 * e] > 0.f)) d0 = 0.f;
-            if (!(x1 * bsc[2 * e + 1] + bsh[2 * e + 1] > 0.f)) d1 = 0.f;
-          }
-          s1[2 * e] += d0; s2[2 * e] += d0 * (x0 - bmu[2 * e]);
-          s1[2 * e + 1] += d1; s2[2 * e + 1] += d1 * (x1 - bmu[2 * e + 1]);
-        }
-      }
-      *reinterpret_cast<v4u*>(a.out + (size_t)orow * a.ldo + n) = o;
-    }
-  }
-  }
-  float* const red = a.stats ? a.stats : a.bnred;
-  if (red) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-#pragma unroll
-      for (int o = LPR; o < 64; o <<= 1) {
-        s1[e] += __shfl_xor(s1[e], o, 64);
-        s2[e] += __shfl_xor(s2[e], o, 64);
-      }
-    }
-    if constexpr (PAIR > 0) {
-      // the wm > 0 waves' own slices are free (their row phase has consumed them): park the sums there; the
-      // wm = 0 wave of the channel range adds the NWM - 1 partners (PAIR floats apart) and issues the atomics
-      if (wm > 0 && lane < LPR) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) { wl[lane * 16 + e] = s1[e]; wl[lane * 16 + 8 + e] = s2[e]; }
-      }
-      __syncthreads();
-      if (wm > 0) return;
-      if (lane < LPR) {
-#pragma unroll
-        for (int k = 1; k < NWM; ++k)
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            s1[e] += wl[k * PAIR + lane * 16 + e];
-            s2[e] += wl[k * PAIR + lane * 16 + 8 + e];
-          }
-      }
-    }
-    if (lane < LPR && nok) {
-      float* sp = red + (size_t)(bid & (BIGDL_STAT_SLOTS - 1)) * 2 * a.Ncol;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        atomicAdd(sp + n + e, s1[e]);
-        atomicAdd(sp + a.Ncol + n + e, s2[e]);
-      }
-    }
-  }
-}
+// nt_epilogue_lds (coalescing epilogue through LDS): conv_epilogue.h
 
 template <int BM, int BN, int WM, bool FASTK>
 __global__ __launch_bounds__(256, 2) void conv_nt_kernel(ConvArgs a) {
@@ -2483,8 +2306,9 @@ __global__ __launch_bounds__(256, 2) void conv_nt_s1_kernel(ConvArgs a) {
         const size_t off = (size_t)m * a.ldo + n;
         pad[rr] = a.addend ? *reinterpret_cast<const v4u*>(a.addend + off) : v4u{0u, 0u, 0u, 0u};
         px[rr] = bnw ? *reinterpret_cast<const v4u*>(a.bnx + off) : v4u{0u, 0u, 0u, 0u};
-        pz[rr] = (bnw && a.bnz) ? *reinterpret_cast<const v4u*>(a.bnz + off)
-                                : v4u{0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
+        pz[rr] = (bnw && a.bnzm) ? mask8_to_bf(a.bnzm[off >> 3])
+                 : (bnw && a.bnz) ? *reinterpret_cast<const v4u*>(a.bnz + off)
+                                  : v4u{0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
       }
     }
     v4f acc[MI][4];
@@ -2555,7 +2379,7 @@ __global__ __launch_bounds__(256, 2) void conv_nt_s1_kernel(ConvArgs a) {
             for (int e = 0; e < 4; ++e) {
               v2f d = {lo_bf(o[e]), hi_bf(o[e])};
               const v2f x = {lo_bf(px[rr][e]), hi_bf(px[rr][e])};
-              if (a.bnz) {
+              if (a.bnz || a.bnzm) {
                 if (!(lo_bf(pz[rr][e]) > 0.f)) d[0] = 0.f;
                 if (!(hi_bf(pz[rr][e]) > 0.f)) d[1] = 0.f;
               } else if (a.bnaff) {
@@ -2694,12 +2518,13 @@ __global__ __launch_bounds__(256) void conv_splitk_epilogue_kernel(ConvArgs a, l
       } else if (bnw) {
         const v4u px = *reinterpret_cast<const v4u*>(a.bnx + off);
         v4u pz = v4u{0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
-        if (a.bnz) pz = *reinterpret_cast<const v4u*>(a.bnz + off);
+        if (a.bnzm) pz = mask8_to_bf(a.bnzm[off >> 3]);
+        else if (a.bnz) pz = *reinterpret_cast<const v4u*>(a.bnz + off);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           float d0 = lo_bf(o[e]), d1 = hi_bf(o[e]);
           const float x0 = lo_bf(px[e]), x1 = hi_bf(px[e]);
-          if (a.bnz) {
+          if (a.bnz || a.bnzm) {
             if (!(lo_bf(pz[e]) > 0.f)) d0 = 0.f;
             if (!(hi_bf(pz[e]) > 0.f)) d1 = 0.f;
           } else if (a.bnaff) {
@@ -2971,6 +2796,7 @@ long bigdl_conv_nt_plan(ConvArgs* a) {
   if (a->Cs % 8 != 0 || a->M <= 0 || conv_impl() < 1) return 0;
   if (a->pstride > 0 && a->pstride != a->Cs) return 0;   // overlapping windows: g4 only, no split-K
   if (conv_impl() == 1 && s1_applies(a)) return 0;
+  if (conv_impl() == 1 && bigdl_conv_halo_applies(a)) return 0;
   if (g_conv_p8 < 0) (void)p8_pick(a);      // reads BIGDL_CONV_P8 once
   const int sk = sk_pick(a);
   if (sk > 0) {
@@ -3010,6 +2836,10 @@ int bigdl_conv_nt(const ConvArgs* a, hipStream_t st) {
   }
   if (impl == 1 && s1_applies(a)) {
     launch_s1_any(*a, st);
+    HIP_LAUNCH_CHECK();
+    return 0;
+  }
+  if (impl == 1 && bigdl_conv_halo_applies(a) && bigdl_conv_halo(a, st) == 0) {
     HIP_LAUNCH_CHECK();
     return 0;
   }

@@ -22,6 +22,7 @@ struct ConvArgs {
   // dm = out masked by the fused ReLU (z > 0 when bnz is set, else x * aff[c] + aff[Ncol + c] > 0, else no mask)
   const uint16_t* bnx;      // BN input x, same placement / ldo as out
   const uint16_t* bnz;      // BN output (post residual + ReLU) or nullptr
+  const uint8_t* bnzm;      // or its sign mask ([rows][Ncol / 8] bytes, bigdl_bn_apply zm), same placement / ldo
   const float* bnmean;      // [Ncol] batch mean
   const float* bnaff;       // [2 Ncol] scale | shift or nullptr
   float* bnred;
@@ -66,6 +67,10 @@ int bigdl_deterministic();
 void bigdl_set_deterministic(int v);
 void bigdl_colsum_bf16_ld(const uint16_t* x, float* out, long P, int K, long ld, hipStream_t st);
 int bigdl_conv_nt(const ConvArgs* a, hipStream_t st);
+// 3x3 / stride-1 / pad-1 forward or data-gradient GEMM from halo tiles (conv_halo.hip)
+int bigdl_conv_halo_applies(const ConvArgs* a);
+int bigdl_conv_halo(const ConvArgs* a, hipStream_t st);
+void bigdl_set_conv_halo(int v);
 // Kernel choice for bigdl_conv_nt: sets a->ksplit and returns the fp32 workspace elements it needs (0: none).
 long bigdl_conv_nt_plan(ConvArgs* a);
 // Batched NT GEMM (bmm.hip): C[b][m][n] (=|+=) alpha * sum_k A[b][m][k] B[b][n][k]; A, B bf16 K-contiguous (K % 32
@@ -96,14 +101,16 @@ void bigdl_bn_finalize(const float* stats, int nslots, const float* gamma, const
                        long P, int C, float eps, float momentum, int training, hipStream_t st);
 void bigdl_bn_slot_reduce(const float* in, int nslots, int C, float* out, hipStream_t st);
 void bigdl_bn_apply(const uint16_t* x, const float* scale, const float* shift, const uint16_t* res,
-                    uint16_t* y, long P, int C, int relu, hipStream_t st);
+                    uint16_t* y, long P, int C, int relu, hipStream_t st, uint8_t* zm = nullptr);
 // aff (optional, [scale C | shift C] of the forward apply): with z == nullptr the ReLU mask is recomputed from x.
 void bigdl_bn_bwd_reduce(const uint16_t* dz, const uint16_t* z, const uint16_t* x, const float* mean,
-                         float* red, long P, int C, const float* aff, hipStream_t st);
+                         float* red, long P, int C, const float* aff, hipStream_t st, const uint8_t* zm = nullptr);
 void bigdl_bn_bwd_apply(const uint16_t* dz, const uint16_t* z, const uint16_t* x, const float* mean,
                         const float* invstd, const float* gamma, const float* red, int nslots, float* coef,
                         uint16_t* dx, uint16_t* dres, float* dgamma, float* dbeta, long P, int C, int training,
-                        const float* aff, hipStream_t st);
+                        const float* aff, hipStream_t st, const uint8_t* zm = nullptr);
+// zm: [P][C / 8] sign bytes of the post-ReLU output (bit e of byte (p, g) = channel 8g + e > 0), written by
+// bigdl_bn_apply when non-null and read in place of z by the backward passes (1/16 of z's bytes)
 
 // elementwise
 void bigdl_relu_fwd(const uint16_t* x, uint16_t* y, long n, hipStream_t st);

@@ -198,6 +198,19 @@ def test_bn_fwd_bwd(res, relu):
     if res:
         mask = (y.float() > 0).float() if relu else 1.0
         assert _rel(dres, gzb.float() * mask) < 1e-2
+    if relu and res:
+        # sign-mask path (bn_apply writes one bit per element; the backward reads it instead of y): same y, the same
+        # residual gradient bit for bit, and the same gradients / reductions up to fp32 atomic order
+        rm2, rv2 = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+        zm = torch.full((N * C * H * W // 8,), 0x5A, dtype=torch.uint8, device=dev)
+        y2, sm2, si2, _ = bn.bn_forward_gpu(x, g, b, rm2, rv2, 1e-3, 0.1, True, res=r, relu=relu, zm=zm)
+        assert torch.equal(y2, y)
+        bits = torch.stack([(zm >> e) & 1 for e in range(8)], dim=1).reshape(N, H, W, C).permute(0, 3, 1, 2)
+        assert torch.equal(bits.bool(), y.float() > 0)
+        dg3, db3 = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
+        dx3, dres3 = bn.bn_backward_gpu(gzb, None, x, sm2, si2, g, dg3, db3, need_dres=True, zm=zm)
+        assert torch.equal(dres3, dres)
+        assert _rel(dx3, dx) < 1e-5 and _rel(dg3, dg) < 1e-5 and _rel(db3, dbt) < 1e-5
 
 
 def test_maxpool_avgpool():
@@ -952,3 +965,76 @@ def test_conv_wgrad_halo_matches_fp32(case):
         assert torch.isfinite(dw).all()
         assert _rel(dw, ref) < 5e-3, _rel(dw, ref)
     assert _rel(outs[0], outs[1]) < 5e-3
+
+
+HALO_CASES = [
+    # N, C, H, K (3x3, stride 1, pad 1): conv_halo_kernel takes fwd / dgrad when H in {56, 28, 14, 7}, C % 32 == 0 and
+    # the output channels are a multiple of its channel tile (64 at H 56, 128 below)
+    (4, 64, 56, 64),       # ResNet-50 layer 2 shape (RB 4 row segments, top / bottom halo variants)
+    (3, 128, 28, 128),     # layer 10 shape (RB 7)
+    (2, 128, 28, 256),     # fwd: two channel tiles; dgrad: 256 -> 128 (8 chunks)
+    (5, 256, 14, 256),     # layer 16 shape (one whole image per tile)
+    (4, 512, 7, 512),      # layer 22 shape (3 stacked images per tile, last tile past the batch)
+    (7, 64, 7, 128),       # stacked images, fwd two chunks; dgrad falls back (64 output channels)
+    (3, 96, 14, 128),      # odd chunk count (3 x 32 channels)
+]
+
+
+@pytest.mark.parametrize("zmask", [False, True])
+@pytest.mark.parametrize("case", HALO_CASES)
+def test_conv_halo_kernel(case, zmask):
+    """3x3 / stride-1 / pad-1 halo-tile kernel (conv_halo.hip: one staged input halo per 32-channel chunk, 9 shifted
+    LDS windows, weight ring) vs fp32 torch: forward + BN statistics, forward + bias + ReLU, data gradient + residual
+    addend + consumer-BN backward reduction under the affine (or z) ReLU mask; and against the im2col kernels
+    (BIGDL_CONV_HALO off)."""
+    from bigdl_amd.ops import bn as bnops
+    from bigdl_amd.ops import conv as cv
+    from bigdl_amd.ops import native
+
+    C_ = native.get()
+    N, C, H, K = case
+    torch.manual_seed(13)
+    dev = _dev()
+    x = torch.randn(N, C, H, H, device=dev).to(BF, memory_format=CL)
+    w = (torch.randn(K, C, 3, 3, device=dev) * (1.0 / (9 * C) ** 0.5)).to(BF, memory_format=CL)
+    b32 = torch.randn(K, device=dev)
+    yr0 = F.conv2d(x.float(), w.float(), padding=1)
+    g = lambda s: torch.Generator(dev).manual_seed(s)  # noqa: E731
+    gy = torch.randn(N, K, H, H, device=dev, generator=g(3)).to(BF, memory_format=CL)
+    add = torch.randn(N, C, H, H, device=dev, generator=g(4)).to(BF, memory_format=CL)
+    bx = torch.randn(N, C, H, H, device=dev, generator=g(5)).to(BF, memory_format=CL)
+    bz = torch.relu(torch.randn(N, C, H, H, device=dev, generator=g(6))).to(BF, memory_format=CL)
+    mean = torch.linspace(-0.1, 0.1, C, device=dev)
+    aff = torch.cat([torch.linspace(0.5, 1.5, C, device=dev), torch.linspace(-0.2, 0.2, C, device=dev)])
+    res = {}
+    for halo in (1, 0):
+        C_.set_conv_halo(halo)
+        try:
+            stats = bnops.new_stats(K, dev)
+            y = cv.conv2d_fwd(x, w, None, (1, 1), (1, 1), stats=stats)
+            y2 = cv.conv2d_fwd(x, w, b32, (1, 1), (1, 1), relu=True)
+            red = bnops.new_stats(C, dev)
+            bn = {"x": bx, "z": bz if zmask else None, "mean": mean, "aff": aff, "red": red}
+            dx = cv.conv2d_dgrad(gy, cv.transpose_w(w), x.shape, (1, 1), (1, 1), addend=add, bn=bn)
+            torch.cuda.synchronize()
+            res[halo] = (y, stats, y2, dx, red, bool(bn.get("done")))
+        finally:
+            C_.set_conv_halo(1)
+    y, stats, y2, dx, red, done = res[1]
+    assert torch.isfinite(y.float()).all() and torch.isfinite(dx.float()).all()
+    assert _rel(y, yr0) < 1e-2
+    st2 = stats.view(bnops.stat_slots(), 2, K).sum(0)
+    assert _rel(st2[0], y.float().sum(dim=(0, 2, 3))) < 1e-4
+    assert _rel(st2[1], (y.float() ** 2).sum(dim=(0, 2, 3))) < 1e-4
+    assert _rel(y2, torch.relu(yr0 + b32.view(1, K, 1, 1))) < 1e-2
+    assert _rel(y, res[0][0]) < 1e-2
+    dxr = torch.nn.grad.conv2d_input(x.shape, w.float(), gy.float(), padding=1) + add.float()
+    assert _rel(dx, dxr) < 1e-2
+    assert _rel(dx, res[0][3]) < 1e-2
+    assert done
+    d = dx.float()
+    mask = (bz.float() > 0) if zmask else (bx.float() * aff[:C].view(1, C, 1, 1) + aff[C:].view(1, C, 1, 1)) > 0
+    dm = d * mask
+    r2 = red.view(bnops.stat_slots(), 2, C).sum(0)
+    assert _rel(r2[0], dm.sum(dim=(0, 2, 3))) < 1e-3
+    assert _rel(r2[1], (dm * (bx.float() - mean.view(1, C, 1, 1))).sum(dim=(0, 2, 3))) < 1e-3

@@ -24,8 +24,8 @@ from bigdl_amd.ops import native  # noqa: E402
 
 SETTERS = {"impl": "set_conv_impl", "g4": "set_conv_g4", "p8": "set_conv_p8", "nt2": "set_conv_nt2",
            "shortk": "set_conv_shortk", "s1": "set_conv_s1", "sk": "set_conv_sk",
-           "halo": "set_wgrad_halo"}
-DEFAULTS = {"impl": 1, "g4": 3, "p8": 1, "nt2": 0, "shortk": 0, "s1": 1, "sk": 0, "halo": 1}
+           "halo": "set_wgrad_halo", "chalo": "set_conv_halo"}
+DEFAULTS = {"impl": 1, "g4": 3, "p8": 1, "nt2": 0, "shortk": 0, "s1": 1, "sk": 0, "halo": 1, "chalo": 1}
 
 
 def parse_variants(spec):
