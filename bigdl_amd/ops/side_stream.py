@@ -27,6 +27,10 @@ import torch
 _ON = [os.environ.get("BIGDL_WGRAD_STREAM", "1") == "1"]
 _N = max(1, int(os.environ.get("BIGDL_WGRAD_STREAMS", "1")))      # round-robin side streams per device
 _PRIO = int(os.environ.get("BIGDL_WGRAD_PRIO", "0"))
+# BIGDL_WGRAD_CUMASK: restrict the side stream to a subset of the CUs (hipExtStreamCreateWithCUMask) so the weight
+# gradients cannot occupy every CU the data-gradient chain needs: "" (default) = all CUs; "stride:K" = every K-th CU;
+# "first:N" = CUs 0..N-1; or comma-separated 32-bit hex words
+_CUMASK = os.environ.get("BIGDL_WGRAD_CUMASK", "")
 _STREAMS = {}
 _PENDING = []
 _RR = [0]
@@ -56,9 +60,37 @@ def stream_for(t):
     dev = t.device.index if t.device.index is not None else torch.cuda.current_device()
     ss = _STREAMS.get(dev)
     if ss is None:
-        ss = _STREAMS[dev] = [torch.cuda.Stream(device=dev, priority=_PRIO) for _ in range(_N)]
+        ss = _STREAMS[dev] = [_new_stream(dev) for _ in range(_N)]
     _RR[0] += 1
     return ss[_RR[0] % len(ss)]
+
+
+def _cu_mask_words(spec, ncu):
+    bits = [False] * ncu
+    if spec.startswith("stride:"):
+        k = int(spec.split(":")[1])
+        for i in range(0, ncu, k):
+            bits[i] = True
+    elif spec.startswith("first:"):
+        for i in range(min(ncu, int(spec.split(":")[1]))):
+            bits[i] = True
+    else:
+        return [int(w, 16) for w in spec.split(",")]
+    words = [0] * ((ncu + 31) // 32)
+    for i, b in enumerate(bits):
+        if b:
+            words[i // 32] |= 1 << (i % 32)
+    return words
+
+
+def _new_stream(dev):
+    if _CUMASK:
+        from . import native
+
+        ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+        h = native.get().cu_masked_stream(dev, _cu_mask_words(_CUMASK, ncu))
+        return torch.cuda.ExternalStream(h, device=dev)
+    return torch.cuda.Stream(device=dev, priority=_PRIO)
 
 
 def begin(s):

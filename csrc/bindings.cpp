@@ -1023,6 +1023,20 @@ void gru_seq_bwd(const Tensor& Wrz16, const Tensor& Wn16, const OptT& h0, const 
 // cs [T, B, H], acts [T, B, 4H]; sync = int32 workspace of lstm_seq_sync_words() words (zeroed by the launch).
 bool lstm_seq_supported(int64_t B, int64_t H) { return bigdl_lstm_seq_supported((int)B, (int)H) != 0; }
 int64_t lstm_seq_sync_words() { return bigdl_lstm_seq_sync_words(); }
+
+// A HIP stream restricted to the CUs whose bits are set in `mask` (32 CUs per word; hipExtStreamCreateWithCUMask).
+// Returned as an integer handle for torch.cuda.ExternalStream; the stream lives for the process.
+int64_t cu_masked_stream(int64_t device, std::vector<int64_t> mask) {
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  (void)hipSetDevice((int)device);
+  std::vector<uint32_t> m(mask.begin(), mask.end());
+  hipStream_t st = nullptr;
+  const hipError_t e = hipExtStreamCreateWithCUMask(&st, (uint32_t)m.size(), m.data());
+  (void)hipSetDevice(prev);
+  TORCH_CHECK(e == hipSuccess, "hipExtStreamCreateWithCUMask failed: ", hipGetErrorString(e));
+  return (int64_t)(uintptr_t)st;
+}
 void lstm_seq_fwd(const Tensor& W16, const Tensor& xg, const OptT& c0, const Tensor& h16, const Tensor& out,
                   const OptT& hT, const Tensor& cs, const Tensor& acts, const Tensor& sync) {
   TORCH_CHECK(xg.dim() == 3 && xg.is_contiguous(), "lstm_seq_fwd: xg must be [B, T, 4H] contiguous");
@@ -1343,6 +1357,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_conv_impl", &bigdl_set_conv_impl);
   m.def("set_conv_s1", &bigdl_set_conv_s1);
   m.def("set_conv_halo", &bigdl_set_conv_halo);
+  m.def("cu_masked_stream", &cu_masked_stream, "HIP stream restricted to a CU mask (32 CUs per word)");
   m.def("set_conv_sk", &bigdl_set_conv_sk);
   m.def("set_wgrad_halo", &bigdl_set_wgrad_halo);
   m.def("set_deterministic", &bigdl_set_deterministic, "1: bitwise-reproducible reductions (no multi-writer float atomics)");

@@ -24,9 +24,9 @@ struct GemmRowMap {
 // are conflict-free — then re-reads it row-wise: a lane owns 8 channels of one pixel, so every store is
 // 16 B and one wave instruction writes 64/(TN/8) whole pixel rows of TN channels. bias / addend / ReLU /
 // BN statistics are applied in the row phase (the addend is read with the same 16-byte coalesced pattern).
-// PAIR > 0: the workgroup's two pixel-half waves (wm = 0 / 1) that share a channel range combine their BN
-// statistics through LDS (PAIR = float offset from the wm = 0 wave's slice to its partner's) and only the wm = 0
-// wave issues the atomics: half the atomic traffic into the statistics slots.
+// PAIR > 0 (= WGN * SL: every wave of the workgroup calls this with its slice at wave * SL, wave = wm * WGN + wn, and
+// NWM pixel-row waves per channel range): the BN statistics / consumer-BN sums of all waves are combined through LDS
+// and committed by the whole workgroup, one full-wave atomic per value (see the commit below).
 template <int MI, int NI, int TM, int TN, int NH = 1, int PAIR = 0, int NWM = 2, class RowMap = GemmRowMap>
 __device__ __forceinline__ void nt_epilogue_lds(const ConvArgs& a, v4f (&acc)[MI][NI], int mbase, int nbase,
                                                 int lane, int bid, float* wl, int wm = 0, RowMap rowmap = {}) {
@@ -162,23 +162,29 @@ __device__ __forceinline__ void nt_epilogue_lds(const ConvArgs& a, v4f (&acc)[MI
       }
     }
     if constexpr (PAIR > 0) {
-      // the wm > 0 waves' own slices are free (their row phase has consumed them): park the sums there; the
-      // wm = 0 wave of the channel range adds the NWM - 1 partners (PAIR floats apart) and issues the atomics
-      if (wm > 0 && lane < LPR) {
+      // Workgroup commit: every wave parks its TN channels' sums in its own (consumed) slice, then the whole workgroup
+      // adds the NWM pixel-row partials of each of its channels and issues ONE atomic per value, with full waves.
+      // A memory-side float atomic costs ~50 ns per wave-instruction per CU whatever its lane count, so the former
+      // 8-lane atomics (16 wave-instructions per wave) bounded statistics-heavy tiles such as the 7x7 stem.
+      // Slices are laid out as wave * SL floats with wave = wm * WGN + wn (PAIR = WGN * SL).
+      if (lane < LPR) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) { wl[lane * 16 + e] = s1[e]; wl[lane * 16 + 8 + e] = s2[e]; }
       }
       __syncthreads();
-      if (wm > 0) return;
-      if (lane < LPR) {
+      const int nwv = (int)(blockDim.x >> 6), wgn = nwv / NWM, sl = PAIR / wgn;
+      const int wave = (int)(threadIdx.x >> 6), wn = wave % wgn;
+      const float* base = wl - wave * sl;
+      const int n0 = nbase - wn * TN, nv = wgn * TN;
+      float* sp = red + (size_t)(bid & (BIGDL_STAT_SLOTS - 1)) * 2 * a.Ncol;
+      for (int t = (int)threadIdx.x; t < 2 * nv; t += (int)blockDim.x) {
+        const int which = t >= nv ? 1 : 0, c = t - which * nv, w2 = c / TN, cl = c - w2 * TN;
+        float v = 0.f;
 #pragma unroll
-        for (int k = 1; k < NWM; ++k)
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            s1[e] += wl[k * PAIR + lane * 16 + e];
-            s2[e] += wl[k * PAIR + lane * 16 + 8 + e];
-          }
+        for (int k = 0; k < NWM; ++k) v += base[(k * wgn + w2) * sl + (cl >> 3) * 16 + which * 8 + (cl & 7)];
+        if (n0 + c < a.Ncol) atomicAdd(sp + which * a.Ncol + n0 + c, v);
       }
+      return;
     }
     if (lane < LPR && nok) {
       float* sp = red + (size_t)(bid & (BIGDL_STAT_SLOTS - 1)) * 2 * a.Ncol;

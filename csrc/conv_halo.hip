@@ -101,7 +101,193 @@ struct HaloRowMap {
   }
 };
 
-template <int W, int RB, int NIMG, int KT, int WPX>
+// ---- epilogues. nt_epilogue_lds (its runtime-flag branches around every optional load put vmcnt(0) waits in front of
+// its stores, and 7 row chunks per tile serialise on them: 42 of the 79 us of the 28x28 layer, BIGDL_CONV_HALO_ABL)
+// is replaced by two branch-free forms; rows without an output pixel get a buffer offset past num_records (stores
+// dropped, loads return 0).
+constexpr unsigned EOOB = 0x7ffffff0u;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* p, size_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)(bytes < 0x7fffffffu ? bytes : 0x7fffffffu),
+                                           0x00020000);
+}
+
+// Workgroup-level commit of per-wave channel sums: every wave parks its 64 channels' (s1, s2) in LDS, then one pass of
+// the workgroup adds the WPX pixel-group partials of each of its KT channels and issues ONE atomic per value: 2 * KT /
+// 256 full-wave atomic instructions per tile instead of 16-32 mostly-idle ones per wave (a memory-side float atomic
+// costs ~50 ns per wave-instruction per CU whatever its lane count: that, not bandwidth, made the epilogue slow).
+template <int WCH, int KT>
+__device__ __forceinline__ void halo_commit(float* red, float* rl, int k0, int Ncol, int bid) {
+  __syncthreads();
+  const int t = threadIdx.x;
+  if (t < 2 * KT) {
+    const int which = t / KT, c = t - which * KT, wc = c / 64, cl = c & 63;
+    float v = 0.f;
+#pragma unroll
+    for (int wp = 0; wp < 4 / WCH; ++wp) v += rl[(wp * WCH + wc) * 128 + which * 64 + cl];
+    atomicAdd(red + (size_t)(bid & (BIGDL_STAT_SLOTS - 1)) * 2 * Ncol + which * Ncol + k0 + c, v);
+  }
+}
+
+// Lean form (no bias / addend / consumer-BN reduction: the forward with optional ReLU and BN statistics): the wave's
+// 64-channel tile goes through its LDS slice once as bf16 ([pixel][8 granules], granule g of pixel p in slot g ^ (p & 7)),
+// then 8 lanes store one pixel's whole 128-byte row (16-byte buffer stores); statistics of the rounded output.
+template <int FM, int FN, int WCH, int KT, class RM>
+__device__ __forceinline__ void halo_epi_lean(const ConvArgs& a, v4f (&acc)[FM][FN], int vbase, int nbase, int lane,
+                                              int bid, unsigned char* sl, const RM& rm, float* rl0, int k0) {
+  float* rl = rl0 + (threadIdx.x >> 6) * 128;
+  static_assert(FN == 4, "64-channel wave tile");
+  constexpr int TM = FM * 16;
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int p = i * 16 + (lane & 15), g = 2 * j + (lane >> 5);
+      const v2u w = {pack2bf(acc[i][j][0], acc[i][j][1]), pack2bf(acc[i][j][2], acc[i][j][3])};
+      *reinterpret_cast<v2u*>(sl + p * 128 + ((g ^ (p & 7)) << 4) + ((lane >> 4) & 1) * 8) = w;
+    }
+  const size_t rows = (size_t)a.Nb * a.OH * a.OW;
+  const __amdgpu_buffer_rsrc_t ro = rsrc_of(a.out, ((rows - 1) * a.ldo + a.Ncol) * 2);
+  const int q = lane & 7;
+  float s1[8], s2[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) s1[e] = s2[e] = 0.f;
+  const bool relu = a.relu != 0, st = a.stats != nullptr;
+#pragma unroll
+  for (int r = 0; r < TM / 8; ++r) {
+    const int p = r * 8 + (lane >> 3);
+    v4u o = *reinterpret_cast<const v4u*>(sl + p * 128 + ((q ^ (p & 7)) << 4));
+    const long orow = rm(a, vbase + p);
+    if (relu) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = pack2bf(fmaxf(lo_bf(o[e]), 0.f), fmaxf(hi_bf(o[e]), 0.f));
+    }
+    if (st) {
+      const float vm = orow >= 0 ? 1.f : 0.f;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float y0 = lo_bf(o[e]) * vm, y1 = hi_bf(o[e]) * vm;
+        s1[2 * e] += y0; s2[2 * e] += y0 * y0;
+        s1[2 * e + 1] += y1; s2[2 * e + 1] += y1 * y1;
+      }
+    }
+    const unsigned off = orow >= 0 ? (unsigned)(((size_t)orow * a.ldo + nbase + q * 8) * 2) : EOOB;
+    __builtin_amdgcn_raw_buffer_store_b128(o, ro, off, 0, 0);
+  }
+  if (st) {          // uniform: every wave of the workgroup takes this branch
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+#pragma unroll
+      for (int o = 8; o < 64; o <<= 1) {
+        s1[e] += __shfl_xor(s1[e], o, 64);
+        s2[e] += __shfl_xor(s2[e], o, 64);
+      }
+    if (lane < 8) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { rl[q * 8 + e] = s1[e]; rl[64 + q * 8 + e] = s2[e]; }
+    }
+    halo_commit<WCH, KT>(a.stats, rl0, k0, a.Ncol, bid);
+  }
+}
+
+// Full form, straight from the accumulators (a lane owns 4 consecutive channels of one pixel per fragment): bias,
+// residual addend (fp32 add before rounding), ReLU, 8-byte stores, BN statistics or the consumer-BN backward reduction
+// of the rounded gradient under the z / sign-mask / affine ReLU mask (nt_epilogue_lds semantics). Every optional
+// operand is loaded unconditionally from its own buffer (a null operand gets num_records 0: loads return 0).
+template <int FM, int FN, int WCH, int KT, class RM>
+__device__ __forceinline__ void halo_epi_full(const ConvArgs& a, v4f (&acc)[FM][FN], int vbase, int nbase, int lane,
+                                              int bid, const RM& rm, float* rl0, int k0) {
+  float* rl = rl0 + (threadIdx.x >> 6) * 128;
+  const size_t rows = (size_t)a.Nb * a.OH * a.OW;
+  const size_t nb2 = ((rows - 1) * a.ldo + a.Ncol) * 2;
+  const __amdgpu_buffer_rsrc_t ro = rsrc_of(a.out, nb2);
+  const __amdgpu_buffer_rsrc_t rad = rsrc_of(a.addend, a.addend ? nb2 : 0);
+  const bool bnw = a.bnred != nullptr && a.stats == nullptr;
+  const __amdgpu_buffer_rsrc_t rbx = rsrc_of(a.bnx, bnw ? nb2 : 0);
+  const __amdgpu_buffer_rsrc_t rbz = rsrc_of(a.bnz, (bnw && a.bnz) ? nb2 : 0);
+  const __amdgpu_buffer_rsrc_t rzm = rsrc_of(a.bnzm, (bnw && a.bnzm) ? nb2 / 16 : 0);
+  const int c4 = 4 * (lane >> 4);
+  float bs[FN][4], mu[FN][4], sc[FN][4], sh[FN][4], s1[FN][4], s2[FN][4];
+#pragma unroll
+  for (int j = 0; j < FN; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int c = nbase + j * 16 + c4 + e;
+      bs[j][e] = a.bias ? a.bias[c] : 0.f;
+      mu[j][e] = bnw ? a.bnmean[c] : 0.f;
+      sc[j][e] = (bnw && a.bnaff) ? a.bnaff[c] : 0.f;
+      sh[j][e] = (bnw && a.bnaff) ? a.bnaff[a.Ncol + c] : 0.f;
+      s1[j][e] = s2[j][e] = 0.f;
+    }
+  const bool relu = a.relu != 0, st = a.stats != nullptr;
+  const int zmode = !bnw ? 0 : a.bnzm ? 1 : a.bnz ? 2 : a.bnaff ? 3 : 0;
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const long orow = rm(a, vbase + i * 16 + (lane & 15));
+    const float vm = orow >= 0 ? 1.f : 0.f;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const size_t el = (size_t)(orow >= 0 ? orow : 0) * a.ldo + nbase + j * 16 + c4;
+      const unsigned off = orow >= 0 ? (unsigned)(el * 2) : EOOB;
+      const v2u ad = __builtin_amdgcn_raw_buffer_load_b64(rad, off, 0, 0);
+      const v2u bx = __builtin_amdgcn_raw_buffer_load_b64(rbx, off, 0, 0);
+      const v2u bz = __builtin_amdgcn_raw_buffer_load_b64(rbz, off, 0, 0);
+      const unsigned zb = __builtin_amdgcn_raw_buffer_load_b8(rzm, orow >= 0 ? (unsigned)(el >> 3) : EOOB, 0, 0);
+      const float adf[4] = {lo_bf(ad[0]), hi_bf(ad[0]), lo_bf(ad[1]), hi_bf(ad[1])};
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float t = acc[i][j][e] + bs[j][e] + adf[e];
+        if (relu) t = fmaxf(t, 0.f);
+        v[e] = t;
+      }
+      const v2u o = {pack2bf(v[0], v[1]), pack2bf(v[2], v[3])};
+      __builtin_amdgcn_raw_buffer_store_b64(o, ro, off, 0, 0);
+      const float y[4] = {lo_bf(o[0]) * vm, hi_bf(o[0]) * vm, lo_bf(o[1]) * vm, hi_bf(o[1]) * vm};
+      if (st) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { s1[j][e] += y[e]; s2[j][e] += y[e] * y[e]; }
+      } else if (bnw) {
+        const float xf[4] = {lo_bf(bx[0]), hi_bf(bx[0]), lo_bf(bx[1]), hi_bf(bx[1])};
+        const float zf[4] = {lo_bf(bz[0]), hi_bf(bz[0]), lo_bf(bz[1]), hi_bf(bz[1])};
+        const unsigned zbits = (zb >> ((nbase + j * 16 + c4) & 7)) & 0xfu;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          bool keep = true;
+          if (zmode == 1) keep = (zbits >> e) & 1u;
+          else if (zmode == 2) keep = zf[e] > 0.f;
+          else if (zmode == 3) keep = xf[e] * sc[j][e] + sh[j][e] > 0.f;
+          const float d = keep ? y[e] : 0.f;
+          s1[j][e] += d;
+          s2[j][e] += d * (xf[e] - mu[j][e]);
+        }
+      }
+    }
+  }
+  float* const red = st ? a.stats : (bnw ? a.bnred : nullptr);
+  if (red) {
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          s1[j][e] += __shfl_xor(s1[j][e], o, 64);
+          s2[j][e] += __shfl_xor(s2[j][e], o, 64);
+        }
+    if ((lane & 15) == 0) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { rl[j * 16 + c4 + e] = s1[j][e]; rl[64 + j * 16 + c4 + e] = s2[j][e]; }
+    }
+    halo_commit<WCH, KT>(red, rl0, k0, a.Ncol, bid);
+  }
+}
+
+// ABL (timing ablations, BIGDL_CONV_HALO_ABL, wrong outputs): bit 0 no epilogue, bit 1 no MFMAs, bit 2 no DMA after
+// the prologue (stale LDS), bit 3 no fragment reads
+// EPI: 0 lean epilogue (no bias / addend / consumer-BN reduction), 1 full epilogue
+template <int W, int RB, int NIMG, int KT, int WPX, int EPI, int ABL = 0>
 __global__ __launch_bounds__(256, 2) void conv_halo_kernel(ConvArgs a) {
   using H = HaloF<W, RB, NIMG, KT, WPX>;
   __shared__ __attribute__((aligned(1024))) unsigned char lds[H::LDS];
@@ -226,31 +412,40 @@ __global__ __launch_bounds__(256, 2) void conv_halo_kernel(ConvArgs a) {
       const int s = ch * 9 + t;
       // slot (s + D) % NSW was read in step s - 1 (retired by the barrier that ended it); x buffer (ch + 1) & 1 was
       // last read by chunk ch - 1
-      if (s + H::D < nk) {
+      if (!(ABL & 4) && s + H::D < nk) {
         constexpr int t2 = (t + H::D) % 9, dc = (t + H::D) / 9;
         issue_w(ch + dc, t2, (s + H::D) % H::NSW);
       }
-      if (t == 0 && ch + 1 < nch) issue_x(ch + 1);
+      if (!(ABL & 4) && t == 0 && ch + 1 < nch) issue_x(ch + 1);
       const int r0 = v0 + tshift[t];
       const unsigned xrd = xb + (unsigned)(r0 * 64 + ((gi ^ hswz(r0)) << 4));
       const unsigned wrs = lds_base + wrd + (unsigned)((s % H::NSW) * H::WBYTES);
       v8s fw[FN], fx[FM];
-      hfor<FN>([&](auto jc) {
-        constexpr int j = decltype(jc)::value;
-        fw[j] = ldsr<j * 16 * 64>(wrs);
-      });
-      hfor<FM>([&](auto ic) {
-        constexpr int i = decltype(ic)::value;
-        fx[i] = ldsr<i * 16 * 64>(xrd);
-      });
+      if constexpr (ABL & 8) {
+        hfor<FN>([&](auto jc) { fw[decltype(jc)::value] = v8s{(short)(xrd & 7), 1, 2, 3, 4, 5, 6, 7}; });
+        hfor<FM>([&](auto ic) { fx[decltype(ic)::value] = v8s{(short)(wrs & 7), 1, 2, 3, 4, 5, 6, 7}; });
+      } else {
+        hfor<FN>([&](auto jc) {
+          constexpr int j = decltype(jc)::value;
+          fw[j] = ldsr<j * 16 * 64>(wrs);
+        });
+        hfor<FM>([&](auto ic) {
+          constexpr int i = decltype(ic)::value;
+          fx[i] = ldsr<i * 16 * 64>(xrd);
+        });
+      }
       // pixel fragment i's MFMAs start once it landed (the weight fragments were read first); the tie keeps every
       // use of fx[i] behind its wait
       hfor<FM>([&](auto ic) {
         constexpr int i = decltype(ic)::value;
         asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(fx[i]) : "n"(FM - 1 - i));
+        if constexpr (!(ABL & 2)) {
 #pragma unroll
-        for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[j], fx[i], acc[i][j], 0, 0, 0);
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[j], fx[i], acc[i][j], 0, 0, 0);
+        } else {
+          acc[i][0][0] += (float)fw[0][0] * (float)fx[i][0];
+        }
       });
       __builtin_amdgcn_sched_barrier(0);
       // retire step s + 1 for every wave: younger than W(s + 1) are W(s + 2 .. s + D) and the x chunk issued at this
@@ -265,14 +460,25 @@ __global__ __launch_bounds__(256, 2) void conv_halo_kernel(ConvArgs a) {
     });
   }
 
-  // epilogue: nt_epilogue_lds over the (now idle) LDS, one 16-row chunk of the wave tile at a time
-  constexpr int NH = FM;
-  constexpr int SL = (H::TM / NH) * H::TN;
-  static_assert(4 * SL * 4 <= H::LDS, "epilogue slices must fit the LDS");
-  float* wl = reinterpret_cast<float*>(lds) + wave * SL;
-  HaloRowMap<W, RB, NIMG> rm{n0, oh0, H::VR * WP};
-  nt_epilogue_lds<FM, FN, H::TM, H::TN, NH, 0, 2, HaloRowMap<W, RB, NIMG>>(a, acc, wpx * H::TM, k0 + wch * H::TN,
-                                                                           lane, bid, wl, 0, rm);
+  if constexpr (ABL & 1) {
+    float t = 0.f;                                 // keep every accumulator (and so every MFMA) alive
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) t += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+    if (t == 123.f) a.out[0] = 1;
+    return;
+  }
+  const HaloRowMap<W, RB, NIMG> rm{n0, oh0, H::VR * WP};
+  // per-wave channel sums go behind the bf16 slices (lean) or at the start of the idle LDS (full)
+  if constexpr (EPI == 0) {
+    static_assert(4 * H::TM * 128 + 4 * 128 * 4 <= H::LDS, "bf16 epilogue slices must fit the LDS");
+    halo_epi_lean<FM, FN, WCH, KT>(a, acc, wpx * H::TM, k0 + wch * H::TN, lane, bid, lds + wave * H::TM * 128, rm,
+                                   reinterpret_cast<float*>(lds + 4 * H::TM * 128), k0);
+  } else {
+    halo_epi_full<FM, FN, WCH, KT>(a, acc, wpx * H::TM, k0 + wch * H::TN, lane, bid, rm, reinterpret_cast<float*>(lds),
+                                   k0);
+  }
 }
 
 template <int W, int RB, int NIMG, int KT, int WPX>
@@ -280,7 +486,17 @@ void launch_halo_f(const ConvArgs& a, hipStream_t st) {
   const int segs = a.Hs / RB;
   const int tiles_m = NIMG == 1 ? a.Nb * segs : (a.Nb + NIMG - 1) / NIMG;
   const int nwg = tiles_m * (a.Ncol / KT);
-  conv_halo_kernel<W, RB, NIMG, KT, WPX><<<dim3(nwg), dim3(256), 0, st>>>(a);
+  static const int abl = [] { const char* e = getenv("BIGDL_CONV_HALO_ABL"); return e ? atoi(e) : 0; }();
+  const bool lean = a.bias == nullptr && a.addend == nullptr && (a.bnred == nullptr || a.stats != nullptr);
+  const dim3 g(nwg), b(256);
+  if (abl == 1) conv_halo_kernel<W, RB, NIMG, KT, WPX, 0, 1><<<g, b, 0, st>>>(a);
+  else if (abl == 3) conv_halo_kernel<W, RB, NIMG, KT, WPX, 0, 3><<<g, b, 0, st>>>(a);
+  else if (abl == 5) conv_halo_kernel<W, RB, NIMG, KT, WPX, 0, 5><<<g, b, 0, st>>>(a);
+  else if (abl == 9) conv_halo_kernel<W, RB, NIMG, KT, WPX, 0, 9><<<g, b, 0, st>>>(a);
+  else if (abl == 13) conv_halo_kernel<W, RB, NIMG, KT, WPX, 0, 13><<<g, b, 0, st>>>(a);
+  else if (abl == 15) conv_halo_kernel<W, RB, NIMG, KT, WPX, 0, 15><<<g, b, 0, st>>>(a);
+  else if (lean) conv_halo_kernel<W, RB, NIMG, KT, WPX, 0><<<g, b, 0, st>>>(a);
+  else conv_halo_kernel<W, RB, NIMG, KT, WPX, 1><<<g, b, 0, st>>>(a);
 }
 
 int g_conv_halo = -1;

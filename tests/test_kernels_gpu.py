@@ -238,6 +238,7 @@ def test_maxpool_avgpool():
 
 @pytest.mark.parametrize("shape,k,s,p,ceil", [((2, 64, 15, 15), 3, 2, 1, False), ((3, 24, 16, 13), 3, 2, 0, True),
                                                 ((2, 8, 112, 112), 3, 2, 1, False), ((2, 16, 9, 9), 3, 1, 1, False),
+                                                ((3, 16, 20, 14), 3, 2, 1, False),
                                                 ((2, 32, 10, 11), 2, 2, 0, False)])
 def test_maxpool_window_variants(shape, k, s, p, ceil):
     """The fixed 3x3/2 kernels and the generic ones against torch (values exact, gradients summed per winner)."""

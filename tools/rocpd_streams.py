@@ -39,6 +39,17 @@ def main(db, marker, k, steps):
         a, b = by[keys[0]], by[keys[1]]
         both = union(a) + union(b) - union(a + b)
         print(f"both of the two busiest streams running: {both / 1e6 / steps:.3f} ms/step")
+    # per-kernel time on each of the two busiest streams (the compute stream is the step's critical path)
+    for key in sorted(by, key=lambda kk: -len(by[kk]))[:2]:
+        agg = {}
+        for n, s, e, sid, qid in rows:
+            if (sid, qid) == key:
+                a = agg.setdefault(n, [0, 0.0])
+                a[0] += 1
+                a[1] += (e - s) / 1e6 / steps
+        print(f"-- stream {key} kernels (ms/step, dispatches/step)")
+        for n, (cnt, ms) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:25]:
+            print(f"{ms:8.3f} {cnt / steps:6.1f}  {n[:120]}")
 
 
 if __name__ == "__main__":
