@@ -1357,6 +1357,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_conv_impl", &bigdl_set_conv_impl);
   m.def("set_conv_s1", &bigdl_set_conv_s1);
   m.def("set_conv_halo", &bigdl_set_conv_halo);
+  m.def("set_stem_fwd", &bigdl_set_stem_fwd);
   m.def("cu_masked_stream", &cu_masked_stream, "HIP stream restricted to a CU mask (32 CUs per word)");
   m.def("set_conv_sk", &bigdl_set_conv_sk);
   m.def("set_wgrad_halo", &bigdl_set_wgrad_halo);

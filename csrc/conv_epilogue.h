@@ -197,4 +197,99 @@ __device__ __forceinline__ void nt_epilogue_lds(const ConvArgs& a, v4f (&acc)[MI
   }
 }
 
+// ---- halo-style epilogues (conv_halo.hip, stem.hip). nt_epilogue_lds (its runtime-flag branches around every optional load put vmcnt(0) waits in front of
+// its stores, and 7 row chunks per tile serialise on them: 42 of the 79 us of the 28x28 layer, BIGDL_CONV_HALO_ABL)
+// is replaced by two branch-free forms; rows without an output pixel get a buffer offset past num_records (stores
+// dropped, loads return 0).
+constexpr unsigned EOOB = 0x7ffffff0u;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* p, size_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)(bytes < 0x7fffffffu ? bytes : 0x7fffffffu),
+                                           0x00020000);
+}
+
+// Workgroup-level commit of per-wave channel sums: every wave parks its 64 channels' (s1, s2) in LDS, then one pass of
+// the workgroup adds the WPX pixel-group partials of each of its KT channels and issues ONE atomic per value: 2 * KT /
+// 256 full-wave atomic instructions per tile instead of 16-32 mostly-idle ones per wave (a memory-side float atomic
+// costs ~50 ns per wave-instruction per CU whatever its lane count: that, not bandwidth, made the epilogue slow).
+template <int WCH, int KT>
+__device__ __forceinline__ void halo_commit(float* red, float* rl, int k0, int Ncol, int bid) {
+  __syncthreads();
+  const int t = threadIdx.x;
+  if (t < 2 * KT) {
+    const int which = t / KT, c = t - which * KT, wc = c / 64, cl = c & 63;
+    float v = 0.f;
+#pragma unroll
+    for (int wp = 0; wp < 4 / WCH; ++wp) v += rl[(wp * WCH + wc) * 128 + which * 64 + cl];
+    atomicAdd(red + (size_t)(bid & (BIGDL_STAT_SLOTS - 1)) * 2 * Ncol + which * Ncol + k0 + c, v);
+  }
+}
+
+// Lean form (no addend / consumer-BN reduction: the forward with optional bias, ReLU and BN statistics): the wave's
+// 64-channel tile goes through its LDS slice once as bf16 (bias added in fp32 before the rounding) ([pixel][8 granules], granule g of pixel p in slot g ^ (p & 7)),
+// then 8 lanes store one pixel's whole 128-byte row (16-byte buffer stores); statistics of the rounded output.
+template <int FM, int FN, int WCH, int KT, class RM>
+__device__ __forceinline__ void halo_epi_lean(const ConvArgs& a, v4f (&acc)[FM][FN], int vbase, int nbase, int lane,
+                                              int bid, unsigned char* sl, const RM& rm, float* rl0, int k0) {
+  float* rl = rl0 + (threadIdx.x >> 6) * 128;
+  static_assert(FN == 4, "64-channel wave tile");
+  constexpr int TM = FM * 16;
+  float bs[FN][4];
+#pragma unroll
+  for (int j = 0; j < FN; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) bs[j][e] = a.bias ? a.bias[nbase + j * 16 + 4 * (lane >> 4) + e] : 0.f;
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int p = i * 16 + (lane & 15), g = 2 * j + (lane >> 5);
+      const v2u w = {pack2bf(acc[i][j][0] + bs[j][0], acc[i][j][1] + bs[j][1]),
+                     pack2bf(acc[i][j][2] + bs[j][2], acc[i][j][3] + bs[j][3])};
+      *reinterpret_cast<v2u*>(sl + p * 128 + ((g ^ (p & 7)) << 4) + ((lane >> 4) & 1) * 8) = w;
+    }
+  const size_t rows = (size_t)a.Nb * a.OH * a.OW;
+  const __amdgpu_buffer_rsrc_t ro = rsrc_of(a.out, ((rows - 1) * a.ldo + a.Ncol) * 2);
+  const int q = lane & 7;
+  float s1[8], s2[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) s1[e] = s2[e] = 0.f;
+  const bool relu = a.relu != 0, st = a.stats != nullptr;
+#pragma unroll
+  for (int r = 0; r < TM / 8; ++r) {
+    const int p = r * 8 + (lane >> 3);
+    v4u o = *reinterpret_cast<const v4u*>(sl + p * 128 + ((q ^ (p & 7)) << 4));
+    const long orow = rm(a, vbase + p);
+    if (relu) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = pack2bf(fmaxf(lo_bf(o[e]), 0.f), fmaxf(hi_bf(o[e]), 0.f));
+    }
+    if (st) {
+      const float vm = orow >= 0 ? 1.f : 0.f;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float y0 = lo_bf(o[e]) * vm, y1 = hi_bf(o[e]) * vm;
+        s1[2 * e] += y0; s2[2 * e] += y0 * y0;
+        s1[2 * e + 1] += y1; s2[2 * e + 1] += y1 * y1;
+      }
+    }
+    const unsigned off = orow >= 0 ? (unsigned)(((size_t)orow * a.ldo + nbase + q * 8) * 2) : EOOB;
+    __builtin_amdgcn_raw_buffer_store_b128(o, ro, off, 0, 0);
+  }
+  if (st) {          // uniform: every wave of the workgroup takes this branch
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+#pragma unroll
+      for (int o = 8; o < 64; o <<= 1) {
+        s1[e] += __shfl_xor(s1[e], o, 64);
+        s2[e] += __shfl_xor(s2[e], o, 64);
+      }
+    if (lane < 8) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { rl[q * 8 + e] = s1[e]; rl[64 + q * 8 + e] = s2[e]; }
+    }
+    halo_commit<WCH, KT>(a.stats, rl0, k0, a.Ncol, bid);
+  }
+}
+
+
 }  // namespace

@@ -2797,6 +2797,7 @@ long bigdl_conv_nt_plan(ConvArgs* a) {
   if (a->pstride > 0 && a->pstride != a->Cs) return 0;   // overlapping windows: g4 only, no split-K
   if (conv_impl() == 1 && s1_applies(a)) return 0;
   if (conv_impl() == 1 && bigdl_conv_halo_applies(a)) return 0;
+  if (conv_impl() == 1 && bigdl_stem_fwd_applies(a)) return 0;
   if (g_conv_p8 < 0) (void)p8_pick(a);      // reads BIGDL_CONV_P8 once
   const int sk = sk_pick(a);
   if (sk > 0) {
@@ -2827,6 +2828,10 @@ int bigdl_conv_nt(const ConvArgs* a, hipStream_t st) {
   if (a->M <= 0) return 0;
   const bool fastk = (a->Cs % BK) == 0;
   const int impl = conv_impl();
+  if (impl == 1 && bigdl_stem_fwd_applies(a) && bigdl_stem_fwd(a, st) == 0) {
+    HIP_LAUNCH_CHECK();
+    return 0;
+  }
   if (a->pstride > 0 && a->pstride != a->Cs) {   // overlapping-window source: the g4 kernel is the one that reads it
     if ((a->Ncol & 7) || (a->ldo & 7) || a->out32 || a->ws || a->bnred || !(fastk || a->Kdim % 8 == 0)) return -4;
     if (a->Ncol <= 64) launch_nt_g4<64, 3>(*a, st);

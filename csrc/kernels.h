@@ -71,6 +71,10 @@ int bigdl_conv_nt(const ConvArgs* a, hipStream_t st);
 int bigdl_conv_halo_applies(const ConvArgs* a);
 int bigdl_conv_halo(const ConvArgs* a, hipStream_t st);
 void bigdl_set_conv_halo(int v);
+// 7x7 / stride-2 pair-view image stem forward (stem_fwd.hip)
+int bigdl_stem_fwd_applies(const ConvArgs* a);
+int bigdl_stem_fwd(const ConvArgs* a, hipStream_t st);
+void bigdl_set_stem_fwd(int v);
 // Kernel choice for bigdl_conv_nt: sets a->ksplit and returns the fp32 workspace elements it needs (0: none).
 long bigdl_conv_nt_plan(ConvArgs* a);
 // Batched NT GEMM (bmm.hip): C[b][m][n] (=|+=) alpha * sum_k A[b][m][k] B[b][n][k]; A, B bf16 K-contiguous (K % 32

@@ -128,6 +128,7 @@ PAIR_CASES = [
     (3, 16, 3, (2, 2), 1, 2, 29, 31),      # odd sizes, 3x3
     (4, 32, 5, (1, 2), 2, 2, 20, 26),      # height stride 1
     (1, 8, 7, (2, 2), 0, 3, 23, 23),       # 1 channel, no padding
+    (3, 64, 7, (2, 2), 3, 2, 224, 224),    # ImageNet stem: the dedicated halo kernel (csrc/stem_fwd.hip)
 ]
 
 
@@ -155,6 +156,45 @@ def test_stem_pixel_pair_conv_matches_cpu(case):
     assert _rel(gg, gc) < 2e-2, _rel(gg, gc)
     for a, b in zip(gpu.parameters()[1], cpu.parameters()[1]):
         assert _rel(a, b) < 1e-2, (a.shape, _rel(a, b))
+
+
+def test_stem_fwd_kernel_matches_gemm_path():
+    """The dedicated 7x7/2 stem kernel (csrc/stem_fwd.hip: input-row halo in LDS, 7 row-tap K-steps, lean epilogue)
+    against fp32 torch and against the implicit-GEMM path it replaces (BIGDL_STEM_FWD off): output, bias + ReLU,
+    BN statistics of the rounded output."""
+    import torch.nn.functional as F
+
+    from bigdl_amd.ops import bn as bnops
+    from bigdl_amd.ops import conv as cv
+    from bigdl_amd.ops import native
+
+    C_ = native.get()
+    torch.manual_seed(5)
+    N = 3
+    x = torch.randn(N, 3, 224, 224, device="cuda")
+    w = (torch.randn(64, 3, 7, 7, device="cuda") * 0.1).to(torch.bfloat16)
+    b = torch.randn(64, device="cuda")
+    OH, OW, S2, _, _ = cv.pair_geometry(224, 224, 7, 7, 2, 3, 3)
+    xp = cv.to_pairs_bf16(x, 7, 7, 2, 3, 3)
+    wp = cv.pair_weight(w.contiguous(memory_format=torch.channels_last))
+    ref = F.conv2d(x.to(torch.bfloat16).float(), w.float(), stride=2, padding=3)
+    res = {}
+    for on in (1, 0):
+        C_.set_stem_fwd(on)
+        try:
+            st = bnops.new_stats(64, "cuda")
+            y = cv.conv2d_pairs_fwd(xp, wp, None, 64, OH, OW, 7, S2, 2, stats=st)
+            y2 = cv.conv2d_pairs_fwd(xp, wp, b, 64, OH, OW, 7, S2, 2, relu=True)
+            torch.cuda.synchronize()
+            res[on] = (y, st, y2)
+        finally:
+            C_.set_stem_fwd(1)
+    y, st, y2 = res[1]
+    assert _rel(y, ref) < 1e-2 and _rel(y, res[0][0]) < 1e-2
+    assert _rel(y2, torch.relu(ref + b.view(1, -1, 1, 1))) < 1e-2
+    s2 = st.view(bnops.stat_slots(), 2, 64).sum(0)
+    assert _rel(s2[0], y.float().sum(dim=(0, 2, 3))) < 1e-4
+    assert _rel(s2[1], (y.float() ** 2).sum(dim=(0, 2, 3))) < 1e-4
 
 
 def _bmm_case(name):
