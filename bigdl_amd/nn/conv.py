@@ -306,6 +306,9 @@ class SpatialConvolution(TensorModule):
             xs = (x.shape[0], Cp, x.shape[2], x.shape[3])
             addend = getattr(self, "_dgrad_addend", None)
             self._dgrad_addend = None
+            addend_zm = None
+            if isinstance(addend, tuple):       # (gradient, sign mask): add gradient where the mask bit is set
+                addend, addend_zm = addend
             if addend is not None and Cp != x.shape[1]:
                 raise RuntimeError("dgrad addend requires unpadded channels")
             bn = None
@@ -318,7 +321,7 @@ class SpatialConvolution(TensorModule):
                 bn = {"x": bx, "z": bz, "zm": bzm, "mean": bmean, "aff": baff,
                       "red": bnops.new_stats(Cp, gy16.device)}
             gi = cv.conv2d_dgrad(gy16, wt, xs, (self.strideH, self.strideW), (ph, pw),
-                                 (self.dilationH, self.dilationW), addend=addend, bn=bn)
+                                 (self.dilationH, self.dilationW), addend=addend, bn=bn, addend_zm=addend_zm)
             if Cp != x.shape[1]:
                 gi = gi[:, : x.shape[1]].contiguous(memory_format=CL)
             elif bn is not None and bn.get("done"):

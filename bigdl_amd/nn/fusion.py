@@ -18,6 +18,8 @@ work the producer already did.
 """
 import os
 
+import torch
+
 from ..utils.table import Table
 from .activation import ReLU
 from .containers import ConcatTable, Sequential, add_activity
@@ -238,22 +240,42 @@ def residual_forward(seq, x):
     return out
 
 
+# measured neutral on ResNet-50 (bn_bwd_apply -0.4 ms, the residual dgrad epilogues +0.3 ms: byte mask loads),
+# so off by default (BIGDL_MASKED_ADDEND=1 enables it)
+MASKED_ADDEND = [os.environ.get("BIGDL_MASKED_ADDEND", "0") != "0"]
+
+
 def residual_backward(seq, x, gradOutput):
     branch, short, bn = seq._residual_plan
-    dh, dres = bn.backward_fused(seq._res_h, gradOutput, need_dres=True)
-    bn.gradInput = dh
-    # shortcut first, so its gradient can be summed inside the epilogue of the branch's first dgrad GEMM
-    gs = short.backward(x, dres)
     mods = branch.modules
     first = mods[0]
-    fold = (isinstance(first, SpatialConvolution) and first.propagateBack and first.nGroup == 1
-            and first.format == "NCHW" and first.nInputPlane % 8 == 0 and gs is not None
-            and gs.dtype == x.dtype and gs.shape == x.shape)
+    can_fold = (isinstance(first, SpatialConvolution) and first.propagateBack and first.nGroup == 1
+                and first.format == "NCHW" and first.nInputPlane % 8 == 0)
+    # identity shortcut: its gradient dres = dz * (y > 0) is never materialised; the block's output gradient and the
+    # BN's sign mask go to the first dgrad GEMM, whose epilogue adds dz where the mask bit is set (one bf16 write
+    # pass less per block: csrc/kernels.h ConvArgs::addzm)
+    masked = None
+    zm = getattr(bn, "_zm", None)
+    if (MASKED_ADDEND[0] and can_fold and zm is not None and type(short).__name__ == "Identity" and first.strideH == 1
+            and first.strideW == 1 and torch.is_tensor(gradOutput) and gradOutput.is_cuda
+            and tuple(gradOutput.shape) == tuple(x.shape) and x.dtype == torch.bfloat16):
+        dh, _ = bn.backward_fused(seq._res_h, gradOutput, need_dres=False)
+        gz = gradOutput
+        if gz.dtype != torch.bfloat16 or not gz.is_contiguous(memory_format=torch.channels_last):
+            gz = gz.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        masked = (gz, zm)
+        gs = None
+    else:
+        dh, dres = bn.backward_fused(seq._res_h, gradOutput, need_dres=True)
+        # shortcut first, so its gradient can be summed inside the epilogue of the branch's first dgrad GEMM
+        gs = short.backward(x, dres)
+    bn.gradInput = dh
+    fold = masked is not None or (can_fold and gs is not None and gs.dtype == x.dtype and gs.shape == x.shape)
     g = dh
     for i in range(len(mods) - 2, -1, -1):
         inp = mods[i - 1].output if i > 0 else x
         if i == 0 and fold:
-            first._dgrad_addend = gs
+            first._dgrad_addend = masked if masked is not None else gs
             # with the shortcut gradient folded in, the dgrad output is the complete gradient of the block
             # input: if that is the previous block's output, its last BN's reduction can run in the epilogue
             first._dgrad_bn_once = _dgrad_bn_enabled()

@@ -156,7 +156,7 @@ def dgrad_phases(H, W, R, S, stride, pad, dil):
     return res
 
 
-def conv2d_dgrad(dy, w16t, x_shape, stride, pad, dil=(1, 1), out=None, addend=None, bn=None):
+def conv2d_dgrad(dy, w16t, x_shape, stride, pad, dil=(1, 1), out=None, addend=None, bn=None, addend_zm=None):
     """dx = conv_transpose(dy, w) [+ addend]. ``w16t`` is the (C, R, S, K)-ordered transposed weight.
 
     Stride > 1 runs one dense implicit GEMM per stride phase (no zero-insertion, no masked MFMAs).
@@ -165,7 +165,8 @@ def conv2d_dgrad(dy, w16t, x_shape, stride, pad, dil=(1, 1), out=None, addend=No
 
     ``bn`` = {"x", "z", "mean", "aff", "red"[, "zm"]}: dx is the gradient of a training BatchNorm's (ReLU-fused)
     output (ReLU mask from z, or its sign mask zm, or x * aff), and the epilogue also accumulates that BN's backward reduction into ``red`` (the pass
-    bn_bwd_reduce would make over dx and x). Only when every pixel of dx is written by a GEMM phase (or the
+    bn_bwd_reduce would make over dx and x). ``addend_zm`` (uint8 sign mask, [P][C / 8]): the addend is added only
+    where its bit is set (every pixel must be covered by a GEMM phase). Only when every pixel of dx is written by a GEMM phase (or the
     uncovered pixels are zero); ``bn["done"]`` reports whether it ran.
     """
     N, C, H, W = x_shape
@@ -177,6 +178,8 @@ def conv2d_dgrad(dy, w16t, x_shape, stride, pad, dil=(1, 1), out=None, addend=No
         addend = addend.contiguous(memory_format=CL)
     if out is None:
         out = torch.empty((N, C, H, W), dtype=BF16, device=dy.device, memory_format=CL)
+    if addend_zm is not None and (addend is None or covered != H * W):
+        raise ValueError("conv2d_dgrad: a masked addend needs an addend and a data gradient that covers every pixel")
     if covered != H * W:
         # pixels no phase reaches: zeros, or the folded residual addend (the phase GEMMs add it to theirs)
         mask = 0
@@ -199,7 +202,7 @@ def conv2d_dgrad(dy, w16t, x_shape, stride, pad, dil=(1, 1), out=None, addend=No
         bn["done"] = True
     for (a, b, nI, nJ, taps) in phases:
         geo = [N, OH, OW, K, nI, nJ, 1, 1, ldw, C, C, H, W, stride[0], stride[1], a, b]
-        C_.conv_nt(dy, w16t, out, None, None, geo, taps, False, addend, **bnk)
+        C_.conv_nt(dy, w16t, out, None, None, geo, taps, False, addend, addend_zm=addend_zm, **bnk)
     return out
 
 

@@ -41,7 +41,7 @@ uint8_t* omzm(const OptT& t, int64_t P, int64_t C, const char* n) {
 void conv_nt(const Tensor& src, const Tensor& wt, const Tensor& out, const OptT& bias, const OptT& stats,
              std::vector<int64_t> geo, std::vector<int64_t> taps, bool relu, const OptT& addend, const OptT& bn_x,
              const OptT& bn_z, const OptT& bn_mean, const OptT& bn_aff, const OptT& bn_red, bool accumulate,
-             const OptT& bn_zm) {
+             const OptT& bn_zm, const OptT& addend_zm) {
   TORCH_CHECK(geo.size() == 17 || geo.size() == 18, "conv_nt: bad geometry");
   if (stats && stats->defined())
     TORCH_CHECK(stats->numel() >= BIGDL_STAT_SLOTS * 2 * geo[9], "conv_nt: stats must hold STAT_SLOTS x 2Ncol");
@@ -56,6 +56,11 @@ void conv_nt(const Tensor& src, const Tensor& wt, const Tensor& out, const OptT&
   if (a.addend) TORCH_CHECK(addend->numel() == out.numel(), "conv_nt: addend must match out");
   a.bnx = ocbf(bn_x, "bn_x"); a.bnz = ocbf(bn_z, "bn_z"); a.bnmean = ocf(bn_mean, "bn_mean");
   a.bnaff = ocf(bn_aff, "bn_aff"); a.bnred = omf(bn_red, "bn_red");
+  a.addzm = nullptr;
+  if (addend_zm && addend_zm->defined()) {
+    TORCH_CHECK(a.addend && geo[10] == geo[9] && geo[9] % 8 == 0, "conv_nt: a masked addend needs ldo == Ncol");
+    a.addzm = omzm(addend_zm, out.numel() / geo[9], geo[9], "addend_zm");
+  }
   a.bnzm = nullptr;
   if (bn_zm && bn_zm->defined()) {
     TORCH_CHECK(geo[10] == geo[9] && geo[9] % 8 == 0, "conv_nt: a sign-mask z needs a dense output (ldo == Ncol)");
@@ -509,7 +514,8 @@ void conv_i8(const Tensor& src, const Tensor& wt, const Tensor& out, const OptT&
   a.out = reinterpret_cast<uint16_t*>(out.data_ptr());
   a.bias = ocf(bias, "bias"); a.stats = nullptr; a.addend = nullptr; a.out32 = nullptr; a.accum32 = 0;
   a.ws = nullptr; a.ksplit = 0; a.pstride = 0;
-  a.bnx = nullptr; a.bnz = nullptr; a.bnzm = nullptr; a.bnmean = nullptr; a.bnaff = nullptr; a.bnred = nullptr;
+  a.bnx = nullptr; a.bnz = nullptr; a.bnzm = nullptr; a.addzm = nullptr; a.bnmean = nullptr; a.bnaff = nullptr;
+  a.bnred = nullptr;
   a.Nb = geo[0]; a.Hs = geo[1]; a.Ws = geo[2]; a.Cs = geo[3]; a.OH = geo[4]; a.OW = geo[5];
   a.mul_h = geo[6]; a.mul_w = geo[7]; a.ldw = geo[8]; a.Ncol = geo[9]; a.ldo = geo[10];
   a.OHo = geo[11]; a.OWo = geo[12]; a.omul_h = geo[13]; a.omul_w = geo[14]; a.ooff_h = geo[15]; a.ooff_w = geo[16];
@@ -1232,7 +1238,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_nt", &conv_nt, py::arg("src"), py::arg("wt"), py::arg("out"), py::arg("bias"), py::arg("stats"),
         py::arg("geo"), py::arg("taps"), py::arg("relu"), py::arg("addend") = py::none(), py::arg("bn_x") = py::none(),
         py::arg("bn_z") = py::none(), py::arg("bn_mean") = py::none(), py::arg("bn_aff") = py::none(),
-        py::arg("bn_red") = py::none(), py::arg("accumulate") = false, py::arg("bn_zm") = py::none());
+        py::arg("bn_red") = py::none(), py::arg("accumulate") = false, py::arg("bn_zm") = py::none(),
+        py::arg("addend_zm") = py::none());
   m.def("conv_wgrad", &conv_wgrad);
   m.def("transpose_krsc", &transpose_krsc);
   m.def("bn_stats", &bn_stats);
@@ -1358,6 +1365,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_conv_s1", &bigdl_set_conv_s1);
   m.def("set_conv_halo", &bigdl_set_conv_halo);
   m.def("set_stem_fwd", &bigdl_set_stem_fwd);
+  m.def("set_stem_wgrad", &bigdl_set_stem_wgrad);
   m.def("cu_masked_stream", &cu_masked_stream, "HIP stream restricted to a CU mask (32 CUs per word)");
   m.def("set_conv_sk", &bigdl_set_conv_sk);
   m.def("set_wgrad_halo", &bigdl_set_wgrad_halo);

@@ -60,6 +60,13 @@ __device__ __forceinline__ v4u mask8_to_bf(unsigned b) {
   for (int e = 0; e < 4; ++e) r[e] = (((b >> (2 * e)) & 1u) ? 0x3f80u : 0u) | (((b >> (2 * e + 1)) & 1u) ? 0x3f800000u : 0u);
   return r;
 }
+// AND-mask of a 16-byte granule of 8 bf16 keeping element e where bit e of b is set (a masked residual addend)
+__device__ __forceinline__ v4u mask8_to_and(unsigned b) {
+  v4u r;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) r[e] = (((b >> (2 * e)) & 1u) ? 0xffffu : 0u) | (((b >> (2 * e + 1)) & 1u) ? 0xffff0000u : 0u);
+  return r;
+}
 // sign-mask byte of 8 bf16 values (bit e: value e > 0)
 __device__ __forceinline__ unsigned bf_to_mask8(const v4u& o) {
   unsigned b = 0;

@@ -74,7 +74,10 @@ __device__ __forceinline__ void nt_epilogue_lds(const ConvArgs& a, v4f (&acc)[MI
     px[rr] = v4u{0u, 0u, 0u, 0u};
     pz[rr] = v4u{0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
     if (orow >= 0) {
-      if (a.addend) pad[rr] = *reinterpret_cast<const v4u*>(a.addend + off);
+      if (a.addend) {
+        pad[rr] = *reinterpret_cast<const v4u*>(a.addend + off);
+        if (a.addzm) pad[rr] &= mask8_to_and(a.addzm[off >> 3]);
+      }
       if (bnw) {
         px[rr] = *reinterpret_cast<const v4u*>(a.bnx + off);
         if (a.bnzm) pz[rr] = mask8_to_bf(a.bnzm[off >> 3]);

@@ -117,6 +117,7 @@ __device__ __forceinline__ void halo_epi_full(const ConvArgs& a, v4f (&acc)[FM][
   const __amdgpu_buffer_rsrc_t rbx = rsrc_of(a.bnx, bnw ? nb2 : 0);
   const __amdgpu_buffer_rsrc_t rbz = rsrc_of(a.bnz, (bnw && a.bnz) ? nb2 : 0);
   const __amdgpu_buffer_rsrc_t rzm = rsrc_of(a.bnzm, (bnw && a.bnzm) ? nb2 / 16 : 0);
+  const __amdgpu_buffer_rsrc_t rzad = rsrc_of(a.addzm, a.addzm ? nb2 / 16 : 0);
   const int c4 = 4 * (lane >> 4);
   float bs[FN][4], mu[FN][4], sc[FN][4], sh[FN][4], s1[FN][4], s2[FN][4];
 #pragma unroll
@@ -140,7 +141,13 @@ __device__ __forceinline__ void halo_epi_full(const ConvArgs& a, v4f (&acc)[FM][
     for (int j = 0; j < FN; ++j) {
       const size_t el = (size_t)(orow >= 0 ? orow : 0) * a.ldo + nbase + j * 16 + c4;
       const unsigned off = orow >= 0 ? (unsigned)(el * 2) : EOOB;
-      const v2u ad = __builtin_amdgcn_raw_buffer_load_b64(rad, off, 0, 0);
+      v2u ad = __builtin_amdgcn_raw_buffer_load_b64(rad, off, 0, 0);
+      if (a.addzm) {
+        const unsigned zb2 = __builtin_amdgcn_raw_buffer_load_b8(rzad, orow >= 0 ? (unsigned)(el >> 3) : EOOB, 0, 0);
+        const unsigned bits = (zb2 >> (el & 7)) & 0xfu;
+        ad[0] &= ((bits & 1u) ? 0xffffu : 0u) | ((bits & 2u) ? 0xffff0000u : 0u);
+        ad[1] &= ((bits & 4u) ? 0xffffu : 0u) | ((bits & 8u) ? 0xffff0000u : 0u);
+      }
       const v2u bx = __builtin_amdgcn_raw_buffer_load_b64(rbx, off, 0, 0);
       const v2u bz = __builtin_amdgcn_raw_buffer_load_b64(rbz, off, 0, 0);
       const unsigned zb = __builtin_amdgcn_raw_buffer_load_b8(rzm, orow >= 0 ? (unsigned)(el >> 3) : EOOB, 0, 0);

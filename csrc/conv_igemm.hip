@@ -73,6 +73,13 @@ __device__ __forceinline__ void nt_epilogue(const ConvArgs& a, v4f (&acc)[MI][NI
 #pragma unroll
           for (int e = 0; e < 4; ++e) ad[e] = (nb + e < a.Ncol) ? bf2f(ap[e]) : 0.f;
         }
+        if (a.addzm) {
+          const size_t el = (size_t)orow * a.ldo + nb;
+          const unsigned bits = (a.addzm[el >> 3] >> (el & 7)) & 0xfu;
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (!((bits >> e) & 1u)) ad[e] = 0.f;
+        }
       }
       float v[4];
 #pragma unroll
@@ -2305,6 +2312,7 @@ __global__ __launch_bounds__(256, 2) void conv_nt_s1_kernel(ConvArgs a) {
         const int m = min(p0 + rr * 8 + (lane >> 3), a.M - 1);
         const size_t off = (size_t)m * a.ldo + n;
         pad[rr] = a.addend ? *reinterpret_cast<const v4u*>(a.addend + off) : v4u{0u, 0u, 0u, 0u};
+        if (a.addzm) pad[rr] &= mask8_to_and(a.addzm[off >> 3]);
         px[rr] = bnw ? *reinterpret_cast<const v4u*>(a.bnx + off) : v4u{0u, 0u, 0u, 0u};
         pz[rr] = (bnw && a.bnzm) ? mask8_to_bf(a.bnzm[off >> 3])
                  : (bnw && a.bnz) ? *reinterpret_cast<const v4u*>(a.bnz + off)
@@ -2497,7 +2505,8 @@ __global__ __launch_bounds__(256) void conv_splitk_epilogue_kernel(ConvArgs a, l
       }
       const size_t off = (size_t)orow * a.ldo + n;
       if (a.addend) {
-        const v4u q = *reinterpret_cast<const v4u*>(a.addend + off);
+        v4u q = *reinterpret_cast<const v4u*>(a.addend + off);
+        if (a.addzm) q &= mask8_to_and(a.addzm[off >> 3]);
 #pragma unroll
         for (int e = 0; e < 4; ++e) { v[2 * e] += lo_bf(q[e]); v[2 * e + 1] += hi_bf(q[e]); }
       }
@@ -3003,6 +3012,13 @@ int bigdl_conv_wgrad_uses_p8(const WgradArgs* a_in) {
 }
 
 long bigdl_conv_wgrad_plan(WgradArgs* a) {
+  if (conv_impl() >= 1) {
+    const long sw = bigdl_stem_wgrad_plan(a);
+    if (sw > 0) {
+      a->splits = -1;                        // the pair-view stem kernel (stem_fwd.hip)
+      return sw;
+    }
+  }
   const int hs = bigdl_wgrad_halo_plan(a);
   if (hs > 0) {
     a->splits = hs;
@@ -3049,6 +3065,11 @@ int bigdl_conv_wgrad(const WgradArgs* a_in, hipStream_t st) {
 
 static int conv_wgrad_impl(const WgradArgs* a_in, hipStream_t st) {
   WgradArgs a = *a_in;
+  if (a.splits == -1 && a.ws != nullptr && bigdl_stem_wgrad_plan(&a) > 0) {
+    const int rc = bigdl_stem_wgrad(&a, st);
+    HIP_LAUNCH_CHECK();
+    return rc;
+  }
   if (a.Cs % 8 != 0 || a.Ncol % 8 != 0 || a.Kdim % 8 != 0) return -1;
   {
     WgradArgs b = a;

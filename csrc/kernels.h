@@ -17,6 +17,8 @@ struct ConvArgs {
   const float* bias;
   float* stats;
   const uint16_t* addend;   // optional [rows][ldo] bf16 added in the epilogue (same placement as out)
+  const uint8_t* addzm;     // optional sign mask of the addend ([rows][Ncol / 8] bytes, ldo == Ncol): the addend is
+                            // added only where its bit is set (a ResNet block's residual gradient dz * (y > 0))
   // Optional BN-backward reduction of the consumer BatchNorm (data-gradient GEMMs only): with bnred set the
   // epilogue accumulates sum(dm) and sum(dm * (x - mean)) per channel into [STAT_SLOTS][2][Ncol] slots, where
   // dm = out masked by the fused ReLU (z > 0 when bnz is set, else x * aff[c] + aff[Ncol + c] > 0, else no mask)
@@ -75,6 +77,9 @@ void bigdl_set_conv_halo(int v);
 int bigdl_stem_fwd_applies(const ConvArgs* a);
 int bigdl_stem_fwd(const ConvArgs* a, hipStream_t st);
 void bigdl_set_stem_fwd(int v);
+long bigdl_stem_wgrad_plan(const WgradArgs* a);
+int bigdl_stem_wgrad(const WgradArgs* a, hipStream_t st);
+void bigdl_set_stem_wgrad(int v);
 // Kernel choice for bigdl_conv_nt: sets a->ksplit and returns the fp32 workspace elements it needs (0: none).
 long bigdl_conv_nt_plan(ConvArgs* a);
 // Batched NT GEMM (bmm.hip): C[b][m][n] (=|+=) alpha * sum_k A[b][m][k] B[b][n][k]; A, B bf16 K-contiguous (K % 32

@@ -197,6 +197,46 @@ def test_stem_fwd_kernel_matches_gemm_path():
     assert _rel(s2[1], (y.float() ** 2).sum(dim=(0, 2, 3))) < 1e-4
 
 
+def test_stem_wgrad_kernel_matches_gemm_path():
+    """The pair-view stem weight-gradient kernel (csrc/stem_fwd.hip: 7 row-tap waves, transposed LDS reads of dy rows
+    and overlapping input windows, fixed-order partial reduce) against the split-K implicit-GEMM path (off) and fp32
+    torch; the bias gradient too."""
+    from bigdl_amd.ops import conv as cv
+    from bigdl_amd.ops import native
+
+    C_ = native.get()
+    torch.manual_seed(6)
+    N = 3
+    x = torch.randn(N, 3, 224, 224, device="cuda")
+    dy = torch.randn(N, 64, 112, 112, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    xp = cv.to_pairs_bf16(x, 7, 7, 2, 3, 3)
+    S2 = 4
+    res = {}
+    for on in (1, 0):
+        C_.set_stem_wgrad(on)
+        try:
+            dwp = torch.zeros(64, 7 * S2 * 8, device="cuda")
+            db = torch.zeros(64, device="cuda")
+            cv.conv2d_pairs_wgrad(dy, xp, 7, S2, 2, dwp, db)
+            torch.cuda.synchronize()
+            res[on] = (dwp, db)
+        finally:
+            C_.set_stem_wgrad(1)
+    assert _rel(res[1][0], res[0][0]) < 1e-3, _rel(res[1][0], res[0][0])
+    assert _rel(res[1][1], res[0][1]) < 1e-4
+    ref = torch.nn.grad.conv2d_weight(x.to(torch.bfloat16).float(), (64, 3, 7, 7), dy.float(), stride=2, padding=3)
+    # pair layout back to (K, C, R, S): w'[k][r][j][e * 4 + c] = w[k][c][r][2 j + e]
+    wpv = res[1][0].view(64, 7, S2, 2, 4)
+    got = torch.zeros(64, 3, 7, 7, device="cuda")
+    for j in range(S2):
+        for e in range(2):
+            s_ = 2 * j + e
+            if s_ < 7:
+                got[:, :, :, s_] = wpv[:, :, j, e, :3].permute(0, 2, 1)
+    assert _rel(got, ref) < 1e-2, _rel(got, ref)
+    assert _rel(res[1][1], dy.float().sum(dim=(0, 2, 3))) < 1e-3
+
+
 def _bmm_case(name):
     from bigdl_amd import nn
     from bigdl_amd.utils.table import Table

@@ -81,6 +81,46 @@ def test_bottleneck_block_fused_matches_cpu(stride, nin, n):
     assert _cos(fg, fc) > 0.97
 
 
+def test_bottleneck_masked_residual_addend(monkeypatch):
+    """Identity-shortcut block with the masked residual addend (nn.fusion.MASKED_ADDEND: the shortcut gradient
+    dz * (y > 0) is never written; the first dgrad GEMM adds dz where the BN sign mask is set) against the dres path:
+    same input gradient and weight gradients (up to fp32 atomic order), and the masked path actually ran."""
+    from bigdl_amd.models.resnet import _Builder
+    from bigdl_amd.nn import fusion
+    from bigdl_amd.nn.fusion import fuse_for_training
+    from bigdl_amd.ops import conv as cv
+
+    b = _Builder("B", True)
+    b.iChannels = 256
+    blk = b.bottleneck(64, 1)
+    _randomize_bn(blk)
+    seen = []
+    orig = cv.conv2d_dgrad
+
+    def spy(*a, **k):
+        seen.append(k.get("addend_zm") is not None)
+        return orig(*a, **k)
+
+    monkeypatch.setattr(cv, "conv2d_dgrad", spy)
+    torch.manual_seed(1)
+    x = torch.randn(4, 256, 14, 14).cuda().to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    gy = torch.randn(4, 256, 14, 14).cuda().to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    res = {}
+    for on in (True, False):
+        m = copy.deepcopy(blk).to("cuda")
+        fuse_for_training(m)
+        fusion.MASKED_ADDEND[0] = on
+        try:
+            m.forward(x)
+            g = m.backward(x, gy)
+        finally:
+            fusion.MASKED_ADDEND[0] = False
+        res[on] = (g.float().clone(), _weight_grads(m))
+    assert any(seen)
+    assert _rel(res[True][0], res[False][0]) < 1e-5
+    assert _rel(res[True][1], res[False][1]) < 1e-4
+
+
 @pytest.mark.parametrize("depth,dataset,img", [(50, "ImageNet", 224), (20, "CIFAR10", 32)])
 def test_resnet_gpu_matches_cpu(depth, dataset, img):
     """Whole network: bf16 activations through 50 layers with batch-4 BN statistics drift a few percent
