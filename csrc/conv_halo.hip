@@ -426,11 +426,13 @@ extern "C" {
 
 void bigdl_set_conv_halo(int v) { g_conv_halo = v; }
 
-// 1 when bigdl_conv_halo takes this forward / data-gradient GEMM (BIGDL_CONV_HALO=0 turns it off)
+// 1 when bigdl_conv_halo takes this forward / data-gradient GEMM (BIGDL_CONV_HALO=0 turns it off; 2 / 3: see below)
 int bigdl_conv_halo_applies(const ConvArgs* a) {
   if (g_conv_halo < 0) {
     const char* e = getenv("BIGDL_CONV_HALO");
-    g_conv_halo = e ? atoi(e) : 1;
+    // default 2: forwards only. The data gradients' full epilogue (per-fragment loads of BN x / masks in front of its
+    // stores) made them slower in the training step than the im2col kernels: 24.51-24.57 vs 24.33-24.35 ms/step
+    g_conv_halo = e ? atoi(e) : 2;
   }
   if (!g_conv_halo || a->ntaps != 9 || a->mul_h != 1 || a->mul_w != 1 || !a->ident_out || a->out32 || a->pstride ||
       a->Hs != a->OH || a->Ws != a->OW || a->Hs != a->Ws || a->Kdim != 9 * a->Cs || (a->Cs % 32) ||
@@ -439,6 +441,9 @@ int bigdl_conv_halo_applies(const ConvArgs* a) {
   const int W = a->Ws;
   const int kt = W == 56 ? 64 : 128;
   if (W != 56 && W != 28 && W != 14 && W != 7) return 0;
+  // 2: only GEMMs with the lean epilogue (forwards); 3: also the full epilogue (data gradients) except at 56 x 56
+  const bool lean = a->addend == nullptr && (a->bnred == nullptr || a->stats != nullptr);
+  if ((g_conv_halo == 2 && !lean) || (g_conv_halo == 3 && !lean && W == 56)) return 0;
   if (a->Ncol % kt) return 0;
   unsigned seen = 0;
   for (int t = 0; t < 9; ++t) {
