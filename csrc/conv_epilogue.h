@@ -230,7 +230,9 @@ __device__ __forceinline__ void halo_commit(float* red, float* rl, int k0, int N
 // Lean form (no addend / consumer-BN reduction: the forward with optional bias, ReLU and BN statistics): the wave's
 // 64-channel tile goes through its LDS slice once as bf16 (bias added in fp32 before the rounding) ([pixel][8 granules], granule g of pixel p in slot g ^ (p & 7)),
 // then 8 lanes store one pixel's whole 128-byte row (16-byte buffer stores); statistics of the rounded output.
-template <int FM, int FN, int WCH, int KT, class RM>
+// BNR: also the consumer-BN backward reduction of the rounded output (data gradients; no addend): every BN x row and
+// mask byte of the wave's tile is loaded into registers BEFORE the first store, so no load waits behind a store.
+template <int FM, int FN, int WCH, int KT, bool BNR = false, class RM>
 __device__ __forceinline__ void halo_epi_lean(const ConvArgs& a, v4f (&acc)[FM][FN], int vbase, int nbase, int lane,
                                               int bid, unsigned char* sl, const RM& rm, float* rl0, int k0) {
   float* rl = rl0 + (threadIdx.x >> 6) * 128;
@@ -257,11 +259,52 @@ __device__ __forceinline__ void halo_epi_lean(const ConvArgs& a, v4f (&acc)[FM][
 #pragma unroll
   for (int e = 0; e < 8; ++e) s1[e] = s2[e] = 0.f;
   const bool relu = a.relu != 0, st = a.stats != nullptr;
+  // consumer-BN operands (BNR): x rows, and the ReLU mask as z rows or sign-mask bytes, or from x * scale + shift
+  constexpr int NRW = BNR ? TM / 8 : 1;
+  // (a bf16 z is not taken here: the caller routes it to the full epilogue; the sign mask stays one byte per row)
+  v4u px[NRW];
+  unsigned zbm[NRW];
+  float bmu[8], bsc[8], bsh[8];
+  int zmode = 0;
+  if constexpr (BNR) {
+    const size_t nb2 = ((rows - 1) * a.ldo + a.Ncol) * 2;
+    const __amdgpu_buffer_rsrc_t rbx = rsrc_of(a.bnx, nb2);
+    const __amdgpu_buffer_rsrc_t rzm = rsrc_of(a.bnzm, a.bnzm ? nb2 / 16 : 0);
+    zmode = a.bnzm ? 1 : a.bnaff ? 3 : 0;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int c = nbase + q * 8 + e;
+      bmu[e] = a.bnmean[c];
+      bsc[e] = a.bnaff ? a.bnaff[c] : 0.f;
+      bsh[e] = a.bnaff ? a.bnaff[a.Ncol + c] : 0.f;
+    }
+#pragma unroll
+    for (int r = 0; r < NRW; ++r) {
+      const long orow = rm(a, vbase + r * 8 + (lane >> 3));
+      const size_t el = (size_t)(orow >= 0 ? orow : 0) * a.ldo + nbase + q * 8;
+      const unsigned off = orow >= 0 ? (unsigned)(el * 2) : EOOB;
+      px[r] = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(rbx, off, 0, 0));
+      zbm[r] = zmode == 1 ? __builtin_amdgcn_raw_buffer_load_b8(rzm, orow >= 0 ? (unsigned)(el >> 3) : EOOB, 0, 0) : 0u;
+    }
+  }
 #pragma unroll
   for (int r = 0; r < TM / 8; ++r) {
     const int p = r * 8 + (lane >> 3);
     v4u o = *reinterpret_cast<const v4u*>(sl + p * 128 + ((q ^ (p & 7)) << 4));
     const long orow = rm(a, vbase + p);
+    if constexpr (BNR) {
+      const float vm = orow >= 0 ? 1.f : 0.f;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float x0 = lo_bf(px[r][e]), x1 = hi_bf(px[r][e]);
+        bool k0m = true, k1m = true;
+        if (zmode == 1) { k0m = (zbm[r] >> (2 * e)) & 1u; k1m = (zbm[r] >> (2 * e + 1)) & 1u; }
+        else if (zmode == 3) { k0m = x0 * bsc[2 * e] + bsh[2 * e] > 0.f; k1m = x1 * bsc[2 * e + 1] + bsh[2 * e + 1] > 0.f; }
+        const float d0 = k0m ? lo_bf(o[e]) * vm : 0.f, d1 = k1m ? hi_bf(o[e]) * vm : 0.f;
+        s1[2 * e] += d0; s2[2 * e] += d0 * (x0 - bmu[2 * e]);
+        s1[2 * e + 1] += d1; s2[2 * e + 1] += d1 * (x1 - bmu[2 * e + 1]);
+      }
+    }
     if (relu) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) o[e] = pack2bf(fmaxf(lo_bf(o[e]), 0.f), fmaxf(hi_bf(o[e]), 0.f));
@@ -278,7 +321,7 @@ __device__ __forceinline__ void halo_epi_lean(const ConvArgs& a, v4f (&acc)[FM][
     const unsigned off = orow >= 0 ? (unsigned)(((size_t)orow * a.ldo + nbase + q * 8) * 2) : EOOB;
     __builtin_amdgcn_raw_buffer_store_b128(o, ro, off, 0, 0);
   }
-  if (st) {          // uniform: every wave of the workgroup takes this branch
+  if (st || BNR) {          // uniform: every wave of the workgroup takes this branch
 #pragma unroll
     for (int e = 0; e < 8; ++e)
 #pragma unroll
@@ -290,7 +333,7 @@ __device__ __forceinline__ void halo_epi_lean(const ConvArgs& a, v4f (&acc)[FM][
 #pragma unroll
       for (int e = 0; e < 8; ++e) { rl[q * 8 + e] = s1[e]; rl[64 + q * 8 + e] = s2[e]; }
     }
-    halo_commit<WCH, KT>(a.stats, rl0, k0, a.Ncol, bid);
+    halo_commit<WCH, KT>(BNR ? a.bnred : a.stats, rl0, k0, a.Ncol, bid);
   }
 }
 

@@ -205,7 +205,7 @@ __device__ __forceinline__ void halo_epi_full(const ConvArgs& a, v4f (&acc)[FM][
 
 // ABL (timing ablations, BIGDL_CONV_HALO_ABL, wrong outputs): bit 0 no epilogue, bit 1 no MFMAs, bit 2 no DMA after
 // the prologue (stale LDS), bit 3 no fragment reads
-// EPI: 0 lean epilogue (no addend / consumer-BN reduction), 1 full epilogue
+// EPI: 0 lean epilogue (no addend / consumer-BN reduction), 2 lean + consumer-BN reduction, 1 full epilogue
 template <int W, int RB, int NIMG, int KT, int WPX, int EPI, int ABL = 0>
 __global__ __launch_bounds__(256, 2) void conv_halo_kernel(ConvArgs a) {
   using H = HaloF<W, RB, NIMG, KT, WPX>;
@@ -390,15 +390,18 @@ __global__ __launch_bounds__(256, 2) void conv_halo_kernel(ConvArgs a) {
   }
   const HaloRowMap<W, RB, NIMG> rm{n0, oh0, H::VR * WP};
   // per-wave channel sums go behind the bf16 slices (lean) or at the start of the idle LDS (full)
-  if constexpr (EPI == 0) {
+  if constexpr (EPI == 0 || EPI == 2) {
     static_assert(4 * H::TM * 128 + 4 * 128 * 4 <= H::LDS, "bf16 epilogue slices must fit the LDS");
-    halo_epi_lean<FM, FN, WCH, KT>(a, acc, wpx * H::TM, k0 + wch * H::TN, lane, bid, lds + wave * H::TM * 128, rm,
-                                   reinterpret_cast<float*>(lds + 4 * H::TM * 128), k0);
+    halo_epi_lean<FM, FN, WCH, KT, EPI == 2>(a, acc, wpx * H::TM, k0 + wch * H::TN, lane, bid,
+                                             lds + wave * H::TM * 128, rm,
+                                             reinterpret_cast<float*>(lds + 4 * H::TM * 128), k0);
   } else {
     halo_epi_full<FM, FN, WCH, KT>(a, acc, wpx * H::TM, k0 + wch * H::TN, lane, bid, rm, reinterpret_cast<float*>(lds),
                                    k0);
   }
 }
+
+int g_conv_halo_bn = 1;     // BIGDL_CONV_HALO_BN=0: data gradients with a BN reduction take the full epilogue
 
 template <int W, int RB, int NIMG, int KT, int WPX>
 void launch_halo_f(const ConvArgs& a, hipStream_t st) {
@@ -407,6 +410,8 @@ void launch_halo_f(const ConvArgs& a, hipStream_t st) {
   const int nwg = tiles_m * (a.Ncol / KT);
   static const int abl = [] { const char* e = getenv("BIGDL_CONV_HALO_ABL"); return e ? atoi(e) : 0; }();
   const bool lean = a.addend == nullptr && (a.bnred == nullptr || a.stats != nullptr);
+  const bool leanbn = a.addend == nullptr && a.bnred != nullptr && a.stats == nullptr && a.bias == nullptr &&
+                      (a.bnz == nullptr || a.bnzm != nullptr);
   const dim3 g(nwg), b(256);
   if (abl == 1) conv_halo_kernel<W, RB, NIMG, KT, WPX, 0, 1><<<g, b, 0, st>>>(a);
   else if (abl == 3) conv_halo_kernel<W, RB, NIMG, KT, WPX, 0, 3><<<g, b, 0, st>>>(a);
@@ -415,6 +420,7 @@ void launch_halo_f(const ConvArgs& a, hipStream_t st) {
   else if (abl == 13) conv_halo_kernel<W, RB, NIMG, KT, WPX, 0, 13><<<g, b, 0, st>>>(a);
   else if (abl == 15) conv_halo_kernel<W, RB, NIMG, KT, WPX, 0, 15><<<g, b, 0, st>>>(a);
   else if (lean) conv_halo_kernel<W, RB, NIMG, KT, WPX, 0><<<g, b, 0, st>>>(a);
+  else if (leanbn && g_conv_halo_bn) conv_halo_kernel<W, RB, NIMG, KT, WPX, 2><<<g, b, 0, st>>>(a);
   else conv_halo_kernel<W, RB, NIMG, KT, WPX, 1><<<g, b, 0, st>>>(a);
 }
 
@@ -430,9 +436,10 @@ void bigdl_set_conv_halo(int v) { g_conv_halo = v; }
 int bigdl_conv_halo_applies(const ConvArgs* a) {
   if (g_conv_halo < 0) {
     const char* e = getenv("BIGDL_CONV_HALO");
-    // default 2: forwards only. The data gradients' full epilogue (per-fragment loads of BN x / masks in front of its
-    // stores) made them slower in the training step than the im2col kernels: 24.51-24.57 vs 24.33-24.35 ms/step
-    g_conv_halo = e ? atoi(e) : 2;
+    // default 1: forwards and data gradients (those with a consumer-BN reduction and no addend take the lean
+    // epilogue with preloaded BN operands: 23.81 ms/step vs 24.20 with the data gradients on the im2col kernels;
+    // 2 = forwards only, 3 = all but the 56 x 56 data gradients)
+    g_conv_halo = e ? atoi(e) : 1;
   }
   if (!g_conv_halo || a->ntaps != 9 || a->mul_h != 1 || a->mul_w != 1 || !a->ident_out || a->out32 || a->pstride ||
       a->Hs != a->OH || a->Ws != a->OW || a->Hs != a->Ws || a->Kdim != 9 * a->Cs || (a->Cs % 32) ||

@@ -3022,7 +3022,7 @@ long bigdl_conv_wgrad_plan(WgradArgs* a) {
   const int hs = bigdl_wgrad_halo_plan(a);
   if (hs > 0) {
     a->splits = hs;
-    return hs > 1 ? (long)hs * a->Ncol * a->Kdim : 0;
+    return hs > 1 ? (long)hs * a->Ncol * a->Kdim + (a->dbias ? (long)hs * a->Ncol : 0) : 0;
   }
   const int p8w = p8w_pick(a);
   if (p8w > 0) {

@@ -206,11 +206,18 @@ __global__ __launch_bounds__(KB * 4, 1) void conv_wgrad_halo_kernel(WgradArgs a)
     }
 
   const unsigned lds_base = (unsigned)(uintptr_t)(LDS_PTR(unsigned char))lds;
-  v4f acc[9][4];
+  v4f acc[9][4], accb[4];
 #pragma unroll
   for (int i = 0; i < 9; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) accb[j] = v4f{0.f, 0.f, 0.f, 0.f};
+  // bias gradient (sum of dy over the pixels): the channel-block-0 waves of the first channel tile multiply their dy
+  // fragments by a ones operand as well (every row of the product is the column sum)
+  const bool bias = a.dbias != nullptr && c0 == 0 && cw == 0;
+  const v8s ones = {(short)0x3f80, (short)0x3f80, (short)0x3f80, (short)0x3f80,
+                    (short)0x3f80, (short)0x3f80, (short)0x3f80, (short)0x3f80};
 
   // prologue: stages 0 .. NS-2 in flight
 #pragma unroll
@@ -254,11 +261,25 @@ __global__ __launch_bounds__(KB * 4, 1) void conv_wgrad_halo_kernel(WgradArgs a)
 #pragma unroll
         for (int kb = 0; kb < 4; ++kb)
           acc[tp][kb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fx[tp % 3], fd[kb], acc[tp][kb], 0, 0, 0);
+        if (tp == 0 && bias) {
+#pragma unroll
+          for (int kb = 0; kb < 4; ++kb) accb[kb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, fd[kb], accb[kb], 0, 0, 0);
+        }
         __builtin_amdgcn_sched_barrier(0);
       }
     });
   }
 
+  // ---- bias: lanes 0..15 hold the column sums of k = k0 + kg * 64 + kb * 16 + lane (row 0 of the product)
+  if (bias && lane < 16) {
+    float* bp = a.ws ? a.ws + (size_t)a.splits * K * a.Kdim + (size_t)split * K : a.dbias;
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+      const int k = k0 + kg * 64 + kb * 16 + lane;
+      if (a.ws) bp[k] = accb[kb][0];
+      else bp[k] += accb[kb][0];
+    }
+  }
   // ---- out: lane holds dW[k][tap * C + c .. c + 3] (4 consecutive c of one k) per accumulator
   const int Kd = a.Kdim;
   float* base = a.ws ? a.ws + (size_t)split * K * Kd : a.dw;
@@ -314,6 +335,16 @@ __global__ __launch_bounds__(256) void halo_reduce_kernel(const float* __restric
   }
 }
 
+// dbias[k] += sum over splits of the bias partials, in split order
+__global__ __launch_bounds__(256) void halo_bias_reduce_kernel(const float* __restrict__ wsb, float* __restrict__ dbias,
+                                                              int K, int splits) {
+  const int k = blockIdx.x * 256 + threadIdx.x;
+  if (k >= K) return;
+  float t = 0.f;
+  for (int sp = 0; sp < splits; ++sp) t += wsb[(size_t)sp * K + k];
+  dbias[k] += t;
+}
+
 template <int W, int RB, int LDSKB>
 void launch_halo(const WgradArgs& a, hipStream_t st) {
   const int ntile = (a.Cs / 64) * (a.Ncol / (a.Ncol % 128 == 0 ? 128 : 64));
@@ -360,7 +391,7 @@ int bigdl_wgrad_halo_plan(WgradArgs* a) {
   const int rb = halo_rb(a->Ws);
   if (rb == 0 || a->R != 3 || a->S != 3 || a->sh != 1 || a->sw != 1 || a->ph != 1 || a->pw != 1 || a->dh != 1 ||
       a->dwl != 1 || a->OH != a->Hs || a->OW != a->Ws || (a->Hs % rb) || (a->Cs % 64) || (a->Ncol % 64) ||
-      a->Kdim != 9 * a->Cs || a->ldy != a->Ncol || a->dbias != nullptr || a->M != a->Nb * a->OH * a->OW || a->M <= 0)
+      a->Kdim != 9 * a->Cs || a->ldy != a->Ncol || a->M != a->Nb * a->OH * a->OW || a->M <= 0)
     return 0;
   const long stages = (long)a->Nb * (a->Hs / rb);
   const int ntile = (a->Cs / 64) * (a->Ncol / (a->Ncol % 128 == 0 ? 128 : 64));
@@ -374,7 +405,8 @@ int bigdl_wgrad_halo_plan(WgradArgs* a) {
 }
 
 // Launch (a->splits / m_per_split from bigdl_wgrad_halo_plan; a->ws = [splits][Ncol][Kdim] partials when splits > 1,
-// summed into a->dw by halo_reduce_kernel, else the kernel adds into a->dw).
+// then [splits][Ncol] bias partials when a->dbias, summed into a->dw / a->dbias in split order, else the kernel adds
+// into a->dw / a->dbias).
 int bigdl_wgrad_halo(const WgradArgs* a, hipStream_t st) {
   const int lds = halo_lds();
   switch (a->Ws) {
@@ -388,6 +420,9 @@ int bigdl_wgrad_halo(const WgradArgs* a, hipStream_t st) {
     const long n4 = (long)a->Ncol * a->Kdim / 4;
     const int aligned = (reinterpret_cast<uintptr_t>(a->dw) & 15) == 0;
     halo_reduce_kernel<<<dim3((unsigned)((n4 + 15) / 16)), dim3(256), 0, st>>>(a->ws, a->dw, n4, a->splits, aligned);
+    if (a->dbias)
+      halo_bias_reduce_kernel<<<dim3((unsigned)((a->Ncol + 255) / 256)), dim3(256), 0, st>>>(
+          a->ws + (size_t)a->splits * a->Ncol * a->Kdim, a->dbias, a->Ncol, a->splits);
   }
   return 0;
 }

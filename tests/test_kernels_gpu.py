@@ -865,7 +865,7 @@ def test_conv_s1_stream_kernel(case, zmask):
             res[s1] = (y, stats, y2, dx, red, bool(bn.get("done")))
         finally:
             C_.set_conv_s1(1)
-    y, stats, y2, dx, red, done = res[1]
+    y, stats, y2, dx, red, done, dx2, red2 = res[1]
     assert _rel(y, yr0) < 1e-2
     st2 = stats.view(bnops.stat_slots(), 2, K).sum(0)
     assert _rel(st2[0], y.float().sum(dim=(0, 2, 3))) < 1e-4
@@ -951,24 +951,30 @@ def test_conv_wgrad_halo_matches_fp32(case):
     x = torch.randn(N, C, H, H, device=dev).to(BF, memory_format=CL)
     gy = torch.randn(N, K, H, H, device=dev).to(BF, memory_format=CL)
     dw0 = torch.randn(K, C, 3, 3, device=dev).contiguous(memory_format=CL)
+    db0 = torch.randn(K, device=dev)
     ref = dw0 + torch.nn.grad.conv2d_weight(x.float(), (K, C, 3, 3), gy.float(), stride=1, padding=1)
+    refb = db0 + gy.float().sum(dim=(0, 2, 3))
     outs = []
     try:
         for on in (1, 0):
             native.get().set_wgrad_halo(on)
-            dw = dw0.clone()
-            cv.conv2d_wgrad(gy, x, dw, None, (1, 1), (1, 1))
+            dw, db = dw0.clone(), db0.clone()
+            cv.conv2d_wgrad(gy, x, dw, db, (1, 1), (1, 1))      # with the bias gradient (the ResNet convs have one)
+            dw2 = dw0.clone()
+            cv.conv2d_wgrad(gy, x, dw2, None, (1, 1), (1, 1))
             torch.cuda.synchronize()
-            outs.append(dw)
+            outs.append((dw, db, dw2))
     finally:
         native.get().set_wgrad_halo(1)
-    for dw in outs:
+    for dw, db, dw2 in outs:
         assert torch.isfinite(dw).all()
         assert _rel(dw, ref) < 5e-3, _rel(dw, ref)
-    assert _rel(outs[0], outs[1]) < 5e-3
+        assert _rel(dw2, ref) < 5e-3, _rel(dw2, ref)
+        assert _rel(db, refb) < 1e-3, _rel(db, refb)
+    assert _rel(outs[0][0], outs[1][0]) < 5e-3
 
 
-HALO_CASES = [
+HALO_FWD_CASES = [
     # N, C, H, K (3x3, stride 1, pad 1): conv_halo_kernel takes fwd / dgrad when H in {56, 28, 14, 7}, C % 32 == 0 and
     # the output channels are a multiple of its channel tile (64 at H 56, 128 below)
     (4, 64, 56, 64),       # ResNet-50 layer 2 shape (RB 4 row segments, top / bottom halo variants)
@@ -981,8 +987,16 @@ HALO_CASES = [
 ]
 
 
-@pytest.mark.parametrize("zmask", [False, True])
-@pytest.mark.parametrize("case", HALO_CASES)
+def _sign_mask(z):
+    """[P][C/8] uint8 sign bytes of an NHWC bf16 tensor (bit e of byte (p, g): z[p][8g + e] > 0)."""
+    N, C, H, W = z.shape
+    b = (z.permute(0, 2, 3, 1).reshape(-1, C // 8, 8) > 0).to(torch.int32)
+    w = (1 << torch.arange(8, device=z.device, dtype=torch.int32))
+    return (b * w).sum(-1).to(torch.uint8).reshape(-1).contiguous()
+
+
+@pytest.mark.parametrize("zmask", [False, True, "zm"])
+@pytest.mark.parametrize("case", HALO_FWD_CASES)
 def test_conv_halo_kernel(case, zmask):
     """3x3 / stride-1 / pad-1 halo-tile kernel (conv_halo.hip: one staged input halo per 32-channel chunk, 9 shifted
     LDS windows, weight ring) vs fp32 torch: forward + BN statistics, forward + bias + ReLU, data gradient + residual
@@ -1015,13 +1029,18 @@ def test_conv_halo_kernel(case, zmask):
             y = cv.conv2d_fwd(x, w, None, (1, 1), (1, 1), stats=stats)
             y2 = cv.conv2d_fwd(x, w, b32, (1, 1), (1, 1), relu=True)
             red = bnops.new_stats(C, dev)
-            bn = {"x": bx, "z": bz if zmask else None, "mean": mean, "aff": aff, "red": red}
+            bn = {"x": bx, "z": bz if zmask is True else None, "zm": _sign_mask(bz) if zmask == "zm" else None,
+                  "mean": mean, "aff": aff, "red": red}
             dx = cv.conv2d_dgrad(gy, cv.transpose_w(w), x.shape, (1, 1), (1, 1), addend=add, bn=bn)
+            # without the addend: the lean epilogue's consumer-BN reduction (the ResNet 3x3 data gradient)
+            red2 = bnops.new_stats(C, dev)
+            bn2 = dict(bn, red=red2)
+            dx2 = cv.conv2d_dgrad(gy, cv.transpose_w(w), x.shape, (1, 1), (1, 1), bn=bn2)
             torch.cuda.synchronize()
-            res[halo] = (y, stats, y2, dx, red, bool(bn.get("done")))
+            res[halo] = (y, stats, y2, dx, red, bool(bn.get("done")), dx2, red2)
         finally:
             C_.set_conv_halo(1)
-    y, stats, y2, dx, red, done = res[1]
+    y, stats, y2, dx, red, done, dx2, red2 = res[1]
     assert torch.isfinite(y.float()).all() and torch.isfinite(dx.float()).all()
     assert _rel(y, yr0) < 1e-2
     st2 = stats.view(bnops.stat_slots(), 2, K).sum(0)
@@ -1039,3 +1058,8 @@ def test_conv_halo_kernel(case, zmask):
     r2 = red.view(bnops.stat_slots(), 2, C).sum(0)
     assert _rel(r2[0], dm.sum(dim=(0, 2, 3))) < 1e-3
     assert _rel(r2[1], (dm * (bx.float() - mean.view(1, C, 1, 1))).sum(dim=(0, 2, 3))) < 1e-3
+    assert _rel(dx2, dxr - add.float()) < 1e-2
+    dm2 = dx2.float() * mask
+    r3 = red2.view(bnops.stat_slots(), 2, C).sum(0)
+    assert _rel(r3[0], dm2.sum(dim=(0, 2, 3))) < 1e-3
+    assert _rel(r3[1], (dm2 * (bx.float() - mean.view(1, C, 1, 1))).sum(dim=(0, 2, 3))) < 1e-3
