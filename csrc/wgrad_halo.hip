@@ -310,17 +310,19 @@ __global__ __launch_bounds__(256) void halo_reduce_kernel(const float* __restric
   __shared__ v4f red[16][17];
   const int e = threadIdx.x & 15, g = threadIdx.x >> 4;
   const long i = (long)blockIdx.x * 16 + e;
-  v4f s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
+  v4f s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f}, s2 = s0, s3 = s0;
   if (i < n4) {
     const v4f* w4 = reinterpret_cast<const v4f*>(ws);
     int sp = g;
-    for (; sp + 16 < splits; sp += 32) {
-      s0 += w4[(long)sp * n4 + i];
-      s1 += w4[(long)(sp + 16) * n4 + i];
+    // four independent loads in flight per trip (the partial rows are read once: latency, not bandwidth, bound)
+    for (; sp + 48 < splits; sp += 64) {
+      const v4f a0 = w4[(long)sp * n4 + i], a1 = w4[(long)(sp + 16) * n4 + i];
+      const v4f a2 = w4[(long)(sp + 32) * n4 + i], a3 = w4[(long)(sp + 48) * n4 + i];
+      s0 += a0; s1 += a1; s2 += a2; s3 += a3;
     }
-    if (sp < splits) s0 += w4[(long)sp * n4 + i];
+    for (; sp < splits; sp += 16) s0 += w4[(long)sp * n4 + i];
   }
-  red[g][e] = s0 + s1;
+  red[g][e] = (s0 + s1) + (s2 + s3);
   __syncthreads();
   if (g == 0 && i < n4) {
     v4f t = red[0][e];
@@ -333,16 +335,6 @@ __global__ __launch_bounds__(256) void halo_reduce_kernel(const float* __restric
       for (int k = 0; k < 4; ++k) dw[4 * i + k] += t[k];
     }
   }
-}
-
-// dbias[k] += sum over splits of the bias partials, in split order
-__global__ __launch_bounds__(256) void halo_bias_reduce_kernel(const float* __restrict__ wsb, float* __restrict__ dbias,
-                                                              int K, int splits) {
-  const int k = blockIdx.x * 256 + threadIdx.x;
-  if (k >= K) return;
-  float t = 0.f;
-  for (int sp = 0; sp < splits; ++sp) t += wsb[(size_t)sp * K + k];
-  dbias[k] += t;
 }
 
 template <int W, int RB, int LDSKB>
@@ -420,9 +412,10 @@ int bigdl_wgrad_halo(const WgradArgs* a, hipStream_t st) {
     const long n4 = (long)a->Ncol * a->Kdim / 4;
     const int aligned = (reinterpret_cast<uintptr_t>(a->dw) & 15) == 0;
     halo_reduce_kernel<<<dim3((unsigned)((n4 + 15) / 16)), dim3(256), 0, st>>>(a->ws, a->dw, n4, a->splits, aligned);
-    if (a->dbias)
-      halo_bias_reduce_kernel<<<dim3((unsigned)((a->Ncol + 255) / 256)), dim3(256), 0, st>>>(
-          a->ws + (size_t)a->splits * a->Ncol * a->Kdim, a->dbias, a->Ncol, a->splits);
+    if (a->dbias)      // [splits][Ncol] bias partials: the same split-parallel reduce (Ncol % 4 == 0)
+      halo_reduce_kernel<<<dim3((unsigned)((a->Ncol / 4 + 15) / 16)), dim3(256), 0, st>>>(
+          a->ws + (size_t)a->splits * a->Ncol * a->Kdim, a->dbias, a->Ncol / 4, a->splits,
+          (reinterpret_cast<uintptr_t>(a->dbias) & 15) == 0);
   }
   return 0;
 }
