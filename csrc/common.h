@@ -11,6 +11,7 @@ typedef uint16_t bf16_t;  // raw bf16 bits (activations / weights in HBM)
 typedef short v8s __attribute__((ext_vector_type(8)));   // 8 x bf16 MFMA operand (4 VGPR)
 typedef short v4s __attribute__((ext_vector_type(4)));   // 4 x bf16 (tr16 read result)
 typedef float v4f __attribute__((ext_vector_type(4)));   // 16x16 MFMA accumulator / 4 x f32
+typedef int v4i __attribute__((ext_vector_type(4)));     // 16x16 i8 MFMA accumulator / operand (16 x int8)
 typedef float v16f __attribute__((ext_vector_type(16))); // 32x32 MFMA accumulator
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));  // 16-byte global access
 typedef unsigned int v2u __attribute__((ext_vector_type(2)));

@@ -203,11 +203,63 @@ __device__ __forceinline__ void halo_epi_full(const ConvArgs& a, v4f (&acc)[FM][
   }
 }
 
+
+// int8 epilogue, straight from the i32 accumulators (lane: 4 consecutive channels of one pixel per fragment):
+// dequantize (per-sample input scale x per-channel weight scale), + bias, ReLU, then requantized int8 (4-byte
+// groups), fp32 or bf16 stores (quant.hip i8_tile_epilogue_direct semantics; no residual addend here).
+template <int FM, int FN, class RM>
+__device__ __forceinline__ void halo_epi_i8(const ConvArgs& a, const I8Epi& ep, v4i (&acc)[FM][FN], int vbase,
+                                            int nbase, int lane, const RM& rm) {
+  const int ohw = a.OH * a.OW;
+  const int nl = 4 * (lane >> 4), ml = lane & 15;
+  const bool q8 = ep.out_mode == 2;
+  const float oi = q8 ? ep.out_inv : 1.f;
+  float ws[FN][4], bs[FN][4];
+#pragma unroll
+  for (int j = 0; j < FN; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int n = nbase + j * 16 + nl + e;
+      ws[j][e] = ep.wscale[n] * oi;
+      bs[j][e] = a.bias ? a.bias[n] * oi : 0.f;
+    }
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const long orow = rm(a, vbase + i * 16 + ml);
+    if (orow < 0) continue;
+    const float xs = ep.xscale ? ep.xscale[orow / ohw] : ep.xs_const;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int n = nbase + j * 16 + nl;
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[e] = (float)acc[i][j][e] * (xs * ws[j][e]) + bs[j][e];
+        if (a.relu) v[e] = fmaxf(v[e], 0.f);
+      }
+      const size_t off = (size_t)orow * a.ldo + n;
+      if (q8) {
+        unsigned pk = 0u;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) pk |= (unsigned)(max(-127, min(127, __float2int_rn(v[e]))) & 0xff) << (8 * e);
+        *reinterpret_cast<unsigned*>(reinterpret_cast<int8_t*>(a.out) + off) = pk;
+      } else if (ep.out_mode == 1) {
+        *reinterpret_cast<v4f*>(reinterpret_cast<float*>(a.out) + off) = v4f{v[0], v[1], v[2], v[3]};
+      } else {
+        *reinterpret_cast<v2u*>(a.out + off) = v2u{pack2bf(v[0], v[1]), pack2bf(v[2], v[3])};
+      }
+    }
+  }
+}
+
 // ABL (timing ablations, BIGDL_CONV_HALO_ABL, wrong outputs): bit 0 no epilogue, bit 1 no MFMAs, bit 2 no DMA after
 // the prologue (stale LDS), bit 3 no fragment reads
-// EPI: 0 lean epilogue (no addend / consumer-BN reduction), 2 lean + consumer-BN reduction, 1 full epilogue
-template <int W, int RB, int NIMG, int KT, int WPX, int EPI, int ABL = 0>
-__global__ __launch_bounds__(256, 2) void conv_halo_kernel(ConvArgs a) {
+// EPI: 0 lean epilogue (no addend / consumer-BN reduction), 2 lean + consumer-BN reduction, 1 full epilogue,
+// 3 int8 (EB = 1: int8 activations and weights, 64-channel chunks on v_mfma_i32_16x16x64_i8, I8Epi epilogue)
+template <int W, int RB, int NIMG, int KT, int WPX, int EPI, int ABL = 0, int EB = 2>
+__global__ __launch_bounds__(256, 2) void conv_halo_kernel(ConvArgs a, I8Epi ep) {
+  static_assert((EB == 1) == (EPI == 3), "int8 operands go with the int8 epilogue");
+  constexpr int CH = 64 / EB;                                 // channels per 64-byte chunk row
   using H = HaloF<W, RB, NIMG, KT, WPX>;
   __shared__ __attribute__((aligned(1024))) unsigned char lds[H::LDS];
   constexpr int WCH = H::WCH, FM = H::FM, FN = H::FN, WP = H::WP;
@@ -225,7 +277,7 @@ __global__ __launch_bounds__(256, 2) void conv_halo_kernel(ConvArgs a) {
   const int n0 = NIMG == 1 ? tm / segs : tm * NIMG;
   const int oh0 = NIMG == 1 ? (tm - n0 * segs) * RB : 0;
   const int k0 = tn * KT;
-  const int nch = C / 32, nk = nch * 9;
+  const int nch = C / CH, nk = nch * 9;
 
   // ---- x DMA: instruction d of wave w fills tile rows (d * 4 + w) * 16 + lane / 4, slot lane & 3 (granule
   // (lane & 3) ^ hswz(row)). Offsets (bytes) from the segment base pixel (n0, oh0 - 1, 0); variant bit 0 / 1 = the
@@ -246,7 +298,7 @@ __global__ __launch_bounds__(256, 2) void conv_halo_kernel(ConvArgs a) {
     // source image row relative to the segment's first row - 1
     const int srow = NIMG == 1 ? hr : (b * IH + i);
     const bool sep = NIMG == 1 ? false : (i == 0);
-    xo[d] = (real && !sep) ? (unsigned)(((srow * W) + (pc - 1)) * C + g * 8) * 2u : OOB;
+    xo[d] = (real && !sep) ? (unsigned)((((srow * W) + (pc - 1)) * C) * EB + g * 16) : OOB;
     if (NIMG == 1 && hr == 0) xtop |= 1u << d;
     if (NIMG == 1 && hr == RB + 1) xbot |= 1u << d;
   }
@@ -256,7 +308,7 @@ __global__ __launch_bounds__(256, 2) void conv_halo_kernel(ConvArgs a) {
   for (int j = 0; j < H::WI; ++j) {
     const int row = (j * 4 + wave) * 16 + (lane >> 2);
     const int g = (lane & 3) ^ hswz(row);
-    wo[j] = (unsigned)((k0 + row) * a.ldw + g * 8) * 2u;
+    wo[j] = (unsigned)((k0 + row) * a.ldw * EB + g * 16);
   }
   const bf16_t* xsrc = reinterpret_cast<const bf16_t*>(a.src);
   const size_t xend = (size_t)a.Nb * IH * W * C;
@@ -271,12 +323,13 @@ __global__ __launch_bounds__(256, 2) void conv_halo_kernel(ConvArgs a) {
   }
   const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<bf16_t*>(reinterpret_cast<const bf16_t*>(a.wt)), (short)0,
-      (int)(((size_t)(a.Ncol - 1) * a.ldw + a.Kdim) * 2), 0x00020000);
+      (int)(((size_t)(a.Ncol - 1) * a.ldw + a.Kdim) * EB), 0x00020000);
 
   auto issue_x = [&](int ch) {
-    const size_t xb = xbase + (size_t)ch * 32;
+    const size_t xb = xbase + (size_t)ch * CH;                 // elements
     const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<bf16_t*>(xsrc + xb), (short)0, (int)((xend - xb) * 2), 0x00020000);
+        const_cast<char*>(reinterpret_cast<const char*>(xsrc) + xb * EB), (short)0, (int)((xend - xb) * EB),
+        0x00020000);
     unsigned char* X = lds + (ch & 1) * H::XBYTES;
 #pragma unroll
     for (int d = 0; d < H::XI; ++d)
@@ -287,7 +340,7 @@ __global__ __launch_bounds__(256, 2) void conv_halo_kernel(ConvArgs a) {
 #pragma unroll
   for (int t = 0; t < 9; ++t) {
     tshift[t] = __builtin_amdgcn_readfirstlane(1 + (1 + a.tap_h[t]) * WP + a.tap_w[t]);
-    twk[t] = __builtin_amdgcn_readfirstlane(a.tap_k[t] * C * 2);
+    twk[t] = __builtin_amdgcn_readfirstlane(a.tap_k[t] * C * EB);
   }
   auto issue_w = [&](int ch, int t, int slot) {
     const int soff = twk[t] + ch * 64;
@@ -309,11 +362,12 @@ __global__ __launch_bounds__(256, 2) void conv_halo_kernel(ConvArgs a) {
   const unsigned wrd = (unsigned)(2 * H::XBYTES + wrow * 64 + ((gi ^ hswz(wrow)) << 4));
   const int v0 = wpx * H::TM + (lane & 15);
 
-  v4f acc[FM][FN];
+  using AccT = std::conditional_t<EB == 1, v4i, v4f>;
+  AccT acc[FM][FN];
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < FN; ++j) acc[i][j] = AccT{0, 0, 0, 0};
 
   // prologue: chunk 0 and weight steps 0 .. D-1; retire step 0 (younger: steps 1 .. D-1)
   issue_x(0);
@@ -360,10 +414,15 @@ __global__ __launch_bounds__(256, 2) void conv_halo_kernel(ConvArgs a) {
         asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(fx[i]) : "n"(FM - 1 - i));
         if constexpr (!(ABL & 2)) {
 #pragma unroll
-          for (int j = 0; j < FN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[j], fx[i], acc[i][j], 0, 0, 0);
+          for (int j = 0; j < FN; ++j) {
+            if constexpr (EB == 1)
+              acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(__builtin_bit_cast(v4i, fw[j]), __builtin_bit_cast(v4i, fx[i]),
+                                                               acc[i][j], 0, 0, 0);
+            else
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[j], fx[i], acc[i][j], 0, 0, 0);
+          }
         } else {
-          acc[i][0][0] += (float)fw[0][0] * (float)fx[i][0];
+          acc[i][0][0] += fw[0][0] * fx[i][0];
         }
       });
       __builtin_amdgcn_sched_barrier(0);
@@ -390,7 +449,9 @@ __global__ __launch_bounds__(256, 2) void conv_halo_kernel(ConvArgs a) {
   }
   const HaloRowMap<W, RB, NIMG> rm{n0, oh0, H::VR * WP};
   // per-wave channel sums go behind the bf16 slices (lean) or at the start of the idle LDS (full)
-  if constexpr (EPI == 0 || EPI == 2) {
+  if constexpr (EPI == 3) {
+    halo_epi_i8<FM, FN>(a, ep, acc, wpx * H::TM, k0 + wch * H::TN, lane, rm);
+  } else if constexpr (EPI == 0 || EPI == 2) {
     static_assert(4 * H::TM * 128 + 4 * 128 * 4 <= H::LDS, "bf16 epilogue slices must fit the LDS");
     halo_epi_lean<FM, FN, WCH, KT, EPI == 2>(a, acc, wpx * H::TM, k0 + wch * H::TN, lane, bid,
                                              lds + wave * H::TM * 128, rm,
@@ -413,18 +474,26 @@ void launch_halo_f(const ConvArgs& a, hipStream_t st) {
   const bool leanbn = a.addend == nullptr && a.bnred != nullptr && a.stats == nullptr && a.bias == nullptr &&
                       (a.bnz == nullptr || a.bnzm != nullptr);
   const dim3 g(nwg), b(256);
-  if (abl == 1) conv_halo_kernel<W, RB, NIMG, KT, WPX, 0, 1><<<g, b, 0, st>>>(a);
-  else if (abl == 3) conv_halo_kernel<W, RB, NIMG, KT, WPX, 0, 3><<<g, b, 0, st>>>(a);
-  else if (abl == 5) conv_halo_kernel<W, RB, NIMG, KT, WPX, 0, 5><<<g, b, 0, st>>>(a);
-  else if (abl == 9) conv_halo_kernel<W, RB, NIMG, KT, WPX, 0, 9><<<g, b, 0, st>>>(a);
-  else if (abl == 13) conv_halo_kernel<W, RB, NIMG, KT, WPX, 0, 13><<<g, b, 0, st>>>(a);
-  else if (abl == 15) conv_halo_kernel<W, RB, NIMG, KT, WPX, 0, 15><<<g, b, 0, st>>>(a);
-  else if (lean) conv_halo_kernel<W, RB, NIMG, KT, WPX, 0><<<g, b, 0, st>>>(a);
-  else if (leanbn && g_conv_halo_bn) conv_halo_kernel<W, RB, NIMG, KT, WPX, 2><<<g, b, 0, st>>>(a);
-  else conv_halo_kernel<W, RB, NIMG, KT, WPX, 1><<<g, b, 0, st>>>(a);
+  if (abl == 1) conv_halo_kernel<W, RB, NIMG, KT, WPX, 0, 1><<<g, b, 0, st>>>(a, I8Epi{});
+  else if (abl == 3) conv_halo_kernel<W, RB, NIMG, KT, WPX, 0, 3><<<g, b, 0, st>>>(a, I8Epi{});
+  else if (abl == 5) conv_halo_kernel<W, RB, NIMG, KT, WPX, 0, 5><<<g, b, 0, st>>>(a, I8Epi{});
+  else if (abl == 9) conv_halo_kernel<W, RB, NIMG, KT, WPX, 0, 9><<<g, b, 0, st>>>(a, I8Epi{});
+  else if (abl == 13) conv_halo_kernel<W, RB, NIMG, KT, WPX, 0, 13><<<g, b, 0, st>>>(a, I8Epi{});
+  else if (abl == 15) conv_halo_kernel<W, RB, NIMG, KT, WPX, 0, 15><<<g, b, 0, st>>>(a, I8Epi{});
+  else if (lean) conv_halo_kernel<W, RB, NIMG, KT, WPX, 0><<<g, b, 0, st>>>(a, I8Epi{});
+  else if (leanbn && g_conv_halo_bn) conv_halo_kernel<W, RB, NIMG, KT, WPX, 2><<<g, b, 0, st>>>(a, I8Epi{});
+  else conv_halo_kernel<W, RB, NIMG, KT, WPX, 1><<<g, b, 0, st>>>(a, I8Epi{});
 }
 
 int g_conv_halo = -1;
+
+template <int W, int RB, int NIMG, int KT, int WPX>
+void launch_halo_i8(const ConvArgs& a, const I8Epi& ep, hipStream_t st) {
+  const int segs = a.Hs / RB;
+  const int tiles_m = NIMG == 1 ? a.Nb * segs : (a.Nb + NIMG - 1) / NIMG;
+  const int nwg = tiles_m * (a.Ncol / KT);
+  conv_halo_kernel<W, RB, NIMG, KT, WPX, 3, 0, 1><<<dim3(nwg), dim3(256), 0, st>>>(a, ep);
+}
 
 }  // namespace
 
@@ -472,6 +541,33 @@ int bigdl_conv_halo(const ConvArgs* a, hipStream_t st) {
     case 28: launch_halo_f<28, 7, 1, 128, 2>(*a, st); break;
     case 14: launch_halo_f<14, 14, 1, 128, 2>(*a, st); break;
     case 7: launch_halo_f<7, 7, 3, 128, 2>(*a, st); break;
+    default: return -1;
+  }
+  return 0;
+}
+
+// int8 form (quant.hip bigdl_conv_i8): the same geometry with 64-channel chunks; no residual addend; 4-byte aligned
+// output groups. BIGDL_CONV_HALO=0 turns it off too.
+int bigdl_conv_halo_i8_applies(const ConvArgs* a, const I8Epi* ep) {
+  if (ep->add8 != nullptr || (a->Cs % 64) || (a->Ncol % 4) || (a->ldo % 4) || (a->ldw % 16)) return 0;
+  if (g_conv_halo < 0) (void)bigdl_conv_halo_applies(a);     // reads BIGDL_CONV_HALO once
+  if (!g_conv_halo) return 0;
+  // bigdl_conv_halo_applies's geometry checks, on int8 operands (16-byte aligned rows)
+  ConvArgs b = *a;
+  b.addend = nullptr; b.bnred = nullptr; b.stats = nullptr;
+  const int keep = g_conv_halo;
+  g_conv_halo = 1;
+  const int ok = bigdl_conv_halo_applies(&b);
+  g_conv_halo = keep;
+  return ok;
+}
+
+int bigdl_conv_halo_i8(const ConvArgs* a, const I8Epi* ep, hipStream_t st) {
+  switch (a->Ws) {
+    case 56: launch_halo_i8<56, 4, 1, 64, 4>(*a, *ep, st); break;
+    case 28: launch_halo_i8<28, 7, 1, 128, 2>(*a, *ep, st); break;
+    case 14: launch_halo_i8<14, 14, 1, 128, 2>(*a, *ep, st); break;
+    case 7: launch_halo_i8<7, 7, 3, 128, 2>(*a, *ep, st); break;
     default: return -1;
   }
   return 0;

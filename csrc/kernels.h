@@ -50,6 +50,19 @@ struct ConvArgs {
   int pstride;
 };
 
+// int8 convolution epilogue (quant.hip, conv_halo.hip): dequantize with the per-sample input scale and the per-channel
+// weight scale, + bias, + an optional int8 residual addend, ReLU, then bf16 / fp32 / requantized int8 stores
+struct I8Epi {
+  const float* xscale;   // [N] per-sample scale, or nullptr -> xs_const
+  float xs_const;
+  const float* wscale;   // [Ncol]
+  int out_mode;          // 0 bf16, 1 fp32, 2 int8
+  float out_inv;         // int8 output: 1 / out_scale
+  const int8_t* add8;    // optional int8 residual addend [M][add_ld] (dequantized with add_scale, before the ReLU)
+  float add_scale;
+  long add_ld;
+};
+
 struct WgradArgs {
   const uint16_t* dy;
   const uint16_t* src;
@@ -73,6 +86,9 @@ int bigdl_conv_nt(const ConvArgs* a, hipStream_t st);
 int bigdl_conv_halo_applies(const ConvArgs* a);
 int bigdl_conv_halo(const ConvArgs* a, hipStream_t st);
 void bigdl_set_conv_halo(int v);
+// the same on the i8 matrix cores (int8 activations / weights, I8Epi epilogue; no residual addend)
+int bigdl_conv_halo_i8_applies(const ConvArgs* a, const I8Epi* ep);
+int bigdl_conv_halo_i8(const ConvArgs* a, const I8Epi* ep, hipStream_t st);
 // 7x7 / stride-2 pair-view image stem forward (stem_fwd.hip)
 int bigdl_stem_fwd_applies(const ConvArgs* a);
 int bigdl_stem_fwd(const ConvArgs* a, hipStream_t st);

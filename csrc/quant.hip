@@ -16,7 +16,6 @@
 
 namespace {
 
-typedef int v4i __attribute__((ext_vector_type(4)));
 
 __device__ __attribute__((aligned(64))) uint8_t g_zero16[64];
 
@@ -119,16 +118,7 @@ __device__ __forceinline__ void glds16(const void* g, LDS_PTR(void) l) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g, l, 16, 0, 0);
 }
 
-struct I8Epi {
-  const float* xscale;   // [N] per-sample scale, or nullptr -> xs_const
-  float xs_const;
-  const float* wscale;   // [Ncol]
-  int out_mode;          // 0 bf16, 1 fp32, 2 int8
-  float out_inv;         // int8 output: 1 / out_scale
-  const int8_t* add8;    // optional int8 residual addend [M][add_ld] (dequantized with add_scale, before the ReLU)
-  float add_scale;
-  long add_ld;
-};
+// I8Epi (the int8 epilogue's scales / output mode / residual addend): csrc/kernels.h
 
 //
 // Tiles: 128 x 128 (2 x 2 waves) by default; narrow layers (Ncol <= 64 / <= 32 — the 147x147 / 73x73 stem convs
@@ -1361,7 +1351,9 @@ int bigdl_conv_i8(const ConvArgs* a, const float* xscale, float xs_const, const 
   const bool fk = a->Cs % QBK == 0;
   const bool g3fk = a->Cs % 64 == 0;
   const long p8_tiles = (long)((a->M + 255) / 256) * ((a->Ncol + 255) / 256);
-  if (i8_s1_applies(*a, ep)) {
+  if (bigdl_conv_halo_i8_applies(a, &ep) && bigdl_conv_halo_i8(a, &ep, st) == 0) {
+    // 3x3 / stride-1 / pad-1: the halo-tile kernel on the i8 matrix cores (conv_halo.hip)
+  } else if (i8_s1_applies(*a, ep)) {
     launch_i8_s1(*a, ep, st);
   } else if (i8_p8() && fk && a->Kdim >= 1024 && a->Ncol >= 256 && a->Ncol % 16 == 0 &&
       (g_i8_p8 == 2 || p8_tiles >= 160)) {

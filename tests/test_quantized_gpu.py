@@ -257,3 +257,46 @@ def test_conv_i8_s1_exact(case):
         if relu:
             yb = yb.clamp(min=0)
         assert _rel(outs[(1, relu)][1], yb) < 1e-2
+
+
+I8_HALO_CASES = [
+    # 3x3 / stride-1 / pad-1 layers the int8 halo-tile kernel takes (csrc/conv_halo.hip EB = 1): H in {56, 28, 14, 7}
+    (2, 64, 56, 56, 64, 3, 3, 1, 1, 1),
+    (2, 128, 28, 28, 128, 3, 3, 1, 1, 1),
+    (3, 256, 14, 14, 256, 3, 3, 1, 1, 1),
+    (4, 512, 7, 7, 512, 3, 3, 1, 1, 1),
+    (5, 64, 7, 7, 128, 3, 3, 1, 1, 1),
+]
+
+
+@pytest.mark.parametrize("case", I8_HALO_CASES)
+def test_conv_i8_halo_exact(case):
+    """int8 3x3 halo kernel: fp32 output equal to the integer conv + bias (unit scales), int8 output with ReLU equal to
+    the exactly clamped integer result, and the same int8 bytes as the im2col int8 kernels (BIGDL_CONV_HALO off)."""
+    from bigdl_amd.ops.conv import _fwd_taps, out_size
+
+    C_ = native.get()
+    _conv_i8_exact(case)
+    N, C, H, W, K, R, S, st, pd, dl = case
+    g = torch.Generator().manual_seed(7)
+    x = torch.randint(-4, 5, (N, H, W, C), generator=g, dtype=torch.int8)
+    w = torch.randint(-4, 5, (K, R, S, C), generator=g, dtype=torch.int8)
+    OH, OW = out_size(H, R, st, pd, dl), out_size(W, S, st, pd, dl)
+    ref = F.conv2d(x.permute(0, 3, 1, 2).double(), w.permute(0, 3, 1, 2).double(), None, st, pd, dl)
+    ref = ref.permute(0, 2, 3, 1).reshape(N * OH * OW, K)
+    bias = torch.randint(-20, 21, (K,), generator=g).float()
+    geo = [N, H, W, C, OH, OW, st, st, R * S * C, K, K, OH, OW, 1, 1, 0, 0]
+    outs = {}
+    for halo in (1, 0):
+        C_.set_conv_halo(halo)
+        try:
+            out = torch.zeros(N * OH * OW, K, dtype=torch.int8, device="cuda")
+            C_.conv_i8(x.cuda(), w.cuda(), out, bias.cuda(), torch.ones(N, device="cuda"),
+                       torch.ones(K, device="cuda"), geo, _fwd_taps(R, S, pd, pd, dl, dl), True, 1.0, 1.0)
+            torch.cuda.synchronize()
+            outs[halo] = out.cpu()
+        finally:
+            C_.set_conv_halo(1)
+    exp = (ref + bias.double()).clamp(0, 127).to(torch.int8)
+    assert torch.equal(outs[1], exp)
+    assert torch.equal(outs[1], outs[0])
