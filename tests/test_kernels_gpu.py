@@ -865,7 +865,7 @@ def test_conv_s1_stream_kernel(case, zmask):
             res[s1] = (y, stats, y2, dx, red, bool(bn.get("done")))
         finally:
             C_.set_conv_s1(1)
-    y, stats, y2, dx, red, done, dx2, red2 = res[1]
+    y, stats, y2, dx, red, done = res[1]
     assert _rel(y, yr0) < 1e-2
     st2 = stats.view(bnops.stat_slots(), 2, K).sum(0)
     assert _rel(st2[0], y.float().sum(dim=(0, 2, 3))) < 1e-4
