@@ -245,6 +245,16 @@ def residual_forward(seq, x):
 MASKED_ADDEND = [os.environ.get("BIGDL_MASKED_ADDEND", "0") != "0"]
 
 
+# BIGDL_SHORTCUT_BN_RED=0: the projection shortcut BN's backward reduction runs as its own pass
+SHORTCUT_BN_RED = [os.environ.get("BIGDL_SHORTCUT_BN_RED", "1") != "0"]
+
+
+def _native_det():
+    from ..ops import native
+
+    return native.deterministic()
+
+
 def residual_backward(seq, x, gradOutput):
     branch, short, bn = seq._residual_plan
     mods = branch.modules
@@ -266,7 +276,22 @@ def residual_backward(seq, x, gradOutput):
         masked = (gz, zm)
         gs = None
     else:
-        dh, dres = bn.backward_fused(seq._res_h, gradOutput, need_dres=True)
+        # projection shortcut ending in a training BN without ReLU: dres is that BN's output gradient, so its
+        # backward reduction rides along in the pass that writes dres (csrc/batchnorm.hip bn_bwd_apply_kernel R2)
+        sec, sbn = None, None
+        if SHORTCUT_BN_RED[0] and isinstance(short, Sequential) and short.modules:
+            sbn = short.modules[-1]
+            xs = getattr(sbn, "_xin", None)
+            xb = getattr(bn, "_xin", None)
+            if (isinstance(sbn, BatchNormalization) and sbn.train and not sbn.fuse_relu and xs is not None
+                    and xb is not None and xs.is_cuda and xs.shape == xb.shape and xs.stride() == xb.stride()
+                    and xs.dtype == torch.bfloat16 and xs.shape[1] % 8 == 0 and not _native_det()):
+                from ..ops import bn as bnops
+
+                sec = (xs, sbn.saveMean, bnops.new_stats(xs.shape[1], xs.device))
+        dh, dres = bn.backward_fused(seq._res_h, gradOutput, need_dres=True, sec=sec)
+        if sec is not None:
+            dres._bn_red = (sbn, sec[2])
         # shortcut first, so its gradient can be summed inside the epilogue of the branch's first dgrad GEMM
         gs = short.backward(x, dres)
     bn.gradInput = dh

@@ -149,7 +149,7 @@ class BatchNormalization(TensorModule):
     def _direct_grads(self):
         return (not self._frozen) and self.affine and self.scaleW == 1.0 and self.scaleB == 1.0
 
-    def backward_fused(self, input, gradOutput, need_dres=False):
+    def backward_fused(self, input, gradOutput, need_dres=False, sec=None):
         """GPU backward that also returns the residual-branch gradient (used by the fused ResNet block)."""
         gz = self._to_nchw(gradOutput)
         x = self._xin
@@ -166,7 +166,8 @@ class BatchNormalization(TensorModule):
         graph_res = getattr(self, "_graph_dres", False)
         dx, dres = bnops.bn_backward_gpu(gz, z, x, self.saveMean, self.saveStd, self.weight, dg, db,
                                          training=self.train, need_dres=need_dres or graph_res,
-                                         sync_fn=self.sync_fn if self.train else None, aff=aff, red=red, zm=zm)
+                                         sync_fn=self.sync_fn if self.train else None, aff=aff, red=red, zm=zm,
+                                         sec=sec)
         if graph_res:
             self._dres = dres
         if not direct and self.affine and not self._frozen:

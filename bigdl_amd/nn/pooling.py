@@ -2,12 +2,17 @@
 VolumetricMaxPooling.scala, VolumetricAveragePooling.scala, TemporalMaxPooling.scala; primitives in
 NNPrimitive.scala:654-1051. GPU engine: 2D NHWC kernels in csrc/elementwise.hip, 3D / temporal pooling on the
 N-d window kernels of csrc/pool_nd.hip."""
+import os
+
 import torch
 import torch.nn.functional as F
 
 from ..ops import pool as P
 from ..ops import pool_nd as PN
 from .abstractnn import AutogradModule, TensorModule
+
+# BIGDL_POOL_BN_RED=0: the stem BN's backward reduction runs as its own pass instead of inside the pool backward
+_POOL_BN_RED = os.environ.get("BIGDL_POOL_BN_RED", "1") != "0"
 
 BF16 = torch.bfloat16
 CL = torch.channels_last
@@ -75,7 +80,14 @@ class SpatialMaxPooling(TensorModule):
         if sq:
             x, g = x.unsqueeze(0), g.unsqueeze(0)
         ph, pw = self._pads(x.shape[2], x.shape[3])
-        if _gpu_ok(x):
+        bn_src = getattr(input, "_bn_bwd", None) if _POOL_BN_RED else None
+        if _gpu_ok(x) and bn_src is not None and bn_src[0].train and not sq:
+            # the input is a training BN's ReLU output (the ResNet stem): reduce that BN's backward statistics here
+            gi, red = P.maxpool_bwd_bnred_gpu(_prep(g), self._idx, x.shape, self.kH, self.kW, self.dH, self.dW, ph, pw,
+                                              bn_src)
+            if red is not None:
+                gi._bn_red = (bn_src[0], red)
+        elif _gpu_ok(x):
             gi = P.maxpool_bwd_gpu(_prep(g), self._idx, x.shape, self.kH, self.kW, self.dH, self.dW, ph, pw)
         elif x.is_cuda:
             geo, _ = PN.pool2d_geo(x.shape, self.kH, self.kW, self.dH, self.dW, ph, pw, self.ceilMode)

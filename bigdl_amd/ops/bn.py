@@ -105,7 +105,7 @@ def bn_forward_gpu(x, gamma, beta, rmean, rvar, eps, momentum, training, stats=N
 
 
 def bn_backward_gpu(dz, z, x, smean, sinv, gamma, dgamma, dbeta, training=True, need_dres=False, need_dx=True,
-                    sync_fn=None, aff=None, red=None, zm=None):
+                    sync_fn=None, aff=None, red=None, zm=None, sec=None):
     """Backward of y = relu?(bn(x) [+ res]).
 
     dz: gradient w.r.t. the (post-relu) output; z: the forward output (ReLU mask) or None. With z None and
@@ -113,6 +113,8 @@ def bn_backward_gpu(dz, z, x, smean, sinv, gamma, dgamma, dbeta, training=True, 
     Returns (dx, dres) — dres is the gradient flowing into the residual branch (= masked dz).
     ``red``: the slotted backward reduction already accumulated by the producer of dz (a dgrad epilogue).
     ``zm``: the forward's sign mask of the output (bn_forward_gpu), used in place of z.
+    ``sec``: (x2, mean2, red2) of a second training BN without ReLU whose output gradient is dres (a projection
+    shortcut): its slotted backward reduction is accumulated into red2 by the same pass (requires need_dres).
     """
     C = x.shape[1]
     P = _P(x)
@@ -130,7 +132,12 @@ def bn_backward_gpu(dz, z, x, smean, sinv, gamma, dgamma, dbeta, training=True, 
     coef = torch.empty(3 * C, dtype=torch.float32, device=x.device)
     dx = torch.empty_like(x) if need_dx else None
     dres = torch.empty_like(x) if need_dres else None
-    C_.bn_bwd_apply(dz, z, x, smean, sinv, gamma, red, nslots, coef, dx, dres, dgamma, dbeta, Ptot, C, aff, zm)
+    if sec is not None and dres is not None and training:
+        x2, mean2, red2 = sec
+        C_.bn_bwd_apply(dz, z, x, smean, sinv, gamma, red, nslots, coef, dx, dres, dgamma, dbeta, Ptot, C, aff, zm,
+                        x2=x2, mean2=mean2, red2=red2)
+    else:
+        C_.bn_bwd_apply(dz, z, x, smean, sinv, gamma, red, nslots, coef, dx, dres, dgamma, dbeta, Ptot, C, aff, zm)
     return dx, dres
 
 

@@ -260,22 +260,27 @@ __device__ __forceinline__ void load8(const float* p, float* v) {
   v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3]; v[4] = b[0]; v[5] = b[1]; v[6] = b[2]; v[7] = b[3];
 }
 
-template <int U>
+// R2: the residual-branch gradient dres (= masked dz) is also the output gradient of a second training BN without
+// ReLU (the projection shortcut's BN of a ResNet downsampling block, input x2 / mean2): its backward reduction
+// (sum dres, sum dres*(x2 - mean2), over dres as stored in bf16) is accumulated here into the slotted `red2`, which
+// saves that BN a chan_reduce pass re-reading dres and x2 (nn/fusion.py residual_backward).
+template <int U, bool R2>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16_t* __restrict__ dz, const bf16_t* __restrict__ z,
                                                            const bf16_t* __restrict__ x, const float* __restrict__ coef,
                                                            bf16_t* __restrict__ dx, bf16_t* __restrict__ dres, long P,
                                                            int C, long rpb, const float* __restrict__ aff,
-                                                           const uint8_t* __restrict__ zm) {
+                                                           const uint8_t* __restrict__ zm, const bf16_t* __restrict__ x2,
+                                                           const float* __restrict__ mean2, float* __restrict__ red2) {
   const int G = C >> 3;
   const bool xmask = z == nullptr && zm == nullptr && aff != nullptr;   // ReLU mask from x*scale + shift (see chan_reduce_kernel)
   const int gbase = blockIdx.y * 256;
   const int gcount = min(256, G - gbase);
   const int rpi = 256 / gcount;
   const int g = gbase + threadIdx.x % gcount, rsub = threadIdx.x / gcount;
-  if (rsub >= rpi) return;
-  const long rbeg = blockIdx.x * rpb, rend = min(P, rbeg + rpb);
+  if (!R2 && rsub >= rpi) return;
+  const long rbeg = blockIdx.x * rpb, rend = rsub < rpi ? min(P, rbeg + rpb) : rbeg;   // idle threads: no rows
   const int c0 = g * 8;
-  float A[8], B[8], D[8], S[8], T[8];
+  float A[8], B[8], D[8], S[8], T[8], M2[8], a1[8], a2[8];
   load8(coef + c0, A);
   load8(coef + C + c0, B);
   load8(coef + 2 * C + c0, D);
@@ -283,8 +288,13 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16_t* __restr
     load8(aff + c0, S);
     load8(aff + C + c0, T);
   }
+  if (R2) {
+    load8(mean2 + c0, M2);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { a1[e] = 0.f; a2[e] = 0.f; }
+  }
   for (long r0 = rbeg + rsub; r0 < rend; r0 += (long)U * rpi) {
-    v4u vd[U], vz[U], vx[U];
+    v4u vd[U], vz[U], vx[U], vx2[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const long r = r0 + (long)u * rpi;
@@ -294,6 +304,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16_t* __restr
       if (zm) vz[u] = mask8_to_bf(zm[i]);
       else if (z) vz[u] = reinterpret_cast<const v4u*>(z)[i];
       vx[u] = reinterpret_cast<const v4u*>(x)[i];
+      if (R2) vx2[u] = reinterpret_cast<const v4u*>(x2)[i];
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -312,11 +323,31 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16_t* __restr
         const float r1v = A[2 * e + 1] * d1 + B[2 * e + 1] * x1 + D[2 * e + 1];
         o[e] = pack2bf(r0v, r1v);
         od[e] = pack2bf(d0, d1);
+        if (R2 && r < rend) {
+          const float q0 = lo_bf(od[e]), q1 = hi_bf(od[e]);
+          a1[2 * e] += q0; a1[2 * e + 1] += q1;
+          a2[2 * e] += q0 * (lo_bf(vx2[u][e]) - M2[2 * e]);
+          a2[2 * e + 1] += q1 * (hi_bf(vx2[u][e]) - M2[2 * e + 1]);
+        }
       }
       if (r < rend) {
         if (dx) reinterpret_cast<v4u*>(dx)[r * G + g] = o;
         if (dres) reinterpret_cast<v4u*>(dres)[r * G + g] = od;
       }
+    }
+  }
+  if (R2) {
+    // per-workgroup sums through LDS (threads of one channel group sit gcount apart), one atomic per value
+    __shared__ float sm[256 * 16];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { sm[threadIdx.x * 16 + e] = a1[e]; sm[threadIdx.x * 16 + 8 + e] = a2[e]; }
+    __syncthreads();
+    for (int w = threadIdx.x; w < gcount * 16; w += 256) {
+      const int gg = w >> 4, slot = w & 15;
+      float t = 0.f;
+      for (int rs = 0; rs < rpi; ++rs) t += sm[(rs * gcount + gg) * 16 + slot];
+      const int ch = (gbase + gg) * 8 + (slot & 7);
+      atomicAdd(red2 + (size_t)(blockIdx.x & (STAT_SLOTS - 1)) * 2 * C + (slot < 8 ? 0 : C) + ch, t);
     }
   }
 }
@@ -411,17 +442,32 @@ void bigdl_bn_bwd_reduce(const uint16_t* dz, const uint16_t* z, const uint16_t* 
 void bigdl_bn_bwd_apply(const uint16_t* dz, const uint16_t* z, const uint16_t* x, const float* mean,
                         const float* invstd, const float* gamma, const float* red, int nslots, float* coef,
                         uint16_t* dx, uint16_t* dres, float* dgamma, float* dbeta, long P, int C, int training,
-                        const float* aff, hipStream_t st, const uint8_t* zm) {
+                        const float* aff, hipStream_t st, const uint8_t* zm, const uint16_t* x2u,
+                        const float* mean2, float* red2) {
+  const bf16_t* x2 = reinterpret_cast<const bf16_t*>(x2u);
   bn_bwd_coeff_kernel<<<(C + 7) / 8, 256, 0, st>>>(red, nslots, mean, invstd, gamma, coef, dgamma, dbeta, P, C,
                                                     training);
   if (dx || dres) {
     long rpb = 0;
     const dim3 grid = stationary_grid(P, C, &rpb);
-    switch (bn_unroll()) {
-      case 1: bn_bwd_apply_kernel<1><<<grid, 256, 0, st>>>(dz, z, x, coef, dx, dres, P, C, rpb, aff, zm); break;
-      case 2: bn_bwd_apply_kernel<2><<<grid, 256, 0, st>>>(dz, z, x, coef, dx, dres, P, C, rpb, aff, zm); break;
-      case 8: bn_bwd_apply_kernel<8><<<grid, 256, 0, st>>>(dz, z, x, coef, dx, dres, P, C, rpb, aff, zm); break;
-      default: bn_bwd_apply_kernel<4><<<grid, 256, 0, st>>>(dz, z, x, coef, dx, dres, P, C, rpb, aff, zm); break;
+    if (red2) {        // second BN's reduction over dres (needs dres)
+#define BWD2(UU) bn_bwd_apply_kernel<UU, true><<<grid, 256, 0, st>>>(dz, z, x, coef, dx, dres, P, C, rpb, aff, zm, x2, mean2, red2)
+      switch (bn_unroll()) {
+        case 1: BWD2(1); break;
+        case 2: BWD2(2); break;
+        case 8: BWD2(8); break;
+        default: BWD2(4); break;
+      }
+#undef BWD2
+    } else {
+#define BWD1(UU) bn_bwd_apply_kernel<UU, false><<<grid, 256, 0, st>>>(dz, z, x, coef, dx, dres, P, C, rpb, aff, zm, nullptr, nullptr, nullptr)
+      switch (bn_unroll()) {
+        case 1: BWD1(1); break;
+        case 2: BWD1(2); break;
+        case 8: BWD1(8); break;
+        default: BWD1(4); break;
+      }
+#undef BWD1
     }
   }
   HIP_LAUNCH_CHECK();

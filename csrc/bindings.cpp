@@ -191,14 +191,22 @@ void bn_bwd_reduce(const Tensor& dz, const OptT& z, const Tensor& x, const Tenso
 void bn_bwd_apply(const Tensor& dz, const OptT& z, const Tensor& x, const Tensor& mean, const Tensor& invstd,
                   const OptT& gamma, const OptT& red, int64_t nslots, const Tensor& coef, const OptT& dx,
                   const OptT& dres, const OptT& dgamma, const OptT& dbeta, int64_t P, int64_t C, const OptT& aff,
-                  const OptT& zm) {
+                  const OptT& zm, const OptT& x2, const OptT& mean2, const OptT& red2) {
   TORCH_CHECK(coef.numel() >= 3 * C, "bn_bwd_apply: coef size");
+  const bool r2 = red2 && red2->defined();
+  if (r2) {
+    TORCH_CHECK(dres && dres->defined() && x2 && x2->defined() && mean2 && mean2->defined(),
+                "bn_bwd_apply: red2 needs dres, x2 and mean2");
+    TORCH_CHECK(x2->numel() == x.numel() && x2->strides() == x.strides(), "bn_bwd_apply: x2 must match x's layout");
+    TORCH_CHECK(mean2->numel() >= C && red2->numel() >= (int64_t)BIGDL_STAT_SLOTS * 2 * C, "bn_bwd_apply: mean2 / red2 size");
+  }
   if (aff && aff->defined()) TORCH_CHECK(aff->numel() >= 2 * C && aff->is_contiguous(), "bn_bwd_apply: aff is [2C]");
   const bool training = red && red->defined();
   bigdl_bn_bwd_apply(cbf(dz, "dz"), ocbf(z, "z"), cbf(x, "x"), cf(mean, "mean"), cf(invstd, "invstd"),
                      ocf(gamma, "gamma"), ocf(red, "red"), (int)nslots, mf(coef, "coef"), ombf(dx, "dx"),
                      ombf(dres, "dres"), omf(dgamma, "dgamma"), omf(dbeta, "dbeta"), P, (int)C, training ? 1 : 0,
-                     ocf(aff, "aff"), stream(), omzm(zm, P, C, "zm"));
+                     ocf(aff, "aff"), stream(), omzm(zm, P, C, "zm"), r2 ? cbf(*x2, "x2") : nullptr,
+                     r2 ? cf(*mean2, "mean2") : nullptr, r2 ? omf(red2, "red2") : nullptr);
 }
 
 void dgrad_fill(const Tensor& out, const OptT& addend, int64_t sh, int64_t sw, int64_t mask) {
@@ -402,6 +410,26 @@ void maxpool_bwd(const Tensor& dy, const Tensor& idx, const Tensor& dx, std::vec
   TORCH_CHECK(g.size() == 12 && g[3] % 8 == 0, "maxpool_bwd: geometry");
   bigdl_maxpool_bwd(cbf(dy, "dy"), (const uint8_t*)idx.data_ptr(), mbf(dx, "dx"), g[0], g[1], g[2], g[3], g[4], g[5],
                     g[6], g[7], g[8], g[9], g[10], g[11], stream());
+}
+// maxpool backward that also accumulates the backward reduction of the BN whose output is the pool's input;
+// returns false (nothing launched) when the fused kernel does not apply
+bool maxpool_bwd_bnred(const Tensor& dy, const Tensor& idx, const Tensor& dx, std::vector<int64_t> g, const Tensor& bx,
+                       const Tensor& mean, const c10::optional<Tensor>& aff, const c10::optional<Tensor>& zm,
+                       const Tensor& red) {
+  TORCH_CHECK(g.size() == 12 && g[3] % 8 == 0, "maxpool_bwd_bnred: geometry");
+  if (!bigdl_maxpool_bwd_bnred_applies(g[0], g[1], g[2], g[3], g[4], g[5], g[6], g[7], g[8], g[9], g[10], g[11]))
+    return false;
+  TORCH_CHECK(bx.numel() == dx.numel() && bx.scalar_type() == at::kBFloat16 && bx.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "maxpool_bwd_bnred: BN input must be bf16 NHWC of the pool input's shape");
+  TORCH_CHECK(mean.scalar_type() == at::kFloat && mean.numel() >= g[3], "maxpool_bwd_bnred: mean");
+  TORCH_CHECK(red.scalar_type() == at::kFloat && red.numel() >= (int64_t)BIGDL_STAT_SLOTS * 2 * g[3], "maxpool_bwd_bnred: red");
+  TORCH_CHECK(aff.has_value() != zm.has_value(), "maxpool_bwd_bnred: exactly one of aff / zm");
+  if (aff) TORCH_CHECK(aff->scalar_type() == at::kFloat && aff->numel() >= 2 * g[3], "maxpool_bwd_bnred: aff");
+  if (zm) TORCH_CHECK(zm->scalar_type() == at::kByte && zm->numel() * 8 >= dx.numel(), "maxpool_bwd_bnred: zm");
+  bigdl_maxpool_bwd_bnred(cbf(dy, "dy"), (const uint8_t*)idx.data_ptr(), mbf(dx, "dx"), g[0], g[3], g[4], g[5],
+                          cbf(bx, "bx"), mean.data_ptr<float>(), aff ? aff->data_ptr<float>() : nullptr,
+                          zm ? (const uint8_t*)zm->data_ptr() : nullptr, red.data_ptr<float>(), stream());
+  return true;
 }
 void avgpool_fwd(const Tensor& x, const Tensor& y, std::vector<int64_t> g, bool count_pad) {
   TORCH_CHECK(g.size() == 12 && g[3] % 8 == 0, "avgpool: geometry");
@@ -1253,9 +1281,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_bwd_apply", &bn_bwd_apply, py::arg("dz"), py::arg("z"), py::arg("x"), py::arg("mean"), py::arg("invstd"),
         py::arg("gamma"), py::arg("red"), py::arg("nslots"), py::arg("coef"), py::arg("dx"), py::arg("dres"),
         py::arg("dgamma"), py::arg("dbeta"), py::arg("P"), py::arg("C"), py::arg("aff") = py::none(),
-        py::arg("zm") = py::none());
+        py::arg("zm") = py::none(), py::arg("x2") = py::none(), py::arg("mean2") = py::none(),
+        py::arg("red2") = py::none());
   m.def("relu_fwd", &relu_fwd);
   m.def("dgrad_fill", &dgrad_fill);
+  m.def("maxpool_bwd_bnred", &maxpool_bwd_bnred, "k3 s2 maxpool backward + the producing BN's backward reduction",
+        py::arg("dy"), py::arg("idx"), py::arg("dx"), py::arg("g"), py::arg("bx"), py::arg("mean"), py::arg("aff"),
+        py::arg("zm"), py::arg("red"));
   m.def("hog_cus", &hog_cus, "n one-wave workgroups holding a whole CU's LDS each, spinning `us` microseconds");
   m.def("spin_us", &spin_us, "device-side delay of `us` microseconds on the current stream (straggler injection)");
   m.def("relu_bwd", &relu_bwd);

@@ -312,12 +312,36 @@ __global__ __launch_bounds__(256) void maxpool_bwd_fixed_kernel(const bf16_t* __
 // only outputs (oh, ow), (oh, ow + 1), (oh + 1, ow), (oh + 1, ow + 1) reach: 4 dy / index loads per 4 dx stores,
 // instead of 4 per store in the input-centric gather (308 -> ~110 us on the 256 x 64 x 112^2 stem output).
 // Window tap t = r * 3 + s of output (oh, ow) is input (2 oh - 1 + r, 2 ow - 1 + s) (maxpool_fwd_fixed_kernel).
+// BNR: dx is the gradient of a training BN's (ReLU-fused) output (the ResNet stem's BN feeds this pool): the kernel
+// also accumulates that BN's backward reduction (sum dz*m, sum dz*m*(x - mean), m the ReLU mask from the sign bits
+// `zm` or from x*scale + shift) into the slotted statistics `red`, so the BN backward skips its chan_reduce pass over
+// dz and x (csrc/batchnorm.hip chan_reduce_kernel MODE 1 computes the same sums). Needs 256 % (C/8) == 0 so a
+// thread's channel group is fixed over the grid-stride loop.
+struct PoolBnRed {
+  const bf16_t* x;      // the BN's input, same layout as dx
+  const float* mean;
+  const float* aff;     // [scale | shift] (mask from x) or nullptr
+  const uint8_t* zm;    // [P][C/8] sign bits or nullptr
+  float* red;           // [STAT_SLOTS][2][C]
+};
+
+template <bool BNR>
 __global__ __launch_bounds__(256) void maxpool_bwd_k3s2_kernel(const bf16_t* __restrict__ dy,
                                                                const uint8_t* __restrict__ idx, bf16_t* __restrict__ dx,
-                                                               int N, int C, int OH, int OW) {
+                                                               int N, int C, int OH, int OW, PoolBnRed br) {
   const int G = C >> 3;
   const long total = (long)N * OH * OW * G;
   const int W = 2 * OW;
+  float s1[8], s2[8], mu[8], sc[8], sf[8];
+  if (BNR) {
+    const int g0 = threadIdx.x % G;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      s1[e] = 0.f; s2[e] = 0.f; mu[e] = br.mean[g0 * 8 + e];
+      sc[e] = br.aff ? br.aff[g0 * 8 + e] : 0.f;
+      sf[e] = br.aff ? br.aff[C + g0 * 8 + e] : 0.f;
+    }
+  }
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
     const int g = (int)(i % G);
     long p = i / G;
@@ -362,10 +386,45 @@ __global__ __launch_bounds__(256) void maxpool_bwd_k3s2_kernel(const bf16_t* __r
       }
     }
     const long row0 = ((long)n * (2 * OH) + 2 * oh) * W + 2 * ow;
-    reinterpret_cast<v4u*>(dx)[row0 * G + g] = q[0];
-    reinterpret_cast<v4u*>(dx)[(row0 + 1) * G + g] = q[1];
-    reinterpret_cast<v4u*>(dx)[(row0 + W) * G + g] = q[2];
-    reinterpret_cast<v4u*>(dx)[(row0 + W + 1) * G + g] = q[3];
+    const long pix[4] = {row0, row0 + 1, row0 + W, row0 + W + 1};
+    if (BNR) {
+      v4u bx[4];
+      unsigned zb[4] = {0xffu, 0xffu, 0xffu, 0xffu};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        bx[k] = reinterpret_cast<const v4u*>(br.x)[pix[k] * G + g];
+        if (br.zm) zb[k] = br.zm[pix[k] * G + g];
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          // the gradient as stored (bf16), as the unfused reduction reads it back
+          const float d = (e & 1) ? hi_bf(q[k][e >> 1]) : lo_bf(q[k][e >> 1]);
+          const float xv = (e & 1) ? hi_bf(bx[k][e >> 1]) : lo_bf(bx[k][e >> 1]);
+          const bool on = br.zm ? ((zb[k] >> e) & 1u) != 0u : (xv * sc[e] + sf[e] > 0.f);
+          const float dm = on ? d : 0.f;
+          s1[e] += dm;
+          s2[e] += dm * (xv - mu[e]);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) reinterpret_cast<v4u*>(dx)[pix[k] * G + g] = q[k];
+  }
+  if (BNR) {
+    // per-workgroup sums through LDS, then one atomic per (slot, channel, sum) (rows of threads share a group)
+    __shared__ float sm[256 * 16];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { sm[threadIdx.x * 16 + e] = s1[e]; sm[threadIdx.x * 16 + 8 + e] = s2[e]; }
+    __syncthreads();
+    const int rows = 256 / G;
+    for (int w = threadIdx.x; w < G * 16; w += 256) {
+      const int gg = w >> 4, slot = w & 15;
+      float t = 0.f;
+      for (int r = 0; r < rows; ++r) t += sm[(r * G + gg) * 16 + slot];
+      const int ch = gg * 8 + (slot & 7);
+      atomicAdd(br.red + (size_t)(blockIdx.x & (BIGDL_STAT_SLOTS - 1)) * 2 * C + (slot < 8 ? 0 : C) + ch, t);
+    }
   }
 }
 
@@ -820,13 +879,33 @@ void bigdl_maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* idx, int N, int 
     maxpool_fwd_kernel<<<grid_cap(outs), 256, 0, st>>>(x, y, idx, N, H, W, C, OH, OW, kh, kw, sh, sw, ph, pw);
   HIP_LAUNCH_CHECK();
 }
+static bool maxpool_k3s2_ok(int H, int W, int C, int OH, int OW, int kh, int kw, int sh, int sw, int ph, int pw,
+                            long ins, long outs) {
+  static const bool k3s2 = [] { const char* e = getenv("BIGDL_POOL_BWD_K3S2"); return e ? atoi(e) != 0 : true; }();
+  return k3s2 && kh == 3 && kw == 3 && sh == 2 && sw == 2 && ph == 1 && pw == 1 && H == 2 * OH && W == 2 * OW &&
+         C % 8 == 0 && ins < (1l << 31) && outs < (1l << 31);
+}
+int bigdl_maxpool_bwd_bnred_applies(int N, int H, int W, int C, int OH, int OW, int kh, int kw, int sh, int sw, int ph,
+                                    int pw) {
+  const long ins = (long)N * H * W * (C / 8), outs = (long)N * OH * OW * C;
+  return maxpool_k3s2_ok(H, W, C, OH, OW, kh, kw, sh, sw, ph, pw, ins, outs) && 256 % (C / 8) == 0 &&
+         !bigdl_deterministic();
+}
+// maxpool backward fused with the backward reduction of the BN that produced the pool's input (see PoolBnRed)
+void bigdl_maxpool_bwd_bnred(const uint16_t* dy, const uint8_t* idx, uint16_t* dx, int N, int C, int OH, int OW,
+                             const uint16_t* bx, const float* mean, const float* aff, const uint8_t* zm, float* red,
+                             hipStream_t st) {
+  const PoolBnRed br{reinterpret_cast<const bf16_t*>(bx), mean, aff, zm, red};
+  maxpool_bwd_k3s2_kernel<true><<<grid_cap((long)N * OH * OW * (C / 8), 2048), 256, 0, st>>>(dy, idx, dx, N, C, OH,
+                                                                                              OW, br);
+  HIP_LAUNCH_CHECK();
+}
 void bigdl_maxpool_bwd(const uint16_t* dy, const uint8_t* idx, uint16_t* dx, int N, int H, int W, int C, int OH,
                        int OW, int kh, int kw, int sh, int sw, int ph, int pw, hipStream_t st) {
   const long ins = (long)N * H * W * (C / 8), outs = (long)N * OH * OW * C;
-  static const bool k3s2 = [] { const char* e = getenv("BIGDL_POOL_BWD_K3S2"); return e ? atoi(e) != 0 : true; }();
-  if (k3s2 && kh == 3 && kw == 3 && sh == 2 && sw == 2 && ph == 1 && pw == 1 && H == 2 * OH && W == 2 * OW &&
-      C % 8 == 0 && ins < (1l << 31) && outs < (1l << 31))
-    maxpool_bwd_k3s2_kernel<<<grid_cap((long)N * OH * OW * (C / 8)), 256, 0, st>>>(dy, idx, dx, N, C, OH, OW);
+  if (maxpool_k3s2_ok(H, W, C, OH, OW, kh, kw, sh, sw, ph, pw, ins, outs))
+    maxpool_bwd_k3s2_kernel<false><<<grid_cap((long)N * OH * OW * (C / 8)), 256, 0, st>>>(dy, idx, dx, N, C, OH, OW,
+                                                                                         PoolBnRed{});
   else if (kh == 3 && kw == 3 && sh == 2 && sw == 2 && ins < (1l << 31) && outs < (1l << 31))
     maxpool_bwd_fixed_kernel<3, 2><<<grid_cap(ins), 256, 0, st>>>(dy, idx, dx, N, H, W, C, OH, OW, ph, pw);
   else

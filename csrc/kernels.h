@@ -133,7 +133,10 @@ void bigdl_bn_bwd_reduce(const uint16_t* dz, const uint16_t* z, const uint16_t* 
 void bigdl_bn_bwd_apply(const uint16_t* dz, const uint16_t* z, const uint16_t* x, const float* mean,
                         const float* invstd, const float* gamma, const float* red, int nslots, float* coef,
                         uint16_t* dx, uint16_t* dres, float* dgamma, float* dbeta, long P, int C, int training,
-                        const float* aff, hipStream_t st, const uint8_t* zm = nullptr);
+                        const float* aff, hipStream_t st, const uint8_t* zm = nullptr,
+                        const uint16_t* x2 = nullptr, const float* mean2 = nullptr, float* red2 = nullptr);
+// x2 / mean2 / red2: also accumulate the backward reduction of a second (ReLU-less) BN whose output gradient is dres
+// (input x2, same layout; mean2) into the slotted red2 (requires dres; csrc/batchnorm.hip bn_bwd_apply_kernel R2)
 // zm: [P][C / 8] sign bytes of the post-ReLU output (bit e of byte (p, g) = channel 8g + e > 0), written by
 // bigdl_bn_apply when non-null and read in place of z by the backward passes (1/16 of z's bytes)
 
@@ -153,6 +156,12 @@ void bigdl_cast_bf16_f32(const uint16_t* x, float* y, long n, hipStream_t st);
 // pooling (NHWC bf16)
 void bigdl_maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* idx, int N, int H, int W, int C, int OH,
                        int OW, int kh, int kw, int sh, int sw, int ph, int pw, hipStream_t st);
+void bigdl_split_reduce_f32(const float* ws, float* dw, long n, int splits, hipStream_t st);
+int bigdl_maxpool_bwd_bnred_applies(int N, int H, int W, int C, int OH, int OW, int kh, int kw, int sh, int sw, int ph,
+                                    int pw);
+void bigdl_maxpool_bwd_bnred(const uint16_t* dy, const uint8_t* idx, uint16_t* dx, int N, int C, int OH, int OW,
+                             const uint16_t* bx, const float* mean, const float* aff, const uint8_t* zm, float* red,
+                             hipStream_t st);
 void bigdl_maxpool_bwd(const uint16_t* dy, const uint8_t* idx, uint16_t* dx, int N, int H, int W, int C,
                        int OH, int OW, int kh, int kw, int sh, int sw, int ph, int pw, hipStream_t st);
 void bigdl_avgpool_fwd(const uint16_t* x, uint16_t* y, int N, int H, int W, int C, int OH, int OW, int kh,

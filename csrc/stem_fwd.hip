@@ -279,21 +279,6 @@ __global__ __launch_bounds__(448, 1) void stem_wgrad_kernel(WgradArgs a) {
   }
 }
 
-// dw[i] += sum over the partials of ws[s][i], in a fixed order
-__global__ __launch_bounds__(256) void stem_wgrad_reduce_kernel(const float* __restrict__ ws, float* __restrict__ dw,
-                                                                int n, int parts) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= n) return;
-  float s0 = 0.f, s1 = 0.f;
-  int k = 0;
-  for (; k + 1 < parts; k += 2) {
-    s0 += ws[(size_t)k * n + i];
-    s1 += ws[(size_t)(k + 1) * n + i];
-  }
-  if (k < parts) s0 += ws[(size_t)k * n + i];
-  dw[i] += s0 + s1;
-}
-
 }  // namespace
 
 extern "C" {
@@ -334,9 +319,8 @@ int bigdl_stem_wgrad(const WgradArgs* a, hipStream_t st) {
   const long tiles = (long)a->Nb * (a->OH / SWRB);
   const int grid = (int)std::min<long>(tiles, stem_wgrad_grid());
   stem_wgrad_kernel<115><<<dim3(grid), dim3(448), 0, st>>>(*a);
-  stem_wgrad_reduce_kernel<<<dim3((64 * 224 + 255) / 256), dim3(256), 0, st>>>(a->ws, a->dw, 64 * 224, grid);
-  if (a->dbias)
-    stem_wgrad_reduce_kernel<<<dim3(1), dim3(256), 0, st>>>(a->ws + (size_t)grid * 64 * 224, a->dbias, 64, grid);
+  bigdl_split_reduce_f32(a->ws, a->dw, 64 * 224, grid, st);
+  if (a->dbias) bigdl_split_reduce_f32(a->ws + (size_t)grid * 64 * 224, a->dbias, 64, grid, st);
   return 0;
 }
 

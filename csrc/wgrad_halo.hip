@@ -420,4 +420,13 @@ int bigdl_wgrad_halo(const WgradArgs* a, hipStream_t st) {
   return 0;
 }
 
+// dw[i] += sum over s of ws[s * n + i] (n % 4 == 0) in a fixed order, split-parallel: the stem weight gradient's
+// per-workgroup partials (csrc/stem_fwd.hip) use the same reduce as the halo weight gradient
+void bigdl_split_reduce_f32(const float* ws, float* dw, long n, int splits, hipStream_t st) {
+  const long n4 = n / 4;
+  halo_reduce_kernel<<<dim3((unsigned)((n4 + 15) / 16)), dim3(256), 0, st>>>(
+      ws, dw, n4, splits, (reinterpret_cast<uintptr_t>(dw) & 15) == 0);
+  HIP_LAUNCH_CHECK();
+}
+
 }  // extern "C"

@@ -213,6 +213,36 @@ def test_bn_fwd_bwd(res, relu):
         assert _rel(dx3, dx) < 1e-5 and _rel(dg3, dg) < 1e-5 and _rel(db3, dbt) < 1e-5
 
 
+@pytest.mark.parametrize("C,zmask", [(64, True), (256, False), (512, True), (2048, True), (24, True)])
+def test_bn_bwd_apply_second_bn_reduction(C, zmask):
+    """The residual-branch gradient pass also reducing a second (ReLU-less) BN over dres (projection shortcut): the
+    slotted sums equal bn_bwd_reduce over the dres it wrote, and dx / dres are unchanged bit for bit."""
+    from bigdl_amd.ops import bn, native
+
+    dev = _dev()
+    torch.manual_seed(2)
+    N, H, W = 3, 7, 9
+    x = (torch.randn(N, C, H, W, device=dev) * 2 + 0.5).to(BF, memory_format=CL)
+    r = torch.randn(N, C, H, W, device=dev).to(BF, memory_format=CL)
+    x2 = (torch.randn(N, C, H, W, device=dev) - 0.2).to(BF, memory_format=CL)
+    g, b = torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev)
+    rm, rv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+    zm = torch.empty(x.numel() // 8, dtype=torch.uint8, device=dev) if zmask else None
+    y, sm, si, _ = bn.bn_forward_gpu(x, g, b, rm, rv, 1e-3, 0.1, True, res=r, relu=True, zm=zm)
+    z = None if zmask else y
+    mean2 = torch.randn(C, device=dev) * 0.1
+    gz = torch.randn(N, C, H, W, device=dev).to(BF, memory_format=CL)
+    dg0, db0 = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
+    dx0, dres0 = bn.bn_backward_gpu(gz, z, x, sm, si, g, dg0, db0, need_dres=True, zm=zm)
+    red2 = bn.new_stats(C, dev)
+    dg1, db1 = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
+    dx1, dres1 = bn.bn_backward_gpu(gz, z, x, sm, si, g, dg1, db1, need_dres=True, zm=zm, sec=(x2, mean2, red2))
+    assert torch.equal(dres1, dres0) and _rel(dx1, dx0) < 1e-5
+    ref = bn.new_stats(C, dev)
+    native.get().bn_bwd_reduce(dres0, None, x2, mean2, ref, N * H * W, C, None, None)
+    assert torch.allclose(red2.view(-1, 2 * C).sum(0), ref.view(-1, 2 * C).sum(0), rtol=1e-4, atol=1e-3)
+
+
 def test_maxpool_avgpool():
     from bigdl_amd.ops import pool
 
@@ -254,6 +284,41 @@ def test_maxpool_window_variants(shape, k, s, p, ceil):
     dx = pool.maxpool_bwd_gpu(gy, idx, x.shape, k, k, s, s, p, p)
     yr.backward(gy.float())
     assert _rel(dx, xr.grad) < 1e-2
+
+
+@pytest.mark.parametrize("shape,mask", [((4, 64, 28, 22), "aff"), ((3, 64, 16, 20), "zm"), ((2, 128, 12, 14), "aff"),
+                                        ((2, 16, 10, 8), "zm")])
+def test_maxpool_bwd_bn_reduction(shape, mask):
+    """k3 s2 maxpool backward fused with the producing BN's backward reduction (the ResNet stem): dx bit-exact vs the
+    plain kernel, the slotted sums vs bn_bwd_reduce over that dx, and the BN backward from them vs the unfused one."""
+    from bigdl_amd.ops import bn, native, pool
+
+    dev = _dev()
+    torch.manual_seed(1)
+    N, C, H, W = shape
+    x = (torch.randn(*shape, device=dev) * 2 + 0.3).to(BF, memory_format=CL)
+    g, b = torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev)
+    rm, rv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+    zm = torch.empty(x.numel() // 8, dtype=torch.uint8, device=dev) if mask == "zm" else None
+    y, sm, si, aff = bn.bn_forward_gpu(x, g, b, rm, rv, 1e-3, 0.1, True, relu=True, zm=zm)
+    p, idx = pool.maxpool_fwd_gpu(y, 3, 3, 2, 2, 1, 1)
+    gp = torch.randn(p.shape, device=dev).to(BF, memory_format=CL)
+    dx0 = pool.maxpool_bwd_gpu(gp, idx, y.shape, 3, 3, 2, 2, 1, 1)
+    src = (None, x, sm, aff if zm is None else None, zm if zm is not None else False)
+    dx1, red = pool.maxpool_bwd_bnred_gpu(gp, idx, y.shape, 3, 3, 2, 2, 1, 1, src)
+    assert red is not None and torch.equal(dx1, dx0)
+    C_ = native.get()
+    ref = bn.new_stats(C, dev)
+    C_.bn_bwd_reduce(dx0, None, x, sm, ref, N * H * W, C, aff if zm is None else None, zm)
+    s_fused = red.view(-1, 2 * C).sum(0)
+    s_ref = ref.view(-1, 2 * C).sum(0)
+    assert torch.allclose(s_fused, s_ref, rtol=1e-4, atol=1e-3)
+    dg0, db0 = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
+    dg1, db1 = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
+    kw = dict(aff=aff) if zm is None else dict(zm=zm)
+    bx0, _ = bn.bn_backward_gpu(dx0, None, x, sm, si, g, dg0, db0, **kw)
+    bx1, _ = bn.bn_backward_gpu(dx1, None, x, sm, si, g, dg1, db1, red=red, **kw)
+    assert _rel(bx1, bx0) < 1e-3 and _rel(dg1, dg0) < 1e-4 and _rel(db1, db0) < 1e-4
 
 
 def test_softmax_xent():

@@ -269,8 +269,12 @@ def test_dgrad_epilogue_bn_reduction_matches_separate_pass(monkeypatch):
 
     monkeypatch.setattr(C_, "bn_bwd_reduce", counting)
     res = {}
+    from bigdl_amd.nn import fusion
+
     for mode in ("0", "1"):
         monkeypatch.setenv("BIGDL_DGRAD_BN", mode)     # fusion on / off (see nn/fusion.py)
+        # projection-shortcut BNs reduced by the pass that writes the residual gradient: on / off with the rest
+        monkeypatch.setattr(fusion, "SHORTCUT_BN_RED", [mode == "1"])
         m = copy.deepcopy(cpu).to("cuda")
         fuse_for_training(m)
         calls.clear()
@@ -281,8 +285,9 @@ def test_dgrad_epilogue_bn_reduction_matches_separate_pass(monkeypatch):
         res[mode] = (gx.float(), _weight_grads(m), len(calls))
     n_bn = sum(isinstance(q, nn.BatchNormalization) for q in cpu.flattened_layers())
     assert res["0"][2] == n_bn
-    # fused: 2 branch BNs per block + block 1's last BN (through block 2's folded conv1 dgrad)
-    assert res["1"][2] == n_bn - 5
+    # fused: 2 branch BNs per block + block 1's last BN (through block 2's folded conv1 dgrad) + both blocks'
+    # projection-shortcut BNs (in their block's residual-gradient pass)
+    assert res["1"][2] == n_bn - 7
     assert _rel(res["1"][0], res["0"][0]) < 2e-2
     assert _rel(res["1"][1], res["0"][1]) < 2e-2
 

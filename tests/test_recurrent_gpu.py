@@ -213,17 +213,25 @@ def _hogged_lstm_forward(timeout_us, hog_us=300e3, n_hog=64, B=128, T=8, H=1024)
     torch.cuda.synchronize()
     native.check_persistent()
     done = torch.zeros(n_hog, dtype=torch.int32, device="cuda")
-    side = torch.cuda.Stream()
+    # a high-priority stream gets a hardware queue of its own: a normal-priority side stream may share the default
+    # stream's queue (GPU_MAX_HW_QUEUES = 4 and earlier tests created many streams), which serialises the two launches
+    side = torch.cuda.Stream(priority=-1)
+    hog_end, run_start = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     C.set_seq_timeout_us(timeout_us)
     try:
         with torch.cuda.stream(side):
             C.hog_cus(n_hog, hog_us, done)
+            hog_end.record()
         time.sleep(0.05)                 # the hog is resident before the persistent launch is queued
+        run_start.record()
         out, cs = run()
         torch.cuda.synchronize()
     finally:
         C.set_seq_timeout_us(0)
     assert int((done > 0).sum()) == n_hog
+    if hog_end.elapsed_time(run_start) > 0:   # the persistent launch started after the hog ended, not beside it
+        native.check_persistent()
+        pytest.skip("the hog and the persistent launch were not concurrent (shared hardware queue)")
     return ref, ref_cs, out, cs
 
 
