@@ -90,7 +90,10 @@ class SegmentedGraph:
         self._g = torch.cuda.CUDAGraph()
         if _DOT_DIR:
             self._g.enable_debug_mode()
-        self._g.capture_begin(pool=self.pool)
+        # thread-local capture: collectives launched eagerly between segments stay in the process group's watchdog
+        # list, and that thread's event queries are illegal under a process-wide ("global") capture — RCCL's watchdog
+        # then aborts the job (hipErrorStreamCaptureUnsupported). Only this thread's calls are restricted.
+        self._g.capture_begin(pool=self.pool, capture_error_mode="thread_local")
 
     def _end(self):
         g = self._g
