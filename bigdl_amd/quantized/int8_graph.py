@@ -18,6 +18,8 @@ Scales: a calibration batch is run through the quantized graph and the abs-max o
 Tensors that must share a scale (a pool's input and output, a concat's inputs and output, pass-through ReLU /
 dropout / flatten) form one class (union-find); the class scale is max |x| / 127 over its members.
 """
+import os
+
 import torch
 
 from ..nn.activation import ReLU
@@ -78,6 +80,17 @@ def _stem_ok(m):
 
     return (os.environ.get("BIGDL_I8_STEM", "1") != "0" and _conv_ok(m) and m.nInputPlane <= 4
             and m.kernelW <= 8 and m.dilationW == 1 and m.dilationH == 1)
+
+
+# BIGDL_I8_STEM_F32=0: quantize the image into the stem's width im2col first instead of inside the stem kernel
+_STEM_F32 = os.environ.get("BIGDL_I8_STEM_F32", "1") != "0"
+
+
+def _wim2col(x, OW, stem, pw, scale):
+    N, _, H, _ = x.shape
+    q = torch.empty((N, H, OW, 32), dtype=torch.int8, device=x.device)
+    native.get().quantize_wim2col_f32(x, q, OW, stem.kernelW, stem.strideW, pw, float(scale))
+    return q
 
 
 def _stem_weight(m):
@@ -355,9 +368,9 @@ class Int8GraphPlan:
             if stem is not None and C == stem.nInputPlane:
                 ph, pw = stem._pads(H, W)
                 OW = out_size(W, stem.kernelW, stem.strideW, pw, 1)
-                q = torch.empty((N, H, OW, 32), dtype=torch.int8, device=x.device)
-                native.get().quantize_wim2col_f32(x, q, OW, stem.kernelW, stem.strideW, pw, float(scale))
-                return I8Stem(q, x, scale, OW)
+                if _STEM_F32 and C <= 3 and W == 224:
+                    return I8Stem(None, x, scale, OW)     # quantized inside the stem kernel (or by stem_run)
+                return I8Stem(_wim2col(x, OW, stem, pw, scale), x, scale, OW)
             q = _i8_buffer((N, H, W, _ceil16(C)), C, x.device)
             native.get().quantize_nchw_f32(x, q, _ceil16(C), float(scale))
             return I8Act(q, C, scale)
@@ -451,16 +464,24 @@ class Int8GraphPlan:
             geo = [N, H, OW, 32, OH, OW, m.strideH, 1, R * 32, K, K, OH, OW, 1, 1, 0, 0]
             relu = m.fuse_relu
             wp = _stem_weight(m)
+            dev = x.x.device
             if out8 and not residual:
-                dst, _ = self._dest(n, N, OH, OW, K, x.data.device)
+                dst, _ = self._dest(n, N, OH, OW, K, dev)
                 geo[10] = dst.stride(2)
-                native.get().conv_i8(x.data, wp, dst, m.bias, None, m.weightScale, geo, taps, relu, float(x.scale),
-                                     float(oscale), None, 0.0)
-                return I8Act(dst, K, oscale)
-            y = torch.empty((N, K, OH, OW), dtype=BF16, device=x.data.device, memory_format=CL)
-            native.get().conv_i8(x.data, wp, y, m.bias, None, m.weightScale, geo, taps, relu, float(x.scale), 0.0,
+                out_t, osc, ret = dst, float(oscale), I8Act(dst, K, oscale)
+            else:
+                out_t = torch.empty((N, K, OH, OW), dtype=BF16, device=dev, memory_format=CL)
+                osc, ret = 0.0, out_t
+            if x.data is None:
+                # fp32 image straight into the stem kernel (the lanes quantize their own operands)
+                if native.get().conv_i8_stem_f32(x.x, wp, out_t, m.bias, m.weightScale, geo, taps, relu,
+                                                 float(x.scale), osc):
+                    return ret
+                _, pw = m._pads(H, W)
+                x.data = _wim2col(x.x, OW, m, pw, x.scale)
+            native.get().conv_i8(x.data, wp, out_t, m.bias, None, m.weightScale, geo, taps, relu, float(x.scale), osc,
                                  None, 0.0)
-            return y
+            return ret
         return run
 
     def _linear_runner(self, n):

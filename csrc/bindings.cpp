@@ -582,6 +582,46 @@ void conv_i8(const Tensor& src, const Tensor& wt, const Tensor& out, const OptT&
   TORCH_CHECK(rc == 0, "conv_i8: unsupported shape (channels must be a multiple of 16)");
 }
 
+// int8 7x7/2 image stem straight from the fp32 NCHW image (conv_halo.hip stem_i8f_kernel): geo / taps are the width-
+// im2col geometry conv_i8 would get for quantize_wim2col_f32's output (Hs = image rows), `scale` the input
+// quantization scale (quantize with 1 / scale, dequantize with scale). Returns false when the kernel does not apply
+// (the caller then quantizes into the im2col and calls conv_i8).
+bool conv_i8_stem_f32(const Tensor& x, const Tensor& wt, const Tensor& out, const OptT& bias, const Tensor& wscale,
+                      std::vector<int64_t> geo, std::vector<int64_t> taps, bool relu, double scale, double out_scale) {
+  TORCH_CHECK(geo.size() == 17 && taps.size() % 3 == 0 && !taps.empty() && taps.size() / 3 <= CONV_MAX_TAPS,
+              "conv_i8_stem_f32: bad geometry");
+  TORCH_CHECK(x.dim() == 4 && x.is_contiguous() && x.scalar_type() == at::kFloat && x.is_cuda() && x.size(0) == geo[0] &&
+                  x.size(2) == geo[1], "conv_i8_stem_f32: x must be the fp32 NCHW image of the geometry");
+  TORCH_CHECK(wt.scalar_type() == at::kChar && wt.is_cuda() && wt.is_contiguous(), "conv_i8_stem_f32: int8 weight");
+  const int mode = out.scalar_type() == at::kFloat ? 1 : out.scalar_type() == at::kChar ? 2 : 0;
+  TORCH_CHECK(mode != 0 || out.scalar_type() == at::kBFloat16, "conv_i8_stem_f32: out bf16, fp32 or int8");
+  TORCH_CHECK(mode != 2 || out_scale > 0, "conv_i8_stem_f32: int8 output needs out_scale > 0");
+  TORCH_CHECK(scale > 0 && wscale.numel() >= geo[9] && wscale.scalar_type() == at::kFloat, "conv_i8_stem_f32: scales");
+  ConvArgs a{};
+  a.src = nullptr;
+  a.wt = reinterpret_cast<const uint16_t*>(wt.data_ptr<int8_t>());
+  a.out = reinterpret_cast<uint16_t*>(out.data_ptr());
+  a.bias = ocf(bias, "bias");
+  a.Nb = geo[0]; a.Hs = geo[1]; a.Ws = geo[2]; a.Cs = geo[3]; a.OH = geo[4]; a.OW = geo[5];
+  a.mul_h = geo[6]; a.mul_w = geo[7]; a.ldw = geo[8]; a.Ncol = geo[9]; a.ldo = geo[10];
+  a.OHo = geo[11]; a.OWo = geo[12]; a.omul_h = geo[13]; a.omul_w = geo[14]; a.ooff_h = geo[15]; a.ooff_w = geo[16];
+  a.ntaps = (int)(taps.size() / 3);
+  a.Kdim = a.ntaps * a.Cs;
+  a.M = a.Nb * a.OH * a.OW;
+  a.ident_out = 1;
+  a.relu = relu ? 1 : 0;
+  for (int t = 0; t < a.ntaps; ++t) {
+    a.tap_h[t] = (short)taps[3 * t]; a.tap_w[t] = (short)taps[3 * t + 1]; a.tap_k[t] = (short)taps[3 * t + 2];
+  }
+  TORCH_CHECK(wt.numel() >= (int64_t)a.Ncol * a.ldw, "conv_i8_stem_f32: weight too small");
+  const int64_t out_avail = (int64_t)(out.storage().nbytes() / out.element_size()) - out.storage_offset();
+  TORCH_CHECK(a.ldo >= a.Ncol && out_avail >= (int64_t)(a.M - 1) * a.ldo + a.Ncol, "conv_i8_stem_f32: out too small");
+  const I8Epi ep{nullptr, (float)scale, wscale.data_ptr<float>(), mode, mode == 2 ? (float)(1.0 / out_scale) : 0.f,
+                 nullptr, 0.f, 0};
+  return bigdl_stem_i8_f32(&a, &ep, x.data_ptr<float>(), (int)x.size(1), (int)x.size(3), (float)(1.0 / scale),
+                           stream()) == 0;
+}
+
 void pool_i8(const Tensor& x, const Tensor& y, std::vector<int64_t> g, bool avg, bool count_pad) {
   // g = [N, H, W, Cp, OH, OW, kh, kw, sh, sw, ph, pw, ldo]
   TORCH_CHECK(g.size() == 13 && x.scalar_type() == at::kChar && y.scalar_type() == at::kChar && x.is_cuda() &&
@@ -1396,6 +1436,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_conv_impl", &bigdl_set_conv_impl);
   m.def("set_conv_s1", &bigdl_set_conv_s1);
   m.def("set_conv_halo", &bigdl_set_conv_halo);
+  m.def("conv_i8_stem_f32", &conv_i8_stem_f32, "int8 7x7/2 stem straight from the fp32 image (false: not applicable)");
+  m.def("set_stem_i8", &bigdl_set_stem_i8, "int8 image stem kernel on (1) / off (0)");
   m.def("set_stem_fwd", &bigdl_set_stem_fwd);
   m.def("set_stem_wgrad", &bigdl_set_stem_wgrad);
   m.def("cu_masked_stream", &cu_masked_stream, "HIP stream restricted to a CU mask (32 CUs per word)");

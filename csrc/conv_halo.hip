@@ -485,6 +485,179 @@ void launch_halo_f(const ConvArgs& a, hipStream_t st) {
   else conv_halo_kernel<W, RB, NIMG, KT, WPX, 1><<<g, b, 0, st>>>(a, I8Epi{});
 }
 
+// ------------------------------------------------------------------------------------------------
+// int8 image stem (7x7 / stride 2 / pad 3, 64 output channels, 224 -> 112) over the width im2col the input quantizer
+// writes (quant.hip quantize_wim2col_f32: row (n, h, ow) = 32 bytes, byte e * 4 + c = q(x[c][h][2 ow + e - 3])): an
+// R x 1 convolution with a reduction of 7 x 32 bytes. A workgroup stages the 13 input rows its 4 output rows need
+// (one contiguous block of the im2col, LDS-DMA; rows above / below the image come back as zeros through out-of-range
+// buffer offsets) plus the 64 x 224 weight (rows padded to 256 bytes, taps 7 zero); each wave computes one output row
+// (7 fragments of 16 columns x 64 channels) in 4 K-steps of v_mfma_i32_16x16x64_i8, a K-step = two row taps (lane
+// group g: row tap 2 s + (g >> 1), bytes (g & 1) * 16 of the 32-byte column). Integer accumulation: bit-equal to the
+// generic int8 implicit GEMM (conv_i8_g3). Epilogue: halo_epi_i8 (dequantize, bias, ReLU, requantize / bf16 / fp32).
+constexpr int SI_RB = 4, SI_OW = 112, SI_ROW = SI_OW * 32, SI_XROWS = 2 * SI_RB + 5;   // 13 staged input rows
+constexpr int SI_XCH = (SI_XROWS * SI_ROW + 1023) / 1024;                           // 1 KiB DMA chunks (46)
+constexpr int SI_XG = (SI_XCH + 3) / 4;                                               // chunks per wave
+constexpr int SI_XB = (SI_XROWS + 1) * SI_ROW;    // + the row wave 3's zero-weight tap 7 reads
+constexpr int SI_WST = 272;                       // weight row stride (256 bytes + 16: conflict-free reads)
+constexpr int SI_WOFF = ((SI_XG * 4 * 1024 > SI_XB ? SI_XG * 4 * 1024 : SI_XB) + 1023) / 1024 * 1024;
+constexpr int SI_LDS = SI_WOFF + 64 * SI_WST;
+
+struct LinRowMap {
+  long base;
+  __device__ __forceinline__ long operator()(const ConvArgs&, int v) const { return base + v; }
+};
+
+__global__ __launch_bounds__(256, 2) void stem_i8_kernel(ConvArgs a, I8Epi ep) {
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[SI_LDS];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tiles_img = a.OH / SI_RB;
+  const int bid = xcd_remap(blockIdx.x, a.Nb * tiles_img);
+  const int n = bid / tiles_img, oh0 = (bid - n * tiles_img) * SI_RB;
+  // im2col rows 2 oh0 - 3 .. 2 oh0 + 9 of image n; offsets before the image wrap to huge unsigned values, past it
+  // they exceed the record count: both read as zeros
+  const int8_t* src = reinterpret_cast<const int8_t*>(a.src) + (size_t)n * a.Hs * SI_ROW;
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(const_cast<int8_t*>(src), (short)0,
+                                                                      a.Hs * SI_ROW, 0x00020000);
+  const int row0 = (2 * oh0 - 3) * SI_ROW;
+#pragma unroll
+  for (int d = 0; d < SI_XG; ++d) {
+    const int ch = d * 4 + wave;
+    if (ch < SI_XCH)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (LDS_PTR(void))(lds + ch * 1024), 16,
+                                               (int)(unsigned)(row0 + (ch * 64 + lane) * 16), 0, 0, 0);
+  }
+  // weights [64][224] -> rows of 256 (+16) bytes, bytes 224..255 (row tap 7) zero
+  const int8_t* wt = reinterpret_cast<const int8_t*>(a.wt);
+#pragma unroll
+  for (int q = tid; q < 64 * 16; q += 256) {
+    const int k = q >> 4, gr = q & 15;
+    const v4u v = gr < 14 ? *reinterpret_cast<const v4u*>(wt + (size_t)k * a.ldw + gr * 16) : v4u{0u, 0u, 0u, 0u};
+    *reinterpret_cast<v4u*>(lds + SI_WOFF + k * SI_WST + gr * 16) = v;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  constexpr int FM = SI_OW / 16;
+  v4i acc[FM][4];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = v4i{0, 0, 0, 0};
+  const int g = lane >> 4, col = lane & 15;
+  const unsigned char* Wl = lds + SI_WOFF + col * SI_WST + g * 16;
+  const unsigned char* Xl = lds + (2 * wave + (g >> 1)) * SI_ROW + col * 32 + (g & 1) * 16;
+#pragma unroll
+  for (int st = 0; st < 4; ++st) {
+    v4i fw[4], fx[FM];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) fw[j] = *reinterpret_cast<const v4i*>(Wl + j * 16 * SI_WST + st * 64);
+#pragma unroll
+    for (int i = 0; i < FM; ++i) fx[i] = *reinterpret_cast<const v4i*>(Xl + 2 * st * SI_ROW + i * 16 * 32);
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fw[j], fx[i], acc[i][j], 0, 0, 0);
+  }
+  const LinRowMap rm{((long)n * a.OH + oh0) * SI_OW};
+  halo_epi_i8<FM, 4>(a, ep, acc, wave * SI_OW, 0, lane, rm);
+}
+
+// The same stem straight from the fp32 NCHW image (C <= 3 channels, 224 x 224): the workgroup stages its 13 input
+// rows x 3 channel planes as fp32 (lane-gathered LDS-DMA: 39 row segments of 896 bytes, rows outside the image read
+// as zeros), quantizes every staged pixel once into an int8 plane [13 rows][3 + 224 + 5 pixels][4 channel bytes]
+// (the quantizer's exact expression, rint(x * inv) clamped to +-127), and reads each MFMA operand — 4 width taps x 4
+// channel bytes of one output column, the 16 bytes the width im2col would hold — as 16 contiguous plane bytes
+// (pixels 2 ow + 4 (g & 1) .. + 3; the 4th tap of the upper group is tap 7, whose weights are zero). No im2col
+// tensor is written or read: the quantize pass (~0.13 ms at batch 256) and the im2col read disappear.
+constexpr int SF_W = 224, SF_SEG = SF_W * 4, SF_NSEG = SI_XROWS * 3;                  // 896-byte row segments
+constexpr int SF_GR = SF_NSEG * (SF_SEG / 16);                                          // 2184 granules
+constexpr int SF_CH = (SF_GR + 63) / 64, SF_XG = (SF_CH + 3) / 4;                       // 35 chunks, 9 per wave
+constexpr int SF_PW = 232;                                   // int8 plane row: 3 pad + 224 + 5 pad pixels x 4 bytes
+constexpr int SF_POFF = SF_XG * 4 * 1024;
+constexpr int SF_WOFF = (SF_POFF + SI_XROWS * SF_PW * 4 + 1023) / 1024 * 1024;
+constexpr int SF_LDS = SF_WOFF + 64 * SI_WST;
+
+__global__ __launch_bounds__(256, 2) void stem_i8f_kernel(ConvArgs a, I8Epi ep, const float* __restrict__ img, int C,
+                                                          float inv) {
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[SF_LDS];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tiles_img = a.OH / SI_RB;
+  const int bid = xcd_remap(blockIdx.x, a.Nb * tiles_img);
+  const int n = bid / tiles_img, oh0 = (bid - n * tiles_img) * SI_RB;
+  const int H = a.Hs;
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(img), (short)0,
+                                                                      (int)((size_t)a.Nb * C * H * SF_SEG), 0x00020000);
+  // LDS segment sg = t * 3 + c holds image row 2 oh0 - 3 + t of channel c (zeros for c >= C or rows off the image)
+#pragma unroll
+  for (int d = 0; d < SF_XG; ++d) {
+    const int ch = d * 4 + wave;
+    const int q = ch * 64 + lane, sg = q / 56, gi = q - sg * 56;
+    const int t = sg / 3, c = sg - t * 3, h = 2 * oh0 - 3 + t;
+    const bool ok = q < SF_GR && c < C && h >= 0 && h < H;
+    const unsigned off = ok ? (unsigned)((((size_t)n * C + c) * H + h) * SF_SEG + gi * 16) : EOOB;
+    if (ch < SF_CH)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (LDS_PTR(void))(lds + ch * 1024), 16, (int)off, 0, 0, 0);
+  }
+  const int8_t* wt = reinterpret_cast<const int8_t*>(a.wt);
+#pragma unroll
+  for (int q = tid; q < 64 * 16; q += 256) {
+    const int k = q >> 4, gr = q & 15;
+    const v4u v = gr < 14 ? *reinterpret_cast<const v4u*>(wt + (size_t)k * a.ldw + gr * 16) : v4u{0u, 0u, 0u, 0u};
+    *reinterpret_cast<v4u*>(lds + SF_WOFF + k * SI_WST + gr * 16) = v;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  {
+    const float* F = reinterpret_cast<const float*>(lds);
+    unsigned* P = reinterpret_cast<unsigned*>(lds + SF_POFF);
+    for (int q = tid; q < SI_XROWS * SF_PW; q += 256) {
+      const int t = q / SF_PW, w = q - t * SF_PW - 3;
+      unsigned u = 0u;
+      if ((unsigned)w < (unsigned)SF_W) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          const int v = max(-127, min(127, __float2int_rn(F[(t * 3 + c) * SF_W + w] * inv)));
+          u |= (unsigned)(v & 0xff) << (8 * c);
+        }
+      }
+      P[q] = u;
+    }
+  }
+  __syncthreads();
+
+  constexpr int FM = SI_OW / 16;
+  v4i acc[FM][4];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = v4i{0, 0, 0, 0};
+  const int g = lane >> 4, col = lane & 15;
+  const unsigned char* Wl = lds + SF_WOFF + col * SI_WST + g * 16;
+#pragma unroll
+  for (int st = 0; st < 4; ++st) {
+    const int r = 2 * st + (g >> 1);                 // row tap of this lane group (7: zero weights, any data)
+    const int t = 2 * wave + (r < 7 ? r : 6);
+    const unsigned char* Pl = lds + SF_POFF + (t * SF_PW + 2 * col + 4 * (g & 1)) * 4;
+    v4i fw[4], fx[FM];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) fw[j] = *reinterpret_cast<const v4i*>(Wl + j * 16 * SI_WST + st * 64);
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const v2u lo = *reinterpret_cast<const v2u*>(Pl + i * 32 * 4), hi = *reinterpret_cast<const v2u*>(Pl + i * 32 * 4 + 8);
+      fx[i] = v4i{(int)lo[0], (int)lo[1], (int)hi[0], (int)hi[1]};
+    }
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fw[j], fx[i], acc[i][j], 0, 0, 0);
+  }
+  const LinRowMap rm{((long)n * a.OH + oh0) * SI_OW};
+  halo_epi_i8<FM, 4>(a, ep, acc, wave * SI_OW, 0, lane, rm);
+}
+
 int g_conv_halo = -1;
 
 template <int W, int RB, int NIMG, int KT, int WPX>
@@ -560,6 +733,40 @@ int bigdl_conv_halo_i8_applies(const ConvArgs* a, const I8Epi* ep) {
   const int ok = bigdl_conv_halo_applies(&b);
   g_conv_halo = keep;
   return ok;
+}
+
+// The int8 stem over the width im2col (see stem_i8_kernel): 7 row taps (r - 3) x 1, 32-byte rows, stride (2, 1),
+// 112 output columns, 64 channels, no residual. BIGDL_STEM_I8=0 turns it off.
+static int g_stem_i8 = -1;
+void bigdl_set_stem_i8(int v) { g_stem_i8 = v; }
+
+int bigdl_stem_i8_applies(const ConvArgs* a, const I8Epi* ep) {
+  if (g_stem_i8 < 0) {
+    const char* e = getenv("BIGDL_STEM_I8");
+    g_stem_i8 = e ? atoi(e) : 1;
+  }
+  if (!g_stem_i8 || ep->add8 != nullptr || a->Cs != 32 || a->ntaps != 7 || a->mul_h != 2 || a->mul_w != 1 ||
+      a->Ws != SI_OW || a->OW != SI_OW || a->OH % SI_RB || a->Hs != 2 * a->OH || a->Ncol != 64 || a->ldw != 224 ||
+      a->Kdim != 224 || !a->ident_out || a->ldo % 4 || a->ldo < 64)
+    return 0;
+  for (int t = 0; t < 7; ++t)
+    if (a->tap_h[t] != t - 3 || a->tap_w[t] != 0 || a->tap_k[t] != t) return 0;
+  if ((size_t)a->Hs * SI_ROW >= (1ull << 31)) return 0;
+  return 1;
+}
+
+int bigdl_stem_i8(const ConvArgs* a, const I8Epi* ep, hipStream_t st) {
+  stem_i8_kernel<<<dim3(a->Nb * (a->OH / SI_RB)), dim3(256), 0, st>>>(*a, *ep);
+  return 0;
+}
+
+// The stem from the fp32 image (stem_i8f_kernel): `a` carries the width-im2col geometry (what bigdl_stem_i8_applies
+// checks, Hs = image rows), img the [N][C][Hs][224] fp32 image, inv the quantizer's 1 / scale. -1: not applicable.
+int bigdl_stem_i8_f32(const ConvArgs* a, const I8Epi* ep, const float* img, int C, int W, float inv, hipStream_t st) {
+  if (!bigdl_stem_i8_applies(a, ep) || W != SF_W || C < 1 || C > 3 || a->src != nullptr) return -1;
+  if ((size_t)a->Nb * C * a->Hs * SF_SEG >= (1ull << 31)) return -1;
+  stem_i8f_kernel<<<dim3(a->Nb * (a->OH / SI_RB)), dim3(256), 0, st>>>(*a, *ep, img, C, inv);
+  return 0;
 }
 
 int bigdl_conv_halo_i8(const ConvArgs* a, const I8Epi* ep, hipStream_t st) {

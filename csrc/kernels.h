@@ -156,6 +156,10 @@ void bigdl_cast_bf16_f32(const uint16_t* x, float* y, long n, hipStream_t st);
 // pooling (NHWC bf16)
 void bigdl_maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* idx, int N, int H, int W, int C, int OH,
                        int OW, int kh, int kw, int sh, int sw, int ph, int pw, hipStream_t st);
+int bigdl_stem_i8_applies(const ConvArgs* a, const I8Epi* ep);
+void bigdl_set_stem_i8(int v);
+int bigdl_stem_i8_f32(const ConvArgs* a, const I8Epi* ep, const float* img, int C, int W, float inv, hipStream_t st);
+int bigdl_stem_i8(const ConvArgs* a, const I8Epi* ep, hipStream_t st);
 void bigdl_split_reduce_f32(const float* ws, float* dw, long n, int splits, hipStream_t st);
 int bigdl_maxpool_bwd_bnred_applies(int N, int H, int W, int C, int OH, int OW, int kh, int kw, int sh, int sw, int ph,
                                     int pw);

@@ -1351,7 +1351,9 @@ int bigdl_conv_i8(const ConvArgs* a, const float* xscale, float xs_const, const 
   const bool fk = a->Cs % QBK == 0;
   const bool g3fk = a->Cs % 64 == 0;
   const long p8_tiles = (long)((a->M + 255) / 256) * ((a->Ncol + 255) / 256);
-  if (bigdl_conv_halo_i8_applies(a, &ep) && bigdl_conv_halo_i8(a, &ep, st) == 0) {
+  if (bigdl_stem_i8_applies(a, &ep) && bigdl_stem_i8(a, &ep, st) == 0) {
+    // the 7x7/2 image stem over its width im2col: staged-row kernel (conv_halo.hip stem_i8_kernel)
+  } else if (bigdl_conv_halo_i8_applies(a, &ep) && bigdl_conv_halo_i8(a, &ep, st) == 0) {
     // 3x3 / stride-1 / pad-1: the halo-tile kernel on the i8 matrix cores (conv_halo.hip)
   } else if (i8_s1_applies(*a, ep)) {
     launch_i8_s1(*a, ep, st);

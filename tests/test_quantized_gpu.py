@@ -300,3 +300,79 @@ def test_conv_i8_halo_exact(case):
     exp = (ref + bias.double()).clamp(0, 127).to(torch.int8)
     assert torch.equal(outs[1], exp)
     assert torch.equal(outs[1], outs[0])
+
+
+@pytest.mark.parametrize("N,H,relu,mode", [(2, 224, True, "i8"), (1, 224, False, "f32"), (3, 224, True, "bf16")])
+def test_stem_i8_kernel_exact(N, H, relu, mode):
+    """int8 7x7/2 image stem over the width im2col (staged-row kernel, conv_halo.hip stem_i8_kernel): fp32 output equal
+    to the exact integer convolution of the quantized image (+ bias, unit scales), and int8 / bf16 outputs equal to the
+    generic int8 implicit GEMM's (BIGDL_STEM_I8 off)."""
+    from bigdl_amd.ops.conv import _fwd_taps
+
+    C_ = native.get()
+    g = torch.Generator().manual_seed(11)
+    K, W, OW, OH = 64, 224, 112, H // 2
+    x = torch.randint(-40, 41, (N, 3, H, W), generator=g).float()          # integers: quantization at scale 1 is exact
+    w = torch.randint(-6, 7, (K, 3, 7, 7), generator=g, dtype=torch.int8)
+    q = torch.empty((N, H, OW, 32), dtype=torch.int8, device="cuda")
+    C_.quantize_wim2col_f32(x.cuda(), q, OW, 7, 2, 3, 1.0)
+    # weight bytes [k][r * 32 + e * 4 + c] (c < 3, e < 7), the im2col's byte order
+    wp = torch.zeros(K, 7, 8, 4, dtype=torch.int8)
+    wp[:, :, :7, :3] = w.permute(0, 2, 3, 1)
+    wp = wp.reshape(K, 224).contiguous()
+    bias = torch.randint(-50, 51, (K,), generator=g).float()
+    geo = [N, H, OW, 32, OH, OW, 2, 1, 224, K, K, OH, OW, 1, 1, 0, 0]
+    dt = {"i8": torch.int8, "f32": torch.float32, "bf16": torch.bfloat16}[mode]
+    outs = {}
+    for on in (1, 0):
+        C_.set_stem_i8(on)
+        try:
+            out = torch.zeros(N * OH * OW, K, dtype=dt, device="cuda")
+            C_.conv_i8(q, wp.cuda(), out, bias.cuda(), None, torch.ones(K, device="cuda"), geo,
+                       _fwd_taps(7, 1, 3, 0, 1, 1), relu, 1.0, 1.0 if mode == "i8" else 0.0, None, 0.0)
+            torch.cuda.synchronize()
+            outs[on] = out.cpu()
+        finally:
+            C_.set_stem_i8(1)
+    # the same from the fp32 image: the kernel quantizes its operands itself (stem_i8f_kernel)
+    out = torch.zeros(N * OH * OW, K, dtype=dt, device="cuda")
+    assert C_.conv_i8_stem_f32(x.cuda(), wp.cuda(), out, bias.cuda(), torch.ones(K, device="cuda"), geo,
+                               _fwd_taps(7, 1, 3, 0, 1, 1), relu, 1.0, 1.0 if mode == "i8" else 0.0)
+    torch.cuda.synchronize()
+    outs["f"] = out.cpu()
+    ref = F.conv2d(x.double(), w.double(), None, 2, 3).permute(0, 2, 3, 1).reshape(-1, K) + bias.double()
+    if relu:
+        ref = ref.clamp_min(0)
+    if mode == "f32":
+        assert torch.equal(outs[1].double(), ref)
+    if mode == "i8":
+        assert torch.equal(outs[1], ref.clamp(-127, 127).round().to(torch.int8))
+    assert torch.equal(outs[1], outs[0])
+    assert torch.equal(outs["f"], outs[1])
+
+
+def test_stem_i8_f32_quantizes_like_the_im2col_pass():
+    """Non-integer image values at a non-unit scale: the stem that quantizes its own operands gives the same int8
+    output as quantize_wim2col_f32 followed by the im2col stem (the same rint(x / scale) per element)."""
+    from bigdl_amd.ops.conv import _fwd_taps
+
+    C_ = native.get()
+    g = torch.Generator().manual_seed(5)
+    N, H, K, OW = 2, 224, 64, 112
+    x = torch.randn(N, 3, H, 224, generator=g) * 2.0
+    scale = float(x.abs().max()) / 127.0
+    w = torch.randint(-20, 21, (K, 224), generator=g, dtype=torch.int8)
+    w.view(K, 7, 8, 4)[:, :, 7, :] = 0
+    w.view(K, 7, 8, 4)[:, :, :, 3] = 0
+    ws = torch.rand(K, generator=g) * 0.01 + 0.001
+    bias = torch.randn(K, generator=g)
+    geo = [N, H, OW, 32, OH := H // 2, OW, 2, 1, 224, K, K, OH, OW, 1, 1, 0, 0]
+    taps = _fwd_taps(7, 1, 3, 0, 1, 1)
+    q = torch.empty((N, H, OW, 32), dtype=torch.int8, device="cuda")
+    C_.quantize_wim2col_f32(x.cuda(), q, OW, 7, 2, 3, scale)
+    a = torch.zeros(N * OH * OW, K, dtype=torch.int8, device="cuda")
+    C_.conv_i8(q, w.cuda(), a, bias.cuda(), None, ws.cuda(), geo, taps, True, scale, 0.05, None, 0.0)
+    b = torch.zeros_like(a)
+    assert C_.conv_i8_stem_f32(x.cuda(), w.cuda(), b, bias.cuda(), ws.cuda(), geo, taps, True, scale, 0.05)
+    torch.cuda.synchronize()
+    assert torch.equal(a.cpu(), b.cpu())
