@@ -44,10 +44,10 @@ def test_conv_i8_requantized_output_into_slice():
 
 @pytest.mark.parametrize("avg,k,s,p,count_pad", [(False, 3, 2, 0, False), (False, 3, 1, 1, False),
                                                 (True, 3, 1, 1, True), (True, 3, 1, 1, False), (True, 8, 8, 0, True)])
-def test_pool_i8_matches_reference(avg, k, s, p, count_pad):
+def test_pool_i8_matches_reference(avg, k, s, p, count_pad, shape=(2, 17, 17, 32)):
     from bigdl_amd.ops.conv import out_size
 
-    N, H, W, C = 2, 17, 17, 32
+    N, H, W, C = shape
     g = torch.Generator().manual_seed(4)
     x = torch.randint(-127, 128, (N, H, W, C), generator=g, dtype=torch.int8)
     OH, OW = out_size(H, k, s, p), out_size(W, k, s, p)
@@ -60,6 +60,13 @@ def test_pool_i8_matches_reference(avg, k, s, p, count_pad):
         ref = F.max_pool2d(xf, k, s, p)
     ref = ref.permute(0, 2, 3, 1)
     assert (y.cpu().double() - ref).abs().max() <= 1
+
+
+@pytest.mark.parametrize("avg,count_pad,shape", [(True, True, (1, 35, 35, 48)), (True, False, (2, 8, 9, 16)),
+                                                  (False, False, (1, 35, 35, 48)), (True, True, (3, 5, 3, 16))])
+def test_pool3s1_i8_runs(avg, count_pad, shape):
+    """3x3 / stride-1 int8 pooling on the run-of-8 kernel (Inception pool branches): partial runs, widths below 8."""
+    test_pool_i8_matches_reference(avg, 3, 1, 1, count_pad, shape)
 
 
 def test_quantize_nchw_input():
