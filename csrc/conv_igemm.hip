@@ -2291,6 +2291,17 @@ __global__ __launch_bounds__(256, 2) void conv_nt_s1_kernel(ConvArgs a) {
   v2f p1[4], p2[4];
 #pragma unroll
   for (int e = 0; e < 4; ++e) p1[e] = p2[e] = v2f{0.f, 0.f};
+  // EXT operands through buffer resources: an absent operand gets a 0-byte resource (its loads return zeros), so the
+  // loads carry no branches — branch joins around loads made the compiler drain vmcnt before the stores (328
+  // branches, 36 vmcnt(0) in the 64-channel EXT kernel); tail rows store through an out-of-range offset
+  const size_t ob = EXT ? ((size_t)(a.M - 1) * a.ldo + a.Ncol) * 2 : 0;
+  const __amdgpu_buffer_rsrc_t r_add = rsrc_of(a.addend, (EXT && a.addend) ? ob : 0);
+  const __amdgpu_buffer_rsrc_t r_azm = rsrc_of(a.addzm, (EXT && a.addzm) ? ob / 16 : 0);
+  const __amdgpu_buffer_rsrc_t r_bx = rsrc_of(a.bnx, bnw ? ob : 0);
+  const __amdgpu_buffer_rsrc_t r_bzm = rsrc_of(a.bnzm, (bnw && a.bnzm) ? ob / 16 : 0);
+  const __amdgpu_buffer_rsrc_t r_out = rsrc_of(a.out, ob);
+  const int zmode = !bnw ? 0 : a.bnzm ? 1 : a.bnaff ? 3 : 0;     // a bf16 z mask is not taken (s1_applies)
+  const bool azm = a.addzm != nullptr;
 
   auto load = [&](v8s (&af)[MI][KF], int t) {
     const int p0 = t * BM + pg * BMW;
@@ -2305,18 +2316,18 @@ __global__ __launch_bounds__(256, 2) void conv_nt_s1_kernel(ConvArgs a) {
 
   auto compute_store = [&](v8s (&af)[MI][KF], int t) {
     const int p0 = t * BM + pg * BMW;
-    v4u pad[EXT ? NR : 1], px[EXT ? NR : 1], pz[EXT ? NR : 1];
+    v4u pad[EXT ? NR : 1], px[EXT ? NR : 1];
+    unsigned pzb[EXT ? NR : 1];          // byte 0: addend mask, byte 1: consumer-BN sign mask
     if constexpr (EXT) {     // epilogue operands first: their latency overlaps the MFMAs and the LDS transpose
 #pragma unroll
       for (int rr = 0; rr < NR; ++rr) {
         const int m = min(p0 + rr * 8 + (lane >> 3), a.M - 1);
         const size_t off = (size_t)m * a.ldo + n;
-        pad[rr] = a.addend ? *reinterpret_cast<const v4u*>(a.addend + off) : v4u{0u, 0u, 0u, 0u};
-        if (a.addzm) pad[rr] &= mask8_to_and(a.addzm[off >> 3]);
-        px[rr] = bnw ? *reinterpret_cast<const v4u*>(a.bnx + off) : v4u{0u, 0u, 0u, 0u};
-        pz[rr] = (bnw && a.bnzm) ? mask8_to_bf(a.bnzm[off >> 3])
-                 : (bnw && a.bnz) ? *reinterpret_cast<const v4u*>(a.bnz + off)
-                                  : v4u{0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
+        const unsigned eb = (unsigned)(off * 2), zo = (unsigned)(off >> 3);
+        pad[rr] = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(r_add, eb, 0, 0));
+        px[rr] = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(r_bx, eb, 0, 0));
+        pzb[rr] = __builtin_amdgcn_raw_buffer_load_b8(r_azm, zo, 0, 0) |
+                  (__builtin_amdgcn_raw_buffer_load_b8(r_bzm, zo, 0, 0) << 8);
       }
     }
     v4f acc[MI][4];
@@ -2357,8 +2368,9 @@ __global__ __launch_bounds__(256, 2) void conv_nt_s1_kernel(ConvArgs a) {
         const v4f hi = *reinterpret_cast<const v4f*>(wl + (p * GPR + ((2 * q + 1) ^ (p & 15))) * 4);
         float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         if constexpr (EXT) {
+          const v4u pa = azm ? (pad[rr] & mask8_to_and(pzb[rr] & 0xffu)) : pad[rr];
 #pragma unroll
-          for (int e = 0; e < 4; ++e) { v[2 * e] += lo_bf(pad[rr][e]); v[2 * e + 1] += hi_bf(pad[rr][e]); }
+          for (int e = 0; e < 4; ++e) { v[2 * e] += lo_bf(pa[e]); v[2 * e + 1] += hi_bf(pa[e]); }
         }
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -2373,30 +2385,40 @@ __global__ __launch_bounds__(256, 2) void conv_nt_s1_kernel(ConvArgs a) {
           for (int e = 0; e < 4; ++e) o[e] = pack2bf(fmaxf(lo_bf(o[e]), 0.f), fmaxf(hi_bf(o[e]), 0.f));
         }
       }
-      if (m < a.M) {
+      if constexpr (EXT) {
+        // branch-free: masks as selects, tail rows contribute zero and store out of range
+        const float vm = m < a.M ? 1.f : 0.f;
+        if (a.stats) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const v2f y = v2f{lo_bf(o[e]), hi_bf(o[e])} * vm;
+            p1[e] += y;
+            p2[e] = __builtin_elementwise_fma(y, y, p2[e]);
+          }
+        } else {
+          const unsigned zb = pzb[rr] >> 8;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            v2f d = v2f{lo_bf(o[e]), hi_bf(o[e])} * vm;
+            const v2f x = {lo_bf(px[rr][e]), hi_bf(px[rr][e])};
+            bool k0 = true, k1 = true;
+            if (zmode == 1) { k0 = (zb >> (2 * e)) & 1u; k1 = (zb >> (2 * e + 1)) & 1u; }
+            else if (zmode == 3) { k0 = x[0] * bsc[2 * e] + bsh[2 * e] > 0.f; k1 = x[1] * bsc[2 * e + 1] + bsh[2 * e + 1] > 0.f; }
+            d[0] = k0 ? d[0] : 0.f;
+            d[1] = k1 ? d[1] : 0.f;
+            p1[e] += d;
+            p2[e] = __builtin_elementwise_fma(d, x - v2f{bmu[2 * e], bmu[2 * e + 1]}, p2[e]);
+          }
+        }
+        const unsigned so = m < a.M ? (unsigned)(((size_t)m * a.ldo + n) * 2) : EOOB;
+        __builtin_amdgcn_raw_buffer_store_b128(o, r_out, so, 0, 0);
+      } else if (m < a.M) {
         if (a.stats) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const v2f y = {lo_bf(o[e]), hi_bf(o[e])};
             p1[e] += y;
             p2[e] = __builtin_elementwise_fma(y, y, p2[e]);
-          }
-        } else if constexpr (EXT) {
-          if (bnw) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              v2f d = {lo_bf(o[e]), hi_bf(o[e])};
-              const v2f x = {lo_bf(px[rr][e]), hi_bf(px[rr][e])};
-              if (a.bnz || a.bnzm) {
-                if (!(lo_bf(pz[rr][e]) > 0.f)) d[0] = 0.f;
-                if (!(hi_bf(pz[rr][e]) > 0.f)) d[1] = 0.f;
-              } else if (a.bnaff) {
-                if (!(x[0] * bsc[2 * e] + bsh[2 * e] > 0.f)) d[0] = 0.f;
-                if (!(x[1] * bsc[2 * e + 1] + bsh[2 * e + 1] > 0.f)) d[1] = 0.f;
-              }
-              p1[e] += d;
-              p2[e] = __builtin_elementwise_fma(d, x - v2f{bmu[2 * e], bmu[2 * e + 1]}, p2[e]);
-            }
           }
         }
         *reinterpret_cast<v4u*>(a.out + (size_t)m * a.ldo + n) = o;
@@ -2732,6 +2754,10 @@ static bool s1_applies(const ConvArgs* a) {
   if (!g_conv_s1 || a->out32 || !a->ident_out || a->ntaps != 1 || a->tap_h[0] || a->tap_w[0] || a->tap_k[0]) return false;
   if (a->mul_h != 1 || a->mul_w != 1 || a->Hs != a->OH || a->Ws != a->OW) return false;
   if ((a->Kdim != 64 && a->Kdim != 128) || a->Cs != a->Kdim || (a->Ncol % 64) || (a->ldo % 8) || (a->ldw % 8)) return false;
+  // the epilogue operands go through 32-bit buffer offsets (bytes of an [M][ldo] bf16 tensor, below the OOB offset)
+  if (((size_t)(a->M - 1) * a->ldo + a->Ncol) * 2 >= 0x7ff00000u) return false;
+  // the consumer-BN ReLU mask as a bf16 z tensor (BIGDL_BN_ZMASK=0) is left to the tile kernels
+  if (a->bnred && !a->stats && a->bnz && !a->bnzm) return false;
   auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
   return al(a->src) && al(a->wt) && al(a->out) && al(a->addend) && al(a->bnx) && al(a->bnz);
 }
