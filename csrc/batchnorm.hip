@@ -41,6 +41,9 @@ __global__ __launch_bounds__(256) void chan_reduce_kernel(const bf16_t* __restri
 #pragma unroll
     for (int e = 0; e < 8; ++e) { a1[e] = 0.f; a2[e] = 0.f; mu[e] = 0.f; sc[e] = 0.f; sh[e] = 0.f; }
     const bool xmask = MODE == 1 && z == nullptr && zm == nullptr && aff != nullptr;
+    const __amdgpu_buffer_rsrc_t rzm = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t*>(zm), (short)0, zm ? (int)min((long)P * C / 8, 0x7fffffffl) : 0, 0x00020000);
+    const bf16_t* zp = (z && !zm) ? z : x;
     if (MODE == 1 && rsub < rpi) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) mu[e] = mean[g * 8 + e];
@@ -55,17 +58,24 @@ __global__ __launch_bounds__(256) void chan_reduce_kernel(const bf16_t* __restri
       // latency-bound at ~2.5 TB/s). Rows past the block end re-read row rbeg and contribute zero.
       for (long r0 = rbeg + rsub; r0 < rend; r0 += (long)U * rpi) {
         v4u vx[U], vd[U], vz[U];
+        unsigned zb[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           const long r = r0 + (long)u * rpi;
           const size_t off = (size_t)(r < rend ? r : rbeg) * C + g * 8;
           vx[u] = *reinterpret_cast<const v4u*>(x + off);
           if (MODE == 1) {
+            // unconditional loads (no branch, no phi): a load under `if (zm)` / `if (z)` made the compiler wait
+            // for it at the join (vmcnt(0) per row), serialising the U rows. Absent masks read x (a cache hit)
+            // or a 0-byte buffer resource, and are ignored below.
             vd[u] = *reinterpret_cast<const v4u*>(dz + off);
-            if (zm) vz[u] = mask8_to_bf(zm[off >> 3]);
-            else if (z) vz[u] = *reinterpret_cast<const v4u*>(z + off);
+            zb[u] = __builtin_amdgcn_raw_buffer_load_b8(rzm, (unsigned)(off >> 3), 0, 0);
+            vz[u] = *reinterpret_cast<const v4u*>(zp + off);
           }
         }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          if (MODE == 1 && zm) vz[u] = mask8_to_bf(zb[u]);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           const bool ok = r0 + (long)u * rpi < rend;
@@ -273,6 +283,9 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16_t* __restr
                                                            const float* __restrict__ mean2, float* __restrict__ red2) {
   const int G = C >> 3;
   const bool xmask = z == nullptr && zm == nullptr && aff != nullptr;   // ReLU mask from x*scale + shift (see chan_reduce_kernel)
+  const __amdgpu_buffer_rsrc_t rzm = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint8_t*>(zm), (short)0, zm ? (int)min(P * C / 8, 0x7fffffffl) : 0, 0x00020000);
+  const bf16_t* zp = (z && !zm) ? z : x;
   const int gbase = blockIdx.y * 256;
   const int gcount = min(256, G - gbase);
   const int rpi = 256 / gcount;
@@ -295,17 +308,21 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16_t* __restr
   }
   for (long r0 = rbeg + rsub; r0 < rend; r0 += (long)U * rpi) {
     v4u vd[U], vz[U], vx[U], vx2[U];
+    unsigned zb[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const long r = r0 + (long)u * rpi;
       const long i = (r < rend ? r : rbeg) * G + g;
       vd[u] = reinterpret_cast<const v4u*>(dz)[i];
-      vz[u] = v4u{0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
-      if (zm) vz[u] = mask8_to_bf(zm[i]);
-      else if (z) vz[u] = reinterpret_cast<const v4u*>(z)[i];
+      // unconditional mask loads (see chan_reduce_kernel): absent masks read x (a cache hit) / a 0-byte resource
+      zb[u] = __builtin_amdgcn_raw_buffer_load_b8(rzm, (unsigned)i, 0, 0);
+      vz[u] = reinterpret_cast<const v4u*>(zp)[i];
       vx[u] = reinterpret_cast<const v4u*>(x)[i];
       if (R2) vx2[u] = reinterpret_cast<const v4u*>(x2)[i];
     }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      vz[u] = zm ? mask8_to_bf(zb[u]) : z ? vz[u] : v4u{0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const long r = r0 + (long)u * rpi;
