@@ -333,13 +333,25 @@ __global__ __launch_bounds__(256) void maxpool_bwd_k3s2_kernel(const bf16_t* __r
   const long total = (long)N * OH * OW * G;
   const int W = 2 * OW;
   float s1[8], s2[8], mu[8], sc[8], sf[8];
+  const __amdgpu_buffer_rsrc_t rzm = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint8_t*>(br.zm), (short)0, br.zm ? (int)min(total * 4, 0x7fffffffl) : 0, 0x00020000);
   if (BNR) {
     const int g0 = threadIdx.x % G;
+    // scale / shift through a buffer resource (0 bytes without aff): a load under `if (aff)` was waited for at the
+    // join, one round trip per element before the first row
+    const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(br.aff), (short)0,
+                                                                        br.aff ? 8 * C : 0, 0x00020000);
+    const v4f m0 = *reinterpret_cast<const v4f*>(br.mean + g0 * 8), m1 = *reinterpret_cast<const v4f*>(br.mean + g0 * 8 + 4);
+    const v4f a0 = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(ra, (unsigned)(g0 * 32), 0, 0));
+    const v4f a1 = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(ra, (unsigned)(g0 * 32 + 16), 0, 0));
+    const v4f b0 = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(ra, (unsigned)((C + g0 * 8) * 4), 0, 0));
+    const v4f b1 = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(ra, (unsigned)((C + g0 * 8) * 4 + 16), 0, 0));
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      s1[e] = 0.f; s2[e] = 0.f; mu[e] = br.mean[g0 * 8 + e];
-      sc[e] = br.aff ? br.aff[g0 * 8 + e] : 0.f;
-      sf[e] = br.aff ? br.aff[C + g0 * 8 + e] : 0.f;
+    for (int e = 0; e < 4; ++e) {
+      s1[e] = s2[e] = s1[e + 4] = s2[e + 4] = 0.f;
+      mu[e] = m0[e]; mu[e + 4] = m1[e];
+      sc[e] = a0[e]; sc[e + 4] = a1[e];
+      sf[e] = b0[e]; sf[e + 4] = b1[e];
     }
   }
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
@@ -389,11 +401,11 @@ __global__ __launch_bounds__(256) void maxpool_bwd_k3s2_kernel(const bf16_t* __r
     const long pix[4] = {row0, row0 + 1, row0 + W, row0 + W + 1};
     if (BNR) {
       v4u bx[4];
-      unsigned zb[4] = {0xffu, 0xffu, 0xffu, 0xffu};
+      unsigned zb[4];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
+      for (int k = 0; k < 4; ++k) {      // unconditional mask byte (0-byte resource when absent): no wait at a join
         bx[k] = reinterpret_cast<const v4u*>(br.x)[pix[k] * G + g];
-        if (br.zm) zb[k] = br.zm[pix[k] * G + g];
+        zb[k] = __builtin_amdgcn_raw_buffer_load_b8(rzm, (unsigned)(pix[k] * G + g), 0, 0);
       }
 #pragma unroll
       for (int k = 0; k < 4; ++k)
