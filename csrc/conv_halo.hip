@@ -214,20 +214,38 @@ __device__ __forceinline__ void halo_epi_i8(const ConvArgs& a, const I8Epi& ep, 
   const int nl = 4 * (lane >> 4), ml = lane & 15;
   const bool q8 = ep.out_mode == 2;
   const float oi = q8 ? ep.out_inv : 1.f;
+  // per-channel scales / bias as 16-byte loads, the bias through a buffer resource (0 bytes without one): the
+  // per-element `a.bias ? a.bias[n] : 0` loads were waited for one by one at the branch joins
   float ws[FN][4], bs[FN][4];
+  {
+    const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.bias), (short)0,
+                                                                        a.bias ? a.Ncol * 4 : 0, 0x00020000);
 #pragma unroll
-  for (int j = 0; j < FN; ++j)
+    for (int j = 0; j < FN; ++j) {
+      const int n = nbase + j * 16 + nl;
+      const v4f w = *reinterpret_cast<const v4f*>(ep.wscale + n);
+      const v4f b = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(rb, (unsigned)(n * 4), 0, 0));
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int n = nbase + j * 16 + nl + e;
-      ws[j][e] = ep.wscale[n] * oi;
-      bs[j][e] = a.bias ? a.bias[n] * oi : 0.f;
+      for (int e = 0; e < 4; ++e) {
+        ws[j][e] = w[e] * oi;
+        bs[j][e] = b[e] * oi;
+      }
     }
+  }
+  // branch-free rows: the per-sample scale through a buffer resource (0 bytes without one), rows without an output
+  // stored at an out-of-range offset (a skipped row / `xscale ? xscale[..] : c` was a wait at each join)
+  const int esz = q8 ? 1 : ep.out_mode == 1 ? 4 : 2;
+  const size_t orows_n = a.ident_out ? (size_t)a.M : (size_t)a.Nb * a.OHo * a.OWo;
+  const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
+      a.out, (short)0, (int)min(((orows_n - 1) * a.ldo + a.Ncol) * esz, (size_t)0x7fffffff), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rxs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(ep.xscale), (short)0,
+                                                                       ep.xscale ? a.Nb * 4 : 0, 0x00020000);
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
     const long orow = rm(a, vbase + i * 16 + ml);
-    if (orow < 0) continue;
-    const float xs = ep.xscale ? ep.xscale[orow / ohw] : ep.xs_const;
+    const float xl = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                   rxs, orow >= 0 ? (unsigned)(orow / ohw * 4) : EOOB, 0, 0));
+    const float xs = ep.xscale ? xl : ep.xs_const;
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
       const int n = nbase + j * 16 + nl;
@@ -237,16 +255,16 @@ __device__ __forceinline__ void halo_epi_i8(const ConvArgs& a, const I8Epi& ep, 
         v[e] = (float)acc[i][j][e] * (xs * ws[j][e]) + bs[j][e];
         if (a.relu) v[e] = fmaxf(v[e], 0.f);
       }
-      const size_t off = (size_t)orow * a.ldo + n;
+      const unsigned off = orow >= 0 ? (unsigned)(((size_t)orow * a.ldo + n) * esz) : EOOB;
       if (q8) {
         unsigned pk = 0u;
 #pragma unroll
         for (int e = 0; e < 4; ++e) pk |= (unsigned)(max(-127, min(127, __float2int_rn(v[e]))) & 0xff) << (8 * e);
-        *reinterpret_cast<unsigned*>(reinterpret_cast<int8_t*>(a.out) + off) = pk;
+        __builtin_amdgcn_raw_buffer_store_b32(pk, ro, off, 0, 0);
       } else if (ep.out_mode == 1) {
-        *reinterpret_cast<v4f*>(reinterpret_cast<float*>(a.out) + off) = v4f{v[0], v[1], v[2], v[3]};
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v4f{v[0], v[1], v[2], v[3]}), ro, off, 0, 0);
       } else {
-        *reinterpret_cast<v2u*>(a.out + off) = v2u{pack2bf(v[0], v[1]), pack2bf(v[2], v[3])};
+        __builtin_amdgcn_raw_buffer_store_b64(v2u{pack2bf(v[0], v[1]), pack2bf(v[2], v[3])}, ro, off, 0, 0);
       }
     }
   }
