@@ -240,12 +240,13 @@ __device__ __forceinline__ void halo_epi_i8(const ConvArgs& a, const I8Epi& ep, 
       a.out, (short)0, (int)min(((orows_n - 1) * a.ldo + a.Ncol) * esz, (size_t)0x7fffffff), 0x00020000);
   const __amdgpu_buffer_rsrc_t rxs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(ep.xscale), (short)0,
                                                                        ep.xscale ? a.Nb * 4 : 0, 0x00020000);
+  const float xs0 = ep.xscale ? 0.f : ep.xs_const;
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
     const long orow = rm(a, vbase + i * 16 + ml);
     const float xl = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
                                                    rxs, orow >= 0 ? (unsigned)(orow / ohw * 4) : EOOB, 0, 0));
-    const float xs = ep.xscale ? xl : ep.xs_const;
+    const float xs = xl + xs0;         // xl reads 0 without per-sample scales
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
       const int n = nbase + j * 16 + nl;

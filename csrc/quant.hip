@@ -1101,13 +1101,29 @@ __global__ __launch_bounds__(256, 2) void conv_i8_s1_kernel(ConvArgs a, I8Epi ep
       wf[j][kk] = *reinterpret_cast<const v4i*>(W8 + (size_t)(c0 + 16 * j + (lane & 15)) * a.ldw + 64 * kk +
                                                 16 * (lane >> 4));
   const float oi = OUT == 2 ? ep.out_inv : 1.f;
+  // 16-byte loads, the bias through a buffer resource (0 bytes without one): per-element `a.bias ? a.bias[..] : 0`
+  // was 16 waited round trips at the start of every workgroup
   float wsc[16], bs[16];
+  {
+    const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.bias), (short)0,
+                                                                        a.bias ? a.Ncol * 4 : 0, 0x00020000);
 #pragma unroll
-  for (int e = 0; e < 16; ++e) {
-    wsc[e] = ep.wscale[n + e] * oi;
-    bs[e] = a.bias ? a.bias[n + e] * oi : 0.f;
+    for (int g = 0; g < 4; ++g) {
+      const v4f w = *reinterpret_cast<const v4f*>(ep.wscale + n + 4 * g);
+      const v4f b = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(rb, (unsigned)((n + 4 * g) * 4), 0, 0));
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        wsc[4 * g + e] = w[e] * oi;
+        bs[4 * g + e] = b[e] * oi;
+      }
+    }
   }
   const float as = ep.add_scale * oi;
+  const __amdgpu_buffer_rsrc_t rxs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(ep.xscale), (short)0,
+                                                                       ep.xscale ? a.Nb * 4 : 0, 0x00020000);
+  const float xs0 = ep.xscale ? 0.f : ep.xs_const;
+  const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
+      a.out, (short)0, (int)(((size_t)(a.M - 1) * a.ldo + a.Ncol) * (OUT == 2 ? 1 : OUT == 1 ? 4 : 2)), 0x00020000);
 
   auto load = [&](v4i (&af)[MI][KF], int t) {
     const int p0 = t * BM + pg * BMW;
@@ -1163,8 +1179,12 @@ __global__ __launch_bounds__(256, 2) void conv_i8_s1_kernel(ConvArgs a, I8Epi ep
         const v4f t4 = *reinterpret_cast<const v4f*>(wl + (p * 16 + ((4 * q + g) ^ (p & 15))) * 4);
         v[4 * g] = t4[0]; v[4 * g + 1] = t4[1]; v[4 * g + 2] = t4[2]; v[4 * g + 3] = t4[3];
       }
-      if (m >= a.M) continue;
-      const float xs = ep.xscale ? ep.xscale[m / ohw] : ep.xs_const;
+      // branch-free row: per-sample scale through a buffer resource, tail rows stored out of range (a skipped row
+      // or `xscale ? xscale[..] : c` was a wait at each join)
+      const bool ok = m < a.M;
+      const float xl = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                     rxs, ok ? (unsigned)(m / ohw * 4) : 0x7ffffff0u, 0, 0));
+      const float xs = xl + xs0;         // xl reads 0 without per-sample scales: no select for the load to sink into
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
         float y = v[e] * (xs * wsc[e]) + bs[e];
@@ -1172,22 +1192,24 @@ __global__ __launch_bounds__(256, 2) void conv_i8_s1_kernel(ConvArgs a, I8Epi ep
         if (a.relu) y = fmaxf(y, 0.f);
         v[e] = y;
       }
-      const size_t off = (size_t)m * a.ldo + n;
+      constexpr int ESZ = OUT == 2 ? 1 : OUT == 1 ? 4 : 2;
+      const unsigned off = ok ? (unsigned)(((size_t)m * a.ldo + n) * ESZ) : 0x7ffffff0u;
       if constexpr (OUT == 2) {
         unsigned pk[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
         for (int e = 0; e < 16; ++e) pk[e >> 2] |= (unsigned)(max(-127, min(127, __float2int_rn(v[e]))) & 0xff) << (8 * (e & 3));
-        *reinterpret_cast<v4u*>(reinterpret_cast<int8_t*>(a.out) + off) = v4u{pk[0], pk[1], pk[2], pk[3]};
+        __builtin_amdgcn_raw_buffer_store_b128(v4u{pk[0], pk[1], pk[2], pk[3]}, ro, off, 0, 0);
       } else if constexpr (OUT == 1) {
-        float* o = reinterpret_cast<float*>(a.out) + off;
 #pragma unroll
-        for (int g = 0; g < 4; ++g) *reinterpret_cast<v4f*>(o + 4 * g) = v4f{v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]};
+        for (int g = 0; g < 4; ++g)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v4f{v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]}),
+                                                 ro, off, 16 * g, 0);
       } else {
-        bf16_t* o = a.out + off;
 #pragma unroll
         for (int g = 0; g < 2; ++g)
-          *reinterpret_cast<v4u*>(o + 8 * g) = v4u{pack2bf(v[8 * g], v[8 * g + 1]), pack2bf(v[8 * g + 2], v[8 * g + 3]),
-                                                   pack2bf(v[8 * g + 4], v[8 * g + 5]), pack2bf(v[8 * g + 6], v[8 * g + 7])};
+          __builtin_amdgcn_raw_buffer_store_b128(v4u{pack2bf(v[8 * g], v[8 * g + 1]), pack2bf(v[8 * g + 2], v[8 * g + 3]),
+                                                     pack2bf(v[8 * g + 4], v[8 * g + 5]), pack2bf(v[8 * g + 6], v[8 * g + 7])},
+                                                 ro, off, 16 * g, 0);
       }
     }
     __builtin_amdgcn_s_waitcnt(0xc07f);   // the slice is rewritten by the next tile
@@ -1220,6 +1242,8 @@ bool i8_s1_applies(const ConvArgs& a, const I8Epi& ep) {
   if ((a.Kdim != 64 && a.Kdim != 128 && a.Kdim != 256) || a.Cs != a.Kdim || (a.Ncol % 64) || (a.ldw % 16)) return false;
   const int osz = ep.out_mode == 2 ? 1 : ep.out_mode == 1 ? 4 : 2;
   if ((a.ldo * osz) % 16 || (ep.add8 && (ep.add_ld % 16))) return false;
+  // stores through a 32-bit buffer offset, below the out-of-range offset used for tail rows
+  if (((size_t)(a.M - 1) * a.ldo + a.Ncol) * osz >= 0x7ff00000u) return false;
   auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
   return al(a.src) && al(a.wt) && al(a.out) && al(ep.add8);
 }
