@@ -240,9 +240,10 @@ def residual_forward(seq, x):
     return out
 
 
-# measured neutral on ResNet-50 (bn_bwd_apply -0.4 ms, the residual dgrad epilogues +0.3 ms: byte mask loads),
-# so off by default (BIGDL_MASKED_ADDEND=1 enables it)
-MASKED_ADDEND = [os.environ.get("BIGDL_MASKED_ADDEND", "0") != "0"]
+# on by default since the streaming 1x1 kernel loads its mask bytes without a branch (ResNet-50 22.91 -> 22.76 ms,
+# profiles/r5_iteration_log.txt; before that the byte loads cost the epilogue what bn_bwd_apply saved);
+# BIGDL_MASKED_ADDEND=0 materialises the residual gradient instead
+MASKED_ADDEND = [os.environ.get("BIGDL_MASKED_ADDEND", "1") != "0"]
 
 
 # BIGDL_SHORTCUT_BN_RED=0: the projection shortcut BN's backward reduction runs as its own pass
