@@ -132,7 +132,20 @@ class SpatialConvolution(TensorModule):
         return y
 
     # ---------------------------------------------------------------- forward
+    def _pre_ok(self, x):
+        """A deferred BN + ReLU input (ops/bn.py deferred) goes to the GEMM as is (applied on load or materialised by
+        the binding) on the plain NCHW path: no SAME padding copy, no pair-view stem, no grouped / fused-graph output."""
+        if not (x.is_cuda and x.dim() == 4 and self.format == "NCHW" and self.nGroup == 1
+                and x.shape[1] == self.nInputPlane and x.shape[1] % 8 == 0 and x.dtype == BF16
+                and x.is_contiguous(memory_format=CL)):
+            return False
+        if self._same_extra(x.shape[2], x.shape[3]) != (0, 0) or self._pair_path(x):
+            return False
+        return getattr(self, "_fuse_out", None) is None and getattr(self, "_fuse_addend", None) is None
+
     def updateOutput(self, input):
+        if getattr(input, "_bn_pre", None) is not None and not self._pre_ok(input):
+            input = bnops.materialize(input)
         x = self._nchw(input)
         squeeze = x.dim() == 3
         if squeeze:
@@ -196,7 +209,9 @@ class SpatialConvolution(TensorModule):
 
     def _fwd_gpu(self, x, ph, pw):
         self._xpair = None
-        if self._pair_path(x) and self.nOutputPlane % 8 == 0:
+        self._x16_pre = None
+        pre = getattr(x, "_bn_pre", None)
+        if self._pair_path(x) and self.nOutputPlane % 8 == 0 and pre is None:
             return self._fwd_gpu_pairs(x, ph, pw)
         x16 = cv.to_nhwc_bf16(x)
         self._x16 = x16
@@ -210,7 +225,14 @@ class SpatialConvolution(TensorModule):
         self._fuse_out = self._fuse_addend = None
         y = cv.conv2d_fwd(x16, w16, self.bias, (self.strideH, self.strideW), (ph, pw),
                           (self.dilationH, self.dilationW), relu=self.fuse_relu, stats=stats, out=out,
-                          addend=addend)
+                          addend=addend, pre=pre)
+        if pre is not None:
+            # applied on load: the weight gradient re-applies it (on its own stream); else the binding materialised it
+            y, mat = y
+            if mat is None:
+                self._x16_pre = pre
+            else:
+                self._x16 = mat
         if stats is not None:
             y._bn_stats = stats
         self._geom = (x.shape, ph, pw)
@@ -388,7 +410,10 @@ class SpatialConvolution(TensorModule):
             return
         x16 = getattr(self, "_x16", None)
         if x16 is None or x16.shape[0] != x.shape[0] or x16.shape[2:] != x.shape[2:]:
-            x16 = cv.to_nhwc_bf16(x)
+            x16 = cv.to_nhwc_bf16(bnops.materialize(x))
+        elif getattr(self, "_x16_pre", None) is not None:
+            # the forward applied a deferred BN + ReLU on load: materialise it here, on the weight-gradient stream
+            x16 = bnops.materialize(bnops.deferred(x16, self._x16_pre))
         st, pd, dl = (self.strideH, self.strideW), (ph, pw), (self.dilationH, self.dilationW)
         if self.nGroup != 1 and self._direct_groups():
             xf = getattr(self, "_xf", None)
@@ -433,6 +458,7 @@ class SpatialConvolution(TensorModule):
     def clearState(self):
         super().clearState()
         self._x16 = None
+        self._x16_pre = None
         self._xpair = None
         return self
 

@@ -47,7 +47,7 @@ def _reset(m):
             x._graph_dres = False
     for x in m.flattened_layers():
         for attr, val in (("emit_stats", False), ("fuse_relu", False), ("passthrough", False),
-                          ("_dgrad_bn_ok", False)):
+                          ("_dgrad_bn_ok", False), ("_defer_ok", False)):
             if hasattr(x, attr):
                 setattr(x, attr, val)
         if isinstance(x, Sequential):
@@ -108,6 +108,12 @@ def _fuse_graph_training(g):
             m.fuse_relu = True
             c.passthrough = True
     _plan_fanout_folds(g, users)
+    for n in g.order:
+        m, u = n.element, only_user(n)
+        if isinstance(m, BatchNormalization) and u is not None and isinstance(u.element, ReLU):
+            v = only_user(u)
+            if v is not None:
+                _plan_deferred_bn(m, u.element, v.element)
     if not _dgrad_bn_enabled():
         return
     for n in g.order:
@@ -219,6 +225,27 @@ def _fuse_sequential(seq):
         elif isinstance(a, (SpatialConvolution, Linear)) and isinstance(b, ReLU):
             a.fuse_relu = True
             b.passthrough = True
+    for a, b, c in zip(mods[:-2], mods[1:-1], mods[2:]):
+        _plan_deferred_bn(a, b, c)
+
+
+def _defer_consumer(c):
+    """Modules that take a deferred BN + ReLU output (ops/bn.py deferred) and apply it on load or materialise it."""
+    from .pooling import SpatialMaxPooling
+
+    if isinstance(c, SpatialConvolution):        # (subclasses that keep the base forward / weight gradient)
+        return (c.nGroup == 1 and c.format == "NCHW" and type(c).updateOutput is SpatialConvolution.updateOutput
+                and type(c)._wgrad_gpu is SpatialConvolution._wgrad_gpu)
+    return type(c) is SpatialMaxPooling and c.format == "NCHW"
+
+
+def _plan_deferred_bn(a, b, c):
+    """BN(+ReLU fused) -> ReLU(pass-through) -> conv / max pool, where the consumer is the ReLU output's only reader:
+    the BN skips its apply pass and hands on a deferred output (csrc/kernels.h ConvArgs::pre). Reference analogue:
+    the MKL-DNN fused BN + ReLU feeding the next primitive's input (S/nn/mkldnn/Fusion.scala:60-217)."""
+    if (isinstance(a, BatchNormalization) and a.fuse_relu and not getattr(a, "_graph_dres", False)
+            and isinstance(b, ReLU) and b.passthrough and _defer_consumer(c)):
+        a._defer_ok = True
 
 
 def residual_forward(seq, x):

@@ -22,6 +22,9 @@ from .abstractnn import AutogradModule, TensorModule
 from .init_methods import Ones, RandomUniform, Zeros
 
 _ZMASK = os.environ.get("BIGDL_BN_ZMASK", "1") != "0"
+# BIGDL_BN_DEFER=0: always materialise a training BN + ReLU output, even where nn.fusion found a consumer that applies
+# it on load (ConvArgs::pre: streaming 1x1 / halo 3x3 forwards, the 3x3/2 max pool)
+_DEFER = [os.environ.get("BIGDL_BN_DEFER", "1") != "0"]
 CL = torch.channels_last
 BF16 = torch.bfloat16
 
@@ -117,6 +120,17 @@ class BatchNormalization(TensorModule):
             zm = None
             if self.train and self.fuse_relu and res is not None and x.shape[1] % 8 == 0 and _ZMASK:
                 zm = torch.empty(x.numel() // 8, dtype=torch.uint8, device=x.device)
+            if (self.train and self.fuse_relu and res is None and getattr(self, "_defer_ok", False) and _DEFER[0]
+                    and x.dim() == 4 and self.dataFormat == "NCHW"):
+                # the only consumer applies relu(x * scale + shift) on load: no apply pass, no output tensor
+                # (nn.fusion plans this for BN -> ReLU -> conv / max pool)
+                sm, si, aff = bnops.bn_prepare_gpu(x, self.weight, self.bias, self.runningMean, self.runningVar,
+                                                   self.eps, self.momentum, stats=stats, sync_fn=self.sync_fn)
+                self.saveMean, self.saveStd = sm, si
+                self._aff, self._zm, self._xin = aff, None, x
+                y = bnops.deferred(x, aff)
+                y._bn_bwd = (self, x, sm, aff, False)
+                return y
             y, sm, si, aff = bnops.bn_forward_gpu(x, self.weight, self.bias, self.runningMean, self.runningVar,
                                                    self.eps, self.momentum, self.train, stats=stats, res=res,
                                                    relu=self.fuse_relu, sync_fn=self.sync_fn if self.train else None,

@@ -7,6 +7,7 @@ import os
 import torch
 import torch.nn.functional as F
 
+from ..ops import bn as bnops
 from ..ops import pool as P
 from ..ops import pool_nd as PN
 from .abstractnn import AutogradModule, TensorModule
@@ -57,13 +58,19 @@ class SpatialMaxPooling(TensorModule):
         return self.padH, self.padW
 
     def updateOutput(self, input):
+        pre = getattr(input, "_bn_pre", None)
+        if pre is not None and not (self.format == "NCHW" and input.dim() == 4 and _gpu_ok(input)
+                                    and _prep(input) is input):
+            input, pre = bnops.materialize(input), None
         x = input.permute(0, 3, 1, 2) if self.format == "NHWC" else input
         sq = x.dim() == 3
         if sq:
             x = x.unsqueeze(0)
         ph, pw = self._pads(x.shape[2], x.shape[3])
         if _gpu_ok(x):
-            y, self._idx = P.maxpool_fwd_gpu(_prep(x), self.kH, self.kW, self.dH, self.dW, ph, pw, self.ceilMode)
+            # a deferred BN + ReLU input (nn.fusion: the ResNet stem) is applied inside the pooling kernel
+            y, self._idx = P.maxpool_fwd_gpu(_prep(x), self.kH, self.kW, self.dH, self.dW, ph, pw, self.ceilMode,
+                                             pre=pre)
         elif x.is_cuda:       # any channel count / dtype / layout: N-d window kernel over N*C planes
             geo, osh = PN.pool2d_geo(x.shape, self.kH, self.kW, self.dH, self.dW, ph, pw, self.ceilMode)
             y, self._idx = PN.pool_nd_fwd(x.contiguous(), osh, geo, True)

@@ -262,6 +262,23 @@ def _rnn_param_grads(dg16, h16, U, WT16):
     return _f32(dh0.view(B, H)), dU.view(G, H)
 
 
+# The whole-sequence backward may add dU straight into the recurrent Linear's gradWeight (no dU buffer, no extra
+# add). That is only the updateGradInput + accGradParameters pair that Recurrent.backward runs back to back: a bare
+# updateGradInput (input gradients only, or called twice) must leave gradWeight alone, so the sink is armed only
+# inside Recurrent.backward, and the buffer is looked up when the backward runs (not the one seen at forward time).
+_SINK_ARMED = [0]
+
+
+def _live_sink(m):
+    if m is None or not _SINK_ARMED[0]:
+        return None
+    g = getattr(m, "gradWeight", None)
+    if (m._frozen or getattr(m, "scaleW", 1.0) != 1.0 or g is None or not g.is_cuda or g.dtype != torch.float32
+            or not g.is_contiguous()):
+        return None
+    return g
+
+
 class _LSTMSeq(torch.autograd.Function):
     """Whole-sequence LSTM (gate order i, g, f, o) with the fused HIP cell kernels on the GPU engine."""
 
@@ -304,7 +321,7 @@ class _LSTMSeq(torch.autograd.Function):
         # gsink: the module's fp32 gradWeight buffer (Recurrent training, scale 1): the whole-sequence backward then
         # accumulates dU straight into it with the weight-gradient kernel (+=) and returns no U gradient — no zeroed
         # temporary and no separate add into gradWeight afterwards
-        ctx.gsink = gsink
+        ctx.gmod = gsink
         B, T, G = xg.shape
         H = G // 4
         if xg.dtype != torch.float32 and not _LSTMSeq._fused_gpu(xg, U):
@@ -374,7 +391,7 @@ class _LSTMSeq(torch.autograd.Function):
             C.lstm_seq_bwd(W16, dout, dhT.contiguous() if dhT is not None else None,
                            dcT.contiguous() if dcT is not None else None, acts, cs, c0.contiguous(), dg16, dxg, dc0,
                            dh0, sync)
-            sink = ctx.gsink
+            sink = _live_sink(ctx.gmod)
             if sink is not None:
                 dU = sink.view(4 * H, H, 1, 1)
             else:
@@ -393,8 +410,9 @@ class _LSTMSeq(torch.autograd.Function):
                             dout[:, t] if dout is not None else None, dhT if t == T - 1 else None, acts[t],
                             cs[t - 1] if t > 0 else c0, cs[t], dc, dxg[:, t], dg16[t])
         dh0, dU = _rnn_param_grads(dg16, h16, U, WT16)
-        if ctx.gsink is not None:
-            ctx.gsink.add_(dU)
+        sink = _live_sink(ctx.gmod)
+        if sink is not None:
+            sink.add_(dU)
             dU = None
         return dxg, dh0, dc, dU, None
 
@@ -417,8 +435,9 @@ class _LSTMSeq(torch.autograd.Function):
             dc_next, dc_prev = dc_prev, dc_next
         hprev = torch.cat([h0.unsqueeze(0), hs[:-1]], 0).reshape(T * B, H)
         dU = dgs.reshape(T * B, 4 * H).t() @ hprev
-        if ctx.gsink is not None:
-            ctx.gsink.add_(dU)
+        sink = _live_sink(ctx.gmod)
+        if sink is not None:
+            sink.add_(dU)
             dU = None
         return dgs.transpose(0, 1), dh_next, dc_next, dU, None
 
@@ -688,12 +707,8 @@ class LSTM(Cell):
                 and bool(ops.native.get().lstm_seq_supported(x2.shape[0], self.hiddenSize)))
 
     def _grad_sink(self, m):
-        """m.gradWeight when a fused backward may accumulate into it directly (see _LSTMSeq.forward)."""
-        g = getattr(m, "gradWeight", None)
-        if (not self.train or m._frozen or getattr(m, "scaleW", 1.0) != 1.0 or g is None or not g.is_cuda
-                or g.dtype != torch.float32 or not g.is_contiguous()):
-            return None
-        return g
+        """m when a fused backward may accumulate into m.gradWeight directly (see _LSTMSeq.forward and _live_sink)."""
+        return m if self.train else None
 
     def sequence(self, x2, hid, mask=None):
         if mask is None and self._fused_ok():
@@ -1027,7 +1042,11 @@ class Recurrent(Container):
             pre._apply_regularizers()
 
     def backward(self, input, gradOutput):
-        self.gradInput = self.updateGradInput(input, gradOutput)
+        _SINK_ARMED[0] += 0 if self._frozen else 1
+        try:
+            self.gradInput = self.updateGradInput(input, gradOutput)
+        finally:
+            _SINK_ARMED[0] -= 0 if self._frozen else 1
         if not self._frozen:
             self.accGradParameters(input, gradOutput)
         return self.gradInput

@@ -104,6 +104,48 @@ def bn_forward_gpu(x, gamma, beta, rmean, rvar, eps, momentum, training, stats=N
     return out, smean, sinv, aff
 
 
+def bn_prepare_gpu(x, gamma, beta, rmean, rvar, eps, momentum, stats=None, sync_fn=None):
+    """The statistics / finalize half of a training bn_forward_gpu without the apply pass: returns (save_mean,
+    save_invstd, aff). The BN + ReLU output relu(x * aff[:C] + aff[C:]) is then applied on load by its consumer
+    (ConvArgs::pre: the streaming 1x1 / halo 3x3 convolutions, the 3x3/2 max pool) or by ``materialize``."""
+    C = x.shape[1]
+    P = _P(x)
+    C_ = native.get()
+    dev = x.device
+    aff = torch.empty(2 * C, dtype=torch.float32, device=dev)
+    smean = torch.empty(C, dtype=torch.float32, device=dev)
+    sinv = torch.empty(C, dtype=torch.float32, device=dev)
+    nslots, Ptot = stat_slots(), P
+    if stats is None:
+        stats = new_stats(C, dev)
+        C_.bn_stats(x, stats, P, C)
+    if sync_fn is not None:
+        stats, nslots, Ptot = _reduce_slots_for_sync(stats, C, P, sync_fn)
+    C_.bn_finalize(stats, nslots, gamma, beta, rmean, rvar, smean, sinv, aff[:C], aff[C:], Ptot, C, float(eps),
+                   float(momentum), True)
+    return smean, sinv, aff
+
+
+def deferred(x, aff):
+    """A deferred BN + ReLU output: a new tensor object over x's storage tagged with ``_bn_pre`` = aff. Only a
+    consumer that applies it (or ``materialize``) may read it; nn.fusion hands it to such consumers only."""
+    y = x.detach()
+    y._bn_pre = aff
+    return y
+
+
+def materialize(t):
+    """The real values of a deferred BN + ReLU output (bn_apply into a new tensor on the current stream); any
+    other tensor is returned as is."""
+    aff = getattr(t, "_bn_pre", None)
+    if aff is None:
+        return t
+    C = t.shape[1]
+    y = torch.empty_like(t)
+    native.get().bn_apply(t, aff[:C], aff[C:], None, y, _P(t), C, True)
+    return y
+
+
 def bn_backward_gpu(dz, z, x, smean, sinv, gamma, dgamma, dbeta, training=True, need_dres=False, need_dx=True,
                     sync_fn=None, aff=None, red=None, zm=None, sec=None):
     """Backward of y = relu?(bn(x) [+ res]).

@@ -67,8 +67,12 @@ def pad_dim(t, dim, mult=8):
     return out
 
 
-def conv2d_fwd(x, w16, bias, stride, pad, dil=(1, 1), relu=False, stats=None, out=None, addend=None):
+def conv2d_fwd(x, w16, bias, stride, pad, dil=(1, 1), relu=False, stats=None, out=None, addend=None, pre=None):
     """y = conv(x, w) + bias [+ addend] (+ReLU); optionally accumulate per-channel (sum, sumsq) of y into ``stats``.
+
+    ``pre`` ([2C] fp32 scale | shift): x is a deferred BatchNorm + ReLU output (ops/bn.py deferred): the kernel reads
+    relu(x * scale + shift). Then returns (y, x_mat) with x_mat the materialised input when no kernel applied it on
+    load (csrc/bindings.cpp conv_nt), else None.
 
     x: (N, C, H, W) bf16 channels_last (C % 8 == 0); w16: (K, C, R, S) bf16 channels_last.
     ``out`` may be a channel slice ``buf[:, c0:c0 + K]`` of a channels_last (N, Ctot, OH, OW) buffer (a concat
@@ -95,12 +99,13 @@ def conv2d_fwd(x, w16, bias, stride, pad, dil=(1, 1), relu=False, stats=None, ou
     geo[10] = ldo
     if stats is not None and native.deterministic():
         # deterministic mode: statistics in a separate one-writer-per-slot reduction, not the GEMM epilogue
-        native.get().conv_nt(x, w16, out, bias, None, geo, _fwd_taps(R, S, ph, pw, dh, dw), relu, addend)
+        mat = native.get().conv_nt(x, w16, out, bias, None, geo, _fwd_taps(R, S, ph, pw, dh, dw), relu, addend,
+                                   pre=pre)
         dense = out if ldo == K else out.contiguous(memory_format=CL)
         native.get().bn_stats(dense, stats, N * OH * OW, K)
-        return out
-    native.get().conv_nt(x, w16, out, bias, stats, geo, _fwd_taps(R, S, ph, pw, dh, dw), relu, addend)
-    return out
+        return (out, mat) if pre is not None else out
+    mat = native.get().conv_nt(x, w16, out, bias, stats, geo, _fwd_taps(R, S, ph, pw, dh, dw), relu, addend, pre=pre)
+    return (out, mat) if pre is not None else out
 
 
 _TAP_CACHE = {}
@@ -376,9 +381,18 @@ def conv2d_pairs_fwd(xp, wp, bias, K, OH, OW, R, S2, sh, relu=False, stats=None)
         # profiles/r5_stem_window.txt) — the stem forward is bound by its 411 MB output + statistics epilogue, not
         # by the gather
         geo = [N, Hp, Wq, 32, OH, OW, sh, 1, R * 32, K, K, OH, OW, 1, 1, 0, 0, 8]
-        native.get().conv_nt(xp, wp, out, bias, stats, geo, _window_taps(R), relu, None)
+        det = stats is not None and native.deterministic()
+        native.get().conv_nt(xp, wp, out, bias, None if det else stats, geo, _window_taps(R), relu, None)
+        if det:
+            native.get().bn_stats(out, stats, N * OH * OW, K)
         return out
     geo = [N, Hp, Wq, 8, OH, OW, sh, 1, R * S2 * 8, K, K, OH, OW, 1, 1, 0, 0]
+    if stats is not None and native.deterministic():
+        # deterministic mode: the stem kernels commit statistics with float atomics from thousands of workgroups;
+        # take them from the one-writer-per-slot reduction instead (as conv2d_fwd does)
+        native.get().conv_nt(xp, wp, out, bias, None, geo, _pair_taps(R, S2), relu, None)
+        native.get().bn_stats(out, stats, N * OH * OW, K)
+        return out
     native.get().conv_nt(xp, wp, out, bias, stats, geo, _pair_taps(R, S2), relu, None)
     return out
 

@@ -22,10 +22,10 @@ def get():
             "bigdl_amd native extension (bigdl_amd/_C*.so) is not built or failed to load: "
             f"{e}. Build it with `python setup.py build_ext --inplace` (hipcc --offload-arch=gfx950)."
         ) from e
+    _check_build()          # raises on a stale build under BIGDL_STRICT_BUILD=1 before the module is published
+    if hasattr(mod, "set_deterministic"):
+        mod.set_deterministic(1 if _DET[0] else 0)
     _C = mod
-    _check_build()
-    if hasattr(_C, "set_deterministic"):
-        _C.set_deterministic(1 if _DET[0] else 0)
     return _C
 
 

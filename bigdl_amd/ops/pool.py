@@ -15,12 +15,14 @@ def pool_out(H, W, kh, kw, sh, sw, ph, pw, ceil):
     return out_size(H, kh, sh, ph, 1, ceil), out_size(W, kw, sw, pw, 1, ceil)
 
 
-def maxpool_fwd_gpu(x, kh, kw, sh, sw, ph, pw, ceil=False):
+def maxpool_fwd_gpu(x, kh, kw, sh, sw, ph, pw, ceil=False, pre=None):
+    """``pre`` ([2C] scale | shift): x is a deferred BatchNorm + ReLU output (ops/bn.py deferred), applied on load by
+    the fixed 3x3/2 kernel (materialised first by the binding otherwise)."""
     N, C, H, W = x.shape
     OH, OW = pool_out(H, W, kh, kw, sh, sw, ph, pw, ceil)
     y = torch.empty((N, C, OH, OW), dtype=x.dtype, device=x.device, memory_format=CL)
     idx = torch.empty((N, C, OH, OW), dtype=torch.uint8, device=x.device, memory_format=CL)
-    native.get().maxpool_fwd(x, y, idx, [N, H, W, C, OH, OW, kh, kw, sh, sw, ph, pw])
+    native.get().maxpool_fwd(x, y, idx, [N, H, W, C, OH, OW, kh, kw, sh, sw, ph, pw], pre)
     return y, idx
 
 

@@ -38,14 +38,21 @@ uint8_t* omzm(const OptT& t, int64_t P, int64_t C, const char* n) {
 
 // geo = [Nb, Hs, Ws, Cs, OH, OW, mul_h, mul_w, ldw, Ncol, ldo, OHo, OWo, omul_h, omul_w, ooff_h, ooff_w]
 // taps = flat [tap_h0, tap_w0, tap_k0, tap_h1, ...]
-void conv_nt(const Tensor& src, const Tensor& wt, const Tensor& out, const OptT& bias, const OptT& stats,
+// pre: optional [2 Cs] fp32 scale | shift of a training BN + ReLU whose input `src` is (ConvArgs::pre). When no kernel
+// applies it on load, the BN output is materialised here (bigdl_bn_apply) and returned so the caller can reuse it (the
+// weight gradient reads it); otherwise returns None.
+OptT conv_nt(const Tensor& src, const Tensor& wt, const Tensor& out, const OptT& bias, const OptT& stats,
              std::vector<int64_t> geo, std::vector<int64_t> taps, bool relu, const OptT& addend, const OptT& bn_x,
              const OptT& bn_z, const OptT& bn_mean, const OptT& bn_aff, const OptT& bn_red, bool accumulate,
-             const OptT& bn_zm, const OptT& addend_zm) {
+             const OptT& bn_zm, const OptT& addend_zm, const OptT& pre) {
   TORCH_CHECK(geo.size() == 17 || geo.size() == 18, "conv_nt: bad geometry");
   if (stats && stats->defined())
     TORCH_CHECK(stats->numel() >= BIGDL_STAT_SLOTS * 2 * geo[9], "conv_nt: stats must hold STAT_SLOTS x 2Ncol");
   TORCH_CHECK(taps.size() % 3 == 0 && !taps.empty() && taps.size() / 3 <= CONV_MAX_TAPS, "conv_nt: bad taps");
+  // the epilogue statistics / BN reductions land through multi-writer float atomics: not in deterministic mode
+  // (callers take bn_stats / bn_bwd_reduce there instead)
+  TORCH_CHECK(!bigdl_deterministic() || (!(stats && stats->defined()) && !(bn_red && bn_red->defined())),
+              "conv_nt: epilogue statistics are not deterministic; use bn_stats in deterministic mode");
   ConvArgs a;
   a.src = cbf(src, "src"); a.wt = cbf(wt, "wt");
   a.out = nullptr; a.out32 = nullptr; a.accum32 = accumulate ? 1 : 0;
@@ -77,6 +84,11 @@ void conv_nt(const Tensor& src, const Tensor& wt, const Tensor& out, const OptT&
   a.OHo = geo[11]; a.OWo = geo[12]; a.omul_h = geo[13]; a.omul_w = geo[14]; a.ooff_h = geo[15]; a.ooff_w = geo[16];
   a.pstride = geo.size() == 18 ? (int)geo[17] : 0;
   TORCH_CHECK(a.pstride >= 0 && a.pstride % 8 == 0, "conv_nt: pixel stride must be a multiple of 8");
+  a.pre = ocf(pre, "pre");
+  if (a.pre)
+    TORCH_CHECK(pre->numel() >= 2 * geo[3] && a.pstride == 0 && src.numel() % geo[3] == 0 &&
+                    (src.is_contiguous() || src.is_contiguous(at::MemoryFormat::ChannelsLast)),
+                "conv_nt: pre must hold 2 x Cs floats for a dense source");
   a.ntaps = (int)(taps.size() / 3);
   a.Kdim = a.ntaps * a.Cs;
   a.M = a.Nb * a.OH * a.OW;
@@ -104,6 +116,15 @@ void conv_nt(const Tensor& src, const Tensor& wt, const Tensor& out, const OptT&
   if (a.addend) TORCH_CHECK(a.ldo == a.Ncol, "conv_nt: an addend needs a dense output (ldo == Ncol)");
   TORCH_CHECK((a.OH - 1) * a.omul_h + a.ooff_h < a.OHo && (a.OW - 1) * a.omul_w + a.ooff_w < a.OWo,
               "conv_nt: output placement out of range");
+  OptT materialised;
+  if (a.pre && !bigdl_conv_pre_applies(&a)) {
+    Tensor y = at::empty_like(src);
+    const int64_t P = src.numel() / a.Cs;
+    bigdl_bn_apply(a.src, a.pre, a.pre + a.Cs, nullptr, (uint16_t*)y.data_ptr(), P, a.Cs, 1, stream(), nullptr);
+    a.src = (const uint16_t*)y.data_ptr();
+    a.pre = nullptr;
+    materialised = y;
+  }
   a.ws = nullptr;
   Tensor ws;
   const long wsn = bigdl_conv_nt_plan(&a);
@@ -114,6 +135,7 @@ void conv_nt(const Tensor& src, const Tensor& wt, const Tensor& out, const OptT&
   const int rc = bigdl_conv_nt(&a, stream());
   TORCH_CHECK(rc == 0, "conv_nt: unsupported shape (channels must be a multiple of 8; fp32 output needs Ncol % 8 "
               "== 0 and no fused stats / BN / ReLU / addend)");
+  return materialised;
 }
 
 // geo = [Nb, Hs, Ws, Cs, OH, OW, R, S, sh, sw, ph, pw, dh, dw, M, Ncol, Kdim, ldy]
@@ -400,11 +422,25 @@ void cast_bf16_f32(const Tensor& x, const Tensor& y) {
 }
 
 // pg = [N, H, W, C, OH, OW, kh, kw, sh, sw, ph, pw]
-void maxpool_fwd(const Tensor& x, const Tensor& y, const Tensor& idx, std::vector<int64_t> g) {
+// pre: optional [2 C] scale | shift of the training BN + ReLU whose input x is (applied on load by the fixed 3x3/2
+// kernel, else materialised first)
+void maxpool_fwd(const Tensor& x, const Tensor& y, const Tensor& idx, std::vector<int64_t> g, const OptT& pre) {
   TORCH_CHECK(g.size() == 12 && g[3] % 8 == 0 && g[6] * g[7] <= 256, "maxpool: geometry");
   TORCH_CHECK(idx.scalar_type() == at::kByte && idx.numel() == y.numel(), "maxpool: idx");
-  bigdl_maxpool_fwd(cbf(x, "x"), mbf(y, "y"), (uint8_t*)idx.data_ptr(), g[0], g[1], g[2], g[3], g[4], g[5], g[6], g[7],
-                    g[8], g[9], g[10], g[11], stream());
+  const float* pr = ocf(pre, "pre");
+  const uint16_t* xs = cbf(x, "x");
+  Tensor tmp;
+  if (pr) {
+    TORCH_CHECK(pre->numel() >= 2 * g[3] && x.numel() == g[0] * g[1] * g[2] * g[3], "maxpool: pre / x");
+    if (!bigdl_maxpool_pre_applies(g[0], g[1], g[2], g[3], g[4], g[5], g[6], g[7], g[8], g[9])) {
+      tmp = at::empty_like(x);
+      bigdl_bn_apply(xs, pr, pr + g[3], nullptr, (uint16_t*)tmp.data_ptr(), x.numel() / g[3], g[3], 1, stream(), nullptr);
+      xs = (const uint16_t*)tmp.data_ptr();
+      pr = nullptr;
+    }
+  }
+  bigdl_maxpool_fwd(xs, mbf(y, "y"), (uint8_t*)idx.data_ptr(), g[0], g[1], g[2], g[3], g[4], g[5], g[6], g[7],
+                    g[8], g[9], g[10], g[11], stream(), pr);
 }
 void maxpool_bwd(const Tensor& dy, const Tensor& idx, const Tensor& dx, std::vector<int64_t> g) {
   TORCH_CHECK(g.size() == 12 && g[3] % 8 == 0, "maxpool_bwd: geometry");
@@ -541,7 +577,7 @@ void conv_i8(const Tensor& src, const Tensor& wt, const Tensor& out, const OptT&
   a.wt = reinterpret_cast<const uint16_t*>(wt.data_ptr<int8_t>());
   a.out = reinterpret_cast<uint16_t*>(out.data_ptr());
   a.bias = ocf(bias, "bias"); a.stats = nullptr; a.addend = nullptr; a.out32 = nullptr; a.accum32 = 0;
-  a.ws = nullptr; a.ksplit = 0; a.pstride = 0;
+  a.ws = nullptr; a.ksplit = 0; a.pstride = 0; a.pre = nullptr;
   a.bnx = nullptr; a.bnz = nullptr; a.bnzm = nullptr; a.addzm = nullptr; a.bnmean = nullptr; a.bnaff = nullptr;
   a.bnred = nullptr;
   a.Nb = geo[0]; a.Hs = geo[1]; a.Ws = geo[2]; a.Cs = geo[3]; a.OH = geo[4]; a.OW = geo[5];
@@ -1307,7 +1343,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("geo"), py::arg("taps"), py::arg("relu"), py::arg("addend") = py::none(), py::arg("bn_x") = py::none(),
         py::arg("bn_z") = py::none(), py::arg("bn_mean") = py::none(), py::arg("bn_aff") = py::none(),
         py::arg("bn_red") = py::none(), py::arg("accumulate") = false, py::arg("bn_zm") = py::none(),
-        py::arg("addend_zm") = py::none());
+        py::arg("addend_zm") = py::none(), py::arg("pre") = py::none());
   m.def("conv_wgrad", &conv_wgrad);
   m.def("transpose_krsc", &transpose_krsc);
   m.def("bn_stats", &bn_stats);
@@ -1354,7 +1390,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("copy_rows_i8", &copy_rows_i8);
   m.def("cast_f32_bf16", &cast_f32_bf16);
   m.def("cast_bf16_f32", &cast_bf16_f32);
-  m.def("maxpool_fwd", &maxpool_fwd);
+  m.def("maxpool_fwd", &maxpool_fwd, py::arg("x"), py::arg("y"), py::arg("idx"), py::arg("g"), py::arg("pre") = py::none());
   m.def("maxpool_bwd", &maxpool_bwd);
   m.def("avgpool_fwd", &avgpool_fwd);
   m.def("avgpool_bwd", &avgpool_bwd);

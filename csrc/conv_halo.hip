@@ -275,12 +275,20 @@ __device__ __forceinline__ void halo_epi_i8(const ConvArgs& a, const I8Epi& ep, 
 // the prologue (stale LDS), bit 3 no fragment reads
 // EPI: 0 lean epilogue (no addend / consumer-BN reduction), 2 lean + consumer-BN reduction, 1 full epilogue,
 // 3 int8 (EB = 1: int8 activations and weights, 64-channel chunks on v_mfma_i32_16x16x64_i8, I8Epi epilogue)
-template <int W, int RB, int NIMG, int KT, int WPX, int EPI, int ABL = 0, int EB = 2>
+// PRE: the source is the input of a training BatchNorm + ReLU (ConvArgs::pre = [scale | shift], C <= PRE_MAXC): each
+// lane rewrites the granules it staged, relu(x * scale + shift) rounded to bf16 (bn_apply_kernel's expression), once
+// its own DMA has landed and before the barrier that publishes the chunk; granules of halo / pad rows (out-of-range
+// offsets, read as zeros) are left zero. The per-channel table sits in LDS behind the pipeline buffers.
+constexpr int PRE_MAXC = 512;
+template <int W, int RB, int NIMG, int KT, int WPX, int EPI, int ABL = 0, int EB = 2, bool PRE = false>
 __global__ __launch_bounds__(256, 2) void conv_halo_kernel(ConvArgs a, I8Epi ep) {
   static_assert((EB == 1) == (EPI == 3), "int8 operands go with the int8 epilogue");
+  static_assert(!PRE || (EB == 2 && EPI == 0), "BN-on-load: bf16 forwards with the lean epilogue");
   constexpr int CH = 64 / EB;                                 // channels per 64-byte chunk row
   using H = HaloF<W, RB, NIMG, KT, WPX>;
-  __shared__ __attribute__((aligned(1024))) unsigned char lds[H::LDS];
+  constexpr int PREB = PRE ? PRE_MAXC * 8 : 0;
+  static_assert(2 * (H::LDS + PREB) <= 160 * 1024, "two workgroups per CU");
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[H::LDS + PREB];
   constexpr int WCH = H::WCH, FM = H::FM, FN = H::FN, WP = H::WP;
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -343,6 +351,42 @@ __global__ __launch_bounds__(256, 2) void conv_halo_kernel(ConvArgs a, I8Epi ep)
   const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<bf16_t*>(reinterpret_cast<const bf16_t*>(a.wt)), (short)0,
       (int)(((size_t)(a.Ncol - 1) * a.ldw + a.Kdim) * EB), 0x00020000);
+  // PRE: rows this lane staged from the image (bit d: instruction d's offset is in range), its granule's channels
+  unsigned xreal = 0;
+  float* const ptab = reinterpret_cast<float*>(lds + H::LDS);
+  if constexpr (PRE) {
+#pragma unroll
+    for (int d = 0; d < H::XI; ++d)
+      if (xo[d] != OOB) xreal |= 1u << d;
+    for (int i = tid; i < C / 2; i += 256)            // [scale C | shift C] as float4s
+      reinterpret_cast<v4f*>(ptab)[i] = reinterpret_cast<const v4f*>(a.pre)[i];
+    __syncthreads();
+  }
+  // granule slot lane & 3 of every row this lane fills holds source granule (lane & 3) ^ hswz(row), and
+  // hswz(row) = 2 * ((lane >> 4) & 1) for all of them
+  const int pre_c = 8 * ((lane & 3) ^ (((lane >> 4) & 1) << 1));
+  auto pre_apply = [&](int ch) {
+    if constexpr (PRE) {
+      unsigned char* X = lds + (ch & 1) * H::XBYTES;
+      const int c = ch * CH + pre_c;
+      const v4f s0 = *reinterpret_cast<const v4f*>(ptab + c), s1 = *reinterpret_cast<const v4f*>(ptab + c + 4);
+      const v4f b0 = *reinterpret_cast<const v4f*>(ptab + C + c), b1 = *reinterpret_cast<const v4f*>(ptab + C + c + 4);
+      const float sc[8] = {s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
+      const float sh[8] = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+#pragma unroll
+      for (int d = 0; d < H::XI; ++d) {
+        if (!((xreal >> d) & 1u)) continue;
+        v4u* q = reinterpret_cast<v4u*>(X + (d * 4 + wave) * 1024 + lane * 16);
+        v4u u = *q;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          u[e] = pack2bf(fmaxf(lo_bf(u[e]) * sc[2 * e] + sh[2 * e], 0.f),
+                         fmaxf(hi_bf(u[e]) * sc[2 * e + 1] + sh[2 * e + 1], 0.f));
+        *q = u;
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");     // the rewritten chunk is complete before the barrier
+    }
+  };
 
   auto issue_x = [&](int ch) {
     const size_t xb = xbase + (size_t)ch * CH;                 // elements
@@ -395,6 +439,7 @@ __global__ __launch_bounds__(256, 2) void conv_halo_kernel(ConvArgs a, I8Epi ep)
     if (s < nk) issue_ws(s);
   if (nk > H::D - 1) vmw<(H::D - 1) * H::WI>();
   else vmw<0>();
+  pre_apply(0);
   __builtin_amdgcn_s_barrier();
 
   for (int ch = 0; ch < nch; ++ch) {
@@ -453,6 +498,10 @@ __global__ __launch_bounds__(256, 2) void conv_halo_kernel(ConvArgs a, I8Epi ep)
       } else {
         vmw<0>();
       }
+      // chunk ch + 1 (issued at t = 0) is older than weight step s + 1 from t = D on: this lane's part has landed
+      if constexpr (PRE && t == H::D) {
+        if (ch + 1 < nch) pre_apply(ch + 1);
+      }
       __builtin_amdgcn_s_barrier();
     });
   }
@@ -499,6 +548,7 @@ void launch_halo_f(const ConvArgs& a, hipStream_t st) {
   else if (abl == 9) conv_halo_kernel<W, RB, NIMG, KT, WPX, 0, 9><<<g, b, 0, st>>>(a, I8Epi{});
   else if (abl == 13) conv_halo_kernel<W, RB, NIMG, KT, WPX, 0, 13><<<g, b, 0, st>>>(a, I8Epi{});
   else if (abl == 15) conv_halo_kernel<W, RB, NIMG, KT, WPX, 0, 15><<<g, b, 0, st>>>(a, I8Epi{});
+  else if (lean && a.pre) conv_halo_kernel<W, RB, NIMG, KT, WPX, 0, 0, 2, true><<<g, b, 0, st>>>(a, I8Epi{});
   else if (lean) conv_halo_kernel<W, RB, NIMG, KT, WPX, 0><<<g, b, 0, st>>>(a, I8Epi{});
   else if (leanbn && g_conv_halo_bn) conv_halo_kernel<W, RB, NIMG, KT, WPX, 2><<<g, b, 0, st>>>(a, I8Epi{});
   else conv_halo_kernel<W, RB, NIMG, KT, WPX, 1><<<g, b, 0, st>>>(a, I8Epi{});
@@ -723,6 +773,13 @@ int bigdl_conv_halo_applies(const ConvArgs* a) {
   if (seen != 0x1ffu) return 0;
   if ((size_t)a->Nb * a->Hs * a->Ws * a->Cs * 2 >= (1ull << 31) - (1ull << 20)) return 0;   // 32-bit buffer offsets
   if ((size_t)a->Ncol * a->ldw * 2 >= (1ull << 31)) return 0;
+  // the epilogue reads / writes out, addend, bnx and the masks through the same 32-bit buffer offsets: the whole
+  // output extent (bf16 rows of ldo) must fit too (int8 callers go through here with the same bound)
+  const size_t M = (size_t)a->Nb * a->OH * a->OW;
+  if (((M - 1) * (size_t)a->ldo + a->Ncol) * 2 >= 0x7ff00000ull) return 0;
+  // a BN applied on load: the lean epilogue only (no addend / consumer-BN reduction), channel table in LDS
+  if (a->pre && (a->addend || (a->bnred && !a->stats) || a->Cs > PRE_MAXC || (g_conv_halo != 1 && g_conv_halo != 2)))
+    return 0;
   auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
   return al(a->src) && al(a->wt) && al(a->out) && al(a->addend) && al(a->bnx) && al(a->bnz);
 }

@@ -2254,12 +2254,12 @@ __global__ __launch_bounds__(512, 2) void conv_nt_p8_kernel(ConvArgs a) {
 //    the end (same-address atomics serialise at the memory side: slots = block id % BIGDL_STAT_SLOTS).
 // Semantics are nt_epilogue_lds's (bias + addend added in fp32 before rounding, ReLU, BN statistics of the rounded
 // output, consumer-BN reduction of the rounded gradient with the z / affine ReLU mask).
-template <int K, int CG, int BMW, bool F32T, bool EXT>
+template <int K, int CG, int BMW, bool F32T, bool EXT, bool PRE = false>
 __global__ __launch_bounds__(256, 2) void conv_nt_s1_kernel(ConvArgs a) {
   constexpr int KF = K / 32, MI = BMW / 16, PGN = 4 / CG, BM = BMW * PGN;
   constexpr int GPR = F32T ? 16 : 8;               // 16-byte granules per 64-channel row of the LDS slice
   constexpr int NR = BMW / 8;                      // row-phase passes (8 pixels x 8 lanes each)
-  __shared__ __attribute__((aligned(16))) unsigned lds[4 * BMW * GPR * 4];
+  __shared__ __attribute__((aligned(16))) unsigned lds[4 * BMW * GPR * 4 + (PRE ? 2 * K : 0)];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int cg = wave % CG, pg = wave / CG;
@@ -2278,6 +2278,15 @@ __global__ __launch_bounds__(256, 2) void conv_nt_s1_kernel(ConvArgs a) {
     for (int kk = 0; kk < KF; ++kk)
       wf[j][kk] = *reinterpret_cast<const v8s*>(a.wt + (size_t)(c0 + 16 * j + (lane & 15)) * a.ldw + 32 * kk +
                                                 8 * (lane >> 4));
+  // PRE: the A operand is relu(x * scale[c] + shift[c]) of the producing BatchNorm (ConvArgs::pre): the [scale K |
+  // shift K] table sits in LDS behind the wave slices (in VGPRs it spilled); a lane's fragment channels are
+  // 32 kk + 8 (lane >> 4) + e
+  const float* ptab = reinterpret_cast<const float*>(lds + 4 * BMW * GPR * 4);
+  if constexpr (PRE) {
+    for (int i = threadIdx.x; i < K / 2; i += 256)
+      reinterpret_cast<v4f*>(lds + 4 * BMW * GPR * 4)[i] = reinterpret_cast<const v4f*>(a.pre)[i];
+    __syncthreads();
+  }
   float bs[8], bmu[8], bsc[8], bsh[8];
   const bool bnw = EXT && a.bnred && !a.stats;
 #pragma unroll
@@ -2335,6 +2344,25 @@ __global__ __launch_bounds__(256, 2) void conv_nt_s1_kernel(ConvArgs a) {
     for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+    if constexpr (PRE) {     // BN apply + ReLU on the loaded operand (bn_apply_kernel's expression and rounding)
+#pragma unroll
+      for (int kk = 0; kk < KF; ++kk) {
+        const int c = 32 * kk + 8 * (lane >> 4);
+        const v4f s0 = *reinterpret_cast<const v4f*>(ptab + c), s1 = *reinterpret_cast<const v4f*>(ptab + c + 4);
+        const v4f b0 = *reinterpret_cast<const v4f*>(ptab + K + c), b1 = *reinterpret_cast<const v4f*>(ptab + K + c + 4);
+        const float sc[8] = {s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
+        const float sh[8] = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+          v4u u = __builtin_bit_cast(v4u, af[i][kk]);
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            u[e] = pack2bf(fmaxf(lo_bf(u[e]) * sc[2 * e] + sh[2 * e], 0.f),
+                           fmaxf(hi_bf(u[e]) * sc[2 * e + 1] + sh[2 * e + 1], 0.f));
+          af[i][kk] = __builtin_bit_cast(v8s, u);
+        }
+      }
+    }
 #pragma unroll
     for (int kk = 0; kk < KF; ++kk)
 #pragma unroll
@@ -2758,11 +2786,13 @@ static bool s1_applies(const ConvArgs* a) {
   if (((size_t)(a->M - 1) * a->ldo + a->Ncol) * 2 >= 0x7ff00000u) return false;
   // the consumer-BN ReLU mask as a bf16 z tensor (BIGDL_BN_ZMASK=0) is left to the tile kernels
   if (a->bnred && !a->stats && a->bnz && !a->bnzm) return false;
+  // a BN applied on load (ConvArgs::pre) only with the plain epilogue (forwards: statistics, ReLU, no bias / addend)
+  if (a->pre && (a->bias || a->addend || (a->bnred && !a->stats))) return false;
   auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
   return al(a->src) && al(a->wt) && al(a->out) && al(a->addend) && al(a->bnx) && al(a->bnz);
 }
 
-template <int K, int CG, int BMW, bool F32T, bool EXT>
+template <int K, int CG, int BMW, bool F32T, bool EXT, bool PRE = false>
 void launch_s1(const ConvArgs& a, hipStream_t st) {
   static int cus = 0;
   if (cus == 0) {
@@ -2775,7 +2805,7 @@ void launch_s1(const ConvArgs& a, hipStream_t st) {
   const int tiles = (a.M + BMW * (4 / CG) - 1) / (BMW * (4 / CG));
   int per = std::max(1, (2 * cus) / nchb);
   per = std::min(per, tiles);
-  conv_nt_s1_kernel<K, CG, BMW, F32T, EXT><<<dim3(per * nchb), dim3(256), 0, st>>>(a);
+  conv_nt_s1_kernel<K, CG, BMW, F32T, EXT, PRE><<<dim3(per * nchb), dim3(256), 0, st>>>(a);
 }
 
 template <int K, int CG>
@@ -2783,7 +2813,9 @@ void launch_s1_cg(const ConvArgs& a, hipStream_t st) {
   const bool ext = a.addend != nullptr || (a.bnred != nullptr && a.stats == nullptr);
   const bool f32t = ext || a.bias != nullptr;
   constexpr int BW = K == 64 ? 64 : 32;            // pixels per wave tile (ubench: 64 / 32 best at K 64 / 128)
-  if (ext) launch_s1<K, CG, BW / 2, true, true>(a, st);
+  // s1_applies: no bias / addend / BN reduction with pre; 32-pixel waves (the 64-pixel K = 64 tile spilled)
+  if (a.pre) launch_s1<K, CG, 32, false, false, true>(a, st);
+  else if (ext) launch_s1<K, CG, BW / 2, true, true>(a, st);
   else if (f32t) launch_s1<K, CG, BW / 2, true, false>(a, st);
   else launch_s1<K, CG, BW, false, false>(a, st);
 }
@@ -2854,8 +2886,21 @@ long bigdl_conv_nt_plan(ConvArgs* a) {
   return 0;
 }
 
+int bigdl_conv_pre_applies(const ConvArgs* a) {
+  if (a->Cs % 8 != 0 || a->Kdim != a->ntaps * a->Cs || a->M <= 0 || a->pstride > 0 || conv_impl() != 1) return 0;
+  if (bigdl_stem_fwd_applies(a)) return 0;
+  return (s1_applies(a) || bigdl_conv_halo_applies(a)) ? 1 : 0;
+}
+
 int bigdl_conv_nt(const ConvArgs* a, hipStream_t st) {
   if (a->Cs % 8 != 0 || a->Kdim != a->ntaps * a->Cs || a->ntaps < 1 || a->ntaps > CONV_MAX_TAPS) return -1;
+  if (a->pre) {     // a BN applied on load: only the kernels that implement it (the caller materialises otherwise)
+    if (!bigdl_conv_pre_applies(a)) return -5;
+    if (s1_applies(a)) launch_s1_any(*a, st);
+    else if (bigdl_conv_halo(a, st) != 0) return -5;
+    HIP_LAUNCH_CHECK();
+    return 0;
+  }
   // the BN-backward reduction lives in the LDS-transposed epilogue only
   if (a->bnred && (a->stats || a->bnx == nullptr || a->bnmean == nullptr || (a->Ncol & 7) || (a->ldo & 7))) return -2;
   // fp32 output exists in the LDS-transposed epilogue only (aligned columns), without stats / BN / ReLU / addend

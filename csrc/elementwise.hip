@@ -208,14 +208,24 @@ __global__ void maxpool_bwd_kernel(const bf16_t* __restrict__ dy, const uint8_t*
 // Fixed K x K / stride-S windows (the 3x3 / 2 stem pools of ResNet and Inception): 32-bit index math (the host
 // checks the element counts) and every window load issued before the first compare, so a lane keeps K*K
 // 16-byte loads in flight instead of walking the window one dependent branch at a time.
-template <int K, int S>
+// PRE: x is the input of a training BatchNorm + ReLU ([scale C | shift C] in `pre`, ConvArgs::pre semantics): every
+// window element is relu(x * scale + shift) rounded to bf16 before the compare (bit-equal to pooling bn_apply's output)
+template <int K, int S, bool PRE = false>
 __global__ __launch_bounds__(256) void maxpool_fwd_fixed_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
                                                                 uint8_t* __restrict__ idx, int N, int H, int W, int C,
-                                                                int OH, int OW, int ph, int pw) {
+                                                                int OH, int OW, int ph, int pw,
+                                                                const float* __restrict__ pre = nullptr) {
   const int G = C >> 3;
   const int total = N * OH * OW * G;
   for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
     const int g = i % G;
+    float psc[8], psh[8];
+    if constexpr (PRE) {
+      const v4f s0 = *reinterpret_cast<const v4f*>(pre + g * 8), s1 = *reinterpret_cast<const v4f*>(pre + g * 8 + 4);
+      const v4f b0 = *reinterpret_cast<const v4f*>(pre + C + g * 8), b1 = *reinterpret_cast<const v4f*>(pre + C + g * 8 + 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { psc[e] = s0[e]; psc[e + 4] = s1[e]; psh[e] = b0[e]; psh[e + 4] = b1[e]; }
+    }
     int p = i / G;
     const int ow = p % OW; p /= OW;
     const int oh = p % OH;
@@ -240,6 +250,12 @@ __global__ __launch_bounds__(256) void maxpool_fwd_fixed_kernel(const bf16_t* __
 #pragma unroll
     for (int t = 0; t < K * K; ++t) {
       if (!ok[t]) continue;
+      if constexpr (PRE) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          v[t][e] = pack2bf(fmaxf(lo_bf(v[t][e]) * psc[2 * e] + psh[2 * e], 0.f),
+                            fmaxf(hi_bf(v[t][e]) * psc[2 * e + 1] + psh[2 * e + 1], 0.f));
+      }
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const float l = lo_bf(v[t][e]), h = hi_bf(v[t][e]);
@@ -883,13 +899,20 @@ void bigdl_cast_bf16_f32(const uint16_t* x, float* y, long n, hipStream_t st) {
   HIP_LAUNCH_CHECK();
 }
 void bigdl_maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* idx, int N, int H, int W, int C, int OH, int OW,
-                       int kh, int kw, int sh, int sw, int ph, int pw, hipStream_t st) {
+                       int kh, int kw, int sh, int sw, int ph, int pw, hipStream_t st, const float* pre) {
   const long outs = (long)N * OH * OW * (C / 8), ins = (long)N * H * W * C;
-  if (kh == 3 && kw == 3 && sh == 2 && sw == 2 && outs < (1l << 31) && ins < (1l << 31))
+  const bool fixed = kh == 3 && kw == 3 && sh == 2 && sw == 2 && outs < (1l << 31) && ins < (1l << 31);
+  if (pre) {   // bigdl_maxpool_pre_applies: the fixed window only
+    maxpool_fwd_fixed_kernel<3, 2, true><<<grid_cap(outs), 256, 0, st>>>(x, y, idx, N, H, W, C, OH, OW, ph, pw, pre);
+  } else if (fixed)
     maxpool_fwd_fixed_kernel<3, 2><<<grid_cap(outs), 256, 0, st>>>(x, y, idx, N, H, W, C, OH, OW, ph, pw);
   else
     maxpool_fwd_kernel<<<grid_cap(outs), 256, 0, st>>>(x, y, idx, N, H, W, C, OH, OW, kh, kw, sh, sw, ph, pw);
   HIP_LAUNCH_CHECK();
+}
+int bigdl_maxpool_pre_applies(int N, int H, int W, int C, int OH, int OW, int kh, int kw, int sh, int sw) {
+  const long outs = (long)N * OH * OW * (C / 8), ins = (long)N * H * W * C;
+  return kh == 3 && kw == 3 && sh == 2 && sw == 2 && outs < (1l << 31) && ins < (1l << 31) && C % 8 == 0;
 }
 static bool maxpool_k3s2_ok(int H, int W, int C, int OH, int OW, int kh, int kw, int sh, int sw, int ph, int pw,
                             long ins, long outs) {

@@ -48,6 +48,11 @@ struct ConvArgs {
   // windows of Cs elements: the bf16 stem's pixel pairs (stem.hip) read 4 consecutive pairs (all 7 width taps of
   // one output column) as one 32-element "pixel" (conv_nt_g4_kernel only)
   int pstride;
+  // optional [2 Cs] fp32 scale | shift of a training BatchNorm + ReLU that produced the source: the kernel reads
+  // relu(x * scale[c] + shift[c]) (rounded to bf16, bit-equal to bigdl_bn_apply's output) instead of x, and zero
+  // padding stays zero — the BN output is never materialised (forward GEMMs of the streaming 1x1 and halo 3x3
+  // kernels only: bigdl_conv_pre_applies)
+  const float* pre;
 };
 
 // int8 convolution epilogue (quant.hip, conv_halo.hip): dequantize with the per-sample input scale and the per-channel
@@ -81,6 +86,8 @@ void bigdl_fill_bytes(void* ptr, int value, long bytes, hipStream_t st);
 int bigdl_deterministic();
 void bigdl_set_deterministic(int v);
 void bigdl_colsum_bf16_ld(const uint16_t* x, float* out, long P, int K, long ld, hipStream_t st);
+// 1 when bigdl_conv_nt can apply a->pre inside the kernel that takes the GEMM (else the caller materialises the source)
+int bigdl_conv_pre_applies(const ConvArgs* a);
 int bigdl_conv_nt(const ConvArgs* a, hipStream_t st);
 // 3x3 / stride-1 / pad-1 forward or data-gradient GEMM from halo tiles (conv_halo.hip)
 int bigdl_conv_halo_applies(const ConvArgs* a);
@@ -155,7 +162,8 @@ void bigdl_cast_bf16_f32(const uint16_t* x, float* y, long n, hipStream_t st);
 
 // pooling (NHWC bf16)
 void bigdl_maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* idx, int N, int H, int W, int C, int OH,
-                       int OW, int kh, int kw, int sh, int sw, int ph, int pw, hipStream_t st);
+                       int OW, int kh, int kw, int sh, int sw, int ph, int pw, hipStream_t st, const float* pre = nullptr);
+int bigdl_maxpool_pre_applies(int N, int H, int W, int C, int OH, int OW, int kh, int kw, int sh, int sw);
 int bigdl_stem_i8_applies(const ConvArgs* a, const I8Epi* ep);
 void bigdl_set_stem_i8(int v);
 int bigdl_stem_i8_f32(const ConvArgs* a, const I8Epi* ep, const float* img, int C, int W, float inv, hipStream_t st);

@@ -106,6 +106,7 @@ def test_bottleneck_masked_residual_addend(monkeypatch):
     x = torch.randn(4, 256, 14, 14).cuda().to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     gy = torch.randn(4, 256, 14, 14).cuda().to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     res = {}
+    saved = fusion.MASKED_ADDEND[0]
     for on in (True, False):
         m = copy.deepcopy(blk).to("cuda")
         fuse_for_training(m)
@@ -114,11 +115,19 @@ def test_bottleneck_masked_residual_addend(monkeypatch):
             m.forward(x)
             g = m.backward(x, gy)
         finally:
-            fusion.MASKED_ADDEND[0] = False
+            fusion.MASKED_ADDEND[0] = saved      # restore the default (on), not a fixed value
         res[on] = (g.float().clone(), _weight_grads(m))
     assert any(seen)
     assert _rel(res[True][0], res[False][0]) < 1e-5
     assert _rel(res[True][1], res[False][1]) < 1e-4
+    # and against the fp32 engine on the CPU (same bf16-rounded input / gradient): only rounding points differ
+    cpu = copy.deepcopy(blk)
+    xc, gyc = x.float().cpu().contiguous(), gy.float().cpu().contiguous()
+    cpu.forward(xc)
+    gc = cpu.backward(xc, gyc)
+    assert _rel(res[True][0], gc) < 5e-2
+    assert _cos(res[True][0], gc) > 0.99
+    assert _cos(res[True][1], _weight_grads(cpu)) > 0.99
 
 
 @pytest.mark.parametrize("depth,dataset,img", [(50, "ImageNet", 224), (20, "CIFAR10", 32)])
