@@ -409,11 +409,13 @@ class SpatialConvolution(TensorModule):
             self._wgrad_gpu_pairs(x, gy16)
             return
         x16 = getattr(self, "_x16", None)
+        pre = None
         if x16 is None or x16.shape[0] != x.shape[0] or x16.shape[2:] != x.shape[2:]:
             x16 = cv.to_nhwc_bf16(bnops.materialize(x))
         elif getattr(self, "_x16_pre", None) is not None:
-            # the forward applied a deferred BN + ReLU on load: materialise it here, on the weight-gradient stream
-            x16 = bnops.materialize(bnops.deferred(x16, self._x16_pre))
+            # the forward applied a deferred BN + ReLU on load: the weight gradient applies it too (halo 3x3 kernel) or
+            # gets it materialised on the weight-gradient stream
+            pre = self._x16_pre
         st, pd, dl = (self.strideH, self.strideW), (ph, pw), (self.dilationH, self.dilationW)
         if self.nGroup != 1 and self._direct_groups():
             xf = getattr(self, "_xf", None)
@@ -443,8 +445,10 @@ class SpatialConvolution(TensorModule):
         K = self.nOutputPlane
         direct = (x16.shape[1] == self.nInputPlane and K % 8 == 0 and self.scaleW == 1.0 and self.scaleB == 1.0
                   and self.gradWeight.is_contiguous(memory_format=CL))
+        if pre is not None and not direct:
+            x16 = bnops.materialize(bnops.deferred(x16, pre))
         if direct:
-            cv.conv2d_wgrad(gy16, x16, self.gradWeight, self.gradBias, st, pd, dl)
+            cv.conv2d_wgrad(gy16, x16, self.gradWeight, self.gradBias, st, pd, dl, pre=pre)
         else:
             gyp = cv.pad_dim(gy16, 1)
             dw = ops.zeros(gyp.shape[1], x16.shape[1], self.kernelH, self.kernelW, device=x.device,

@@ -229,14 +229,28 @@ def _fuse_sequential(seq):
         _plan_deferred_bn(a, b, c)
 
 
+# Which consumers take a deferred BN + ReLU output (BIGDL_BN_DEFER): 1 (default) = the 3x3/2 max pool only (it
+# applies it on load at no cost; the ResNet stem BN loses its 411 MB apply pass); 2 = also 3x3 / stride-1 convs (halo
+# forward + halo weight gradient apply it on load); 0 = none. Level 2 is correct (tests/test_bn_defer_gpu.py) but
+# slower on ResNet-50: the on-load transform costs the latency-bound halo kernels more than the HBM-rate apply pass
+# it removes (+0.13 ms fwd, +0.42 ms weight gradients vs -0.38 ms of apply passes: profiles/r6_iteration_log.txt)
+DEFER_LEVEL = [int(os.environ.get("BIGDL_BN_DEFER", "1") or 0)]
+
+
 def _defer_consumer(c):
-    """Modules that take a deferred BN + ReLU output (ops/bn.py deferred) and apply it on load or materialise it."""
+    """Modules that take a deferred BN + ReLU output (ops/bn.py deferred) and apply it on load in every pass that
+    reads it: the 3x3/2 max pool, and (level 2) 3x3 / stride-1 convolutions (halo forward and halo weight gradient;
+    other shapes get it materialised by the binding). A 1x1 consumer is never deferred: its weight gradient would have
+    to materialise the BN output on the side stream, which moves the apply pass instead of removing it."""
     from .pooling import SpatialMaxPooling
 
     if isinstance(c, SpatialConvolution):        # (subclasses that keep the base forward / weight gradient)
+        if DEFER_LEVEL[0] < 2:
+            return False
         return (c.nGroup == 1 and c.format == "NCHW" and type(c).updateOutput is SpatialConvolution.updateOutput
-                and type(c)._wgrad_gpu is SpatialConvolution._wgrad_gpu)
-    return type(c) is SpatialMaxPooling and c.format == "NCHW"
+                and type(c)._wgrad_gpu is SpatialConvolution._wgrad_gpu and c.kernelW == 3 and c.kernelH == 3
+                and c.strideW == 1 and c.strideH == 1 and c.dilationW == 1 and c.dilationH == 1)
+    return DEFER_LEVEL[0] >= 1 and type(c) is SpatialMaxPooling and c.format == "NCHW"
 
 
 def _plan_deferred_bn(a, b, c):

@@ -23,7 +23,7 @@ from .init_methods import Ones, RandomUniform, Zeros
 
 _ZMASK = os.environ.get("BIGDL_BN_ZMASK", "1") != "0"
 # BIGDL_BN_DEFER=0: always materialise a training BN + ReLU output, even where nn.fusion found a consumer that applies
-# it on load (ConvArgs::pre: streaming 1x1 / halo 3x3 forwards, the 3x3/2 max pool)
+# it on load (ConvArgs::pre). See nn.fusion._defer_consumer for which consumers each level defers to.
 _DEFER = [os.environ.get("BIGDL_BN_DEFER", "1") != "0"]
 CL = torch.channels_last
 BF16 = torch.bfloat16

@@ -405,8 +405,11 @@ def conv2d_pairs_wgrad(dy, xp, R, S2, sh, dwp32, dbias32):
     native.get().conv_wgrad(dy, xp, dwp32, dbias32, geo)
 
 
-def conv2d_wgrad(dy, x, dw32, dbias32, stride, pad, dil=(1, 1)):
-    """dW (fp32, (K, C, R, S) channels_last buffer) += conv weight gradient; dbias += sum(dy)."""
+def conv2d_wgrad(dy, x, dw32, dbias32, stride, pad, dil=(1, 1), pre=None):
+    """dW (fp32, (K, C, R, S) channels_last buffer) += conv weight gradient; dbias += sum(dy).
+
+    ``pre`` ([2C] scale | shift): x is a deferred BatchNorm + ReLU output (ops/bn.py deferred): the halo 3x3 weight
+    gradient applies it on load; any other kernel gets the materialised input (csrc/bindings.cpp conv_wgrad)."""
     N, C, H, W = x.shape
     _, K, OH, OW = dy.shape
     Kw, Cw, R, S = dw32.shape
@@ -416,12 +419,16 @@ def conv2d_wgrad(dy, x, dw32, dbias32, stride, pad, dil=(1, 1)):
     ph, pw = pad
     dh, dw = dil
     geo = [N, H, W, C, OH, OW, R, S, sh, sw, ph, pw, dh, dw, N * OH * OW, K, R * S * C, K]
+    if pre is not None and _gemm_shaped(dy, x, dw32, stride, pad, dil):
+        from . import bn as bnops
+
+        x, pre = bnops.materialize(bnops.deferred(x, pre)), None
     if (P >= 512 and ((K + 127) // 128) * ((C + 127) // 128) >= 192 and _gemm_shaped(dy, x, dw32, stride, pad, dil)
             and not native.get().conv_wgrad_uses_p8(geo, dbias32 is not None)):
         gemm_wgrad_nt(dy.reshape(P, K) if dy.is_contiguous() else dy.permute(0, 2, 3, 1).reshape(P, K),
                       x.reshape(P, C) if x.is_contiguous() else x.permute(0, 2, 3, 1).reshape(P, C), dw32, dbias32)
         return
-    native.get().conv_wgrad(dy, x, dw32, dbias32, geo)
+    native.get().conv_wgrad(dy, x, dw32, dbias32, geo, pre)
 
 
 # ------------------------------------------------------------------------------------------------

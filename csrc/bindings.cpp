@@ -139,7 +139,10 @@ OptT conv_nt(const Tensor& src, const Tensor& wt, const Tensor& out, const OptT&
 }
 
 // geo = [Nb, Hs, Ws, Cs, OH, OW, R, S, sh, sw, ph, pw, dh, dw, M, Ncol, Kdim, ldy]
-void conv_wgrad(const Tensor& dy, const Tensor& src, const Tensor& dw, const OptT& dbias, std::vector<int64_t> geo) {
+// pre: optional [2 Cs] scale | shift of the training BN + ReLU whose input `src` is (WgradArgs::pre): applied on load
+// by the halo 3x3 weight gradient, else the BN output is materialised here first (bigdl_bn_apply)
+void conv_wgrad(const Tensor& dy, const Tensor& src, const Tensor& dw, const OptT& dbias, std::vector<int64_t> geo,
+                const OptT& pre) {
   TORCH_CHECK(geo.size() == 18, "conv_wgrad: bad geometry");
   WgradArgs a;
   a.dy = cbf(dy, "dy"); a.src = cbf(src, "src"); a.dw = mf(dw, "dw"); a.dbias = omf(dbias, "dbias");
@@ -148,6 +151,24 @@ void conv_wgrad(const Tensor& dy, const Tensor& src, const Tensor& dw, const Opt
   a.m_per_split = 0;
   a.ws = nullptr;
   a.splits = 0;
+  a.pre = ocf(pre, "pre");
+  Tensor det_ws;
+  a.det_ws = nullptr;
+  if (bigdl_deterministic() && a.dbias) {
+    det_ws = at::empty({(int64_t)BIGDL_DET_SLOTS * a.Ncol}, dw.options().dtype(at::kFloat));
+    a.det_ws = det_ws.data_ptr<float>();
+  }
+  Tensor mat;
+  if (a.pre) {
+    TORCH_CHECK(pre->numel() >= 2 * a.Cs && src.numel() % a.Cs == 0, "conv_wgrad: pre must hold 2 x Cs floats");
+    if (!bigdl_wgrad_pre_applies(&a)) {
+      mat = at::empty_like(src);
+      bigdl_bn_apply(a.src, a.pre, a.pre + a.Cs, nullptr, (uint16_t*)mat.data_ptr(), src.numel() / a.Cs, a.Cs, 1,
+                     stream(), nullptr);
+      a.src = (const uint16_t*)mat.data_ptr();
+      a.pre = nullptr;
+    }
+  }
   TORCH_CHECK(dw.numel() >= (int64_t)a.Ncol * a.Kdim, "conv_wgrad: dw too small");
   TORCH_CHECK(a.M == a.Nb * a.OH * a.OW, "conv_wgrad: M mismatch");
   TORCH_CHECK(dy.numel() >= (int64_t)(a.M - 1) * a.ldy + a.Ncol, "conv_wgrad: dy too small");
@@ -529,7 +550,11 @@ void optim_step(int64_t method, const Tensor& x, const Tensor& g, const Tensor& 
   TORCH_CHECK(bigdl_optim_step((int)method, &hp, mf(x, "x"), cf(g, "g"), mf(s1, "s1"), omf(s2, "s2"),
                                ombf(w16, "w16"), x.numel(), stream()) == 0, "optim_step: unknown method");
 }
-void sumsq(const Tensor& x, const Tensor& out) { bigdl_sumsq(cf(x, "x"), mf(out, "out"), x.numel(), stream()); }
+void sumsq(const Tensor& x, const Tensor& out) {
+  Tensor ws;      // deterministic mode: per-call slot workspace (re-entrant across streams)
+  if (bigdl_deterministic()) ws = at::empty({BIGDL_DET_SLOTS}, out.options().dtype(at::kFloat));
+  bigdl_sumsq(cf(x, "x"), mf(out, "out"), x.numel(), stream(), ws.defined() ? ws.data_ptr<float>() : nullptr);
+}
 void scale_f32(const Tensor& x, const OptT& sdev, double s) {
   bigdl_scale_f32(mf(x, "x"), x.numel(), ocf(sdev, "scale"), (float)s, stream());
 }
@@ -1290,7 +1315,10 @@ void gconv(int64_t pass, const Tensor& x_or_dx, const Tensor& w_or_dw, const Opt
 void colsum_bf16(const Tensor& x, const Tensor& out) {
   TORCH_CHECK(x.dim() == 2 && x.is_contiguous() && x.size(1) % 8 == 0, "colsum_bf16: x must be [P, K] contiguous, K % 8 == 0");
   TORCH_CHECK(out.is_contiguous() && out.numel() == x.size(1), "colsum_bf16: out must hold K floats");
-  bigdl_colsum_bf16(cbf(x, "x"), mf(out, "out"), x.size(0), (int)x.size(1), stream());
+  Tensor ws;
+  if (bigdl_deterministic()) ws = at::empty({(int64_t)BIGDL_DET_SLOTS * x.size(1)}, out.options().dtype(at::kFloat));
+  bigdl_colsum_bf16(cbf(x, "x"), mf(out, "out"), x.size(0), (int)x.size(1), stream(),
+                    ws.defined() ? ws.data_ptr<float>() : nullptr);
 }
 int64_t rows_of(const OptT& t, int64_t B, int64_t cols, const char* name) {
   if (!(t && t->defined())) return 0;
@@ -1344,7 +1372,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("bn_z") = py::none(), py::arg("bn_mean") = py::none(), py::arg("bn_aff") = py::none(),
         py::arg("bn_red") = py::none(), py::arg("accumulate") = false, py::arg("bn_zm") = py::none(),
         py::arg("addend_zm") = py::none(), py::arg("pre") = py::none());
-  m.def("conv_wgrad", &conv_wgrad);
+  m.def("conv_wgrad", &conv_wgrad, py::arg("dy"), py::arg("src"), py::arg("dw"), py::arg("dbias"), py::arg("geo"),
+        py::arg("pre") = py::none());
   m.def("transpose_krsc", &transpose_krsc);
   m.def("bn_stats", &bn_stats);
   m.def("bn_finalize", &bn_finalize);

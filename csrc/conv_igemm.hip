@@ -1761,9 +1761,9 @@ __global__ __launch_bounds__(512, 1) void conv_nt_w8_kernel(ConvArgs a) {
 // tail past Kdim loads zeros.
 // BM = 256 (BIGDL_CONV_G4=6/7): 2 x 2 waves of 128 x 64, 32 MFMAs per wave between barriers instead of 16, 24 KB
 // stages, 2 workgroups per CU.
-// ABN = 1: timing ablation only (wrong outputs) — a per-channel scale / shift + ReLU applied to every A fragment after
-// its LDS read, coefficients loaded per K-step (what folding a BN apply into the consumer's operand would cost).
-__device__ float g_abn_tab[2 * 4096];
+// ABN = 1: timing ablation (BIGDL_G4_ABN=1 with ConvArgs::pre set; padding taps are not masked, so only 1x1 outputs
+// are right) — the BN scale / shift + ReLU applied to every A fragment after its LDS read, coefficients loaded per
+// K-step (what folding a BN apply into this tile's operand costs; round 4: +1.15 ms on the forward convs).
 template <int BN, int NS, bool FASTK = true, int BM = 128, int ABN = 0>
 // NS = 2 (short-K variant, BIGDL_CONV_SHORTK): Kdim <= 64, both K-steps issued up front, 32 KB of stages and four
 // workgroups per CU for these one-DMA-round, epilogue-heavy tiles (the caller guarantees nk <= 2).
@@ -1894,10 +1894,10 @@ __global__ __launch_bounds__(256, NS == 2 ? 4 : ((NS == 3 && BM == 128) ? 3 : 2)
 #pragma unroll
     for (int i = 0; i < MI; ++i) fa[i] = *reinterpret_cast<const v8s*>(A + (wm * TM + i * 16) * BKS + foff);
     if constexpr (ABN) {
-      const int c0 = ((kt * BKS) % a.Cs + 8 * (lane >> 4)) & 4095;
-      const v4f s0 = *reinterpret_cast<const v4f*>(g_abn_tab + c0), s1 = *reinterpret_cast<const v4f*>(g_abn_tab + c0 + 4);
-      const v4f t0 = *reinterpret_cast<const v4f*>(g_abn_tab + 4096 + c0), t1 = *reinterpret_cast<const v4f*>(g_abn_tab + 4096 + c0 + 4);
-      const float sc[8] = {s0[0] + 1.f, s0[1] + 1.f, s0[2] + 1.f, s0[3] + 1.f, s1[0] + 1.f, s1[1] + 1.f, s1[2] + 1.f, s1[3] + 1.f};
+      const int c0 = (kt * BKS) % a.Cs + 8 * (lane >> 4);
+      const v4f s0 = *reinterpret_cast<const v4f*>(a.pre + c0), s1 = *reinterpret_cast<const v4f*>(a.pre + c0 + 4);
+      const v4f t0 = *reinterpret_cast<const v4f*>(a.pre + a.Cs + c0), t1 = *reinterpret_cast<const v4f*>(a.pre + a.Cs + c0 + 4);
+      const float sc[8] = {s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
       const float sh[8] = {t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]};
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
@@ -2255,7 +2255,7 @@ __global__ __launch_bounds__(512, 2) void conv_nt_p8_kernel(ConvArgs a) {
 // Semantics are nt_epilogue_lds's (bias + addend added in fp32 before rounding, ReLU, BN statistics of the rounded
 // output, consumer-BN reduction of the rounded gradient with the z / affine ReLU mask).
 template <int K, int CG, int BMW, bool F32T, bool EXT, bool PRE = false>
-__global__ __launch_bounds__(256, 2) void conv_nt_s1_kernel(ConvArgs a) {
+__global__ __launch_bounds__(256, K >= 256 ? 1 : 2) void conv_nt_s1_kernel(ConvArgs a) {
   constexpr int KF = K / 32, MI = BMW / 16, PGN = 4 / CG, BM = BMW * PGN;
   constexpr int GPR = F32T ? 16 : 8;               // 16-byte granules per 64-channel row of the LDS slice
   constexpr int NR = BMW / 8;                      // row-phase passes (8 pixels x 8 lanes each)
@@ -2735,7 +2735,8 @@ template <int BN, int NS, int BM = 128>
 void launch_nt_g4(const ConvArgs& a, hipStream_t st) {
   const int nwg = ((a.M + BM - 1) / BM) * ((a.Ncol + BN - 1) / BN);
   static const int abn = [] { const char* e = getenv("BIGDL_G4_ABN"); return e ? atoi(e) : 0; }();
-  if (abn && BM == 128 && NS == 3 && a.Cs % 32 == 0) conv_nt_g4_kernel<BN, NS, true, BM, 1><<<dim3(nwg), dim3(256), 0, st>>>(a);
+  if (abn && a.pre && BM == 128 && NS == 3 && a.Cs % 32 == 0)
+    conv_nt_g4_kernel<BN, NS, true, BM, 1><<<dim3(nwg), dim3(256), 0, st>>>(a);
   else if (a.Cs % 32 == 0) conv_nt_g4_kernel<BN, NS, true, BM><<<dim3(nwg), dim3(256), 0, st>>>(a);
   else conv_nt_g4_kernel<BN, NS, false, BM><<<dim3(nwg), dim3(256), 0, st>>>(a);
 }
@@ -2772,22 +2773,27 @@ static bool conv_shortk() {
   return g_conv_shortk != 0;
 }
 
-// BIGDL_CONV_S1 (default 1): the streaming 1x1 kernel (conv_nt_s1_kernel) wherever it applies; 0 = off (A/B)
+// BIGDL_CONV_S1 (default 2): the streaming 1x1 kernel (conv_nt_s1_kernel) wherever it applies, Kdim 64 / 128 / 256;
+// 1 = Kdim 64 / 128 only (round 5; the 256-deep form runs one workgroup per CU with 128 weight VGPRs per wave:
+// ResNet-50 22.62 -> 22.31 ms/step interleaved A/B, profiles/r6_iteration_log.txt); 0 = off (A/B)
 int g_conv_s1 = -1;
 static bool s1_applies(const ConvArgs* a) {
   if (g_conv_s1 < 0) {
     const char* e = getenv("BIGDL_CONV_S1");
-    g_conv_s1 = e ? atoi(e) : 1;
+    g_conv_s1 = e ? atoi(e) : 2;
   }
   if (!g_conv_s1 || a->out32 || !a->ident_out || a->ntaps != 1 || a->tap_h[0] || a->tap_w[0] || a->tap_k[0]) return false;
   if (a->mul_h != 1 || a->mul_w != 1 || a->Hs != a->OH || a->Ws != a->OW) return false;
-  if ((a->Kdim != 64 && a->Kdim != 128) || a->Cs != a->Kdim || (a->Ncol % 64) || (a->ldo % 8) || (a->ldw % 8)) return false;
+  // BIGDL_CONV_S1 = 2 also takes Kdim 256 (128 VGPRs of weights per wave, 16-pixel wave tiles)
+  if ((a->Kdim != 64 && a->Kdim != 128 && !(a->Kdim == 256 && g_conv_s1 >= 2)) || a->Cs != a->Kdim ||
+      (a->Ncol % 64) || (a->ldo % 8) || (a->ldw % 8))
+    return false;
   // the epilogue operands go through 32-bit buffer offsets (bytes of an [M][ldo] bf16 tensor, below the OOB offset)
   if (((size_t)(a->M - 1) * a->ldo + a->Ncol) * 2 >= 0x7ff00000u) return false;
   // the consumer-BN ReLU mask as a bf16 z tensor (BIGDL_BN_ZMASK=0) is left to the tile kernels
   if (a->bnred && !a->stats && a->bnz && !a->bnzm) return false;
-  // a BN applied on load (ConvArgs::pre) only with the plain epilogue (forwards: statistics, ReLU, no bias / addend)
-  if (a->pre && (a->bias || a->addend || (a->bnred && !a->stats))) return false;
+  // a BN applied on load (ConvArgs::pre) only with the forward epilogues (bias, statistics, ReLU; no addend)
+  if (a->pre && (a->addend || (a->bnred && !a->stats))) return false;
   auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
   return al(a->src) && al(a->wt) && al(a->out) && al(a->addend) && al(a->bnx) && al(a->bnz);
 }
@@ -2803,7 +2809,8 @@ void launch_s1(const ConvArgs& a, hipStream_t st) {
   }
   const int nchb = a.Ncol / (64 * CG);
   const int tiles = (a.M + BMW * (4 / CG) - 1) / (BMW * (4 / CG));
-  int per = std::max(1, (2 * cus) / nchb);
+  constexpr int occ = K >= 256 ? 1 : 2;            // workgroups per CU (K = 256: 128 weight VGPRs per wave)
+  int per = std::max(1, (occ * cus) / nchb);
   per = std::min(per, tiles);
   conv_nt_s1_kernel<K, CG, BMW, F32T, EXT, PRE><<<dim3(per * nchb), dim3(256), 0, st>>>(a);
 }
@@ -2812,12 +2819,21 @@ template <int K, int CG>
 void launch_s1_cg(const ConvArgs& a, hipStream_t st) {
   const bool ext = a.addend != nullptr || (a.bnred != nullptr && a.stats == nullptr);
   const bool f32t = ext || a.bias != nullptr;
+  if constexpr (K == 256) {       // 128 VGPRs of weights per wave: 16-pixel wave tiles in every variant
+    if (a.pre && f32t) launch_s1<K, CG, 16, true, false, true>(a, st);
+    else if (a.pre) launch_s1<K, CG, 16, false, false, true>(a, st);
+    else if (ext) launch_s1<K, CG, 16, true, true>(a, st);
+    else if (f32t) launch_s1<K, CG, 16, true, false>(a, st);
+    else launch_s1<K, CG, 16, false, false>(a, st);
+  } else {
   constexpr int BW = K == 64 ? 64 : 32;            // pixels per wave tile (ubench: 64 / 32 best at K 64 / 128)
   // s1_applies: no bias / addend / BN reduction with pre; 32-pixel waves (the 64-pixel K = 64 tile spilled)
-  if (a.pre) launch_s1<K, CG, 32, false, false, true>(a, st);
+  if (a.pre && f32t) launch_s1<K, CG, BW / 2, true, false, true>(a, st);     // + bias (ResNet convs carry one)
+  else if (a.pre) launch_s1<K, CG, 32, false, false, true>(a, st);
   else if (ext) launch_s1<K, CG, BW / 2, true, true>(a, st);
   else if (f32t) launch_s1<K, CG, BW / 2, true, false>(a, st);
   else launch_s1<K, CG, BW, false, false>(a, st);
+  }
 }
 
 static void launch_s1_any(const ConvArgs& a, hipStream_t st) {
@@ -2826,10 +2842,14 @@ static void launch_s1_any(const ConvArgs& a, hipStream_t st) {
     if (cg == 4) launch_s1_cg<64, 4>(a, st);
     else if (cg == 2) launch_s1_cg<64, 2>(a, st);
     else launch_s1_cg<64, 1>(a, st);
-  } else {
+  } else if (a.Kdim == 128) {
     if (cg == 4) launch_s1_cg<128, 4>(a, st);
     else if (cg == 2) launch_s1_cg<128, 2>(a, st);
     else launch_s1_cg<128, 1>(a, st);
+  } else {
+    if (cg == 4) launch_s1_cg<256, 4>(a, st);
+    else if (cg == 2) launch_s1_cg<256, 2>(a, st);
+    else launch_s1_cg<256, 1>(a, st);
   }
 }
 
@@ -3128,7 +3148,7 @@ int bigdl_conv_wgrad(const WgradArgs* a_in, hipStream_t st) {
     WgradArgs b = *a_in;
     b.dbias = nullptr;
     const int rc = conv_wgrad_impl(&b, st);
-    if (rc == 0) bigdl_colsum_bf16_ld(a_in->dy, a_in->dbias, a_in->M, a_in->Ncol, a_in->ldy, st);
+    if (rc == 0) bigdl_colsum_bf16_ld(a_in->dy, a_in->dbias, a_in->M, a_in->Ncol, a_in->ldy, st, a_in->det_ws);
     return rc;
   }
   return conv_wgrad_impl(a_in, st);
@@ -3136,6 +3156,16 @@ int bigdl_conv_wgrad(const WgradArgs* a_in, hipStream_t st) {
 
 static int conv_wgrad_impl(const WgradArgs* a_in, hipStream_t st) {
   WgradArgs a = *a_in;
+  if (a.pre) {      // a BN applied on load: the halo kernel only (the binding materialises everything else)
+    WgradArgs b = a;
+    const int hs = bigdl_wgrad_halo_plan(&b);
+    if (hs <= 0 || hs != a.splits || (hs > 1 && a.ws == nullptr)) return -6;
+    b.splits = hs;
+    b.ws = hs > 1 ? a.ws : nullptr;
+    const int rc = bigdl_wgrad_halo(&b, st);
+    HIP_LAUNCH_CHECK();
+    return rc;
+  }
   if (a.splits == -1 && a.ws != nullptr && bigdl_stem_wgrad_plan(&a) > 0) {
     const int rc = bigdl_stem_wgrad(&a, st);
     HIP_LAUNCH_CHECK();

@@ -725,20 +725,22 @@ __global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ x,
   if (threadIdx.x == 0) atomicAdd(out, sm[0] + sm[1] + sm[2] + sm[3]);
 }
 
-__device__ float g_sumsq_slots[128];
-__global__ __launch_bounds__(256) void sumsq_det_kernel(const float* __restrict__ x, long n) {
+// the 128 per-block partials go to a caller-provided workspace (a caching-allocator tensor of the launching stream),
+// not a process-global device array: concurrent launches on different streams (the weight-gradient stream, prediction
+// replicas) cannot overwrite each other's slots
+__global__ __launch_bounds__(256) void sumsq_det_kernel(const float* __restrict__ x, long n, float* __restrict__ slots) {
   float acc = 0.f;
   GRID_STRIDE(i, n) { const float v = x[i]; acc += v * v; }
   acc = wave_sum(acc);
   __shared__ float sm[4];
   if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = acc;
   __syncthreads();
-  if (threadIdx.x == 0) g_sumsq_slots[blockIdx.x] = sm[0] + sm[1] + sm[2] + sm[3];
+  if (threadIdx.x == 0) slots[blockIdx.x] = sm[0] + sm[1] + sm[2] + sm[3];
 }
-__global__ void sumsq_det_finish_kernel(float* __restrict__ out) {
+__global__ void sumsq_det_finish_kernel(float* __restrict__ out, const float* __restrict__ slots) {
   if (threadIdx.x == 0) {
     float t = 0.f;
-    for (int s = 0; s < 128; ++s) t += g_sumsq_slots[s];
+    for (int s = 0; s < 128; ++s) t += slots[s];
     out[0] += t;
   }
 }
@@ -829,15 +831,13 @@ int bigdl_deterministic() {
 }
 void bigdl_set_deterministic(int v) { g_det = v ? 1 : 0; }
 
-void bigdl_colsum_bf16(const uint16_t* x, float* out, long P, int K, hipStream_t st) {
-  bigdl_colsum_bf16_ld(x, out, P, K, K, st);
+void bigdl_colsum_bf16(const uint16_t* x, float* out, long P, int K, hipStream_t st, float* det_ws) {
+  bigdl_colsum_bf16_ld(x, out, P, K, K, st, det_ws);
 }
-// Deterministic column sum: row block y writes its partial to its own slot (plain stores, no atomics), then one
-// fixed-order pass adds the slots into out (one writer per column).
-constexpr int DET_SLOTS = 128, DET_MAXK = 8192;
-__device__ float g_colsum_slots[DET_SLOTS * DET_MAXK];
+// Deterministic column sum: row block y writes its partial to its own slot of the caller's workspace ([by][K] fp32;
+// plain stores, no atomics), then one fixed-order pass adds the slots into out (one writer per column).
 __global__ void __launch_bounds__(256) colsum_det_kernel(const bf16_t* __restrict__ x, long P, int K,
-                                                        long rows_per_block, long ld) {
+                                                        long rows_per_block, long ld, float* __restrict__ slots) {
   __shared__ float part[4][64][9];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int c0 = (blockIdx.x * 64 + lane) * 8;
@@ -857,29 +857,30 @@ __global__ void __launch_bounds__(256) colsum_det_kernel(const bf16_t* __restric
   if (wave == 0 && c0 < K) {
 #pragma unroll
     for (int e = 0; e < 8; ++e)
-      g_colsum_slots[(size_t)blockIdx.y * DET_MAXK + c0 + e] =
-          part[0][lane][e] + part[1][lane][e] + part[2][lane][e] + part[3][lane][e];
+      slots[(size_t)blockIdx.y * K + c0 + e] = part[0][lane][e] + part[1][lane][e] + part[2][lane][e] + part[3][lane][e];
   }
 }
-__global__ void __launch_bounds__(256) colsum_det_finish_kernel(float* __restrict__ out, int K, int nslots) {
+__global__ void __launch_bounds__(256) colsum_det_finish_kernel(float* __restrict__ out, int K, int nslots,
+                                                               const float* __restrict__ slots) {
   const int c = blockIdx.x * 256 + threadIdx.x;
   if (c >= K) return;
   float t = 0.f;
-  for (int s = 0; s < nslots; ++s) t += g_colsum_slots[(size_t)s * DET_MAXK + c];
+  for (int s = 0; s < nslots; ++s) t += slots[(size_t)s * K + c];
   out[c] += t;
 }
 
-// out[k] += sum over P rows (row stride ld, ld % 8 == 0) of x[r][k]
-void bigdl_colsum_bf16_ld(const uint16_t* x, float* out, long P, int K, long ld, hipStream_t st) {
+// out[k] += sum over P rows (row stride ld, ld % 8 == 0) of x[r][k]. Deterministic mode: with det_ws (>= BIGDL_DET_SLOTS
+// x K floats) the slotted two-pass form, else one row block (one writer per column, slower).
+void bigdl_colsum_bf16_ld(const uint16_t* x, float* out, long P, int K, long ld, hipStream_t st, float* det_ws) {
   const int bx = (K / 8 + 63) / 64;
   long by = (P + 255) / 256;                   // >= 64 rows per wave, ~2048 blocks at most
-  if (bigdl_deterministic() && K <= DET_MAXK) {
-    if (by > DET_SLOTS) by = DET_SLOTS;
+  if (bigdl_deterministic() && det_ws != nullptr) {
+    if (by > BIGDL_DET_SLOTS) by = BIGDL_DET_SLOTS;
     if (by < 1) by = 1;
     const long rpb = (P + by - 1) / by;
     by = (P + rpb - 1) / rpb;
-    colsum_det_kernel<<<dim3(bx, (unsigned)by), 256, 0, st>>>(x, P, K, rpb, ld);
-    colsum_det_finish_kernel<<<(K + 255) / 256, 256, 0, st>>>(out, K, (int)by);
+    colsum_det_kernel<<<dim3(bx, (unsigned)by), 256, 0, st>>>(x, P, K, rpb, ld, det_ws);
+    colsum_det_finish_kernel<<<(K + 255) / 256, 256, 0, st>>>(out, K, (int)by, det_ws);
     HIP_LAUNCH_CHECK();
     return;
   }
@@ -988,10 +989,14 @@ void bigdl_adam_step(float* w, const float* g, float* m, float* v, uint16_t* w16
   adam_kernel<<<grid_cap(n), 256, 0, st>>>(w, g, m, v, w16, n, lr, beta1, beta2, eps, wd, bc1, bc2);
   HIP_LAUNCH_CHECK();
 }
-void bigdl_sumsq(const float* x, float* out, long n, hipStream_t st) {
+void bigdl_sumsq(const float* x, float* out, long n, hipStream_t st, float* det_ws) {
   if (bigdl_deterministic()) {   // fixed order: per-block partials into slots, then one ordered sum
-    sumsq_det_kernel<<<DET_SLOTS, 256, 0, st>>>(x, n);
-    sumsq_det_finish_kernel<<<1, 64, 0, st>>>(out);
+    if (det_ws != nullptr) {
+      sumsq_det_kernel<<<BIGDL_DET_SLOTS, 256, 0, st>>>(x, n, det_ws);
+      sumsq_det_finish_kernel<<<1, 64, 0, st>>>(out, det_ws);
+    } else {
+      sumsq_kernel<<<1, 256, 0, st>>>(x, out, n);       // one block: one atomic
+    }
     HIP_LAUNCH_CHECK();
     return;
   }

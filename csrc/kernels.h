@@ -79,13 +79,20 @@ struct WgradArgs {
   int m_per_split;
   float* ws;       // split-K partials [splits][Ncol][Kdim] (nullptr: fp32 atomics into dw)
   int splits;
+  float* det_ws;    // deterministic mode with dbias: BIGDL_DET_SLOTS x Ncol floats for the bias column sum
+  // optional [2 Cs] scale | shift: src is the input of a training BN + ReLU, read as relu(src * scale + shift)
+  // (ConvArgs::pre semantics; the halo 3x3 weight gradient only: bigdl_wgrad_pre_applies)
+  const float* pre;
 };
 
 extern "C" {
 void bigdl_fill_bytes(void* ptr, int value, long bytes, hipStream_t st);
 int bigdl_deterministic();
 void bigdl_set_deterministic(int v);
-void bigdl_colsum_bf16_ld(const uint16_t* x, float* out, long P, int K, long ld, hipStream_t st);
+// deterministic-mode partial slots (bigdl_colsum_bf16_ld / bigdl_sumsq workspaces: DET_SLOTS x K / DET_SLOTS floats)
+#define BIGDL_DET_SLOTS 128
+void bigdl_colsum_bf16_ld(const uint16_t* x, float* out, long P, int K, long ld, hipStream_t st,
+                          float* det_ws = nullptr);
 // 1 when bigdl_conv_nt can apply a->pre inside the kernel that takes the GEMM (else the caller materialises the source)
 int bigdl_conv_pre_applies(const ConvArgs* a);
 int bigdl_conv_nt(const ConvArgs* a, hipStream_t st);
@@ -157,7 +164,7 @@ void bigdl_add_bf16(const uint16_t* a, const uint16_t* b, uint16_t* y, long n, h
 void bigdl_nchw_f32_to_nhwc_bf16(const float* x, uint16_t* y, int N, int C, int H, int W, int Cp,
                                  hipStream_t st);
 void bigdl_cast_f32_bf16(const float* x, uint16_t* y, long n, hipStream_t st);
-void bigdl_colsum_bf16(const uint16_t* x, float* out, long P, int K, hipStream_t st);
+void bigdl_colsum_bf16(const uint16_t* x, float* out, long P, int K, hipStream_t st, float* det_ws = nullptr);
 void bigdl_cast_bf16_f32(const uint16_t* x, float* y, long n, hipStream_t st);
 
 // pooling (NHWC bf16)
@@ -192,7 +199,7 @@ void bigdl_sgd_step(float* w, const float* g, float* mom, uint16_t* w16, long n,
                     const float* seg_wd, int nseg, long base, hipStream_t st);
 void bigdl_adam_step(float* w, const float* g, float* m, float* v, uint16_t* w16, long n, float lr,
                      float beta1, float beta2, float eps, float wd, float bc1, float bc2, hipStream_t st);
-void bigdl_sumsq(const float* x, float* out, long n, hipStream_t st);
+void bigdl_sumsq(const float* x, float* out, long n, hipStream_t st, float* det_ws = nullptr);
 void bigdl_scale_f32(float* x, long n, const float* scale_dev, float scale, hipStream_t st);
 
 // LSTM cell pointwise (gates pre-activations -> c, h), fwd & bwd
@@ -254,6 +261,8 @@ int bigdl_lstm_drop_rep_bwd(const float* dy, long dys_g, int ldy, float* dx, lon
 void bigdl_lstm_pack_gate_w(const float* W, const float* b1, const float* b2, int H, int Kin, int Kp, uint16_t* out,
                             uint16_t* outT, hipStream_t st);
 int bigdl_wgrad_halo_plan(WgradArgs* a);
+// 1 when bigdl_conv_wgrad applies a->pre on load (the halo kernel takes the GEMM), else the caller materialises src
+int bigdl_wgrad_pre_applies(const WgradArgs* a);
 int bigdl_wgrad_halo(const WgradArgs* a, hipStream_t st);
 void bigdl_set_i8_s1(int v);
 int bigdl_get_conv_impl();

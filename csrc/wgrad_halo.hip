@@ -97,10 +97,14 @@ __device__ __forceinline__ void vm_wait_stages(int k) {   // wait until <= k sta
   vm_wait<0>();
 }
 
-template <int W, int RB, int KB, int LDSKB>
+// PRE: x is the input of a training BatchNorm + ReLU (WgradArgs::pre): once a stage's DMAs have landed, each lane
+// rewrites the x granules it staged as relu(x * scale + shift) rounded to bf16 (bn_apply_kernel's expression), before
+// the barrier that publishes the stage; granules of pad columns / rows outside the image stay zero. The 64 channels'
+// scale / shift sit in LDS behind the stages.
+template <int W, int RB, int KB, int LDSKB, bool PRE = false>
 __global__ __launch_bounds__(KB * 4, 1) void conv_wgrad_halo_kernel(WgradArgs a) {
   using H = Halo<W, RB, KB, LDSKB>;
-  __shared__ __attribute__((aligned(1024))) unsigned char lds[H::NS * H::STAGE];
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[H::NS * H::STAGE + (PRE ? 512 : 0)];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -152,6 +156,14 @@ __global__ __launch_bounds__(KB * 4, 1) void conv_wgrad_halo_kernel(WgradArgs a)
   const bf16_t* dsrc = reinterpret_cast<const bf16_t*>(a.dy);
   const size_t xend = (size_t)a.Nb * IH * W * C, dend = (size_t)(a.M - 1) * a.ldy + K;
 
+  float* const ptab = reinterpret_cast<float*>(lds + H::NS * H::STAGE);
+  if constexpr (PRE) {                  // [scale 64 | shift 64] of channels c0 .. c0 + 63
+    if (tid < 32) {
+      const int h = tid >> 4, i = tid & 15;
+      reinterpret_cast<v4f*>(ptab)[tid] = reinterpret_cast<const v4f*>(a.pre + h * C + c0)[i];
+    }
+    __syncthreads();
+  }
   // stages are issued in order: walk (image, first row) instead of dividing the stage index each time
   int nx = st0 / spi, ohx = (st0 - nx * spi) * RB;
   auto issue = [&](int buf) {
@@ -227,6 +239,34 @@ __global__ __launch_bounds__(KB * 4, 1) void conv_wgrad_halo_kernel(WgradArgs a)
   for (int i = 0; i < nst; ++i) {
     // stage i landed (this wave's DMAs), then every wave's (barrier); the barrier also retires stage i-1's reads
     vm_wait_stages<H::D, H::NS - 2>(min(H::NS - 2, nst - 1 - i));
+    if constexpr (PRE) {
+      const int sg = st0 + i, oh0 = (sg % spi) * RB;
+      const int v = (oh0 == 0 ? 1 : 0) | (oh0 + RB == IH ? 2 : 0);
+      const unsigned xb = (unsigned)(uintptr_t)(LDS_PTR(unsigned char))lds + (unsigned)((i % H::NS) * H::STAGE);
+#pragma unroll
+      for (int d = 0; d < H::XG; ++d) {
+        const unsigned off = v == 0 ? xv[0][d] : v == 1 ? xv[1][d] : v == 2 ? xv[2][d] : xv[3][d];
+        if (off == OOB) continue;
+        const int slot = (d * H::NW + wave) * 64 + lane;
+        const int g = (slot & 7) ^ hf128(slot >> 3);
+        const unsigned ta = (unsigned)(uintptr_t)(LDS_PTR(float))ptab + (unsigned)(g * 32);
+        const unsigned addr = xb + (unsigned)(slot * 16);
+        v4u u;
+        v4f s0, s1, b0, b1;
+        // inline asm LDS accesses: a plain load here would make the compiler drain every in-flight stage DMA
+        asm volatile("ds_read_b128 %0, %5\n\tds_read_b128 %1, %6 offset:0\n\tds_read_b128 %2, %6 offset:16\n\t"
+                     "ds_read_b128 %3, %6 offset:256\n\tds_read_b128 %4, %6 offset:272\n\ts_waitcnt lgkmcnt(0)"
+                     : "=v"(u), "=v"(s0), "=v"(s1), "=v"(b0), "=v"(b1) : "v"(addr), "v"(ta) : "memory");
+        const float sc[8] = {s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
+        const float sh[8] = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          u[e] = pack2bf(fmaxf(lo_bf(u[e]) * sc[2 * e] + sh[2 * e], 0.f),
+                         fmaxf(hi_bf(u[e]) * sc[2 * e + 1] + sh[2 * e + 1], 0.f));
+        asm volatile("ds_write_b128 %0, %1" ::"v"(addr), "v"(u) : "memory");
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     if (i + H::NS - 1 < nst) issue((i + H::NS - 1) % H::NS);
@@ -341,13 +381,21 @@ template <int W, int RB, int LDSKB>
 void launch_halo(const WgradArgs& a, hipStream_t st) {
   const int ntile = (a.Cs / 64) * (a.Ncol / (a.Ncol % 128 == 0 ? 128 : 64));
   const int spad = (a.splits + 7) / 8 * 8;
-  if (a.Ncol % 128 == 0) conv_wgrad_halo_kernel<W, RB, 128, LDSKB><<<dim3(ntile * spad), dim3(512), 0, st>>>(a);
-  else conv_wgrad_halo_kernel<W, RB, 64, LDSKB><<<dim3(ntile * spad), dim3(256), 0, st>>>(a);
+  if (a.pre) {     // (launch_halo_lds: the 80 KB budget, so the channel table fits behind the stages)
+    if constexpr (LDSKB <= 80) {
+      if (a.Ncol % 128 == 0) conv_wgrad_halo_kernel<W, RB, 128, LDSKB, true><<<dim3(ntile * spad), dim3(512), 0, st>>>(a);
+      else conv_wgrad_halo_kernel<W, RB, 64, LDSKB, true><<<dim3(ntile * spad), dim3(256), 0, st>>>(a);
+    }
+  } else if (a.Ncol % 128 == 0) {
+    conv_wgrad_halo_kernel<W, RB, 128, LDSKB><<<dim3(ntile * spad), dim3(512), 0, st>>>(a);
+  } else {
+    conv_wgrad_halo_kernel<W, RB, 64, LDSKB><<<dim3(ntile * spad), dim3(256), 0, st>>>(a);
+  }
 }
 
 template <int W, int RB>
 void launch_halo_lds(const WgradArgs& a, int lds, hipStream_t st) {
-  if (lds <= 80) launch_halo<W, RB, 80>(a, st);
+  if (lds <= 80 || a.pre) launch_halo<W, RB, 80>(a, st);
   else launch_halo<W, RB, 160>(a, st);
 }
 
@@ -394,6 +442,11 @@ int bigdl_wgrad_halo_plan(WgradArgs* a) {
   splits = (stages + sps - 1) / sps;
   a->m_per_split = (int)sps;
   return (int)splits;
+}
+
+int bigdl_wgrad_pre_applies(const WgradArgs* a) {
+  WgradArgs b = *a;
+  return bigdl_wgrad_halo_plan(&b) > 0 ? 1 : 0;
 }
 
 // Launch (a->splits / m_per_split from bigdl_wgrad_halo_plan; a->ws = [splits][Ncol][Kdim] partials when splits > 1,

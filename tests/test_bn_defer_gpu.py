@@ -64,12 +64,14 @@ def test_halo_pre(case):
 
 
 # N, C, H, K: 1x1 / stride 1 with 64 or 128 input channels (the streaming kernel): ResNet-50 stage 1-2 conv3 shapes
-S1_CASES = [(2, 64, 56, 256), (2, 128, 28, 512), (3, 64, 7, 64), (2, 128, 14, 128)]
+S1_CASES = [(2, 64, 56, 256), (2, 128, 28, 512), (3, 64, 7, 64), (2, 128, 14, 128), (2, 256, 14, 1024),
+            (3, 256, 9, 64)]
 
 
+@pytest.mark.parametrize("bias", [False, True])
 @pytest.mark.parametrize("relu", [False, True])
 @pytest.mark.parametrize("case", S1_CASES)
-def test_s1_pre(case, relu):
+def test_s1_pre(case, relu, bias):
     from bigdl_amd.ops import bn as bnops
     from bigdl_amd.ops import conv as cv
 
@@ -79,16 +81,17 @@ def test_s1_pre(case, relu):
     x = torch.randn(N, C, H, H, device=dev).to(BF, memory_format=CL)
     w = (torch.randn(K, C, 1, 1, device=dev) * (1.0 / C ** 0.5)).to(BF, memory_format=CL)
     aff = _aff(C, dev)
+    b = torch.randn(K, device=dev) if bias else None
     ymat = bnops.materialize(bnops.deferred(x, aff))
     st0, st1 = bnops.new_stats(K, dev), bnops.new_stats(K, dev)
-    y0 = cv.conv2d_fwd(ymat, w, None, (1, 1), (0, 0), relu=relu, stats=st0)
-    y1, mat = cv.conv2d_fwd(x, w, None, (1, 1), (0, 0), relu=relu, stats=st1, pre=aff)
+    y0 = cv.conv2d_fwd(ymat, w, b, (1, 1), (0, 0), relu=relu, stats=st0)
+    y1, mat = cv.conv2d_fwd(x, w, b, (1, 1), (0, 0), relu=relu, stats=st1, pre=aff)
     torch.cuda.synchronize()
     assert mat is None, "the streaming 1x1 kernel should apply the BN on load"
     assert torch.equal(y1, y0)
     # (the two launches may use different grids, so compare the slot sums, not the slots)
     assert _rel(st1.view(bnops.stat_slots(), 2, K).sum(0), st0.view(bnops.stat_slots(), 2, K).sum(0)) < 1e-5
-    yr = F.conv2d(_ref_input(x, aff), w.float())
+    yr = F.conv2d(_ref_input(x, aff), w.float(), b)
     if relu:
         yr = torch.relu(yr)
     assert _rel(y1, yr) < 1e-2
@@ -128,7 +131,7 @@ def test_maxpool_pre():
     torch.cuda.synchronize()
     assert torch.equal(y1, y0) and torch.equal(i1, i0)
     yr = F.max_pool2d(_ref_input(x, aff), 3, 2, 1)
-    assert _rel(y1, yr) < 1e-6
+    assert _rel(y1, yr) < 1e-3      # (torch rounds x * s before + b; the kernels fuse the multiply-add)
 
 
 def _grads(m):
@@ -146,7 +149,7 @@ def test_bottleneck_deferred_matches_materialised(n, H):
     """A ResNet bottleneck with BN1 / BN2 deferred into the 3x3 halo and 1x1 streaming forwards (and re-applied for
     the weight gradients on the side stream) against BIGDL_BN_DEFER off: same output, input and weight gradients."""
     from bigdl_amd.models.resnet import _Builder
-    from bigdl_amd.nn import normalization
+    from bigdl_amd.nn import fusion, normalization
     from bigdl_amd.nn.fusion import fuse_for_training
 
     b = _Builder("B", True)
@@ -160,7 +163,8 @@ def test_bottleneck_deferred_matches_materialised(n, H):
     x = torch.randn(2, 4 * n, H, H).cuda().to(BF).contiguous(memory_format=CL)
     gy = torch.randn(2, 4 * n, H, H).cuda().to(BF).contiguous(memory_format=CL)
     res = {}
-    saved = normalization._DEFER[0]
+    saved, saved_lvl = normalization._DEFER[0], fusion.DEFER_LEVEL[0]
+    fusion.DEFER_LEVEL[0] = 2          # 3x3 consumers too
     try:
         for on in (True, False):
             normalization._DEFER[0] = on
@@ -171,12 +175,39 @@ def test_bottleneck_deferred_matches_materialised(n, H):
             convs = [l for l in branch.modules if type(l).__name__.endswith("Convolution")]
             if on:
                 assert getattr(branch.modules[2].output, "_bn_pre", None) is not None
-                assert convs[1]._x16_pre is not None and convs[2]._x16_pre is not None, "applied on load"
+                assert convs[1]._x16_pre is not None, "applied on load"
             g = m.backward(x, gy).float().clone()
             torch.cuda.synchronize()
             res[on] = (y, g, _grads(m))
     finally:
-        normalization._DEFER[0] = saved
+        normalization._DEFER[0], fusion.DEFER_LEVEL[0] = saved, saved_lvl
     assert _rel(res[True][0], res[False][0]) < 1e-3
     assert _rel(res[True][1], res[False][1]) < 1e-2
     assert _rel(res[True][2], res[False][2]) < 1e-2
+
+
+@pytest.mark.parametrize("case", HALO_CASES)
+def test_wgrad_halo_pre(case):
+    """The halo 3x3 weight gradient applying a deferred BN + ReLU to its x tiles: bit-equal to the same kernel on the
+    materialised input (fixed-order split reduce), and vs fp32 torch (conv2d_weight) and the bias column sums."""
+    from bigdl_amd.ops import bn as bnops
+    from bigdl_amd.ops import conv as cv
+
+    N, C, H, K = case
+    dev = torch.device("cuda:0")
+    torch.manual_seed(17)
+    x = torch.randn(N, C, H, H, device=dev).to(BF, memory_format=CL)
+    gy = torch.randn(N, K, H, H, device=dev).to(BF, memory_format=CL)
+    aff = _aff(C, dev)
+    ymat = bnops.materialize(bnops.deferred(x, aff))
+    dws = []
+    for src, pre in ((ymat, None), (x, aff)):
+        dw = torch.zeros(K, C, 3, 3, device=dev).contiguous(memory_format=CL)
+        db = torch.zeros(K, device=dev)
+        cv.conv2d_wgrad(gy, src, dw, db, (1, 1), (1, 1), pre=pre)
+        dws.append((dw, db))
+    torch.cuda.synchronize()
+    assert torch.equal(dws[1][0], dws[0][0]) and torch.equal(dws[1][1], dws[0][1])
+    ref = torch.nn.grad.conv2d_weight(_ref_input(x, aff), (K, C, 3, 3), gy.float(), padding=1)
+    assert _rel(dws[1][0], ref) < 1e-2
+    assert _rel(dws[1][1], gy.float().sum(dim=(0, 2, 3))) < 1e-3

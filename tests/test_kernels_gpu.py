@@ -884,6 +884,9 @@ S1_CASES = [
     (3, 128, 11, 192),     # Ncol 192: three one-group channel blocks, M tail
     (4, 192, 9, 128),      # dgrad 128 -> 192
     (7, 128, 10, 128),     # two channel groups both ways
+    (8, 256, 14, 1024),    # fwd K 256 -> 1024 (layer 13 shape: one workgroup per CU, 128 weight VGPRs per wave)
+    (6, 1024, 14, 256),    # dgrad 256 -> 1024 with addend + consumer-BN reduction (layer 15 data gradient)
+    (5, 256, 13, 64),      # fwd K 256 -> 64 with an M tail; dgrad 64 -> 256
 ]
 
 
@@ -907,7 +910,7 @@ def test_conv_s1_stream_kernel(case, zmask):
     b32 = torch.randn(K, device=dev)
     yr0 = F.conv2d(x.float(), w.float())
     res = {}
-    for s1 in (1, 0):
+    for s1 in (2, 0):
         C_.set_conv_s1(s1)
         try:
             stats = bnops.new_stats(K, dev)
@@ -929,15 +932,15 @@ def test_conv_s1_stream_kernel(case, zmask):
             torch.cuda.synchronize()
             res[s1] = (y, stats, y2, dx, red, bool(bn.get("done")))
         finally:
-            C_.set_conv_s1(1)
-    y, stats, y2, dx, red, done = res[1]
+            C_.set_conv_s1(2)
+    y, stats, y2, dx, red, done = res[2]
     assert _rel(y, yr0) < 1e-2
     st2 = stats.view(bnops.stat_slots(), 2, K).sum(0)
     assert _rel(st2[0], y.float().sum(dim=(0, 2, 3))) < 1e-4
     assert _rel(st2[1], (y.float() ** 2).sum(dim=(0, 2, 3))) < 1e-4
     assert _rel(y2, torch.relu(yr0 + b32.view(1, K, 1, 1))) < 1e-2
     assert torch.equal(y, res[0][0])                   # same fp32 sums, same rounding
-    gy = res[1][3]  # placeholder to keep names short below
+    gy = res[2][3]  # placeholder to keep names short below
     gyr = (torch.randn(N, K, H, H, device=dev, generator=torch.Generator(dev).manual_seed(3))).to(BF).float()
     addr = torch.randn(N, C, H, H, device=dev, generator=torch.Generator(dev).manual_seed(4)).to(BF).float()
     dxr = torch.nn.grad.conv2d_input(x.shape, w.float(), gyr) + addr

@@ -61,30 +61,46 @@ def test_inception_v1_backward_runs():
 
 
 def test_fusion_plans_deferred_bn():
-    """nn.fusion defers the apply pass of every BN + ReLU whose only reader is a conv or the stem max pool (ResNet-50:
-    BN1 / BN2 of the 16 bottlenecks and the stem BN); residual BNs (BN3) and shortcut BNs keep theirs."""
+    """nn.fusion defers the apply pass of every BN + ReLU whose only reader is a 3x3 / stride-1 conv or the stem max
+    pool (ResNet-50: BN1 of the 13 bottlenecks whose 3x3 has stride 1, and the stem BN); the others keep theirs."""
     from bigdl_amd import nn
     from bigdl_amd.models.resnet import DatasetType, ResNet
     from bigdl_amd.nn.fusion import fuse_for_training, unfuse
 
+    from bigdl_amd.nn import fusion
+
     m = ResNet(1000, 50, dataSet=DatasetType.ImageNet)
     fuse_for_training(m)
     bns = [l for l in m.flattened_layers() if isinstance(l, nn.BatchNormalization)]
+    assert len(bns) == 53 and sum(1 for l in bns if getattr(l, "_defer_ok", False)) == 1    # default: the stem BN
+    saved = fusion.DEFER_LEVEL[0]
+    fusion.DEFER_LEVEL[0] = 2
+    try:
+        fuse_for_training(m)
+    finally:
+        fusion.DEFER_LEVEL[0] = saved
     deferred = [l for l in bns if getattr(l, "_defer_ok", False)]
-    assert len(bns) == 53 and len(deferred) == 33
+    assert len(deferred) == 14
     assert all(l.fuse_relu for l in deferred)
     unfuse(m)
     assert not any(getattr(l, "_defer_ok", False) for l in bns)
 
 
 def test_graph_fusion_plans_deferred_bn():
-    """The same deferral decided on a Graph's edges (ResNetGraph): 33 of the 53 BNs."""
+    """The same deferral decided on a Graph's edges (ResNetGraph): 14 of the 53 BNs."""
     from bigdl_amd import nn
     from bigdl_amd.models.resnet import DatasetType, ResNetGraph
     from bigdl_amd.nn.fusion import fuse_for_training
 
+    from bigdl_amd.nn import fusion
+
     g = ResNetGraph(1000, 50, dataSet=DatasetType.ImageNet)
-    fuse_for_training(g)
+    saved = fusion.DEFER_LEVEL[0]
+    fusion.DEFER_LEVEL[0] = 2
+    try:
+        fuse_for_training(g)
+    finally:
+        fusion.DEFER_LEVEL[0] = saved
     bns = [l for l in g.flattened_layers() if isinstance(l, nn.BatchNormalization)]
     assert len(bns) == 53
-    assert sum(1 for l in bns if getattr(l, "_defer_ok", False)) == 33
+    assert sum(1 for l in bns if getattr(l, "_defer_ok", False)) == 14
