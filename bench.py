@@ -300,6 +300,18 @@ def main():
     dt = float(t.item())
     loss = float(step.loss.item()) if step.loss is not None else float("nan")
     step.flush()
+    # device-timed phases (optim/phase_timer.py) of the eager steps (a HIP-graph replay records none: then they come
+    # from the eager warm-up steps); the exposed collective wait is the max over ranks
+    phase = step.phase.summary(last=args.steps) if step.phase is not None else None
+    comm_exposed = None
+    if phase is not None:
+        ce = torch.tensor([phase["comm_exposed_ms"]], device=dev)
+        if world > 1:
+            import torch.distributed as dist
+
+            dist.all_reduce(ce, op=dist.ReduceOp.MAX)
+        comm_exposed = round(float(ce.item()), 3)
+        phase["source"] = "eager warm-up steps" if graph is not None else "timed steps"
     ms = dt / args.steps * 1e3
     ips = B * world * args.steps / dt
     if rank == 0:
@@ -314,6 +326,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": (round(ips / BASELINE, 4) if BASELINE else None),
+            "comm_exposed_ms": comm_exposed if step.comm.active else None,
             "dtype": "bf16",
             "data": "synthetic (random 3x224x224 images, random labels; random-init weights)",
             "config": {"model": f"ResNet-{args.depth} v1.5 (BigDL ImageNet builder{', Graph form' if args.graph_model else ''})", "global_batch": B * world,
@@ -323,7 +336,8 @@ def main():
                            if step.comm.active else " (one rank: no gradient exchange)"),
                        "hip_graph": graph is not None, "graph_vs_eager": decision,
                        "wgrad_side_stream": side_stream.enabled(), "bucketed_overlap": step.bucketed is not None,
-                       "grad_compress": step.comm.wire_format, "final_loss": round(loss, 4)},
+                       "grad_compress": step.comm.wire_format, "final_loss": round(loss, 4),
+                       "phase_ms": phase},
         }), flush=True)
     Engine.shutdown()
 

@@ -14,6 +14,7 @@ MFMA-friendly NHWC physical layout) and the hot layers dispatch to the gfx950 HI
 """
 import copy
 import itertools
+import os
 import time
 
 import torch
@@ -293,6 +294,51 @@ class MklInt8Convertible:
         return self
 
 
+# Module timing (reference AbstractModule.scala:168-196 getTimes: forward / backward time per module, nanoseconds).
+# Host timing around an asynchronous GPU launch measures only the enqueue, so with device timing on
+# (``AbstractModule.setDeviceTiming(True)``, ``bigdl.module.deviceTiming`` or BIGDL_DEVICE_TIMES=1) a GPU call records
+# a pair of HIP timing events on the current stream instead, and getTimes() resolves the pending pairs into device
+# nanoseconds (elapsed time between the events: the module's own kernels plus whatever else that stream ran in
+# between; work the module forks onto the weight-gradient side stream is not included). Inside a HIP-graph capture
+# no events are recorded (the host time is kept).
+DEVICE_TIMING = [os.environ.get("BIGDL_DEVICE_TIMES", "0") not in ("0", "")]
+
+
+def _on_cuda(x):
+    if isinstance(x, torch.Tensor):
+        return x.is_cuda
+    if isinstance(x, (list, tuple)):
+        return any(_on_cuda(v) for v in x)
+    if hasattr(x, "values") and callable(x.values):
+        try:
+            return any(_on_cuda(v) for v in x.values())
+        except Exception:
+            return False
+    return False
+
+
+def _t_begin(x):
+    """Start token of a timed module call: a recorded HIP event (device timing on, GPU input, not capturing) or the
+    host clock."""
+    if DEVICE_TIMING[0] and _on_cuda(x) and not torch.cuda.is_current_stream_capturing():
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        return ev
+    return time.perf_counter_ns()
+
+
+def _t_end(m, tok, attr):
+    """Close a timed call started by _t_begin: host time is added to ``attr`` now, an event pair is queued on the module
+    and resolved by getTimes()."""
+    if isinstance(tok, int):
+        setattr(m, attr, getattr(m, attr) + time.perf_counter_ns() - tok)
+        return
+    end = torch.cuda.Event(enable_timing=True)
+    end.record()
+    pend = m.__dict__.setdefault("_dev_times", [])
+    pend.append((attr, tok, end))
+
+
 class AbstractModule(MklInt8Convertible, metaclass=_RecordInit):
     """Base of every layer and container."""
 
@@ -346,7 +392,7 @@ class AbstractModule(MklInt8Convertible, metaclass=_RecordInit):
 
     # ------------------------------------------------------------------ forward / backward
     def forward(self, input):
-        t0 = time.perf_counter_ns()
+        t0 = _t_begin(input)
         if getattr(input, "_is_bigdl_tensor", False):     # bigdl_amd.tensor.Tensor -> its torch tensor
             input = input._t
         try:
@@ -359,11 +405,11 @@ class AbstractModule(MklInt8Convertible, metaclass=_RecordInit):
                 except Exception:
                     pass
             raise
-        self.forward_time += time.perf_counter_ns() - t0
+        _t_end(self, t0, "forward_time")
         return self.output
 
     def backward(self, input, gradOutput):
-        t0 = time.perf_counter_ns()
+        t0 = _t_begin(gradOutput)
         if getattr(input, "_is_bigdl_tensor", False):
             input = input._t
         if getattr(gradOutput, "_is_bigdl_tensor", False):
@@ -372,7 +418,7 @@ class AbstractModule(MklInt8Convertible, metaclass=_RecordInit):
         if not self._frozen:
             self.accGradParameters(input, gradOutput)
             self._apply_regularizers()
-        self.backward_time += time.perf_counter_ns() - t0
+        _t_end(self, t0, "backward_time")
         return self.gradInput
 
     def __call__(self, *nodes):
@@ -576,7 +622,22 @@ class AbstractModule(MklInt8Convertible, metaclass=_RecordInit):
         return self.scaleB
 
     # ------------------------------------------------------------------ timing
+    @staticmethod
+    def setDeviceTiming(on=True):
+        """GPU modules report device time (HIP events) in getTimes instead of host enqueue time."""
+        DEVICE_TIMING[0] = bool(on)
+
+    def _resolve_times(self):
+        pend = self.__dict__.get("_dev_times")
+        if not pend:
+            return
+        for attr, a, b in pend:
+            b.synchronize()
+            setattr(self, attr, getattr(self, attr) + int(a.elapsed_time(b) * 1e6))
+        pend.clear()
+
     def getTimes(self):
+        self._resolve_times()
         return [(self, self.forward_time, self.backward_time)]
 
     def getTimesGroupByModuleType(self):
@@ -588,6 +649,7 @@ class AbstractModule(MklInt8Convertible, metaclass=_RecordInit):
         return [(k, f, b) for k, (f, b) in agg.items()]
 
     def resetTimes(self):
+        self.__dict__.pop("_dev_times", None)
         self.forward_time = 0
         self.backward_time = 0
 

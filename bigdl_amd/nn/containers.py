@@ -8,7 +8,7 @@ import copy
 import torch
 
 from ..utils.table import Table
-from .abstractnn import AbstractModule, activity_apply
+from .abstractnn import AbstractModule, _t_begin, _t_end, activity_apply
 
 
 def add_activity(a, b):
@@ -138,6 +138,7 @@ class Container(AbstractModule):
         return self
 
     def getTimes(self):
+        self._resolve_times()
         out = [(self, self.forward_time, self.backward_time)]
         for m in self.modules:
             out.extend(m.getTimes())
@@ -177,21 +178,19 @@ class Sequential(Container):
         return x
 
     def backward(self, input, gradOutput):
-        import time
-
-        t0 = time.perf_counter_ns()
+        t0 = _t_begin(gradOutput)
         if self._residual_plan is not None:
             from .fusion import residual_backward
 
             self.gradInput = residual_backward(self, input, gradOutput)
-            self.backward_time += time.perf_counter_ns() - t0
+            _t_end(self, t0, "backward_time")
             return self.gradInput
         g = gradOutput
         for i in range(len(self.modules) - 1, -1, -1):
             inp = self.modules[i - 1].output if i > 0 else input
             g = self.modules[i].backward(inp, g)
         self.gradInput = g
-        self.backward_time += time.perf_counter_ns() - t0
+        _t_end(self, t0, "backward_time")
         return g
 
     def updateGradInput(self, input, gradOutput):

@@ -22,7 +22,7 @@ from ..ops import bn as bnops
 from ..ops import conv as cv
 from ..ops import conv_fn
 from ..ops import side_stream
-from .abstractnn import AutogradModule, TensorModule
+from .abstractnn import AutogradModule, TensorModule, _t_begin, _t_end
 from .init_methods import RandomUniform, Zeros
 
 CL = torch.channels_last
@@ -370,9 +370,7 @@ class SpatialConvolution(TensorModule):
         side = None if self._frozen else side_stream.stream_for(gradOutput)
         if side is None:
             return super().backward(input, gradOutput)
-        import time
-
-        t0 = time.perf_counter_ns()
+        t0 = _t_begin(gradOutput)
         self.gradInput = self.updateGradInput(input, gradOutput)
         # weight gradient on the side stream, concurrent with the data-gradient chain (ops/side_stream.py)
         side_stream.begin(side)
@@ -381,7 +379,7 @@ class SpatialConvolution(TensorModule):
             self._apply_regularizers()
         side_stream.keep(side, input, gradOutput, self.output, getattr(self, "_x16", None),
                          *(getattr(self, "_xpair", None) or (None,))[:1])
-        self.backward_time += time.perf_counter_ns() - t0
+        _t_end(self, t0, "backward_time")
         return self.gradInput
 
     def accGradParameters(self, input, gradOutput):

@@ -7,12 +7,11 @@ Build with ``node = Layer(...).inputs(prev_node, ...)`` (or ``Layer(...)(prev)``
 predecessors receives a 1-based Table of their outputs in edge order. Execution follows a topological
 order computed once; backward walks it in reverse, summing gradients at fan-out nodes.
 """
-import time
 
 import torch
 
 from ..utils.table import Table
-from .abstractnn import AbstractModule
+from .abstractnn import AbstractModule, _t_begin, _t_end
 from .activation import Identity
 from .containers import Container, add_activity
 
@@ -246,9 +245,9 @@ class Graph(Container):
         return True
 
     def backward(self, input, gradOutput):
-        t0 = time.perf_counter_ns()
+        t0 = _t_begin(gradOutput)
         self.gradInput = self._run_backward(input, gradOutput, True, True)
-        self.backward_time += time.perf_counter_ns() - t0
+        _t_end(self, t0, "backward_time")
         return self.gradInput
 
     def updateGradInput(self, input, gradOutput):

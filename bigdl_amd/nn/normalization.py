@@ -18,7 +18,7 @@ import torch.nn.functional as F
 
 from .. import ops
 from ..ops import bn as bnops
-from .abstractnn import AutogradModule, TensorModule
+from .abstractnn import AutogradModule, TensorModule, _t_begin, _t_end
 from .init_methods import Ones, RandomUniform, Zeros
 
 _ZMASK = os.environ.get("BIGDL_BN_ZMASK", "1") != "0"
@@ -190,9 +190,7 @@ class BatchNormalization(TensorModule):
         return self._from_nchw(dx), dres
 
     def backward(self, input, gradOutput):
-        import time
-
-        t0 = time.perf_counter_ns()
+        t0 = _t_begin(gradOutput)
         x = self._to_nchw(input)
         if self._gpu_ok(x):
             self.gradInput, _ = self.backward_fused(input, gradOutput)
@@ -200,7 +198,7 @@ class BatchNormalization(TensorModule):
             self.gradInput = self.updateGradInput(input, gradOutput)
             if not self._frozen:
                 self.accGradParameters(input, gradOutput)
-        self.backward_time += time.perf_counter_ns() - t0
+        _t_end(self, t0, "backward_time")
         return self.gradInput
 
     def _cpu_grads(self, gradOutput):

@@ -453,6 +453,12 @@ class Optimizer:
                     timing["host_ms"] = (time.perf_counter() - timing["h0"]) * 1e3
             if finished is None or finished:
                 step.throttle()      # the host stays at most TrainStep.MAX_INFLIGHT iterations ahead of the device
+                # device-timed phases of the iterations the device finished meanwhile (optim/phase_timer.py)
+                from .phase_timer import METRIC_NAMES
+
+                for ph in getattr(step, "phase_done", None) or ():
+                    for k, name in METRIC_NAMES.items():
+                        self.metrics.add(name, ph[k] / 1e3)
             # (a dropped rank skips it: its backlog must not hold the host, the pacer bounds it next iteration)
             self.metrics.add("computing time", time.perf_counter() - t1)
             records = batch.size() * world

@@ -9,10 +9,6 @@ On MI355X the "pool of clones" is a pool of replicas that share one copy of the 
 HIP stream, so concurrent requests overlap on the device. ``predict(bytes)`` uses a small self-describing tensor wire format
 (JSON header + raw little-endian payload) instead of the reference's protobuf Activity message.
 """
-import io
-import json
-import struct
-
 import torch
 
 from ..dataset.core import AbstractDataSet, DataSet, MiniBatch, Sample, SampleToMiniBatch, samples_to_minibatch
@@ -151,55 +147,97 @@ LocalPredictor = Predictor
 
 
 # ------------------------------------------------------------------------------------- wire format
+# The reference's bytes protocol (S/optim/PredictionService.scala:178-280): an activity is one protobuf ``AttrValue``
+# of bigdl.proto (utils/bigdl_proto.py schema) —
+#   Tensor              -> AttrValue{dataType: TENSOR, tensorValue: BigDLTensor with its TensorStorage inline}
+#   Table(key, Tensor)  -> AttrValue{dataType: ARRAY_VALUE, arrayValue{datatype: TENSOR, tensor: [isKeyPrimitive (BOOL
+#                          scalar), keys..., values...]}}, a primitive key as a scalar tensor of its type
+# and a failure comes back as a STRING scalar tensor ("Exception caught during [stage]! ..."), which decodes to a str.
+def _bigdl_tensor(x):
+    """BigDLTensor dict (storage included) of a torch tensor, or of a str / Python scalar key (a scalar tensor)."""
+    from ..utils import bigdl_proto as bp
+
+    if isinstance(x, str):
+        return {"datatype": ["STRING"], "size": [], "stride": [], "offset": [1], "dimension": [0], "nElements": [1],
+                "isScalar": [True], "storage": [{"datatype": ["STRING"], "string_data": [x], "id": [1]}], "id": [1],
+                "tensorType": ["DENSE"]}
+    if isinstance(x, bool):
+        x = torch.tensor(x)
+    elif isinstance(x, int):
+        x = torch.tensor(x, dtype=torch.int32 if -(1 << 31) <= x < (1 << 31) else torch.int64)
+    elif isinstance(x, float):
+        x = torch.tensor(x, dtype=torch.float32)
+    if not isinstance(x, torch.Tensor):
+        raise TypeError(f"PredictionService: unsupported activity element {type(x).__name__}")
+    x = x.detach().cpu()
+    if x.dtype in (torch.uint8, torch.int8):
+        x = x.to(torch.int32)
+    ctx = bp._SerCtx()
+    tid = _one_id(bp._tensor_attr(x, ctx))
+    return ctx.storages[tid]
+
+
+def _one_id(d):
+    return d["id"][0]
+
+
 def serialize_activity(a):
-    """Activity (Tensor or Table of tensors) -> bytes."""
-    tensors, meta = [], []
+    """Activity (Tensor, Table of tensors keyed by primitives or tensors, or an error message str) -> bytes of a
+    bigdl.proto ``AttrValue`` (PredictionService.serializeActivity)."""
+    from ..utils import bigdl_proto as bp
 
-    def enc(x):
-        if isinstance(x, torch.Tensor):
-            t = x.detach().cpu().contiguous()
-            meta_t = {"t": "tensor", "dtype": str(t.dtype).split(".")[-1], "shape": list(t.shape), "i": len(tensors)}
-            tensors.append(t)
-            return meta_t
-        if isinstance(x, Table):
-            return {"t": "table", "items": [[k, enc(v)] for k, v in x.items()]}
-        raise TypeError(type(x))
+    if isinstance(a, Table):
+        items = list(a.items())
+        if not items:
+            raise ValueError("PredictionService: cannot serialize an empty Table")
+        prim = not isinstance(items[0][0], torch.Tensor)
+        tensors = [_bigdl_tensor(torch.tensor(prim))] + [_bigdl_tensor(k) for k, _ in items] + \
+                  [_bigdl_tensor(v) for _, v in items]
+        attr = {"dataType": ["ARRAY_VALUE"],
+                "arrayValue": [{"size": [len(tensors)], "datatype": ["TENSOR"], "tensor": tensors}]}
+    elif isinstance(a, (torch.Tensor, str)):
+        attr = {"dataType": ["TENSOR"], "tensorValue": [_bigdl_tensor(a)]}
+    else:
+        raise TypeError(f"PredictionService: unsupported activity type {type(a).__name__}")
+    return bp.SCHEMA.encode("AttrValue", attr)
 
-    header = json.dumps(enc(a)).encode()
-    buf = io.BytesIO()
-    buf.write(struct.pack("<I", len(header)))
-    buf.write(header)
-    for t in tensors:
-        raw = t.view(torch.uint8).numpy().tobytes() if t.numel() else b""
-        buf.write(struct.pack("<Q", len(raw)))
-        buf.write(raw)
-    return buf.getvalue()
+
+def _tensor_of(d):
+    from ..utils import bigdl_proto as bp
+
+    st = bp._one(d, "storage", {})
+    if bp._one(d, "datatype") == "STRING" or bp._one(st, "datatype") == "STRING":
+        vals = st.get("string_data", [])
+        return vals[0] if len(vals) == 1 else list(vals)
+    return bp._tensor_from(d, bp._LoadCtx({}))
 
 
 def deserialize_activity(b):
-    mv = memoryview(b)
-    (hl,) = struct.unpack_from("<I", mv, 0)
-    header = json.loads(bytes(mv[4:4 + hl]).decode())
-    off = 4 + hl
-    blobs = []
-    while off < len(b):
-        (n,) = struct.unpack_from("<Q", mv, off)
-        off += 8
-        blobs.append(bytes(mv[off:off + n]))
-        off += n
+    """bytes of a bigdl.proto ``AttrValue`` -> Tensor / Table (PredictionService.deSerializeActivity); a STRING tensor
+    (the error Activity) decodes to its str."""
+    from ..utils import bigdl_proto as bp
 
-    def dec(m):
-        if m["t"] == "tensor":
-            dt = getattr(torch, m["dtype"])
-            raw = bytearray(blobs[m["i"]])
-            t = torch.frombuffer(raw, dtype=torch.uint8) if raw else torch.empty(0, dtype=torch.uint8)
-            return t.view(dt).reshape(m["shape"]).clone()
-        t = Table()
-        for k, v in m["items"]:
-            t[k if not (isinstance(k, str) and k.isdigit()) else int(k)] = dec(v)
-        return t
+    attr = bp.SCHEMA.decode("AttrValue", bytes(b))
+    dt = bp._one(attr, "dataType")
+    if dt == "ARRAY_VALUE":
+        ts = [_tensor_of(t) for t in bp._one(attr, "arrayValue", {}).get("tensor", [])]
+        n = (len(ts) - 1) // 2
+        prim = bool(ts[0].item()) if isinstance(ts[0], torch.Tensor) else bool(ts[0])
+        keys = [(k.item() if isinstance(k, torch.Tensor) else k) if prim else k for k in ts[1:n + 1]]
+        out = Table()
+        for k, v in zip(keys, ts[n + 1:]):
+            out[k] = v
+        return out
+    if dt == "TENSOR" or "tensorValue" in attr:
+        return _tensor_of(bp._one(attr, "tensorValue", {}))
+    raise ValueError(f"PredictionService: unsupported AttrValue dataType {dt}")
 
-    return dec(header)
+
+def _error_activity(stage, e):
+    """The reference's errorTensor: a STRING scalar naming the stage and the exception."""
+    import traceback
+
+    return f"Exception caught during [{stage}]! \n{e}\n" + "".join(traceback.format_tb(e.__traceback__)[-3:])
 
 
 def _share_weights(src, dst):
@@ -238,13 +276,19 @@ class PredictionService:
             self._pool.put((m, stream))
 
     def predict(self, request):
+        """Activity in, Activity out; or bigdl.proto ``AttrValue`` bytes in, bytes out (the reference's protocol,
+        PredictionService.scala:113-160). Failures come back as the reference's error Activity (a STRING scalar)
+        instead of raising."""
         if isinstance(request, (bytes, bytearray, memoryview)):
             try:
                 act = deserialize_activity(bytes(request))
-                out = self._run(act)
+            except Exception as e:
+                return serialize_activity(_error_activity("DeSerialize Input", e))
+            out = self._run(act)
+            try:
                 return serialize_activity(out)
-            except Exception as e:  # reference returns an error Activity instead of throwing
-                return serialize_activity(Table(torch.tensor([0.0]), torch.tensor(list(str(e).encode()), dtype=torch.uint8)))
+            except Exception as e:
+                return serialize_activity(_error_activity("Serialize Output", e))
         return self._run(request)
 
     def _run(self, act):
@@ -254,10 +298,15 @@ class PredictionService:
         try:
             dev = getattr(model, "device", torch.device("cpu"))
             ctx = torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()
-            with ctx, torch.no_grad():
-                act = act.to(dev) if hasattr(act, "to") else act
-                out = model.forward(act)
-                out = out.float().cpu() if isinstance(out, torch.Tensor) else out.to("cpu")
-            return out
+            try:
+                with ctx, torch.no_grad():
+                    act = act.to(dev) if hasattr(act, "to") else act
+                    out = model.forward(act)
+            except Exception as e:      # the reference returns its error Activity (PredictionService.scala:84-87)
+                return _error_activity("running forward", e)
+            try:
+                return out.float().cpu() if isinstance(out, torch.Tensor) else out.to("cpu")
+            except Exception as e:
+                return _error_activity("Clone Result", e)
         finally:
             self._pool.put((model, stream))

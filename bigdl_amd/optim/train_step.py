@@ -289,6 +289,11 @@ class TrainStep:
             owned = [(self.comm.start, self.comm.end)]
         self.plan = build_update_plan(owned, self.splits, self.w16, self.seg)
         self._pending_gather = False
+        from .phase_timer import PhaseTimer
+
+        # device-timed phases (compute / exposed reduce-scatter / exposed all-gather / update), optim/phase_timer.py
+        self.phase = PhaseTimer(enabled=self.device.type == "cuda"
+                                and os.environ.get("BIGDL_PHASE_TIMING", "1") != "0")
 
     # ------------------------------------------------------------------ pieces
     def zero_grad(self):
@@ -300,6 +305,7 @@ class TrainStep:
     def forward_backward(self, x, y):
         m, c = self.model, self.criterion
         m.training()
+        self.phase.begin_step()
         bk = self.bucketed
         if bk is not None:
             bk.begin_step()
@@ -320,6 +326,7 @@ class TrainStep:
         finally:
             if convs:
                 cv.end_dgrad_weights()
+        self.phase.mark("bwd")
         return loss
 
     def forward_backward_step(self, x, y):
@@ -375,15 +382,21 @@ class TrainStep:
         gradient is averaged over the ranks that finished and the update is skipped when fewer than
         ``min_finished`` did. Returns False when the update was skipped."""
         if finished is not None:
-            return self._sync_and_update_weighted(loss, finished)
+            ok = self._sync_and_update_weighted(loss, finished)
+            self.phase.end_step()
+            return ok
         if self.bucketed is not None:
             self.bucketed.update(loss)
             self._pending_gather = True
+            self.phase.end_step()
             return True
-        self.comm.reduce_scatter_gradients(self.g, out=self.g_shard)
+        with self.phase.span("rs", self.comm.active):
+            self.comm.reduce_scatter_gradients(self.g, out=self.g_shard)
         self.apply_processors()
         self.optimize_pieces(loss)
-        self.comm.all_gather_weights(self.w, self.w16)
+        with self.phase.span("ag", self.comm.active):
+            self.comm.all_gather_weights(self.w, self.w16)
+        self.phase.end_step()
         return True
 
     min_finished = 0.0
@@ -515,6 +528,7 @@ class TrainStep:
         from ..ops import native
 
         native.check_persistent()
+        self.phase_done = self.phase.collect()     # phases of the iterations that completed (no synchronisation)
 
     # ------------------------------------------------------------------ optimizer state (checkpoints)
     def _method_layout(self):

@@ -172,7 +172,8 @@ class BucketedGradSync:
         for b in buckets:
             h = self.ag_works.pop(b, None)
             if h is not None:
-                h.wait()
+                with self.step.phase.span("ag"):     # the compute stream's stall on this all-gather (phase_timer)
+                    h.wait()
 
     def gather_all(self):
         if not self.ag_works:
@@ -263,7 +264,8 @@ class BucketedGradSync:
             for b in list(self.launch_log):
                 h = self.works.pop(b)
                 if h is not None:
-                    h.wait()
+                    with step.phase.span("rs"):
+                        h.wait()
             step.apply_processors()
             step.optimize_pieces(loss)
             return
@@ -271,7 +273,8 @@ class BucketedGradSync:
         for b in list(self.launch_log):                   # in launch order: the earliest collectives land first
             h = self.works.pop(b)
             if h is not None:
-                h.wait()
+                with step.phase.span("rs"):               # the compute stream's stall on this reduce-scatter
+                    h.wait()
             b0, b1 = self.bounds[b]
             pieces = [p for p in step.plan if b0 <= p.lo and p.hi <= b1]
             for p in pieces:

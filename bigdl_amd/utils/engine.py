@@ -159,6 +159,10 @@ class _Engine:
             from ..ops import native
 
             native.set_deterministic(str(v).lower() in ("1", "true", "yes"))
+        elif k == "bigdl.module.deviceTiming":      # getTimes in device time (HIP events) for GPU modules
+            from ..nn import abstractnn
+
+            abstractnn.DEVICE_TIMING[0] = str(v).lower() in ("1", "true", "yes")
 
     def getProperty(self, k, default=None):
         return self.properties.get(k, os.environ.get(k, default))

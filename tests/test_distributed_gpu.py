@@ -161,3 +161,66 @@ def test_one_graph_step_with_forked_branches_matches_eager(wgrad_stream):
     errs = run_distributed(_fork_one_graph, 1, (("A", "B", "C", "H"),), engine="gpu", backend="nccl",
                            env={"BIGDL_FORCE_COLLECTIVES": "1", "BIGDL_WGRAD_STREAM": wgrad_stream})[0]
     assert all(e < 1e-7 for e in errs), errs
+
+
+def _rccl_vs_local(rank, world, compress):
+    """5 eager steps with the RCCL bucketed path forced on one rank (reduce-scatters launched from the weight-gradient
+    stream) while a 200 us spin kernel heads every weight-gradient launch on that stream, against the same 5 steps
+    with no collectives at all."""
+    from bigdl_amd import nn
+    from bigdl_amd import optim as O
+    from bigdl_amd.ops import native
+    from bigdl_amd.ops import side_stream as ss
+    from bigdl_amd.optim.train_step import TrainStep
+
+    dev = torch.device("cuda", 0)
+    X, Y = _batch(16)
+    X, Y = X.to(dev), Y.to(dev)
+    done = torch.zeros(1, dtype=torch.int32, device=dev)
+    orig_begin = ss.begin
+
+    def slow_begin(s):
+        cur = orig_begin(s)
+        with torch.cuda.stream(s):
+            native.get().spin_us(200.0, done)      # the weight gradients behind it land 200 us late
+        return cur
+
+    outs = []
+    for forced in (True, False):
+        os.environ["BIGDL_FORCE_COLLECTIVES"] = "1" if forced else "0"
+        model = _cnn(True)
+        step = TrainStep(model, nn.CrossEntropyCriterion(), O.SGD(0.05, momentum=0.9, dampening=0.0), device=dev,
+                         compress=compress if forced else None, overlap=forced, bucket_elems=4096)
+        assert step.comm.active == forced and (step.bucketed is not None) == forced
+        ss.begin = slow_begin if forced else orig_begin
+        try:
+            for _ in range(5):
+                step.step(X, Y)
+            log = list(step.bucketed.launch_log) if forced else None
+            nb = len(step.bucketed.bounds) if forced else 0
+        finally:
+            ss.begin = orig_begin
+        step.gather_model()
+        torch.cuda.synchronize()
+        phase = step.phase.summary()
+        outs.append((step.w[:step.total].clone().cpu(), log, nb, phase))
+    os.environ["BIGDL_FORCE_COLLECTIVES"] = "1"
+    return outs
+
+
+@pytest.mark.parametrize("compress", [None, "bf16"])
+def test_rccl_bucketed_side_stream_matches_no_collectives(compress):
+    """The RCCL branch that launches bucket reduce-scatters from the weight-gradient stream (parallel/bucketed.py
+    _launch) must wait for every weight gradient of the bucket: with that stream delayed by a spin kernel the weights
+    after 5 steps still match a run without collectives (fp32 exchange: to rounding; bf16 exchange: bf16 tolerance).
+    Buckets launch in reverse execution order (last layers' gradients first), and the step's device-timed phases
+    (optim/phase_timer.py) report the exposed reduce-scatter / all-gather waits."""
+    res = run_distributed(_rccl_vs_local, 1, (compress,), engine="gpu", backend="nccl",
+                          env={"BIGDL_FORCE_COLLECTIVES": "1", "BIGDL_WGRAD_STREAM": "1"})[0]
+    (wf, log, nb, phase), (wl, _, _, phase_l) = res
+    rel = float((wf - wl).norm() / wl.norm())
+    assert rel < (2e-2 if compress else 1e-5), rel
+    assert nb > 2 and sorted(log) == list(range(nb)), log
+    assert log == sorted(log, reverse=True), log
+    assert phase is not None and phase["steps"] >= 1 and phase["rs_wait_ms"] >= 0.0 and phase["compute_ms"] > 0.0
+    assert phase_l is not None and phase_l["comm_exposed_ms"] == 0.0

@@ -223,6 +223,69 @@ def test_prediction_service_bytes_roundtrip():
     assert torch.equal(t[2], torch.arange(3))
 
 
+def _pb_varint(v):
+    out = bytearray()
+    while True:
+        b = v & 0x7F
+        v >>= 7
+        out.append(b | (0x80 if v else 0))
+        if not v:
+            return bytes(out)
+
+
+def _pb_field(num, wire, payload):
+    import struct
+
+    if wire == 0:
+        return _pb_varint(num << 3) + _pb_varint(payload)
+    if wire == 2:
+        return _pb_varint(num << 3 | 2) + _pb_varint(len(payload)) + payload
+    raise ValueError(wire)
+
+
+def _pb_packed_ints(num, vals):
+    return _pb_field(num, 2, b"".join(_pb_varint(v) for v in vals))
+
+
+def test_prediction_service_decodes_hand_built_attrvalue():
+    """The bytes protocol is bigdl.proto's AttrValue (S/optim/PredictionService.scala:184-280): a message assembled
+    here field by field (proto3 packed repeated fields, as the JVM writes them) decodes to the tensor / table, the
+    service answers in the same encoding, and a malformed request gets the reference's STRING error Activity."""
+    import struct
+
+    from bigdl_amd.optim.predictor import deserialize_activity, serialize_activity
+
+    vals = [0.5, -1.0, 2.0, 3.25, 4.0, -6.5]
+    storage = (_pb_field(1, 0, 2) + _pb_field(2, 2, struct.pack("<6f", *vals)) + _pb_field(9, 0, 7))   # FLOAT
+    tensor = (_pb_field(1, 0, 2) + _pb_packed_ints(2, [2, 3]) + _pb_packed_ints(3, [3, 1]) + _pb_field(4, 0, 1)
+              + _pb_field(5, 0, 2) + _pb_field(6, 0, 6) + _pb_field(8, 2, storage) + _pb_field(9, 0, 6))
+    attr = _pb_field(1, 0, 10) + _pb_field(10, 2, tensor)                 # dataType TENSOR, tensorValue
+    t = deserialize_activity(attr)
+    assert t.dtype == torch.float32 and torch.equal(t, torch.tensor(vals).view(2, 3))
+
+    def scalar(dt, field, payload):                                      # a scalar key tensor of one element
+        st = _pb_field(1, 0, dt) + payload
+        return _pb_field(1, 0, dt) + _pb_field(5, 0, 0) + _pb_field(6, 0, 1) + _pb_field(7, 0, 1) + \
+            _pb_field(4, 0, 1) + _pb_field(8, 2, st)
+    is_prim = scalar(5, 4, _pb_field(4, 0, 1))                            # BOOL true (bool_data)
+    key1 = scalar(0, 6, _pb_field(6, 0, 1))                               # INT32 1 (int_data)
+    key2 = scalar(0, 6, _pb_field(6, 0, 2))
+    arr = _pb_field(1, 0, 5) + _pb_field(2, 0, 10) + b"".join(_pb_field(10, 2, x) for x in (is_prim, key1, key2,
+                                                                                           tensor, tensor))
+    tab = deserialize_activity(_pb_field(1, 0, 15) + _pb_field(15, 2, arr))   # ARRAY_VALUE
+    assert sorted(tab.keys()) == [1, 2] and torch.equal(tab[2], torch.tensor(vals).view(2, 3))
+    # our encoding decodes back (tensor keys too) and the service speaks it
+    model = _mlp()
+    svc = O.PredictionService(model)
+    x = torch.randn(3, 4)
+    out = deserialize_activity(svc.predict(serialize_activity(x)))
+    assert torch.allclose(out, model.forward(x), atol=1e-6)
+    err = deserialize_activity(svc.predict(b"\x0a\xff\xff"))
+    assert isinstance(err, str) and "DeSerialize Input" in err
+    bad = deserialize_activity(svc.predict(serialize_activity(torch.randn(3, 7))))   # wrong width: forward fails
+    assert isinstance(bad, str) and "running forward" in bad
+
+
 def test_prediction_service_replica_pool_concurrent():
     from concurrent.futures import ThreadPoolExecutor
 
