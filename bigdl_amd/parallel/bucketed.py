@@ -232,6 +232,7 @@ class BucketedGradSync:
             self._fwd[k] = n - 1
             return
         self._fwd[k] = 0
+        ready = []
         for li in self.sub_leaves.get(k, ()):
             if li in self._done:
                 continue
@@ -242,7 +243,11 @@ class BucketedGradSync:
             for b in self.leaf_buckets[li]:
                 self._rem[b] -= 1
                 if self._rem[b] == 0:
-                    self._launch(b)
+                    ready.append(b)
+        # buckets completed by the same backward launch last-first: launch order is the reverse of the flat-buffer
+        # (= forward execution) order, identical on every rank
+        for b in sorted(ready, reverse=True):
+            self._launch(b)
 
     def begin_backward(self):
         if self.step.defer_sync:

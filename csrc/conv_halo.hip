@@ -373,16 +373,26 @@ __global__ __launch_bounds__(256, 2) void conv_halo_kernel(ConvArgs a, I8Epi ep)
       const v4f b0 = *reinterpret_cast<const v4f*>(ptab + C + c), b1 = *reinterpret_cast<const v4f*>(ptab + C + c + 4);
       const float sc[8] = {s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
       const float sh[8] = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+      // every granule's read in flight at once, one wait, then branch-free rewrites (halo / pad granules keep zero)
+      const unsigned xa = (unsigned)(uintptr_t)(LDS_PTR(unsigned char))X + (unsigned)(wave * 1024 + lane * 16);
+      v4u u[H::XI];
+#pragma unroll
+      for (int d = 0; d < H::XI; ++d)
+        asm volatile("ds_read_b128 %0, %1" : "=v"(u[d]) : "v"(xa + (unsigned)(d * 4096)) : "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      // tie every loaded value to a volatile asm behind the wait: the arithmetic on it cannot be hoisted above it
+#pragma unroll
+      for (int d = 0; d < H::XI; ++d) asm volatile("" : "+v"(u[d]));
 #pragma unroll
       for (int d = 0; d < H::XI; ++d) {
-        if (!((xreal >> d) & 1u)) continue;
-        v4u* q = reinterpret_cast<v4u*>(X + (d * 4 + wave) * 1024 + lane * 16);
-        v4u u = *q;
+        const bool real = (xreal >> d) & 1u;
+        v4u t;
 #pragma unroll
         for (int e = 0; e < 4; ++e)
-          u[e] = pack2bf(fmaxf(lo_bf(u[e]) * sc[2 * e] + sh[2 * e], 0.f),
-                         fmaxf(hi_bf(u[e]) * sc[2 * e + 1] + sh[2 * e + 1], 0.f));
-        *q = u;
+          t[e] = pack2bf(fmaxf(lo_bf(u[d][e]) * sc[2 * e] + sh[2 * e], 0.f),
+                         fmaxf(hi_bf(u[d][e]) * sc[2 * e + 1] + sh[2 * e + 1], 0.f));
+        const v4u o = real ? t : u[d];
+        asm volatile("ds_write_b128 %0, %1" ::"v"(xa + (unsigned)(d * 4096)), "v"(o) : "memory");
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");     // the rewritten chunk is complete before the barrier
     }

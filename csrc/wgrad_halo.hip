@@ -243,27 +243,48 @@ __global__ __launch_bounds__(KB * 4, 1) void conv_wgrad_halo_kernel(WgradArgs a)
       const int sg = st0 + i, oh0 = (sg % spi) * RB;
       const int v = (oh0 == 0 ? 1 : 0) | (oh0 + RB == IH ? 2 : 0);
       const unsigned xb = (unsigned)(uintptr_t)(LDS_PTR(unsigned char))lds + (unsigned)((i % H::NS) * H::STAGE);
+      // inline asm LDS accesses (a plain load here would make the compiler drain every in-flight stage DMA): every
+      // granule's read issued at once, one wait, then branch-free rewrites (pad / out-of-image granules keep zero).
+      // A lane's granule g = (slot & 7) ^ hf128(row) with slot & 7 = lane & 7 and row = slot >> 3, so g depends on d:
+      // its 8 scale / shift pairs are read per granule.
+      constexpr int PG = H::XG < 4 ? H::XG : 4;            // granules per batch (8 at once spilled)
 #pragma unroll
-      for (int d = 0; d < H::XG; ++d) {
-        const unsigned off = v == 0 ? xv[0][d] : v == 1 ? xv[1][d] : v == 2 ? xv[2][d] : xv[3][d];
-        if (off == OOB) continue;
-        const int slot = (d * H::NW + wave) * 64 + lane;
-        const int g = (slot & 7) ^ hf128(slot >> 3);
-        const unsigned ta = (unsigned)(uintptr_t)(LDS_PTR(float))ptab + (unsigned)(g * 32);
-        const unsigned addr = xb + (unsigned)(slot * 16);
-        v4u u;
-        v4f s0, s1, b0, b1;
-        // inline asm LDS accesses: a plain load here would make the compiler drain every in-flight stage DMA
-        asm volatile("ds_read_b128 %0, %5\n\tds_read_b128 %1, %6 offset:0\n\tds_read_b128 %2, %6 offset:16\n\t"
-                     "ds_read_b128 %3, %6 offset:256\n\tds_read_b128 %4, %6 offset:272\n\ts_waitcnt lgkmcnt(0)"
-                     : "=v"(u), "=v"(s0), "=v"(s1), "=v"(b0), "=v"(b1) : "v"(addr), "v"(ta) : "memory");
-        const float sc[8] = {s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
-        const float sh[8] = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+      for (int d0 = 0; d0 < H::XG; d0 += PG) {
+        v4u u[PG];
+        v4f s0[PG], s1[PG], b0[PG], b1[PG];
 #pragma unroll
-        for (int e = 0; e < 4; ++e)
-          u[e] = pack2bf(fmaxf(lo_bf(u[e]) * sc[2 * e] + sh[2 * e], 0.f),
-                         fmaxf(hi_bf(u[e]) * sc[2 * e + 1] + sh[2 * e + 1], 0.f));
-        asm volatile("ds_write_b128 %0, %1" ::"v"(addr), "v"(u) : "memory");
+        for (int q = 0; q < PG; ++q) {
+          const int d = d0 + q;
+          if (d >= H::XG) break;
+          const int slot = (d * H::NW + wave) * 64 + lane;
+          const int g = (slot & 7) ^ hf128(slot >> 3);
+          const unsigned ta = (unsigned)(uintptr_t)(LDS_PTR(float))ptab + (unsigned)(g * 32);
+          const unsigned addr = xb + (unsigned)(slot * 16);
+          asm volatile("ds_read_b128 %0, %5\n\tds_read_b128 %1, %6 offset:0\n\tds_read_b128 %2, %6 offset:16\n\t"
+                       "ds_read_b128 %3, %6 offset:256\n\tds_read_b128 %4, %6 offset:272"
+                       : "=v"(u[q]), "=v"(s0[q]), "=v"(s1[q]), "=v"(b0[q]), "=v"(b1[q]) : "v"(addr), "v"(ta) : "memory");
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        // tie the loaded values to volatile asms behind the wait (their arithmetic cannot be hoisted above it)
+#pragma unroll
+        for (int q = 0; q < PG; ++q) asm volatile("" : "+v"(u[q]), "+v"(s0[q]), "+v"(s1[q]), "+v"(b0[q]), "+v"(b1[q]));
+#pragma unroll
+        for (int q = 0; q < PG; ++q) {
+          const int d = d0 + q;
+          if (d >= H::XG) break;
+          const unsigned off = v == 0 ? xv[0][d] : v == 1 ? xv[1][d] : v == 2 ? xv[2][d] : xv[3][d];
+          const int slot = (d * H::NW + wave) * 64 + lane;
+          const unsigned addr = xb + (unsigned)(slot * 16);
+          const float sc[8] = {s0[q][0], s0[q][1], s0[q][2], s0[q][3], s1[q][0], s1[q][1], s1[q][2], s1[q][3]};
+          const float sh[8] = {b0[q][0], b0[q][1], b0[q][2], b0[q][3], b1[q][0], b1[q][1], b1[q][2], b1[q][3]};
+          v4u t;
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            t[e] = pack2bf(fmaxf(lo_bf(u[q][e]) * sc[2 * e] + sh[2 * e], 0.f),
+                           fmaxf(hi_bf(u[q][e]) * sc[2 * e + 1] + sh[2 * e + 1], 0.f));
+          const v4u o = off != OOB ? t : u[q];
+          asm volatile("ds_write_b128 %0, %1" ::"v"(addr), "v"(o) : "memory");
+        }
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }

@@ -47,9 +47,14 @@ def test_get_times_reports_device_time():
     assert top_f > 0 and top_b > 0
     convs = [t for t in times if isinstance(t[0], nn.SpatialConvolution)]
     assert len(convs) == 53 and all(f > 0 for _, f, _ in convs)
+    # the top-level Sequential's children tile its forward on the stream; leaves inside fused residual blocks are run
+    # by their block (nn/fusion.py residual_forward calls the last BN's updateOutput), so the leaf sum is a lower bound
+    kid_ids = {id(m) for m in model.modules}
+    kid_f = sum(f for m, f, _ in times if id(m) in kid_ids) / 1e6
+    assert abs(kid_f - top_f) <= 0.1 * top_f, (kid_f, top_f)
     leaf_ids = {id(m) for m in _leaves(model)}
     leaf_f = sum(f for m, f, _ in times if id(m) in leaf_ids) / 1e6
-    assert abs(leaf_f - top_f) <= 0.1 * top_f, (leaf_f, top_f)
+    assert 0.3 * top_f < leaf_f <= 1.05 * top_f, (leaf_f, top_f)
     assert abs(top_f - outer_ms) <= 0.25 * outer_ms, (top_f, outer_ms)
     # host timing (device timing off) measures the enqueue only: no event pairs are queued
     model.resetTimes()
