@@ -1,7 +1,9 @@
 """Per-layer roofline of the ResNet-50 (224x224) convolutions at batch 256 on one MI355X.
 
 For every distinct conv shape (tools/bench_conv.py SHAPES, with its count in the network) and every pass — fwd (with
-the BN-statistics epilogue, as in training), dgrad, wgrad (fp32 weight gradient incl. any split-K reduce) — it prints
+the conv bias and the BN-statistics epilogue, as in training), dgrad, wgrad (fp32 weight gradient + bias gradient incl.
+any split reduce) — through the paths the training step takes (the stem as the pixel-pair view from the fp32 image,
+ops/conv.py conv2d_pairs_*; the data gradients without the fused consumer-BN epilogue) — it prints
 FLOPs, the minimum HBM bytes (every operand read once, the result written once), the measured device time (CUDA
 events, median of --iters launches), the bound max(FLOP / 2.5 PF, bytes / 8 TB/s) and measured / bound. Totals are
 weighted by the layer counts. ``--hbm`` prices bytes at another bandwidth (6.3 TB/s = the measured copy rate).
@@ -65,15 +67,29 @@ def main():
         dw = torch.zeros(K, C, R, R, device=dev).contiguous(memory_format=CL)
         db = torch.zeros(K, device=dev)
         stats = bnops.new_stats(K, dev)
+        bias = torch.zeros(K, device=dev)
         fl = 2.0 * N * OH * OH * K * C * R * R
         bx, bw, by = N * H * H * C * 2, K * C * R * R * 2, N * OH * OH * K * 2
         passes = {
-            "fwd": (lambda: cv.conv2d_fwd(x, w, None, (st, st), (pd, pd), stats=stats), bx + bw + by),
+            "fwd": (lambda: cv.conv2d_fwd(x, w, bias, (st, st), (pd, pd), stats=stats), bx + bw + by),
             "dgrad": (lambda: cv.conv2d_dgrad(gy, wt, x.shape, (st, st), (pd, pd)), by + bw + bx),
             "wgrad": (lambda: cv.conv2d_wgrad(gy, x, dw, db, (st, st), (pd, pd)), by + bx + K * C * R * R * 4),
         }
         if si == 0:
-            passes.pop("dgrad")          # the stem's input gradient is never computed
+            # the stem as the step runs it: 3-channel fp32 image -> pixel-pair view (8 channels per 2 columns), the
+            # pair-view kernels for fwd / wgrad; its input gradient is never computed
+            img = torch.randn(N, 3, H, H, device=dev)
+            OHp, OWp, S2, _, _ = cv.pair_geometry(H, H, R, R, st, pd, pd)
+            xp = cv.to_pairs_bf16(img, R, R, st, pd, pd)
+            wp = cv.pair_weight((torch.randn(K, 3, R, R, device=dev) * 0.05).to(BF, memory_format=CL))
+            dwp = torch.zeros(K, R * S2 * 8, device=dev)
+            fl = 2.0 * N * OH * OH * K * 3 * R * R
+            bx = N * H * H * 3 * 4
+            passes = {
+                "fwd": (lambda: cv.conv2d_pairs_fwd(xp, wp, bias, K, OHp, OWp, R, S2, st, stats=stats),
+                        bx + bw + by),
+                "wgrad": (lambda: cv.conv2d_pairs_wgrad(gy, xp, R, S2, st, dwp, db), by + bx + K * 3 * R * R * 4),
+            }
         for name, (fn, byt) in passes.items():
             us = timed(fn, a.iters)
             bound = max(fl / PEAK, byt / hbm) * 1e6
