@@ -7,8 +7,16 @@ GPU engine: Linear runs on the MFMA GEMM kernels of csrc/conv_igemm.hip (a Linea
 convolution over a 1x1 image: fwd = NT GEMM with fused bias/ReLU, dgrad = NT GEMM against the transposed
 weight, wgrad = split-K TN GEMM accumulated in fp32 into the flat gradient buffer). Feature sizes that are
 not multiples of 8 are zero-padded on the fly.
+
+Large plain GEMMs (a language model's vocabulary projection, an RNN's input projection: M >= 8192 rows, K >= 512,
+N >= 2048) go to hipBLASLt instead (torch.addmm / torch.mm with fp32 accumulation; the weight gradient in fp32
+straight from the GEMM, the bias gradient as one extra ones-column of the input): on the PTB LM's shapes it runs
+15-40 % faster than the in-tree tiles (tools/lm_gemm_vs_blas.py, profiles/r6_lm_gemm_vs_hipblaslt.log), while the
+convolution-shaped and fused GEMMs stay on the in-tree kernels, which beat it there (tools/gemm_vs_blas.py).
+BIGDL_LINEAR_BLAS=0 keeps every Linear on the in-tree kernels.
 """
 import math
+import os
 
 import torch
 import torch.nn.functional as F
@@ -25,6 +33,13 @@ CL = torch.channels_last
 
 def _pad8(n):
     return -(-n // 8) * 8
+
+
+_BLAS = [os.environ.get("BIGDL_LINEAR_BLAS", "1") != "0"]
+
+
+def _blas_shape(M, K, N):
+    return M >= 8192 and K >= 512 and N >= 2048
 
 
 class Linear(TensorModule):
@@ -80,6 +95,32 @@ class Linear(TensorModule):
             x = F.pad(x, (0, Ip - self.inputSize))
         return x.view(B, Ip, 1, 1)
 
+    def _use_blas(self, M):
+        if not _BLAS[0] or self._padded() or self.fuse_relu or not _blas_shape(M, self.inputSize, self.outputSize):
+            return False
+        from ..ops import native
+
+        return not native.deterministic()
+
+    def _blas_fwd(self, x):
+        """hipBLASLt forward; keeps [x | 1 | 0...] (bf16, one extra 8-column block) for the weight gradient, whose
+        GEMM then yields the bias gradient as its last column."""
+        M, K = x.shape
+        x16 = x if x.dtype == BF16 else (ops.to_bf16(x.contiguous()) if x.dtype == torch.float32 else x.to(BF16))
+        w16 = self.w16("weight")
+        if self.bias is not None:
+            xe = torch.empty(M, K + 8, dtype=BF16, device=x.device)
+            xe[:, :K].copy_(x16)
+            xe[:, K:].zero_()
+            xe[:, K].fill_(1.0)
+            self._xe = xe
+            y = torch.addmm(self.bias.to(BF16), xe[:, :K], w16.t())
+        else:
+            self._xe = x16.contiguous()
+            y = torch.mm(self._xe, w16.t())
+        self._x4 = None
+        return y
+
     def updateOutput(self, input):
         x = input
         lead = None
@@ -88,7 +129,10 @@ class Linear(TensorModule):
         elif x.dim() > 2:
             lead = x.shape[:-1]
             x = x.reshape(-1, x.shape[-1])
-        if x.is_cuda:
+        self._xe = None
+        if x.is_cuda and self._use_blas(x.shape[0]):
+            y = self._blas_fwd(x)
+        elif x.is_cuda:
             x4 = self._x4d(x)
             self._x4 = x4
             bias = self.bias
@@ -122,7 +166,11 @@ class Linear(TensorModule):
 
     def updateGradInput(self, input, gradOutput):
         g = self._gy2d(gradOutput)
-        if g.is_cuda:
+        if g.is_cuda and getattr(self, "_xe", None) is not None:
+            g16 = ops.to_bf16(g) if g.dtype == torch.float32 else g.to(BF16).contiguous()
+            self._g16 = g16
+            gi = torch.mm(g16, self.w16("weight"))
+        elif g.is_cuda:
             B = g.shape[0]
             Op, Ip = _pad8(self.outputSize), _pad8(self.inputSize)
             g16 = ops.to_bf16(g) if g.dtype == torch.float32 else g.to(BF16).contiguous()
@@ -140,6 +188,17 @@ class Linear(TensorModule):
 
     def accGradParameters(self, input, gradOutput):
         g = self._gy2d(gradOutput)
+        if g.is_cuda and getattr(self, "_xe", None) is not None:
+            g16 = getattr(self, "_g16", None)
+            if g16 is None or g16.dim() != 2 or g16.shape[0] != g.shape[0]:
+                g16 = ops.to_bf16(g) if g.dtype == torch.float32 else g.to(BF16).contiguous()
+            K = self.inputSize
+            gw = torch.mm(g16.t(), self._xe, out_dtype=torch.float32)     # [N, K (+8)] fp32 from the GEMM
+            self.gradWeight.add_(gw[:, :K], alpha=self.scaleW)
+            if self.bias is not None:
+                self.gradBias.add_(gw[:, K], alpha=self.scaleB)
+            self._g16 = None
+            return
         if g.is_cuda:
             g4 = getattr(self, "_g16", None)
             if g4 is None or g4.shape[0] != g.shape[0]:

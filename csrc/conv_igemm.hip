@@ -2784,9 +2784,11 @@ static bool s1_applies(const ConvArgs* a) {
   }
   if (!g_conv_s1 || a->out32 || !a->ident_out || a->ntaps != 1 || a->tap_h[0] || a->tap_w[0] || a->tap_k[0]) return false;
   if (a->mul_h != 1 || a->mul_w != 1 || a->Hs != a->OH || a->Ws != a->OW) return false;
-  // BIGDL_CONV_S1 = 2 also takes Kdim 256 (128 VGPRs of weights per wave, 16-pixel wave tiles)
-  if ((a->Kdim != 64 && a->Kdim != 128 && !(a->Kdim == 256 && g_conv_s1 >= 2)) || a->Cs != a->Kdim ||
-      (a->Ncol % 64) || (a->ldo % 8) || (a->ldw % 8))
+  // BIGDL_CONV_S1 = 2 also takes Kdim 256 (128 VGPRs of weights per wave, 16-pixel wave tiles); 3 = Kdim 256 only
+  // without the extended epilogue (addend / consumer-BN reduction: data gradients stay on the tile kernels)
+  const bool ext = a->addend != nullptr || (a->bnred != nullptr && a->stats == nullptr);
+  if ((a->Kdim != 64 && a->Kdim != 128 && !(a->Kdim == 256 && (g_conv_s1 == 2 || (g_conv_s1 == 3 && !ext)))) ||
+      a->Cs != a->Kdim || (a->Ncol % 64) || (a->ldo % 8) || (a->ldw % 8))
     return false;
   // the epilogue operands go through 32-bit buffer offsets (bytes of an [M][ldo] bf16 tensor, below the OOB offset)
   if (((size_t)(a->M - 1) * a->ldo + a->Ncol) * 2 >= 0x7ff00000u) return false;
