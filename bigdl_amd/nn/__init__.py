@@ -22,3 +22,4 @@ from ..optim.regularizer import L1L2Regularizer, L1Regularizer, L2Regularizer  #
 from ..utils.table import T, Table  # noqa: F401
 from .module import Module  # noqa: F401
 from . import primitive as NNPrimitive  # noqa: E402,F401
+from . import mkldnn  # noqa: E402,F401  (nn.mkldnn.RNN: the fused multi-layer RNN primitive)

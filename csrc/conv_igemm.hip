@@ -2257,6 +2257,10 @@ __global__ __launch_bounds__(512, 2) void conv_nt_p8_kernel(ConvArgs a) {
 template <int K, int CG, int BMW, bool F32T, bool EXT, bool PRE = false>
 __global__ __launch_bounds__(256, K >= 256 ? 1 : 2) void conv_nt_s1_kernel(ConvArgs a) {
   constexpr int KF = K / 32, MI = BMW / 16, PGN = 4 / CG, BM = BMW * PGN;
+  // EXT operands one tile ahead of their use (PF); K = 128 pays for the registers with a double instead of a triple
+  // register buffer of A tiles (2 WG/CU: 256 VGPRs)
+  constexpr bool PF = EXT && K >= 128;
+  constexpr int NB = (EXT && K == 128) ? 2 : 3;
   constexpr int GPR = F32T ? 16 : 8;               // 16-byte granules per 64-channel row of the LDS slice
   constexpr int NR = BMW / 8;                      // row-phase passes (8 pixels x 8 lanes each)
   __shared__ __attribute__((aligned(16))) unsigned lds[4 * BMW * GPR * 4 + (PRE ? 2 * K : 0)];
@@ -2323,22 +2327,33 @@ __global__ __launch_bounds__(256, K >= 256 ? 1 : 2) void conv_nt_s1_kernel(ConvA
     }
   };
 
-  auto compute_store = [&](v8s (&af)[MI][KF], int t) {
-    const int p0 = t * BM + pg * BMW;
-    v4u pad[EXT ? NR : 1], px[EXT ? NR : 1];
-    unsigned pzb[EXT ? NR : 1];          // byte 0: addend mask, byte 1: consumer-BN sign mask
-    if constexpr (EXT) {     // epilogue operands first: their latency overlaps the MFMAs and the LDS transpose
+  // epilogue operands of a tile (EXT): addend / BN x rows and their mask bytes; with PF they are loaded one tile
+  // ahead (issued before the previous tile's MFMAs) instead of at the start of the tile that consumes them
+  // (mask bytes kept apart until use: combining them where they are loaded would wait for the loads there)
+  struct ExtOps { v4u pad[EXT ? NR : 1], px[EXT ? NR : 1]; unsigned pza[EXT ? NR : 1], pzz[EXT ? NR : 1]; };
+  auto load_ext = [&](ExtOps& e, int t) {
+    if constexpr (EXT) {
+      const int p0 = t * BM + pg * BMW;
 #pragma unroll
       for (int rr = 0; rr < NR; ++rr) {
         const int m = min(p0 + rr * 8 + (lane >> 3), a.M - 1);
         const size_t off = (size_t)m * a.ldo + n;
         const unsigned eb = (unsigned)(off * 2), zo = (unsigned)(off >> 3);
-        pad[rr] = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(r_add, eb, 0, 0));
-        px[rr] = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(r_bx, eb, 0, 0));
-        pzb[rr] = __builtin_amdgcn_raw_buffer_load_b8(r_azm, zo, 0, 0) |
-                  (__builtin_amdgcn_raw_buffer_load_b8(r_bzm, zo, 0, 0) << 8);
+        e.pad[rr] = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(r_add, eb, 0, 0));
+        e.px[rr] = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(r_bx, eb, 0, 0));
+        e.pza[rr] = __builtin_amdgcn_raw_buffer_load_b8(r_azm, zo, 0, 0);     // addend mask
+        e.pzz[rr] = __builtin_amdgcn_raw_buffer_load_b8(r_bzm, zo, 0, 0);     // consumer-BN sign mask
       }
     }
+  };
+
+  auto compute_store = [&](v8s (&af)[MI][KF], ExtOps& eo, int t) {
+    const int p0 = t * BM + pg * BMW;
+    ExtOps el;
+    if constexpr (EXT && !PF) load_ext(el, t);   // epilogue operands first: latency overlaps the MFMAs
+    ExtOps& e = PF ? eo : el;
+    auto& pad = e.pad;
+    auto& px = e.px;
     v4f acc[MI][4];
 #pragma unroll
     for (int i = 0; i < MI; ++i)
@@ -2396,7 +2411,7 @@ __global__ __launch_bounds__(256, K >= 256 ? 1 : 2) void conv_nt_s1_kernel(ConvA
         const v4f hi = *reinterpret_cast<const v4f*>(wl + (p * GPR + ((2 * q + 1) ^ (p & 15))) * 4);
         float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         if constexpr (EXT) {
-          const v4u pa = azm ? (pad[rr] & mask8_to_and(pzb[rr] & 0xffu)) : pad[rr];
+          const v4u pa = azm ? (pad[rr] & mask8_to_and(e.pza[rr] & 0xffu)) : pad[rr];
 #pragma unroll
           for (int e = 0; e < 4; ++e) { v[2 * e] += lo_bf(pa[e]); v[2 * e + 1] += hi_bf(pa[e]); }
         }
@@ -2424,7 +2439,7 @@ __global__ __launch_bounds__(256, K >= 256 ? 1 : 2) void conv_nt_s1_kernel(ConvA
             p2[e] = __builtin_elementwise_fma(y, y, p2[e]);
           }
         } else {
-          const unsigned zb = pzb[rr] >> 8;
+          const unsigned zb = e.pzz[rr] & 0xffu;
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             v2f d = v2f{lo_bf(o[e]), hi_bf(o[e])} * vm;
@@ -2454,19 +2469,40 @@ __global__ __launch_bounds__(256, K >= 256 ? 1 : 2) void conv_nt_s1_kernel(ConvA
     }
   };
 
-  v8s a0[MI][KF], a1[MI][KF], a2[MI][KF];
   int t = wgi;
-  if (t < ntiles) load(a0, t);
-  if (t + ngr < ntiles) load(a1, t + ngr);
-  for (; t < ntiles; t += 3 * ngr) {
-    if (t + 2 * ngr < ntiles) load(a2, t + 2 * ngr);
-    compute_store(a0, t);
-    if (t + ngr >= ntiles) break;
-    if (t + 3 * ngr < ntiles) load(a0, t + 3 * ngr);
-    compute_store(a1, t + ngr);
-    if (t + 2 * ngr >= ntiles) break;
-    if (t + 4 * ngr < ntiles) load(a1, t + 4 * ngr);
-    compute_store(a2, t + 2 * ngr);
+  if constexpr (NB == 2) {
+    v8s a0[MI][KF], a1[MI][KF];
+    ExtOps e0, e1;
+    if (t < ntiles) load(a0, t);
+    if constexpr (PF) load_ext(e0, t);       // rows are clamped: a tile past the end reads valid rows, unused
+    for (; t < ntiles; t += 2 * ngr) {
+      if (t + ngr < ntiles) load(a1, t + ngr);
+      if constexpr (PF) load_ext(e1, t + ngr);
+      compute_store(a0, e0, t);
+      if (t + ngr >= ntiles) break;
+      if (t + 2 * ngr < ntiles) load(a0, t + 2 * ngr);
+      if constexpr (PF) load_ext(e0, t + 2 * ngr);
+      compute_store(a1, e1, t + ngr);
+    }
+  } else {
+    v8s a0[MI][KF], a1[MI][KF], a2[MI][KF];
+    ExtOps e0, e1, e2;     // live only with PF (two at a time: the consumed tile's and the next one's)
+    if (t < ntiles) load(a0, t);
+    if (t + ngr < ntiles) load(a1, t + ngr);
+    if constexpr (PF) load_ext(e0, t);
+    for (; t < ntiles; t += 3 * ngr) {
+      if (t + 2 * ngr < ntiles) load(a2, t + 2 * ngr);
+      if constexpr (PF) load_ext(e1, t + ngr);
+      compute_store(a0, e0, t);
+      if (t + ngr >= ntiles) break;
+      if (t + 3 * ngr < ntiles) load(a0, t + 3 * ngr);
+      if constexpr (PF) load_ext(e2, t + 2 * ngr);
+      compute_store(a1, e1, t + ngr);
+      if (t + 2 * ngr >= ntiles) break;
+      if (t + 4 * ngr < ntiles) load(a1, t + 4 * ngr);
+      if constexpr (PF) load_ext(e0, t + 3 * ngr);
+      compute_store(a2, e2, t + 2 * ngr);
+    }
   }
   float* const red = a.stats ? a.stats : (bnw ? a.bnred : nullptr);
   if (red) {
