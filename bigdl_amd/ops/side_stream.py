@@ -18,7 +18,14 @@ Ordering rules:
     collective is launched (parallel/bucketed.py);
   * inside a HIP-graph capture this is an ordinary fork / join of the capture stream.
 On by default (``BIGDL_WGRAD_STREAM=0`` disables): ResNet-50 b256 eager 29.40 -> 27.84 ms/step on one MI355X
-(profiles/r3_wgrad_side_stream_ab.txt); extra side streams or stream priorities measured no better.
+(profiles/r3_wgrad_side_stream_ab.txt); extra side streams measured no better.
+
+Queue priority: the compute stream is the critical path (busy ~21.9 of a ~22.1 ms step) and the side stream's
+weight gradients only fill around it, so training runs the compute stream at HIGH queue priority
+(``priority_compute_stream``, called by TrainStep; ``BIGDL_COMPUTE_PRIO=0`` keeps the default stream): when both
+streams have workgroups waiting, the dispatcher takes the data-gradient chain's first. ResNet-50 b256
+11,200 -> 11,690 img/s interleaved on one box (profiles/r6_iteration_log.txt). Raising the SIDE stream's priority
+instead (``BIGDL_WGRAD_PRIO=-1``, round 3) measured no better: that is the wrong direction.
 """
 import os
 
@@ -91,6 +98,62 @@ def _new_stream(dev):
         h = native.get().cu_masked_stream(dev, _cu_mask_words(_CUMASK, ncu))
         return torch.cuda.ExternalStream(h, device=dev)
     return torch.cuda.Stream(device=dev, priority=_PRIO)
+
+
+_COMPUTE_PRIO = os.environ.get("BIGDL_COMPUTE_PRIO", "-1")
+_HP = {}
+
+
+def _ranks_share_gpus():
+    """True when more ranks than visible GPUs run on this node (single-GPU multi-rank rehearsals): raised-priority
+    queues of several processes on ONE device measured to serialise against each other (a straggler rank's 600 ms
+    spin kernel held the other rank's whole iteration, tests/test_straggler_gpu.py), so the one-process-per-GPU
+    priority split is kept to that layout."""
+    import torch.distributed as dist
+
+    world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else \
+        int(os.environ.get("LOCAL_WORLD_SIZE", os.environ.get("WORLD_SIZE", "1")))
+    return world > max(1, torch.cuda.device_count())
+
+
+def priority_compute_stream(device):
+    """Make a high-priority stream the current stream of ``device`` (once; the old current stream's queued work is
+    waited for). No-op when disabled, inside a capture, or when the current stream already has raised priority."""
+    try:
+        prio = int(_COMPUTE_PRIO)
+    except ValueError:
+        prio = 0
+    dev = torch.device(device)
+    if prio >= 0 or dev.type != "cuda" or not torch.cuda.is_available() or torch.cuda.is_current_stream_capturing():
+        return None
+    if _ranks_share_gpus():
+        return None
+    cur = torch.cuda.current_stream(dev)
+    if cur.priority < 0:
+        return cur
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    s = _HP.get(idx)
+    if s is None:
+        s = _HP[idx] = torch.cuda.Stream(device=idx, priority=prio)
+    s.wait_stream(cur)
+    torch.cuda.set_stream(s)
+    return s
+
+
+def peer_stream(device):
+    """A new stream at the current compute stream's priority, for work the compute stream must not starve (the
+    straggler drop's control and late-exchange streams): a raised-priority queue with a kernel in flight holds back
+    lower-priority queues' dispatch, measured on the straggler test (a dropped rank's exchange waited out its 600 ms
+    spin kernel)."""
+    dev = torch.device(device)
+    return torch.cuda.Stream(device=dev, priority=torch.cuda.current_stream(dev).priority)
+
+
+def compute_priority_enabled():
+    try:
+        return int(_COMPUTE_PRIO) < 0
+    except ValueError:
+        return False
 
 
 def begin(s):

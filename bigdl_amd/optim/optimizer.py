@@ -615,7 +615,9 @@ class _StragglerDrop:
         if not torch.cuda.is_available() or self.opt._step is None or self.opt._step.device.type != "cuda":
             return contextlib.nullcontext()
         if self._ctrl is None:
-            self._ctrl = torch.cuda.Stream(device=self.opt._step.device)
+            from ..ops import side_stream
+
+            self._ctrl = side_stream.peer_stream(self.opt._step.device)
         return torch.cuda.stream(self._ctrl)
     def timed_out(self, elapsed):
         return self.forced is None and elapsed > self.threshold

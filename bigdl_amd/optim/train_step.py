@@ -235,6 +235,10 @@ class TrainStep:
         from ..utils.engine import Engine
 
         self.device = torch.device(device) if device is not None else Engine.device()
+        if self.device.type == "cuda":
+            from ..ops import side_stream
+
+            side_stream.priority_compute_stream(self.device)     # data-gradient chain ahead of the side stream
         self.model = model
         self.criterion = criterion
         self.methods = dict(optim_method) if isinstance(optim_method, dict) else {model.getName(): optim_method}
@@ -416,7 +420,9 @@ class TrainStep:
         if not late:
             return self._weighted_exchange(loss, finished, self.g)
         if getattr(self, "_late_stream", None) is None:
-            self._late_stream = torch.cuda.Stream(device=self.device)
+            from ..ops import side_stream
+
+            self._late_stream = side_stream.peer_stream(self.device)
             with torch.cuda.stream(self._late_stream):     # zeroed on the stream that reads it (the compute stream
                 self._late_g = ops.zero_(torch.empty_like(self.g))   # may be backlogged: a fill there races the use)
         cur = torch.cuda.current_stream(self.device)

@@ -118,7 +118,8 @@ def test_bottleneck_masked_residual_addend(monkeypatch):
             fusion.MASKED_ADDEND[0] = saved      # restore the default (on), not a fixed value
         res[on] = (g.float().clone(), _weight_grads(m))
     assert any(seen)
-    assert _rel(res[True][0], res[False][0]) < 1e-5
+    # fp32 atomic order in the BN backward reductions (slotted, scheduling-dependent) flips isolated bf16 roundings
+    assert _rel(res[True][0], res[False][0]) < 1e-4
     assert _rel(res[True][1], res[False][1]) < 1e-4
     # and against the fp32 engine on the CPU (same bf16-rounded input / gradient): only rounding points differ
     cpu = copy.deepcopy(blk)
@@ -180,6 +181,13 @@ def test_train_step_gpu_decreases_loss():
     y = torch.randint(1, 11, (32,), device="cuda").float()
     losses = [float(st.step(x, y)) for _ in range(30)]
     assert losses[-1] < losses[0] * 0.5, losses
+    # the training step runs on a high-priority compute stream (ops/side_stream.py priority_compute_stream): the
+    # weight-gradient side stream stays at normal priority
+    from bigdl_amd.ops import side_stream
+
+    assert torch.cuda.current_stream().priority < 0
+    ss = side_stream.stream_for(x)
+    assert ss is not None and ss.priority == 0
 
 
 def test_lenet_gpu_matches_cpu():
