@@ -399,8 +399,10 @@ void launch_reduce(int mode, const bf16_t* x, const bf16_t* dz, const bf16_t* z,
   const int rpi = 256 / (G < 256 ? G : 256);
   long blocks = (P + rpi * 16 - 1) / (rpi * 16);   // >= 16 rows per thread
   if (blocks > 2048) blocks = 2048;
-  // deterministic mode: one block per statistics slot, so every slot word receives a single atomic onto zero
-  if (bigdl_deterministic() && blocks > STAT_SLOTS) blocks = STAT_SLOTS;
+  // deterministic mode: at most two blocks per statistics slot, so every slot word receives at most two atomics
+  // onto zero — fl(0 + a + b) is the same in either arrival order (IEEE addition commutes; only a third addend
+  // makes the order visible) — and the reduction keeps one workgroup per CU instead of half the chip
+  if (bigdl_deterministic() && blocks > 2 * STAT_SLOTS) blocks = 2 * STAT_SLOTS;
   if (blocks < 1) blocks = 1;
   const long rpb = (P + blocks - 1) / blocks;
   blocks = (P + rpb - 1) / rpb;

@@ -740,7 +740,7 @@ __global__ __launch_bounds__(256) void sumsq_det_kernel(const float* __restrict_
 __global__ void sumsq_det_finish_kernel(float* __restrict__ out, const float* __restrict__ slots) {
   if (threadIdx.x == 0) {
     float t = 0.f;
-    for (int s = 0; s < 128; ++s) t += slots[s];
+    for (int s = 0; s < BIGDL_DET_SLOTS; ++s) t += slots[s];
     out[0] += t;
   }
 }
@@ -836,37 +836,65 @@ void bigdl_colsum_bf16(const uint16_t* x, float* out, long P, int K, hipStream_t
 }
 // Deterministic column sum: row block y writes its partial to its own slot of the caller's workspace ([by][K] fp32;
 // plain stores, no atomics), then one fixed-order pass adds the slots into out (one writer per column).
+// Deterministic column sums, pass 1: block (bx, by) sums the channel groups [bx * CGB, + CGB) (8 channels each,
+// CGB = min(K / 8, 64)) over its row range into slots[by][.]. A wave covers 64 / CGB rows per trip with every lane
+// busy (narrow K no longer idles most of the wave), 4 rows per lane in flight; the block's partials meet in LDS in a
+// fixed order.
 __global__ void __launch_bounds__(256) colsum_det_kernel(const bf16_t* __restrict__ x, long P, int K,
                                                         long rows_per_block, long ld, float* __restrict__ slots) {
-  __shared__ float part[4][64][9];
+  constexpr int U = 4;
+  __shared__ float part[256][9];
+  const int Kg = K >> 3;
+  const int CGB = Kg < 64 ? Kg : 64, RW = 64 / CGB;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int c0 = (blockIdx.x * 64 + lane) * 8;
+  const int cgl = lane % CGB, ro = lane / CGB;
+  const int cg = blockIdx.x * CGB + cgl;
   const long r0 = (long)blockIdx.y * rows_per_block;
   const long r1 = r0 + rows_per_block < P ? r0 + rows_per_block : P;
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  if (c0 < K) {
-    for (long r = r0 + wave; r < r1; r += 4) {
-      const v4u q = *reinterpret_cast<const v4u*>(x + r * ld + c0);
+  if (ro < RW && cg < Kg) {
+    const long step = 4L * RW;
+    for (long r = r0 + wave * RW + ro; r < r1; r += U * step) {
+      v4u q[U];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) { acc[2 * e] += lo_bf(q[e]); acc[2 * e + 1] += hi_bf(q[e]); }
+      for (int u = 0; u < U; ++u) {
+        const long rr = r + u * step;
+        q[u] = *reinterpret_cast<const v4u*>(x + (rr < r1 ? rr : r) * ld + cg * 8);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const float m = r + u * step < r1 ? 1.f : 0.f;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { acc[2 * e] += m * lo_bf(q[u][e]); acc[2 * e + 1] += m * hi_bf(q[u][e]); }
+      }
     }
   }
 #pragma unroll
-  for (int e = 0; e < 8; ++e) part[wave][lane][e] = acc[e];
+  for (int e = 0; e < 8; ++e) part[threadIdx.x][e] = acc[e];
   __syncthreads();
-  if (wave == 0 && c0 < K) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e)
-      slots[(size_t)blockIdx.y * K + c0 + e] = part[0][lane][e] + part[1][lane][e] + part[2][lane][e] + part[3][lane][e];
+  for (int c = threadIdx.x; c < CGB * 8; c += 256) {
+    const int g = c >> 3, e = c & 7;
+    if (blockIdx.x * CGB + g >= Kg) continue;
+    float t = 0.f;
+    for (int w = 0; w < 4; ++w)
+      for (int rr = 0; rr < RW; ++rr) t += part[w * 64 + rr * CGB + g][e];
+    slots[(size_t)blockIdx.y * K + (blockIdx.x * CGB + g) * 8 + e] = t;
   }
 }
 __global__ void __launch_bounds__(256) colsum_det_finish_kernel(float* __restrict__ out, int K, int nslots,
                                                                const float* __restrict__ slots) {
   const int c = blockIdx.x * 256 + threadIdx.x;
   if (c >= K) return;
-  float t = 0.f;
-  for (int s = 0; s < nslots; ++s) t += slots[(size_t)s * K + c];
-  out[c] += t;
+  // 8 interleaved partial sums (slot s into t[s % 8]), combined in a fixed order: deterministic, and the loads of
+  // 8 slots are in flight together instead of one dependent chain
+  float t[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  int s = 0;
+  for (; s + 8 <= nslots; s += 8) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) t[u] += slots[(size_t)(s + u) * K + c];
+  }
+  for (; s < nslots; ++s) t[s & 7] += slots[(size_t)s * K + c];
+  out[c] += ((t[0] + t[1]) + (t[2] + t[3])) + ((t[4] + t[5]) + (t[6] + t[7]));
 }
 
 // out[k] += sum over P rows (row stride ld, ld % 8 == 0) of x[r][k]. Deterministic mode: with det_ws (>= BIGDL_DET_SLOTS
