@@ -33,7 +33,7 @@ def module_key(cls):
         return "keras." + cls.__name__
     if mod == "bigdl_amd.nn.tf_ops":
         return "ops." + cls.__name__
-    if mod in ("bigdl_amd.nn.ops", "bigdl_amd.nn.tf", "bigdl_amd.nn.onnx"):
+    if mod in ("bigdl_amd.nn.ops", "bigdl_amd.nn.tf", "bigdl_amd.nn.onnx", "bigdl_amd.nn.mkldnn"):
         return mod[len("bigdl_amd."):] + "." + cls.__name__
     return cls.__name__
 

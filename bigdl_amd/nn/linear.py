@@ -24,6 +24,7 @@ import torch.nn.functional as F
 from .. import ops
 from ..ops import conv as cv
 from ..ops import conv_fn
+from ..ops import native
 from .abstractnn import AutogradModule, TensorModule
 from .init_methods import RandomUniform
 
@@ -110,11 +111,9 @@ class Linear(TensorModule):
         w16 = self.w16("weight")
         if self.bias is not None:
             xe = torch.empty(M, K + 8, dtype=BF16, device=x.device)
-            xe[:, :K].copy_(x16)
-            xe[:, K:].zero_()
-            xe[:, K].fill_(1.0)
+            native.get().ones_col_pack(x16.contiguous(), xe)      # [x | 1 | 0...] in one pass (no aten fills)
             self._xe = xe
-            y = torch.addmm(self.bias.to(BF16), xe[:, :K], w16.t())
+            y = torch.addmm(self.w16("bias"), xe[:, :K], w16.t())
         else:
             self._xe = x16.contiguous()
             y = torch.mm(self._xe, w16.t())
@@ -194,9 +193,13 @@ class Linear(TensorModule):
                 g16 = ops.to_bf16(g) if g.dtype == torch.float32 else g.to(BF16).contiguous()
             K = self.inputSize
             gw = torch.mm(g16.t(), self._xe, out_dtype=torch.float32)     # [N, K (+8)] fp32 from the GEMM
-            self.gradWeight.add_(gw[:, :K], alpha=self.scaleW)
-            if self.bias is not None:
+            if self.bias is not None and self.gradWeight.is_contiguous():
+                native.get().ones_col_acc(gw, self.gradWeight, self.gradBias, self.scaleW, self.scaleB)
+            elif self.bias is not None:
+                self.gradWeight.add_(gw[:, :K], alpha=self.scaleW)
                 self.gradBias.add_(gw[:, K], alpha=self.scaleB)
+            else:
+                self.gradWeight.add_(gw, alpha=self.scaleW)
             self._g16 = None
             return
         if g.is_cuda:

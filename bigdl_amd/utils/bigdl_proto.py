@@ -588,7 +588,7 @@ def _class_for(module_type, engine_key=None):
     elif name.startswith("nn.tf."):
         cands = ["nn.tf." + name[6:], name[6:]]
     elif name.startswith("nn.mkldnn.") or name.startswith("nn.quantized."):
-        cands = [name.split(".")[-1]]
+        cands = [name, name.split(".")[-1]]     # nn.mkldnn.RNN is its own class; other MKL-DNN layers map by name
     elif name.startswith("nn."):
         cands = [name[3:]]
     cands.append(name.split(".")[-1])

@@ -1312,6 +1312,20 @@ void gconv(int64_t pass, const Tensor& x_or_dx, const Tensor& w_or_dw, const Opt
   else { c.x = cf(x, "x"); c.dwt = mf(w, "dw"); c.db = omf(b_or_db, "db"); c.dy = cf(y, "dy"); }
   TORCH_CHECK(bigdl_gconv(&c, (int)pass, stream()) == 0, "gconv: bad geometry");
 }
+void ones_col_pack(const Tensor& x, const Tensor& xe) {
+  TORCH_CHECK(x.dim() == 2 && x.is_contiguous() && x.size(1) % 8 == 0, "ones_col_pack: x must be [M, K] contiguous, K % 8 == 0");
+  TORCH_CHECK(xe.dim() == 2 && xe.is_contiguous() && xe.size(0) == x.size(0) && xe.size(1) == x.size(1) + 8,
+              "ones_col_pack: xe must be [M, K + 8] contiguous");
+  bigdl_ones_col_pack(cbf(x, "x"), mbf(xe, "xe"), x.size(0), (int)x.size(1), stream());
+}
+void ones_col_acc(const Tensor& gw, const Tensor& gW, const OptT& gB, double sW, double sB) {
+  TORCH_CHECK(gW.dim() == 2 && gW.is_contiguous() && gW.size(1) % 4 == 0, "ones_col_acc: gW must be [N, K] contiguous");
+  TORCH_CHECK(gw.is_contiguous() && gw.dim() == 2 && gw.size(0) == gW.size(0) && gw.size(1) == gW.size(1) + 8,
+              "ones_col_acc: gw must be [N, K + 8] contiguous");
+  if (gB && gB->defined()) TORCH_CHECK(gB->numel() == gW.size(0) && gB->is_contiguous(), "ones_col_acc: gB is [N]");
+  bigdl_ones_col_acc(cf(gw, "gw"), mf(gW, "gW"), omf(gB, "gB"), gW.size(0), (int)gW.size(1), (float)sW, (float)sB,
+                     stream());
+}
 void colsum_bf16(const Tensor& x, const Tensor& out) {
   TORCH_CHECK(x.dim() == 2 && x.is_contiguous() && x.size(1) % 8 == 0, "colsum_bf16: x must be [P, K] contiguous, K % 8 == 0");
   TORCH_CHECK(out.is_contiguous() && out.numel() == x.size(1), "colsum_bf16: out must hold K floats");
@@ -1484,6 +1498,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gru_seq_bwd", &gru_seq_bwd);
   m.def("lstm_seq_bwd", &lstm_seq_bwd);
   m.def("colsum_bf16", &colsum_bf16);
+  m.def("ones_col_pack", &ones_col_pack);
+  m.def("ones_col_acc", &ones_col_acc);
   m.def("layernorm_fwd", &layernorm_fwd);
   m.def("attn_fwd", &attn_fwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("bias"), py::arg("H"),
         py::arg("causal"), py::arg("o"), py::arg("lse"), py::arg("drop_p") = 0.0, py::arg("seed") = 0);

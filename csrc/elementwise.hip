@@ -919,6 +919,47 @@ void bigdl_colsum_bf16_ld(const uint16_t* x, float* out, long P, int K, long ld,
   HIP_LAUNCH_CHECK();
 }
 
+// Linear on hipBLASLt (nn/linear.py): the weight-gradient GEMM's B operand is [x | 1 | 0 x 7] (bf16, K + 8 columns)
+// so its last useful column is the bias gradient. Pack: one 16-byte granule per thread (K % 8 == 0).
+__global__ void ones_col_pack_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ xe, long M, int K) {
+  const int gpr = K / 8 + 1;
+  const long total = M * gpr;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / gpr;
+    const int g = (int)(i - r * gpr);
+    v4u v;
+    if (g < gpr - 1) v = *reinterpret_cast<const v4u*>(x + r * K + g * 8);
+    else v = v4u{0x3f80u, 0u, 0u, 0u};                  // bf16 1.0 then zeros
+    *reinterpret_cast<v4u*>(xe + r * (K + 8) + g * 8) = v;
+  }
+}
+// gW[n][k] += sW * gw[n][k], gB[n] += sB * gw[n][K] (gw: [N][K + 8] fp32 from the GEMM)
+__global__ void ones_col_acc_kernel(const float* __restrict__ gw, float* __restrict__ gW, float* __restrict__ gB, long N,
+                                    int K, float sW, float sB) {
+  const int cpr = K / 4 + 1;                           // float4 chunks per row, then one bias word
+  const long total = N * cpr;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long n = i / cpr;
+    const int c = (int)(i - n * cpr);
+    if (c < cpr - 1) {
+      const v4f g = *reinterpret_cast<const v4f*>(gw + n * (K + 8) + c * 4);
+      v4f w = *reinterpret_cast<const v4f*>(gW + n * K + c * 4);
+      w += g * sW;
+      *reinterpret_cast<v4f*>(gW + n * K + c * 4) = w;
+    } else if (gB) {
+      gB[n] += sB * gw[n * (K + 8) + K];
+    }
+  }
+}
+
+void bigdl_ones_col_pack(const uint16_t* x, uint16_t* xe, long M, int K, hipStream_t st) {
+  ones_col_pack_kernel<<<grid_cap(M * (K / 8 + 1)), 256, 0, st>>>(x, xe, M, K);
+  HIP_LAUNCH_CHECK();
+}
+void bigdl_ones_col_acc(const float* gw, float* gW, float* gB, long N, int K, float sW, float sB, hipStream_t st) {
+  ones_col_acc_kernel<<<grid_cap(N * (K / 4 + 1)), 256, 0, st>>>(gw, gW, gB, N, K, sW, sB);
+  HIP_LAUNCH_CHECK();
+}
 void bigdl_cast_f32_bf16(const float* x, uint16_t* y, long n, hipStream_t st) {
   cast_f32_bf16_kernel<<<grid_cap(n / 4 + 1), 256, 0, st>>>(x, y, n);
   HIP_LAUNCH_CHECK();

@@ -165,6 +165,9 @@ void bigdl_nchw_f32_to_nhwc_bf16(const float* x, uint16_t* y, int N, int C, int 
                                  hipStream_t st);
 void bigdl_cast_f32_bf16(const float* x, uint16_t* y, long n, hipStream_t st);
 void bigdl_colsum_bf16(const uint16_t* x, float* out, long P, int K, hipStream_t st, float* det_ws = nullptr);
+// [M][K] bf16 -> [M][K + 8] = [x | 1 | 0...]; gW += sW * gw[:, :K], gB += sB * gw[:, K] (gw [N][K + 8] fp32)
+void bigdl_ones_col_pack(const uint16_t* x, uint16_t* xe, long M, int K, hipStream_t st);
+void bigdl_ones_col_acc(const float* gw, float* gW, float* gB, long N, int K, float sW, float sB, hipStream_t st);
 void bigdl_cast_bf16_f32(const uint16_t* x, float* y, long n, hipStream_t st);
 
 // pooling (NHWC bf16)

@@ -82,6 +82,7 @@ ARGS = {
     "nn.tf.Conv3DBackpropInputV2": (1, 1, 1), "nn.tf.Enter": ("frame",), "nn.tf.MaxPoolGrad": (2, 2, 1, 1),
     "nn.tf.SplitAndSelect": (1, 1, 2), "nn.tf.StridedSlice": ([(1, 1, 2, 1)],),
     "nn.tf.Variable": (lambda: torch.ones(3),),
+    "nn.mkldnn.RNN": ("vanilla_lstm", 4, 4, "eltwise_tanh", "bidirectional_sum", 2),
 }
 
 # containers that are built by adding their cell / body (reference SerializerSpec builds them the same way)
