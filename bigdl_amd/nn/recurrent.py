@@ -19,6 +19,8 @@ loop entirely: a sequence-level autograd Function runs ``h @ U^T`` (library GEMM
 the gradient of both in one pass) per step, and computes dU with ONE [4H, T*B] x [T*B, H] GEMM after the
 reverse sweep instead of T small ones.
 """
+import os
+
 import torch
 import torch.nn.functional as F
 
@@ -279,6 +281,18 @@ def _live_sink(m):
     return g
 
 
+# BIGDL_RNN_WGRAD_BLAS=0 keeps the whole-sequence LSTM's recurrent weight gradient on the in-tree kernel (A/B)
+_RWG_BLAS = [os.environ.get("BIGDL_RNN_WGRAD_BLAS", "1") != "0"]
+
+
+def _recurrent_wgrad_blas(rows, H):
+    """The recurrent weight gradient dU = dg^T h of the whole-sequence LSTM on hipBLASLt (the Linear route's shape
+    rule, nn/linear.py _blas_shape; not in deterministic mode). LSTM LM 11.81 -> 11.47 ms/iteration."""
+    from . import linear
+
+    return _RWG_BLAS[0] and linear._blas_shape(rows, H, 4 * H) and not ops.native.deterministic()
+
+
 class _LSTMSeq(torch.autograd.Function):
     """Whole-sequence LSTM (gate order i, g, f, o) with the fused HIP cell kernels on the GPU engine."""
 
@@ -392,6 +406,15 @@ class _LSTMSeq(torch.autograd.Function):
                            dcT.contiguous() if dcT is not None else None, acts, cs, c0.contiguous(), dg16, dxg, dc0,
                            dh0, sync)
             sink = _live_sink(ctx.gmod)
+            if _recurrent_wgrad_blas(T * B, H):
+                # dU (+)= dg^T h over all T * B rows on hipBLASLt, accumulated in place (beta = 1) into the fp32
+                # gradient: the [4H x H x T*B] GEMM is the shape the Linear route measured fastest there
+                # (profiles/r6_lm_gemm_vs_hipblaslt.log: 532 -> 355 us)
+                a, b = dg16.view(T * B, 4 * H).t(), h16[:T].view(T * B, H)
+                if sink is not None and sink.is_contiguous():
+                    torch.addmm(sink, a, b, out_dtype=torch.float32, out=sink)
+                    return dxg, dh0, dc0, None, None
+                return dxg, dh0, dc0, torch.mm(a, b, out_dtype=torch.float32), None
             if sink is not None:
                 dU = sink.view(4 * H, H, 1, 1)
             else:
