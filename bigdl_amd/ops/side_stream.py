@@ -111,9 +111,14 @@ def _ranks_share_gpus():
     priority split is kept to that layout."""
     import torch.distributed as dist
 
-    world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else \
-        int(os.environ.get("LOCAL_WORLD_SIZE", os.environ.get("WORLD_SIZE", "1")))
-    return world > max(1, torch.cuda.device_count())
+    local = os.environ.get("LOCAL_WORLD_SIZE")          # ranks on THIS node (torch.distributed.run sets it)
+    if local:
+        ranks = int(local)
+    elif dist.is_available() and dist.is_initialized():
+        ranks = dist.get_world_size()
+    else:
+        ranks = int(os.environ.get("WORLD_SIZE", "1"))
+    return ranks > max(1, torch.cuda.device_count())
 
 
 def priority_compute_stream(device):
