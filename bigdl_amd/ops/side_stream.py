@@ -23,7 +23,8 @@ On by default (``BIGDL_WGRAD_STREAM=0`` disables): ResNet-50 b256 eager 29.40 ->
 Queue priority: the compute stream is the critical path (busy ~21.9 of a ~22.1 ms step) and the side stream's
 weight gradients only fill around it, so training runs the compute stream at HIGH queue priority
 (``priority_compute_stream``, called by TrainStep; ``BIGDL_COMPUTE_PRIO=0`` keeps the default stream): when both
-streams have workgroups waiting, the dispatcher takes the data-gradient chain's first. ResNet-50 b256
+streams have workgroups waiting, the dispatcher takes the data-gradient chain's first. RCCL's streams stay at
+normal priority (utils/engine.py). ResNet-50 b256
 11,200 -> 11,690 img/s interleaved on one box (profiles/r6_iteration_log.txt). Raising the SIDE stream's priority
 instead (``BIGDL_WGRAD_PRIO=-1``, round 3) measured no better: that is the wrong direction.
 """

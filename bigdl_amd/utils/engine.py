@@ -102,14 +102,10 @@ class _Engine:
             kw.update(store=td.PrefixStore(f"bigdl/attempt_{attempt}", base), rank=rank, world_size=world)
         if backend == "nccl":
             torch.cuda.set_device(self.local_rank())
-            from ..ops import side_stream
-
-            if side_stream.compute_priority_enabled():
-                # RCCL's streams at the compute stream's raised priority (ops/side_stream.py): the bucketed
-                # reduce-scatters must not wait for the data-gradient chain to drain before they dispatch
-                opts = td.ProcessGroupNCCL.Options()
-                opts.is_high_priority_stream = True
-                kw["pg_options"] = opts
+            # RCCL keeps its default (normal-priority) streams: a raised-priority compute stream still leaves
+            # normal-priority work dispatching beside it (tools/stream_prio_probe.py: 0.3 ms behind a running
+            # raised-priority kernel), while raised-priority streams could share hardware queues with the compute
+            # stream and serialise the bucketed reduce-scatters behind the backward
             td.init_process_group(backend, device_id=torch.device("cuda", self.local_rank()), **kw)
         else:
             td.init_process_group(backend, **kw)

@@ -26,14 +26,8 @@ def _worker(rank, world, port, fn, args, q, engine="cpu", backend="gloo", env=No
         if backend == "nccl":
             import torch
 
-            from ..ops import side_stream
-
             torch.cuda.set_device(0)
-            kw = {}
-            if side_stream.compute_priority_enabled():      # as Engine.init: RCCL at the compute stream's priority
-                kw["pg_options"] = dist.ProcessGroupNCCL.Options()
-                kw["pg_options"].is_high_priority_stream = True
-            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0), **kw)
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
         else:
             dist.init_process_group("gloo", rank=rank, world_size=world)
         from .engine import Engine, EngineType
