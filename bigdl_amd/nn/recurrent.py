@@ -285,12 +285,14 @@ def _live_sink(m):
 _RWG_BLAS = [os.environ.get("BIGDL_RNN_WGRAD_BLAS", "1") != "0"]
 
 
-def _recurrent_wgrad_blas(rows, H):
-    """The recurrent weight gradient dU = dg^T h of the whole-sequence LSTM on hipBLASLt (the Linear route's shape
-    rule, nn/linear.py _blas_shape; not in deterministic mode). LSTM LM 11.81 -> 11.47 ms/iteration."""
+def _recurrent_wgrad_blas(rows, H, n=None):
+    """The recurrent weight gradients of the whole-sequence LSTM / GRU (dU = dg^T h, [n x H] over all T * B rows;
+    n = 4H for the LSTM) on hipBLASLt: the Linear route's shape rule (nn/linear.py _blas_shape), not in
+    deterministic mode. LSTM LM 11.81 -> 11.46 ms/iteration."""
     from . import linear
 
-    return _RWG_BLAS[0] and linear._blas_shape(rows, H, 4 * H) and not ops.native.deterministic()
+    n = 4 * H if n is None else n
+    return _RWG_BLAS[0] and linear._blas_shape(rows, H, n) and not ops.native.deterministic()
 
 
 class _LSTMSeq(torch.autograd.Function):
@@ -532,13 +534,15 @@ class _GRUSeq(torch.autograd.Function):
             sync = torch.empty(C.lstm_seq_sync_words(), dtype=torch.int32, device=out.device)
             C.gru_seq_bwd(Wrz, Wn, h0, gates, out, dout.contiguous() if dout is not None else None,
                           dhT.contiguous() if dhT is not None else None, dx, dn16, drz16, dh0, sync)
-            dUrz = out.new_empty(2 * H, H, 1, 1)
-            C.fill_bytes(dUrz, 0)
-            cv.conv2d_wgrad(drz16.view(T * B, 2 * H, 1, 1), h16[:T].view(T * B, H, 1, 1), dUrz, None, (1, 1), (0, 0))
-            dUn = out.new_empty(H, H, 1, 1)
-            C.fill_bytes(dUn, 0)
-            cv.conv2d_wgrad(dn16.view(T * B, H, 1, 1), rh16.view(T * B, H, 1, 1), dUn, None, (1, 1), (0, 0))
-            return dx, dh0, dUrz.view(2 * H, H), dUn.view(H, H)
+            def wgrad(g16, x16, n):        # [n, H] = g^T x over all T * B rows (hipBLASLt where the LSTM's rule says)
+                if _recurrent_wgrad_blas(T * B, H, n):
+                    return torch.mm(g16.view(T * B, n).t(), x16.view(T * B, H), out_dtype=torch.float32)
+                d = out.new_empty(n, H, 1, 1)
+                C.fill_bytes(d, 0)
+                cv.conv2d_wgrad(g16.view(T * B, n, 1, 1), x16.view(T * B, H, 1, 1), d, None, (1, 1), (0, 0))
+                return d.view(n, H)
+
+            return dx, dh0, wgrad(drz16, h16[:T], 2 * H), wgrad(dn16, rh16, H)
         UrzT = Urz.detach().t().contiguous().to(bf)       # [H, 2H]: D = drz . U_rz
         UnT = Un.detach().t().contiguous().to(bf)         # [H, H]:  D = dn . U_n
         dout = dout.contiguous() if dout is not None else None

@@ -77,3 +77,38 @@ def test_recurrent_weight_gradient_blas_route_matches():
         R._RWG_BLAS[0] = saved
     assert torch.equal(res[True][0], res[False][0])         # the input gradient does not depend on the route
     assert _rel(res[True][1], res[False][1]) < 1e-5        # fp32 accumulation both ways: summation order only
+
+
+def test_gru_recurrent_weight_gradient_blas_route_matches():
+    """The whole-sequence GRU's [2H x H] recurrent weight gradient on hipBLASLt (n = 2H meets the shape rule at
+    H = 1024; the [H x H] one stays on the in-tree kernel) against the in-tree kernel on the same inputs."""
+    import copy
+
+    from bigdl_amd import nn, ops
+    from bigdl_amd.nn import recurrent as R
+
+    B, T, H = 64, 128, 1024
+    if not ops.native.get().gru_seq_supported(B, H):
+        pytest.skip("whole-sequence GRU not available for this shape")
+    torch.manual_seed(6)
+    base = nn.Recurrent().add(nn.GRU(H, H))
+    x = (torch.randn(B, T, H) * 0.5).cuda()
+    gy = (torch.randn(B, T, H) * 0.1).cuda()
+    res = {}
+    saved = R._RWG_BLAS[0]
+    try:
+        for on in (True, False):
+            R._RWG_BLAS[0] = on
+            assert R._recurrent_wgrad_blas(B * T, H, 2 * H) == on and not R._recurrent_wgrad_blas(B * T, H, H)
+            m = copy.deepcopy(base).cuda()
+            m.training()
+            m.forward(x)
+            gi = m.backward(x, gy)
+            torch.cuda.synchronize()
+            res[on] = (gi.float().cpu(), m.cell.h2g.gradWeight.float().cpu().clone(),
+                       m.cell.h2n.gradWeight.float().cpu().clone())
+    finally:
+        R._RWG_BLAS[0] = saved
+    assert _rel(res[True][0], res[False][0]) < 1e-6
+    assert _rel(res[True][1], res[False][1]) < 1e-5
+    assert _rel(res[True][2], res[False][2]) < 1e-5          # (fp32 atomic order of the in-tree kernel only)
