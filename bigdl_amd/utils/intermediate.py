@@ -188,6 +188,14 @@ class IRToBlas:
         """A layer for the element: the source layer itself when ``share`` (toGraph), else a rebuilt copy."""
         if e.general or (share and e.source is not None):
             return e.source
+        if e.op in ("Recurrent", "BiRecurrent") and e.source is not None:
+            # the cell is added after construction (Recurrent.add), not a constructor argument: copy the layer
+            import copy
+
+            m = copy.deepcopy(e.source)
+            if e.name:
+                m.setName(e.name)
+            return m
         m = module_class(e.op)(*e.args, **e.kwargs)
         for k, v in e.attrs.items():
             if k not in ("fuse_relu", "passthrough", "emit_stats", "train"):
@@ -316,7 +324,68 @@ class IRToDnn:
                         p.element = _fold_affine_into_conv(pe, *aff)
                         replaced[n.id] = p
         IRToDnn._replace(graph, nodes, replaced)
+        IRToDnn._merge_lstm_stacks(graph)
         return graph
+
+    @staticmethod
+    def _plain_lstm(e):
+        """The LSTM cell of a Recurrent element when it is the primitive's vanilla LSTM (no dropout, default
+        activations, no batch-norm pre-topology, no masking), else None."""
+        from ..nn.recurrent import LSTM, Recurrent
+
+        m = e.source
+        if e.op != "Recurrent" or not isinstance(m, Recurrent) or type(m.cell) is not LSTM:
+            return None
+        c = m.cell
+        if m.bn is not None or m.maskZero or not c._fused_ok() or c.preTopology is None:
+            return None
+        return c
+
+    @staticmethod
+    def _merge_lstm_stacks(graph):
+        """Chains of two or more plain Recurrent(LSTM(H, H)) layers, each the only consumer of the previous, become
+        ONE nn.mkldnn.RNN(VanillaLstm, H, H, layers = L) element (the reference primitive's `layers`,
+        S/nn/mkldnn/RNN.scala:87-92: stacked layers need inputSize == hiddenSize), with the weights moved into its
+        ldigo layout and gate order."""
+        from ..nn.mkldnn import _ORDER, AlgKind
+
+        nodes, nexts = IRToDnn._nexts(graph)
+        replaced, taken = {}, set()
+        order = list(_ORDER[AlgKind.VanillaLstm])
+        for n in nodes:
+            c = IRToDnn._plain_lstm(n.element)
+            if n.id in taken or c is None or c.inputSize != c.hiddenSize:
+                continue
+            H = c.hiddenSize
+            chain = [n]
+            while True:
+                nx = nexts[chain[-1].id]
+                if len(nx) != 1 or len(nx[0].prevs) != 1:
+                    break
+                c2 = IRToDnn._plain_lstm(nx[0].element)
+                if c2 is None or c2.inputSize != H or c2.hiddenSize != H:
+                    break
+                chain.append(nx[0])
+            if len(chain) < 2:
+                continue
+            L = len(chain)
+            w = torch.empty(L, 1, H, 4, H)
+            wi = torch.empty(L, 1, H, 4, H)
+            b = torch.zeros(L, 1, 4, H)
+            with torch.no_grad():
+                for l, node in enumerate(chain):
+                    cell = node.element.source.cell
+                    w[l, 0] = cell.preTopology.weight.detach().float().cpu().view(4, H, H)[order].permute(2, 0, 1)
+                    wi[l, 0] = cell.h2g.weight.detach().float().cpu().view(4, H, H)[order].permute(2, 0, 1)
+                    if cell.preTopology.bias is not None:
+                        b[l, 0] = cell.preTopology.bias.detach().float().cpu().view(4, H)[order]
+            e = IRElement("nn.mkldnn.RNN", ("vanilla_lstm", H, H, "eltwise_tanh", "unidirectional_left2right", L),
+                          {"inputFormat": "ntc"}, {"weight": w, "bias": b, "weight_i": wi}, chain[0].element.name)
+            merged = IRNode(e)
+            merged.prevs = list(chain[0].prevs)
+            replaced[chain[-1].id] = merged
+            taken.update(x.id for x in chain)
+        IRToDnn._replace(graph, nodes, replaced)
 
     @staticmethod
     def relu_plan(g):

@@ -179,3 +179,26 @@ def test_argument_checks():
     rnn = dnn.RNN(dnn.AlgKind.VanillaLstm, 3, 5)
     with pytest.raises(ValueError):
         rnn.forward(torch.rand(2, 3, 4))
+
+
+def test_dnn_lowering_merges_lstm_stacks():
+    """ConversionUtils.convert(model, "dnn") for inference turns a chain of plain Recurrent(LSTM(H, H)) layers into
+    ONE nn.mkldnn.RNN with layers = chain length (weights moved into the ldigo layout / primitive gate order); a first
+    layer whose input size differs from H stays a Recurrent (the primitive stacks need inputSize == hiddenSize)."""
+    from bigdl_amd.utils.intermediate import ConversionUtils
+
+    torch.manual_seed(7)
+    m = nn.Sequential()
+    m.add(nn.Recurrent().add(nn.LSTM(5, 8)))
+    for _ in range(3):
+        m.add(nn.Recurrent().add(nn.LSTM(8, 8)))
+    m.add(nn.TimeDistributed(nn.Linear(8, 4)))
+    m.evaluate()
+    x = torch.randn(2, 6, 5)
+    ref = m.forward(x)
+    g = ConversionUtils.convert(m, "dnn", device="cpu", train=False)
+    layers = g.flattened_layers()
+    rnns = [q for q in layers if isinstance(q, dnn.RNN)]
+    assert len(rnns) == 1 and rnns[0].layers == 3 and rnns[0].inputFormat == "ntc"
+    assert sum(isinstance(q, nn.Recurrent) for q in layers) == 1
+    assert torch.allclose(g.forward(x), ref, atol=1e-5)

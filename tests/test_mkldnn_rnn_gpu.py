@@ -44,3 +44,22 @@ def test_rnn_gpu_matches_cpu(mode, direction, layers):
     assert _rel(gx_g, gx_c) < 3e-2
     for gname in ("gradWeight", "gradWeight_i", "gradBias"):
         assert _rel(getattr(gpu, gname), getattr(cpu, gname)) < 3e-2, gname
+
+
+def test_ptb_lm_dnn_lowering_on_gpu():
+    """The PTB LM (LookupTable -> 2 x Recurrent(LSTM 256) -> TimeDistributed(Linear)) lowered for inference: the LSTM
+    stack becomes one nn.mkldnn.RNN(layers = 2) on the persistent kernels, same output as the Recurrent stack."""
+    from bigdl_amd.models.rnn import PTBModel
+    from bigdl_amd.nn import mkldnn as dnn
+    from bigdl_amd.utils.intermediate import ConversionUtils
+
+    torch.manual_seed(8)
+    m = PTBModel.lstm(500, 256, 500, 2)
+    m.evaluate()
+    ids = torch.randint(1, 501, (32, 20)).float()
+    ref = m.forward(ids).float()
+    g = ConversionUtils.convert(m, "dnn", device="cuda", train=False)
+    rnns = [q for q in g.flattened_layers() if isinstance(q, dnn.RNN)]
+    assert len(rnns) == 1 and rnns[0].layers == 2
+    out = g.forward(ids.cuda()).float().cpu()
+    assert _rel(out, ref) < 2e-2
