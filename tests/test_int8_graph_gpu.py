@@ -63,9 +63,12 @@ def test_pool_i8_matches_reference(avg, k, s, p, count_pad, shape=(2, 17, 17, 32
 
 
 @pytest.mark.parametrize("avg,count_pad,shape", [(True, True, (1, 35, 35, 48)), (True, False, (2, 8, 9, 16)),
-                                                  (False, False, (1, 35, 35, 48)), (True, True, (3, 5, 3, 16))])
+                                                  (False, False, (1, 35, 35, 48)), (True, True, (3, 5, 3, 16)),
+                                                  (True, True, (2, 17, 17, 768)), (True, True, (2, 8, 8, 2048)),
+                                                  (False, False, (1, 17, 17, 528))])
 def test_pool3s1_i8_runs(avg, count_pad, shape):
-    """3x3 / stride-1 int8 pooling on the run-of-8 kernel (Inception pool branches): partial runs, widths below 8."""
+    """3x3 / stride-1 int8 pooling (Inception pool branches): partial runs, widths below 8, and Inception's wide
+    channel counts (768 / 2048 / 528)."""
     test_pool_i8_matches_reference(avg, 3, 1, 1, count_pad, shape)
 
 
