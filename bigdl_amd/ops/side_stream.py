@@ -147,19 +147,10 @@ def priority_compute_stream(device):
 
 
 def peer_stream(device):
-    """A new stream at the current compute stream's priority, for work the compute stream must not starve (the
-    straggler drop's control and late-exchange streams): a raised-priority queue with a kernel in flight holds back
-    lower-priority queues' dispatch, measured on the straggler test (a dropped rank's exchange waited out its 600 ms
-    spin kernel)."""
+    """A new stream at the current compute stream's priority, for the straggler drop's control and late-exchange
+    streams: work the compute stream waits on should not queue behind it at a lower priority."""
     dev = torch.device(device)
     return torch.cuda.Stream(device=dev, priority=torch.cuda.current_stream(dev).priority)
-
-
-def compute_priority_enabled():
-    try:
-        return int(_COMPUTE_PRIO) < 0
-    except ValueError:
-        return False
 
 
 def begin(s):
