@@ -64,6 +64,7 @@ struct LstmSeqArgs {
   unsigned* herr;          // process-wide host-mapped error word (device address)
   unsigned long long spin; // bound of every wait, wall-clock ticks (100 MHz)
   int B, H, T, Bg;
+  int late;                // the publishing wave stores its outputs after the hand-off (BIGDL_LSTM_LATE)
 };
 
 // Host-mapped (fine-grained, coherent) error word shared by every persistent kernel of the process: a timeout stores
@@ -233,6 +234,10 @@ __global__ __launch_bounds__(512, 1) void lstm_seq_fwd_kernel(LstmSeqArgs a) {
         acc1[tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[s + 1], h1, acc1[tt], 0, 0, 0);
       }
     }
+    // the publishing wave (0) stores its outputs AFTER the hand-off: its drain (vmcnt(0) before the counter add)
+    // then waits for the state stores only, not for the scattered c / gate-activation stores (a.late; 0 = before)
+    const bool late = wave == 0 && a.late;
+    float kh[NT], kc[NT], ka[NT][4];
 #pragma unroll
     for (int tt = 0; tt < NT; ++tt) {
       const v4f gs = acc0[tt] + acc1[tt];
@@ -240,7 +245,9 @@ __global__ __launch_bounds__(512, 1) void lstm_seq_fwd_kernel(LstmSeqArgs a) {
                   og = sigm(gs[3] + x[tt][3]);
       c[tt] = fg * c[tt] + ig * gg;
       const float h = og * tanh_f(c[tt]);
-      if (live[tt]) {
+      kh[tt] = h; kc[tt] = c[tt];
+      ka[tt][0] = ig; ka[tt][1] = gg; ka[tt][2] = fg; ka[tt][3] = og;
+      if (live[tt] && !late) {
         const int bt = b[tt];
         if constexpr (!BIO) static_cast<float*>(a.out)[((size_t)bt * a.T + t) * H + j] = h;
         if (t == a.T - 1 && a.hT) a.hT[(size_t)bt * H + j] = h;
@@ -253,18 +260,37 @@ __global__ __launch_bounds__(512, 1) void lstm_seq_fwd_kernel(LstmSeqArgs a) {
     __syncthreads();
     if (wave == 0) {   // publish: R rows x 64 B, lane -> (row, 16-byte quarter); drained before the counter add
       const __amdgpu_buffer_rsrc_t r = rsrc(a.h16 + (t + 1) * slab, (int)(slab * 2));
+      v4u hvs[NT];
 #pragma unroll
       for (int tt = 0; tt < NT; ++tt) {
         const int row = tt * 16 + (lane >> 2), qq = lane & 3;
+        hvs[tt] = *reinterpret_cast<const v4u*>(hst + min(row, R - 1) * 32 + qq * 8);
         if (row < nb) {
-          const v4u hv = *reinterpret_cast<const v4u*>(hst + row * 32 + qq * 8);
-          st_sc1(hv, r, (int)(((b_lo + row) * H + m * 32 + qq * 8) * 2));
+          st_sc1(hvs[tt], r, (int)(((b_lo + row) * H + m * 32 + qq * 8) * 2));
           if constexpr (BIO)   // the layer output is the same bf16 h: one plain 16-byte store per lane
-            *reinterpret_cast<v4u*>(static_cast<bf16_t*>(a.out) + ((size_t)(b_lo + row) * a.T + t) * H + m * 32 + qq * 8) = hv;
+            if (!a.late)
+              *reinterpret_cast<v4u*>(static_cast<bf16_t*>(a.out) + ((size_t)(b_lo + row) * a.T + t) * H + m * 32 + qq * 8) = hvs[tt];
         }
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (lane == 0) signal(cnt);
+      if (a.late) {      // wave 0's outputs, behind the hand-off
+#pragma unroll
+        for (int tt = 0; tt < NT; ++tt) {
+          const int row = tt * 16 + (lane >> 2), qq = lane & 3;
+          if constexpr (BIO)
+            if (row < nb)
+              *reinterpret_cast<v4u*>(static_cast<bf16_t*>(a.out) + ((size_t)(b_lo + row) * a.T + t) * H + m * 32 + qq * 8) = hvs[tt];
+          if (live[tt]) {
+            const int bt = b[tt];
+            if constexpr (!BIO) static_cast<float*>(a.out)[((size_t)bt * a.T + t) * H + j] = kh[tt];
+            if (t == a.T - 1 && a.hT) a.hT[(size_t)bt * H + j] = kh[tt];
+            a.cs[((size_t)t * a.B + bt) * H + j] = kc[tt];
+            float* ap = a.acts + ((size_t)t * a.B + bt) * 4 * H + j;
+            ap[0] = ka[tt][0]; ap[H] = ka[tt][1]; ap[2 * H] = ka[tt][2]; ap[3 * H] = ka[tt][3];
+          }
+        }
+      }
     }
   }
 }
@@ -426,19 +452,32 @@ __global__ __launch_bounds__(512, 1) void lstm_seq_bwd_kernel(LstmSeqArgs a) {
     __syncthreads();
     if (wave == 0) {   // publish R rows x 4 gates x 64 B; drained before the counter add
       const __amdgpu_buffer_rsrc_t r = rsrc(a.dg16 + t * slab, (int)(slab * 2));
+      v4u gvs[4 * NT];
 #pragma unroll
       for (int k = 0; k < 4 * NT; ++k) {
         const int cidx = lane + 64 * k, row = cidx >> 4, gt = (cidx >> 2) & 3, qq = cidx & 3;
+        gvs[k] = *reinterpret_cast<const v4u*>(dst + (min(row, R - 1) * 4 + gt) * 32 + qq * 8);
         if (row < nb) {
-          const v4u gv = *reinterpret_cast<const v4u*>(dst + (row * 4 + gt) * 32 + qq * 8);
-          st_sc1(gv, r, (int)(((b_lo + row) * G4 + gt * H + m * 32 + qq * 8) * 2));
+          st_sc1(gvs[k], r, (int)(((b_lo + row) * G4 + gt * H + m * 32 + qq * 8) * 2));
           if constexpr (BIO)   // the input-projection gradient is the same bf16 dg: plain 16-byte store
-            *reinterpret_cast<v4u*>(static_cast<bf16_t*>(a.dxg) + ((size_t)(b_lo + row) * a.T + t) * G4 + gt * H + m * 32 +
-                                    qq * 8) = gv;
+            if (!a.late)
+              *reinterpret_cast<v4u*>(static_cast<bf16_t*>(a.dxg) + ((size_t)(b_lo + row) * a.T + t) * G4 + gt * H +
+                                      m * 32 + qq * 8) = gvs[k];
         }
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (lane == 0) signal(cnt);
+      if constexpr (BIO) {
+        if (a.late) {   // (as in the forward) the dxg copy behind the hand-off
+#pragma unroll
+          for (int k = 0; k < 4 * NT; ++k) {
+            const int cidx = lane + 64 * k, row = cidx >> 4, gt = (cidx >> 2) & 3, qq = cidx & 3;
+            if (row < nb)
+              *reinterpret_cast<v4u*>(static_cast<bf16_t*>(a.dxg) + ((size_t)(b_lo + row) * a.T + t) * G4 + gt * H +
+                                      m * 32 + qq * 8) = gvs[k];
+          }
+        }
+      }
     }
   }
 #pragma unroll
@@ -929,6 +968,8 @@ int bigdl_lstm_seq_fwd(const uint16_t* W16, const void* xg, const float* c0, uin
   a.W16 = W16; a.xg = xg; a.c0 = c0; a.h16 = h16; a.out = out; a.hT = hT; a.cs = cs; a.acts = acts; a.sync = sync;
   a.B = B; a.H = H; a.T = T; a.Bg = (B + NGRP - 1) / NGRP;
   a.herr = host_err_dev(); a.spin = g_spin_ticks;
+  static const int late = [] { const char* e = getenv("BIGDL_LSTM_LATE"); return e ? atoi(e) : 1; }();
+  a.late = late;
   bigdl_fill_bytes(sync, 0, (long)sizeof(unsigned) * bigdl_lstm_seq_sync_words(), st);   // kernel: graph-safe
   const dim3 grid(NGRP * (H / 32));
 #define SEQ_FWD(K)                                                                       \
@@ -958,6 +999,8 @@ int bigdl_lstm_seq_bwd(const uint16_t* W16, const void* dout, const float* dhT, 
   a.cs = const_cast<float*>(cs); a.c0 = c0; a.dg16 = dg16; a.dxg = dxg; a.dc0 = dc0; a.dh0 = dh0; a.sync = sync;
   a.B = B; a.H = H; a.T = T; a.Bg = (B + NGRP - 1) / NGRP;
   a.herr = host_err_dev(); a.spin = g_spin_ticks;
+  static const int late = [] { const char* e = getenv("BIGDL_LSTM_LATE"); return e ? atoi(e) : 1; }();
+  a.late = late;
   bigdl_fill_bytes(sync, 0, (long)sizeof(unsigned) * bigdl_lstm_seq_sync_words(), st);   // kernel: graph-safe
   const dim3 grid(NGRP * (H / 32));
 #define SEQ_BWD(K)                                                                       \
