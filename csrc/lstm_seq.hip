@@ -220,18 +220,25 @@ __global__ __launch_bounds__(512, 1) void lstm_seq_fwd_kernel(LstmSeqArgs a) {
       }
     }
     __syncthreads();
-    v4f acc0[NT], acc1[NT];
+    // CH independent accumulator chains per batch tile (4 with one tile: a dependent MFMA waits out the previous
+    // one's passes, so two chains left the matrix core idle between issues)
+    constexpr int CH = NT == 1 ? 4 : 2;
+    v4f acc[CH][NT];
 #pragma unroll
-    for (int tt = 0; tt < NT; ++tt) acc0[tt] = acc1[tt] = v4f{0.f, 0.f, 0.f, 0.f};
+    for (int q = 0; q < CH; ++q)
 #pragma unroll
-    for (int s = 0; s < KS; s += 2) {
+      for (int tt = 0; tt < NT; ++tt) acc[q][tt] = v4f{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < KS; s += CH) {
       if ((s & (8 / NT - 1)) == 0) asm volatile("" ::: "memory");     // <= 8 fragment reads in flight (VGPRs)
 #pragma unroll
       for (int tt = 0; tt < NT; ++tt) {
         const bf16_t* hb = hs + (tt * 16 + col) * HP + 8 * G;
-        const v8s h0 = *reinterpret_cast<const v8s*>(hb + s * 32), h1 = *reinterpret_cast<const v8s*>(hb + (s + 1) * 32);
-        acc0[tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[s], h0, acc0[tt], 0, 0, 0);
-        acc1[tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[s + 1], h1, acc1[tt], 0, 0, 0);
+#pragma unroll
+        for (int q = 0; q < CH; ++q) {
+          const v8s hq = *reinterpret_cast<const v8s*>(hb + (s + q) * 32);
+          acc[q][tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[s + q], hq, acc[q][tt], 0, 0, 0);
+        }
       }
     }
     // the publishing wave (0) stores its outputs AFTER the hand-off: its drain (vmcnt(0) before the counter add)
@@ -240,7 +247,9 @@ __global__ __launch_bounds__(512, 1) void lstm_seq_fwd_kernel(LstmSeqArgs a) {
     float kh[NT], kc[NT], ka[NT][4];
 #pragma unroll
     for (int tt = 0; tt < NT; ++tt) {
-      const v4f gs = acc0[tt] + acc1[tt];
+      v4f gs = acc[0][tt];
+#pragma unroll
+      for (int q = 1; q < CH; ++q) gs += acc[q][tt];
       const float ig = sigm(gs[0] + x[tt][0]), gg = tanh_f(gs[1] + x[tt][1]), fg = sigm(gs[2] + x[tt][2]),
                   og = sigm(gs[3] + x[tt][3]);
       c[tt] = fg * c[tt] + ig * gg;
