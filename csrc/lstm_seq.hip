@@ -243,7 +243,7 @@ __global__ __launch_bounds__(512, 1) void lstm_seq_fwd_kernel(LstmSeqArgs a) {
     }
     // the publishing wave (0) stores its outputs AFTER the hand-off: its drain (vmcnt(0) before the counter add)
     // then waits for the state stores only, not for the scattered c / gate-activation stores (a.late; 0 = before)
-    const bool late = wave == 0 && a.late;
+    const bool late = wave == 0 && NT == 1 && a.late;   // (two-tile groups measured slower: B 256)
     float kh[NT], kc[NT], ka[NT][4];
 #pragma unroll
     for (int tt = 0; tt < NT; ++tt) {
@@ -269,27 +269,27 @@ __global__ __launch_bounds__(512, 1) void lstm_seq_fwd_kernel(LstmSeqArgs a) {
     __syncthreads();
     if (wave == 0) {   // publish: R rows x 64 B, lane -> (row, 16-byte quarter); drained before the counter add
       const __amdgpu_buffer_rsrc_t r = rsrc(a.h16 + (t + 1) * slab, (int)(slab * 2));
-      v4u hvs[NT];
 #pragma unroll
       for (int tt = 0; tt < NT; ++tt) {
         const int row = tt * 16 + (lane >> 2), qq = lane & 3;
-        hvs[tt] = *reinterpret_cast<const v4u*>(hst + min(row, R - 1) * 32 + qq * 8);
         if (row < nb) {
-          st_sc1(hvs[tt], r, (int)(((b_lo + row) * H + m * 32 + qq * 8) * 2));
+          const v4u hv = *reinterpret_cast<const v4u*>(hst + row * 32 + qq * 8);
+          st_sc1(hv, r, (int)(((b_lo + row) * H + m * 32 + qq * 8) * 2));
           if constexpr (BIO)   // the layer output is the same bf16 h: one plain 16-byte store per lane
-            if (!a.late)
-              *reinterpret_cast<v4u*>(static_cast<bf16_t*>(a.out) + ((size_t)(b_lo + row) * a.T + t) * H + m * 32 + qq * 8) = hvs[tt];
+            if (!(NT == 1 && a.late))
+              *reinterpret_cast<v4u*>(static_cast<bf16_t*>(a.out) + ((size_t)(b_lo + row) * a.T + t) * H + m * 32 + qq * 8) = hv;
         }
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (lane == 0) signal(cnt);
-      if (a.late) {      // wave 0's outputs, behind the hand-off
+      if (NT == 1 && a.late) {      // wave 0's outputs, behind the hand-off
 #pragma unroll
         for (int tt = 0; tt < NT; ++tt) {
           const int row = tt * 16 + (lane >> 2), qq = lane & 3;
-          if constexpr (BIO)
+          if constexpr (BIO)   // re-read from LDS: hst is not rewritten before this wave reaches the next barrier
             if (row < nb)
-              *reinterpret_cast<v4u*>(static_cast<bf16_t*>(a.out) + ((size_t)(b_lo + row) * a.T + t) * H + m * 32 + qq * 8) = hvs[tt];
+              *reinterpret_cast<v4u*>(static_cast<bf16_t*>(a.out) + ((size_t)(b_lo + row) * a.T + t) * H + m * 32 + qq * 8) =
+                  *reinterpret_cast<const v4u*>(hst + row * 32 + qq * 8);
           if (live[tt]) {
             const int bt = b[tt];
             if constexpr (!BIO) static_cast<float*>(a.out)[((size_t)bt * a.T + t) * H + j] = kh[tt];
@@ -400,19 +400,40 @@ __global__ __launch_bounds__(512, 1) void lstm_seq_bwd_kernel(LstmSeqArgs a) {
         {   // dg_{t+1} of this tile's rows of the group -> LDS (rows past the group read as zero)
           const int rows = max(0, min(16, nb - tt * 16));
           const __amdgpu_buffer_rsrc_t r = rsrc(a.dg16 + (t + 1) * slab + (size_t)(b_lo + tt * 16) * G4, rows * G4 * 2);
-          constexpr int U = CH < 4 ? CH : 4;     // loads in flight per thread (VGPR budget: W takes 128)
-#pragma unroll
-          for (int h = 0; h < CH; h += U) {
-            v4u v[U];
+          // U loads per batch (VGPR budget: W takes 128), two batches in flight: batch h + 1 is issued before
+          // batch h is written to LDS, so the CH / U batches do not each pay a full L2 round trip
+          constexpr int U = CH < 4 ? CH : 4;
+          auto ld = [&](v4u (&v)[U], int h) {
 #pragma unroll
             for (int u = 0; u < U; ++u) {
               const int qc = tid + 512 * (h + u), row = qc / (G4 / 8), c8 = qc % (G4 / 8);
               v[u] = ld_sc1(r, (row * G4 + c8 * 8) * 2);
             }
+          };
+          auto st = [&](const v4u (&v)[U], int h) {
 #pragma unroll
             for (int u = 0; u < U; ++u) {
               const int qc = tid + 512 * (h + u), row = qc / (G4 / 8), c8 = qc % (G4 / 8);
               *reinterpret_cast<v4u*>(dgs + row * DP + c8 * 8) = v[u];
+            }
+          };
+          if constexpr (NT == 1) {
+            v4u va[U], vb[U];
+            ld(va, 0);
+#pragma unroll
+            for (int h = 0; h < CH; h += 2 * U) {
+              if (h + U < CH) ld(vb, h + U);
+              st(va, h);
+              if (h + U >= CH) break;
+              if (h + 2 * U < CH) ld(va, h + 2 * U);
+              st(vb, h + U);
+            }
+          } else {       // (two 16-row tiles: no registers for a second batch)
+#pragma unroll
+            for (int h = 0; h < CH; h += U) {
+              v4u v[U];
+              ld(v, h);
+              st(v, h);
             }
           }
         }
@@ -461,29 +482,29 @@ __global__ __launch_bounds__(512, 1) void lstm_seq_bwd_kernel(LstmSeqArgs a) {
     __syncthreads();
     if (wave == 0) {   // publish R rows x 4 gates x 64 B; drained before the counter add
       const __amdgpu_buffer_rsrc_t r = rsrc(a.dg16 + t * slab, (int)(slab * 2));
-      v4u gvs[4 * NT];
 #pragma unroll
       for (int k = 0; k < 4 * NT; ++k) {
         const int cidx = lane + 64 * k, row = cidx >> 4, gt = (cidx >> 2) & 3, qq = cidx & 3;
-        gvs[k] = *reinterpret_cast<const v4u*>(dst + (min(row, R - 1) * 4 + gt) * 32 + qq * 8);
         if (row < nb) {
-          st_sc1(gvs[k], r, (int)(((b_lo + row) * G4 + gt * H + m * 32 + qq * 8) * 2));
+          const v4u gv = *reinterpret_cast<const v4u*>(dst + (row * 4 + gt) * 32 + qq * 8);
+          st_sc1(gv, r, (int)(((b_lo + row) * G4 + gt * H + m * 32 + qq * 8) * 2));
           if constexpr (BIO)   // the input-projection gradient is the same bf16 dg: plain 16-byte store
-            if (!a.late)
+            if (!(NT == 1 && a.late))
               *reinterpret_cast<v4u*>(static_cast<bf16_t*>(a.dxg) + ((size_t)(b_lo + row) * a.T + t) * G4 + gt * H +
-                                      m * 32 + qq * 8) = gvs[k];
+                                      m * 32 + qq * 8) = gv;
         }
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (lane == 0) signal(cnt);
       if constexpr (BIO) {
-        if (a.late) {   // (as in the forward) the dxg copy behind the hand-off
+        if (NT == 1 && a.late) {   // (as in the forward) the dxg copy behind the hand-off, re-read from LDS: the tile is not
+                        // rewritten before this wave reaches the next step's barrier
 #pragma unroll
           for (int k = 0; k < 4 * NT; ++k) {
             const int cidx = lane + 64 * k, row = cidx >> 4, gt = (cidx >> 2) & 3, qq = cidx & 3;
             if (row < nb)
               *reinterpret_cast<v4u*>(static_cast<bf16_t*>(a.dxg) + ((size_t)(b_lo + row) * a.T + t) * G4 + gt * H +
-                                      m * 32 + qq * 8) = gvs[k];
+                                      m * 32 + qq * 8) = *reinterpret_cast<const v4u*>(dst + (row * 4 + gt) * 32 + qq * 8);
           }
         }
       }
