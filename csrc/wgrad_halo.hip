@@ -338,6 +338,7 @@ __global__ __launch_bounds__(KB * 4, 1) void conv_wgrad_halo_kernel(WgradArgs a)
     for (int kb = 0; kb < 4; ++kb) {
       const int k = k0 + kg * 64 + kb * 16 + lane;
       if (a.ws) bp[k] = accb[kb][0];
+      else if (a.splits > 1) unsafeAtomicAdd(bp + k, accb[kb][0]);
       else bp[k] += accb[kb][0];
     }
   }
@@ -353,6 +354,9 @@ __global__ __launch_bounds__(KB * 4, 1) void conv_wgrad_halo_kernel(WgradArgs a)
       float* o = base + (size_t)k * Kd + tp * C + c0 + cw * 16 + 4 * G;
       if (a.ws) {
         *reinterpret_cast<v4f*>(o) = acc[tp][kb];
+      } else if (a.splits > 1) {    // atomic mode (halo_atomic): the splits meet in dW through fp32 atomics
+#pragma unroll
+        for (int e = 0; e < 4; ++e) unsafeAtomicAdd(o + e, acc[tp][kb][e]);
       } else if (aligned) {
         *reinterpret_cast<v4f*>(o) += acc[tp][kb];
       } else {
@@ -430,6 +434,13 @@ int halo_lds() {
   static const int v = [] { const char* e = getenv("BIGDL_WGRAD_HALO_LDS"); return e ? atoi(e) : 80; }();
   return v;
 }
+// BIGDL_WGRAD_HALO_ATOMIC=1: with splits > 1 the splits add into dW / dbias with fp32 atomics instead of writing
+// workspace partials for halo_reduce_kernel (one fp32 copy of dW per split written and re-read); never in
+// deterministic mode (atomic order)
+bool halo_atomic() {
+  static const int v = [] { const char* e = getenv("BIGDL_WGRAD_HALO_ATOMIC"); return e ? atoi(e) : 0; }();
+  return v != 0 && !bigdl_deterministic();
+}
 int halo_wgs() {
   static const int v = [] { const char* e = getenv("BIGDL_WGRAD_HALO_WGS"); return e ? atoi(e) : 256; }();
   return v;
@@ -473,8 +484,11 @@ int bigdl_wgrad_pre_applies(const WgradArgs* a) {
 // Launch (a->splits / m_per_split from bigdl_wgrad_halo_plan; a->ws = [splits][Ncol][Kdim] partials when splits > 1,
 // then [splits][Ncol] bias partials when a->dbias, summed into a->dw / a->dbias in split order, else the kernel adds
 // into a->dw / a->dbias).
-int bigdl_wgrad_halo(const WgradArgs* a, hipStream_t st) {
+int bigdl_wgrad_halo(const WgradArgs* a_in, hipStream_t st) {
   const int lds = halo_lds();
+  WgradArgs b = *a_in;
+  if (b.splits > 1 && halo_atomic()) b.ws = nullptr;
+  const WgradArgs* a = &b;
   switch (a->Ws) {
     case 56: launch_halo_lds<56, 1>(*a, lds, st); break;
     case 28: launch_halo_lds<28, 2>(*a, lds, st); break;
